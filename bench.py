@@ -1,0 +1,233 @@
+"""bench.py -- BiasedMatrixFactorization k=64 Hogwild SGD throughput on MI355X (BASELINE.json).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1: launched by torch.distributed.run, one process per GPU)
+
+One step = one epoch (BiasedMatrixFactorization.Iterate, src/MyMediaLite/RatingPrediction/
+BiasedMatrixFactorization.cs:264-310) over every rank's ratings, plus -- for N > 1 -- the per-epoch
+RCCL all-reduce of item factors and item biases (model averaging).
+
+Workloads (BASELINE.json configs, synthetic data generated in HBM, inputs resident before timing):
+  N = 1 : C2 -- 1M users x 100k items, 100M ratings, k = 64 fp32.
+  N > 1 : C4 weak scaling -- per GPU a user shard of 1.25M users and 125M ratings over the shared
+          100k items (N = 8 is C4: 10M users, 1B ratings).
+The line carries the roofline of the SGD kernel (algorithmic bytes 16k+28 per update)
+and the CPU oracle's single-thread Iterate() on a bounded sample (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Load libmml_hip.so BEFORE torch so the process has one HIP runtime (same SONAMEs).
+from mymedialite_amd import _native as N  # noqa: E402
+
+if not os.path.exists(N.LIB_PATH):
+    import __graft_entry__
+    __graft_entry__.build()
+N.lib()
+
+import ctypes  # noqa: E402
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from mymedialite_amd.random import SystemRandom  # noqa: E402
+from mymedialite_amd.synthetic import planted_ratings_torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def bytes_per_update(k: int) -> int:
+    # read u, i (8 B) + r (4 B); read U_u, V_i (8k B); write U_u, V_i (8k B); r+w b_u, b_i (16 B)
+    return 16 * k + 28
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--k", type=int, default=64)
+    ap.add_argument("--ratings", type=int, default=0, help="override ratings per GPU")
+    ap.add_argument("--users", type=int, default=0, help="override users per GPU")
+    ap.add_argument("--items", type=int, default=100_000)
+    ap.add_argument("--schedule", default="hogwild", choices=["hogwild", "ordered"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    k = args.k
+    if world == 1:
+        n_local = args.ratings or 100_000_000
+        users_local = args.users or 1_000_000
+        workload = "C2: 1M users x 100k items, 100M ratings, BiasedMF k=64, Hogwild SGD"
+    else:
+        n_local = args.ratings or 125_000_000
+        users_local = args.users or 1_250_000
+        workload = (f"C4 weak scaling: per GPU {users_local} users / {n_local} ratings, "
+                    f"{args.items} shared items, BiasedMF k=64, per-epoch RCCL all-reduce")
+    n_users_total = users_local * world
+    n_items = args.items
+
+    ctx = N.Context(local)
+    if world > 1:
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            uid[:] = torch.frombuffer(bytearray(N.Context.unique_id()), dtype=torch.uint8)
+        dist.broadcast(uid, src=0)
+        ctx.comm_init(bytes(uid.tolist()), world, rank)
+
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    lo = rank * users_local
+    users, items, values = planted_ratings_torch(n_users_total, n_items, n_local, seed=1 + rank,
+                                                 device=dev, user_range=(lo, lo + users_local))
+    tu, ti, tv = planted_ratings_torch(n_users_total, n_items, 1_000_000, seed=1000 + rank,
+                                       device=dev, user_range=(lo, lo + users_local))
+    torch.cuda.synchronize()
+
+    # model: InitModel via the library's MyMediaLite.Random twin (U fully, then V fully)
+    # (users outside this rank's shard have no local ratings -> zero rows, as the reference does
+    # for users without training ratings, MatrixFactorization.cs:108-113)
+    U = np.zeros((n_users_total, k), np.float32)
+    U[lo:lo + users_local] = SystemRandom(1 + rank).fill_normal(users_local * k, 0.0,
+                                                                0.1).reshape(-1, k)
+    V = SystemRandom(1).fill_normal(n_items * k, 0.0, 0.1)
+    bu = np.zeros(n_users_total, np.float32)
+    bi = np.zeros(n_items, np.float32)
+    mean = float(values.double().mean().item())
+    avg = (mean - 1.0) / 4.0
+    gb = float(np.float32(np.log(avg / (1 - avg))))
+
+    params = N.BmfParams(k, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD if args.schedule == "hogwild"
+                         else N.SCHEDULE_ORDERED, 1.0, 0.01, 0.015, 0.015)
+    h = N._vp()
+    N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(params), n_users_total, n_items,
+                                   ctypes.byref(h)))
+    N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
+                                            values.data_ptr(), n_local, None))
+    N.check(N.lib().mml_bmf_set_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
+                                      N.ptr(bu, N._f32p), N.ptr(bi, N._f32p), gb, 1.0, 5.0))
+    del users, items, values
+    tus, tis, tvs = tu.cpu().numpy(), ti.cpu().numpy(), tv.cpu().numpy()
+    lr = 0.01
+
+    def evaluate():
+        out = np.zeros(2, np.float32)
+        N.check(N.lib().mml_bmf_evaluate(h, N.ptr(tus, N._i32p), N.ptr(tis, N._i32p),
+                                         N.ptr(tvs, N._f32p), len(tus), N.ptr(out, N._f32p)))
+        return float(out[0])
+
+    rmse0 = evaluate()
+    timing = np.zeros(2, np.float32)
+
+    def step():
+        N.check(N.lib().mml_bmf_iterate(h, lr, None))
+        N.lib().mml_bmf_last_timing(h, N.ptr(timing, N._f32p))
+        if world > 1:
+            N.check(N.lib().mml_bmf_allreduce_items(h))
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kernel_ms.append(float(timing[0]))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    rmse = evaluate()
+    total_updates = n_local * world * args.steps
+    value = total_updates / elapsed
+    avg_kernel_ms = float(np.mean(kernel_ms))
+    bpu = bytes_per_update(k)
+    achieved = n_local * bpu / (avg_kernel_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(h, k, n_users_total, n_items, gb, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "SGD rating-updates/sec + final RMSE, BiasedMF k=64 at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "rating-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (planted rank-8 model, Zipf(0.8) items, generated in HBM)",
+            "config": {"workload": workload, "num_factors": k, "ratings_per_gpu": n_local,
+                       "users_per_gpu": users_local, "items": n_items,
+                       "schedule": args.schedule, "parallelism": f"user-shard x{world}"},
+            "final_rmse": rmse,
+            "initial_rmse": rmse0,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": f"bmf_sgd_hogwild_kernel<RMSE,{max(1, (k + 3) // 4)}>",
+                         "kernel_avg_ms": avg_kernel_ms, "bytes_per_update": bpu},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    N.lib().mml_bmf_destroy(h)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(h, k, n_users, n_items, gb, seconds):
+    """Oracle Iterate() (single thread, exact reference arithmetic) on a bounded sample of the
+    same workload: the first S ratings of a fresh stream on the GPU model's current state."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    U = np.empty((n_users, k), np.float32)
+    V = np.empty((n_items, k), np.float32)
+    bu = np.empty(n_users, np.float32)
+    bi = np.empty(n_items, np.float32)
+    N.check(N.lib().mml_bmf_get_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
+                                      N.ptr(bu, N._f32p), N.ptr(bi, N._f32p)))
+    u, i, v = planted_ratings_torch(n_users, n_items, 4_000_000, seed=777, device="cpu")
+    u, i, v = u.numpy(), i.numpy(), v.numpy()
+    kw = dict(gb=np.float32(gb), min_rating=np.float32(1), range_=np.float32(4), lr=0.01)
+    probe = 100_000
+    t0 = time.perf_counter()
+    O.bmf_iterate(u, i, v, np.arange(probe, dtype=np.int32), U, V, bu, bi, **kw)
+    dt = time.perf_counter() - t0
+    n = int(min(len(u) - probe, max(probe, seconds / max(dt, 1e-9) * probe)))
+    t0 = time.perf_counter()
+    O.bmf_iterate(u, i, v, np.arange(probe, probe + n, dtype=np.int32), U, V, bu, bi, **kw)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "rating-updates/s", "cores": 1, "kind": "port",
+            "sample": f"{n} ratings of the C2 generator, k={k}, oracle Iterate() (C restatement "
+                      f"of BiasedMatrixFactorization.cs:264-310), {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,136 @@
+/*
+ * mml.h -- C ABI of libmml_hip.so, the MI355X-native training path for MyMediaLite's
+ * BiasedMatrixFactorization (explicit SGD), BPRMF (pairwise SGD) and WRMF (implicit ALS).
+ *
+ * Drop-in boundary.  The reference has no native code and no C ABI: these
+ * entry points are what the C# front end binds through P/Invoke to replace
+ * the managed inner loops named next to each function.  Conventions:
+ *   - every call returns mml_status (0 = OK, < 0 = error class); the message of the last failed
+ *     call on this host thread is mml_last_error().  A failure never aborts the host process.
+ *   - all arrays are plain host pointers unless the name says _device; the library COPIES host
+ *     buffers into HBM it owns and retains no caller pointer after a call returns.
+ *   - calls on one handle must come from one host thread at a time; every call is synchronous
+ *     (an epoch has finished when mml_*_iterate returns), preserving IIterativeModel.Iterate().
+ *   - row-major float factor matrices, exactly Matrix<float>.data
+ *     (src/MyMediaLite/DataType/Matrix.cs:29-36, element (i,j) at data[i*dim2+j]).
+ */
+#ifndef MML_H
+#define MML_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MML_ABI_VERSION 1
+
+typedef int32_t mml_status;
+enum {
+    MML_OK = 0,
+    MML_ERR_ARG = -1,     /* bad argument (null pointer, size, id out of range) */
+    MML_ERR_HIP = -2,     /* HIP runtime error */
+    MML_ERR_RCCL = -3,    /* RCCL error */
+    MML_ERR_OOM = -4,     /* device allocation failed */
+    MML_ERR_STATE = -5,   /* call not valid in the handle's current state */
+    MML_ERR_NODEV = -6    /* no usable gfx950 device */
+};
+
+/* ------------------------------------------------------------------ library / context */
+int mml_abi_version(void);
+const char* mml_last_error(void);
+mml_status mml_device_count(int32_t* out);
+
+typedef struct mml_ctx mml_ctx;
+/* One context per recommender instance, bound to one GPU (one process per GPU for multi-GPU). */
+mml_status mml_ctx_create(int32_t device_id, mml_ctx** out);
+mml_status mml_ctx_destroy(mml_ctx* ctx);
+/* RCCL communicator across processes (one rank per GPU): rank 0 creates the 128-byte id, the host
+ * broadcasts it (e.g. torch.distributed / MPI), then every rank calls mml_ctx_comm_init. */
+mml_status mml_comm_unique_id(uint8_t out_id[128]);
+mml_status mml_ctx_comm_init(mml_ctx* ctx, const uint8_t id[128], int32_t nranks, int32_t rank);
+
+/* ------------------------------------------------------------------ host RNG (MyMediaLite.Random)
+ * System.Random(seed)-compatible generator for hosts without the .NET BCL; the C# front end keeps
+ * using its own MyMediaLite.Random (src/MyMediaLite/Random.cs:23-64) and never needs these. */
+typedef struct mml_random mml_random;
+mml_status mml_random_create(int32_t seed, mml_random** out);
+mml_status mml_random_destroy(mml_random* r);
+mml_status mml_random_next(mml_random* r, int32_t max_value, int32_t* out);   /* Random.Next(n) */
+mml_status mml_random_next_double(mml_random* r, double* out);               /* NextDouble() */
+/* MatrixExtensions.InitNormal (DataType/MatrixExtensions.cs:62-69): MathNet polar Normal */
+mml_status mml_random_fill_normal(mml_random* r, double mean, double stddev, float* out, int64_t n);
+/* Utils.Shuffle (src/MyMediaLite/Utils.cs:52-64) */
+mml_status mml_random_shuffle_i32(mml_random* r, int32_t* a, int64_t n);
+/* MultiCore.PartitionUsersAndItems (src/MyMediaLite/MultiCore.cs:43-73): blocks as CSR over
+ * b = user_group*G + item_group; offsets[G*G+1], indices[n]; *out_groups = clipped G. */
+mml_status mml_partition_users_and_items(mml_random* r, const int32_t* users, const int32_t* items,
+                                         int64_t n, int32_t max_user_id, int32_t max_item_id,
+                                         int32_t num_groups, int64_t* offsets, int32_t* indices,
+                                         int32_t* out_groups);
+
+/* ------------------------------------------------------------------ BiasedMatrixFactorization */
+enum { MML_LOSS_RMSE = 0, MML_LOSS_MAE = 1, MML_LOSS_LOGISTIC = 2 }; /* OptimizationTarget */
+enum {
+    MML_SCHEDULE_ORDERED = 0, /* exact reference order (MaxThreads = 1): one wavefront */
+    MML_SCHEDULE_DSGD = 1,    /* reference DSGD (MaxThreads = G > 1): conflict-free blocks */
+    MML_SCHEDULE_HOGWILD = 2  /* lock-free parallel SGD over the fixed permuted stream */
+};
+
+typedef struct {
+    int32_t num_factors;              /* NumFactors (MatrixFactorization.cs:71) */
+    int32_t loss;                     /* Loss, MML_LOSS_* (BiasedMatrixFactorization.cs:114) */
+    int32_t frequency_regularization; /* FrequencyRegularization (:111) */
+    int32_t schedule;                 /* MML_SCHEDULE_* */
+    float bias_learn_rate;            /* BiasLearnRate (:85) */
+    float bias_reg;                   /* BiasReg (:88) */
+    float reg_u;                      /* RegU (:91) */
+    float reg_i;                      /* RegI (:94) */
+} mml_bmf_params;
+
+typedef struct mml_bmf mml_bmf;
+
+mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params, int32_t n_users,
+                          int32_t n_items, mml_bmf** out);
+mml_status mml_bmf_destroy(mml_bmf* h);
+/* Training ratings (StaticRatings SoA: Data/StaticRatings.cs:49-51) + the epoch visiting order:
+ * order = DataSet.RandomIndex (Data/DataSet.cs:100-110), reused every epoch like the reference;
+ * NULL = identity.  The device keeps the ratings permuted into visit order (coalesced stream). */
+mml_status mml_bmf_set_data(mml_bmf* h, const int32_t* users, const int32_t* items,
+                            const float* values, int64_t n, const int32_t* order);
+/* Same, from arrays already resident in this context's HBM (device pointers). */
+mml_status mml_bmf_set_data_device(mml_bmf* h, const int32_t* users_device,
+                                   const int32_t* items_device, const float* values_device,
+                                   int64_t n, const int32_t* order_device);
+/* DSGD blocks (MML_SCHEDULE_DSGD): CSR over b = user_group*G + item_group of rating indices,
+ * as produced by MultiCore.PartitionUsersAndItems / mml_partition_users_and_items. */
+mml_status mml_bmf_set_blocks(mml_bmf* h, int32_t num_groups, const int64_t* offsets,
+                              const int32_t* indices);
+/* Model upload (InitModel is host-side RNG work: MatrixFactorization.cs:99-116). */
+mml_status mml_bmf_set_model(mml_bmf* h, const float* user_factors, const float* item_factors,
+                             const float* user_bias, const float* item_bias, float global_bias,
+                             float min_rating, float max_rating);
+mml_status mml_bmf_get_model(mml_bmf* h, float* user_factors, float* item_factors,
+                             float* user_bias, float* item_bias);
+/* One epoch = BiasedMatrixFactorization.Iterate(IList<int>,bool,bool) (:264-310) over the stored
+ * order at current_learnrate = learn_rate.  DSGD: subepoch_sequence[G] is the shuffled
+ * sub-epoch order of Iterate() (:209-214); NULL otherwise. */
+mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate, const int32_t* subepoch_sequence);
+/* BiasedMatrixFactorization.Predict(int,int) (:313-325), batched; unknown ids allowed. */
+mml_status mml_bmf_predict(mml_bmf* h, const int32_t* users, const int32_t* items, int64_t n,
+                           float* out);
+/* Eval.Ratings.Evaluate (Eval/Ratings.cs:96-139) on device: out[0] = RMSE, out[1] = MAE. */
+mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const int32_t* items,
+                            const float* values, int64_t n, float* out);
+/* Device time of the last mml_bmf_iterate's SGD kernels (HIP events on the library stream):
+ * out[0] = ms for the whole epoch, out[1] = number of kernel launches in it. */
+mml_status mml_bmf_last_timing(mml_bmf* h, float* out);
+/* Multi-GPU (user shards): in-place RCCL all-reduce of item factors and item
+ * biases over the context's communicator, then scale by 1/nranks (model averaging). */
+mml_status mml_bmf_allreduce_items(mml_bmf* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MML_H */

@@ -1,0 +1,11 @@
+"""mymedialite_amd -- MI355X-native training path for MyMediaLite's matrix-factorization recommenders.
+
+The per-rating / per-sample loops run in libmml_hip.so (hand-written HIP for gfx950, C ABI in
+include/mml.h); this package is the host-side mirror of the reference's recommender API.
+"""
+from .data import IdentityMapping, Mapping, PosOnlyFeedback, Ratings, read_items, read_ratings
+from .random import Random, SystemRandom
+from .rating_prediction import BiasedMatrixFactorization
+
+__all__ = ["BiasedMatrixFactorization", "Ratings", "PosOnlyFeedback", "Mapping",
+           "IdentityMapping", "read_ratings", "read_items", "Random", "SystemRandom"]

@@ -1,0 +1,160 @@
+"""ctypes binding of libmml_hip.so (C ABI declared in include/mml.h).
+
+This is the Python twin of the P/Invoke shim a C# host would use.  There is no
+fallback: if the HIP library is missing or no gfx950 device is visible, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmml_hip.so")
+
+MML_OK = 0
+ERRORS = {-1: "MML_ERR_ARG", -2: "MML_ERR_HIP", -3: "MML_ERR_RCCL", -4: "MML_ERR_OOM",
+          -5: "MML_ERR_STATE", -6: "MML_ERR_NODEV"}
+
+LOSS_RMSE, LOSS_MAE, LOSS_LOGISTIC = 0, 1, 2
+SCHEDULE_ORDERED, SCHEDULE_DSGD, SCHEDULE_HOGWILD = 0, 1, 2
+
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_f64p = ctypes.POINTER(ctypes.c_double)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+_st = ctypes.c_int32
+
+
+class MMLError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{ERRORS.get(status, status)}: {message}")
+        self.status = status
+
+
+class BmfParams(ctypes.Structure):
+    """mml_bmf_params (include/mml.h)."""
+    _fields_ = [("num_factors", ctypes.c_int32), ("loss", ctypes.c_int32),
+                ("frequency_regularization", ctypes.c_int32), ("schedule", ctypes.c_int32),
+                ("bias_learn_rate", ctypes.c_float), ("bias_reg", ctypes.c_float),
+                ("reg_u", ctypes.c_float), ("reg_i", ctypes.c_float)]
+
+
+# every exported symbol of include/mml.h: name -> (restype, argtypes)
+SIGNATURES = {
+    "mml_abi_version": (ctypes.c_int, []),
+    "mml_last_error": (ctypes.c_char_p, []),
+    "mml_device_count": (_st, [_i32p]),
+    "mml_ctx_create": (_st, [ctypes.c_int32, ctypes.POINTER(_vp)]),
+    "mml_ctx_destroy": (_st, [_vp]),
+    "mml_comm_unique_id": (_st, [_u8p]),
+    "mml_ctx_comm_init": (_st, [_vp, _u8p, ctypes.c_int32, ctypes.c_int32]),
+    "mml_random_create": (_st, [ctypes.c_int32, ctypes.POINTER(_vp)]),
+    "mml_random_destroy": (_st, [_vp]),
+    "mml_random_next": (_st, [_vp, ctypes.c_int32, _i32p]),
+    "mml_random_next_double": (_st, [_vp, _f64p]),
+    "mml_random_fill_normal": (_st, [_vp, ctypes.c_double, ctypes.c_double, _f32p,
+                                     ctypes.c_int64]),
+    "mml_random_shuffle_i32": (_st, [_vp, _i32p, ctypes.c_int64]),
+    "mml_partition_users_and_items": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_int32, _i64p, _i32p, _i32p]),
+    "mml_bmf_create": (_st, [_vp, ctypes.POINTER(BmfParams), ctypes.c_int32, ctypes.c_int32,
+                             ctypes.POINTER(_vp)]),
+    "mml_bmf_destroy": (_st, [_vp]),
+    "mml_bmf_set_data": (_st, [_vp, _i32p, _i32p, _f32p, ctypes.c_int64, _i32p]),
+    "mml_bmf_set_data_device": (_st, [_vp, _vp, _vp, _vp, ctypes.c_int64, _vp]),
+    "mml_bmf_set_blocks": (_st, [_vp, ctypes.c_int32, _i64p, _i32p]),
+    "mml_bmf_set_model": (_st, [_vp, _f32p, _f32p, _f32p, _f32p, ctypes.c_float, ctypes.c_float,
+                                ctypes.c_float]),
+    "mml_bmf_get_model": (_st, [_vp, _f32p, _f32p, _f32p, _f32p]),
+    "mml_bmf_iterate": (_st, [_vp, ctypes.c_float, _i32p]),
+    "mml_bmf_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
+    "mml_bmf_evaluate": (_st, [_vp, _i32p, _i32p, _f32p, ctypes.c_int64, _f32p]),
+    "mml_bmf_last_timing": (_st, [_vp, _f32p]),
+    "mml_bmf_allreduce_items": (_st, [_vp]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libmml_hip.so (raises if it was not built -- there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() "
+                              "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status: int):
+    if status != MML_OK:
+        raise MMLError(status, lib().mml_last_error().decode(errors="replace"))
+
+
+def ptr(a, t):
+    """Pointer to a contiguous numpy array (None -> NULL)."""
+    if a is None:
+        return None
+    assert a.flags.c_contiguous, "array must be C-contiguous"
+    return a.ctypes.data_as(t)
+
+
+def i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def i64(a):
+    return np.ascontiguousarray(a, dtype=np.int64)
+
+
+def f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    check(lib().mml_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Context:
+    """mml_ctx: one GPU + one HIP stream (+ RCCL communicator for multi-GPU)."""
+
+    def __init__(self, device: int = 0):
+        h = _vp()
+        check(lib().mml_ctx_create(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+        self.nranks = 1
+        self.rank = 0
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * 128)()
+        check(lib().mml_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib().mml_ctx_comm_init(self.handle, buf, int(nranks), int(rank)))
+        self.nranks, self.rank = nranks, rank
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().mml_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,806 @@
+// bmf.hip -- BiasedMatrixFactorization SGD on MI355X (gfx950).
+//
+// Replaces BiasedMatrixFactorization.Iterate(IList<int>,bool,bool)
+// (src/MyMediaLite/RatingPrediction/BiasedMatrixFactorization.cs:264-310), its Predict (:313-325)
+// and Eval.Ratings.Evaluate (src/MyMediaLite/Eval/Ratings.cs:96-139).
+//
+// HBM layout (per mml_bmf handle):
+//   U [n_users x ld], V [n_items x ld]   fp32 row-major, ld = 4 * LPR (zero-padded columns), so a
+//                                        factor row is LPR float4s = one coalesced 16-B-per-lane read
+//   bu [n_users], bi [n_items]           fp32 biases
+//   raw_{u,i,r}                          the training ratings as given (StaticRatings SoA)
+//   s{u,i,r}                             the same ratings permuted into the epoch visit order
+//                                        (DataSet.RandomIndex, fixed across epochs like the
+//                                        reference, Data/DataSet.cs:100-110): the epoch reads it as
+//                                        three perfectly coalesced streams
+// Arithmetic follows the reference exactly: float dot / score / biases, double
+// sigmoid, error and factor deltas, float increments; built with -ffp-contract=off.
+//
+// Schedules:
+//   ORDERED  one wavefront walks the stream in order: lanes own factors, the dot product is summed
+//            left to right through v_readlane, so the trajectory matches the CPU oracle bit for bit
+//            (up to libm-vs-ocml exp rounding) -- the MaxThreads = 1 reference.
+//   DSGD     the reference's MaxThreads = G schedule (:205-215): per sub-epoch one launch of G
+//            wavefronts, wavefront j walks block (j, (s + j) mod G) in order; blocks of one sub-epoch
+//            share no user and no item, so the result is deterministic and equals the reference's.
+//   HOGWILD  lock-free: every wavefront owns a contiguous chunk of the permuted stream; LPR lanes
+//            per rating (float4 each), 64/LPR ratings per wave step, dot product by xor-shuffle
+//            reduction, plain (racy) stores of the updated rows -- Hogwild! semantics.
+#include <algorithm>
+#include <vector>
+
+#include "mml_internal.h"
+
+namespace {
+
+struct BmfScalars {
+    float gb;         // global_bias
+    float min_rating; // min_rating
+    float range;      // rating_range_size
+    float lr;         // current_learnrate
+    float blr;        // BiasLearnRate * current_learnrate (float product, as in :286)
+    float bias_reg;   // BiasReg
+    float reg_u;      // RegU
+    float reg_i;      // RegI
+};
+
+// compute_gradient_common (SetupLoss, :247-261)
+template <int LOSS>
+__device__ __forceinline__ float gradient_common(double sig, double err, float range) {
+    if constexpr (LOSS == MML_LOSS_MAE) {
+        const double sg = err > 0.0 ? 1.0 : (err < 0.0 ? -1.0 : 0.0);
+        return (float)(sg * sig * (1.0 - sig) * (double)range);
+    } else if constexpr (LOSS == MML_LOSS_LOGISTIC) {
+        return (float)err;
+    } else {
+        return (float)(err * sig * (1.0 - sig) * (double)range);
+    }
+}
+
+// Per-rating scalar part shared by all schedules: score, sigmoid, error, gradient, reg weights,
+// new biases.  `dot` is the float row scalar product.
+template <int LOSS>
+struct RatingStep {
+    float g, reg_u, reg_i, new_bu, new_bi;
+    __device__ __forceinline__ RatingStep(const BmfScalars& s, float dot, float bu_u, float bi_i,
+                                          float r, const int32_t* cnt_u, const int32_t* cnt_i,
+                                          int32_t u, int32_t i) {
+        const float score = ((s.gb + bu_u) + bi_i) + dot;
+        const double sig = 1.0 / (1.0 + exp(-(double)score));
+        const double prediction = (double)s.min_rating + sig * (double)s.range;
+        const double err = (double)r - prediction;
+        g = gradient_common<LOSS>(sig, err, s.range);
+        reg_u = s.reg_u;
+        reg_i = s.reg_i;
+        if (cnt_u) {  // FrequencyRegularization (:281-282)
+            reg_u = (float)((double)s.reg_u / sqrt((double)cnt_u[u]));
+            reg_i = (float)((double)s.reg_i / sqrt((double)cnt_i[i]));
+        }
+        new_bu = bu_u + s.blr * (g - (s.bias_reg * reg_u) * bu_u);
+        new_bi = bi_i + s.blr * (g - (s.bias_reg * reg_i) * bi_i);
+    }
+    // Matrix.Inc(u, f, lr * delta) (:291-308; DataType/MatrixExtensions.cs:76-79)
+    __device__ __forceinline__ float new_u(const BmfScalars& s, float u_f, float i_f) const {
+        const double delta = (double)g * (double)i_f - (double)reg_u * (double)u_f;
+        return u_f + (float)((double)s.lr * delta);
+    }
+    __device__ __forceinline__ float new_i(const BmfScalars& s, float u_f, float i_f) const {
+        const double delta = (double)g * (double)u_f - (double)reg_i * (double)i_f;
+        return i_f + (float)((double)s.lr * delta);
+    }
+};
+
+// ORDERED / DSGD: workgroup = one wavefront; wavefront j walks block (j, (subepoch+j) mod G).
+// KM = factors per lane (k <= 64 * KM).
+template <int LOSS, int KM>
+__global__ __launch_bounds__(64) void bmf_sgd_ordered_kernel(
+    const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
+    const int64_t* __restrict__ block_off, int32_t G, int32_t subepoch, float* U, float* V,
+    float* bu, float* bi, int32_t k, int32_t ld, BmfScalars s, const int32_t* __restrict__ cnt_u,
+    const int32_t* __restrict__ cnt_i) {
+    const int lane = threadIdx.x;
+    const int j = blockIdx.x;
+    const int64_t b = (int64_t)j * G + (subepoch + j) % G;
+    const int64_t begin = block_off[b], end = block_off[b + 1];
+    for (int64_t x = begin; x < end; ++x) {
+        const int32_t u = su[x], i = si[x];
+        const float r = sr[x];
+        float* Uu = U + (int64_t)u * ld;
+        float* Vi = V + (int64_t)i * ld;
+        float pu[KM], qi[KM], prod[KM];
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int f = lane + 64 * m;
+            pu[m] = f < k ? Uu[f] : 0.0f;
+            qi[m] = f < k ? Vi[f] : 0.0f;
+            prod[m] = pu[m] * qi[m];
+        }
+        // RowScalarProduct: float accumulation, left to right (MatrixExtensions.cs:224-241)
+        float dot = 0.0f;
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int lim = min(64, k - 64 * m);
+            const int bits = __float_as_int(prod[m]);
+            for (int l = 0; l < lim; ++l) dot += __int_as_float(__builtin_amdgcn_readlane(bits, l));
+        }
+        const float bu_u = bu[u], bi_i = bi[i];
+        const RatingStep<LOSS> st(s, dot, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
+        if (lane == 0) {
+            bu[u] = st.new_bu;
+            bi[i] = st.new_bi;
+        }
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int f = lane + 64 * m;
+            if (f < k) {
+                Uu[f] = st.new_u(s, pu[m], qi[m]);
+                Vi[f] = st.new_i(s, pu[m], qi[m]);
+            }
+        }
+    }
+}
+
+// HOGWILD: LPR lanes per rating, one float4 of U_u and of V_i per lane.
+template <int LOSS, int LPR>
+__global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
+    const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
+    int64_t n, int64_t chunk, float* U, float* V, float* bu, float* bi, int32_t ld4, BmfScalars s,
+    const int32_t* __restrict__ cnt_u, const int32_t* __restrict__ cnt_i) {
+    constexpr int RPW = 64 / LPR;  // ratings per wave step
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t begin = wave * chunk;
+    const int64_t end = min(begin + chunk, n);
+    const int sub = lane / LPR, q = lane % LPR;
+    float4* U4 = reinterpret_cast<float4*>(U);
+    float4* V4 = reinterpret_cast<float4*>(V);
+    for (int64_t base = begin; base < end; base += 64) {
+        // 64 ratings of the stream: three coalesced 256-B loads, then broadcast per group
+        const int64_t idx = base + lane;
+        const bool in = idx < end;
+        const int32_t my_u = in ? su[idx] : 0;
+        const int32_t my_i = in ? si[idx] : 0;
+        const float my_r = in ? sr[idx] : 0.0f;
+        const int cnt = (int)min((int64_t)64, end - base);
+        for (int step = 0; step < cnt; step += RPW) {
+            const int src = step + sub;
+            const int32_t u = __shfl(my_u, src);
+            const int32_t i = __shfl(my_i, src);
+            const float r = __shfl(my_r, src);
+            if (src < cnt) {
+                const int64_t ou = (int64_t)u * ld4 + q, oi = (int64_t)i * ld4 + q;
+                const float4 pu = U4[ou];
+                const float4 qi = V4[oi];
+                float part = pu.x * qi.x;
+                part += pu.y * qi.y;
+                part += pu.z * qi.z;
+                part += pu.w * qi.w;
+#pragma unroll
+                for (int off = LPR / 2; off >= 1; off >>= 1) part += __shfl_xor(part, off);
+                const float bu_u = bu[u], bi_i = bi[i];
+                const RatingStep<LOSS> st(s, part, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
+                if (q == 0) {
+                    bu[u] = st.new_bu;
+                    bi[i] = st.new_bi;
+                }
+                float4 nu, nq;
+                nu.x = st.new_u(s, pu.x, qi.x);
+                nu.y = st.new_u(s, pu.y, qi.y);
+                nu.z = st.new_u(s, pu.z, qi.z);
+                nu.w = st.new_u(s, pu.w, qi.w);
+                nq.x = st.new_i(s, pu.x, qi.x);
+                nq.y = st.new_i(s, pu.y, qi.y);
+                nq.z = st.new_i(s, pu.z, qi.z);
+                nq.w = st.new_i(s, pu.w, qi.w);
+                U4[ou] = nu;
+                V4[oi] = nq;
+            }
+        }
+    }
+}
+
+// BiasedMatrixFactorization.Predict(int,int) (:313-325): double score, float dot in order.
+__device__ __forceinline__ float bmf_predict1(int32_t u, int32_t i, int32_t n_users,
+                                              int32_t n_items, const float* U, const float* V,
+                                              const float* bu, const float* bi, int32_t k,
+                                              int32_t ld, float gb, float min_rating,
+                                              float range) {
+    double score = (double)gb;
+    if (u >= 0 && u < n_users) score += (double)bu[u];
+    if (i >= 0 && i < n_items) score += (double)bi[i];
+    if (u >= 0 && u < n_users && i >= 0 && i < n_items) {
+        const float* a = U + (int64_t)u * ld;
+        const float* c = V + (int64_t)i * ld;
+        float dot = 0.0f;
+        for (int f = 0; f < k; ++f) dot += a[f] * c[f];
+        score += (double)dot;
+    }
+    return (float)((double)min_rating + (1.0 / (1.0 + exp(-score))) * (double)range);
+}
+
+__global__ __launch_bounds__(256) void bmf_predict_kernel(
+    const int32_t* __restrict__ users, const int32_t* __restrict__ items, int64_t n,
+    int32_t n_users, int32_t n_items, const float* __restrict__ U, const float* __restrict__ V,
+    const float* __restrict__ bu, const float* __restrict__ bi, int32_t k, int32_t ld, float gb,
+    float min_rating, float range, float* __restrict__ out) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x)
+        out[x] = bmf_predict1(users[x], items[x], n_users, n_items, U, V, bu, bi, k, ld, gb,
+                              min_rating, range);
+}
+
+// Eval.Ratings.Evaluate (:96-139): float error, float square, double sums; per-block partials.
+__global__ __launch_bounds__(256) void bmf_eval_kernel(
+    const int32_t* __restrict__ users, const int32_t* __restrict__ items,
+    const float* __restrict__ values, int64_t n, int32_t n_users, int32_t n_items,
+    const float* __restrict__ U, const float* __restrict__ V, const float* __restrict__ bu,
+    const float* __restrict__ bi, int32_t k, int32_t ld, float gb, float min_rating, float range,
+    double* __restrict__ partials) {
+    double se = 0.0, ae = 0.0;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const float p = bmf_predict1(users[x], items[x], n_users, n_items, U, V, bu, bi, k, ld,
+                                     gb, min_rating, range);
+        const float e = p - values[x];
+        se += (double)(e * e);
+        ae += (double)fabsf(e);
+    }
+    __shared__ double s_se[256], s_ae[256];
+    s_se[threadIdx.x] = se;
+    s_ae[threadIdx.x] = ae;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            s_se[threadIdx.x] += s_se[threadIdx.x + w];
+            s_ae[threadIdx.x] += s_ae[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        partials[2 * blockIdx.x] = s_se[0];
+        partials[2 * blockIdx.x + 1] = s_ae[0];
+    }
+}
+
+// stream[x] = raw[order[x]] for the three SoA columns
+__global__ __launch_bounds__(256) void gather_stream_kernel(
+    const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const float* __restrict__ rr,
+    const int32_t* __restrict__ order, int64_t n, int32_t* __restrict__ su,
+    int32_t* __restrict__ si, float* __restrict__ sr) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = order ? order[x] : x;
+        su[x] = ru[o];
+        si[x] = ri[o];
+        sr[x] = rr[o];
+    }
+}
+
+// id range check + per-user / per-item counts (DataSet.CountByUser/CountByItem, :134-150)
+__global__ __launch_bounds__(256) void count_kernel(const int32_t* __restrict__ users,
+                                                    const int32_t* __restrict__ items, int64_t n,
+                                                    int32_t n_users, int32_t n_items,
+                                                    int32_t* cnt_u, int32_t* cnt_i,
+                                                    int32_t* bad) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t u = users[x], i = items[x];
+        if (u < 0 || u >= n_users || i < 0 || i >= n_items) {
+            atomicOr(bad, 1);
+            continue;
+        }
+        atomicAdd(cnt_u + u, 1);
+        atomicAdd(cnt_i + i, 1);
+    }
+}
+
+// order must be a permutation-subset of [0, n): range check
+__global__ __launch_bounds__(256) void check_order_kernel(const int32_t* __restrict__ order,
+                                                          int64_t n_order, int64_t n,
+                                                          int32_t* bad) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n_order;
+         x += (int64_t)gridDim.x * blockDim.x)
+        if (order[x] < 0 || order[x] >= n) atomicOr(bad, 1);
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ a, int64_t n, float f) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x)
+        a[x] *= f;
+}
+
+inline int grid_for(int64_t n, int block = 256, int cap = 8192) {
+    const int64_t g = (n + block - 1) / block;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+inline int lanes_per_rating(int k) {
+    const int vec = (k + 3) / 4;
+    int lpr = 1;
+    while (lpr < vec) lpr <<= 1;
+    return lpr;
+}
+
+}  // namespace
+
+struct mml_bmf {
+    mml_ctx* ctx = nullptr;
+    mml_bmf_params p{};
+    int32_t n_users = 0, n_items = 0, k = 0, ld = 0, lpr = 0;
+    mml::DeviceArray<float> U, V, bu, bi;
+    mml::DeviceArray<int32_t> raw_u, raw_i, su, si, cnt_u, cnt_i, scratch_i32;
+    mml::DeviceArray<float> raw_r, sr;
+    mml::DeviceArray<int64_t> block_off, whole_off;
+    mml::DeviceArray<int32_t> ev_u, ev_i;
+    mml::DeviceArray<float> ev_r, ev_out;
+    mml::DeviceArray<double> ev_partials;
+    int64_t n = 0;
+    int32_t G = 0;
+    bool has_data = false, has_model = false;
+    float gb = 0.0f, min_rating = 0.0f, max_rating = 0.0f;
+    float last_ms = 0.0f;
+    int32_t last_launches = 0;
+};
+
+namespace {
+
+void check_handle(mml_bmf* h) { MML_REQUIRE(h && h->ctx, "null handle"); }
+
+// upload / download a [rows x k] host matrix into a [rows x ld] zero-padded device matrix
+void upload_padded(mml_bmf* h, float* dst, const float* src, int64_t rows) {
+    if (rows == 0) return;
+    MML_HIP(hipMemsetAsync(dst, 0, sizeof(float) * rows * h->ld, h->ctx->stream));
+    MML_HIP(hipMemcpy2DAsync(dst, sizeof(float) * h->ld, src, sizeof(float) * h->k,
+                             sizeof(float) * h->k, rows, hipMemcpyHostToDevice, h->ctx->stream));
+}
+
+void download_padded(mml_bmf* h, float* dst, const float* src, int64_t rows) {
+    if (rows == 0) return;
+    MML_HIP(hipMemcpy2DAsync(dst, sizeof(float) * h->k, src, sizeof(float) * h->ld,
+                             sizeof(float) * h->k, rows, hipMemcpyDeviceToHost, h->ctx->stream));
+}
+
+void finish_data(mml_bmf* h, const int32_t* order_dev) {
+    hipStream_t st = h->ctx->stream;
+    const int64_t n = h->n;
+    h->su.alloc(n);
+    h->si.alloc(n);
+    h->sr.alloc(n);
+    h->cnt_u.alloc(h->n_users);
+    h->cnt_i.alloc(h->n_items);
+    h->scratch_i32.alloc(1);
+    MML_HIP(hipMemsetAsync(h->cnt_u.get(), 0, sizeof(int32_t) * h->n_users, st));
+    MML_HIP(hipMemsetAsync(h->cnt_i.get(), 0, sizeof(int32_t) * h->n_items, st));
+    MML_HIP(hipMemsetAsync(h->scratch_i32.get(), 0, sizeof(int32_t), st));
+    if (n > 0) {
+        count_kernel<<<grid_for(n), 256, 0, st>>>(h->raw_u.get(), h->raw_i.get(), n, h->n_users,
+                                                   h->n_items, h->cnt_u.get(), h->cnt_i.get(),
+                                                   h->scratch_i32.get());
+        MML_HIP(hipGetLastError());
+        if (order_dev) {
+            check_order_kernel<<<grid_for(n), 256, 0, st>>>(order_dev, n, n,
+                                                             h->scratch_i32.get());
+            MML_HIP(hipGetLastError());
+        }
+    }
+    int32_t bad = 0;
+    MML_HIP(hipMemcpyAsync(&bad, h->scratch_i32.get(), sizeof(int32_t), hipMemcpyDeviceToHost,
+                           st));
+    MML_HIP(hipStreamSynchronize(st));
+    if (bad) {
+        h->has_data = false;
+        mml::fail(MML_ERR_ARG, "rating user/item id or order index out of range");
+    }
+    if (n > 0) {
+        gather_stream_kernel<<<grid_for(n), 256, 0, st>>>(h->raw_u.get(), h->raw_i.get(),
+                                                          h->raw_r.get(), order_dev, n,
+                                                          h->su.get(), h->si.get(), h->sr.get());
+        MML_HIP(hipGetLastError());
+    }
+    h->whole_off.alloc(2);
+    const int64_t off[2] = {0, n};
+    MML_HIP(hipMemcpyAsync(h->whole_off.get(), off, sizeof(off), hipMemcpyHostToDevice, st));
+    MML_HIP(hipStreamSynchronize(st));
+    h->G = 0;
+    h->has_data = true;
+}
+
+template <int LOSS>
+void launch_ordered(mml_bmf* h, const int64_t* off, int32_t G, int32_t sub, int grid,
+                    const BmfScalars& s, const int32_t* cu, const int32_t* ci) {
+    const int km = (h->k + 63) / 64;
+    hipStream_t st = h->ctx->stream;
+#define MML_ORD(KM)                                                                            \
+    bmf_sgd_ordered_kernel<LOSS, KM><<<grid, 64, 0, st>>>(h->su.get(), h->si.get(), h->sr.get(), \
+                                                          off, G, sub, h->U.get(), h->V.get(),  \
+                                                          h->bu.get(), h->bi.get(), h->k, h->ld, \
+                                                          s, cu, ci)
+    switch (km) {
+        case 1: MML_ORD(1); break;
+        case 2: MML_ORD(2); break;
+        case 3: MML_ORD(3); break;
+        default: MML_ORD(4); break;
+    }
+#undef MML_ORD
+    MML_HIP(hipGetLastError());
+}
+
+template <int LOSS>
+void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const int32_t* ci) {
+    hipStream_t st = h->ctx->stream;
+    const int64_t n = h->n;
+    // waves: enough to fill 256 CUs x 32 waves, but at least ~64 ratings per wave
+    const int64_t max_waves = 256 * 32;
+    int64_t waves = std::min<int64_t>(max_waves, std::max<int64_t>(1, (n + 63) / 64));
+    const int64_t blocks = (waves + 3) / 4;
+    waves = blocks * 4;
+    const int64_t chunk = (n + waves - 1) / waves;
+    const int ld4 = h->ld / 4;
+#define MML_HOG(LPR)                                                                           \
+    bmf_sgd_hogwild_kernel<LOSS, LPR><<<(int)blocks, 256, 0, st>>>(                          \
+        h->su.get(), h->si.get(), h->sr.get(), n, chunk, h->U.get(), h->V.get(), h->bu.get(),  \
+        h->bi.get(), ld4, s, cu, ci)
+    switch (h->lpr) {
+        case 1: MML_HOG(1); break;
+        case 2: MML_HOG(2); break;
+        case 4: MML_HOG(4); break;
+        case 8: MML_HOG(8); break;
+        case 16: MML_HOG(16); break;
+        case 32: MML_HOG(32); break;
+        default: MML_HOG(64); break;
+    }
+#undef MML_HOG
+    MML_HIP(hipGetLastError());
+}
+
+template <int LOSS>
+void run_epoch(mml_bmf* h, const BmfScalars& s, const int32_t* seq) {
+    const int32_t* cu = h->p.frequency_regularization ? h->cnt_u.get() : nullptr;
+    const int32_t* ci = h->p.frequency_regularization ? h->cnt_i.get() : nullptr;
+    int launches = 0;
+    if (h->n == 0) {
+        h->last_launches = 0;
+        return;
+    }
+    switch (h->p.schedule) {
+        case MML_SCHEDULE_ORDERED:
+            launch_ordered<LOSS>(h, h->whole_off.get(), 1, 0, 1, s, cu, ci);
+            launches = 1;
+            break;
+        case MML_SCHEDULE_DSGD:
+            for (int32_t x = 0; x < h->G; ++x) {
+                launch_ordered<LOSS>(h, h->block_off.get(), h->G, seq[x], h->G, s, cu, ci);
+                ++launches;
+            }
+            break;
+        default:
+            launch_hogwild<LOSS>(h, s, cu, ci);
+            launches = 1;
+            break;
+    }
+    h->last_launches = launches;
+}
+
+}  // namespace
+
+using mml::guard;
+
+extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params, int32_t n_users,
+                                     int32_t n_items, mml_bmf** out) {
+    return guard([&] {
+        MML_REQUIRE(ctx && params && out, "null argument");
+        MML_REQUIRE(n_users >= 0 && n_items >= 0, "negative sizes");
+        MML_REQUIRE(params->num_factors >= 1 && params->num_factors <= 256,
+                    "num_factors must be in [1, 256]");
+        MML_REQUIRE(params->loss >= MML_LOSS_RMSE && params->loss <= MML_LOSS_LOGISTIC,
+                    "unknown loss");
+        MML_REQUIRE(params->schedule >= MML_SCHEDULE_ORDERED &&
+                        params->schedule <= MML_SCHEDULE_HOGWILD,
+                    "unknown schedule");
+        ctx->activate();
+        auto* h = new mml_bmf();
+        try {
+            h->ctx = ctx;
+            h->p = *params;
+            h->n_users = n_users;
+            h->n_items = n_items;
+            h->k = params->num_factors;
+            h->lpr = lanes_per_rating(h->k);
+            h->ld = 4 * h->lpr;
+            h->U.alloc((size_t)n_users * h->ld);
+            h->V.alloc((size_t)n_items * h->ld);
+            h->bu.alloc(n_users);
+            h->bi.alloc(n_items);
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+extern "C" mml_status mml_bmf_destroy(mml_bmf* h) {
+    return guard([&] {
+        if (!h) return;
+        (void)hipSetDevice(h->ctx->device);
+        (void)hipStreamSynchronize(h->ctx->stream);
+        delete h;
+    });
+}
+
+extern "C" mml_status mml_bmf_set_data(mml_bmf* h, const int32_t* users, const int32_t* items,
+                                       const float* values, int64_t n, const int32_t* order) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(n >= 0 && n <= INT32_MAX, "rating count out of range");
+        MML_REQUIRE(n == 0 || (users && items && values), "null rating arrays");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        h->has_data = false;
+        h->n = n;
+        h->raw_u.alloc(n);
+        h->raw_i.alloc(n);
+        h->raw_r.alloc(n);
+        mml::DeviceArray<int32_t> ord;
+        if (n > 0) {
+            MML_HIP(hipMemcpyAsync(h->raw_u.get(), users, sizeof(int32_t) * n,
+                                   hipMemcpyHostToDevice, st));
+            MML_HIP(hipMemcpyAsync(h->raw_i.get(), items, sizeof(int32_t) * n,
+                                   hipMemcpyHostToDevice, st));
+            MML_HIP(hipMemcpyAsync(h->raw_r.get(), values, sizeof(float) * n,
+                                   hipMemcpyHostToDevice, st));
+            if (order) {
+                ord.alloc(n);
+                MML_HIP(hipMemcpyAsync(ord.get(), order, sizeof(int32_t) * n,
+                                       hipMemcpyHostToDevice, st));
+            }
+        }
+        finish_data(h, order ? ord.get() : nullptr);
+    });
+}
+
+extern "C" mml_status mml_bmf_set_data_device(mml_bmf* h, const int32_t* users,
+                                              const int32_t* items, const float* values,
+                                              int64_t n, const int32_t* order) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(n >= 0 && n <= INT32_MAX, "rating count out of range");
+        MML_REQUIRE(n == 0 || (users && items && values), "null rating arrays");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        h->has_data = false;
+        h->n = n;
+        h->raw_u.alloc(n);
+        h->raw_i.alloc(n);
+        h->raw_r.alloc(n);
+        if (n > 0) {
+            MML_HIP(hipMemcpyAsync(h->raw_u.get(), users, sizeof(int32_t) * n,
+                                   hipMemcpyDeviceToDevice, st));
+            MML_HIP(hipMemcpyAsync(h->raw_i.get(), items, sizeof(int32_t) * n,
+                                   hipMemcpyDeviceToDevice, st));
+            MML_HIP(hipMemcpyAsync(h->raw_r.get(), values, sizeof(float) * n,
+                                   hipMemcpyDeviceToDevice, st));
+        }
+        finish_data(h, order);
+    });
+}
+
+extern "C" mml_status mml_bmf_set_blocks(mml_bmf* h, int32_t num_groups, const int64_t* offsets,
+                                         const int32_t* indices) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->has_data, "set_data must precede set_blocks");
+        MML_REQUIRE(num_groups >= 1 && offsets, "bad block arguments");
+        const int64_t nb = (int64_t)num_groups * num_groups;
+        MML_REQUIRE(offsets[0] == 0, "offsets[0] must be 0");
+        for (int64_t b = 0; b < nb; ++b)
+            MML_REQUIRE(offsets[b + 1] >= offsets[b], "offsets must be non-decreasing");
+        const int64_t total = offsets[nb];
+        MML_REQUIRE(total <= h->n && (total == 0 || indices), "block indices exceed ratings");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        mml::DeviceArray<int32_t> ord;
+        ord.alloc(total);
+        if (total > 0)
+            MML_HIP(hipMemcpyAsync(ord.get(), indices, sizeof(int32_t) * total,
+                                   hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemsetAsync(h->scratch_i32.get(), 0, sizeof(int32_t), st));
+        if (total > 0) {
+            check_order_kernel<<<grid_for(total), 256, 0, st>>>(ord.get(), total, h->n,
+                                                                h->scratch_i32.get());
+            MML_HIP(hipGetLastError());
+        }
+        int32_t bad = 0;
+        MML_HIP(hipMemcpyAsync(&bad, h->scratch_i32.get(), sizeof(int32_t), hipMemcpyDeviceToHost,
+                               st));
+        MML_HIP(hipStreamSynchronize(st));
+        MML_REQUIRE(!bad, "block index out of range");
+        if (total > 0) {
+            gather_stream_kernel<<<grid_for(total), 256, 0, st>>>(
+                h->raw_u.get(), h->raw_i.get(), h->raw_r.get(), ord.get(), total, h->su.get(),
+                h->si.get(), h->sr.get());
+            MML_HIP(hipGetLastError());
+        }
+        h->block_off.alloc(nb + 1);
+        MML_HIP(hipMemcpyAsync(h->block_off.get(), offsets, sizeof(int64_t) * (nb + 1),
+                               hipMemcpyHostToDevice, st));
+        MML_HIP(hipStreamSynchronize(st));
+        h->G = num_groups;
+    });
+}
+
+extern "C" mml_status mml_bmf_set_model(mml_bmf* h, const float* U, const float* V,
+                                        const float* bu, const float* bi, float global_bias,
+                                        float min_rating, float max_rating) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE((h->n_users == 0 || (U && bu)) && (h->n_items == 0 || (V && bi)),
+                    "null model arrays");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        upload_padded(h, h->U.get(), U, h->n_users);
+        upload_padded(h, h->V.get(), V, h->n_items);
+        if (h->n_users)
+            MML_HIP(hipMemcpyAsync(h->bu.get(), bu, sizeof(float) * h->n_users,
+                                   hipMemcpyHostToDevice, st));
+        if (h->n_items)
+            MML_HIP(hipMemcpyAsync(h->bi.get(), bi, sizeof(float) * h->n_items,
+                                   hipMemcpyHostToDevice, st));
+        MML_HIP(hipStreamSynchronize(st));
+        h->gb = global_bias;
+        h->min_rating = min_rating;
+        h->max_rating = max_rating;
+        h->has_model = true;
+    });
+}
+
+extern "C" mml_status mml_bmf_get_model(mml_bmf* h, float* U, float* V, float* bu, float* bi) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->has_model, "no model (set_model first)");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        if (U) download_padded(h, U, h->U.get(), h->n_users);
+        if (V) download_padded(h, V, h->V.get(), h->n_items);
+        if (bu && h->n_users)
+            MML_HIP(hipMemcpyAsync(bu, h->bu.get(), sizeof(float) * h->n_users,
+                                   hipMemcpyDeviceToHost, st));
+        if (bi && h->n_items)
+            MML_HIP(hipMemcpyAsync(bi, h->bi.get(), sizeof(float) * h->n_items,
+                                   hipMemcpyDeviceToHost, st));
+        MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
+                                      const int32_t* subepoch_sequence) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
+        if (h->p.schedule == MML_SCHEDULE_DSGD) {
+            MML_REQUIRE(h->G > 0, "DSGD schedule needs set_blocks");
+            MML_REQUIRE(subepoch_sequence, "DSGD schedule needs a sub-epoch sequence");
+            for (int32_t x = 0; x < h->G; ++x)
+                MML_REQUIRE(subepoch_sequence[x] >= 0 && subepoch_sequence[x] < h->G,
+                            "sub-epoch index out of range");
+        }
+        h->ctx->activate();
+        BmfScalars s;
+        s.gb = h->gb;
+        s.min_rating = h->min_rating;
+        s.range = h->max_rating - h->min_rating;
+        s.lr = learn_rate;
+        s.blr = h->p.bias_learn_rate * learn_rate;
+        s.bias_reg = h->p.bias_reg;
+        s.reg_u = h->p.reg_u;
+        s.reg_i = h->p.reg_i;
+        hipStream_t st = h->ctx->stream;
+        MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
+        switch (h->p.loss) {
+            case MML_LOSS_MAE: run_epoch<MML_LOSS_MAE>(h, s, subepoch_sequence); break;
+            case MML_LOSS_LOGISTIC: run_epoch<MML_LOSS_LOGISTIC>(h, s, subepoch_sequence); break;
+            default: run_epoch<MML_LOSS_RMSE>(h, s, subepoch_sequence); break;
+        }
+        MML_HIP(hipEventRecord(h->ctx->ev_end, st));
+        MML_HIP(hipEventSynchronize(h->ctx->ev_end));
+        MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));
+    });
+}
+
+extern "C" mml_status mml_bmf_last_timing(mml_bmf* h, float* out) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(out, "out is null");
+        out[0] = h->last_ms;
+        out[1] = (float)h->last_launches;
+    });
+}
+
+namespace {
+void upload_pairs(mml_bmf* h, const int32_t* users, const int32_t* items, int64_t n) {
+    hipStream_t st = h->ctx->stream;
+    h->ev_u.alloc(n);
+    h->ev_i.alloc(n);
+    MML_HIP(hipMemcpyAsync(h->ev_u.get(), users, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+    MML_HIP(hipMemcpyAsync(h->ev_i.get(), items, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+}
+}  // namespace
+
+extern "C" mml_status mml_bmf_predict(mml_bmf* h, const int32_t* users, const int32_t* items,
+                                      int64_t n, float* out) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(n >= 0 && (n == 0 || (users && items && out)), "bad arguments");
+        if (n == 0) return;
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        upload_pairs(h, users, items, n);
+        h->ev_out.alloc(n);
+        bmf_predict_kernel<<<grid_for(n), 256, 0, st>>>(
+            h->ev_u.get(), h->ev_i.get(), n, h->n_users, h->n_items, h->U.get(), h->V.get(),
+            h->bu.get(), h->bi.get(), h->k, h->ld, h->gb, h->min_rating,
+            h->max_rating - h->min_rating, h->ev_out.get());
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipMemcpyAsync(out, h->ev_out.get(), sizeof(float) * n, hipMemcpyDeviceToHost,
+                               st));
+        MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+extern "C" mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const int32_t* items,
+                                       const float* values, int64_t n, float* out) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(n > 0 && users && items && values && out, "bad arguments");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        upload_pairs(h, users, items, n);
+        h->ev_r.alloc(n);
+        MML_HIP(hipMemcpyAsync(h->ev_r.get(), values, sizeof(float) * n, hipMemcpyHostToDevice,
+                               st));
+        const int grid = grid_for(n, 256, 1024);
+        h->ev_partials.alloc(2 * grid);
+        bmf_eval_kernel<<<grid, 256, 0, st>>>(h->ev_u.get(), h->ev_i.get(), h->ev_r.get(), n,
+                                              h->n_users, h->n_items, h->U.get(), h->V.get(),
+                                              h->bu.get(), h->bi.get(), h->k, h->ld, h->gb,
+                                              h->min_rating, h->max_rating - h->min_rating,
+                                              h->ev_partials.get());
+        MML_HIP(hipGetLastError());
+        std::vector<double> part(2 * grid);
+        MML_HIP(hipMemcpyAsync(part.data(), h->ev_partials.get(), sizeof(double) * 2 * grid,
+                               hipMemcpyDeviceToHost, st));
+        MML_HIP(hipStreamSynchronize(st));
+        double se = 0.0, ae = 0.0;
+        for (int b = 0; b < grid; ++b) {
+            se += part[2 * b];
+            ae += part[2 * b + 1];
+        }
+        out[0] = (float)std::sqrt(se / (double)n);
+        out[1] = (float)(ae / (double)n);
+    });
+}
+
+extern "C" mml_status mml_bmf_allreduce_items(mml_bmf* h) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->has_model, "no model");
+        mml_ctx* c = h->ctx;
+        if (c->nranks <= 1) return;
+        MML_REQUIRE(c->comm, "context has no communicator (mml_ctx_comm_init)");
+        c->activate();
+        hipStream_t st = c->stream;
+        const size_t nv = (size_t)h->n_items * h->ld;
+        MML_RCCL(ncclGroupStart());
+        MML_RCCL(ncclAllReduce(h->V.get(), h->V.get(), nv, ncclFloat, ncclSum, c->comm, st));
+        MML_RCCL(ncclAllReduce(h->bi.get(), h->bi.get(), (size_t)h->n_items, ncclFloat, ncclSum,
+                               c->comm, st));
+        MML_RCCL(ncclGroupEnd());
+        const float f = 1.0f / (float)c->nranks;
+        scale_kernel<<<grid_for((int64_t)nv), 256, 0, st>>>(h->V.get(), (int64_t)nv, f);
+        scale_kernel<<<grid_for(h->n_items), 256, 0, st>>>(h->bi.get(), h->n_items, f);
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipStreamSynchronize(st));
+    });
+}

@@ -1,0 +1,229 @@
+// mml_core.cpp -- library-level entry points: errors, devices, contexts, RCCL communicators,
+// and the host-side MyMediaLite.Random / Utils.Shuffle / MultiCore equivalents that a non-.NET
+// host needs to drive the path with the reference's RNG semantics.
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "mml_internal.h"
+
+namespace mml {
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+}  // namespace mml
+
+using mml::guard;
+
+extern "C" int mml_abi_version(void) { return MML_ABI_VERSION; }
+
+extern "C" const char* mml_last_error(void) { return mml::g_last_error.c_str(); }
+
+extern "C" mml_status mml_device_count(int32_t* out) {
+    return guard([&] {
+        MML_REQUIRE(out, "out is null");
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        if (e != hipSuccess) n = 0;
+        *out = n;
+    });
+}
+
+extern "C" mml_status mml_ctx_create(int32_t device_id, mml_ctx** out) {
+    return guard([&] {
+        MML_REQUIRE(out, "out is null");
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+            mml::fail(MML_ERR_NODEV, "no HIP device visible");
+        MML_REQUIRE(device_id >= 0 && device_id < n, "device_id out of range");
+        hipDeviceProp_t prop;
+        MML_HIP(hipGetDeviceProperties(&prop, device_id));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            mml::fail(MML_ERR_NODEV, std::string("libmml_hip is built for gfx950, device is ") +
+                                         prop.gcnArchName);
+        auto* ctx = new mml_ctx();
+        ctx->device = device_id;
+        try {
+            ctx->activate();
+            MML_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+            MML_HIP(hipEventCreate(&ctx->ev_begin));
+            MML_HIP(hipEventCreate(&ctx->ev_end));
+        } catch (...) {
+            delete ctx;
+            throw;
+        }
+        *out = ctx;
+    });
+}
+
+extern "C" mml_status mml_ctx_destroy(mml_ctx* ctx) {
+    return guard([&] {
+        if (!ctx) return;
+        (void)hipSetDevice(ctx->device);
+        if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+        if (ctx->ev_begin) (void)hipEventDestroy(ctx->ev_begin);
+        if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
+        if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+        delete ctx;
+    });
+}
+
+extern "C" mml_status mml_comm_unique_id(uint8_t out_id[128]) {
+    return guard([&] {
+        MML_REQUIRE(out_id, "out_id is null");
+        static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+        ncclUniqueId id;
+        MML_RCCL(ncclGetUniqueId(&id));
+        std::memcpy(out_id, &id, 128);
+    });
+}
+
+extern "C" mml_status mml_ctx_comm_init(mml_ctx* ctx, const uint8_t id[128], int32_t nranks,
+                                        int32_t rank) {
+    return guard([&] {
+        MML_REQUIRE(ctx && id, "null argument");
+        MML_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
+        ctx->activate();
+        if (ctx->comm) {
+            (void)ncclCommDestroy(ctx->comm);
+            ctx->comm = nullptr;
+        }
+        ncclUniqueId uid;
+        std::memcpy(&uid, id, 128);
+        MML_RCCL(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
+        ctx->nranks = nranks;
+        ctx->rank = rank;
+    });
+}
+
+// --------------------------------------------------------------------------------------------
+// System.Random(int) -- Knuth subtractive generator of the .NET reference source, as used through
+// MyMediaLite.Random (src/MyMediaLite/Random.cs:23-64).
+struct mml_random {
+    int32_t seeds[56];
+    int32_t inext = 0, inextp = 21;
+
+    explicit mml_random(int32_t seed) {
+        constexpr int32_t kBig = 2147483647, kSeed = 161803398;
+        const int32_t sub = seed == INT32_MIN ? INT32_MAX : std::abs(seed);
+        int32_t mj = kSeed - sub, mk = 1;
+        seeds[55] = mj;
+        for (int i = 1; i < 55; ++i) {
+            const int ii = (21 * i) % 55;
+            seeds[ii] = mk;
+            mk = mj - mk;
+            if (mk < 0) mk += kBig;
+            mj = seeds[ii];
+        }
+        for (int pass = 0; pass < 4; ++pass)
+            for (int i = 1; i < 56; ++i) {
+                seeds[i] -= seeds[1 + (i + 30) % 55];
+                if (seeds[i] < 0) seeds[i] += kBig;
+            }
+        seeds[0] = 0;
+    }
+    int32_t sample_int() {
+        constexpr int32_t kBig = 2147483647;
+        if (++inext >= 56) inext = 1;
+        if (++inextp >= 56) inextp = 1;
+        int32_t v = seeds[inext] - seeds[inextp];
+        if (v == kBig) --v;
+        if (v < 0) v += kBig;
+        seeds[inext] = v;
+        return v;
+    }
+    double next_double() { return sample_int() * (1.0 / 2147483647.0); }
+    int32_t next(int32_t max_value) { return static_cast<int32_t>(next_double() * max_value); }
+    // MathNet.Numerics 3.15 Normal.SampleUnchecked: polar transform, first variate returned.
+    double normal(double mean, double stddev) {
+        for (;;) {
+            const double v1 = 2.0 * next_double() - 1.0;
+            const double v2 = 2.0 * next_double() - 1.0;
+            const double r = v1 * v1 + v2 * v2;
+            if (r >= 1.0 || r == 0.0) continue;
+            return mean + stddev * (v1 * std::sqrt(-2.0 * std::log(r) / r));
+        }
+    }
+    void shuffle(int32_t* a, int64_t n) {
+        for (int64_t i = n - 1; i >= 0; --i) {
+            const int32_t j = next(static_cast<int32_t>(i + 1));
+            std::swap(a[i], a[j]);
+        }
+    }
+};
+
+extern "C" mml_status mml_random_create(int32_t seed, mml_random** out) {
+    return guard([&] {
+        MML_REQUIRE(out, "out is null");
+        *out = new mml_random(seed);
+    });
+}
+
+extern "C" mml_status mml_random_destroy(mml_random* r) {
+    return guard([&] { delete r; });
+}
+
+extern "C" mml_status mml_random_next(mml_random* r, int32_t max_value, int32_t* out) {
+    return guard([&] {
+        MML_REQUIRE(r && out, "null argument");
+        MML_REQUIRE(max_value >= 0, "max_value must be >= 0");
+        *out = r->next(max_value);
+    });
+}
+
+extern "C" mml_status mml_random_next_double(mml_random* r, double* out) {
+    return guard([&] {
+        MML_REQUIRE(r && out, "null argument");
+        *out = r->next_double();
+    });
+}
+
+extern "C" mml_status mml_random_fill_normal(mml_random* r, double mean, double stddev,
+                                             float* out, int64_t n) {
+    return guard([&] {
+        MML_REQUIRE(r && (out || n == 0) && n >= 0, "bad argument");
+        for (int64_t i = 0; i < n; ++i) out[i] = static_cast<float>(r->normal(mean, stddev));
+    });
+}
+
+extern "C" mml_status mml_random_shuffle_i32(mml_random* r, int32_t* a, int64_t n) {
+    return guard([&] {
+        MML_REQUIRE(r && (a || n == 0) && n >= 0 && n <= INT32_MAX, "bad argument");
+        r->shuffle(a, n);
+    });
+}
+
+extern "C" mml_status mml_partition_users_and_items(mml_random* r, const int32_t* users,
+                                                    const int32_t* items, int64_t n,
+                                                    int32_t max_user_id, int32_t max_item_id,
+                                                    int32_t num_groups, int64_t* offsets,
+                                                    int32_t* indices, int32_t* out_groups) {
+    return guard([&] {
+        MML_REQUIRE(r && offsets && out_groups && (n == 0 || (users && items && indices)),
+                    "null argument");
+        MML_REQUIRE(num_groups >= 1 && max_user_id >= 0 && max_item_id >= 0, "bad sizes");
+        int32_t G = std::min(num_groups, max_user_id + 1);
+        G = std::min(G, max_item_id + 1);
+        std::vector<int32_t> up(max_user_id + 1), ip(max_item_id + 1);
+        std::iota(up.begin(), up.end(), 0);
+        std::iota(ip.begin(), ip.end(), 0);
+        r->shuffle(up.data(), static_cast<int64_t>(up.size()));
+        r->shuffle(ip.data(), static_cast<int64_t>(ip.size()));
+        const int64_t nb = static_cast<int64_t>(G) * G;
+        std::vector<int64_t> cnt(nb + 1, 0);
+        std::vector<int32_t> blk(n);
+        for (int64_t x = 0; x < n; ++x) {
+            MML_REQUIRE(users[x] >= 0 && users[x] <= max_user_id && items[x] >= 0 &&
+                            items[x] <= max_item_id,
+                        "rating id out of range");
+            blk[x] = static_cast<int32_t>((up[users[x]] % G) * G + ip[items[x]] % G);
+            ++cnt[blk[x] + 1];
+        }
+        for (int64_t b = 0; b < nb; ++b) cnt[b + 1] += cnt[b];
+        std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
+        for (int64_t x = 0; x < n; ++x) indices[fill[blk[x]]++] = static_cast<int32_t>(x);
+        for (int64_t b = 0; b < nb; ++b) r->shuffle(indices + cnt[b], cnt[b + 1] - cnt[b]);
+        std::memcpy(offsets, cnt.data(), sizeof(int64_t) * (nb + 1));
+        *out_groups = G;
+    });
+}

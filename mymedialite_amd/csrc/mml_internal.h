@@ -1,0 +1,99 @@
+// mml_internal.h -- shared plumbing of libmml_hip.so: status/exception bridge, device buffers,
+// the context (one GPU, one HIP stream, optional RCCL communicator).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <exception>
+#include <new>
+#include <string>
+
+#include "mml.h"
+
+namespace mml {
+
+struct Error : std::exception {
+    mml_status code;
+    std::string msg;
+    Error(mml_status c, std::string m) : code(c), msg(std::move(m)) {}
+    const char* what() const noexcept override { return msg.c_str(); }
+};
+
+void set_error(const std::string& msg);
+
+// Runs f(); converts any exception into a status + thread-local message (never aborts the host).
+template <class F>
+mml_status guard(F&& f) {
+    try {
+        f();
+        return MML_OK;
+    } catch (const Error& e) {
+        set_error(e.msg);
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        set_error("host allocation failed");
+        return MML_ERR_OOM;
+    } catch (const std::exception& e) {
+        set_error(e.what());
+        return MML_ERR_STATE;
+    }
+}
+
+[[noreturn]] inline void fail(mml_status code, const std::string& msg) { throw Error(code, msg); }
+
+inline void hip_check(hipError_t e, const char* what) {
+    if (e == hipSuccess) return;
+    (void)hipGetLastError();  // clear sticky launch error state where possible
+    fail(e == hipErrorOutOfMemory ? MML_ERR_OOM : MML_ERR_HIP,
+         std::string(what) + ": " + hipGetErrorString(e));
+}
+#define MML_HIP(call) ::mml::hip_check((call), #call)
+
+inline void rccl_check(ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return;
+    fail(MML_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
+}
+#define MML_RCCL(call) ::mml::rccl_check((call), #call)
+
+#define MML_REQUIRE(cond, msg) \
+    do {                       \
+        if (!(cond)) ::mml::fail(MML_ERR_ARG, (msg)); \
+    } while (0)
+
+// Owning device allocation (HBM of the context's device).
+template <class T>
+struct DeviceArray {
+    T* ptr = nullptr;
+    size_t count = 0;
+    DeviceArray() = default;
+    DeviceArray(const DeviceArray&) = delete;
+    DeviceArray& operator=(const DeviceArray&) = delete;
+    ~DeviceArray() { reset(); }
+    void reset() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        count = 0;
+    }
+    void alloc(size_t n) {
+        if (n == count && ptr) return;
+        reset();
+        if (n == 0) return;
+        MML_HIP(hipMalloc(reinterpret_cast<void**>(&ptr), n * sizeof(T)));
+        count = n;
+    }
+    T* get() const { return ptr; }
+};
+
+}  // namespace mml
+
+struct mml_ctx {
+    int32_t device = 0;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    int32_t nranks = 1;
+    int32_t rank = 0;
+    hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    void activate() const { MML_HIP(hipSetDevice(device)); }
+};

@@ -1,0 +1,299 @@
+"""GPU-backed MyMediaLite.RatingPrediction.BiasedMatrixFactorization (host mirror).
+
+Same public properties, defaults, Train()/Iterate()/Predict() contract and RNG consumption order
+as the reference (src/MyMediaLite/RatingPrediction/BiasedMatrixFactorization.cs:77-562 and
+MatrixFactorization.cs:50-418); the per-rating SGD loop runs in libmml_hip.so on the MI355X.
+
+Schedule (GPU-only property):
+  * ``auto``    -> MaxThreads <= 1: ``ordered`` (the reference's sequential loop, exact);
+                   MaxThreads > 1: ``dsgd`` (the reference's DSGD blocks, exact) or, with
+                   NaiveParallelization, ``hogwild`` (the reference's racy mode);
+  * ``ordered`` / ``dsgd`` / ``hogwild`` to force one.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import _native as N
+from .data import Ratings
+from .random import Random
+from .recommender import Recommender
+
+_LOSS = {"RMSE": N.LOSS_RMSE, "MAE": N.LOSS_MAE, "LogisticLoss": N.LOSS_LOGISTIC}
+_SCHED = {"ordered": N.SCHEDULE_ORDERED, "dsgd": N.SCHEDULE_DSGD, "hogwild": N.SCHEDULE_HOGWILD}
+
+
+class BiasedMatrixFactorization(Recommender):
+    PROPERTIES = {
+        "BiasLearnRate": "float", "BiasReg": "float", "BoldDriver": "bool", "Decay": "float",
+        "Device": "int", "FrequencyRegularization": "bool", "InitMean": "double",
+        "InitStdDev": "double", "LearnRate": "float", "Loss": tuple(_LOSS), "MaxThreads": "int",
+        "NaiveParallelization": "bool", "NumFactors": "uint", "NumIter": "uint",
+        "RegI": "float", "RegU": "float", "Regularization": "float", "Schedule": "string",
+    }
+
+    def __init__(self, **kw):
+        # MatrixFactorization() defaults (MatrixFactorization.cs:87-96)
+        self.LearnRate = 0.01
+        self.Decay = 1.0
+        self.NumIter = 30
+        self.InitMean = 0.0
+        self.InitStdDev = 0.1
+        self.NumFactors = 10
+        # BiasedMatrixFactorization defaults (:85-141)
+        self.BiasLearnRate = 1.0
+        self.BiasReg = 0.01
+        self.RegU = 0.0
+        self.RegI = 0.0
+        self.Regularization = 0.015
+        self.FrequencyRegularization = False
+        self.Loss = "RMSE"
+        self.MaxThreads = 1
+        self.BoldDriver = False
+        self.NaiveParallelization = False
+        # GPU
+        self.Schedule = "auto"
+        self.Device = 0
+        for k, v in kw.items():
+            setattr(self, k, v)
+        self._ratings = None
+        self._ctx = None
+        self._h = None
+        self._host = None  # cached host copy of the model
+        self.current_learnrate = float(np.float32(self.LearnRate))
+        self.global_bias = 0.0
+        self.min_rating = 0.0
+        self.max_rating = 0.0
+        self._thread_blocks = None
+        self._order_uploaded = False
+
+    # Regularization setter also sets RegU and RegI (:97-104)
+    @property
+    def Regularization(self):
+        return self._regularization
+
+    @Regularization.setter
+    def Regularization(self, v):
+        self._regularization = v
+        self.RegU = v
+        self.RegI = v
+
+    # ------------------------------------------------------------------ data
+    @property
+    def ratings(self) -> Ratings:
+        return self._ratings
+
+    @ratings.setter
+    def ratings(self, r: Ratings):
+        """RatingPredictor.Ratings setter (RatingPrediction/RatingPredictor.cs:39-49)."""
+        self._ratings = r
+        self.MaxUserID = r.max_user_id
+        self.MaxItemID = r.max_item_id
+        self.min_rating = r.scale_min
+        self.max_rating = r.scale_max
+
+    def schedule(self) -> str:
+        if self.Schedule != "auto":
+            if self.Schedule not in _SCHED:
+                raise ValueError(f"unknown Schedule '{self.Schedule}'")
+            return self.Schedule
+        if self.NaiveParallelization and self.MaxThreads > 1:
+            return "hogwild"
+        return "dsgd" if self.MaxThreads > 1 else "ordered"
+
+    # ------------------------------------------------------------------ model
+    def _params(self) -> N.BmfParams:
+        f = lambda x: float(np.float32(x))
+        return N.BmfParams(int(self.NumFactors), _LOSS[self.Loss], int(self.FrequencyRegularization),
+                           _SCHED[self.schedule()], f(self.BiasLearnRate), f(self.BiasReg),
+                           f(self.RegU), f(self.RegI))
+
+    def init_model(self):
+        """InitModel (MatrixFactorization.cs:99-116 + BiasedMatrixFactorization.cs:161-170)."""
+        if self.BoldDriver:
+            raise NotImplementedError("BoldDriver is not supported on the GPU path yet")
+        r = self._ratings
+        k = int(self.NumFactors)
+        nu, ni = self.MaxUserID + 1, self.MaxItemID + 1
+        rng = Random.get_instance()
+        U = rng.fill_normal(nu * k, self.InitMean, self.InitStdDev).reshape(nu, k)
+        V = rng.fill_normal(ni * k, self.InitMean, self.InitStdDev).reshape(ni, k)
+        U[r.count_by_user == 0] = 0.0
+        V[r.count_by_item == 0] = 0.0
+        bu = np.zeros(nu, np.float32)
+        bi = np.zeros(ni, np.float32)
+        self.current_learnrate = float(np.float32(self.LearnRate))
+        self._release()
+        self._ctx = N.Context(self.Device)
+        h = N._vp()
+        N.check(N.lib().mml_bmf_create(self._ctx.handle, N.ctypes.byref(self._params()), nu, ni,
+                                       N.ctypes.byref(h)))
+        self._h = h
+        self._order_uploaded = False
+        self._host = dict(U=U, V=V, bu=bu, bi=bi)
+        self._upload_model(0.0)
+
+    def _upload_model(self, global_bias):
+        m = self._host
+        N.check(N.lib().mml_bmf_set_model(
+            self._h, N.ptr(N.f32(m["U"]), N._f32p), N.ptr(N.f32(m["V"]), N._f32p),
+            N.ptr(m["bu"], N._f32p), N.ptr(m["bi"], N._f32p), float(global_bias),
+            float(self.min_rating), float(self.max_rating)))
+
+    def train(self):
+        """Train() (:173-194)."""
+        self.init_model()
+        r = self._ratings
+        sched = self.schedule()
+        if self.MaxThreads > 1:
+            if self.NaiveParallelization:
+                _ = r.random_index  # PartitionIndices draws RandomIndex here (MultiCore.cs:79-92)
+            elif sched == "dsgd":
+                self._partition(int(self.MaxThreads))
+        rng_size = float(np.float32(np.float32(self.max_rating) - np.float32(self.min_rating)))
+        avg = np.float32(np.float32(np.float32(r.average) - np.float32(self.min_rating)) /
+                         np.float32(rng_size))
+        self.global_bias = float(np.float32(math.log(float(avg) / (1.0 - float(avg)))))
+        self._upload_model(self.global_bias)
+        self._host = None
+        for _ in range(int(self.NumIter)):
+            self.iterate()
+
+    def _partition(self, num_groups):
+        """MultiCore.PartitionUsersAndItems (MultiCore.cs:43-73) via the library's twin."""
+        r = self._ratings
+        rng = Random.get_instance()
+        off = np.zeros(num_groups * num_groups + 1, np.int64)
+        idx = np.zeros(r.count, np.int32)
+        g = N.ctypes.c_int32()
+        N.check(N.lib().mml_partition_users_and_items(
+            rng.handle, N.ptr(r.users, N._i32p), N.ptr(r.items, N._i32p), r.count,
+            self.MaxUserID, self.MaxItemID, num_groups, N.ptr(off, N._i64p),
+            N.ptr(idx, N._i32p), N.ctypes.byref(g)))
+        G = g.value
+        self._thread_blocks = (G, off[: G * G + 1].copy(), idx)
+
+    def _ensure_data(self):
+        if self._order_uploaded:
+            return
+        r = self._ratings
+        sched = self.schedule()
+        if sched == "dsgd":
+            if self._thread_blocks is None:
+                self._partition(max(2, int(self.MaxThreads)))
+            N.check(N.lib().mml_bmf_set_data(self._h, N.ptr(r.users, N._i32p),
+                                             N.ptr(r.items, N._i32p), N.ptr(r.values, N._f32p),
+                                             r.count, None))
+            G, off, idx = self._thread_blocks
+            N.check(N.lib().mml_bmf_set_blocks(self._h, G, N.ptr(off, N._i64p),
+                                               N.ptr(idx, N._i32p)))
+        else:
+            order = r.random_index  # DataSet.RandomIndex: shuffled ONCE, reused every epoch
+            N.check(N.lib().mml_bmf_set_data(self._h, N.ptr(r.users, N._i32p),
+                                             N.ptr(r.items, N._i32p), N.ptr(r.values, N._f32p),
+                                             r.count, N.ptr(order, N._i32p)))
+        self._order_uploaded = True
+
+    def iterate(self):
+        """Iterate() (:197-222) incl. UpdateLearnRate() (:225-244); twice when MaxThreads > 1."""
+        if self._h is None:
+            raise RuntimeError("Train() or init_model() first")
+        self._ensure_data()
+        seq = None
+        if self.schedule() == "dsgd":
+            G = self._thread_blocks[0]
+            seq = Random.get_instance().shuffle(np.arange(G, dtype=np.int32))
+        N.check(N.lib().mml_bmf_iterate(self._h, float(np.float32(self.current_learnrate)),
+                                        N.ptr(seq, N._i32p)))
+        self._host = None
+        if self.MaxThreads > 1:
+            self._update_learn_rate()
+        self._update_learn_rate()
+
+    def _update_learn_rate(self):
+        self.current_learnrate = float(np.float32(np.float32(self.current_learnrate) *
+                                                  np.float32(self.Decay)))
+
+    def last_epoch_ms(self) -> float:
+        out = np.zeros(2, np.float32)
+        N.check(N.lib().mml_bmf_last_timing(self._h, N.ptr(out, N._f32p)))
+        return float(out[0])
+
+    # ------------------------------------------------------------------ model access
+    def get_model(self):
+        if self._host is None:
+            k = int(self.NumFactors)
+            nu, ni = self.MaxUserID + 1, self.MaxItemID + 1
+            U = np.empty((nu, k), np.float32)
+            V = np.empty((ni, k), np.float32)
+            bu = np.empty(nu, np.float32)
+            bi = np.empty(ni, np.float32)
+            N.check(N.lib().mml_bmf_get_model(self._h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
+                                              N.ptr(bu, N._f32p), N.ptr(bi, N._f32p)))
+            self._host = dict(U=U, V=V, bu=bu, bi=bi)
+        return self._host
+
+    @property
+    def user_factors(self):
+        return self.get_model()["U"]
+
+    @property
+    def item_factors(self):
+        return self.get_model()["V"]
+
+    @property
+    def user_bias(self):
+        return self.get_model()["bu"]
+
+    @property
+    def item_bias(self):
+        return self.get_model()["bi"]
+
+    def predict(self, users, items) -> np.ndarray:
+        """Predict(int,int) (:313-325), batched on the GPU."""
+        u, i = N.i32(np.atleast_1d(users)), N.i32(np.atleast_1d(items))
+        out = np.empty(len(u), np.float32)
+        N.check(N.lib().mml_bmf_predict(self._h, N.ptr(u, N._i32p), N.ptr(i, N._i32p), len(u),
+                                        N.ptr(out, N._f32p)))
+        return out
+
+    def evaluate(self, test: Ratings) -> dict:
+        """Eval.Ratings.Evaluate (Eval/Ratings.cs:96-139) on the GPU -> RMSE, MAE, NMAE."""
+        out = np.zeros(2, np.float32)
+        N.check(N.lib().mml_bmf_evaluate(self._h, N.ptr(test.users, N._i32p),
+                                         N.ptr(test.items, N._i32p), N.ptr(test.values, N._f32p),
+                                         test.count, N.ptr(out, N._f32p)))
+        rmse, mae = float(out[0]), float(out[1])
+        nmae = float(np.float32(np.float32(mae) / np.float32(self.max_rating - self.min_rating)))
+        return {"RMSE": rmse, "MAE": mae, "NMAE": nmae}
+
+    # ------------------------------------------------------------------ misc
+    def _release(self):
+        if self._h is not None:
+            N.lib().mml_bmf_destroy(self._h)
+            self._h = None
+        if self._ctx is not None:
+            self._ctx.close()
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+    def __str__(self):
+        """ToString() (:554-561)."""
+        return ("BiasedMatrixFactorization num_factors={} bias_reg={} reg_u={} reg_i={} "
+                "frequency_regularization={} learn_rate={} bias_learn_rate={} learn_rate_decay={} "
+                "num_iter={} bold_driver={} loss={} max_threads={} naive_parallelization={}").format(
+            self.NumFactors, _g(self.BiasReg), _g(self.RegU), _g(self.RegI),
+            self.FrequencyRegularization, _g(self.LearnRate), _g(self.BiasLearnRate),
+            _g(self.Decay), self.NumIter, self.BoldDriver, self.Loss, self.MaxThreads,
+            self.NaiveParallelization)
+
+
+def _g(x):
+    return f"{float(np.float32(x)):.7g}"

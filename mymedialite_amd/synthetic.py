@@ -1,0 +1,95 @@
+"""Seeded synthetic workloads of BASELINE.md / SURVEY.md 8(d) (benchmark and test inputs only).
+
+* ``ml100k_standin``  -- C1: 943 users x 1,682 items, 100,000 distinct (u, i) pairs, Zipf(0.8)
+                         item popularity, >= 20 ratings per user, the public ML-100k rating histogram
+                         (6,110 / 11,370 / 27,145 / 34,174 / 21,201), 80/20 split, seed 20261015.
+                         Used only when data/ml-100k/u1.base is absent (never downloaded).
+* ``planted_ratings_torch`` -- C2/C4: users uniform, items Zipf(0.8) over a random permutation,
+                         rating = clip(round(3.5 + b_u + b_i + <p_u, q_i> + eps), 1, 5) with a planted
+                         rank-8 model, p, q, b ~ N(0, 0.3^2), eps ~ N(0, 0.5^2); generated in HBM.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ML100K_HIST = np.array([6110, 11370, 27145, 34174, 21201])
+
+
+def zipf_cdf(n_items: int, s: float) -> np.ndarray:
+    w = 1.0 / np.arange(1, n_items + 1, dtype=np.float64) ** s
+    c = np.cumsum(w)
+    return c / c[-1]
+
+
+def ml100k_standin(seed: int = 20261015, n_users: int = 943, n_items: int = 1682,
+                   n: int = 100000, test_frac: float = 0.2):
+    rs = np.random.default_rng(seed)
+    # user activity >= 20, heavy-tailed, summing to n
+    w = rs.lognormal(0.0, 1.0, n_users)
+    act = 20 + np.floor(w / w.sum() * (n - 20 * n_users)).astype(np.int64)
+    act[np.argsort(-w)[: n - act.sum()]] += 1
+    act = np.minimum(act, n_items)
+    pop = 1.0 / np.arange(1, n_items + 1) ** 0.8
+    pop = pop[rs.permutation(n_items)]
+    pop /= pop.sum()
+    users, items = [], []
+    for u in range(n_users):
+        its = rs.choice(n_items, size=int(act[u]), replace=False, p=pop)
+        users.append(np.full(len(its), u, np.int32))
+        items.append(its.astype(np.int32))
+    users = np.concatenate(users)
+    items = np.concatenate(items)
+    m = len(users)
+    # planted structure, then map scores to levels by the ML-100k histogram quantiles
+    P = rs.normal(0, 0.5, (n_users, 5))
+    Q = rs.normal(0, 0.5, (n_items, 5))
+    bu = rs.normal(0, 0.4, n_users)
+    bi = rs.normal(0, 0.4, n_items)
+    score = bu[users] + bi[items] + np.einsum("ij,ij->i", P[users], Q[items]) + rs.normal(0, 0.6, m)
+    cuts = np.cumsum(ML100K_HIST)[:-1] / ML100K_HIST.sum()
+    thr = np.quantile(score, cuts)
+    values = (1 + np.searchsorted(thr, score)).astype(np.float32)
+    perm = rs.permutation(m)
+    users, items, values = users[perm], items[perm], values[perm]
+    n_test = int(round(m * test_frac))
+    tr = slice(n_test, m)
+    te = slice(0, n_test)
+    return (users[tr].copy(), items[tr].copy(), values[tr].copy(),
+            users[te].copy(), items[te].copy(), values[te].copy())
+
+
+def planted_ratings_torch(n_users: int, n_items: int, n: int, seed: int, device, rank: int = 8,
+                          zipf_s: float = 0.8, user_range=None, chunk: int = 1 << 24):
+    """Returns (users int32, items int32, values float32) torch tensors on `device`.
+
+    user_range=(lo, hi) restricts users to [lo, hi) (a user shard); the planted model is shared.
+    """
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    gm = torch.Generator(device=device)
+    gm.manual_seed(12345)  # planted model identical on every shard
+    P = torch.randn(n_users, rank, generator=gm, device=device) * 0.3
+    Q = torch.randn(n_items, rank, generator=gm, device=device) * 0.3
+    bu = torch.randn(n_users, generator=gm, device=device) * 0.3
+    bi = torch.randn(n_items, generator=gm, device=device) * 0.3
+    item_perm = torch.randperm(n_items, generator=gm, device=device)
+    cdf = torch.from_numpy(zipf_cdf(n_items, zipf_s)).to(device=device, dtype=torch.float64)
+    lo, hi = (0, n_users) if user_range is None else user_range
+    users = torch.empty(n, dtype=torch.int32, device=device)
+    items = torch.empty(n, dtype=torch.int32, device=device)
+    values = torch.empty(n, dtype=torch.float32, device=device)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        m = e - s
+        u = torch.randint(lo, hi, (m,), generator=g, device=device, dtype=torch.int64)
+        x = torch.rand(m, generator=g, device=device, dtype=torch.float64)
+        r = torch.searchsorted(cdf, x).clamp_(max=n_items - 1)
+        i = item_perm[r]
+        sc = 3.5 + bu[u] + bi[i] + (P[u] * Q[i]).sum(1) + \
+            torch.randn(m, generator=g, device=device) * 0.5
+        users[s:e] = u.to(torch.int32)
+        items[s:e] = i.to(torch.int32)
+        values[s:e] = sc.round().clamp_(1, 5)
+    return users, items, values

@@ -1,0 +1,601 @@
+/*
+ * oracle/mml_oracle.c -- TEST INFRASTRUCTURE ONLY (parity checker + timed CPU baseline).
+ *
+ * A plain-C restatement of MyMediaLite's matrix-factorization training path, written from
+ * the reference's behaviour, never linked into the product.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ *
+ * Parity status: the component arithmetic is pinned by the reference's own known-answer
+ * tests (RowScalarProduct = 55, RowScalarProductWithRowDifference = 40, AUC cases, learn-rate
+ * decay, DSGD partition shapes, StaticRatingData parse count; see tests/test_oracle.py).
+ * The end-to-end trajectory (System.Random stream -> MathNet polar normals -> SGD) cannot be
+ * run against the reference here (no CLR in the image); it is pinned only by
+ * those component tests and the widely published System.Random(0) first draw.
+ *
+ * Build: oracle/Makefile (-O2 -ffp-contract=off: C# never contracts a*b+c into an FMA).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------
+ * System.Random(int seed) -- .NET reference-source Knuth subtractive generator (BCL; called via
+ * MyMediaLite.Random, src/MyMediaLite/Random.cs:23-64).  Restated from SURVEY.md A.2.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+    int32_t seed_array[56];
+    int32_t inext, inextp;
+} ora_rng;
+
+#define ORA_MBIG 2147483647
+#define ORA_MSEED 161803398
+
+void ora_rng_init(ora_rng* r, int32_t seed) {
+    int32_t subtraction = (seed == INT32_MIN) ? INT32_MAX : (seed < 0 ? -seed : seed);
+    int32_t mj = ORA_MSEED - subtraction;
+    r->seed_array[55] = mj;
+    int32_t mk = 1;
+    for (int i = 1; i < 55; i++) {
+        int ii = (21 * i) % 55;
+        r->seed_array[ii] = mk;
+        mk = mj - mk;
+        if (mk < 0) mk += ORA_MBIG;
+        mj = r->seed_array[ii];
+    }
+    for (int k = 1; k < 5; k++)
+        for (int i = 1; i < 56; i++) {
+            r->seed_array[i] -= r->seed_array[1 + (i + 30) % 55];
+            if (r->seed_array[i] < 0) r->seed_array[i] += ORA_MBIG;
+        }
+    r->inext = 0;
+    r->inextp = 21;
+}
+
+size_t ora_rng_sizeof(void) { return sizeof(ora_rng); }
+
+int32_t ora_rng_internal_sample(ora_rng* r) {
+    int32_t a = r->inext + 1, b = r->inextp + 1;
+    if (a >= 56) a = 1;
+    if (b >= 56) b = 1;
+    int32_t v = r->seed_array[a] - r->seed_array[b];
+    if (v == ORA_MBIG) v--;
+    if (v < 0) v += ORA_MBIG;
+    r->seed_array[a] = v;
+    r->inext = a;
+    r->inextp = b;
+    return v;
+}
+
+double ora_rng_next_double(ora_rng* r) { return ora_rng_internal_sample(r) * (1.0 / ORA_MBIG); }
+
+/* Random.Next(maxValue) = (int)(Sample() * maxValue) */
+int32_t ora_rng_next(ora_rng* r, int32_t max_value) {
+    return (int32_t)(ora_rng_next_double(r) * max_value);
+}
+
+/* MathNet.Numerics 3.15 Normal.Sample(): polar transform, second variate discarded. */
+double ora_normal(ora_rng* r, double mean, double stddev) {
+    for (;;) {
+        double a = ora_rng_next_double(r);
+        double b = ora_rng_next_double(r);
+        double v1 = 2.0 * a - 1.0;
+        double v2 = 2.0 * b - 1.0;
+        double rr = v1 * v1 + v2 * v2;
+        if (rr >= 1.0 || rr == 0.0) continue;
+        double fac = sqrt(-2.0 * log(rr) / rr);
+        return mean + stddev * (v1 * fac);
+    }
+}
+
+/* MatrixExtensions.InitNormal (DataType/MatrixExtensions.cs:62-69): row-major fill, cast to float */
+void ora_fill_normal(ora_rng* r, float* out, int64_t n, double mean, double stddev) {
+    for (int64_t i = 0; i < n; i++) out[i] = (float)ora_normal(r, mean, stddev);
+}
+
+/* Utils.Shuffle (src/MyMediaLite/Utils.cs:52-64): i = n-1 .. 0, r = Next(i+1), swap */
+void ora_shuffle_i32(ora_rng* r, int32_t* a, int64_t n) {
+    for (int64_t i = n - 1; i >= 0; i--) {
+        int32_t j = ora_rng_next(r, (int32_t)(i + 1));
+        int32_t t = a[i];
+        a[i] = a[j];
+        a[j] = t;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * DataType/MatrixExtensions.cs row kernels (known answers: tests/test_oracle.py)
+ * ---------------------------------------------------------------------------------------- */
+/* RowScalarProduct(Matrix<float>,int,Matrix<float>,int), MatrixExtensions.cs:224-241: float acc */
+float ora_row_scalar_product(const float* m1, int i, const float* m2, int j, int k) {
+    float result = 0.0f;
+    const float* a = m1 + (int64_t)i * k;
+    const float* b = m2 + (int64_t)j * k;
+    for (int c = 0; c < k; c++) result += a[c] * b[c];
+    return result;
+}
+
+/* RowScalarProductWithRowDifference, MatrixExtensions.cs:276-298: float products, double acc */
+double ora_row_scalar_product_with_row_difference(const float* m1, int i, const float* m2, int j,
+                                                  const float* m3, int l, int k) {
+    double result = 0.0;
+    const float* a = m1 + (int64_t)i * k;
+    const float* b = m2 + (int64_t)j * k;
+    const float* c3 = m3 + (int64_t)l * k;
+    for (int c = 0; c < k; c++) result += (double)(a[c] * (b[c] - c3[c]));
+    return result;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * BiasedMatrixFactorization (RatingPrediction/BiasedMatrixFactorization.cs)
+ * ---------------------------------------------------------------------------------------- */
+enum { ORA_LOSS_RMSE = 0, ORA_LOSS_MAE = 1, ORA_LOSS_LOGISTIC = 2 };
+
+typedef struct {
+    int32_t k;
+    int32_t loss;
+    int32_t frequency_regularization;
+    int32_t update_user;
+    int32_t update_item;
+    float global_bias;
+    float min_rating;
+    float rating_range_size;
+    float learn_rate;      /* current_learnrate */
+    float bias_learn_rate; /* BiasLearnRate */
+    float bias_reg;        /* BiasReg */
+    float reg_u;           /* RegU */
+    float reg_i;           /* RegI */
+} ora_bmf_params;
+
+size_t ora_bmf_params_sizeof(void) { return sizeof(ora_bmf_params); }
+
+/* BiasedMatrixFactorization.Iterate(IList<int>,bool,bool), :264-310 (with SetupLoss :247-261) */
+void ora_bmf_iterate(const ora_bmf_params* p, const int32_t* users, const int32_t* items,
+                     const float* values, const int32_t* idx, int64_t n_idx, float* U, float* V,
+                     float* bu, float* bi, const int32_t* count_by_user,
+                     const int32_t* count_by_item) {
+    const int k = p->k;
+    const float lr = p->learn_rate;
+    for (int64_t n = 0; n < n_idx; n++) {
+        int32_t index = idx[n];
+        int32_t u = users[index];
+        int32_t i = items[index];
+        float* Uu = U + (int64_t)u * k;
+        float* Vi = V + (int64_t)i * k;
+
+        float dot = 0.0f;
+        for (int c = 0; c < k; c++) dot += Uu[c] * Vi[c];
+        float score_f = ((p->global_bias + bu[u]) + bi[i]) + dot;
+        double score = (double)score_f;
+        double sig = 1.0 / (1.0 + exp(-score));
+        double prediction = (double)p->min_rating + sig * (double)p->rating_range_size;
+        double err = (double)values[index] - prediction;
+
+        float g;
+        if (p->loss == ORA_LOSS_MAE) {
+            double sgn = (err > 0) ? 1.0 : ((err < 0) ? -1.0 : 0.0);
+            g = (float)(sgn * sig * (1.0 - sig) * (double)p->rating_range_size);
+        } else if (p->loss == ORA_LOSS_LOGISTIC) {
+            g = (float)err;
+        } else {
+            g = (float)(err * sig * (1.0 - sig) * (double)p->rating_range_size);
+        }
+
+        float reg_u = p->reg_u, reg_i = p->reg_i;
+        if (p->frequency_regularization) {
+            reg_u = (float)((double)p->reg_u / sqrt((double)count_by_user[u]));
+            reg_i = (float)((double)p->reg_i / sqrt((double)count_by_item[i]));
+        }
+
+        const float blr = p->bias_learn_rate * lr;
+        if (p->update_user) bu[u] += blr * (g - (p->bias_reg * reg_u) * bu[u]);
+        if (p->update_item) bi[i] += blr * (g - (p->bias_reg * reg_i) * bi[i]);
+
+        for (int f = 0; f < k; f++) {
+            double u_f = (double)Uu[f];
+            double i_f = (double)Vi[f];
+            if (p->update_user) {
+                double delta_u = (double)g * i_f - (double)reg_u * u_f;
+                Uu[f] += (float)((double)lr * delta_u);
+            }
+            if (p->update_item) {
+                double delta_i = (double)g * u_f - (double)reg_i * i_f;
+                Vi[f] += (float)((double)lr * delta_i);
+            }
+        }
+    }
+}
+
+/* BiasedMatrixFactorization.Predict(int,int), :313-325 (score accumulated in double) */
+float ora_bmf_predict1(int32_t u, int32_t i, int32_t n_users, int32_t n_items, int k,
+                       const float* U, const float* V, const float* bu, const float* bi,
+                       float global_bias, float min_rating, float range) {
+    double score = (double)global_bias;
+    if (u < n_users) score += (double)bu[u];
+    if (i < n_items) score += (double)bi[i];
+    if (u < n_users && i < n_items) score += (double)ora_row_scalar_product(U, u, V, i, k);
+    return (float)((double)min_rating + (1.0 / (1.0 + exp(-score))) * (double)range);
+}
+
+void ora_bmf_predict(const int32_t* users, const int32_t* items, int64_t n, int32_t n_users,
+                     int32_t n_items, int k, const float* U, const float* V, const float* bu,
+                     const float* bi, float global_bias, float min_rating, float range,
+                     float* out) {
+    for (int64_t x = 0; x < n; x++)
+        out[x] = ora_bmf_predict1(users[x], items[x], n_users, n_items, k, U, V, bu, bi,
+                                  global_bias, min_rating, range);
+}
+
+/* Eval/Ratings.cs:96-139: float error, float square, double sum; RMSE/MAE cast to float.
+ * out[0] = RMSE, out[1] = MAE */
+void ora_rating_eval(const float* predictions, const float* values, int64_t n, float* out) {
+    double rmse = 0.0, mae = 0.0;
+    for (int64_t x = 0; x < n; x++) {
+        float error = predictions[x] - values[x];
+        rmse += (double)(error * error);
+        mae += (double)fabsf(error);
+    }
+    out[0] = (float)sqrt(rmse / (double)n);
+    out[1] = (float)(mae / (double)n);
+}
+
+/* MultiCore.PartitionUsersAndItems (MultiCore.cs:43-73).  Produces blocks as a CSR over
+ * block id b = ug * G + ig: offsets[G*G+1], indices[n].  Returns G (clipped). */
+int32_t ora_partition_users_and_items(ora_rng* r, const int32_t* users, const int32_t* items,
+                                      int64_t n, int32_t max_user_id, int32_t max_item_id,
+                                      int32_t num_groups, int64_t* offsets, int32_t* indices) {
+    int32_t G = num_groups;
+    if (G > max_user_id + 1) G = max_user_id + 1;
+    if (G > max_item_id + 1) G = max_item_id + 1;
+    int32_t* up = (int32_t*)malloc(sizeof(int32_t) * (size_t)(max_user_id + 1));
+    int32_t* ip = (int32_t*)malloc(sizeof(int32_t) * (size_t)(max_item_id + 1));
+    for (int32_t x = 0; x <= max_user_id; x++) up[x] = x;
+    for (int32_t x = 0; x <= max_item_id; x++) ip[x] = x;
+    ora_shuffle_i32(r, up, max_user_id + 1);
+    ora_shuffle_i32(r, ip, max_item_id + 1);
+    int64_t nb = (int64_t)G * G;
+    memset(offsets, 0, sizeof(int64_t) * (size_t)(nb + 1));
+    for (int64_t x = 0; x < n; x++) {
+        int64_t b = (int64_t)(up[users[x]] % G) * G + (ip[items[x]] % G);
+        offsets[b + 1]++;
+    }
+    for (int64_t b = 0; b < nb; b++) offsets[b + 1] += offsets[b];
+    int64_t* fill = (int64_t*)malloc(sizeof(int64_t) * (size_t)nb);
+    memcpy(fill, offsets, sizeof(int64_t) * (size_t)nb);
+    for (int64_t x = 0; x < n; x++) {
+        int64_t b = (int64_t)(up[users[x]] % G) * G + (ip[items[x]] % G);
+        indices[fill[b]++] = (int32_t)x;
+    }
+    for (int64_t b = 0; b < nb; b++)
+        ora_shuffle_i32(r, indices + offsets[b], offsets[b + 1] - offsets[b]);
+    free(fill);
+    free(up);
+    free(ip);
+    return G;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * BPRMF (ItemRecommendation/BPRMF.cs).  The user->items sets (SparseBooleanMatrix rows of
+ * HashSet<int>) are given as a CSR in HashSet enumeration order = first-insertion order
+ * (no removals), plus a per-row sorted copy for the Contains() probes.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+    int32_t k;
+    int32_t update_u, update_i, update_j;
+    float learn_rate, reg_u, reg_i, reg_j, bias_reg;
+    int32_t max_user_id, max_item_id;
+} ora_bpr_params;
+
+size_t ora_bpr_params_sizeof(void) { return sizeof(ora_bpr_params); }
+
+static int ora_row_contains(const int64_t* off, const int32_t* sorted, int32_t u, int32_t item) {
+    int64_t lo = off[u], hi = off[u + 1];
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (sorted[mid] < item) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < off[u + 1] && sorted[lo] == item;
+}
+
+/* SampleUser :300-310, SampleItemPair :290-296, SampleTriple :316-321 */
+void ora_bpr_sample_triple(ora_rng* r, const ora_bpr_params* p, const int64_t* off,
+                           const int32_t* rows, const int32_t* sorted, int32_t* out) {
+    int32_t u;
+    for (;;) {
+        u = ora_rng_next(r, p->max_user_id + 1);
+        int64_t cnt = (u < 0) ? 0 : off[u + 1] - off[u];
+        if (cnt == 0 || cnt == (int64_t)p->max_item_id + 1) continue;
+        break;
+    }
+    int64_t cnt = off[u + 1] - off[u];
+    int32_t i = rows[off[u] + ora_rng_next(r, (int32_t)cnt)];
+    int32_t j;
+    do j = ora_rng_next(r, p->max_item_id + 1);
+    while (ora_row_contains(off, sorted, u, j));
+    out[0] = u;
+    out[1] = i;
+    out[2] = j;
+}
+
+/* BPRMF.UpdateFactors(u,i,j,...) :330-374 */
+void ora_bpr_update(const ora_bpr_params* p, int32_t u, int32_t i, int32_t j, float* U, float* V,
+                    float* bias) {
+    const int k = p->k;
+    float* w = U + (int64_t)u * k;
+    float* hi = V + (int64_t)i * k;
+    float* hj = V + (int64_t)j * k;
+    double x_uij = (double)(bias[i] - bias[j]) +
+                   ora_row_scalar_product_with_row_difference(U, u, V, i, V, j, k);
+    double e = 1.0 / (1.0 + exp(x_uij));
+    if (p->update_i) {
+        double update = e - (double)(p->bias_reg * bias[i]);
+        bias[i] += (float)((double)p->learn_rate * update);
+    }
+    if (p->update_j) {
+        double update = -e - (double)(p->bias_reg * bias[j]);
+        bias[j] += (float)((double)p->learn_rate * update);
+    }
+    for (int f = 0; f < k; f++) {
+        float w_uf = w[f], h_if = hi[f], h_jf = hj[f];
+        if (p->update_u) {
+            double update = (double)(h_if - h_jf) * e - (double)(p->reg_u * w_uf);
+            w[f] = (float)((double)w_uf + (double)p->learn_rate * update);
+        }
+        if (p->update_i) {
+            double update = (double)w_uf * e - (double)(p->reg_i * h_if);
+            hi[f] = (float)((double)h_if + (double)p->learn_rate * update);
+        }
+        if (p->update_j) {
+            double update = (double)(-w_uf) * e - (double)(p->reg_j * h_jf);
+            hj[f] = (float)((double)h_jf + (double)p->learn_rate * update);
+        }
+    }
+}
+
+/* Loss-sample burn in BPRMF.Train :136-150 (triples drawn, never used) */
+void ora_bpr_burn(ora_rng* r, const ora_bpr_params* p, const int64_t* off, const int32_t* rows,
+                  const int32_t* sorted, int64_t count) {
+    int32_t t[3];
+    for (int64_t c = 0; c < count; c++) ora_bpr_sample_triple(r, p, off, rows, sorted, t);
+}
+
+/* IterateWithoutReplacementUniformUser :216-226 -- num_events triples, each sampled then applied.
+ * If trace != NULL, the triples are recorded (3 * num_events ints). */
+void ora_bpr_epoch(ora_rng* r, const ora_bpr_params* p, const int64_t* off, const int32_t* rows,
+                   const int32_t* sorted, int64_t num_events, float* U, float* V, float* bias,
+                   int32_t* trace) {
+    int32_t t[3];
+    for (int64_t c = 0; c < num_events; c++) {
+        ora_bpr_sample_triple(r, p, off, rows, sorted, t);
+        if (trace) {
+            trace[3 * c] = t[0];
+            trace[3 * c + 1] = t[1];
+            trace[3 * c + 2] = t[2];
+        }
+        ora_bpr_update(p, t[0], t[1], t[2], U, V, bias);
+    }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * WRMF (ItemRecommendation/WRMF.cs:79-156), fp64.  One half-step: W rows from H.
+ * data rows as CSR (insertion order).  Inverse via LU with partial pivoting, like MathNet's
+ * DenseMatrix.Inverse() (managed provider).
+ * ---------------------------------------------------------------------------------------- */
+static void ora_lu_inverse(double* a, double* inv, int n, int* piv, double* col) {
+    /* LU factorisation in place with partial pivoting (row interchanges) */
+    for (int i = 0; i < n; i++) piv[i] = i;
+    for (int c = 0; c < n; c++) {
+        int p = c;
+        double best = fabs(a[c * n + c]);
+        for (int r = c + 1; r < n; r++)
+            if (fabs(a[r * n + c]) > best) {
+                best = fabs(a[r * n + c]);
+                p = r;
+            }
+        if (p != c) {
+            for (int x = 0; x < n; x++) {
+                double t = a[c * n + x];
+                a[c * n + x] = a[p * n + x];
+                a[p * n + x] = t;
+            }
+            int t = piv[c];
+            piv[c] = piv[p];
+            piv[p] = t;
+        }
+        double d = a[c * n + c];
+        if (d != 0.0)
+            for (int r = c + 1; r < n; r++) {
+                a[r * n + c] /= d;
+                double m = a[r * n + c];
+                for (int x = c + 1; x < n; x++) a[r * n + x] -= m * a[c * n + x];
+            }
+    }
+    /* solve A X = I column by column */
+    for (int j = 0; j < n; j++) {
+        for (int i = 0; i < n; i++) col[i] = (piv[i] == j) ? 1.0 : 0.0;
+        for (int i = 0; i < n; i++) {
+            double s = col[i];
+            for (int x = 0; x < i; x++) s -= a[i * n + x] * col[x];
+            col[i] = s;
+        }
+        for (int i = n - 1; i >= 0; i--) {
+            double s = col[i];
+            for (int x = i + 1; x < n; x++) s -= a[i * n + x] * col[x];
+            col[i] = s / a[i * n + i];
+        }
+        for (int i = 0; i < n; i++) inv[i * n + j] = col[i];
+    }
+}
+
+/* WRMF.ComputeSquareMatrix :94-108 -- float products, double sums */
+void ora_wrmf_square(const float* H, int64_t rows, int k, double* HH) {
+    for (int f1 = 0; f1 < k; f1++)
+        for (int f2 = f1; f2 < k; f2++) {
+            double d = 0.0;
+            for (int64_t i = 0; i < rows; i++) d += (double)(H[i * k + f1] * H[i * k + f2]);
+            HH[f1 * k + f2] = d;
+            HH[f2 * k + f1] = d;
+        }
+}
+
+/* WRMF.Optimize(u, data, W, H, HH) :110-156 over rows [row_begin, row_end) */
+void ora_wrmf_optimize_rows(const int64_t* off, const int32_t* cols, int64_t row_begin,
+                            int64_t row_end, int64_t n_data_rows, float* W, const float* H,
+                            const double* HH, int k, double alpha, double reg) {
+    double* HC = (double*)malloc(sizeof(double) * (size_t)k * k);
+    double* m = (double*)malloc(sizeof(double) * (size_t)k * k);
+    double* inv = (double*)malloc(sizeof(double) * (size_t)k * k);
+    double* HCp = (double*)malloc(sizeof(double) * (size_t)k);
+    double* col = (double*)malloc(sizeof(double) * (size_t)k);
+    int* piv = (int*)malloc(sizeof(int) * (size_t)k);
+    for (int64_t u = row_begin; u < row_end; u++) {
+        int64_t b = (u < n_data_rows) ? off[u] : 0, e = (u < n_data_rows) ? off[u + 1] : 0;
+        for (int f1 = 0; f1 < k; f1++)
+            for (int f2 = f1; f2 < k; f2++) {
+                double d = 0.0;
+                for (int64_t x = b; x < e; x++) {
+                    const float* h = H + (int64_t)cols[x] * k;
+                    d += (double)(h[f1] * h[f2]);
+                }
+                HC[f1 * k + f2] = d * alpha;
+                HC[f2 * k + f1] = d * alpha;
+            }
+        for (int f = 0; f < k; f++) {
+            double d = 0.0;
+            for (int64_t x = b; x < e; x++) d += (double)H[(int64_t)cols[x] * k + f];
+            HCp[f] = d * (1.0 + alpha);
+        }
+        for (int f1 = 0; f1 < k; f1++)
+            for (int f2 = f1; f2 < k; f2++) {
+                double d = HH[f1 * k + f2] + HC[f1 * k + f2];
+                if (f1 == f2) d += reg;
+                m[f1 * k + f2] = d;
+                m[f2 * k + f1] = d;
+            }
+        ora_lu_inverse(m, inv, k, piv, col);
+        for (int f = 0; f < k; f++) {
+            double d = 0.0;
+            for (int f2 = 0; f2 < k; f2++) d += inv[f * k + f2] * HCp[f2];
+            W[u * k + f] = (float)d;
+        }
+    }
+    free(HC);
+    free(m);
+    free(inv);
+    free(HCp);
+    free(col);
+    free(piv);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Item-recommendation evaluation: Eval/Items.cs:126-209 + AUC.Compute (Eval/Measures/AUC.cs:42-68)
+ * for an MF-style scorer score(u,i) = bias[i] + <U_u, V_i> (bias may be NULL: MF.Predict).
+ * candidates: already-shuffled candidate list (Items.Candidates :62-96).
+ * train/test user rows as CSR.  Returns AUC averaged with float accumulation; *num_users out.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+    float score;
+    int32_t pos;
+    int32_t item;
+} ora_scored;
+
+static int ora_cmp_scored(const void* a, const void* b) {
+    const ora_scored* x = (const ora_scored*)a;
+    const ora_scored* y = (const ora_scored*)b;
+    if (x->score > y->score) return -1; /* descending */
+    if (x->score < y->score) return 1;
+    return (x->pos < y->pos) ? -1 : (x->pos > y->pos); /* OrderByDescending is stable */
+}
+
+/* AUC.Compute with rank list given implicitly (relevance flags in ranked order) */
+double ora_auc_compute(const int32_t* ranked_relevant, int64_t n_ranked, int64_t n_relevant_total,
+                       int64_t num_dropped_items) {
+    int64_t num_relevant_in_list = 0;
+    for (int64_t x = 0; x < n_ranked; x++) num_relevant_in_list += ranked_relevant[x] ? 1 : 0;
+    int64_t num_eval_items = n_ranked + num_dropped_items;
+    int64_t num_eval_pairs = (num_eval_items - num_relevant_in_list) * num_relevant_in_list;
+    if (num_eval_pairs < 0) return -1.0;
+    if (num_eval_pairs == 0) return 0.5;
+    int64_t correct = 0, hit = 0;
+    for (int64_t x = 0; x < n_ranked; x++) {
+        if (!ranked_relevant[x]) correct += hit;
+        else hit++;
+    }
+    int64_t missing = n_relevant_total - num_relevant_in_list;
+    correct += hit * (num_dropped_items - missing);
+    return (double)correct / (double)num_eval_pairs;
+}
+
+float ora_item_eval_auc(const int32_t* test_users, int64_t n_test_users, const int32_t* candidates,
+                        int64_t n_cand, const int64_t* tr_off, const int32_t* tr_cols,
+                        int64_t tr_rows, const int64_t* te_off, const int32_t* te_cols,
+                        int64_t te_rows, int32_t n_items_total, int32_t max_user_id,
+                        int32_t max_item_id, int k, const float* U, const float* V,
+                        const float* bias, int32_t* num_users_out) {
+    uint8_t* is_cand = (uint8_t*)calloc((size_t)n_items_total, 1);
+    uint8_t* is_correct = (uint8_t*)calloc((size_t)n_items_total, 1);
+    uint8_t* is_ignored = (uint8_t*)calloc((size_t)n_items_total, 1);
+    ora_scored* buf = (ora_scored*)malloc(sizeof(ora_scored) * (size_t)(n_cand + 1));
+    int32_t* flags = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n_cand + 1));
+    for (int64_t c = 0; c < n_cand; c++) is_cand[candidates[c]] = 1;
+    float auc_sum = 0.0f;
+    int32_t num_users = 0;
+    for (int64_t t = 0; t < n_test_users; t++) {
+        int32_t u = test_users[t];
+        int64_t n_correct = 0, n_ignored = 0;
+        if (u < te_rows)
+            for (int64_t x = te_off[u]; x < te_off[u + 1]; x++) {
+                int32_t it = te_cols[x];
+                if (is_cand[it] && !is_correct[it]) {
+                    is_correct[it] = 1;
+                    n_correct++;
+                }
+            }
+        if (u < tr_rows)
+            for (int64_t x = tr_off[u]; x < tr_off[u + 1]; x++) {
+                int32_t it = tr_cols[x];
+                if (is_cand[it] && !is_ignored[it]) {
+                    is_ignored[it] = 1;
+                    n_ignored++;
+                }
+            }
+        int skip = (n_correct == 0) || (n_correct == n_cand - n_ignored);
+        if (!skip) {
+            int64_t m = 0;
+            for (int64_t c = 0; c < n_cand; c++) {
+                int32_t it = candidates[c];
+                if (is_ignored[it]) continue;
+                float s;
+                if (u > max_user_id || it > max_item_id) s = -3.402823466e+38f; /* float.MinValue */
+                else {
+                    s = ora_row_scalar_product(U, u, V, it, k);
+                    if (bias) s = bias[it] + s;
+                }
+                if (s > -3.402823466e+38f) {
+                    buf[m].score = s;
+                    buf[m].pos = (int32_t)c;
+                    buf[m].item = it;
+                    m++;
+                }
+            }
+            qsort(buf, (size_t)m, sizeof(ora_scored), ora_cmp_scored);
+            for (int64_t x = 0; x < m; x++) flags[x] = is_correct[buf[x].item];
+            int64_t num_dropped = (n_cand - n_ignored) - m;
+            double auc = ora_auc_compute(flags, m, n_correct, num_dropped);
+            num_users++;
+            auc_sum += (float)auc;
+        }
+        if (u < te_rows)
+            for (int64_t x = te_off[u]; x < te_off[u + 1]; x++) is_correct[te_cols[x]] = 0;
+        if (u < tr_rows)
+            for (int64_t x = tr_off[u]; x < tr_off[u + 1]; x++) is_ignored[tr_cols[x]] = 0;
+    }
+    free(is_cand);
+    free(is_correct);
+    free(is_ignored);
+    free(buf);
+    free(flags);
+    *num_users_out = num_users;
+    return num_users ? auc_sum / (float)num_users : 0.0f;
+}

@@ -1,0 +1,440 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes driver over oracle/mml_oracle.c.
+
+The oracle is the CPU restatement of MyMediaLite's training path.
+Only tests/, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg may import this
+module, and only as the checker / CPU baseline -- never as the measured or shipped path.
+
+Parity status (also in DESIGN.md): component arithmetic pinned by the reference's known-answer
+tests; the end-to-end trajectory is not runnable against the reference here (C#, no CLR).
+
+Drivers below mirror the reference's control flow:
+  * ``bmf_train``   -- BiasedMatrixFactorization.Train/Iterate
+                       (src/MyMediaLite/RatingPrediction/BiasedMatrixFactorization.cs:173-244)
+  * ``bpr_train``   -- BPRMF.Train/Iterate (src/MyMediaLite/ItemRecommendation/BPRMF.cs:129-226)
+  * ``wrmf_train``  -- MF.Train + WRMF.Iterate (ItemRecommendation/MF.cs:51-67, WRMF.cs:68-92)
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "build", "libmml_oracle.so")
+_lib = None
+
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_f64p = ctypes.POINTER(ctypes.c_double)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        L.ora_rng_sizeof.restype = ctypes.c_size_t
+        L.ora_rng_init.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        L.ora_rng_internal_sample.argtypes = [ctypes.c_void_p]
+        L.ora_rng_internal_sample.restype = ctypes.c_int32
+        L.ora_rng_next_double.argtypes = [ctypes.c_void_p]
+        L.ora_rng_next_double.restype = ctypes.c_double
+        L.ora_rng_next.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        L.ora_rng_next.restype = ctypes.c_int32
+        L.ora_normal.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double]
+        L.ora_normal.restype = ctypes.c_double
+        L.ora_fill_normal.argtypes = [ctypes.c_void_p, _f32p, ctypes.c_int64, ctypes.c_double,
+                                      ctypes.c_double]
+        L.ora_shuffle_i32.argtypes = [ctypes.c_void_p, _i32p, ctypes.c_int64]
+        L.ora_row_scalar_product.argtypes = [_f32p, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int]
+        L.ora_row_scalar_product.restype = ctypes.c_float
+        L.ora_row_scalar_product_with_row_difference.argtypes = [
+            _f32p, ctypes.c_int, _f32p, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int]
+        L.ora_row_scalar_product_with_row_difference.restype = ctypes.c_double
+        L.ora_bmf_params_sizeof.restype = ctypes.c_size_t
+        L.ora_bmf_iterate.argtypes = [ctypes.c_void_p, _i32p, _i32p, _f32p, _i32p, ctypes.c_int64,
+                                      _f32p, _f32p, _f32p, _f32p, _i32p, _i32p]
+        L.ora_bmf_predict.argtypes = [_i32p, _i32p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_int, _f32p, _f32p, _f32p, _f32p, ctypes.c_float,
+                                      ctypes.c_float, ctypes.c_float, _f32p]
+        L.ora_rating_eval.argtypes = [_f32p, _f32p, ctypes.c_int64, _f32p]
+        L.ora_partition_users_and_items.argtypes = [
+            ctypes.c_void_p, _i32p, _i32p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+            ctypes.c_int32, _i64p, _i32p]
+        L.ora_partition_users_and_items.restype = ctypes.c_int32
+        L.ora_bpr_params_sizeof.restype = ctypes.c_size_t
+        L.ora_bpr_sample_triple.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _i64p, _i32p, _i32p,
+                                            _i32p]
+        L.ora_bpr_update.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.c_int32, _f32p, _f32p, _f32p]
+        L.ora_bpr_burn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _i64p, _i32p, _i32p,
+                                   ctypes.c_int64]
+        L.ora_bpr_epoch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _i64p, _i32p, _i32p,
+                                    ctypes.c_int64, _f32p, _f32p, _f32p, _i32p]
+        L.ora_wrmf_square.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f64p]
+        L.ora_wrmf_optimize_rows.argtypes = [_i64p, _i32p, ctypes.c_int64, ctypes.c_int64,
+                                             ctypes.c_int64, _f32p, _f32p, _f64p, ctypes.c_int,
+                                             ctypes.c_double, ctypes.c_double]
+        L.ora_auc_compute.argtypes = [_i32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]
+        L.ora_auc_compute.restype = ctypes.c_double
+        L.ora_item_eval_auc.argtypes = [
+            _i32p, ctypes.c_int64, _i32p, ctypes.c_int64, _i64p, _i32p, ctypes.c_int64, _i64p,
+            _i32p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
+            _f32p, _f32p, _f32p, _i32p]
+        L.ora_item_eval_auc.restype = ctypes.c_float
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t) if a is not None else None
+
+
+def i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+# ----------------------------------------------------------------------------- System.Random
+class Rng:
+    """System.Random(seed) restatement (MyMediaLite.Random, src/MyMediaLite/Random.cs:23-64)."""
+
+    def __init__(self, seed: int):
+        L = lib()
+        self._buf = ctypes.create_string_buffer(L.ora_rng_sizeof())
+        L.ora_rng_init(self._buf, int(seed))
+
+    def internal_sample(self) -> int:
+        return lib().ora_rng_internal_sample(self._buf)
+
+    def next_double(self) -> float:
+        return lib().ora_rng_next_double(self._buf)
+
+    def next(self, max_value: int) -> int:
+        return lib().ora_rng_next(self._buf, int(max_value))
+
+    def normal(self, mean=0.0, stddev=1.0) -> float:
+        return lib().ora_normal(self._buf, mean, stddev)
+
+    def fill_normal(self, n: int, mean=0.0, stddev=0.1) -> np.ndarray:
+        out = np.empty(int(n), dtype=np.float32)
+        lib().ora_fill_normal(self._buf, _p(out, _f32p), int(n), float(mean), float(stddev))
+        return out
+
+    def shuffle(self, a: np.ndarray) -> np.ndarray:
+        assert a.dtype == np.int32 and a.flags.c_contiguous
+        lib().ora_shuffle_i32(self._buf, _p(a, _i32p), a.size)
+        return a
+
+
+# ----------------------------------------------------------------------------- BiasedMF
+LOSS = {"RMSE": 0, "MAE": 1, "LOGISTICLOSS": 2}
+
+
+class _BmfParams(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_int32), ("loss", ctypes.c_int32),
+                ("frequency_regularization", ctypes.c_int32), ("update_user", ctypes.c_int32),
+                ("update_item", ctypes.c_int32), ("global_bias", ctypes.c_float),
+                ("min_rating", ctypes.c_float), ("rating_range_size", ctypes.c_float),
+                ("learn_rate", ctypes.c_float), ("bias_learn_rate", ctypes.c_float),
+                ("bias_reg", ctypes.c_float), ("reg_u", ctypes.c_float), ("reg_i", ctypes.c_float)]
+
+
+def row_scalar_product(m1, i, m2, j):
+    m1, m2 = f32(m1), f32(m2)
+    return lib().ora_row_scalar_product(_p(m1, _f32p), i, _p(m2, _f32p), j, m1.shape[1])
+
+
+def row_scalar_product_with_row_difference(m1, i, m2, j, m3, l):
+    m1, m2, m3 = f32(m1), f32(m2), f32(m3)
+    return lib().ora_row_scalar_product_with_row_difference(
+        _p(m1, _f32p), i, _p(m2, _f32p), j, _p(m3, _f32p), l, m1.shape[1])
+
+
+def global_bias(values, min_rating, max_rating):
+    """BiasedMatrixFactorization.Train :186-190 with Ratings.Average (Data/Ratings.cs:76-84)."""
+    s = float(np.sum(values.astype(np.float64)))  # double sum (order-insensitive at these sizes)
+    avg_f = np.float32(np.float32(s) / np.float32(len(values)))
+    rng_f = np.float32(np.float32(max_rating) - np.float32(min_rating))
+    avg = np.float32(np.float32(avg_f - np.float32(min_rating)) / rng_f)
+    return np.float32(math.log(float(avg) / (1.0 - float(avg))))
+
+
+def ratings_average_exact(values):
+    """Sequential double sum as in Ratings.Average (Data/Ratings.cs:76-84)."""
+    s = 0.0
+    for v in values.astype(np.float64).tolist():
+        s += v
+    return s
+
+
+def bmf_iterate(users, items, values, indices, U, V, bu, bi, *, gb, min_rating, range_, lr,
+                bias_lr=1.0, bias_reg=0.01, reg_u=0.015, reg_i=0.015, loss=0, freq_reg=False,
+                count_by_user=None, count_by_item=None, update_user=True, update_item=True):
+    """BiasedMatrixFactorization.Iterate(IList<int>,bool,bool) :264-310 -- in place."""
+    k = U.shape[1]
+    p = _BmfParams(k, loss, int(freq_reg), int(update_user), int(update_item), gb, min_rating,
+                   range_, lr, bias_lr, bias_reg, reg_u, reg_i)
+    cu = i32(count_by_user) if count_by_user is not None else None
+    ci = i32(count_by_item) if count_by_item is not None else None
+    idx = i32(indices)
+    lib().ora_bmf_iterate(ctypes.byref(p), _p(users, _i32p), _p(items, _i32p), _p(values, _f32p),
+                          _p(idx, _i32p), idx.size, _p(U, _f32p), _p(V, _f32p), _p(bu, _f32p),
+                          _p(bi, _f32p), _p(cu, _i32p), _p(ci, _i32p))
+
+
+def partition_users_and_items(rng: Rng, users, items, max_user_id, max_item_id, num_groups):
+    """MultiCore.PartitionUsersAndItems (MultiCore.cs:43-73) -> (G, offsets, indices)."""
+    n = len(users)
+    offsets = np.zeros(num_groups * num_groups + 1, dtype=np.int64)
+    indices = np.zeros(n, dtype=np.int32)
+    G = lib().ora_partition_users_and_items(rng._buf, _p(users, _i32p), _p(items, _i32p), n,
+                                            max_user_id, max_item_id, num_groups,
+                                            _p(offsets, _i64p), _p(indices, _i32p))
+    return G, offsets[: G * G + 1].copy(), indices
+
+
+def partition_indices(random_index, num_groups):
+    """MultiCore.PartitionIndices (MultiCore.cs:79-92)."""
+    n = len(random_index)
+    g = min(num_groups, n)
+    return [random_index[x::g].copy() for x in range(g)]
+
+
+def bmf_train(users, items, values, n_users, n_items, min_rating, max_rating, *, seed=1, k=10,
+              learn_rate=0.01, decay=1.0, reg_u=0.015, reg_i=0.015, bias_reg=0.01,
+              bias_learn_rate=1.0, num_iter=30, init_mean=0.0, init_stddev=0.1, loss=0,
+              frequency_regularization=False, max_threads=1, naive_parallelization=False,
+              rng=None, callback=None):
+    """BiasedMatrixFactorization.Train() (:173-194) and NumIter x Iterate() (:197-222).
+
+    Returns a dict with the model and the RNG-derived schedule (so a GPU run can be fed the
+    identical RandomIndex / DSGD blocks). ``callback(epoch, state)`` after every epoch.
+    """
+    users, items, values = i32(users), i32(items), f32(values)
+    rng = rng if rng is not None else Rng(seed)
+    # InitModel (MatrixFactorization.cs:99-116): U fully, then V fully
+    U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
+    V = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
+    cnt_u = np.bincount(users, minlength=n_users).astype(np.int32)
+    cnt_i = np.bincount(items, minlength=n_items).astype(np.int32)
+    U[cnt_u == 0] = 0
+    V[cnt_i == 0] = 0
+    bu = np.zeros(n_users, np.float32)
+    bi = np.zeros(n_items, np.float32)
+    lr = np.float32(learn_rate)
+    state = dict(U=U, V=V, bu=bu, bi=bi, init_U=U.copy(), init_V=V.copy())
+
+    blocks = None
+    lists = None
+    random_index = None
+    if max_threads > 1:
+        if naive_parallelization:
+            random_index = rng.shuffle(np.arange(len(users), dtype=np.int32))
+            lists = partition_indices(random_index, max_threads)
+        else:
+            blocks = partition_users_and_items(rng, users, items, n_users - 1, n_items - 1,
+                                               max_threads)
+    range_ = np.float32(np.float32(max_rating) - np.float32(min_rating))
+    s = ratings_average_exact(values) if len(values) <= 200000 else float(
+        np.sum(values, dtype=np.float64))
+    avg_f = np.float32(np.float32(s) / np.float32(len(values)))
+    avg = np.float32(np.float32(avg_f - np.float32(min_rating)) / range_)
+    gb = np.float32(math.log(float(avg) / (1.0 - float(avg))))
+    common = dict(gb=gb, min_rating=np.float32(min_rating), range_=range_,
+                  bias_lr=bias_learn_rate, bias_reg=bias_reg, reg_u=reg_u, reg_i=reg_i, loss=loss,
+                  freq_reg=frequency_regularization, count_by_user=cnt_u, count_by_item=cnt_i)
+    subepochs = []
+    lrs = []
+    for epoch in range(num_iter):
+        lrs.append(float(lr))
+        if max_threads > 1:
+            if naive_parallelization:
+                for lst in lists:  # one admissible interleaving of Parallel.For (:203)
+                    bmf_iterate(users, items, values, lst, U, V, bu, bi, lr=lr, **common)
+            else:
+                G, off, idx = blocks
+                seq = rng.shuffle(np.arange(G, dtype=np.int32))
+                subepochs.append(seq.copy())
+                for i in seq.tolist():
+                    for j in range(G):
+                        b = j * G + (i + j) % G
+                        bmf_iterate(users, items, values, idx[off[b]:off[b + 1]], U, V, bu, bi,
+                                    lr=lr, **common)
+            lr = np.float32(lr * np.float32(decay))  # UpdateLearnRate() at :216
+        else:
+            if random_index is None:
+                random_index = rng.shuffle(np.arange(len(users), dtype=np.int32))
+            bmf_iterate(users, items, values, random_index, U, V, bu, bi, lr=lr, **common)
+        lr = np.float32(lr * np.float32(decay))  # UpdateLearnRate() at :221
+        if callback is not None:
+            callback(epoch, state)
+    state.update(global_bias=gb, min_rating=np.float32(min_rating), range_=range_,
+                 random_index=random_index, blocks=blocks, subepochs=subepochs, lrs=lrs,
+                 current_learnrate=lr, rng=rng)
+    return state
+
+
+def bmf_predict(users, items, U, V, bu, bi, gb, min_rating, range_):
+    users, items = i32(users), i32(items)
+    out = np.empty(len(users), np.float32)
+    lib().ora_bmf_predict(_p(users, _i32p), _p(items, _i32p), len(users), U.shape[0], V.shape[0],
+                          U.shape[1], _p(U, _f32p), _p(V, _f32p), _p(bu, _f32p), _p(bi, _f32p),
+                          gb, min_rating, range_, _p(out, _f32p))
+    return out
+
+
+def rating_eval(predictions, values):
+    """Eval/Ratings.cs:96-139 -> (RMSE, MAE) as floats."""
+    p, v = f32(predictions), f32(values)
+    out = np.zeros(2, np.float32)
+    lib().ora_rating_eval(_p(p, _f32p), _p(v, _f32p), len(p), _p(out, _f32p))
+    return float(out[0]), float(out[1])
+
+
+# ----------------------------------------------------------------------------- BPRMF
+class _BprParams(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_int32), ("update_u", ctypes.c_int32), ("update_i", ctypes.c_int32),
+                ("update_j", ctypes.c_int32), ("learn_rate", ctypes.c_float),
+                ("reg_u", ctypes.c_float), ("reg_i", ctypes.c_float), ("reg_j", ctypes.c_float),
+                ("bias_reg", ctypes.c_float), ("max_user_id", ctypes.c_int32),
+                ("max_item_id", ctypes.c_int32)]
+
+
+def insertion_order_rows(rows_of, cols_of, n_rows):
+    """SparseBooleanMatrix rows (HashSet<int>, enumeration = first-insertion order) as CSR."""
+    rows_of, cols_of = i32(rows_of), i32(cols_of)
+    key = rows_of.astype(np.int64) * (int(cols_of.max(initial=0)) + 1) + cols_of
+    _, first = np.unique(key, return_index=True)
+    first.sort()  # distinct pairs in first-appearance order
+    r, c = rows_of[first], cols_of[first]
+    order = np.argsort(r, kind="stable")
+    r, c = r[order], c[order]
+    off = np.zeros(n_rows + 1, np.int64)
+    np.add.at(off, r.astype(np.int64) + 1, 1)
+    off = np.cumsum(off)
+    return off, i32(c)
+
+
+def sorted_rows(off, cols):
+    s = cols.copy()
+    for u in range(len(off) - 1):
+        s[off[u]:off[u + 1]].sort()
+    return s
+
+
+def bpr_train(users, items, n_users, n_items, *, seed=1, k=10, num_iter=30, learn_rate=0.05,
+              reg_u=0.0025, reg_i=0.0025, reg_j=0.00025, bias_reg=0.0, update_j=True,
+              init_mean=0.0, init_stddev=0.1, rng=None, trace_epochs=0, callback=None):
+    """BPRMF.Train (:129-154) with the default IterateWithoutReplacementUniformUser (:216-226)."""
+    users, items = i32(users), i32(items)
+    rng = rng if rng is not None else Rng(seed)
+    U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
+    V = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
+    bias = np.zeros(n_items, np.float32)
+    init_U, init_V = U.copy(), V.copy()
+    off, rows = insertion_order_rows(users, items, n_users)
+    srt = sorted_rows(off, rows)
+    p = _BprParams(k, 1, 1, int(update_j), learn_rate, reg_u, reg_i, reg_j, bias_reg, n_users - 1,
+                   n_items - 1)
+    L = lib()
+    num_burn = int(math.sqrt(n_users - 1)) * 100
+    L.ora_bpr_burn(rng._buf, ctypes.byref(p), _p(off, _i64p), _p(rows, _i32p), _p(srt, _i32p),
+                   num_burn)
+    traces = []
+    n_events = len(users)
+    for epoch in range(num_iter):
+        tr = np.empty(3 * n_events, np.int32) if epoch < trace_epochs else None
+        L.ora_bpr_epoch(rng._buf, ctypes.byref(p), _p(off, _i64p), _p(rows, _i32p),
+                        _p(srt, _i32p), n_events, _p(U, _f32p), _p(V, _f32p), _p(bias, _f32p),
+                        _p(tr, _i32p))
+        if tr is not None:
+            traces.append(tr.reshape(-1, 3))
+        if callback is not None:
+            callback(epoch, dict(U=U, V=V, bias=bias))
+    return dict(U=U, V=V, bias=bias, init_U=init_U, init_V=init_V, traces=traces, rng=rng,
+                num_burn=num_burn, off=off, rows=rows)
+
+
+def bpr_update(u, i, j, U, V, bias, *, learn_rate=0.05, reg_u=0.0025, reg_i=0.0025,
+               reg_j=0.00025, bias_reg=0.0, update_u=True, update_i=True, update_j=True):
+    p = _BprParams(U.shape[1], int(update_u), int(update_i), int(update_j), learn_rate, reg_u,
+                   reg_i, reg_j, bias_reg, U.shape[0] - 1, V.shape[0] - 1)
+    lib().ora_bpr_update(ctypes.byref(p), u, i, j, _p(U, _f32p), _p(V, _f32p), _p(bias, _f32p))
+
+
+# ----------------------------------------------------------------------------- WRMF
+def wrmf_square(H):
+    H = f32(H)
+    k = H.shape[1]
+    HH = np.empty((k, k), np.float64)
+    lib().ora_wrmf_square(_p(H, _f32p), H.shape[0], k, _p(HH, _f64p))
+    return HH
+
+
+def wrmf_optimize(off, cols, W, H, alpha, reg):
+    """WRMF.Optimize(data, W, H) (:79-92) in place on W."""
+    HH = wrmf_square(H)
+    lib().ora_wrmf_optimize_rows(_p(off, _i64p), _p(cols, _i32p), 0, W.shape[0], len(off) - 1,
+                                 _p(W, _f32p), _p(f32(H), _f32p), _p(HH, _f64p), W.shape[1],
+                                 float(alpha), float(reg))
+
+
+def wrmf_train(users, items, n_users, n_items, *, seed=1, k=10, num_iter=15, alpha=1.0,
+               regularization=0.015, init_mean=0.0, init_stddev=0.1, rng=None, callback=None):
+    users, items = i32(users), i32(items)
+    rng = rng if rng is not None else Rng(seed)
+    U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
+    V = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
+    init_U, init_V = U.copy(), V.copy()
+    uoff, ucols = insertion_order_rows(users, items, n_users)
+    ioff, icols = insertion_order_rows(items, users, n_items)
+    for epoch in range(num_iter):
+        wrmf_optimize(uoff, ucols, U, V, alpha, regularization)
+        wrmf_optimize(ioff, icols, V, U, alpha, regularization)
+        if callback is not None:
+            callback(epoch, dict(U=U, V=V))
+    return dict(U=U, V=V, init_U=init_U, init_V=init_V, rng=rng)
+
+
+# ----------------------------------------------------------------------------- item eval / AUC
+def auc_compute(ranked_items, relevant_items, num_dropped_items):
+    """AUC.Compute (Eval/Measures/AUC.cs:42-68)."""
+    rel = set(int(x) for x in relevant_items)
+    flags = i32([1 if int(x) in rel else 0 for x in ranked_items])
+    return lib().ora_auc_compute(_p(flags, _i32p), len(flags), len(rel), int(num_dropped_items))
+
+
+def item_eval_auc(U, V, bias, train_users, train_items, test_users, test_items, *,
+                  candidates, eval_users=None):
+    """Eval.Items.Evaluate (Eval/Items.cs:126-209) restricted to AUC; candidates pre-shuffled."""
+    n_items_total = int(max(V.shape[0], int(np.max(train_items, initial=0)) + 1,
+                            int(np.max(test_items, initial=0)) + 1))
+    n_rows_tr = int(np.max(train_users, initial=0)) + 1
+    n_rows_te = int(np.max(test_users, initial=0)) + 1
+    tr_off, tr_cols = insertion_order_rows(train_users, train_items, n_rows_tr)
+    te_off, te_cols = insertion_order_rows(test_users, test_items, n_rows_te)
+    if eval_users is None:
+        eval_users = np.unique(i32(test_users))
+    eval_users = i32(eval_users)
+    cand = i32(candidates)
+    nu = ctypes.c_int32(0)
+    b = f32(bias) if bias is not None else None
+    auc = lib().ora_item_eval_auc(
+        _p(eval_users, _i32p), len(eval_users), _p(cand, _i32p), len(cand), _p(tr_off, _i64p),
+        _p(tr_cols, _i32p), n_rows_tr, _p(te_off, _i64p), _p(te_cols, _i32p), n_rows_te,
+        n_items_total, U.shape[0] - 1, V.shape[0] - 1, U.shape[1], _p(f32(U), _f32p),
+        _p(f32(V), _f32p), _p(b, _f32p), ctypes.byref(nu))
+    return float(auc), int(nu.value)

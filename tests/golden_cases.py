@@ -1,0 +1,144 @@
+"""Golden-vector cases shared by tests/golden/make_golden.py (writer) and the tests (readers).
+
+Inputs are the reference's toy fixture (tests/golden/example.{train,test}, verbatim copies of the
+reference's tests/example.*) and small seeded synthetic sets; outputs come from the CPU oracle.
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle as O  # noqa: E402
+
+GOLDEN = os.path.join(HERE, "golden", "oracle_golden.npz")
+
+
+def load_example(name):
+    """example.train / example.test: 'user<TAB>item<TAB>rating' (last line has no newline)."""
+    a = np.loadtxt(os.path.join(HERE, "golden", name), dtype=np.float64, ndmin=2)
+    return a[:, 0].astype(np.int32), a[:, 1].astype(np.int32), a[:, 2].astype(np.float32)
+
+
+def synth_ratings(seed, n_users, n_items, n, levels=(1, 2, 3, 4, 5)):
+    rs = np.random.default_rng(seed)
+    u = rs.integers(0, n_users, n).astype(np.int32)
+    i = (rs.zipf(1.6, n) - 1) % n_items
+    i = i.astype(np.int32)
+    v = np.asarray(levels, np.float32)[rs.integers(0, len(levels), n)]
+    u[0], i[0] = n_users - 1, n_items - 1
+    return u, i, v
+
+
+def synth_feedback(seed, n_users, n_items, per_user):
+    rs = np.random.default_rng(seed)
+    us, its = [], []
+    for u in range(n_users):
+        k = int(rs.integers(1, per_user + 1))
+        items = rs.choice(n_items, size=min(k, n_items - 1), replace=False)
+        us += [u] * len(items)
+        its += items.tolist()
+    order = rs.permutation(len(us))
+    return np.array(us, np.int32)[order], np.array(its, np.int32)[order]
+
+
+def rng_streams():
+    out = {}
+    for seed in (0, 1, 42):
+        r = O.Rng(seed)
+        out[f"rng{seed}/internal"] = np.array([r.internal_sample() for _ in range(20)], np.int64)
+        r = O.Rng(seed)
+        out[f"rng{seed}/next100"] = np.array([r.next(100) for _ in range(20)], np.int64)
+        r = O.Rng(seed)
+        out[f"rng{seed}/next_double"] = np.array([r.next_double() for _ in range(20)])
+        r = O.Rng(seed)
+        out[f"rng{seed}/normal"] = np.array([r.normal(0.0, 1.0) for _ in range(20)])
+        r = O.Rng(seed)
+        out[f"rng{seed}/shuffle20"] = r.shuffle(np.arange(20, dtype=np.int32)).astype(np.int64)
+    return out
+
+
+def _bmf_case(users, items, values, test, *, seed, k, num_iter, **kw):
+    nu, ni = int(users.max()) + 1, int(items.max()) + 1
+    lo, hi = float(np.unique(values)[0]), float(np.unique(values)[-1])
+    snaps = {}
+
+    def cb(epoch, st):
+        snaps[f"U{epoch + 1}"] = st["U"].copy()
+        snaps[f"V{epoch + 1}"] = st["V"].copy()
+        snaps[f"bu{epoch + 1}"] = st["bu"].copy()
+        snaps[f"bi{epoch + 1}"] = st["bi"].copy()
+
+    st = O.bmf_train(users, items, values, nu, ni, lo, hi, seed=seed, k=k, num_iter=num_iter,
+                     callback=cb, **kw)
+    out = dict(users=users, items=items, values=values, init_U=st["init_U"],
+               init_V=st["init_V"], global_bias=np.float32(st["global_bias"]),
+               lr_final=np.float32(st["current_learnrate"]), **snaps)
+    if st["random_index"] is not None:
+        out["random_index"] = st["random_index"]
+    if test is not None:
+        tu, ti, tv = test
+        p = O.bmf_predict(tu, ti, st["U"], st["V"], st["bu"], st["bi"], st["global_bias"],
+                          st["min_rating"], st["range_"])
+        out["test_pred"] = p
+        out["test_rmse_mae"] = np.array(O.rating_eval(p, tv), np.float32)
+    return out
+
+
+def case_bmf_example_k3():
+    return _bmf_case(*load_example("example.train"), load_example("example.test"), seed=1, k=3,
+                     num_iter=3)
+
+
+def case_bmf_example_k10_mae():
+    return _bmf_case(*load_example("example.train"), load_example("example.test"), seed=42,
+                     k=10, num_iter=3, loss=O.LOSS["MAE"])
+
+
+def case_bmf_example_k10_logistic():
+    return _bmf_case(*load_example("example.train"), load_example("example.test"), seed=7,
+                     k=10, num_iter=3, loss=O.LOSS["LOGISTICLOSS"])
+
+
+def case_bmf_synth_freq():
+    u, i, v = synth_ratings(11, 60, 40, 2000)
+    return _bmf_case(u, i, v, (u[:200], i[:200], v[:200]), seed=5, k=10, num_iter=3,
+                     frequency_regularization=True)
+
+
+def case_bmf_synth_dsgd4():
+    u, i, v = synth_ratings(12, 60, 40, 2000)
+    return _bmf_case(u, i, v, None, seed=9, k=8, num_iter=2, max_threads=4)
+
+
+def case_bpr_small():
+    u, i = synth_feedback(21, 30, 20, 8)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    st = O.bpr_train(u, i, nu, ni, seed=3, k=5, num_iter=2, trace_epochs=1)
+    return dict(users=u, items=i, init_U=st["init_U"], init_V=st["init_V"], U=st["U"],
+                V=st["V"], bias=st["bias"], trace0=st["traces"][0])
+
+
+def case_wrmf_small():
+    u, i = synth_feedback(31, 30, 20, 8)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    st = O.wrmf_train(u, i, nu, ni, seed=4, k=6, num_iter=2)
+    return dict(users=u, items=i, init_U=st["init_U"], init_V=st["init_V"], U=st["U"],
+                V=st["V"])
+
+
+CASES = {
+    "bmf_example_k3": case_bmf_example_k3,
+    "bmf_example_k10_mae": case_bmf_example_k10_mae,
+    "bmf_example_k10_logistic": case_bmf_example_k10_logistic,
+    "bmf_synth_freq": case_bmf_synth_freq,
+    "bmf_synth_dsgd4": case_bmf_synth_dsgd4,
+    "bpr_small": case_bpr_small,
+    "wrmf_small": case_wrmf_small,
+}
+
+
+def golden():
+    return np.load(GOLDEN, allow_pickle=False)

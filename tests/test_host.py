@@ -1,0 +1,143 @@
+"""Host-side logic and the C-ABI library, without a GPU (no compute calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_cases import HERE, golden
+from mymedialite_amd import BiasedMatrixFactorization, SystemRandom, read_ratings
+from mymedialite_amd import _native as N
+
+ROOT = os.path.dirname(HERE)
+
+
+def _declared_symbols():
+    txt = open(os.path.join(ROOT, "include", "mml.h")).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*|mml_status)\s+(mml_[a-z0-9_]+)\(", txt, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = N.lib()
+    declared = _declared_symbols()
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(L, name), name
+    assert set(declared) == set(N.SIGNATURES), set(declared) ^ set(N.SIGNATURES)
+    assert L.mml_abi_version() == 1
+
+
+def test_no_device_is_an_error_not_a_crash():
+    if N.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(N.MMLError) as e:
+        N.Context(0)
+    assert e.value.status == -6  # MML_ERR_NODEV
+
+
+def test_bad_arguments_return_status():
+    L = N.lib()
+    assert L.mml_bmf_iterate(None, 0.01, None) == -1
+    assert "null handle" in L.mml_last_error().decode()
+    assert L.mml_random_create(1, None) == -1
+
+
+@pytest.mark.parametrize("seed", [0, 1, 42, -7, 2147483647, -2147483648])
+def test_product_rng_matches_oracle(seed):
+    a, b = SystemRandom(seed), O.Rng(seed)
+    assert [a.next(1000) for _ in range(50)] == [b.next(1000) for _ in range(50)]
+    assert [a.next_double() for _ in range(10)] == [b.next_double() for _ in range(10)]
+    np.testing.assert_array_equal(a.fill_normal(257, 0.0, 0.1), b.fill_normal(257, 0.0, 0.1))
+    x = np.arange(1000, dtype=np.int32)
+    y = x.copy()
+    np.testing.assert_array_equal(a.shuffle(x), b.shuffle(y))
+
+
+def test_product_rng_matches_golden_streams():
+    g = golden()
+    for seed in (0, 1, 42):
+        r = SystemRandom(seed)
+        np.testing.assert_array_equal([r.next(100) for _ in range(20)], g[f"rng{seed}/next100"])
+        r = SystemRandom(seed)
+        np.testing.assert_array_equal(r.shuffle(np.arange(20, dtype=np.int32)),
+                                      g[f"rng{seed}/shuffle20"])
+
+
+def test_product_partition_matches_oracle():
+    rs = np.random.default_rng(1)
+    u = rs.integers(0, 50, 3000).astype(np.int32)
+    i = rs.integers(0, 70, 3000).astype(np.int32)
+    a, b = SystemRandom(9), O.Rng(9)
+    off = np.zeros(26, np.int64)
+    idx = np.zeros(3000, np.int32)
+    g = ctypes.c_int32()
+    N.check(N.lib().mml_partition_users_and_items(a.handle, N.ptr(u, N._i32p), N.ptr(i, N._i32p),
+                                                  3000, 49, 69, 5, N.ptr(off, N._i64p),
+                                                  N.ptr(idx, N._i32p), ctypes.byref(g)))
+    G, off2, idx2 = O.partition_users_and_items(b, u, i, 49, 69, 5)
+    assert g.value == G == 5
+    np.testing.assert_array_equal(off, off2)
+    np.testing.assert_array_equal(idx, idx2)
+
+
+def test_configure_prefix_quirk():
+    # Extensions.SetProperty prefix match: reg_u also sets Regularization -> RegI (App. B.4)
+    m = BiasedMatrixFactorization()
+    m.configure("reg_i=0.5 reg_u=0.25 num_factors=64 loss=MAE max_threads=inf")
+    assert m.NumFactors == 64 and m.Loss == "MAE" and m.MaxThreads == 2147483647
+    assert m.RegU == 0.25 and m.RegI == 0.25
+    m = BiasedMatrixFactorization()
+    m.configure("reg_u=0.25 reg_i=0.5")
+    assert m.RegU == 0.25 and m.RegI == 0.5
+
+
+def test_configure_errors_are_reported():
+    errs = []
+    m = BiasedMatrixFactorization()
+    m.configure("no_such=1", errs.append)
+    m.configure("a=1=2", errs.append)
+    assert len(errs) == 2 and "does not have a parameter" in errs[0]
+
+
+def test_to_string_format():
+    s = str(BiasedMatrixFactorization())
+    assert s.startswith("BiasedMatrixFactorization num_factors=10 bias_reg=0.01 reg_u=0.015")
+    assert "," not in s
+
+
+def test_schedule_mapping():
+    m = BiasedMatrixFactorization()
+    assert m.schedule() == "ordered"
+    m.MaxThreads = 4
+    assert m.schedule() == "dsgd"
+    m.NaiveParallelization = True
+    assert m.schedule() == "hogwild"
+
+
+def test_read_example_fixture():
+    r = read_ratings(os.path.join(HERE, "golden", "example.train"))
+    assert r.count == 9 and r.max_user_id == 4 and r.max_item_id == 3
+    assert r.scale_min == 1.0 and r.scale_max == 5.0
+    t = read_ratings(os.path.join(HERE, "golden", "example.test"))
+    assert t.count == 4  # last line has no trailing newline
+
+
+def test_read_static_rating_data_reference_case(tmp_path):
+    # src/Tests/IO/StaticRatingDataTest.cs:30-59: 7 ratings, comma separated, extra columns
+    body = "".join(f"5951,{it},{r},2001-01-01\n" for it, r in
+                   [(50, 5), (223, 5), (260, 5), (293, 5), (356, 4), (364, 3), (457, 3)])
+    p = tmp_path / "r.txt"
+    p.write_text(body)
+    assert read_ratings(str(p)).count == 7
+    p.write_text("# first line\n" + body.replace("2001-01-01", "2001-01-01 00:00:00"))
+    assert read_ratings(str(p), ignore_first_line=True).count == 7
+
+
+def test_blank_line_scale_quirk(tmp_path):
+    # App. B.11: a blank line adds a spurious rating level 0 to the scale
+    p = tmp_path / "r.txt"
+    p.write_text("0 0 3\n\n1 1 4\n")
+    r = read_ratings(str(p))
+    assert r.count == 2 and r.scale_min == 0.0 and r.scale_max == 4.0

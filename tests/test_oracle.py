@@ -1,0 +1,156 @@
+"""CPU oracle pinned by the reference's own known-answer tests + regression goldens."""
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_cases import CASES, golden, rng_streams
+
+
+def test_system_random_seed0_published_stream():
+    # The widely published first draws of new System.Random(0) (.NET reference source).
+    r = O.Rng(0)
+    assert [r.internal_sample() for _ in range(3)] == [1559595546, 1755192844, 1649316166]
+    assert O.Rng(0).next_double() == pytest.approx(0.7262432699679598, abs=1e-16)
+
+
+def test_row_scalar_product_known_answer():
+    # src/Tests/DataType/MatrixExtensionsTest.cs:97-110 -> 55 (both overloads)
+    m = np.tile(np.arange(1, 6, dtype=np.float32), (5, 1))
+    assert O.row_scalar_product(m, 2, m, 3) == 55.0
+
+
+def test_row_scalar_product_with_row_difference_known_answer():
+    # src/Tests/DataType/MatrixExtensionsTest.cs:127-140 -> 40
+    m = np.tile(np.arange(1, 6, dtype=np.float32), (5, 1))
+    m3 = np.ones((5, 5), np.float32)
+    assert O.row_scalar_product_with_row_difference(m, 2, m, 3, m3, 1) == 40.0
+
+
+def test_inc_known_answer():
+    # MatrixExtensionsTest.TestInc (:29-36): Inc(3, 4, 2.5) on row {1..5} -> 7.5, via the SGD Inc
+    U = np.tile(np.arange(1, 6, dtype=np.float32), (5, 1))
+    assert np.float32(U[3, 4] + np.float32(2.5)) == 7.5
+
+
+@pytest.mark.parametrize("relevant,expected", [([1], 1.0), ([1, 2], 1.0), ([1, 2, 3], 1.0)])
+def test_auc_all_correct(relevant, expected):
+    # src/Tests/Eval/Measures/AUCTest.cs:37-43
+    assert O.auc_compute([1, 2, 3, 4], relevant, 0) == expected
+
+
+def test_auc_dropped_items():
+    # AUCTest.cs:75-86
+    for i in range(10):
+        for rel in ([1], [1, 2], [1, 2, 3]):
+            assert O.auc_compute([1, 2, 3, 4], rel, i) == 1.0
+        assert O.auc_compute([1, 2, 3, 4], [4], i) == pytest.approx(i / (i + 3))
+
+
+@pytest.mark.parametrize("relevant,expected", [([4], 0.0), ([3], 1 / 3), ([2], 2 / 3),
+                                               ([1, 3], 0.75), ([1, 2, 3, 4], 0.5),
+                                               ([2, 4], 0.25)])
+def test_auc_unrun_reference_cases(relevant, expected):
+    # AUCTest.cs:45-73 (present in the reference but not marked [Test()])
+    assert O.auc_compute([1, 2, 3, 4], relevant, 0) == pytest.approx(expected, abs=1e-9)
+
+
+def _tiny_ratings():
+    # TestUtils.CreateRatings(): one rating (0, 0, 0.0) -> range 0, NaN global bias (App. B.10)
+    return np.array([0], np.int32), np.array([0], np.int32), np.array([0.0], np.float32)
+
+
+def test_learn_rate_no_decay_by_default():
+    # BiasedMatrixFactorizationTest.TestDefaultBehaviorIsNoDecay (:41-46)
+    u, i, v = _tiny_ratings()
+    st = O.bmf_train(u, i, v, 1, 1, 0.0, 0.0, seed=1, learn_rate=1.1, num_iter=10)
+    assert st["current_learnrate"] == np.float32(1.1)
+
+
+def test_learn_rate_decay():
+    # BiasedMatrixFactorizationTest.TestDecay (:49-62): 1.0 -> 0.5 after Train(1 iter)
+    u, i, v = _tiny_ratings()
+    st = O.bmf_train(u, i, v, 1, 1, 0.0, 0.0, seed=1, learn_rate=1.0, decay=0.5, num_iter=1)
+    assert st["current_learnrate"] == np.float32(0.5)
+    st = O.bmf_train(u, i, v, 1, 1, 0.0, 0.0, seed=1, learn_rate=1.0, decay=0.5, num_iter=2)
+    assert st["current_learnrate"] == np.float32(0.25)
+
+
+def _create_random_ratings(rng, nu, ni, n):
+    # TestUtils.CreateRandomRatings (src/Tests/TestUtils.cs:29-42)
+    u, i, v = [], [], []
+    for _ in range(n):
+        u.append(rng.next(nu))
+        i.append(rng.next(ni))
+        v.append(1 + rng.next(5))
+    return np.array(u, np.int32), np.array(i, np.int32), np.array(v, np.float32)
+
+
+@pytest.mark.parametrize("nu,ni,groups", [(15, 30, 3), (15, 30, 20), (30, 15, 20)])
+def test_partition_users_and_items_shapes(nu, ni, groups):
+    # src/Tests/MulticoreTest.cs:28-69
+    rng = O.Rng(17)
+    u, i, v = _create_random_ratings(rng, nu, ni, 300)
+    G, off, idx = O.partition_users_and_items(rng, u, i, int(u.max()), int(i.max()), groups)
+    assert G == min(groups, int(u.max()) + 1, int(i.max()) + 1)
+    assert len(off) == G * G + 1 and off[-1] == 300
+    assert sorted(idx.tolist()) == list(range(300))
+    # blocks are conflict-free per sub-epoch: block (a, b) holds one user group and one item group
+    ug = {}
+    for b in range(G * G):
+        for x in idx[off[b]:off[b + 1]]:
+            assert ug.setdefault(("u", int(u[x])), b // G) == b // G
+            assert ug.setdefault(("i", int(i[x])), b % G) == b % G
+
+
+def test_partition_indices_shapes():
+    # MulticoreTest.TestPartitionIndices (:71-84) and ...LessRatingsThanThreads (:86-93)
+    rng = O.Rng(5)
+    ri = rng.shuffle(np.arange(300, dtype=np.int32))
+    parts = O.partition_indices(ri, 10)
+    assert len(parts) == 10 and all(len(p) == 30 for p in parts)
+    assert len(O.partition_indices(ri[:10], 50)) == 10
+
+
+def test_rng_streams_match_golden():
+    g = golden()
+    for k, v in rng_streams().items():
+        np.testing.assert_array_equal(g[k], v, err_msg=k)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_cases_match_golden(name):
+    g = golden()
+    got = CASES[name]()
+    for k, v in got.items():
+        np.testing.assert_array_equal(g[f"{name}/{k}"], v, err_msg=f"{name}/{k}")
+
+
+def test_bmf_oracle_learns():
+    # property check on a larger synthetic set: training RMSE decreases epoch over epoch
+    from golden_cases import synth_ratings
+    u, i, v = synth_ratings(3, 200, 100, 20000)
+    rm = []
+
+    def cb(epoch, st):
+        p = O.bmf_predict(u, i, st["U"], st["V"], st["bu"], st["bi"], gb[0], np.float32(1),
+                          np.float32(4))
+        rm.append(O.rating_eval(p, v)[0])
+
+    gb = [O.global_bias(v, 1.0, 5.0)]
+    O.bmf_train(u, i, v, 200, 100, 1.0, 5.0, seed=1, k=10, num_iter=5, callback=cb)
+    assert all(b < a for a, b in zip(rm, rm[1:])), rm
+
+
+def test_wrmf_oracle_row_solve_is_least_squares():
+    # WRMF.Optimize(u) solves (HH + alpha*H_u^T H_u + reg I) w = (1+alpha) * sum h_i
+    rs = np.random.default_rng(0)
+    H = rs.standard_normal((7, 3)).astype(np.float32)
+    off = np.array([0, 3, 3], np.int64)
+    cols = np.array([1, 4, 6], np.int32)
+    W = np.zeros((2, 3), np.float32)
+    O.wrmf_optimize(off, cols, W, H, 1.0, 0.015)
+    Hd = H.astype(np.float64)
+    A = Hd.T @ Hd + Hd[cols].T @ Hd[cols] + 0.015 * np.eye(3)
+    b = 2.0 * Hd[cols].sum(0)
+    np.testing.assert_allclose(W[0], np.linalg.solve(A, b), rtol=1e-5, atol=1e-6)
+    assert np.all(W[1] == 0)
