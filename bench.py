@@ -25,7 +25,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Load libmml_hip.so BEFORE torch so the process has one HIP runtime (same SONAMEs).
+# _native.lib() imports torch first, so libmml_hip.so binds to torch's HIP runtime (one per process).
 from mymedialite_amd import _native as N  # noqa: E402
 
 if not os.path.exists(N.LIB_PATH):

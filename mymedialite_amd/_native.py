@@ -83,6 +83,14 @@ def lib():
     """Load libmml_hip.so (raises if it was not built -- there is no CPU fallback)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same SONAME as
+        # /opt/rocm's).  Loading torch first makes this library bind to torch's runtime so device
+        # memory and streams are shared; loading it first would leave torch with a second,
+        # unusable runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() "
                               "(hipcc --offload-arch=gfx950); there is no CPU fallback")

@@ -27,6 +27,7 @@
 //            per rating (float4 each), 64/LPR ratings per wave step, dot product by xor-shuffle
 //            reduction, plain (racy) stores of the updated rows -- Hogwild! semantics.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "mml_internal.h"
@@ -84,9 +85,12 @@ struct RatingStep {
         const double delta = (double)g * (double)i_f - (double)reg_u * (double)u_f;
         return u_f + (float)((double)s.lr * delta);
     }
-    __device__ __forceinline__ float new_i(const BmfScalars& s, float u_f, float i_f) const {
+    __device__ __forceinline__ float inc_i(const BmfScalars& s, float u_f, float i_f) const {
         const double delta = (double)g * (double)u_f - (double)reg_i * (double)i_f;
-        return i_f + (float)((double)s.lr * delta);
+        return (float)((double)s.lr * delta);
+    }
+    __device__ __forceinline__ float new_i(const BmfScalars& s, float u_f, float i_f) const {
+        return i_f + inc_i(s, u_f, i_f);
     }
 };
 
@@ -140,7 +144,10 @@ __global__ __launch_bounds__(64) void bmf_sgd_ordered_kernel(
     }
 }
 
-// HOGWILD: LPR lanes per rating, one float4 of U_u and of V_i per lane.
+// HOGWILD: LPR lanes per rating, one float4 of U_u and of V_i per lane (one 16-B load and store per
+// row per lane), plain racy stores of the new rows and biases (Hogwild!).  A float-atomic variant
+// for item rows (no lost updates) was measured 7.5x slower on C2 (memory-side atomics serialise on
+// hot Zipf items) for no RMSE gain at that scale, so it is not kept.
 template <int LOSS, int LPR>
 __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
@@ -175,6 +182,7 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
                 part += pu.y * qi.y;
                 part += pu.z * qi.z;
                 part += pu.w * qi.w;
+                // xor butterfly: every lane of the group ends with the bit-identical sum
 #pragma unroll
                 for (int off = LPR / 2; off >= 1; off >>= 1) part += __shfl_xor(part, off);
                 const float bu_u = bu[u], bi_i = bi[i];
@@ -183,17 +191,10 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
                     bu[u] = st.new_bu;
                     bi[i] = st.new_bi;
                 }
-                float4 nu, nq;
-                nu.x = st.new_u(s, pu.x, qi.x);
-                nu.y = st.new_u(s, pu.y, qi.y);
-                nu.z = st.new_u(s, pu.z, qi.z);
-                nu.w = st.new_u(s, pu.w, qi.w);
-                nq.x = st.new_i(s, pu.x, qi.x);
-                nq.y = st.new_i(s, pu.y, qi.y);
-                nq.z = st.new_i(s, pu.z, qi.z);
-                nq.w = st.new_i(s, pu.w, qi.w);
-                U4[ou] = nu;
-                V4[oi] = nq;
+                U4[ou] = make_float4(st.new_u(s, pu.x, qi.x), st.new_u(s, pu.y, qi.y),
+                                     st.new_u(s, pu.z, qi.z), st.new_u(s, pu.w, qi.w));
+                V4[oi] = make_float4(st.new_i(s, pu.x, qi.x), st.new_i(s, pu.y, qi.y),
+                                     st.new_i(s, pu.z, qi.z), st.new_i(s, pu.w, qi.w));
             }
         }
     }
@@ -429,9 +430,16 @@ template <int LOSS>
 void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const int32_t* ci) {
     hipStream_t st = h->ctx->stream;
     const int64_t n = h->n;
-    // waves: enough to fill 256 CUs x 32 waves, but at least ~64 ratings per wave
+    // waves: up to 256 CUs x 32, but every wave walks at least min_chunk ratings of the stream in
+    // order, which bounds the updates in flight to ~n / min_chunk * (64 / LPR).  Hogwild's staleness
+    // on a hot item scales with (updates in flight) x sum_i p_i^2 (p_i = item share), so small,
+    // skewed sets need few waves (C1: 4 waves) while C2 saturates HBM from ~1000 waves on.
+    static const int64_t min_chunk = [] {
+        const char* e = std::getenv("MML_HOGWILD_MIN_CHUNK");
+        return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)16384;
+    }();
     const int64_t max_waves = 256 * 32;
-    int64_t waves = std::min<int64_t>(max_waves, std::max<int64_t>(1, (n + 63) / 64));
+    int64_t waves = std::min<int64_t>(max_waves, std::max<int64_t>(1, n / min_chunk));
     const int64_t blocks = (waves + 3) / 4;
     waves = blocks * 4;
     const int64_t chunk = (n + waves - 1) / waves;
