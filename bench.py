@@ -121,6 +121,10 @@ def main():
                                             values.data_ptr(), n_local, None))
     N.check(N.lib().mml_bmf_set_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
                                       N.ptr(bu, N._f32p), N.ptr(bi, N._f32p), gb, 1.0, 5.0))
+    # bounded host sample of the same workload for the CPU baseline (rank 0, N = 1)
+    n_cpu = min(n_local, 40_000_000)
+    cpu_sample = (users[:n_cpu].cpu().numpy(), items[:n_cpu].cpu().numpy(),
+                  values[:n_cpu].cpu().numpy()) if (rank == 0 and world == 1) else None
     del users, items, values
     tus, tis, tvs = tu.cpu().numpy(), ti.cpu().numpy(), tv.cpu().numpy()
     lr = 0.01
@@ -167,7 +171,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(h, k, n_users_total, n_items, gb, args.cpu_seconds)
+        cpu = cpu_baseline(h, k, n_users_total, n_items, gb, args.cpu_seconds, cpu_sample)
 
     if rank == 0:
         line = {
@@ -201,9 +205,10 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(h, k, n_users, n_items, gb, seconds):
+def cpu_baseline(h, k, n_users, n_items, gb, seconds, sample):
     """Oracle Iterate() (single thread, exact reference arithmetic) on a bounded sample of the
-    same workload: the first S ratings of a fresh stream on the GPU model's current state."""
+    same workload: a prefix of the very ratings stream the GPU trains on, applied to the GPU
+    model's current state, sized for ~`seconds` of CPU work."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -213,10 +218,9 @@ def cpu_baseline(h, k, n_users, n_items, gb, seconds):
     bi = np.empty(n_items, np.float32)
     N.check(N.lib().mml_bmf_get_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
                                       N.ptr(bu, N._f32p), N.ptr(bi, N._f32p)))
-    u, i, v = planted_ratings_torch(n_users, n_items, 4_000_000, seed=777, device="cpu")
-    u, i, v = u.numpy(), i.numpy(), v.numpy()
+    u, i, v = sample
     kw = dict(gb=np.float32(gb), min_rating=np.float32(1), range_=np.float32(4), lr=0.01)
-    probe = 100_000
+    probe = 200_000
     t0 = time.perf_counter()
     O.bmf_iterate(u, i, v, np.arange(probe, dtype=np.int32), U, V, bu, bi, **kw)
     dt = time.perf_counter() - t0
@@ -225,8 +229,9 @@ def cpu_baseline(h, k, n_users, n_items, gb, seconds):
     O.bmf_iterate(u, i, v, np.arange(probe, probe + n, dtype=np.int32), U, V, bu, bi, **kw)
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "rating-updates/s", "cores": 1, "kind": "port",
-            "sample": f"{n} ratings of the C2 generator, k={k}, oracle Iterate() (C restatement "
-                      f"of BiasedMatrixFactorization.cs:264-310), {dt:.1f} s"}
+            "sample": f"{n} ratings of the C2 stream itself (the GPU's training data), k={k}, "
+                      f"oracle Iterate() = C restatement of BiasedMatrixFactorization.cs:264-310, "
+                      f"single thread, {dt:.1f} s"}
 
 
 if __name__ == "__main__":

@@ -74,7 +74,9 @@ enum { MML_LOSS_RMSE = 0, MML_LOSS_MAE = 1, MML_LOSS_LOGISTIC = 2 }; /* Optimiza
 enum {
     MML_SCHEDULE_ORDERED = 0, /* exact reference order (MaxThreads = 1): one wavefront */
     MML_SCHEDULE_DSGD = 1,    /* reference DSGD (MaxThreads = G > 1): conflict-free blocks */
-    MML_SCHEDULE_HOGWILD = 2  /* lock-free parallel SGD over the fixed permuted stream */
+    MML_SCHEDULE_HOGWILD = 2, /* lock-free parallel SGD over the fixed permuted stream */
+    MML_SCHEDULE_HOGWILD_COHERENT = 3 /* Hogwild with agent-coherent (sc1) row accesses: no per-XCD
+                                         cache replicas of hot rows; slower on skewed items */
 };
 
 typedef struct {
@@ -128,6 +130,75 @@ mml_status mml_bmf_last_timing(mml_bmf* h, float* out);
 /* Multi-GPU (user shards): in-place RCCL all-reduce of item factors and item
  * biases over the context's communicator, then scale by 1/nranks (model averaging). */
 mml_status mml_bmf_allreduce_items(mml_bmf* h);
+
+/* ------------------------------------------------------------------ BPRMF */
+enum {
+    MML_BPR_SAMPLER_UNIFORM_USER = 0, /* default: IterateWithoutReplacementUniformUser (BPRMF.cs:216-226) */
+    MML_BPR_SAMPLER_UNIFORM_PAIR = 1  /* IterateWithoutReplacementUniformPair over the visit order
+                                         (:248-268; MultiCoreBPRMF's sampler, MultiCoreBPRMF.cs:49-63) */
+};
+
+typedef struct {
+    int32_t num_factors; /* NumFactors (MF.cs:43-45) */
+    int32_t sampler;     /* MML_BPR_SAMPLER_*: UniformUserSampling / WithReplacement (BPRMF.cs:79-82) */
+    int32_t update_j;    /* UpdateJ (:100) */
+    float learn_rate;    /* LearnRate (:88) */
+    float reg_u;         /* RegU (:91) */
+    float reg_i;         /* RegI (:94) */
+    float reg_j;         /* RegJ (:97) */
+    float bias_reg;      /* BiasReg (:85) */
+} mml_bpr_params;
+
+typedef struct mml_bpr mml_bpr;
+
+mml_status mml_bpr_create(mml_ctx* ctx, const mml_bpr_params* params, int32_t n_users,
+                          int32_t n_items, mml_bpr** out);
+mml_status mml_bpr_destroy(mml_bpr* h);
+/* Positive-only events (PosOnlyFeedback, Data/PosOnlyFeedback.cs:32-206; duplicates allowed and
+ * counted in Feedback.Count = samples per epoch); order = Feedback.RandomIndex for UNIFORM_PAIR. */
+mml_status mml_bpr_set_data(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t n,
+                            const int32_t* order);
+/* Model upload / download: U [n_users x k], V [n_items x k], item_bias [n_items]
+ * (InitModel: MF.cs:51-58 + BPRMF.cs:121-126). */
+mml_status mml_bpr_set_model(mml_bpr* h, const float* user_factors, const float* item_factors,
+                             const float* item_bias);
+mml_status mml_bpr_get_model(mml_bpr* h, float* user_factors, float* item_factors,
+                             float* item_bias);
+/* One epoch = BPRMF.Iterate() (:160-178): Feedback.Count sampled triples, each followed by
+ * UpdateFactors (:330-374).  seed keys the counter-based sampler (e.g. drawn from the host RNG). */
+mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed);
+/* BPRMF.Predict (:425-431), batched: float.MinValue for ids beyond the model. */
+mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t n,
+                           float* out);
+mml_status mml_bpr_last_timing(mml_bpr* h, float* out);
+/* Multi-GPU (user shards): RCCL all-reduce of item factors + item biases, scaled by 1/nranks. */
+mml_status mml_bpr_allreduce_items(mml_bpr* h);
+
+/* ------------------------------------------------------------------ WRMF */
+typedef struct {
+    int32_t num_factors;   /* NumFactors (MF.cs:43-45); <= 64 on this build */
+    int32_t reserved;
+    double alpha;          /* Alpha (WRMF.cs:56) */
+    double regularization; /* Regularization (WRMF.cs:59) */
+} mml_wrmf_params;
+
+typedef struct mml_wrmf mml_wrmf;
+
+mml_status mml_wrmf_create(mml_ctx* ctx, const mml_wrmf_params* params, int32_t n_users,
+                           int32_t n_items, mml_wrmf** out);
+mml_status mml_wrmf_destroy(mml_wrmf* h);
+/* Positive-only events; the user->items and item->users sets (Feedback.UserMatrix / ItemMatrix,
+ * Data/PosOnlyFeedback.cs:35-83) are built from them. */
+mml_status mml_wrmf_set_data(mml_wrmf* h, const int32_t* users, const int32_t* items, int64_t n);
+mml_status mml_wrmf_set_model(mml_wrmf* h, const float* user_factors, const float* item_factors);
+mml_status mml_wrmf_get_model(mml_wrmf* h, float* user_factors, float* item_factors);
+/* One WRMF.Iterate() (WRMF.cs:68-73): Optimize(users | items) then Optimize(items | users),
+ * each = ComputeSquareMatrix (:94-108) + one k x k solve per row (:110-156), fp64. */
+mml_status mml_wrmf_iterate(mml_wrmf* h);
+/* MF.Predict (MF.cs:151-157): float.MinValue for ids beyond the model. */
+mml_status mml_wrmf_predict(mml_wrmf* h, const int32_t* users, const int32_t* items, int64_t n,
+                            float* out);
+mml_status mml_wrmf_last_timing(mml_wrmf* h, float* out);
 
 #ifdef __cplusplus
 }

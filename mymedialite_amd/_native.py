@@ -17,7 +17,7 @@ ERRORS = {-1: "MML_ERR_ARG", -2: "MML_ERR_HIP", -3: "MML_ERR_RCCL", -4: "MML_ERR
           -5: "MML_ERR_STATE", -6: "MML_ERR_NODEV"}
 
 LOSS_RMSE, LOSS_MAE, LOSS_LOGISTIC = 0, 1, 2
-SCHEDULE_ORDERED, SCHEDULE_DSGD, SCHEDULE_HOGWILD = 0, 1, 2
+SCHEDULE_ORDERED, SCHEDULE_DSGD, SCHEDULE_HOGWILD, SCHEDULE_HOGWILD_COHERENT = 0, 1, 2, 3
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
@@ -41,6 +41,22 @@ class BmfParams(ctypes.Structure):
                 ("bias_learn_rate", ctypes.c_float), ("bias_reg", ctypes.c_float),
                 ("reg_u", ctypes.c_float), ("reg_i", ctypes.c_float)]
 
+
+class BprParams(ctypes.Structure):
+    """mml_bpr_params (include/mml.h)."""
+    _fields_ = [("num_factors", ctypes.c_int32), ("sampler", ctypes.c_int32),
+                ("update_j", ctypes.c_int32), ("learn_rate", ctypes.c_float),
+                ("reg_u", ctypes.c_float), ("reg_i", ctypes.c_float), ("reg_j", ctypes.c_float),
+                ("bias_reg", ctypes.c_float)]
+
+
+BPR_SAMPLER_UNIFORM_USER, BPR_SAMPLER_UNIFORM_PAIR = 0, 1
+
+
+class WrmfParams(ctypes.Structure):
+    """mml_wrmf_params (include/mml.h)."""
+    _fields_ = [("num_factors", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("alpha", ctypes.c_double), ("regularization", ctypes.c_double)]
 
 # every exported symbol of include/mml.h: name -> (restype, argtypes)
 SIGNATURES = {
@@ -74,6 +90,25 @@ SIGNATURES = {
     "mml_bmf_evaluate": (_st, [_vp, _i32p, _i32p, _f32p, ctypes.c_int64, _f32p]),
     "mml_bmf_last_timing": (_st, [_vp, _f32p]),
     "mml_bmf_allreduce_items": (_st, [_vp]),
+    "mml_bpr_create": (_st, [_vp, ctypes.POINTER(BprParams), ctypes.c_int32, ctypes.c_int32,
+                             ctypes.POINTER(_vp)]),
+    "mml_bpr_destroy": (_st, [_vp]),
+    "mml_bpr_set_data": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _i32p]),
+    "mml_bpr_set_model": (_st, [_vp, _f32p, _f32p, _f32p]),
+    "mml_bpr_get_model": (_st, [_vp, _f32p, _f32p, _f32p]),
+    "mml_bpr_iterate": (_st, [_vp, ctypes.c_uint64]),
+    "mml_bpr_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
+    "mml_bpr_last_timing": (_st, [_vp, _f32p]),
+    "mml_bpr_allreduce_items": (_st, [_vp]),
+    "mml_wrmf_create": (_st, [_vp, ctypes.POINTER(WrmfParams), ctypes.c_int32, ctypes.c_int32,
+                              ctypes.POINTER(_vp)]),
+    "mml_wrmf_destroy": (_st, [_vp]),
+    "mml_wrmf_set_data": (_st, [_vp, _i32p, _i32p, ctypes.c_int64]),
+    "mml_wrmf_set_model": (_st, [_vp, _f32p, _f32p]),
+    "mml_wrmf_get_model": (_st, [_vp, _f32p, _f32p]),
+    "mml_wrmf_iterate": (_st, [_vp]),
+    "mml_wrmf_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
+    "mml_wrmf_last_timing": (_st, [_vp, _f32p]),
 }
 
 _lib = None

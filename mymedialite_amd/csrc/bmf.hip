@@ -26,6 +26,7 @@
 //   HOGWILD  lock-free: every wavefront owns a contiguous chunk of the permuted stream; LPR lanes
 //            per rating (float4 each), 64/LPR ratings per wave step, dot product by xor-shuffle
 //            reduction, plain (racy) stores of the updated rows -- Hogwild! semantics.
+//   HOGWILD_COHERENT  the same with sc1 (agent-coherent) row and bias accesses, see load4 below.
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
@@ -144,11 +145,56 @@ __global__ __launch_bounds__(64) void bmf_sgd_ordered_kernel(
     }
 }
 
+
+// Row / bias access forms.  COH = false: plain loads/stores (cached in the CU's L1 and the XCD's
+// L2).  COH = true: agent-scope relaxed atomics = global_load/store ... sc1, which bypass the
+// non-coherent per-CU L1 and keep the eight per-XCD L2s from holding private dirty copies of a
+// row (MI355X_MICROARCH.md, inter-workgroup visibility).  Plain Hogwild on MI355X therefore runs
+// ~8 cache-level replicas of the hot Zipf items whose write-backs overwrite each other; COH makes
+// every update land in one coherent copy, at the price of hot-row traffic at the memory side.
+template <bool COH>
+__device__ __forceinline__ float4 load4(const float4* p) {
+    if constexpr (COH) {
+        const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+        const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long b =
+            __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return make_float4(__uint_as_float((unsigned)a), __uint_as_float((unsigned)(a >> 32)),
+                           __uint_as_float((unsigned)b), __uint_as_float((unsigned)(b >> 32)));
+    } else {
+        return *p;
+    }
+}
+template <bool COH>
+__device__ __forceinline__ void store4(float4* p, float4 v) {
+    if constexpr (COH) {
+        unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+        const unsigned long long a = (unsigned long long)__float_as_uint(v.x) |
+                                     ((unsigned long long)__float_as_uint(v.y) << 32);
+        const unsigned long long b = (unsigned long long)__float_as_uint(v.z) |
+                                     ((unsigned long long)__float_as_uint(v.w) << 32);
+        __hip_atomic_store(q, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *p = v;
+    }
+}
+template <bool COH>
+__device__ __forceinline__ float load1(const float* p) {
+    if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool COH>
+__device__ __forceinline__ void store1(float* p, float v) {
+    if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
 // HOGWILD: LPR lanes per rating, one float4 of U_u and of V_i per lane (one 16-B load and store per
 // row per lane), plain racy stores of the new rows and biases (Hogwild!).  A float-atomic variant
 // for item rows (no lost updates) was measured 7.5x slower on C2 (memory-side atomics serialise on
 // hot Zipf items) for no RMSE gain at that scale, so it is not kept.
-template <int LOSS, int LPR>
+template <int LOSS, int LPR, bool COH>
 __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
     int64_t n, int64_t chunk, float* U, float* V, float* bu, float* bi, int32_t ld4, BmfScalars s,
@@ -176,8 +222,8 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
             const float r = __shfl(my_r, src);
             if (src < cnt) {
                 const int64_t ou = (int64_t)u * ld4 + q, oi = (int64_t)i * ld4 + q;
-                const float4 pu = U4[ou];
-                const float4 qi = V4[oi];
+                const float4 pu = load4<COH>(U4 + ou);
+                const float4 qi = load4<COH>(V4 + oi);
                 float part = pu.x * qi.x;
                 part += pu.y * qi.y;
                 part += pu.z * qi.z;
@@ -185,16 +231,16 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
                 // xor butterfly: every lane of the group ends with the bit-identical sum
 #pragma unroll
                 for (int off = LPR / 2; off >= 1; off >>= 1) part += __shfl_xor(part, off);
-                const float bu_u = bu[u], bi_i = bi[i];
+                const float bu_u = load1<COH>(bu + u), bi_i = load1<COH>(bi + i);
                 const RatingStep<LOSS> st(s, part, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
                 if (q == 0) {
-                    bu[u] = st.new_bu;
-                    bi[i] = st.new_bi;
+                    store1<COH>(bu + u, st.new_bu);
+                    store1<COH>(bi + i, st.new_bi);
                 }
-                U4[ou] = make_float4(st.new_u(s, pu.x, qi.x), st.new_u(s, pu.y, qi.y),
-                                     st.new_u(s, pu.z, qi.z), st.new_u(s, pu.w, qi.w));
-                V4[oi] = make_float4(st.new_i(s, pu.x, qi.x), st.new_i(s, pu.y, qi.y),
-                                     st.new_i(s, pu.z, qi.z), st.new_i(s, pu.w, qi.w));
+                store4<COH>(U4 + ou, make_float4(st.new_u(s, pu.x, qi.x), st.new_u(s, pu.y, qi.y),
+                                             st.new_u(s, pu.z, qi.z), st.new_u(s, pu.w, qi.w)));
+                store4<COH>(V4 + oi, make_float4(st.new_i(s, pu.x, qi.x), st.new_i(s, pu.y, qi.y),
+                                             st.new_i(s, pu.z, qi.z), st.new_i(s, pu.w, qi.w)));
             }
         }
     }
@@ -444,10 +490,16 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     waves = blocks * 4;
     const int64_t chunk = (n + waves - 1) / waves;
     const int ld4 = h->ld / 4;
-#define MML_HOG(LPR)                                                                           \
-    bmf_sgd_hogwild_kernel<LOSS, LPR><<<(int)blocks, 256, 0, st>>>(                          \
+    const bool coh = h->p.schedule == MML_SCHEDULE_HOGWILD_COHERENT;
+#define MML_HOG1(LPR, COH)                                                                     \
+    bmf_sgd_hogwild_kernel<LOSS, LPR, COH><<<(int)blocks, 256, 0, st>>>(                     \
         h->su.get(), h->si.get(), h->sr.get(), n, chunk, h->U.get(), h->V.get(), h->bu.get(),  \
         h->bi.get(), ld4, s, cu, ci)
+#define MML_HOG(LPR)          \
+    if (coh)                  \
+        MML_HOG1(LPR, true);  \
+    else                      \
+        MML_HOG1(LPR, false)
     switch (h->lpr) {
         case 1: MML_HOG(1); break;
         case 2: MML_HOG(2); break;
@@ -458,6 +510,7 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
         default: MML_HOG(64); break;
     }
 #undef MML_HOG
+#undef MML_HOG1
     MML_HIP(hipGetLastError());
 }
 
@@ -503,7 +556,7 @@ extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params,
         MML_REQUIRE(params->loss >= MML_LOSS_RMSE && params->loss <= MML_LOSS_LOGISTIC,
                     "unknown loss");
         MML_REQUIRE(params->schedule >= MML_SCHEDULE_ORDERED &&
-                        params->schedule <= MML_SCHEDULE_HOGWILD,
+                        params->schedule <= MML_SCHEDULE_HOGWILD_COHERENT,
                     "unknown schedule");
         ctx->activate();
         auto* h = new mml_bmf();

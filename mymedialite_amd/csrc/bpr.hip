@@ -1,0 +1,462 @@
+// bpr.hip -- BPRMF pairwise SGD on MI355X (gfx950).
+//
+// Replaces BPRMF.Iterate() with its default sampler IterateWithoutReplacementUniformUser
+// (src/MyMediaLite/ItemRecommendation/BPRMF.cs:160-226), the triple samplers SampleUser /
+// SampleItemPair / SampleOtherItem (:275-321), UpdateFactors (:330-374) and Predict (:425-431).
+//
+// HBM layout (per mml_bpr handle):
+//   U [n_users x ld], V [n_items x ld]  fp32 row-major, ld = 4 * LPR (zero padded)
+//   bias [n_items]                      item biases
+//   off [n_users + 1] (int64), cols     user -> positive items, CSR, each row sorted and
+//                                       de-duplicated (the SparseBooleanMatrix sets)
+//   eligible [n_eligible]               users with 0 < |S_u| < n_items (SampleUser's acceptance set)
+//   ev_u, ev_i                          the events in visit order (UNIFORM_PAIR sampler only)
+//
+// Sampling is counter-based (splitmix64 of seed, sample index, draw index): sample s of an epoch is
+// a pure function of (seed, s), independent of which wave draws it.  The reference draws from one
+// sequential System.Random stream (variable draws per sample, HashSet insertion order for
+// ElementAt), which cannot be parallelised bit-exactly; the distribution is the same:
+//   u ~ Uniform(eligible)      == SampleUser's rejection loop
+//   i ~ Uniform(S_u)           == user_items.ElementAt(random.Next(|S_u|))
+//   j ~ Uniform(I \ S_u)       == SampleItemPair / SampleOtherItem's rejection loop
+// Parity is therefore statistical (AUC, tests/test_bpr_gpu.py).
+//
+// Update (Hogwild!, LPR lanes per triple, one float4 per lane of U_u, V_i, V_j): the reference's
+// float/double arithmetic -- x_uij = (b_i - b_j) + sum_f (double)(w_f * (h_if - h_jf)), double
+// sigmoid, double deltas, float stores -- with the f-sum as per-lane partials + xor butterfly.
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+#include "mml_internal.h"
+
+namespace {
+
+struct BprScalars {
+    float lr, reg_u, reg_i, reg_j, bias_reg;
+    int32_t update_j;
+};
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// uniform integer in [0, n) from draw d of sample s (Lemire multiply-shift on 32 high bits)
+__device__ __forceinline__ uint32_t draw(uint64_t seed, uint64_t s, uint32_t d, uint32_t n) {
+    const uint64_t x = splitmix64(seed ^ (s * 0xD1B54A32D192ED03ull + d));
+    return (uint32_t)(((x >> 32) * (uint64_t)n) >> 32);
+}
+
+// is item j in the sorted row [b, e)?  The LPR lanes of a group test a window of LPR entries per
+// round (one coalesced load), switching to a group-uniform binary search for long rows.
+template <int LPR>
+__device__ __forceinline__ bool row_contains(const int32_t* __restrict__ cols, int64_t b,
+                                             int64_t e, int32_t j, int q) {
+    if (e - b <= 4 * LPR) {
+        bool hit = false;
+        for (int64_t x = b + q; x < e; x += LPR) hit |= (cols[x] == j);
+        // OR over the group's lanes
+#pragma unroll
+        for (int off = LPR / 2; off >= 1; off >>= 1) hit |= (bool)__shfl_xor((int)hit, off);
+        return hit;
+    }
+    int64_t lo = b, hi = e;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (cols[mid] < j) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < e && cols[lo] == j;
+}
+
+template <int LPR, bool PAIR>
+__global__ __launch_bounds__(256) void bpr_hogwild_kernel(
+    const int64_t* __restrict__ off, const int32_t* __restrict__ cols,
+    const int32_t* __restrict__ eligible, int32_t n_eligible, const int32_t* __restrict__ ev_u,
+    const int32_t* __restrict__ ev_i, int64_t n_samples, int64_t chunk, int32_t n_items,
+    uint64_t seed, float* U, float* V, float* bias, int32_t ld4, BprScalars s) {
+    constexpr int RPW = 64 / LPR;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t begin = wave * chunk;
+    const int64_t end = min(begin + chunk, n_samples);
+    const int sub = lane / LPR, q = lane % LPR;
+    float4* U4 = reinterpret_cast<float4*>(U);
+    float4* V4 = reinterpret_cast<float4*>(V);
+    for (int64_t base = begin; base < end; base += RPW) {
+        const int64_t smp = base + sub;
+        if (smp >= end) continue;
+        int32_t u, i;
+        if constexpr (PAIR) {
+            u = ev_u[smp];
+            i = ev_i[smp];
+        } else {
+            u = eligible[draw(seed, smp, 0, (uint32_t)n_eligible)];
+            const int64_t b = off[u];
+            const uint32_t deg = (uint32_t)(off[u + 1] - b);
+            i = cols[b + draw(seed, smp, 1, deg)];
+        }
+        const int64_t ou = (int64_t)u * ld4 + q, oi = (int64_t)i * ld4 + q;
+        const float4 w = U4[ou];
+        const float4 hi = V4[oi];
+        const int64_t rb = off[u], re = off[u + 1];
+        int32_t j;
+        for (uint32_t d = 2;; ++d) {
+            j = (int32_t)draw(seed, smp, d, (uint32_t)n_items);
+            if (!row_contains<LPR>(cols, rb, re, j, q)) break;
+        }
+        const int64_t oj = (int64_t)j * ld4 + q;
+        const float4 hj = V4[oj];
+        double part = (double)(w.x * (hi.x - hj.x));
+        part += (double)(w.y * (hi.y - hj.y));
+        part += (double)(w.z * (hi.z - hj.z));
+        part += (double)(w.w * (hi.w - hj.w));
+#pragma unroll
+        for (int o = LPR / 2; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+        const float bi = bias[i], bj = bias[j];
+        const double x_uij = (double)(bi - bj) + part;
+        const double e = 1.0 / (1.0 + exp(x_uij));
+        if (q == 0) {
+            bias[i] = bi + (float)((double)s.lr * (e - (double)(s.bias_reg * bi)));
+            if (s.update_j) bias[j] = bj + (float)((double)s.lr * (-e - (double)(s.bias_reg * bj)));
+        }
+        const double lr = s.lr;
+        auto upd_u = [&](float wf, float hif, float hjf) {
+            return (float)((double)wf + lr * ((double)(hif - hjf) * e - (double)(s.reg_u * wf)));
+        };
+        auto upd_i = [&](float wf, float hif) {
+            return (float)((double)hif + lr * ((double)wf * e - (double)(s.reg_i * hif)));
+        };
+        auto upd_j = [&](float wf, float hjf) {
+            return (float)((double)hjf + lr * ((double)(-wf) * e - (double)(s.reg_j * hjf)));
+        };
+        U4[ou] = make_float4(upd_u(w.x, hi.x, hj.x), upd_u(w.y, hi.y, hj.y),
+                             upd_u(w.z, hi.z, hj.z), upd_u(w.w, hi.w, hj.w));
+        V4[oi] = make_float4(upd_i(w.x, hi.x), upd_i(w.y, hi.y), upd_i(w.z, hi.z),
+                             upd_i(w.w, hi.w));
+        if (s.update_j)
+            V4[oj] = make_float4(upd_j(w.x, hj.x), upd_j(w.y, hj.y), upd_j(w.z, hj.z),
+                                 upd_j(w.w, hj.w));
+    }
+}
+
+// BPRMF.Predict (:425-431): item_bias[i] + RowScalarProduct (float, left to right);
+// float.MinValue for ids beyond the model.  MF.Predict (WRMF) passes bias = nullptr.
+__global__ __launch_bounds__(256) void mf_predict_kernel(
+    const int32_t* __restrict__ users, const int32_t* __restrict__ items, int64_t n,
+    int32_t n_users, int32_t n_items, const float* __restrict__ U, const float* __restrict__ V,
+    const float* __restrict__ bias, int32_t k, int32_t ld, float* __restrict__ out) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t u = users[x], i = items[x];
+        if (u < 0 || u >= n_users || i < 0 || i >= n_items) {
+            out[x] = -3.402823466e+38f;
+            continue;
+        }
+        const float* a = U + (int64_t)u * ld;
+        const float* c = V + (int64_t)i * ld;
+        float dot = 0.0f;
+        for (int f = 0; f < k; ++f) dot += a[f] * c[f];
+        out[x] = bias ? bias[i] + dot : dot;
+    }
+}
+
+inline int grid_for(int64_t n, int block = 256, int cap = 8192) {
+    const int64_t g = (n + block - 1) / block;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+inline int lanes_per_row(int k) {
+    const int vec = (k + 3) / 4;
+    int lpr = 1;
+    while (lpr < vec) lpr <<= 1;
+    return lpr;
+}
+
+}  // namespace
+
+struct mml_bpr {
+    mml_ctx* ctx = nullptr;
+    mml_bpr_params p{};
+    int32_t n_users = 0, n_items = 0, k = 0, ld = 0, lpr = 0;
+    mml::DeviceArray<float> U, V, bias, ev_out;
+    mml::DeviceArray<int64_t> off;
+    mml::DeviceArray<int32_t> cols, eligible, ev_u, ev_i, q_u, q_i;
+    int64_t n_events = 0, nnz = 0;
+    int32_t n_eligible = 0;
+    bool has_data = false, has_model = false, has_order = false;
+    float last_ms = 0.0f;
+};
+
+namespace {
+
+void upload_padded(mml_bpr* h, float* dst, const float* src, int64_t rows) {
+    if (rows == 0) return;
+    MML_HIP(hipMemsetAsync(dst, 0, sizeof(float) * rows * h->ld, h->ctx->stream));
+    MML_HIP(hipMemcpy2DAsync(dst, sizeof(float) * h->ld, src, sizeof(float) * h->k,
+                             sizeof(float) * h->k, rows, hipMemcpyHostToDevice, h->ctx->stream));
+}
+
+void download_padded(mml_bpr* h, float* dst, const float* src, int64_t rows) {
+    if (rows == 0) return;
+    MML_HIP(hipMemcpy2DAsync(dst, sizeof(float) * h->k, src, sizeof(float) * h->ld,
+                             sizeof(float) * h->k, rows, hipMemcpyDeviceToHost, h->ctx->stream));
+}
+
+}  // namespace
+
+using mml::guard;
+
+extern "C" mml_status mml_bpr_create(mml_ctx* ctx, const mml_bpr_params* params, int32_t n_users,
+                                     int32_t n_items, mml_bpr** out) {
+    return guard([&] {
+        MML_REQUIRE(ctx && params && out, "null argument");
+        MML_REQUIRE(n_users >= 1 && n_items >= 2, "need >= 1 user and >= 2 items");
+        MML_REQUIRE(params->num_factors >= 1 && params->num_factors <= 256,
+                    "num_factors must be in [1, 256]");
+        MML_REQUIRE(params->sampler == MML_BPR_SAMPLER_UNIFORM_USER ||
+                        params->sampler == MML_BPR_SAMPLER_UNIFORM_PAIR,
+                    "unknown sampler");
+        ctx->activate();
+        auto* h = new mml_bpr();
+        try {
+            h->ctx = ctx;
+            h->p = *params;
+            h->n_users = n_users;
+            h->n_items = n_items;
+            h->k = params->num_factors;
+            h->lpr = lanes_per_row(h->k);
+            h->ld = 4 * h->lpr;
+            h->U.alloc((size_t)n_users * h->ld);
+            h->V.alloc((size_t)n_items * h->ld);
+            h->bias.alloc(n_items);
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+extern "C" mml_status mml_bpr_destroy(mml_bpr* h) {
+    return guard([&] {
+        if (!h) return;
+        (void)hipSetDevice(h->ctx->device);
+        (void)hipStreamSynchronize(h->ctx->stream);
+        delete h;
+    });
+}
+
+extern "C" mml_status mml_bpr_set_data(mml_bpr* h, const int32_t* users, const int32_t* items,
+                                       int64_t n, const int32_t* order) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(n >= 1 && users && items, "need >= 1 event");
+        for (int64_t x = 0; x < n; ++x)
+            MML_REQUIRE(users[x] >= 0 && users[x] < h->n_users && items[x] >= 0 &&
+                            items[x] < h->n_items,
+                        "event user/item id out of range");
+        if (order)
+            for (int64_t x = 0; x < n; ++x)
+                MML_REQUIRE(order[x] >= 0 && order[x] < n, "order index out of range");
+        // user -> sorted distinct items (CSR), built on the host (counting sort by user)
+        std::vector<int64_t> off(h->n_users + 1, 0);
+        for (int64_t x = 0; x < n; ++x) ++off[users[x] + 1];
+        for (int32_t u = 0; u < h->n_users; ++u) off[u + 1] += off[u];
+        std::vector<int32_t> cols(n);
+        {
+            std::vector<int64_t> fill(off.begin(), off.end() - 1);
+            for (int64_t x = 0; x < n; ++x) cols[fill[users[x]]++] = items[x];
+        }
+        std::vector<int64_t> doff(h->n_users + 1, 0);
+        int64_t w = 0;
+        std::vector<int32_t> elig;
+        for (int32_t u = 0; u < h->n_users; ++u) {
+            auto b = cols.begin() + off[u], e = cols.begin() + off[u + 1];
+            std::sort(b, e);
+            auto last = std::unique(b, e);
+            for (auto it = b; it != last; ++it) cols[w++] = *it;
+            doff[u + 1] = w;
+            const int64_t deg = doff[u + 1] - doff[u];
+            if (deg > 0 && deg < h->n_items) elig.push_back(u);
+        }
+        MML_REQUIRE(!elig.empty(), "no user has 0 < |items| < n_items");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        h->nnz = w;
+        h->n_events = n;
+        h->n_eligible = (int32_t)elig.size();
+        h->off.alloc(h->n_users + 1);
+        h->cols.alloc(w);
+        h->eligible.alloc(elig.size());
+        MML_HIP(hipMemcpyAsync(h->off.get(), doff.data(), sizeof(int64_t) * doff.size(),
+                               hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(h->cols.get(), cols.data(), sizeof(int32_t) * w,
+                               hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(h->eligible.get(), elig.data(), sizeof(int32_t) * elig.size(),
+                               hipMemcpyHostToDevice, st));
+        // events in visit order (UNIFORM_PAIR): Feedback.RandomIndex order
+        std::vector<int32_t> eu(n), ei(n);
+        for (int64_t x = 0; x < n; ++x) {
+            const int64_t o = order ? order[x] : x;
+            eu[x] = users[o];
+            ei[x] = items[o];
+        }
+        h->ev_u.alloc(n);
+        h->ev_i.alloc(n);
+        MML_HIP(hipMemcpyAsync(h->ev_u.get(), eu.data(), sizeof(int32_t) * n,
+                               hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(h->ev_i.get(), ei.data(), sizeof(int32_t) * n,
+                               hipMemcpyHostToDevice, st));
+        MML_HIP(hipStreamSynchronize(st));
+        h->has_data = true;
+    });
+}
+
+extern "C" mml_status mml_bpr_set_model(mml_bpr* h, const float* U, const float* V,
+                                        const float* item_bias) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(U && V && item_bias, "null model arrays");
+        h->ctx->activate();
+        upload_padded(h, h->U.get(), U, h->n_users);
+        upload_padded(h, h->V.get(), V, h->n_items);
+        MML_HIP(hipMemcpyAsync(h->bias.get(), item_bias, sizeof(float) * h->n_items,
+                               hipMemcpyHostToDevice, h->ctx->stream));
+        MML_HIP(hipStreamSynchronize(h->ctx->stream));
+        h->has_model = true;
+    });
+}
+
+extern "C" mml_status mml_bpr_get_model(mml_bpr* h, float* U, float* V, float* item_bias) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(h->has_model, "no model");
+        h->ctx->activate();
+        if (U) download_padded(h, U, h->U.get(), h->n_users);
+        if (V) download_padded(h, V, h->V.get(), h->n_items);
+        if (item_bias)
+            MML_HIP(hipMemcpyAsync(item_bias, h->bias.get(), sizeof(float) * h->n_items,
+                                   hipMemcpyDeviceToHost, h->ctx->stream));
+        MML_HIP(hipStreamSynchronize(h->ctx->stream));
+    });
+}
+
+extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        BprScalars s;
+        s.lr = h->p.learn_rate;
+        s.reg_u = h->p.reg_u;
+        s.reg_i = h->p.reg_i;
+        s.reg_j = h->p.reg_j;
+        s.bias_reg = h->p.bias_reg;
+        s.update_j = h->p.update_j;
+        const int64_t n = h->n_events;  // Feedback.Count samples per epoch (:218)
+        static const int64_t min_chunk = [] {
+            const char* e = std::getenv("MML_HOGWILD_MIN_CHUNK");
+            return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)16384;
+        }();
+        int64_t waves = std::min<int64_t>(256 * 32, std::max<int64_t>(1, n / min_chunk));
+        const int64_t blocks = (waves + 3) / 4;
+        waves = blocks * 4;
+        const int64_t chunk = (n + waves - 1) / waves;
+        const bool pair = h->p.sampler == MML_BPR_SAMPLER_UNIFORM_PAIR;
+        MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
+#define MML_BPR(LPR)                                                                            \
+    if (pair)                                                                                   \
+        bpr_hogwild_kernel<LPR, true><<<(int)blocks, 256, 0, st>>>(                           \
+            h->off.get(), h->cols.get(), h->eligible.get(), h->n_eligible, h->ev_u.get(),       \
+            h->ev_i.get(), n, chunk, h->n_items, seed, h->U.get(), h->V.get(), h->bias.get(),   \
+            h->ld / 4, s);                                                                      \
+    else                                                                                        \
+        bpr_hogwild_kernel<LPR, false><<<(int)blocks, 256, 0, st>>>(                          \
+            h->off.get(), h->cols.get(), h->eligible.get(), h->n_eligible, h->ev_u.get(),       \
+            h->ev_i.get(), n, chunk, h->n_items, seed, h->U.get(), h->V.get(), h->bias.get(),   \
+            h->ld / 4, s)
+        switch (h->lpr) {
+            case 1: MML_BPR(1); break;
+            case 2: MML_BPR(2); break;
+            case 4: MML_BPR(4); break;
+            case 8: MML_BPR(8); break;
+            case 16: MML_BPR(16); break;
+            case 32: MML_BPR(32); break;
+            default: MML_BPR(64); break;
+        }
+#undef MML_BPR
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipEventRecord(h->ctx->ev_end, st));
+        MML_HIP(hipEventSynchronize(h->ctx->ev_end));
+        MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));
+    });
+}
+
+extern "C" mml_status mml_bpr_last_timing(mml_bpr* h, float* out) {
+    return guard([&] {
+        MML_REQUIRE(h && out, "null argument");
+        out[0] = h->last_ms;
+        out[1] = 1.0f;
+    });
+}
+
+extern "C" mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const int32_t* items,
+                                      int64_t n, float* out) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(n >= 0 && (n == 0 || (users && items && out)), "bad arguments");
+        if (n == 0) return;
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        h->q_u.alloc(n);
+        h->q_i.alloc(n);
+        h->ev_out.alloc(n);
+        MML_HIP(hipMemcpyAsync(h->q_u.get(), users, sizeof(int32_t) * n, hipMemcpyHostToDevice,
+                               st));
+        MML_HIP(hipMemcpyAsync(h->q_i.get(), items, sizeof(int32_t) * n, hipMemcpyHostToDevice,
+                               st));
+        mf_predict_kernel<<<grid_for(n), 256, 0, st>>>(h->q_u.get(), h->q_i.get(), n, h->n_users,
+                                                       h->n_items, h->U.get(), h->V.get(),
+                                                       h->bias.get(), h->k, h->ld,
+                                                       h->ev_out.get());
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipMemcpyAsync(out, h->ev_out.get(), sizeof(float) * n, hipMemcpyDeviceToHost,
+                               st));
+        MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+__global__ __launch_bounds__(256) void bpr_scale_kernel(float* __restrict__ a, int64_t n,
+                                                        float f) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x)
+        a[x] *= f;
+}
+
+extern "C" mml_status mml_bpr_allreduce_items(mml_bpr* h) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        mml_ctx* c = h->ctx;
+        if (c->nranks <= 1) return;
+        MML_REQUIRE(c->comm, "context has no communicator (mml_ctx_comm_init)");
+        c->activate();
+        hipStream_t st = c->stream;
+        const size_t nv = (size_t)h->n_items * h->ld;
+        MML_RCCL(ncclGroupStart());
+        MML_RCCL(ncclAllReduce(h->V.get(), h->V.get(), nv, ncclFloat, ncclSum, c->comm, st));
+        MML_RCCL(ncclAllReduce(h->bias.get(), h->bias.get(), (size_t)h->n_items, ncclFloat,
+                               ncclSum, c->comm, st));
+        MML_RCCL(ncclGroupEnd());
+        const float f = 1.0f / (float)c->nranks;
+        bpr_scale_kernel<<<grid_for((int64_t)nv), 256, 0, st>>>(h->V.get(), (int64_t)nv, f);
+        bpr_scale_kernel<<<grid_for(h->n_items), 256, 0, st>>>(h->bias.get(), h->n_items, f);
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipStreamSynchronize(st));
+    });
+}

@@ -1,0 +1,261 @@
+"""GPU-backed MyMediaLite.ItemRecommendation recommenders (host mirrors).
+
+* ``BPRMF`` -- src/MyMediaLite/ItemRecommendation/BPRMF.cs:73-552 (+ MF.cs:29-196): same public
+  properties and defaults; Train() = InitModel + NumIter x Iterate(); the triple sampling and
+  UpdateFactors run in libmml_hip.so (bpr.hip).
+* ``WRMF``  -- src/MyMediaLite/ItemRecommendation/WRMF.cs:53-180: implicit ALS, fp64 row solves on
+  the GPU (wrmf.hip).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .data import PosOnlyFeedback
+from .random import Random
+from .recommender import Recommender
+
+
+class _MFBase(Recommender):
+    """ItemRecommendation.MF (MF.cs:29-196): factor matrices, InitModel, Train loop."""
+
+    def __init__(self):
+        self.InitMean = 0.0
+        self.InitStdDev = 0.1
+        self.NumFactors = 10
+        self.NumIter = 30
+        self.Device = 0
+        self._feedback = None
+        self._ctx = None
+        self._h = None
+        self._host = None
+
+    @property
+    def feedback(self) -> PosOnlyFeedback:
+        return self._feedback
+
+    @feedback.setter
+    def feedback(self, f: PosOnlyFeedback):
+        """ItemRecommender.Feedback setter (ItemRecommendation/ItemRecommender.cs:45-53)."""
+        self._feedback = f
+        self.MaxUserID = f.max_user_id
+        self.MaxItemID = f.max_item_id
+
+    def _init_factors(self):
+        """MF.InitModel (MF.cs:51-58): U fully, then V fully, N(InitMean, InitStdDev)."""
+        k = int(self.NumFactors)
+        nu, ni = self.MaxUserID + 1, self.MaxItemID + 1
+        rng = Random.get_instance()
+        U = rng.fill_normal(nu * k, self.InitMean, self.InitStdDev).reshape(nu, k)
+        V = rng.fill_normal(ni * k, self.InitMean, self.InitStdDev).reshape(ni, k)
+        return U, V
+
+    def train(self):
+        """MF.Train (MF.cs:61-67)."""
+        self.init_model()
+        for _ in range(int(self.NumIter)):
+            self.iterate()
+
+    def _release(self):
+        raise NotImplementedError
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+
+class BPRMF(_MFBase):
+    PROPERTIES = {
+        "BiasReg": "float", "Device": "int", "InitMean": "double", "InitStdDev": "double",
+        "LearnRate": "float", "NumFactors": "uint", "NumIter": "uint", "RegI": "float",
+        "RegJ": "float", "RegU": "float", "UniformUserSampling": "bool", "UpdateJ": "bool",
+        "WithReplacement": "bool",
+    }
+
+    def __init__(self, **kw):
+        super().__init__()
+        # BPRMF defaults (BPRMF.cs:79-100)
+        self.WithReplacement = False
+        self.UniformUserSampling = True
+        self.BiasReg = 0.0
+        self.LearnRate = 0.05
+        self.RegU = 0.0025
+        self.RegI = 0.0025
+        self.RegJ = 0.00025
+        self.UpdateJ = True
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+    def _sampler(self) -> int:
+        if self.WithReplacement:
+            raise NotImplementedError(
+                "WithReplacement=true samplers (BPRMF.cs:183-211, :231-243) are not on the GPU path")
+        return N.BPR_SAMPLER_UNIFORM_USER if self.UniformUserSampling else \
+            N.BPR_SAMPLER_UNIFORM_PAIR
+
+    def init_model(self):
+        """InitModel (BPRMF.cs:121-126): MF factors + zero item biases; data to the device."""
+        U, V = self._init_factors()
+        bias = np.zeros(self.MaxItemID + 1, np.float32)
+        self._release()
+        self._ctx = N.Context(self.Device)
+        f = lambda x: float(np.float32(x))
+        p = N.BprParams(int(self.NumFactors), self._sampler(), int(bool(self.UpdateJ)),
+                        f(self.LearnRate), f(self.RegU), f(self.RegI), f(self.RegJ),
+                        f(self.BiasReg))
+        h = N._vp()
+        N.check(N.lib().mml_bpr_create(self._ctx.handle, ctypes.byref(p), self.MaxUserID + 1,
+                                       self.MaxItemID + 1, ctypes.byref(h)))
+        self._h = h
+        fb = self._feedback
+        order = None
+        if not self.UniformUserSampling:  # Feedback.RandomIndex (:250), shuffled once
+            order = Random.get_instance().shuffle(np.arange(fb.count, dtype=np.int32))
+        N.check(N.lib().mml_bpr_set_data(h, N.ptr(fb.users, N._i32p), N.ptr(fb.items, N._i32p),
+                                         fb.count, N.ptr(order, N._i32p)))
+        N.check(N.lib().mml_bpr_set_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
+                                          N.ptr(bias, N._f32p)))
+        self._host = dict(U=U, V=V, bias=bias)
+
+    def iterate(self):
+        """Iterate() (:160-178): one epoch of Feedback.Count sampled triples on the GPU.  The
+        device sampler is keyed by a 62-bit seed drawn from MyMediaLite.Random per epoch."""
+        rng = Random.get_instance()
+        seed = (rng.next(2147483647) << 31) ^ rng.next(2147483647)
+        N.check(N.lib().mml_bpr_iterate(self._h, ctypes.c_uint64(seed)))
+        self._host = None
+
+    def last_epoch_ms(self) -> float:
+        out = np.zeros(2, np.float32)
+        N.check(N.lib().mml_bpr_last_timing(self._h, N.ptr(out, N._f32p)))
+        return float(out[0])
+
+    def get_model(self):
+        if self._host is None:
+            k = int(self.NumFactors)
+            U = np.empty((self.MaxUserID + 1, k), np.float32)
+            V = np.empty((self.MaxItemID + 1, k), np.float32)
+            b = np.empty(self.MaxItemID + 1, np.float32)
+            N.check(N.lib().mml_bpr_get_model(self._h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
+                                              N.ptr(b, N._f32p)))
+            self._host = dict(U=U, V=V, bias=b)
+        return self._host
+
+    @property
+    def user_factors(self):
+        return self.get_model()["U"]
+
+    @property
+    def item_factors(self):
+        return self.get_model()["V"]
+
+    @property
+    def item_bias(self):
+        return self.get_model()["bias"]
+
+    def predict(self, users, items) -> np.ndarray:
+        """Predict(int,int) (:425-431), batched on the GPU."""
+        u, i = N.i32(np.atleast_1d(users)), N.i32(np.atleast_1d(items))
+        out = np.empty(len(u), np.float32)
+        N.check(N.lib().mml_bpr_predict(self._h, N.ptr(u, N._i32p), N.ptr(i, N._i32p), len(u),
+                                        N.ptr(out, N._f32p)))
+        return out
+
+    def _release(self):
+        if self._h is not None:
+            N.lib().mml_bpr_destroy(self._h)
+            self._h = None
+        if self._ctx is not None:
+            self._ctx.close()
+            self._ctx = None
+
+    def __str__(self):
+        """BPRMF.ToString() (BPRMF.cs:540-551)."""
+        g = lambda x: f"{float(np.float32(x)):.7g}"
+        return (f"BPRMF num_factors={self.NumFactors} bias_reg={g(self.BiasReg)} "
+                f"reg_u={g(self.RegU)} reg_i={g(self.RegI)} reg_j={g(self.RegJ)} "
+                f"num_iter={self.NumIter} LearnRate={g(self.LearnRate)} "
+                f"uniform_user_sampling={self.UniformUserSampling} "
+                f"with_replacement={self.WithReplacement} update_j={self.UpdateJ}")
+
+
+class WRMF(_MFBase):
+    PROPERTIES = {
+        "Alpha": "double", "Device": "int", "InitMean": "double", "InitStdDev": "double",
+        "NumFactors": "uint", "NumIter": "uint", "Regularization": "double",
+    }
+
+    def __init__(self, **kw):
+        super().__init__()
+        self.Alpha = 1.0             # WRMF.cs:56
+        self.Regularization = 0.015  # WRMF.cs:59
+        self.NumIter = 15            # WRMF() :62-65
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+    def init_model(self):
+        """MF.InitModel (MF.cs:51-58) + the feedback sets on the device."""
+        U, V = self._init_factors()
+        self._release()
+        self._ctx = N.Context(self.Device)
+        p = N.WrmfParams(int(self.NumFactors), 0, float(self.Alpha), float(self.Regularization))
+        h = N._vp()
+        N.check(N.lib().mml_wrmf_create(self._ctx.handle, ctypes.byref(p), self.MaxUserID + 1,
+                                        self.MaxItemID + 1, ctypes.byref(h)))
+        self._h = h
+        fb = self._feedback
+        N.check(N.lib().mml_wrmf_set_data(h, N.ptr(fb.users, N._i32p), N.ptr(fb.items, N._i32p),
+                                          fb.count))
+        N.check(N.lib().mml_wrmf_set_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p)))
+        self._host = dict(U=U, V=V)
+
+    def iterate(self):
+        """WRMF.Iterate() (:68-73) on the GPU."""
+        N.check(N.lib().mml_wrmf_iterate(self._h))
+        self._host = None
+
+    def last_epoch_ms(self) -> float:
+        out = np.zeros(2, np.float32)
+        N.check(N.lib().mml_wrmf_last_timing(self._h, N.ptr(out, N._f32p)))
+        return float(out[0])
+
+    def get_model(self):
+        if self._host is None:
+            k = int(self.NumFactors)
+            U = np.empty((self.MaxUserID + 1, k), np.float32)
+            V = np.empty((self.MaxItemID + 1, k), np.float32)
+            N.check(N.lib().mml_wrmf_get_model(self._h, N.ptr(U, N._f32p), N.ptr(V, N._f32p)))
+            self._host = dict(U=U, V=V)
+        return self._host
+
+    @property
+    def user_factors(self):
+        return self.get_model()["U"]
+
+    @property
+    def item_factors(self):
+        return self.get_model()["V"]
+
+    def predict(self, users, items) -> np.ndarray:
+        u, i = N.i32(np.atleast_1d(users)), N.i32(np.atleast_1d(items))
+        out = np.empty(len(u), np.float32)
+        N.check(N.lib().mml_wrmf_predict(self._h, N.ptr(u, N._i32p), N.ptr(i, N._i32p), len(u),
+                                         N.ptr(out, N._f32p)))
+        return out
+
+    def _release(self):
+        if self._h is not None:
+            N.lib().mml_wrmf_destroy(self._h)
+            self._h = None
+        if self._ctx is not None:
+            self._ctx.close()
+            self._ctx = None
+
+    def __str__(self):
+        """WRMF.ToString() (WRMF.cs:170-177)."""
+        return (f"WRMF num_factors={self.NumFactors} regularization={self.Regularization:g} "
+                f"alpha={self.Alpha:g} num_iter={self.NumIter}")

@@ -8,7 +8,8 @@ Schedule (GPU-only property):
   * ``auto``    -> MaxThreads <= 1: ``ordered`` (the reference's sequential loop, exact);
                    MaxThreads > 1: ``dsgd`` (the reference's DSGD blocks, exact) or, with
                    NaiveParallelization, ``hogwild`` (the reference's racy mode);
-  * ``ordered`` / ``dsgd`` / ``hogwild`` to force one.
+  * ``ordered`` / ``dsgd`` / ``hogwild`` / ``hogwild_coherent`` to force one (the last keeps every
+    row access agent-coherent: closer to the sequential trajectory, slower on hot items).
 """
 from __future__ import annotations
 
@@ -22,7 +23,8 @@ from .random import Random
 from .recommender import Recommender
 
 _LOSS = {"RMSE": N.LOSS_RMSE, "MAE": N.LOSS_MAE, "LogisticLoss": N.LOSS_LOGISTIC}
-_SCHED = {"ordered": N.SCHEDULE_ORDERED, "dsgd": N.SCHEDULE_DSGD, "hogwild": N.SCHEDULE_HOGWILD}
+_SCHED = {"ordered": N.SCHEDULE_ORDERED, "dsgd": N.SCHEDULE_DSGD, "hogwild": N.SCHEDULE_HOGWILD,
+          "hogwild_coherent": N.SCHEDULE_HOGWILD_COHERENT}
 
 
 class BiasedMatrixFactorization(Recommender):

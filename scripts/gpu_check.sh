@@ -19,4 +19,14 @@ rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench_$TAG.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o bench \
     -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/bench_prof_$TAG.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -2 gpurun_out/bench_prof_$TAG.log
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+
+# HBM traffic counters, one counter group per pass (gfx950: FETCH_SIZE and WRITE_SIZE do not fit
+# one TCC pass), kernel trace only -- no sys/runtime/hip trace next to --pmc.
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc_${c}_$TAG -o pmc \
+      -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_${c}_$TAG.log 2>&1
+  rc=$?; echo "pmc $c rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done
+exit 0

@@ -1,0 +1,7 @@
+#!/bin/bash
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
+RUN_ORACLE=1 MML_HOGWILD_MIN_CHUNK=1000000 timeout -k 10 300 python scripts/exp_hogwild_mid.py 400000 100000 4000000 2>&1 | grep -E "oracle|hogwild" || exit 1
+for c in 100000 16384 4096 1024; do
+  RUN_ORACLE=0 MML_HOGWILD_MIN_CHUNK=$c timeout -k 10 300 python scripts/exp_hogwild_mid.py 400000 100000 4000000 2>&1 | grep hogwild || exit 1
+done
