@@ -476,16 +476,18 @@ template <int LOSS>
 void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const int32_t* ci) {
     hipStream_t st = h->ctx->stream;
     const int64_t n = h->n;
-    // waves: up to 256 CUs x 32, but every wave walks at least min_chunk ratings of the stream in
-    // order, which bounds the updates in flight to ~n / min_chunk * (64 / LPR).  Hogwild's staleness
-    // on a hot item scales with (updates in flight) x sum_i p_i^2 (p_i = item share), so small,
-    // skewed sets need few waves (C1: 4 waves) while C2 saturates HBM from ~1000 waves on.
+    // waves: up to 256 CUs x 32 (all resident at once), each walking >= min_chunk ratings of the
+    // stream in order.  Fewer than 16 waves' worth of work runs as ONE workgroup: a single CU keeps
+    // every row in one L1/L2, whereas 2+ workgroups land on different XCDs whose private write-back
+    // L2s replicate hot rows ("Hogwild and per-XCD caches"; C1: 4 waves on one CU
+    // RMSE +0.007 vs sequential, 19 waves on 5 CUs +0.12).  Measured on C2: 8,192 waves 21.3 ms,
+    // 6,103 waves 22.9 ms; a software-pipelined variant (rows one step ahead) was not faster.
     static const int64_t min_chunk = [] {
         const char* e = std::getenv("MML_HOGWILD_MIN_CHUNK");
-        return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)16384;
+        return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)12000;
     }();
-    const int64_t max_waves = 256 * 32;
-    int64_t waves = std::min<int64_t>(max_waves, std::max<int64_t>(1, n / min_chunk));
+    int64_t waves = std::min<int64_t>(256 * 32, std::max<int64_t>(1, n / min_chunk));
+    if (waves < 16) waves = 4;
     const int64_t blocks = (waves + 3) / 4;
     waves = blocks * 4;
     const int64_t chunk = (n + waves - 1) / waves;
@@ -495,11 +497,12 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     bmf_sgd_hogwild_kernel<LOSS, LPR, COH><<<(int)blocks, 256, 0, st>>>(                     \
         h->su.get(), h->si.get(), h->sr.get(), n, chunk, h->U.get(), h->V.get(), h->bu.get(),  \
         h->bi.get(), ld4, s, cu, ci)
-#define MML_HOG(LPR)          \
-    if (coh)                  \
-        MML_HOG1(LPR, true);  \
-    else                      \
-        MML_HOG1(LPR, false)
+#define MML_HOG(LPR)             \
+    if (coh) {                   \
+        MML_HOG1(LPR, true);     \
+    } else {                     \
+        MML_HOG1(LPR, false);    \
+    }
     switch (h->lpr) {
         case 1: MML_HOG(1); break;
         case 2: MML_HOG(2); break;
