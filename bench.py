@@ -37,8 +37,9 @@ import ctypes  # noqa: E402
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
+from mymedialite_amd.distributed import (env_rank, init_host_group, max_over_ranks,  # noqa: E402
+                                         share_unique_id)
 from mymedialite_amd.random import SystemRandom  # noqa: E402
 from mymedialite_amd.synthetic import planted_ratings_torch  # noqa: E402
 
@@ -64,11 +65,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("gloo", init_method="env://")
+    world, rank, local = env_rank()
+    init_host_group(world)  # gloo, host coordination only; the data path is RCCL
     k = args.k
     if world == 1:
         n_local = args.ratings or 100_000_000
@@ -84,11 +82,7 @@ def main():
 
     ctx = N.Context(local)
     if world > 1:
-        uid = torch.zeros(128, dtype=torch.uint8)
-        if rank == 0:
-            uid[:] = torch.frombuffer(bytearray(N.Context.unique_id()), dtype=torch.uint8)
-        dist.broadcast(uid, src=0)
-        ctx.comm_init(bytes(uid.tolist()), world, rank)
+        ctx.comm_init(share_unique_id(rank, N.Context.unique_id), world, rank)
 
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
@@ -147,7 +141,7 @@ def main():
     for _ in range(args.warmup):
         step()
     if world > 1:
-        dist.barrier()
+        torch.distributed.barrier()
     torch.cuda.synchronize()
     kernel_ms = []
     t0 = time.perf_counter()
@@ -156,18 +150,23 @@ def main():
         kernel_ms.append(float(timing[0]))
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed)
     rmse = evaluate()
     total_updates = n_local * world * args.steps
     value = total_updates / elapsed
     avg_kernel_ms = float(np.mean(kernel_ms))
     bpu = bytes_per_update(k)
     achieved = n_local * bpu / (avg_kernel_ms * 1e-3) / 1e9
+    traffic, traffic_note = None, None
+    tf = os.path.join(ROOT, "profiles", "hogwild_c2_traffic.json")
+    if os.path.exists(tf) and k == 64 and n_local == 100_000_000 and world == 1:
+        t = json.load(open(tf))
+        traffic = t["traffic_bytes_per_launch"] / (avg_kernel_ms * 1e-3) / 1e9
+        traffic_note = (f"{t['traffic_bytes_per_launch'] / 1e9:.1f} GB per launch (PMC FETCH_SIZE/"
+                        f"WRITE_SIZE, calibrated on a known-byte run: {tf[len(ROOT) + 1:]}) vs "
+                        f"{n_local * bpu / 1e9:.1f} GB algorithmic")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -193,7 +192,8 @@ def main():
             "final_rmse": rmse,
             "initial_rmse": rmse0,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_note": traffic_note,
                          "kernel": f"bmf_sgd_hogwild_kernel<RMSE,{max(1, (k + 3) // 4)}>",
                          "kernel_avg_ms": avg_kernel_ms, "bytes_per_update": bpu},
             "cpu_baseline": cpu,
@@ -202,7 +202,7 @@ def main():
     N.lib().mml_bmf_destroy(h)
     ctx.close()
     if world > 1:
-        dist.destroy_process_group()
+        torch.distributed.destroy_process_group()
 
 
 def cpu_baseline(h, k, n_users, n_items, gb, seconds, sample):

@@ -29,4 +29,12 @@ for c in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "pmc $c rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/cal_${c}_$TAG -o cal \
+     -- python scripts/pmc_calibrate.py > gpurun_out/cal_${c}_$TAG.log 2>&1
+  rc=$?; echo "cal $c rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done
+python scripts/pmc_traffic.py gpurun_out/pmc_FETCH_SIZE_$TAG gpurun_out/pmc_WRITE_SIZE_$TAG \
+    gpurun_out/cal_FETCH_SIZE_$TAG gpurun_out/cal_WRITE_SIZE_$TAG gpurun_out/traffic_$TAG.json
 exit 0

@@ -1,0 +1,104 @@
+"""N > 1 path on the CPU: world_size-2 gloo processes (the GPU collective is RCCL inside the
+library; here we test the host orchestration and the user-shard + item-averaging algorithm with
+the oracle standing in for each rank's GPU epoch)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from mymedialite_amd.distributed import balanced_user_shards, shard_ratings
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_balanced_user_shards():
+    rs = np.random.default_rng(0)
+    cnt = rs.integers(0, 200, 1000)
+    for world in (1, 2, 3, 8):
+        b = balanced_user_shards(cnt, world)
+        assert b[0] == 0 and b[-1] == 1000 and np.all(np.diff(b) >= 0)
+        loads = [cnt[b[r]:b[r + 1]].sum() for r in range(world)]
+        assert sum(loads) == cnt.sum()
+        assert max(loads) - min(loads) <= 2 * cnt.max() + 1
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tests")]
+    import torch
+    import torch.distributed as dist
+
+    import oracle as O
+    from golden_cases import synth_ratings
+    from mymedialite_amd.distributed import (init_host_group, max_over_ranks, share_unique_id,
+                                             balanced_user_shards, shard_ratings)
+
+    init_host_group(world)
+    uid = share_unique_id(rank, lambda: bytes(range(128)))
+    assert uid == bytes(range(128))
+    t = max_over_ranks(float(rank + 1))
+    # user-sharded SGD epoch + item averaging (what bench.py does with RCCL on the GPU)
+    u, i, v = synth_ratings(7, 400, 120, 30000)
+    nu, ni, k = 400, 120, 8
+    r = O.Rng(1)
+    U = r.fill_normal(nu * k, 0, 0.1).reshape(nu, k)
+    V = r.fill_normal(ni * k, 0, 0.1).reshape(ni, k)
+    bu, bi = np.zeros(nu, np.float32), np.zeros(ni, np.float32)
+    gb = O.global_bias(v, 1.0, 5.0)
+    b = balanced_user_shards(np.bincount(u, minlength=nu), world)
+    su, si, sv = shard_ratings(u, i, v, b, rank)
+    kw = dict(gb=gb, min_rating=np.float32(1), range_=np.float32(4), lr=np.float32(0.01))
+    for _ in range(3):
+        O.bmf_iterate(su, si, sv, np.arange(len(su), dtype=np.int32), U, V, bu, bi, **kw)
+        tv = torch.from_numpy(np.concatenate([V.ravel(), bi]))
+        dist.all_reduce(tv)
+        tv /= world
+        V[:] = tv[: ni * k].numpy().reshape(ni, k)
+        bi[:] = tv[ni * k:].numpy()
+    # every rank holds the same items; users are rank-local
+    lo, hi = b[rank], b[rank + 1]
+    np.save(os.path.join(out_dir, f"r{rank}.npy"),
+            np.concatenate([[t], V.ravel(), bi, U[lo:hi].ravel()]).astype(np.float64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_user_shards_with_item_averaging(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    a, b = np.load(tmp_path / "r0.npy"), np.load(tmp_path / "r1.npy")
+    assert a[0] == b[0] == 2.0  # max over ranks
+    nik = 120 * 8 + 120
+    np.testing.assert_array_equal(a[1:1 + nik], b[1:1 + nik])  # identical item side after averaging
+
+    # the averaged 2-rank model learns like the single-rank one (statistical check)
+    import oracle as O
+    from golden_cases import synth_ratings
+    u, i, v = synth_ratings(7, 400, 120, 30000)
+    V = a[1:1 + 960].astype(np.float32).reshape(120, 8)
+    bi = a[1 + 960:1 + nik].astype(np.float32)
+    cnt = np.bincount(u, minlength=400)
+    bnd = balanced_user_shards(cnt, 2)
+    U = np.concatenate([a[1 + nik:], b[1 + nik:]]).astype(np.float32).reshape(400, 8)
+    bu = np.zeros(400, np.float32)  # user biases are rank-local; evaluate with factors + item side
+    gb = O.global_bias(v, 1.0, 5.0)
+    p = O.bmf_predict(u, i, U, V, bu, bi, gb, np.float32(1), np.float32(4))
+    rm2 = O.rating_eval(p, v)[0]
+    r = O.Rng(1)
+    U0 = r.fill_normal(400 * 8, 0, 0.1).reshape(400, 8)
+    V0 = r.fill_normal(120 * 8, 0, 0.1).reshape(120, 8)
+    p0 = O.bmf_predict(u, i, U0, V0, bu, np.zeros(120, np.float32), gb, np.float32(1),
+                       np.float32(4))
+    assert rm2 < O.rating_eval(p0, v)[0]
+    assert bnd[1] > 0
