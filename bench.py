@@ -63,7 +63,11 @@ def main():
     ap.add_argument("--schedule", default="hogwild", choices=["hogwild", "ordered"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3"],
+                    help="c2 (default; N>1 = C4 weak scaling): BiasedMF; c3: BPRMF k=128")
     args = ap.parse_args()
+    if args.workload == "c3":
+        return bench_bpr(args)
 
     world, rank, local = env_rank()
     init_host_group(world)  # gloo, host coordination only; the data path is RCCL
@@ -232,6 +236,113 @@ def cpu_baseline(h, k, n_users, n_items, gb, seconds, sample):
             "sample": f"{n} ratings of the C2 stream itself (the GPU's training data), k={k}, "
                       f"oracle Iterate() = C restatement of BiasedMatrixFactorization.cs:264-310, "
                       f"single thread, {dt:.1f} s"}
+
+
+def bench_bpr(args):
+    """C3: BPRMF, 10M users x 1M items, 500M positive events, k = 128, one GPU.  One step = one
+    BPRMF.Iterate() = Feedback.Count sampled triples (BPRMF.cs:160-226)."""
+    world, rank, local = env_rank()
+    if world != 1:
+        raise SystemExit("the C3 workload is a single-GPU configuration")
+    k = 128 if args.k == 64 else args.k
+    n_users, n_items = args.users or 10_000_000, 1_000_000
+    n = args.ratings or 500_000_000
+    ctx = N.Context(local)
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2)
+    from mymedialite_amd.synthetic import zipf_cdf
+    cdf = torch.from_numpy(zipf_cdf(n_items, 0.8)).to(dev)
+    perm = torch.randperm(n_items, generator=g, device=dev)
+    users = torch.empty(n, dtype=torch.int32, device=dev)
+    items = torch.empty(n, dtype=torch.int32, device=dev)
+    for s0 in range(0, n, 1 << 26):
+        e = min(n, s0 + (1 << 26))
+        users[s0:e] = torch.randint(0, n_users, (e - s0,), generator=g, device=dev,
+                                    dtype=torch.int32)
+        x = torch.rand(e - s0, generator=g, device=dev, dtype=torch.float64)
+        items[s0:e] = perm[torch.searchsorted(cdf, x).clamp_(max=n_items - 1)].to(torch.int32)
+    torch.cuda.synchronize()
+    p = N.BprParams(k, N.BPR_SAMPLER_UNIFORM_USER, 1, 0.05, 0.0025, 0.0025, 0.00025, 0.0)
+    h = N._vp()
+    N.check(N.lib().mml_bpr_create(ctx.handle, ctypes.byref(p), n_users, n_items,
+                                   ctypes.byref(h)))
+    t0 = time.perf_counter()
+    N.check(N.lib().mml_bpr_set_data_device(h, users.data_ptr(), items.data_ptr(), n, None))
+    ingest_s = time.perf_counter() - t0
+    del users, items
+    torch.cuda.empty_cache()
+    N.check(N.lib().mml_bpr_init_model(h, 2, 0.0, 0.1))
+    timing = np.zeros(2, np.float32)
+    for w in range(args.warmup):
+        N.check(N.lib().mml_bpr_iterate(h, 1000 + w))
+    torch.cuda.synchronize()
+    ms = []
+    t0 = time.perf_counter()
+    for step in range(args.steps):
+        N.check(N.lib().mml_bpr_iterate(h, 2000 + step))
+        N.lib().mml_bpr_last_timing(h, N.ptr(timing, N._f32p))
+        ms.append(float(timing[0]))
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    bpu = 24 * k + 32  # U_u, V_i, V_j read + write (24k) + b_i, b_j (16) + sampling (16)
+    avg_ms = float(np.mean(ms))
+    achieved = n * bpu / (avg_ms * 1e-3) / 1e9
+    cpu = None if args.no_cpu_baseline else cpu_baseline_bpr(k, args.cpu_seconds)
+    line = {
+        "metric": "BPR triple-updates/sec, BPRMF k=128 (C3)", "value": n * args.steps / elapsed,
+        "unit": "triple-updates/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (users uniform, items Zipf(0.8), generated in HBM)",
+        "config": {"workload": "C3: BPRMF 10M users x 1M items, 500M positives, k=128",
+                   "num_factors": k, "events": n, "users": n_users, "items": n_items,
+                   "sampler": "uniform_user (BPRMF default)", "device_ingest_s": ingest_s},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": f"bpr_hogwild_kernel<{max(1, (k + 3) // 4)},false>",
+                     "kernel_avg_ms": avg_ms, "bytes_per_update": bpu},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    N.lib().mml_bpr_destroy(h)
+    ctx.close()
+
+
+def cpu_baseline_bpr(k, seconds):
+    """Oracle BPR epoch (exact System.Random stream, single thread) on a 100k x 10k replica of the
+    C3 generator, run for ~`seconds`; reported as triples/s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    rs = np.random.default_rng(3)
+    nu, ni, n = 100_000, 10_000, 2_000_000
+    from mymedialite_amd.synthetic import zipf_cdf
+    u = rs.integers(0, nu, n).astype(np.int32)
+    i = np.searchsorted(zipf_cdf(ni, 0.8), rs.random(n)).clip(max=ni - 1).astype(np.int32)
+    off, rows = O.insertion_order_rows(u, i, nu)
+    srt = O.sorted_rows(off, rows)
+    rng = O.Rng(1)
+    U = rng.fill_normal(nu * k, 0, 0.1).reshape(nu, k)
+    V = rng.fill_normal(ni * k, 0, 0.1).reshape(ni, k)
+    b = np.zeros(ni, np.float32)
+    p = O._BprParams(k, 1, 1, 1, 0.05, 0.0025, 0.0025, 0.00025, 0.0, nu - 1, ni - 1)
+    L = O.lib()
+    probe = 20_000
+    t0 = time.perf_counter()
+    L.ora_bpr_epoch(rng._buf, ctypes.byref(p), O._p(off, O._i64p), O._p(rows, O._i32p),
+                    O._p(srt, O._i32p), probe, O._p(U, O._f32p), O._p(V, O._f32p),
+                    O._p(b, O._f32p), None)
+    dt = time.perf_counter() - t0
+    m = int(max(probe, seconds / max(dt, 1e-9) * probe))
+    t0 = time.perf_counter()
+    L.ora_bpr_epoch(rng._buf, ctypes.byref(p), O._p(off, O._i64p), O._p(rows, O._i32p),
+                    O._p(srt, O._i32p), m, O._p(U, O._f32p), O._p(V, O._f32p), O._p(b, O._f32p),
+                    None)
+    dt = time.perf_counter() - t0
+    return {"value": m / dt, "unit": "triple-updates/s", "cores": 1, "kind": "port",
+            "sample": f"{m} triples on a 100k x 10k replica of the C3 generator (2M events), k={k}, "
+                      f"oracle BPRMF sampler + UpdateFactors (BPRMF.cs:216-374), {dt:.1f} s"}
 
 
 if __name__ == "__main__":

@@ -158,12 +158,20 @@ mml_status mml_bpr_destroy(mml_bpr* h);
  * counted in Feedback.Count = samples per epoch); order = Feedback.RandomIndex for UNIFORM_PAIR. */
 mml_status mml_bpr_set_data(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t n,
                             const int32_t* order);
+/* Same from arrays already in this context's HBM; the sets are built on the device (csr.hip). */
+mml_status mml_bpr_set_data_device(mml_bpr* h, const int32_t* users_device,
+                                   const int32_t* items_device, int64_t n,
+                                   const int32_t* order_device);
 /* Model upload / download: U [n_users x k], V [n_items x k], item_bias [n_items]
  * (InitModel: MF.cs:51-58 + BPRMF.cs:121-126). */
 mml_status mml_bpr_set_model(mml_bpr* h, const float* user_factors, const float* item_factors,
                              const float* item_bias);
 mml_status mml_bpr_get_model(mml_bpr* h, float* user_factors, float* item_factors,
                              float* item_bias);
+/* InitModel on the device for models too large for the host RNG chain (C3: 1.4e9 normals):
+ * N(mean, stddev) from a counter-based generator keyed by seed; item biases = 0.  Statistically,
+ * not bitwise, equal to MF.InitModel's MathNet draws (MF.cs:51-58). */
+mml_status mml_bpr_init_model(mml_bpr* h, uint64_t seed, double mean, double stddev);
 /* One epoch = BPRMF.Iterate() (:160-178): Feedback.Count sampled triples, each followed by
  * UpdateFactors (:330-374).  seed keys the counter-based sampler (e.g. drawn from the host RNG). */
 mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed);

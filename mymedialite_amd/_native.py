@@ -94,8 +94,10 @@ SIGNATURES = {
                              ctypes.POINTER(_vp)]),
     "mml_bpr_destroy": (_st, [_vp]),
     "mml_bpr_set_data": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _i32p]),
+    "mml_bpr_set_data_device": (_st, [_vp, _vp, _vp, ctypes.c_int64, _vp]),
     "mml_bpr_set_model": (_st, [_vp, _f32p, _f32p, _f32p]),
     "mml_bpr_get_model": (_st, [_vp, _f32p, _f32p, _f32p]),
+    "mml_bpr_init_model": (_st, [_vp, ctypes.c_uint64, ctypes.c_double, ctypes.c_double]),
     "mml_bpr_iterate": (_st, [_vp, ctypes.c_uint64]),
     "mml_bpr_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
     "mml_bpr_last_timing": (_st, [_vp, _f32p]),

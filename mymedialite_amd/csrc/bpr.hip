@@ -250,69 +250,89 @@ extern "C" mml_status mml_bpr_destroy(mml_bpr* h) {
     });
 }
 
+namespace {
+
+__global__ __launch_bounds__(256) void bpr_gather_events_kernel(
+    const int32_t* __restrict__ users, const int32_t* __restrict__ items,
+    const int32_t* __restrict__ order, int64_t n, int32_t* __restrict__ eu,
+    int32_t* __restrict__ ei) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = order ? order[x] : x;
+        eu[x] = users[o];
+        ei[x] = items[o];
+    }
+}
+
+// Common device path: CSR of the sets on the device, eligible users, events in visit order.
+void bpr_ingest(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t n,
+                const int32_t* order) {
+    hipStream_t st = h->ctx->stream;
+    mml::DeviceCsr csr;
+    mml::build_csr_device(users, items, n, h->n_users, h->n_items, st, csr);
+    std::vector<int32_t> elig;
+    for (int32_t u = 0; u < h->n_users; ++u) {
+        const int32_t d = csr.deg_host[u];
+        if (d > 0 && d < h->n_items) elig.push_back(u);  // SampleUser's acceptance set
+    }
+    MML_REQUIRE(!elig.empty(), "no user has 0 < |items| < n_items");
+    h->off.swap(csr.off);
+    h->cols.swap(csr.cols);
+    h->nnz = csr.nnz;
+    h->n_events = n;
+    h->n_eligible = (int32_t)elig.size();
+    h->eligible.alloc(elig.size());
+    MML_HIP(hipMemcpyAsync(h->eligible.get(), elig.data(), sizeof(int32_t) * elig.size(),
+                           hipMemcpyHostToDevice, st));
+    if (h->p.sampler == MML_BPR_SAMPLER_UNIFORM_PAIR) {
+        h->ev_u.alloc(n);
+        h->ev_i.alloc(n);
+        bpr_gather_events_kernel<<<grid_for(n), 256, 0, st>>>(users, items, order, n,
+                                                              h->ev_u.get(), h->ev_i.get());
+        MML_HIP(hipGetLastError());
+    }
+    MML_HIP(hipStreamSynchronize(st));
+    h->has_data = true;
+}
+
+}  // namespace
+
 extern "C" mml_status mml_bpr_set_data(mml_bpr* h, const int32_t* users, const int32_t* items,
                                        int64_t n, const int32_t* order) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
         MML_REQUIRE(n >= 1 && users && items, "need >= 1 event");
-        for (int64_t x = 0; x < n; ++x)
-            MML_REQUIRE(users[x] >= 0 && users[x] < h->n_users && items[x] >= 0 &&
-                            items[x] < h->n_items,
-                        "event user/item id out of range");
         if (order)
             for (int64_t x = 0; x < n; ++x)
                 MML_REQUIRE(order[x] >= 0 && order[x] < n, "order index out of range");
-        // user -> sorted distinct items (CSR), built on the host (counting sort by user)
-        std::vector<int64_t> off(h->n_users + 1, 0);
-        for (int64_t x = 0; x < n; ++x) ++off[users[x] + 1];
-        for (int32_t u = 0; u < h->n_users; ++u) off[u + 1] += off[u];
-        std::vector<int32_t> cols(n);
-        {
-            std::vector<int64_t> fill(off.begin(), off.end() - 1);
-            for (int64_t x = 0; x < n; ++x) cols[fill[users[x]]++] = items[x];
-        }
-        std::vector<int64_t> doff(h->n_users + 1, 0);
-        int64_t w = 0;
-        std::vector<int32_t> elig;
-        for (int32_t u = 0; u < h->n_users; ++u) {
-            auto b = cols.begin() + off[u], e = cols.begin() + off[u + 1];
-            std::sort(b, e);
-            auto last = std::unique(b, e);
-            for (auto it = b; it != last; ++it) cols[w++] = *it;
-            doff[u + 1] = w;
-            const int64_t deg = doff[u + 1] - doff[u];
-            if (deg > 0 && deg < h->n_items) elig.push_back(u);
-        }
-        MML_REQUIRE(!elig.empty(), "no user has 0 < |items| < n_items");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
-        h->nnz = w;
-        h->n_events = n;
-        h->n_eligible = (int32_t)elig.size();
-        h->off.alloc(h->n_users + 1);
-        h->cols.alloc(w);
-        h->eligible.alloc(elig.size());
-        MML_HIP(hipMemcpyAsync(h->off.get(), doff.data(), sizeof(int64_t) * doff.size(),
-                               hipMemcpyHostToDevice, st));
-        MML_HIP(hipMemcpyAsync(h->cols.get(), cols.data(), sizeof(int32_t) * w,
-                               hipMemcpyHostToDevice, st));
-        MML_HIP(hipMemcpyAsync(h->eligible.get(), elig.data(), sizeof(int32_t) * elig.size(),
-                               hipMemcpyHostToDevice, st));
-        // events in visit order (UNIFORM_PAIR): Feedback.RandomIndex order
-        std::vector<int32_t> eu(n), ei(n);
-        for (int64_t x = 0; x < n; ++x) {
-            const int64_t o = order ? order[x] : x;
-            eu[x] = users[o];
-            ei[x] = items[o];
+        h->has_data = false;
+        mml::DeviceArray<int32_t> du, di, dord;
+        du.alloc(n);
+        di.alloc(n);
+        MML_HIP(hipMemcpyAsync(du.get(), users, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(di.get(), items, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+        if (order) {
+            dord.alloc(n);
+            MML_HIP(hipMemcpyAsync(dord.get(), order, sizeof(int32_t) * n, hipMemcpyHostToDevice,
+                                   st));
         }
-        h->ev_u.alloc(n);
-        h->ev_i.alloc(n);
-        MML_HIP(hipMemcpyAsync(h->ev_u.get(), eu.data(), sizeof(int32_t) * n,
-                               hipMemcpyHostToDevice, st));
-        MML_HIP(hipMemcpyAsync(h->ev_i.get(), ei.data(), sizeof(int32_t) * n,
-                               hipMemcpyHostToDevice, st));
-        MML_HIP(hipStreamSynchronize(st));
-        h->has_data = true;
+        bpr_ingest(h, du.get(), di.get(), n, order ? dord.get() : nullptr);
+    });
+}
+
+extern "C" mml_status mml_bpr_set_data_device(mml_bpr* h, const int32_t* users,
+                                              const int32_t* items, int64_t n,
+                                              const int32_t* order) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(n >= 1 && users && items, "need >= 1 event");
+        MML_REQUIRE(!order || h->p.sampler == MML_BPR_SAMPLER_UNIFORM_PAIR,
+                    "a device order is only used by the UNIFORM_PAIR sampler");
+        h->ctx->activate();
+        h->has_data = false;
+        bpr_ingest(h, users, items, n, order);
     });
 }
 
@@ -327,6 +347,48 @@ extern "C" mml_status mml_bpr_set_model(mml_bpr* h, const float* U, const float*
         MML_HIP(hipMemcpyAsync(h->bias.get(), item_bias, sizeof(float) * h->n_items,
                                hipMemcpyHostToDevice, h->ctx->stream));
         MML_HIP(hipStreamSynchronize(h->ctx->stream));
+        h->has_model = true;
+    });
+}
+
+namespace {
+
+// N(mean, stddev) fill of a [rows x ld] matrix (first k columns, padding zero) from a counter-based
+// generator: element e -> splitmix64(seed ^ e) -> Box-Muller.  Used for models too large for the
+// host RNG chain (C3: 1.41e9 normals); statistically, not bitwise, equal to InitNormal.
+__global__ __launch_bounds__(256) void init_normal_kernel(float* __restrict__ M, int64_t rows,
+                                                          int32_t k, int32_t ld, uint64_t seed,
+                                                          double mean, double stddev) {
+    const int64_t total = rows * ld;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t c = (int32_t)(e % ld);
+        if (c >= k) {
+            M[e] = 0.0f;
+            continue;
+        }
+        const uint64_t x = splitmix64(seed ^ (uint64_t)e * 0x9E3779B97F4A7C15ull);
+        const double u1 = ((x >> 11) + 1.0) * (1.0 / 9007199254740993.0);  // (0, 1]
+        const double u2 = (double)(splitmix64(x) >> 11) * (1.0 / 9007199254740992.0);
+        const double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+        M[e] = (float)(mean + stddev * z);
+    }
+}
+
+}  // namespace
+
+extern "C" mml_status mml_bpr_init_model(mml_bpr* h, uint64_t seed, double mean, double stddev) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        init_normal_kernel<<<8192, 256, 0, st>>>(h->U.get(), h->n_users, h->k, h->ld, seed, mean,
+                                                 stddev);
+        init_normal_kernel<<<8192, 256, 0, st>>>(h->V.get(), h->n_items, h->k, h->ld,
+                                                 seed ^ 0x5DEECE66Dull, mean, stddev);
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipMemsetAsync(h->bias.get(), 0, sizeof(float) * h->n_items, st));
+        MML_HIP(hipStreamSynchronize(st));
         h->has_model = true;
     });
 }

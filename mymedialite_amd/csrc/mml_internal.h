@@ -9,6 +9,8 @@
 #include <exception>
 #include <new>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "mml.h"
 
@@ -84,7 +86,21 @@ struct DeviceArray {
         count = n;
     }
     T* get() const { return ptr; }
+    void swap(DeviceArray& o) noexcept {
+        std::swap(ptr, o.ptr);
+        std::swap(count, o.count);
+    }
 };
+
+// CSR of the distinct (row, col) pairs of an event list, rows sorted by col (csr.hip).
+struct DeviceCsr {
+    DeviceArray<int64_t> off;   // [n_rows + 1]
+    DeviceArray<int32_t> cols;  // [nnz]
+    int64_t nnz = 0;
+    std::vector<int32_t> deg_host;  // distinct entries per row (host copy)
+};
+void build_csr_device(const int32_t* rows_device, const int32_t* cols_device, int64_t n,
+                      int32_t n_rows, int32_t n_cols, hipStream_t st, DeviceCsr& out);
 
 }  // namespace mml
 
