@@ -63,11 +63,14 @@ def main():
     ap.add_argument("--schedule", default="hogwild", choices=["hogwild", "ordered"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3"],
-                    help="c2 (default; N>1 = C4 weak scaling): BiasedMF; c3: BPRMF k=128")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
+                    help="c2 (default; N>1 = C4 weak scaling): BiasedMF; c3: BPRMF k=128; "
+                         "c5: WRMF k=256")
     args = ap.parse_args()
     if args.workload == "c3":
         return bench_bpr(args)
+    if args.workload == "c5":
+        return bench_wrmf(args)
 
     world, rank, local = env_rank()
     init_host_group(world)  # gloo, host coordination only; the data path is RCCL
@@ -308,6 +311,104 @@ def bench_bpr(args):
     print(json.dumps(line), flush=True)
     N.lib().mml_bpr_destroy(h)
     ctx.close()
+
+
+def bench_wrmf(args):
+    """C5 on one GPU: WRMF k=256, 5M users x 500k items, 500M positives (100 per user, Zipf(0.8)
+    items).  One step = one WRMF.Iterate() (WRMF.cs:68-73).  Flops per iteration as SURVEY 8(d)."""
+    world, rank, local = env_rank()
+    if world != 1:
+        raise SystemExit("the C5 bench runs one GPU here (row-shard all-gather: next)")
+    k = 256 if args.k == 64 else args.k
+    n_users, n_items = args.users or 5_000_000, 500_000
+    per_user = 100
+    n = n_users * per_user if not args.ratings else args.ratings
+    ctx = N.Context(local)
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    from mymedialite_amd.synthetic import zipf_cdf
+    cdf = torch.from_numpy(zipf_cdf(n_items, 0.8)).to(dev)
+    perm = torch.randperm(n_items, generator=g, device=dev)
+    users = (torch.arange(n, device=dev, dtype=torch.int64) // per_user).to(torch.int32)
+    items = torch.empty(n, dtype=torch.int32, device=dev)
+    for s0 in range(0, n, 1 << 26):
+        e = min(n, s0 + (1 << 26))
+        x = torch.rand(e - s0, generator=g, device=dev, dtype=torch.float64)
+        items[s0:e] = perm[torch.searchsorted(cdf, x).clamp_(max=n_items - 1)].to(torch.int32)
+    torch.cuda.synchronize()
+    p = N.WrmfParams(k, 0, 1.0, 0.015)
+    h = N._vp()
+    N.check(N.lib().mml_wrmf_create(ctx.handle, ctypes.byref(p), n_users, n_items,
+                                    ctypes.byref(h)))
+    t0 = time.perf_counter()
+    N.check(N.lib().mml_wrmf_set_data_device(h, users.data_ptr(), items.data_ptr(), n))
+    ingest_s = time.perf_counter() - t0
+    del users, items
+    torch.cuda.empty_cache()
+    N.check(N.lib().mml_wrmf_init_model(h, 5, 0.0, 0.1))
+    timing = np.zeros(2, np.float32)
+    for _ in range(args.warmup):
+        N.check(N.lib().mml_wrmf_iterate(h))
+    torch.cuda.synchronize()
+    ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        N.check(N.lib().mml_wrmf_iterate(h))
+        N.lib().mml_wrmf_last_timing(h, N.ptr(timing, N._f32p))
+        ms.append(float(timing[0]))
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    nnz = n  # distinct after de-duplication is slightly lower; SURVEY counts 500M
+    half = lambda rows, other: 2 * nnz * k * k + 2 * other * k * k + rows * (k ** 3 / 3 + 2 * k * k) \
+        + 2 * nnz * k
+    flops = half(n_users, n_items) + half(n_items, n_users)
+    tflops = flops / (np.mean(ms) * 1e-3) / 1e12
+    line = {
+        "metric": "WRMF iterations/sec, k=256 (C5, 1 GPU)", "value": args.steps / elapsed,
+        "unit": "iterations/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32 (k > 128: fp32 solve; HH in fp64)",
+        "data": "synthetic (100 positives per user, items Zipf(0.8), generated in HBM)",
+        "config": {"workload": "C5: WRMF 5M users x 500k items, 500M positives, k=256",
+                   "num_factors": k, "events": n, "users": n_users, "items": n_items,
+                   "alpha": 1.0, "regularization": 0.015, "device_ingest_s": ingest_s},
+        "roofline": {"bound": "mfma", "achieved": tflops, "peak": 157.3, "unit": "TFLOP/s",
+                     "frac": tflops / 157.3, "traffic": None,
+                     "kernel": "wrmf_solve_packed_kernel<float,256> + wrmf_gram_*",
+                     "kernel_avg_ms": float(np.mean(ms)), "flops_per_iteration": flops},
+        "cpu_baseline": None if args.no_cpu_baseline else cpu_baseline_wrmf(k, args.cpu_seconds,
+                                                                          n_users, n_items,
+                                                                          per_user),
+    }
+    print(json.dumps(line), flush=True)
+    N.lib().mml_wrmf_destroy(h)
+    ctx.close()
+
+
+def cpu_baseline_wrmf(k, seconds, n_users, n_items, per_user):
+    """Oracle WRMF row solve (fp64, single thread, WRMF.cs:110-156) timed on a sample of rows,
+    extrapolated to one iteration's rows (stated as extrapolated)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    rs = np.random.default_rng(5)
+    H = (rs.standard_normal((n_items, k)) * 0.1).astype(np.float32)
+    rows = 8
+    off = np.arange(0, (rows + 1) * per_user, per_user, dtype=np.int64)
+    cols = rs.integers(0, n_items, rows * per_user).astype(np.int32)
+    W = np.zeros((rows, k), np.float32)
+    HH = np.zeros((k, k), np.float64)
+    t0 = time.perf_counter()
+    O.lib().ora_wrmf_optimize_rows(O._p(off, O._i64p), O._p(cols, O._i32p), 0, rows, rows,
+                                   O._p(W, O._f32p), O._p(H, O._f32p), O._p(HH, O._f64p), k, 1.0,
+                                   0.015)
+    dt = (time.perf_counter() - t0) / rows
+    it = dt * (n_users + n_items)
+    return {"value": 1.0 / it, "unit": "iterations/s", "cores": 1, "kind": "port",
+            "sample": f"{rows} row solves (deg {per_user}, k={k}) of the oracle's fp64 "
+                      f"WRMF.Optimize(u) = {dt * 1e3:.1f} ms/row, extrapolated to "
+                      f"{n_users + n_items} rows per iteration (HH not included)"}
 
 
 def cpu_baseline_bpr(k, seconds):

@@ -184,7 +184,8 @@ mml_status mml_bpr_allreduce_items(mml_bpr* h);
 
 /* ------------------------------------------------------------------ WRMF */
 typedef struct {
-    int32_t num_factors;   /* NumFactors (MF.cs:43-45); <= 64 on this build */
+    int32_t num_factors;   /* NumFactors (MF.cs:43-45), <= 256: k <= 128 solves in fp64, k > 128
+                              in fp32 (packed A must fit the 160 KiB LDS) */
     int32_t reserved;
     double alpha;          /* Alpha (WRMF.cs:56) */
     double regularization; /* Regularization (WRMF.cs:59) */
@@ -198,6 +199,10 @@ mml_status mml_wrmf_destroy(mml_wrmf* h);
 /* Positive-only events; the user->items and item->users sets (Feedback.UserMatrix / ItemMatrix,
  * Data/PosOnlyFeedback.cs:35-83) are built from them. */
 mml_status mml_wrmf_set_data(mml_wrmf* h, const int32_t* users, const int32_t* items, int64_t n);
+mml_status mml_wrmf_set_data_device(mml_wrmf* h, const int32_t* users_device,
+                                    const int32_t* items_device, int64_t n);
+/* InitModel on the device (counter-based N(mean, stddev)); see mml_bpr_init_model. */
+mml_status mml_wrmf_init_model(mml_wrmf* h, uint64_t seed, double mean, double stddev);
 mml_status mml_wrmf_set_model(mml_wrmf* h, const float* user_factors, const float* item_factors);
 mml_status mml_wrmf_get_model(mml_wrmf* h, float* user_factors, float* item_factors);
 /* One WRMF.Iterate() (WRMF.cs:68-73): Optimize(users | items) then Optimize(items | users),

@@ -106,6 +106,8 @@ SIGNATURES = {
                               ctypes.POINTER(_vp)]),
     "mml_wrmf_destroy": (_st, [_vp]),
     "mml_wrmf_set_data": (_st, [_vp, _i32p, _i32p, ctypes.c_int64]),
+    "mml_wrmf_set_data_device": (_st, [_vp, _vp, _vp, ctypes.c_int64]),
+    "mml_wrmf_init_model": (_st, [_vp, ctypes.c_uint64, ctypes.c_double, ctypes.c_double]),
     "mml_wrmf_set_model": (_st, [_vp, _f32p, _f32p]),
     "mml_wrmf_get_model": (_st, [_vp, _f32p, _f32p]),
     "mml_wrmf_iterate": (_st, [_vp]),

@@ -14,8 +14,9 @@
 //
 // HBM layout: U [n_users x k], V [n_items x k] fp32 row-major (exactly Matrix<float>), the data as
 // two CSRs (user -> items, item -> users; sorted, de-duplicated = the SparseBooleanMatrix sets).
-// This round covers k <= 64 (A in LDS as double: 32 KiB); k = 256 (C5) needs the register-tiled
-// MFMA path described in DESIGN.md.
+// k <= 64: A in LDS as a full double matrix (32 KiB), column Cholesky (exact parity path).
+// 64 < k <= 128: block-packed lower triangle in double; 128 < k <= 256 (C5): the same in float
+// (140 KiB of LDS) -- see wrmf_solve_blocked_kernel.
 #include <algorithm>
 #include <vector>
 
@@ -26,37 +27,52 @@ namespace {
 constexpr int kMaxK = 64;
 constexpr int kChunk = 32;  // item rows staged in LDS per pass
 
-// Partial H^T H over a slice of rows: each thread owns entries e = t, t + 256, ... of the k x k
-// matrix (only f1 <= f2 are used later), rows are staged through LDS kChunk at a time.
+// Partial H^T H over a slice of rows, tiled: workgroup (tile, slice) computes one 64 x 64 tile
+// (ti <= tj) of HH over rows [slice * rows_per_slice, ...), each thread a 4 x 4 patch in double;
+// the tile's two 64-column strips of H are staged through LDS kChunk rows at a time.  Products are
+// float, sums double, like WRMF.ComputeSquareMatrix (WRMF.cs:94-108).
 __global__ __launch_bounds__(256) void wrmf_gram_partial_kernel(const float* __restrict__ H,
                                                                 int64_t rows, int32_t k,
-                                                                int64_t rows_per_block,
+                                                                int64_t rows_per_slice,
                                                                 double* __restrict__ partial) {
-    __shared__ float hs[kChunk][kMaxK];
+    __shared__ float sa[kChunk][64];
+    __shared__ float sb[kChunk][64];
     const int t = threadIdx.x;
-    const int kk = k * k;
-    double acc[kMaxK * kMaxK / 256];
-    for (int x = 0; x < kMaxK * kMaxK / 256; ++x) acc[x] = 0.0;
-    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-    const int64_t r1 = min(rows, r0 + rows_per_block);
+    const int nt = (k + 63) / 64;
+    int tile = blockIdx.x, ti = 0;
+    while (tile >= nt - ti) {  // enumerate (ti, tj) with ti <= tj
+        tile -= nt - ti;
+        ++ti;
+    }
+    const int tj = ti + tile;
+    const int slice = blockIdx.y;
+    const int pr = (t / 16) * 4, pc = (t % 16) * 4;  // this thread's 4 x 4 patch in the tile
+    double acc[4][4] = {};
+    const int64_t r0 = (int64_t)slice * rows_per_slice;
+    const int64_t r1 = min(rows, r0 + rows_per_slice);
     for (int64_t base = r0; base < r1; base += kChunk) {
         const int nr = (int)min((int64_t)kChunk, r1 - base);
         __syncthreads();
-        for (int e = t; e < nr * k; e += 256) hs[e / k][e % k] = H[(base + e / k) * k + e % k];
+        for (int e = t; e < kChunk * 64; e += 256) {
+            const int c = e / 64, f = e % 64;
+            const int fa = ti * 64 + f, fb = tj * 64 + f;
+            sa[c][f] = (c < nr && fa < k) ? H[(base + c) * k + fa] : 0.0f;
+            sb[c][f] = (c < nr && fb < k) ? H[(base + c) * k + fb] : 0.0f;
+        }
         __syncthreads();
-        for (int x = 0; x < kMaxK * kMaxK / 256; ++x) {
-            const int e = t + 256 * x;
-            if (e >= kk) break;
-            const int f1 = e / k, f2 = e % k;
-            double a = acc[x];
-            for (int c = 0; c < nr; ++c) a += (double)(hs[c][f1] * hs[c][f2]);
-            acc[x] = a;
+        for (int c = 0; c < nr; ++c) {
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) acc[x][y] += (double)(sa[c][pr + x] * sb[c][pc + y]);
         }
     }
-    for (int x = 0; x < kMaxK * kMaxK / 256; ++x) {
-        const int e = t + 256 * x;
-        if (e < kk) partial[(int64_t)blockIdx.x * kk + e] = acc[x];
-    }
+    const int64_t kk = (int64_t)k * k;
+    for (int x = 0; x < 4; ++x)
+        for (int y = 0; y < 4; ++y) {
+            const int f1 = ti * 64 + pr + x, f2 = tj * 64 + pc + y;
+            if (f1 < k && f2 < k) partial[(int64_t)slice * kk + (int64_t)f1 * k + f2] = acc[x][y];
+        }
 }
 
 // HH = sum of the partials in block order (deterministic), mirrored from the upper triangle.
@@ -67,7 +83,7 @@ __global__ __launch_bounds__(256) void wrmf_gram_reduce_kernel(const double* __r
     const int kk = k * k;
     if (e >= kk) return;
     const int f1 = e / k, f2 = e % k;
-    const int src = f1 <= f2 ? e : f2 * k + f1;
+    const int src = (f1 / 64) <= (f2 / 64) ? e : f2 * k + f1;
     double s = 0.0;
     for (int p = 0; p < nparts; ++p) s += partial[(int64_t)p * kk + src];
     HH[e] = s;
@@ -156,6 +172,315 @@ __global__ __launch_bounds__(256) void wrmf_solve_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k in (64, 256]: one workgroup (4 waves) per row; A lives in LDS as a BLOCK-PACKED lower triangle
+// of 8 x 8 blocks (block (bi, bj), bj <= bi, stored contiguously: element (i, j) at
+// BP(i/8, j/8) + 8*(i%8) + j%8), so every phase moves whole 32-B (float) / 64-B (double) block rows
+// with 16-B LDS accesses.  T = double for k <= 128 (78 KiB), float for k <= 256 (140 KiB; the
+// reference's doubles do not fit the 160 KiB LDS at k = 256).  b is appended as row k, so the
+// forward substitution L y = b happens inside the factorisation (y = row k of L).  Per row:
+//   1. Gram S = sum_i h_i h_i^T into A's blocks (acc in registers per block, chunks of the row's
+//      item vectors staged in LDS), b = sum_i h_i;
+//   2. A = HHp + alpha * S (HHp = HH + reg I, block-packed once per half-step), row k = (1+alpha) b;
+//   3. blocked right-looking Cholesky: wave 0 factors block column p in registers (pivot rows
+//      p*8+c live in lane c: broadcast by v_readlane), then all waves apply the rank-8 update to the
+//      trailing blocks;
+//   4. blocked backward substitution L^T w = y, one 8-block at a time.
+template <typename T>
+__device__ __forceinline__ void lds_load8(const T* p, T (&v)[8]) {
+    if constexpr (sizeof(T) == 4) {
+        const float4 a = reinterpret_cast<const float4*>(p)[0];
+        const float4 b = reinterpret_cast<const float4*>(p)[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const double2 a = reinterpret_cast<const double2*>(p)[x];
+            v[2 * x] = a.x;
+            v[2 * x + 1] = a.y;
+        }
+    }
+}
+__device__ __forceinline__ float bcast(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ double bcast(double v, int lane) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)u, lane);
+    const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Block rows are stored bank-rotated: the 16-B chunks of a block (16 for float, 32 for double)
+// are rotated by the block's linear index, so 16 lanes that touch the same row of 16 different
+// blocks (Gram, trailing update) hit 16 different LDS bank groups instead of one (a 16-way
+// conflict for ds_read_b128 with 256-B blocks: MI355X_MICROARCH.md, LDS).
+template <typename T>
+__device__ __forceinline__ int chunk_addr(int q, int chunk) {
+    constexpr int NCH = 64 * (int)sizeof(T) / 16;  // 16-B chunks per block
+    constexpr int PER = 16 / (int)sizeof(T);       // T per chunk
+    return q * 64 + ((chunk + q) & (NCH - 1)) * PER;
+}
+template <typename T>
+__device__ __forceinline__ void row_load8(const T* A, int q, int x, T (&v)[8]) {
+    constexpr int CPR = 8 * (int)sizeof(T) / 16;  // chunks per 8-element row
+    constexpr int PER = 16 / (int)sizeof(T);
+#pragma unroll
+    for (int c = 0; c < CPR; ++c) {
+        const T* p = A + chunk_addr<T>(q, x * CPR + c);
+        if constexpr (sizeof(T) == 4) {
+            const float4 a = *reinterpret_cast<const float4*>(p);
+            v[c * PER] = a.x; v[c * PER + 1] = a.y; v[c * PER + 2] = a.z; v[c * PER + 3] = a.w;
+        } else {
+            const double2 a = *reinterpret_cast<const double2*>(p);
+            v[c * PER] = a.x; v[c * PER + 1] = a.y;
+        }
+    }
+}
+template <typename T>
+__device__ __forceinline__ void row_store8(T* A, int q, int x, const T (&v)[8]) {
+    constexpr int CPR = 8 * (int)sizeof(T) / 16;
+    constexpr int PER = 16 / (int)sizeof(T);
+#pragma unroll
+    for (int c = 0; c < CPR; ++c) {
+        T* p = A + chunk_addr<T>(q, x * CPR + c);
+        if constexpr (sizeof(T) == 4)
+            *reinterpret_cast<float4*>(p) =
+                make_float4(v[c * PER], v[c * PER + 1], v[c * PER + 2], v[c * PER + 3]);
+        else
+            *reinterpret_cast<double2*>(p) = make_double2(v[c * PER], v[c * PER + 1]);
+    }
+}
+// element (x, y) of block q
+template <typename T>
+__device__ __forceinline__ int elem(int q, int x, int y) {
+    constexpr int PER = 16 / (int)sizeof(T);
+    return chunk_addr<T>(q, (x * 8 + y) / PER) + (x * 8 + y) % PER;
+}
+__device__ __forceinline__ int bidx(int bi, int bj) { return bi * (bi + 1) / 2 + bj; }
+
+template <int KMAX>
+struct BlockedGeom {
+    static constexpr int NB1 = (KMAX + 8) / 8;  // block rows for rows 0..KMAX (b row included)
+    static constexpr int NBLK = NB1 * (NB1 + 1) / 2;
+    static constexpr int CH = 16;
+    static constexpr int RPL = (KMAX + 1 + 63) / 64;  // panel rows per lane
+};
+
+__device__ __forceinline__ void decode_lower(int q, int& bi, int& bj) {
+    bi = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+    while (bi * (bi + 1) / 2 > q) --bi;
+    while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+    bj = q - bi * (bi + 1) / 2;
+}
+
+// HHp = HH + reg * I in the block-packed layout (zero outside the k x k lower triangle)
+template <typename T, int KMAX>
+__global__ __launch_bounds__(256) void wrmf_pack_hh_kernel(const double* __restrict__ HH, int32_t k,
+                                                           double reg, T* __restrict__ HHp) {
+    using G = BlockedGeom<KMAX>;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < G::NBLK * 64;
+         e += gridDim.x * blockDim.x) {
+        int bi, bj;
+        const int q = e / 64, x = (e % 64) / 8, y = e % 8;
+        decode_lower(q, bi, bj);
+        const int i = bi * 8 + x, j = bj * 8 + y;
+        double v = 0.0;
+        if (i < k && j < k && j <= i) v = HH[i * k + j] + (i == j ? reg : 0.0);
+        HHp[elem<T>(q, x, y)] = (T)v;
+    }
+}
+
+template <typename T, int KMAX>
+__global__ __launch_bounds__(256, 1) void wrmf_solve_blocked_kernel(
+    const int64_t* __restrict__ off, const int32_t* __restrict__ cols, int64_t n_data_rows,
+    int64_t n_rows, float* __restrict__ W, const float* __restrict__ H, const T* __restrict__ HHp,
+    int32_t k, double alpha) {
+    using G = BlockedGeom<KMAX>;
+    constexpr int CH = G::CH, RPL = G::RPL;
+    constexpr int A_BYTES = G::NBLK * 64 * (int)sizeof(T);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* A = reinterpret_cast<T*>(smem);
+    float* hs = reinterpret_cast<float*>(smem + A_BYTES);  // [CH][KMAX]
+    T* wv = reinterpret_cast<T*>(hs + CH * KMAX);          // [KMAX]
+    int32_t* idx = reinterpret_cast<int32_t*>(wv + KMAX);  // [CH]
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int nb = (k + 7) / 8;        // block rows/cols of A proper
+    const int nbr = k / 8 + 1;         // block rows incl. the b row (row k)
+    const int ngram = nb * (nb + 1) / 2;
+    constexpr int V4 = 16 / (int)sizeof(T);  // T per 16-B granule
+    auto E = [](int i, int j) { return elem<T>(bidx(i >> 3, j >> 3), i & 7, j & 7); };
+    for (int64_t row = blockIdx.x; row < n_rows; row += gridDim.x) {
+        const int64_t rb = row < n_data_rows ? off[row] : 0;
+        const int64_t re = row < n_data_rows ? off[row + 1] : 0;
+        __syncthreads();
+        for (int g = t; g < G::NBLK * 64 / V4; g += 256)
+            reinterpret_cast<float4*>(A)[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+        T hsum = (T)0;
+        // ---- 1. Gram
+        for (int64_t base = rb; base < re; base += CH) {
+            const int nr = (int)min((int64_t)CH, re - base);
+            __syncthreads();
+            if (t < nr) idx[t] = cols[base + t];
+            __syncthreads();
+            for (int e = t; e < CH * KMAX; e += 256) {
+                const int c = e / KMAX, f = e % KMAX;
+                hs[e] = (c < nr && f < k) ? H[(int64_t)idx[c] * k + f] : 0.0f;
+            }
+            __syncthreads();
+            for (int q = t; q < ngram; q += 256) {
+                int bi, bj;
+                decode_lower(q, bi, bj);
+                T acc[8][8];
+#pragma unroll
+                for (int x = 0; x < 8; ++x) row_load8(A, q, x, acc[x]);
+                for (int c = 0; c < nr; ++c) {
+                    float xa[8], ya[8];
+                    lds_load8(hs + c * KMAX + bi * 8, xa);
+                    lds_load8(hs + c * KMAX + bj * 8, ya);
+#pragma unroll
+                    for (int x = 0; x < 8; ++x)
+#pragma unroll
+                        for (int y = 0; y < 8; ++y) acc[x][y] += (T)(xa[x] * ya[y]);
+                }
+#pragma unroll
+                for (int x = 0; x < 8; ++x) row_store8(A, q, x, acc[x]);
+            }
+            if (t < k)
+                for (int c = 0; c < nr; ++c) hsum += (T)hs[c * KMAX + t];
+        }
+        __syncthreads();
+        // ---- 2. A = HHp + alpha * S; row k = (1 + alpha) * b
+        for (int e = t; e < G::NBLK * 64; e += 256) A[e] = HHp[e] + (T)alpha * A[e];
+        __syncthreads();
+        if (t < k) A[E(k, t)] = hsum * (T)(1.0 + alpha);
+        __syncthreads();
+        // ---- 3. blocked Cholesky (columns 0..k-1, rows 0..k)
+        for (int p = 0; p < nb; ++p) {
+            const int j0 = p * 8, pw = min(8, k - j0);
+            if (wave == 0) {
+                T pv[RPL][8];
+#pragma unroll
+                for (int m = 0; m < RPL; ++m) {
+                    const int r = j0 + lane + 64 * m;
+                    if (r <= k) row_load8(A, bidx(r >> 3, p), r & 7, pv[m]);
+                    else
+#pragma unroll
+                        for (int c = 0; c < 8; ++c) pv[m][c] = (T)0;
+                }
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    if (c >= pw) break;
+                    const int j = j0 + c;  // pivot row j lives in lane c, slot 0
+                    const T djj = sqrt(bcast(pv[0][c], c));
+                    const T inv = (T)1 / djj;
+#pragma unroll
+                    for (int m = 0; m < RPL; ++m) {
+                        const int r = j0 + lane + 64 * m;
+                        if (r == j) pv[m][c] = djj;
+                        else if (r > j && r <= k) pv[m][c] *= inv;
+                    }
+#pragma unroll
+                    for (int l = c + 1; l < 8; ++l) {
+                        if (l >= pw) break;
+                        const T ljl = bcast(pv[0][c], l);  // L[j0 + l][j]
+#pragma unroll
+                        for (int m = 0; m < RPL; ++m) {
+                            const int r = j0 + lane + 64 * m;
+                            if (r >= j0 + l && r <= k) pv[m][l] -= pv[m][c] * ljl;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < RPL; ++m) {
+                    const int r = j0 + lane + 64 * m;
+                    if (r <= k) row_store8(A, bidx(r >> 3, p), r & 7, pv[m]);
+                }
+            }
+            __syncthreads();
+            // trailing blocks (bi, bj): p < bj <= bi, bi < nbr (rows <= k), bj < nb (cols < k)
+            const int tn = nbr - (p + 1);           // block rows in the trailing part
+            const int tcols = nb - (p + 1);         // block cols in the trailing part
+            const int ntr = tn * (tn + 1) / 2;
+            if (tcols > 0)
+                for (int q = t; q < ntr; q += 256) {
+                    int di, dj;
+                    decode_lower(q, di, dj);
+                    if (dj >= tcols) continue;
+                    const int bi = p + 1 + di, bj = p + 1 + dj;
+                    const int qi = bidx(bi, p), qj = bidx(bj, p), qa = bidx(bi, bj);
+                    T li[8][8], lj[8][8];
+#pragma unroll
+                    for (int x = 0; x < 8; ++x) {
+                        row_load8(A, qi, x, li[x]);
+                        row_load8(A, qj, x, lj[x]);
+                    }
+#pragma unroll
+                    for (int x = 0; x < 8; ++x) {
+                        T a[8];
+                        row_load8(A, qa, x, a);
+#pragma unroll
+                        for (int y = 0; y < 8; ++y) {
+                            T sacc = a[y];
+#pragma unroll
+                            for (int c = 0; c < 8; ++c) sacc -= li[x][c] * lj[y][c];
+                            a[y] = sacc;
+                        }
+                        row_store8(A, qa, x, a);
+                    }
+                }
+            __syncthreads();
+        }
+        // ---- 4. backward substitution L^T w = y
+        if (t < k) wv[t] = A[E(k, t)];
+        __syncthreads();
+        for (int p = nb - 1; p >= 0; --p) {
+            const int j0 = p * 8, pw = min(8, k - j0);
+            if (wave == 0) {
+                T L[8][8], w[8];
+#pragma unroll
+                for (int x = 0; x < 8; ++x) row_load8(A, bidx(p, p), x, L[x]);
+#pragma unroll
+                for (int x = 0; x < 8; ++x) w[x] = x < pw ? wv[j0 + x] : (T)0;
+#pragma unroll
+                for (int j = 7; j >= 0; --j) {
+                    if (j < pw) {
+                        T v = w[j];
+#pragma unroll
+                        for (int i = j + 1; i < 8; ++i)
+                            if (i < pw) v -= L[i][j] * w[i];
+                        w[j] = v / L[j][j];
+                    }
+                }
+                if (lane < pw) {
+                    T out = w[0];
+#pragma unroll
+                    for (int x = 1; x < 8; ++x)
+                        if (lane == x) out = w[x];
+                    wv[j0 + lane] = out;
+                }
+            }
+            __syncthreads();
+            for (int i = t; i < j0; i += 256) {
+                T v = wv[i];
+                const int qb = bidx(p, i >> 3);
+                for (int j = 0; j < pw; ++j) v -= A[elem<T>(qb, j, i & 7)] * wv[j0 + j];
+                wv[i] = v;
+            }
+            __syncthreads();
+        }
+        if (t < k) W[row * k + t] = (float)wv[t];
+    }
+}
+
+template <typename T, int KMAX>
+constexpr size_t blocked_lds_bytes() {
+    return (size_t)BlockedGeom<KMAX>::NBLK * 64 * sizeof(T) +
+           (size_t)BlockedGeom<KMAX>::CH * KMAX * sizeof(float) + (size_t)KMAX * sizeof(T) +
+           (size_t)BlockedGeom<KMAX>::CH * sizeof(int32_t);
+}
+
 __global__ __launch_bounds__(256) void wrmf_predict_kernel(
     const int32_t* __restrict__ users, const int32_t* __restrict__ items, int64_t n,
     int32_t n_users, int32_t n_items, const float* __restrict__ U, const float* __restrict__ V,
@@ -208,22 +533,55 @@ struct mml_wrmf {
     bool has_data = false, has_model = false;
     float last_ms = 0.0f;
     int32_t last_launches = 0;
+    int32_t nparts = 1;
+    int64_t nnz = 0;
+    mml::DeviceArray<uint8_t> hhp;  // HH + reg I, block-packed (k > 64 path)
 };
 
 namespace {
+
+template <typename T, int KMAX>
+void run_blocked(mml_wrmf* h, float* W, int64_t w_rows, const float* H, const int64_t* off,
+                 const int32_t* cols, int64_t n_data_rows) {
+    hipStream_t st = h->ctx->stream;
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wrmf_solve_blocked_kernel<T, KMAX>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)blocked_lds_bytes<T, KMAX>());
+        return true;
+    }();
+    (void)attr;
+    constexpr int nblk = BlockedGeom<KMAX>::NBLK;
+    h->hhp.alloc((size_t)nblk * 64 * sizeof(T));
+    T* hhp = reinterpret_cast<T*>(h->hhp.get());
+    wrmf_pack_hh_kernel<T, KMAX><<<(nblk * 64 + 255) / 256, 256, 0, st>>>(
+        h->HH.get(), h->k, h->p.regularization, hhp);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(w_rows, 256 * 4));
+    wrmf_solve_blocked_kernel<T, KMAX><<<grid, 256, blocked_lds_bytes<T, KMAX>(), st>>>(
+        off, cols, n_data_rows, w_rows, W, H, hhp, h->k, h->p.alpha);
+}
 
 void half_step(mml_wrmf* h, float* W, int64_t w_rows, const float* H, int64_t h_rows,
                const int64_t* off, const int32_t* cols, int64_t n_data_rows, int& launches) {
     hipStream_t st = h->ctx->stream;
     const int k = h->k;
-    const int nparts = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (h_rows + 255) / 256));
-    const int64_t rpb = (h_rows + nparts - 1) / nparts;
-    wrmf_gram_partial_kernel<<<nparts, 256, 0, st>>>(H, h_rows, k, rpb, h->partial.get());
+    const int nt = (k + 63) / 64;
+    const int tiles = nt * (nt + 1) / 2;
+    const int nparts = h->nparts;
+    const int64_t rps = (h_rows + nparts - 1) / nparts;
+    wrmf_gram_partial_kernel<<<dim3(tiles, nparts), 256, 0, st>>>(H, h_rows, k, rps,
+                                                                 h->partial.get());
     wrmf_gram_reduce_kernel<<<(k * k + 255) / 256, 256, 0, st>>>(h->partial.get(), nparts, k,
                                                                   h->HH.get());
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(w_rows, 256 * 16));
-    wrmf_solve_kernel<<<grid, 256, 0, st>>>(off, cols, n_data_rows, w_rows, W, H, h->HH.get(), k,
-                                            h->p.alpha, h->p.regularization);
+    if (k <= kMaxK) {
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(w_rows, 256 * 16));
+        wrmf_solve_kernel<<<grid, 256, 0, st>>>(off, cols, n_data_rows, w_rows, W, H, h->HH.get(),
+                                                k, h->p.alpha, h->p.regularization);
+    } else if (k <= 128) {
+        run_blocked<double, 128>(h, W, w_rows, H, off, cols, n_data_rows);
+    } else {
+        run_blocked<float, 256>(h, W, w_rows, H, off, cols, n_data_rows);
+    }
     MML_HIP(hipGetLastError());
     launches += 3;
 }
@@ -237,8 +595,8 @@ extern "C" mml_status mml_wrmf_create(mml_ctx* ctx, const mml_wrmf_params* param
     return guard([&] {
         MML_REQUIRE(ctx && params && out, "null argument");
         MML_REQUIRE(n_users >= 1 && n_items >= 1, "need >= 1 user and item");
-        MML_REQUIRE(params->num_factors >= 1 && params->num_factors <= kMaxK,
-                    "num_factors must be in [1, 64] on this build");
+        MML_REQUIRE(params->num_factors >= 1 && params->num_factors <= 256,
+                    "num_factors must be in [1, 256]");
         ctx->activate();
         auto* h = new mml_wrmf();
         try {
@@ -250,7 +608,10 @@ extern "C" mml_status mml_wrmf_create(mml_ctx* ctx, const mml_wrmf_params* param
             h->U.alloc((size_t)n_users * h->k);
             h->V.alloc((size_t)n_items * h->k);
             h->HH.alloc((size_t)h->k * h->k);
-            h->partial.alloc((size_t)1024 * h->k * h->k);
+            // Gram partial slices: <= 1024 and <= 32M doubles of workspace
+            h->nparts = (int)std::max<int64_t>(
+                1, std::min<int64_t>(1024, ((int64_t)32 << 20) / ((int64_t)h->k * h->k)));
+            h->partial.alloc((size_t)h->nparts * h->k * h->k);
         } catch (...) {
             delete h;
             throw;
@@ -299,6 +660,62 @@ extern "C" mml_status mml_wrmf_set_data(mml_wrmf* h, const int32_t* users, const
                                    hipMemcpyHostToDevice, st));
         MML_HIP(hipStreamSynchronize(st));
         h->has_data = true;
+    });
+}
+
+extern "C" mml_status mml_wrmf_set_data_device(mml_wrmf* h, const int32_t* users,
+                                               const int32_t* items, int64_t n) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(n >= 0 && (n == 0 || (users && items)), "bad event arrays");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        h->has_data = false;
+        mml::DeviceCsr ucsr, icsr;
+        mml::build_csr_device(users, items, n, h->n_users, h->n_items, st, ucsr);
+        mml::build_csr_device(items, users, n, h->n_items, h->n_users, st, icsr);
+        h->uoff.swap(ucsr.off);
+        h->ucols.swap(ucsr.cols);
+        h->ioff.swap(icsr.off);
+        h->icols.swap(icsr.cols);
+        h->nnz = ucsr.nnz;
+        h->has_data = true;
+    });
+}
+
+namespace {
+__device__ __forceinline__ uint64_t wrmf_mix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__global__ __launch_bounds__(256) void wrmf_init_normal_kernel(float* __restrict__ M, int64_t n,
+                                                               uint64_t seed, double mean,
+                                                               double stddev) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t x = wrmf_mix(seed ^ (uint64_t)e * 0x9E3779B97F4A7C15ull);
+        const double u1 = ((x >> 11) + 1.0) * (1.0 / 9007199254740993.0);
+        const double u2 = (double)(wrmf_mix(x) >> 11) * (1.0 / 9007199254740992.0);
+        M[e] = (float)(mean + stddev * sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+    }
+}
+}  // namespace
+
+extern "C" mml_status mml_wrmf_init_model(mml_wrmf* h, uint64_t seed, double mean,
+                                          double stddev) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        wrmf_init_normal_kernel<<<8192, 256, 0, st>>>(h->U.get(), (int64_t)h->n_users * h->k, seed,
+                                                      mean, stddev);
+        wrmf_init_normal_kernel<<<8192, 256, 0, st>>>(h->V.get(), (int64_t)h->n_items * h->k,
+                                                      seed ^ 0x5DEECE66Dull, mean, stddev);
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipStreamSynchronize(st));
+        h->has_model = true;
     });
 }
 

@@ -1,7 +1,9 @@
 """WRMF on the MI355X vs the CPU oracle (fp64 restatement of WRMF.cs:79-156).
 
 Both sides solve the same SPD systems in double (oracle: LU + explicit inverse like MathNet;
-device: Cholesky); factors are compared after the cast to float: |dW| <= 1e-5 * (1 + |W|).
+device: Cholesky); factors are compared after the cast to float: |dW| <= 1e-5 * (1 + |W|) for
+k <= 128 (fp64 on the device).  For 128 < k <= 256 the device stores A in fp32 (the packed lower
+triangle must fit the 160 KiB LDS): |dW| <= 2e-3 * (1 + |W|), stated and measured below.
 """
 import numpy as np
 import pytest
@@ -58,3 +60,17 @@ def test_wrmf_empty_rows_and_predict():
     p = m.predict(np.array([0, 9], np.int32), np.array([1, 1], np.int32))
     ref = O.row_scalar_product(m.user_factors, 0, m.item_factors, 1)
     assert p[0] == np.float32(ref) and p[1] == np.float32(-3.402823466e+38)
+
+
+@pytest.mark.parametrize("k,tol", [(65, 1e-5), (128, 1e-5), (129, 2e-3), (256, 2e-3)])
+def test_wrmf_large_k_matches_oracle(k, tol):
+    u, i = synth_feedback(70 + k, 160, 120, 40)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    st = O.wrmf_train(u, i, nu, ni, seed=3, k=k, num_iter=1)
+    Random.set_seed(3)
+    m = WRMF(NumFactors=k, NumIter=1)
+    m.feedback = PosOnlyFeedback(u, i)
+    m.train()
+    du, dv = _close(m.user_factors, st["U"]), _close(m.item_factors, st["V"])
+    print(f"WRMF k={k}: max rel diff U {du:.2e} V {dv:.2e}")
+    assert du <= tol and dv <= tol
