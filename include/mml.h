@@ -179,6 +179,15 @@ mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed);
 mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t n,
                            float* out);
 mml_status mml_bpr_last_timing(mml_bpr* h, float* out);
+/* Eval.Items.Evaluate's AUC (Eval/Items.cs:126-209 + Recommender.Recommend n = -1 +
+ * Eval/Measures/AUC.cs:42-68) on the device for the eval users: candidates = the already shuffled
+ * candidate list (Items.Candidates, :62-96), the users' test items as CSR (test_off[n_users + 1],
+ * distinct items per user); the training items of the handle's data are ignored per user.
+ * out_auc[x] = that user's AUC, NaN for users the reference skips (no relevant candidate, or
+ * only relevant ones).  The host averages (float accumulation, Items.cs:177-188). */
+mml_status mml_bpr_auc(mml_bpr* h, const int32_t* candidates, int32_t n_candidates,
+                       const int32_t* users, int32_t n_users, const int64_t* test_off,
+                       const int32_t* test_items, double* out_auc);
 /* Multi-GPU (user shards): RCCL all-reduce of item factors + item biases, scaled by 1/nranks. */
 mml_status mml_bpr_allreduce_items(mml_bpr* h);
 
@@ -212,6 +221,10 @@ mml_status mml_wrmf_iterate(mml_wrmf* h);
 mml_status mml_wrmf_predict(mml_wrmf* h, const int32_t* users, const int32_t* items, int64_t n,
                             float* out);
 mml_status mml_wrmf_last_timing(mml_wrmf* h, float* out);
+/* As mml_bpr_auc for the WRMF (MF.Predict) scorer. */
+mml_status mml_wrmf_auc(mml_wrmf* h, const int32_t* candidates, int32_t n_candidates,
+                        const int32_t* users, int32_t n_users, const int64_t* test_off,
+                        const int32_t* test_items, double* out_auc);
 
 #ifdef __cplusplus
 }

@@ -101,6 +101,8 @@ SIGNATURES = {
     "mml_bpr_iterate": (_st, [_vp, ctypes.c_uint64]),
     "mml_bpr_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
     "mml_bpr_last_timing": (_st, [_vp, _f32p]),
+    "mml_bpr_auc": (_st, [_vp, _i32p, ctypes.c_int32, _i32p, ctypes.c_int32, _i64p, _i32p,
+                          _f64p]),
     "mml_bpr_allreduce_items": (_st, [_vp]),
     "mml_wrmf_create": (_st, [_vp, ctypes.POINTER(WrmfParams), ctypes.c_int32, ctypes.c_int32,
                               ctypes.POINTER(_vp)]),
@@ -113,6 +115,8 @@ SIGNATURES = {
     "mml_wrmf_iterate": (_st, [_vp]),
     "mml_wrmf_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
     "mml_wrmf_last_timing": (_st, [_vp, _f32p]),
+    "mml_wrmf_auc": (_st, [_vp, _i32p, ctypes.c_int32, _i32p, ctypes.c_int32, _i64p, _i32p,
+                           _f64p]),
 }
 
 _lib = None

@@ -522,3 +522,16 @@ extern "C" mml_status mml_bpr_allreduce_items(mml_bpr* h) {
         MML_HIP(hipStreamSynchronize(st));
     });
 }
+
+extern "C" mml_status mml_bpr_auc(mml_bpr* h, const int32_t* candidates, int32_t n_candidates,
+                                  const int32_t* users, int32_t n_users, const int64_t* test_off,
+                                  const int32_t* test_items, double* out_auc) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(h->has_model && h->has_data, "model and training data required");
+        h->ctx->activate();
+        mml::item_auc(h->ctx->stream, h->U.get(), h->ld, h->n_users, h->V.get(), h->ld, h->n_items,
+                      h->bias.get(), h->k, h->off.get(), h->cols.get(), h->n_users, candidates,
+                      n_candidates, users, n_users, test_off, test_items, out_auc);
+    });
+}

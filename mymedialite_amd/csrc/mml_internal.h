@@ -102,6 +102,13 @@ struct DeviceCsr {
 void build_csr_device(const int32_t* rows_device, const int32_t* cols_device, int64_t n,
                       int32_t n_rows, int32_t n_cols, hipStream_t st, DeviceCsr& out);
 
+// Eval.Items AUC for an MF scorer (auc.hip): per-user AUC, NaN for users Items.Evaluate skips.
+void item_auc(hipStream_t st, const float* U, int32_t ldu, int32_t n_users_model, const float* V,
+              int32_t ldv, int32_t n_items_model, const float* bias, int32_t k,
+              const int64_t* tr_off, const int32_t* tr_cols, int32_t n_tr_rows,
+              const int32_t* candidates, int32_t n_cand, const int32_t* users, int32_t n_eval,
+              const int64_t* test_off, const int32_t* test_items, double* out_auc);
+
 }  // namespace mml
 
 struct mml_ctx {

@@ -803,3 +803,16 @@ extern "C" mml_status mml_wrmf_predict(mml_wrmf* h, const int32_t* users, const 
         MML_HIP(hipStreamSynchronize(st));
     });
 }
+
+extern "C" mml_status mml_wrmf_auc(mml_wrmf* h, const int32_t* candidates, int32_t n_candidates,
+                                   const int32_t* users, int32_t n_users, const int64_t* test_off,
+                                   const int32_t* test_items, double* out_auc) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(h->has_model && h->has_data, "model and training data required");
+        h->ctx->activate();
+        mml::item_auc(h->ctx->stream, h->U.get(), h->k, h->n_users, h->V.get(), h->k, h->n_items,
+                      nullptr, h->k, h->uoff.get(), h->ucols.get(), h->n_users, candidates,
+                      n_candidates, users, n_users, test_off, test_items, out_auc);
+    });
+}

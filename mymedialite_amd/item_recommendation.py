@@ -58,6 +58,58 @@ class _MFBase(Recommender):
         for _ in range(int(self.NumIter)):
             self.iterate()
 
+    def _auc_symbol(self):
+        raise NotImplementedError
+
+    def evaluate_auc(self, test: PosOnlyFeedback, test_users=None, candidate_items=None):
+        """Eval.Items.Evaluate (Eval/Items.cs:126-209) restricted to AUC, scored on the GPU.
+
+        test_users: default test.AllUsers (distinct users of ``test``, ascending).
+        candidate_items: default CandidateItems.OVERLAP (items of both test and training,
+        ascending); the order given is the tie-break order of the ranking.  The training
+        items ignored per user are the model's own feedback (RepeatedEvents.No).
+        Returns {"AUC": mean over evaluated users (float accumulation, :177-188),
+        "num_users": ..., "num_items": len(candidates), "per_user": float64 array (NaN =
+        skipped)}."""
+        if self._h is None:
+            raise RuntimeError("model not initialised: call train()/init_model() first")
+        tu, ti = N.i32(test.users), N.i32(test.items)
+        if test_users is None:
+            test_users = np.unique(tu)
+        users = N.i32(test_users)
+        if candidate_items is None:
+            candidate_items = np.intersect1d(np.unique(ti), np.unique(N.i32(self._feedback.items)))
+        cand = N.i32(candidate_items)
+        # distinct test items per evaluated user, packed in test_users order
+        order = np.lexsort((ti, tu))
+        su, si = tu[order], ti[order]
+        keep = np.ones(len(su), bool)
+        keep[1:] = (su[1:] != su[:-1]) | (si[1:] != si[:-1])
+        su, si = su[keep], si[keep]
+        lo = np.searchsorted(su, users, side="left")
+        hi = np.searchsorted(su, users, side="right")
+        cnt = (hi - lo).astype(np.int64)
+        off = np.zeros(len(users) + 1, np.int64)
+        np.cumsum(cnt, out=off[1:])
+        items = np.concatenate([si[a:b] for a, b in zip(lo, hi)]) if len(users) else \
+            np.zeros(0, np.int32)
+        items = N.i32(items)
+        out = np.empty(len(users), np.float64)
+        if len(users) and len(cand):
+            N.check(getattr(N.lib(), self._auc_symbol())(
+                self._h, N.ptr(cand, N._i32p), len(cand), N.ptr(users, N._i32p), len(users),
+                N.ptr(off, N._i64p), N.ptr(items, N._i32p), N.ptr(out, N._f64p)))
+        else:
+            out[:] = np.nan
+        acc = np.float32(0.0)
+        n = 0
+        for a in out:
+            if not np.isnan(a):
+                acc = np.float32(acc + np.float32(a))
+                n += 1
+        return {"AUC": float(np.float32(acc / np.float32(n))) if n else 0.0, "num_users": n,
+                "num_items": int(len(cand)), "per_user": out}
+
     def _release(self):
         raise NotImplementedError
 
@@ -89,6 +141,9 @@ class BPRMF(_MFBase):
         self.UpdateJ = True
         for k, v in kw.items():
             setattr(self, k, v)
+
+    def _auc_symbol(self):
+        return "mml_bpr_auc"
 
     def _sampler(self) -> int:
         if self.WithReplacement:
@@ -196,6 +251,9 @@ class WRMF(_MFBase):
         self.NumIter = 15            # WRMF() :62-65
         for k, v in kw.items():
             setattr(self, k, v)
+
+    def _auc_symbol(self):
+        return "mml_wrmf_auc"
 
     def init_model(self):
         """MF.InitModel (MF.cs:51-58) + the feedback sets on the device."""
