@@ -109,6 +109,22 @@ void item_auc(hipStream_t st, const float* U, int32_t ldu, int32_t n_users_model
               const int32_t* candidates, int32_t n_cand, const int32_t* users, int32_t n_eval,
               const int64_t* test_off, const int32_t* test_items, double* out_auc);
 
+// WRMF row solves on the matrix cores for 128 < k <= 256 (wrmf_tiles.hip): a per-CSR plan of
+// light rows (degree-descending work list) and heavy rows (split Gram segments).
+struct WrmfTilePlan {
+    DeviceArray<int32_t> light, heavy_dev, counter;
+    int32_t n_light = 0;
+    std::vector<int32_t> heavy;
+    std::vector<int64_t> seg_first;  // per heavy row: first segment (+ sentinel)
+    DeviceArray<uint8_t> segs;
+    DeviceArray<float> hht;
+    DeviceArray<double> gram;
+};
+void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p);
+void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, const int64_t* off,
+                     const int32_t* cols, const double* HH, int32_t k, double alpha, double reg,
+                     int& launches);
+
 }  // namespace mml
 
 struct mml_ctx {

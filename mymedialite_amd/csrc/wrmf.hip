@@ -18,6 +18,8 @@
 // 64 < k <= 128: block-packed lower triangle in double; 128 < k <= 256 (C5): the same in float
 // (140 KiB of LDS) -- see wrmf_solve_blocked_kernel.
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "mml_internal.h"
@@ -536,9 +538,19 @@ struct mml_wrmf {
     int32_t nparts = 1;
     int64_t nnz = 0;
     mml::DeviceArray<uint8_t> hhp;  // HH + reg I, block-packed (k > 64 path)
+    mml::WrmfTilePlan uplan, iplan;  // k > 128: matrix-core row solves (wrmf_tiles.hip)
 };
 
 namespace {
+
+// MML_WRMF_SOLVER=blocked keeps the LDS-packed fp32 solver for k > 128 (A/B measurements)
+bool use_blocked_solver() {
+    static const bool v = [] {
+        const char* e = std::getenv("MML_WRMF_SOLVER");
+        return e && std::string(e) == "blocked";
+    }();
+    return v;
+}
 
 template <typename T, int KMAX>
 void run_blocked(mml_wrmf* h, float* W, int64_t w_rows, const float* H, const int64_t* off,
@@ -579,11 +591,22 @@ void half_step(mml_wrmf* h, float* W, int64_t w_rows, const float* H, int64_t h_
                                                 k, h->p.alpha, h->p.regularization);
     } else if (k <= 128) {
         run_blocked<double, 128>(h, W, w_rows, H, off, cols, n_data_rows);
-    } else {
+    } else if (use_blocked_solver()) {
         run_blocked<float, 256>(h, W, w_rows, H, off, cols, n_data_rows);
+    } else {
+        MML_REQUIRE(w_rows == n_data_rows, "tile solver expects one CSR row per factor row");
+        mml::wrmf_tile_solve(st, W == h->U.get() ? h->uplan : h->iplan, W, H, off, cols,
+                             h->HH.get(), k, h->p.alpha, h->p.regularization, launches);
     }
     MML_HIP(hipGetLastError());
     launches += 3;
+}
+
+// k > 128: per-CSR row plans for the matrix-core solver, from the row degrees
+void make_plans(mml_wrmf* h, const std::vector<int64_t>& udeg, const std::vector<int64_t>& ideg) {
+    if (h->k <= 128) return;
+    mml::wrmf_tile_plan(udeg, h->ctx->stream, h->uplan);
+    mml::wrmf_tile_plan(ideg, h->ctx->stream, h->iplan);
 }
 
 }  // namespace
@@ -659,6 +682,10 @@ extern "C" mml_status mml_wrmf_set_data(mml_wrmf* h, const int32_t* users, const
             MML_HIP(hipMemcpyAsync(h->icols.get(), icols.data(), sizeof(int32_t) * icols.size(),
                                    hipMemcpyHostToDevice, st));
         MML_HIP(hipStreamSynchronize(st));
+        std::vector<int64_t> udeg(h->n_users), ideg(h->n_items);
+        for (int32_t r = 0; r < h->n_users; ++r) udeg[r] = uoff[r + 1] - uoff[r];
+        for (int32_t r = 0; r < h->n_items; ++r) ideg[r] = ioff[r + 1] - ioff[r];
+        make_plans(h, udeg, ideg);
         h->has_data = true;
     });
 }
@@ -679,6 +706,8 @@ extern "C" mml_status mml_wrmf_set_data_device(mml_wrmf* h, const int32_t* users
         h->ioff.swap(icsr.off);
         h->icols.swap(icsr.cols);
         h->nnz = ucsr.nnz;
+        make_plans(h, std::vector<int64_t>(ucsr.deg_host.begin(), ucsr.deg_host.end()),
+                   std::vector<int64_t>(icsr.deg_host.begin(), icsr.deg_host.end()));
         h->has_data = true;
     });
 }
