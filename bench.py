@@ -314,20 +314,23 @@ def bench_bpr(args):
 
 
 def bench_wrmf(args):
-    """C5 on one GPU: WRMF k=256, 5M users x 500k items, 500M positives (100 per user, Zipf(0.8)
-    items).  One step = one WRMF.Iterate() (WRMF.cs:68-73).  Flops per iteration as SURVEY 8(d)."""
+    """C5: WRMF k=256, 5M users x 500k items, 500M positives (100 per user, Zipf(0.8) items).
+    One step = one WRMF.Iterate() (WRMF.cs:68-73).  Flops per iteration as SURVEY 8(d).  With N
+    ranks (torch.distributed.run) every rank holds the data, solves its row shards and the shards
+    are all-gathered over RCCL after each half-step (strong scaling: the work is fixed)."""
     world, rank, local = env_rank()
-    if world != 1:
-        raise SystemExit("the C5 bench runs one GPU here (row-shard all-gather: next)")
+    init_host_group(world)
     k = 256 if args.k == 64 else args.k
     n_users, n_items = args.users or 5_000_000, 500_000
     per_user = 100
     n = n_users * per_user if not args.ratings else args.ratings
     ctx = N.Context(local)
+    if world > 1:  # row shards per rank, all-gathered after each half-step (SURVEY 8(e))
+        ctx.comm_init(share_unique_id(rank, N.Context.unique_id), world, rank)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     g = torch.Generator(device=dev)
-    g.manual_seed(5)
+    g.manual_seed(5)  # every rank generates the same full data set
     from mymedialite_amd.synthetic import zipf_cdf
     cdf = torch.from_numpy(zipf_cdf(n_items, 0.8)).to(dev)
     perm = torch.randperm(n_items, generator=g, device=dev)
@@ -352,6 +355,8 @@ def bench_wrmf(args):
     for _ in range(args.warmup):
         N.check(N.lib().mml_wrmf_iterate(h))
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
     ms = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -359,16 +364,19 @@ def bench_wrmf(args):
         N.lib().mml_wrmf_last_timing(h, N.ptr(timing, N._f32p))
         ms.append(float(timing[0]))
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     nnz = n  # distinct after de-duplication is slightly lower; SURVEY counts 500M
     half = lambda rows, other: 2 * nnz * k * k + 2 * other * k * k + rows * (k ** 3 / 3 + 2 * k * k) \
         + 2 * nnz * k
     flops = half(n_users, n_items) + half(n_items, n_users)
     tflops = flops / (np.mean(ms) * 1e-3) / 1e12
     line = {
-        "metric": "WRMF iterations/sec, k=256 (C5, 1 GPU)", "value": args.steps / elapsed,
-        "unit": "iterations/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "metric": "WRMF iterations/sec, k=256 (C5)", "value": args.steps / elapsed,
+        "unit": "iterations/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None, "dtype": "f32 (k > 128: fp32 solve; HH in fp64)",
         "data": "synthetic (100 positives per user, items Zipf(0.8), generated in HBM)",
         "config": {"workload": "C5: WRMF 5M users x 500k items, 500M positives, k=256",
@@ -376,13 +384,15 @@ def bench_wrmf(args):
                    "alpha": 1.0, "regularization": 0.015, "device_ingest_s": ingest_s},
         "roofline": {"bound": "mfma", "achieved": tflops, "peak": 157.3, "unit": "TFLOP/s",
                      "frac": tflops / 157.3, "traffic": None,
-                     "kernel": "wrmf_solve_packed_kernel<float,256> + wrmf_gram_*",
+                     "kernel": "wrmf_tile_solve_kernel + wrmf_tile_gram_kernel + wrmf_gram_*",
                      "kernel_avg_ms": float(np.mean(ms)), "flops_per_iteration": flops},
-        "cpu_baseline": None if args.no_cpu_baseline else cpu_baseline_wrmf(k, args.cpu_seconds,
-                                                                          n_users, n_items,
-                                                                          per_user),
+        "cpu_baseline": None if (args.no_cpu_baseline or world > 1) else cpu_baseline_wrmf(
+            k, args.cpu_seconds, n_users, n_items, per_user),
     }
-    print(json.dumps(line), flush=True)
+    if world > 1:
+        line["config"]["parallelism"] = f"row shards x{world}, RCCL all-gather per half-step"
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     N.lib().mml_wrmf_destroy(h)
     ctx.close()
 

@@ -69,6 +69,12 @@ mml_status mml_partition_users_and_items(mml_random* r, const int32_t* users, co
                                          int32_t num_groups, int64_t* offsets, int32_t* indices,
                                          int32_t* out_groups);
 
+/* Row shards for one process per GPU (WRMF): contiguous ranges [bounds[r],
+ * bounds[r+1]) of n rows with balanced work (row weight = deg + k/2); bounds[parts + 1].
+ * Host-only; every rank derives the same shards from the same degrees. */
+mml_status mml_balanced_rows(const int64_t* deg, int64_t n, int32_t k, int32_t parts,
+                             int64_t* bounds);
+
 /* ------------------------------------------------------------------ BiasedMatrixFactorization */
 enum { MML_LOSS_RMSE = 0, MML_LOSS_MAE = 1, MML_LOSS_LOGISTIC = 2 }; /* OptimizationTarget */
 enum {

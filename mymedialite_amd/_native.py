@@ -76,6 +76,7 @@ SIGNATURES = {
     "mml_random_shuffle_i32": (_st, [_vp, _i32p, ctypes.c_int64]),
     "mml_partition_users_and_items": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, ctypes.c_int32,
                                             ctypes.c_int32, ctypes.c_int32, _i64p, _i32p, _i32p]),
+    "mml_balanced_rows": (_st, [_i64p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _i64p]),
     "mml_bmf_create": (_st, [_vp, ctypes.POINTER(BmfParams), ctypes.c_int32, ctypes.c_int32,
                              ctypes.POINTER(_vp)]),
     "mml_bmf_destroy": (_st, [_vp]),

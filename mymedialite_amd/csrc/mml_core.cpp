@@ -1,6 +1,7 @@
 // mml_core.cpp -- library-level entry points: errors, devices, contexts, RCCL communicators,
 // and the host-side MyMediaLite.Random / Utils.Shuffle / MultiCore equivalents that a non-.NET
 // host needs to drive the path with the reference's RNG semantics.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -225,5 +226,32 @@ extern "C" mml_status mml_partition_users_and_items(mml_random* r, const int32_t
         for (int64_t b = 0; b < nb; ++b) r->shuffle(indices + cnt[b], cnt[b + 1] - cnt[b]);
         std::memcpy(offsets, cnt.data(), sizeof(int64_t) * (nb + 1));
         *out_groups = G;
+    });
+}
+
+namespace mml {
+std::vector<int64_t> balanced_rows(const std::vector<int64_t>& deg, int32_t k, int32_t parts) {
+    const int64_t n = (int64_t)deg.size();
+    std::vector<int64_t> b(parts + 1, n);
+    b[0] = 0;
+    double total = 0.0;
+    for (int64_t r = 0; r < n; ++r) total += (double)deg[r] + 0.5 * k;
+    double acc = 0.0;
+    int part = 1;
+    for (int64_t r = 0; r < n && part < parts; ++r) {
+        acc += (double)deg[r] + 0.5 * k;
+        while (part < parts && acc >= total * part / parts) b[part++] = r + 1;
+    }
+    for (int p = 1; p <= parts; ++p) b[p] = std::max(b[p], b[p - 1]);
+    return b;
+}
+}  // namespace mml
+
+extern "C" mml_status mml_balanced_rows(const int64_t* deg, int64_t n, int32_t k, int32_t parts,
+                                        int64_t* bounds) {
+    return guard([&] {
+        MML_REQUIRE(bounds && parts >= 1 && n >= 0 && (deg || n == 0), "bad argument");
+        const auto b = mml::balanced_rows(std::vector<int64_t>(deg, deg + n), k, parts);
+        std::memcpy(bounds, b.data(), sizeof(int64_t) * (parts + 1));
     });
 }

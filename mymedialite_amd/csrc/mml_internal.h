@@ -109,6 +109,9 @@ void item_auc(hipStream_t st, const float* U, int32_t ldu, int32_t n_users_model
               const int32_t* candidates, int32_t n_cand, const int32_t* users, int32_t n_eval,
               const int64_t* test_off, const int32_t* test_items, double* out_auc);
 
+// contiguous row shards with balanced work (weight deg + k/2), bounds[parts + 1] (mml_core.cpp)
+std::vector<int64_t> balanced_rows(const std::vector<int64_t>& deg, int32_t k, int32_t parts);
+
 // WRMF row solves on the matrix cores for 128 < k <= 256 (wrmf_tiles.hip): a per-CSR plan of
 // light rows (degree-descending work list) and heavy rows (split Gram segments).
 struct WrmfTilePlan {
@@ -120,7 +123,8 @@ struct WrmfTilePlan {
     DeviceArray<float> hht;
     DeviceArray<double> gram;
 };
-void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p);
+void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p, int64_t r0,
+                    int64_t r1);  // rows [r0, r1) of this rank
 void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, const int64_t* off,
                      const int32_t* cols, const double* HH, int32_t k, double alpha, double reg,
                      int& launches);

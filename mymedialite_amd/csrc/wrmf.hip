@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void wrmf_gram_reduce_kernel(const double* __r
 // One workgroup per row of W.
 __global__ __launch_bounds__(256) void wrmf_solve_kernel(
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols, int64_t n_data_rows,
-    int64_t n_rows, float* __restrict__ W, const float* __restrict__ H,
+    int64_t row_begin, int64_t row_end, float* __restrict__ W, const float* __restrict__ H,
     const double* __restrict__ HH, int32_t k, double alpha, double reg) {
     __shared__ double A[kMaxK][kMaxK + 1];
     __shared__ double bv[kMaxK];
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void wrmf_solve_kernel(
     __shared__ int32_t idx[kChunk];
     const int t = threadIdx.x;
     const int kk = k * k;
-    for (int64_t row = blockIdx.x; row < n_rows; row += gridDim.x) {
+    for (int64_t row = row_begin + blockIdx.x; row < row_end; row += gridDim.x) {
         const int64_t b = row < n_data_rows ? off[row] : 0;
         const int64_t e = row < n_data_rows ? off[row + 1] : 0;
         double acc[kMaxK * kMaxK / 256];
@@ -297,7 +297,8 @@ __global__ __launch_bounds__(256) void wrmf_pack_hh_kernel(const double* __restr
 template <typename T, int KMAX>
 __global__ __launch_bounds__(256, 1) void wrmf_solve_blocked_kernel(
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols, int64_t n_data_rows,
-    int64_t n_rows, float* __restrict__ W, const float* __restrict__ H, const T* __restrict__ HHp,
+    int64_t row_begin, int64_t row_end, float* __restrict__ W, const float* __restrict__ H,
+    const T* __restrict__ HHp,
     int32_t k, double alpha) {
     using G = BlockedGeom<KMAX>;
     constexpr int CH = G::CH, RPL = G::RPL;
@@ -313,7 +314,7 @@ __global__ __launch_bounds__(256, 1) void wrmf_solve_blocked_kernel(
     const int ngram = nb * (nb + 1) / 2;
     constexpr int V4 = 16 / (int)sizeof(T);  // T per 16-B granule
     auto E = [](int i, int j) { return elem<T>(bidx(i >> 3, j >> 3), i & 7, j & 7); };
-    for (int64_t row = blockIdx.x; row < n_rows; row += gridDim.x) {
+    for (int64_t row = row_begin + blockIdx.x; row < row_end; row += gridDim.x) {
         const int64_t rb = row < n_data_rows ? off[row] : 0;
         const int64_t re = row < n_data_rows ? off[row + 1] : 0;
         __syncthreads();
@@ -539,6 +540,10 @@ struct mml_wrmf {
     int64_t nnz = 0;
     mml::DeviceArray<uint8_t> hhp;  // HH + reg I, block-packed (k > 64 path)
     mml::WrmfTilePlan uplan, iplan;  // k > 128: matrix-core row solves (wrmf_tiles.hip)
+    // row shards (one process per GPU): rank r solves rows [ub[r], ub[r+1]) of U and
+    // [ib[r], ib[r+1]) of V; the halves are exchanged by an all-gather (grouped broadcasts)
+    std::vector<int64_t> udeg, ideg, ub, ib;
+    int32_t shard_nranks = 0, shard_rank = -1;
 };
 
 namespace {
@@ -553,7 +558,7 @@ bool use_blocked_solver() {
 }
 
 template <typename T, int KMAX>
-void run_blocked(mml_wrmf* h, float* W, int64_t w_rows, const float* H, const int64_t* off,
+void run_blocked(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, const int64_t* off,
                  const int32_t* cols, int64_t n_data_rows) {
     hipStream_t st = h->ctx->stream;
     static const bool attr = [] {
@@ -568,12 +573,13 @@ void run_blocked(mml_wrmf* h, float* W, int64_t w_rows, const float* H, const in
     T* hhp = reinterpret_cast<T*>(h->hhp.get());
     wrmf_pack_hh_kernel<T, KMAX><<<(nblk * 64 + 255) / 256, 256, 0, st>>>(
         h->HH.get(), h->k, h->p.regularization, hhp);
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(w_rows, 256 * 4));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(r1 - r0, 256 * 4));
     wrmf_solve_blocked_kernel<T, KMAX><<<grid, 256, blocked_lds_bytes<T, KMAX>(), st>>>(
-        off, cols, n_data_rows, w_rows, W, H, hhp, h->k, h->p.alpha);
+        off, cols, n_data_rows, r0, r1, W, H, hhp, h->k, h->p.alpha);
 }
 
-void half_step(mml_wrmf* h, float* W, int64_t w_rows, const float* H, int64_t h_rows,
+// W rows [r0, r1) <- H (all h_rows rows); off/cols: the CSR of W's rows
+void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, int64_t h_rows,
                const int64_t* off, const int32_t* cols, int64_t n_data_rows, int& launches) {
     hipStream_t st = h->ctx->stream;
     const int k = h->k;
@@ -585,28 +591,58 @@ void half_step(mml_wrmf* h, float* W, int64_t w_rows, const float* H, int64_t h_
                                                                  h->partial.get());
     wrmf_gram_reduce_kernel<<<(k * k + 255) / 256, 256, 0, st>>>(h->partial.get(), nparts, k,
                                                                   h->HH.get());
+    launches += 2;
+    if (r1 <= r0) return;
     if (k <= kMaxK) {
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(w_rows, 256 * 16));
-        wrmf_solve_kernel<<<grid, 256, 0, st>>>(off, cols, n_data_rows, w_rows, W, H, h->HH.get(),
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(r1 - r0, 256 * 16));
+        wrmf_solve_kernel<<<grid, 256, 0, st>>>(off, cols, n_data_rows, r0, r1, W, H, h->HH.get(),
                                                 k, h->p.alpha, h->p.regularization);
     } else if (k <= 128) {
-        run_blocked<double, 128>(h, W, w_rows, H, off, cols, n_data_rows);
+        run_blocked<double, 128>(h, W, r0, r1, H, off, cols, n_data_rows);
     } else if (use_blocked_solver()) {
-        run_blocked<float, 256>(h, W, w_rows, H, off, cols, n_data_rows);
+        run_blocked<float, 256>(h, W, r0, r1, H, off, cols, n_data_rows);
     } else {
-        MML_REQUIRE(w_rows == n_data_rows, "tile solver expects one CSR row per factor row");
         mml::wrmf_tile_solve(st, W == h->U.get() ? h->uplan : h->iplan, W, H, off, cols,
                              h->HH.get(), k, h->p.alpha, h->p.regularization, launches);
     }
     MML_HIP(hipGetLastError());
-    launches += 3;
+    launches += 1;
 }
 
-// k > 128: per-CSR row plans for the matrix-core solver, from the row degrees
-void make_plans(mml_wrmf* h, const std::vector<int64_t>& udeg, const std::vector<int64_t>& ideg) {
-    if (h->k <= 128) return;
-    mml::wrmf_tile_plan(udeg, h->ctx->stream, h->uplan);
-    mml::wrmf_tile_plan(ideg, h->ctx->stream, h->iplan);
+// all-gather of the row shards of W [rows x k] in place: one broadcast per rank, grouped
+void allgather_rows(mml_wrmf* h, float* W, const std::vector<int64_t>& b) {
+    mml_ctx* c = h->ctx;
+    MML_RCCL(ncclGroupStart());
+    for (int r = 0; r < c->nranks; ++r) {
+        const size_t cnt = (size_t)(b[r + 1] - b[r]) * h->k;
+        if (!cnt) continue;
+        float* p = W + (size_t)b[r] * h->k;
+        MML_RCCL(ncclBroadcast(p, p, cnt, ncclFloat, r, c->comm, c->stream));
+    }
+    MML_RCCL(ncclGroupEnd());
+}
+
+// (re)derive the shards for the context's communicator and the row plans of this rank
+void ensure_shards(mml_wrmf* h) {
+    const int32_t nr = h->ctx->comm ? h->ctx->nranks : 1;
+    const int32_t rk = h->ctx->comm ? h->ctx->rank : 0;
+    if (nr == h->shard_nranks && rk == h->shard_rank) return;
+    h->ub = mml::balanced_rows(h->udeg, h->k, nr);
+    h->ib = mml::balanced_rows(h->ideg, h->k, nr);
+    if (h->k > 128) {
+        mml::wrmf_tile_plan(h->udeg, h->ctx->stream, h->uplan, h->ub[rk], h->ub[rk + 1]);
+        mml::wrmf_tile_plan(h->ideg, h->ctx->stream, h->iplan, h->ib[rk], h->ib[rk + 1]);
+    }
+    h->shard_nranks = nr;
+    h->shard_rank = rk;
+}
+
+// the row degrees of both CSRs (host): shard bounds and the k > 128 row plans derive from them
+void set_degrees(mml_wrmf* h, std::vector<int64_t> udeg, std::vector<int64_t> ideg) {
+    h->udeg = std::move(udeg);
+    h->ideg = std::move(ideg);
+    h->shard_nranks = 0;
+    h->shard_rank = -1;
 }
 
 }  // namespace
@@ -685,7 +721,7 @@ extern "C" mml_status mml_wrmf_set_data(mml_wrmf* h, const int32_t* users, const
         std::vector<int64_t> udeg(h->n_users), ideg(h->n_items);
         for (int32_t r = 0; r < h->n_users; ++r) udeg[r] = uoff[r + 1] - uoff[r];
         for (int32_t r = 0; r < h->n_items; ++r) ideg[r] = ioff[r + 1] - ioff[r];
-        make_plans(h, udeg, ideg);
+        set_degrees(h, std::move(udeg), std::move(ideg));
         h->has_data = true;
     });
 }
@@ -706,8 +742,8 @@ extern "C" mml_status mml_wrmf_set_data_device(mml_wrmf* h, const int32_t* users
         h->ioff.swap(icsr.off);
         h->icols.swap(icsr.cols);
         h->nnz = ucsr.nnz;
-        make_plans(h, std::vector<int64_t>(ucsr.deg_host.begin(), ucsr.deg_host.end()),
-                   std::vector<int64_t>(icsr.deg_host.begin(), icsr.deg_host.end()));
+        set_degrees(h, std::vector<int64_t>(ucsr.deg_host.begin(), ucsr.deg_host.end()),
+                    std::vector<int64_t>(icsr.deg_host.begin(), icsr.deg_host.end()));
         h->has_data = true;
     });
 }
@@ -786,11 +822,16 @@ extern "C" mml_status mml_wrmf_iterate(mml_wrmf* h) {
         hipStream_t st = h->ctx->stream;
         int launches = 0;
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
-        // WRMF.Iterate (:68-73): users from items, then items from the updated users
-        half_step(h, h->U.get(), h->n_users, h->V.get(), h->n_items, h->uoff.get(),
+        ensure_shards(h);
+        const int rk = h->shard_rank;
+        // WRMF.Iterate (:68-73): users from items, then items from the updated users; with
+        // several ranks each solves its row shard and the shards are all-gathered in between
+        half_step(h, h->U.get(), h->ub[rk], h->ub[rk + 1], h->V.get(), h->n_items, h->uoff.get(),
                   h->ucols.get(), h->n_users, launches);
-        half_step(h, h->V.get(), h->n_items, h->U.get(), h->n_users, h->ioff.get(),
+        if (h->shard_nranks > 1) allgather_rows(h, h->U.get(), h->ub);
+        half_step(h, h->V.get(), h->ib[rk], h->ib[rk + 1], h->U.get(), h->n_users, h->ioff.get(),
                   h->icols.get(), h->n_items, launches);
+        if (h->shard_nranks > 1) allgather_rows(h, h->V.get(), h->ib);
         MML_HIP(hipEventRecord(h->ctx->ev_end, st));
         MML_HIP(hipEventSynchronize(h->ctx->ev_end));
         MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));

@@ -81,12 +81,20 @@ struct Smem {
     float wv[kHSW];
     float sv[32];
     float part[kNT][32];
+    float park[kSlots][4][64][4];       // one wave's accumulators during a diagonal factorisation
     int32_t row;
 };
 
 struct Tiles {
     int I[kSlots], J[kSlots];
 };
+
+// Makes the tile ids opaque at the top of a loop body, so the compiler recomputes the (cheap)
+// tile-derived offsets there instead of hoisting dozens of them out of the loop and spilling them.
+__device__ __forceinline__ void launder(Tiles& tl) {
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) asm volatile("" : "+s"(tl.I[s]), "+s"(tl.J[s]));
+}
 
 __device__ __forceinline__ void my_tiles(int wave, int nr, int ntile, Tiles& tl) {
 #pragma unroll
@@ -104,7 +112,7 @@ __device__ __forceinline__ void my_tiles(int wave, int nr, int ntile, Tiles& tl)
 // Staging: thread t gathers vector c = t / 32 of the chunk, floats u = t % 32 (+ 32 j) of it (float4
 // when k % 4 == 0); the next chunk's gathers and the index of the one after are in flight while the
 // current chunk's MFMAs run.
-__device__ __forceinline__ void gram_accumulate(Smem& sm, f32x16 (&acc)[kSlots], const Tiles& tl,
+__device__ __forceinline__ void gram_accumulate(Smem& sm, f32x16 (&acc)[kSlots], Tiles& tl,
                                                 const int32_t* __restrict__ cols, int64_t b,
                                                 int64_t e, const float* __restrict__ H, int k,
                                                 int hsw) {
@@ -152,6 +160,17 @@ __device__ __forceinline__ void gram_accumulate(Smem& sm, f32x16 (&acc)[kSlots],
         for (int f = k + u; f < hsw; f += 32) dst[f] = (live && f == kb) ? 1.0f : 0.0f;
     };
     if (e <= b) return;
+    // per-lane operand offsets of the owned tiles (unused slots read offset 0 with weight 0)
+    int offJ[kSlots], offI[kSlots];
+    float mJ[kSlots];
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+        const bool ok = tl.I[s] >= 0;
+        const int cj = 32 * tl.J[s] + q;
+        offJ[s] = ok ? cj : 0;
+        offI[s] = ok ? 32 * tl.I[s] + q : 0;
+        mJ[s] = (ok && cj < k) ? 1.0f : 0.0f;
+    }
     auto idx_at = [&](int64_t base) -> int32_t {
         return base + c < e ? cols[base + c] : 0;
     };
@@ -174,14 +193,9 @@ __device__ __forceinline__ void gram_accumulate(Smem& sm, f32x16 (&acc)[kSlots],
         for (int cc = 0; cc < nrc; cc += 2) {
             const float* hr = buf + (cc + h) * kHSW;
 #pragma unroll
-            for (int s = 0; s < kSlots; ++s) {
-                if (tl.I[s] < 0) continue;
-                const int cj = 32 * tl.J[s] + q;
-                float a = hr[cj];
-                a = cj < k ? a : 0.0f;
-                const float bb = hr[32 * tl.I[s] + q];
-                acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc[s], 0, 0, 0);
-            }
+            for (int s = 0; s < kSlots; ++s)  // straight line: unused slots multiply by 0
+                acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(hr[offJ[s]] * mJ[s], hr[offI[s]],
+                                                              acc[s], 0, 0, 0);
         }
         if (more) stash(sm.u.hs[cur ^ 1], nb + c < e);
         __syncthreads();
@@ -242,13 +256,11 @@ __global__ __launch_bounds__(256) void wrmf_tile_hh_kernel(const double* __restr
     }
 }
 
-// One wave: T = L^{-1} for the diagonal tile held (in the transposed C/D layout) in `tile`:
+// One wave: T = L^{-1} for the diagonal tile the caller wrote to sm.dg (row-major):
 // L = chol(tile) with row q of the tile in lane q (v_readlane broadcasts of the pivot column), then
 // column q of T in lane q from the rows of L broadcast out of LDS.  Writes tT[c][m] = T[m][c].
-__device__ __forceinline__ void diag_factor(Smem& sm, const f32x16& tile, float (*tT)[kTS]) {
+__device__ __forceinline__ void diag_factor(Smem& sm, float (*tT)[kTS]) {
     const int lane = threadIdx.x & 63, q = lane & 31, h = lane >> 5;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) sm.dg[q][rho(g, h)] = tile[g];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -293,6 +305,34 @@ __device__ __forceinline__ void diag_factor(Smem& sm, const f32x16& tile, float 
         for (int m = 0; m < 32; ++m) tT[q][m] = tc[m];
 }
 
+// The calling wave parks its accumulators in LDS around diag_factor, so the factorisation's
+// registers do not have to coexist with the tiles (which would spill).
+__device__ __forceinline__ void factor_tile(Smem& sm, f32x16 (&acc)[kSlots], int slot,
+                                            float (*tT)[kTS]) {
+    const int lane = threadIdx.x & 63, q = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+        if (s == slot)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) sm.dg[q][rho(g, h)] = acc[s][g];
+#pragma unroll
+        for (int g = 0; g < 16; g += 4)
+            *reinterpret_cast<float4*>(&sm.park[s][g / 4][lane][0]) =
+                make_float4(acc[s][g], acc[s][g + 1], acc[s][g + 2], acc[s][g + 3]);
+    }
+    diag_factor(sm, tT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s)
+#pragma unroll
+        for (int g = 0; g < 16; g += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(&sm.park[s][g / 4][lane][0]);
+            acc[s][g] = v.x; acc[s][g + 1] = v.y; acc[s][g + 2] = v.z; acc[s][g + 3] = v.w;
+        }
+}
+
 __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, int32_t* __restrict__ counter,
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols, float* __restrict__ W,
@@ -312,10 +352,8 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
         __syncthreads();
         const int li = sm.row;
         if (li >= n_list) break;
-        // opaque per row: keeps the compiler from hoisting tile-derived invariants (and the
-        // row-invariant HHt loads) out of the row loop, where they would be spilled
-#pragma unroll
-        for (int s = 0; s < kSlots; ++s) asm volatile("" : "+s"(tl.I[s]), "+s"(tl.J[s]));
+        // (also keeps the row-invariant HHt loads inside the row loop)
+        launder(tl);
         const int32_t row = rows[li];
         const int64_t rb = off[row], re = off[row + 1];
         if (re == rb) {  // no entries: A^{-1} 0 = 0 (WRMF.cs:126-155)
@@ -356,19 +394,10 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
         // ---- 3. blocked Cholesky by 32-column panels, with a one-panel lookahead: the owner of
         //         the next diagonal tile updates and factors it first, while the other waves are
         //         still applying the current panel to the rest of the trailing matrix
-        {
-            f32x16 dt;
-            bool own = false;
-#pragma unroll
-            for (int s = 0; s < kSlots; ++s)
-                if (s * kWaves + wave == 0) {
-                    dt = acc[s];
-                    own = true;
-                }
-            if (own && !(dbg & 1)) diag_factor(sm, dt, sm.tT[0]);
-        }
+        if (wave == 0 && !(dbg & 1)) factor_tile(sm, acc, 0, sm.tT[0]);  // tile (0, 0): slot 0
         __syncthreads();
         for (int J = 0; J < nt; ++J) {
+            launder(tl);
             const int td = tile_id(J, J, nr), tdn = tile_id(J + 1, J + 1, nr);
             float (*tT)[kTS] = sm.tT[J & 1];
             // (c) L_IJ = A'_IJ T_J^T for the tiles below; the panel goes to LDS; the diagonal
@@ -400,22 +429,19 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
             (void)td;
             __syncthreads();
             // (d) trailing update A'_IK -= L_KJ L_IJ^T, K > J; tile (J+1, J+1) first, then factored
-            {
-                f32x16 dt;
-                bool own = false;
+            if (J + 1 < nt && (tdn % kWaves) == wave) {
+                const int own = tdn / kWaves;
 #pragma unroll
                 for (int s = 0; s < kSlots; ++s) {
-                    if (s * kWaves + wave != tdn || J + 1 >= nt) continue;
+                    if (s != own) continue;
                     const float* lr = sm.u.pn[0][q];
                     if (!(dbg & 2))
 #pragma unroll
                         for (int st = 0; st < 16; ++st)
                             acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(
                                 -lr[2 * st + h], lr[2 * st + h], acc[s], 0, 0, 0);
-                    dt = acc[s];
-                    own = true;
                 }
-                if (own && !(dbg & 1)) diag_factor(sm, dt, sm.tT[(J + 1) & 1]);
+                if (!(dbg & 1)) factor_tile(sm, acc, own, sm.tT[(J + 1) & 1]);
             }
 #pragma unroll
             for (int s = 0; s < kSlots; ++s) {
@@ -433,6 +459,7 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
         // ---- 4. backward substitution L^T w = y (padding entries come out 0)
         for (int J = nt - 1; J >= 0; --J) {
             if (dbg & 4) break;
+            launder(tl);
             __syncthreads();
 #pragma unroll
             for (int s = 0; s < kSlots; ++s) {
@@ -493,14 +520,15 @@ constexpr int64_t kGramBatchBytes = (int64_t)1 << 30;
 
 namespace mml {
 
-void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p) {
+void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p, int64_t r0,
+                    int64_t r1) {
     const int32_t n = (int32_t)deg.size();
     // light rows by degree, descending (longest first: the work queue then ends on short rows)
     std::vector<int32_t> light, heavy;
     std::vector<int64_t> begin(n + 1, 0);
     for (int32_t r = 0; r < n; ++r) begin[r + 1] = begin[r] + deg[r];
     std::vector<int64_t> bucket(kHeavy + 2, 0);
-    for (int32_t r = 0; r < n; ++r)
+    for (int32_t r = (int32_t)r0; r < (int32_t)r1; ++r)
         if (deg[r] <= kHeavy) ++bucket[kHeavy - deg[r]];
         else heavy.push_back(r);
     int64_t acc = 0;
@@ -510,7 +538,7 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
         acc += c;
     }
     light.resize(acc);
-    for (int32_t r = 0; r < n; ++r)
+    for (int32_t r = (int32_t)r0; r < (int32_t)r1; ++r)
         if (deg[r] <= kHeavy) light[bucket[kHeavy - deg[r]]++] = r;
     std::sort(heavy.begin(), heavy.end(), [&](int32_t a, int32_t b) { return deg[a] > deg[b]; });
     std::vector<Seg> segs;

@@ -2,7 +2,8 @@
 
 The data path is RCCL inside libmml_hip.so (``mml_bmf_allreduce_items`` /
 ``mml_bpr_allreduce_items``: one in-place all-reduce of item factors + item biases per epoch, then
-1/N scaling).  This module only does what the host must: pick the user shard, share the RCCL
+1/N scaling; WRMF: each rank solves a row shard of every half-step and ``mml_wrmf_iterate``
+all-gathers the shards with grouped broadcasts).  This module only does what the host must: pick the user shard, share the RCCL
 unique id over the already-initialised torch.distributed group (gloo; RANK/WORLD_SIZE/MASTER_* from
 torch.distributed.run), and reduce timings.  Rendezvous is always 127.0.0.1 here.
 """
@@ -38,6 +39,26 @@ def balanced_user_shards(count_by_user: np.ndarray, world: int) -> np.ndarray:
         b[r] = int(np.searchsorted(c, total * r / world, side="left")) + 1
     b[world] = len(count_by_user)
     return np.maximum.accumulate(np.minimum(b, len(count_by_user)))
+
+
+def balanced_rows(deg, k: int, parts: int) -> np.ndarray:
+    """WRMF row shards (mirror of mml_balanced_rows): contiguous ranges with balanced work, a row
+    weighing its entries + k/2 (its Cholesky); bounds[0] = 0 <= ... <= bounds[parts] = n."""
+    deg = np.asarray(deg, np.int64)
+    n = len(deg)
+    b = np.full(parts + 1, n, np.int64)
+    b[0] = 0
+    w = deg.astype(np.float64) + 0.5 * k
+    total = float(w.sum())
+    acc, part = 0.0, 1
+    for r in range(n):
+        if part >= parts:
+            break
+        acc += float(w[r])
+        while part < parts and acc >= total * part / parts:
+            b[part] = r + 1
+            part += 1
+    return np.maximum.accumulate(b)
 
 
 def shard_ratings(users, items, values, bounds: np.ndarray, rank: int):

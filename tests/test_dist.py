@@ -102,3 +102,80 @@ def test_two_rank_user_shards_with_item_averaging(tmp_path):
                        np.float32(4))
     assert rm2 < O.rating_eval(p0, v)[0]
     assert bnd[1] > 0
+
+
+# ------------------------------------------------------------------ WRMF row shards + all-gather
+def test_balanced_rows_library_matches_mirror():
+    """mml_balanced_rows (host-only C-ABI helper, no GPU) == distributed.balanced_rows."""
+    from mymedialite_amd import _native as N
+    from mymedialite_amd.distributed import balanced_rows
+    rs = np.random.default_rng(3)
+    for n, parts, k in [(0, 1, 8), (1, 4, 256), (57, 3, 10), (5000, 8, 256), (400, 2, 64)]:
+        deg = rs.zipf(1.6, n).clip(max=10_000).astype(np.int64) if n else np.zeros(0, np.int64)
+        out = np.zeros(parts + 1, np.int64)
+        N.check(N.lib().mml_balanced_rows(N.ptr(deg, N._i64p), n, k, parts, N.ptr(out, N._i64p)))
+        ref = balanced_rows(deg, k, parts)
+        np.testing.assert_array_equal(out, ref)
+        assert out[0] == 0 and out[-1] == n and np.all(np.diff(out) >= 0)
+        if n > 100:
+            w = deg + 0.5 * k
+            loads = [w[out[r]:out[r + 1]].sum() for r in range(parts)]
+            assert max(loads) <= w.sum() / parts + w.max() + 1e-9
+
+
+def _wrmf_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tests")]
+    import torch
+    import torch.distributed as dist
+
+    import oracle as O
+    from golden_cases import synth_feedback
+    from mymedialite_amd.distributed import balanced_rows, init_host_group
+
+    init_host_group(world)
+    u, i = synth_feedback(9, 300, 140, 25)
+    nu, ni, k = 300, 140, 6
+    r = O.Rng(4)
+    U = r.fill_normal(nu * k, 0, 0.1).reshape(nu, k)
+    V = r.fill_normal(ni * k, 0, 0.1).reshape(ni, k)
+    uoff, ucols = O.insertion_order_rows(u, i, nu)
+    ioff, icols = O.insertion_order_rows(i, u, ni)
+    ub = balanced_rows(np.diff(uoff), k, world)
+    ib = balanced_rows(np.diff(ioff), k, world)
+
+    def half(off, cols, W, H, b):
+        # this rank's rows (HH from the full, replicated H), then the all-gather that
+        # mml_wrmf_iterate does with one RCCL broadcast per rank
+        HH = O.wrmf_square(H)
+        O.lib().ora_wrmf_optimize_rows(O._p(off, O._i64p), O._p(cols, O._i32p), int(b[rank]),
+                                       int(b[rank + 1]), len(off) - 1, O._p(W, O._f32p),
+                                       O._p(O.f32(H), O._f32p), O._p(HH, O._f64p), k, 1.0, 0.015)
+        for src in range(world):
+            t = torch.from_numpy(np.ascontiguousarray(W[b[src]:b[src + 1]]))
+            dist.broadcast(t, src=src)
+            W[b[src]:b[src + 1]] = t.numpy()
+
+    for _ in range(2):
+        half(uoff, ucols, U, V, ub)
+        half(ioff, icols, V, U, ib)
+    np.save(os.path.join(out_dir, f"w{rank}.npy"), np.concatenate([U.ravel(), V.ravel()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_wrmf_row_shards_equal_single_process(tmp_path):
+    """WRMF rows are independent within a half-step: sharding the rows over 2 ranks and
+    all-gathering after each half gives exactly the single-process model."""
+    world = 2
+    mp.spawn(_wrmf_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    a, b = np.load(tmp_path / "w0.npy"), np.load(tmp_path / "w1.npy")
+    np.testing.assert_array_equal(a, b)
+    import oracle as O
+    from golden_cases import synth_feedback
+    u, i = synth_feedback(9, 300, 140, 25)
+    st = O.wrmf_train(u, i, 300, 140, seed=4, k=6, num_iter=2)
+    np.testing.assert_array_equal(a, np.concatenate([st["U"].ravel(), st["V"].ravel()]))

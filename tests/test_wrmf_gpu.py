@@ -74,3 +74,33 @@ def test_wrmf_large_k_matches_oracle(k, tol):
     du, dv = _close(m.user_factors, st["U"]), _close(m.item_factors, st["V"])
     print(f"WRMF k={k}: max rel diff U {du:.2e} V {dv:.2e}")
     assert du <= tol and dv <= tol
+
+
+@pytest.mark.parametrize("k", [32, 200])
+def test_wrmf_with_communicator_matches_single(k):
+    """A one-rank RCCL communicator takes the sharded iterate path (shards from mml_balanced_rows,
+    all-gathers skipped at one rank): the model is identical to the plain run."""
+    import ctypes
+    from mymedialite_amd import _native as N
+    u, i = synth_feedback(90 + k, 400, 150, 30)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    out = []
+    for use_comm in (False, True):
+        ctx = N.Context(0)
+        if use_comm:
+            ctx.comm_init(N.Context.unique_id(), 1, 0)
+        p = N.WrmfParams(k, 0, 1.0, 0.015)
+        h = N._vp()
+        N.check(N.lib().mml_wrmf_create(ctx.handle, ctypes.byref(p), nu, ni, ctypes.byref(h)))
+        N.check(N.lib().mml_wrmf_set_data(h, N.ptr(u, N._i32p), N.ptr(i, N._i32p), len(u)))
+        N.check(N.lib().mml_wrmf_init_model(h, 3, 0.0, 0.1))
+        for _ in range(2):
+            N.check(N.lib().mml_wrmf_iterate(h))
+        U = np.empty((nu, k), np.float32)
+        V = np.empty((ni, k), np.float32)
+        N.check(N.lib().mml_wrmf_get_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p)))
+        N.lib().mml_wrmf_destroy(h)
+        ctx.close()
+        out.append((U, V))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
