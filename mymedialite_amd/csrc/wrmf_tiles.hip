@@ -52,6 +52,14 @@ constexpr int kDG = 36;                                  // diagonal-tile row st
 
 __device__ __forceinline__ int rho(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
 
+// threadIdx.x made opaque at the call site: lane-derived constants (row selectors, LDS offsets)
+// are then recomputed in each phase instead of being hoisted out of the row loop and spilled
+__device__ __forceinline__ int opaque_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 __device__ __forceinline__ float lane_bcast(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
@@ -119,7 +127,7 @@ __device__ __forceinline__ void gram_accumulate(Smem& sm, f32x16 (&acc)[kSlots],
     static_assert(kCH * 32 == kThreads, "one staging thread group of 32 per vector");
     constexpr int kQ = 2;   // float4 per thread (k <= 256)
     constexpr int kS = 8;   // scalars per thread (k <= 256)
-    const int t = threadIdx.x, lane = t & 63, q = lane & 31, h = lane >> 5;
+    const int t = opaque_tid(), lane = t & 63, q = lane & 31, h = lane >> 5;
     const int c = t >> 5, u = t & 31;
     const int kb = hsw - 32;
     const bool vec = (k & 3) == 0;
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(256) void wrmf_tile_hh_kernel(const double* __restr
 // L = chol(tile) with row q of the tile in lane q (v_readlane broadcasts of the pivot column), then
 // column q of T in lane q from the rows of L broadcast out of LDS.  Writes tT[c][m] = T[m][c].
 __device__ __forceinline__ void diag_factor(Smem& sm, float (*tT)[kTS]) {
-    const int lane = threadIdx.x & 63, q = lane & 31, h = lane >> 5;
+    const int lane = opaque_tid() & 63, q = lane & 31, h = lane >> 5;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -309,7 +317,7 @@ __device__ __forceinline__ void diag_factor(Smem& sm, float (*tT)[kTS]) {
 // registers do not have to coexist with the tiles (which would spill).
 __device__ __forceinline__ void factor_tile(Smem& sm, f32x16 (&acc)[kSlots], int slot,
                                             float (*tT)[kTS]) {
-    const int lane = threadIdx.x & 63, q = lane & 31, h = lane >> 5;
+    const int lane = opaque_tid() & 63, q = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {
         if (s == slot)
@@ -339,14 +347,14 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
     const float* __restrict__ H, const float* __restrict__ HHt, const double* __restrict__ gram,
     int32_t k, float alpha, int32_t dbg) {
     __shared__ Smem sm;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, q = lane & 31, h = lane >> 5;
+    const int wave = threadIdx.x >> 6;
     const int nt = (k + 31) >> 5, nr = nt + 1;
-    const int kb = 32 * nt;  // the b row
     const int ntile = nt * nr - nt * (nt - 1) / 2;
     const int hsw = 32 * nr;
     Tiles tl;
     my_tiles(wave, nr, ntile, tl);
     for (;;) {
+        const int t = opaque_tid(), lane = t & 63, q = lane & 31, h = lane >> 5;
         __syncthreads();
         if (t == 0) sm.row = atomicAdd(counter, 1);
         __syncthreads();
