@@ -122,12 +122,16 @@ struct WrmfTilePlan {
     DeviceArray<uint8_t> segs;
     DeviceArray<float> hht;
     DeviceArray<double> gram;
+    // Woodbury rows (1 <= deg <= 128), by 32-column group of their degree
+    DeviceArray<int32_t> wood[4];
+    int32_t n_wood[4] = {0, 0, 0, 0};
+    DeviceArray<float> linv, linvt, qbuf, tbuf;  // L^{-1}, L^{-T} of HH + reg I; Q = H L^{-T}; t rows
 };
 void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p, int64_t r0,
-                    int64_t r1);  // rows [r0, r1) of this rank
-void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, const int64_t* off,
-                     const int32_t* cols, const double* HH, int32_t k, double alpha, double reg,
-                     int& launches);
+                    int64_t r1, bool woodbury);  // rows [r0, r1) of this rank
+void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
+                     const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
+                     double alpha, double reg, int& launches);
 
 }  // namespace mml
 

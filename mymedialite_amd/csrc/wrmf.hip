@@ -557,6 +557,15 @@ bool use_blocked_solver() {
     return v;
 }
 
+// MML_WRMF_WOODBURY=0 solves every row directly (A/B measurements of the Woodbury rows)
+bool no_woodbury() {
+    static const bool v = [] {
+        const char* e = std::getenv("MML_WRMF_WOODBURY");
+        return e && std::string(e) == "0";
+    }();
+    return v;
+}
+
 template <typename T, int KMAX>
 void run_blocked(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, const int64_t* off,
                  const int32_t* cols, int64_t n_data_rows) {
@@ -602,7 +611,7 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
     } else if (use_blocked_solver()) {
         run_blocked<float, 256>(h, W, r0, r1, H, off, cols, n_data_rows);
     } else {
-        mml::wrmf_tile_solve(st, W == h->U.get() ? h->uplan : h->iplan, W, H, off, cols,
+        mml::wrmf_tile_solve(st, W == h->U.get() ? h->uplan : h->iplan, W, H, h_rows, off, cols,
                              h->HH.get(), k, h->p.alpha, h->p.regularization, launches);
     }
     MML_HIP(hipGetLastError());
@@ -630,8 +639,9 @@ void ensure_shards(mml_wrmf* h) {
     h->ub = mml::balanced_rows(h->udeg, h->k, nr);
     h->ib = mml::balanced_rows(h->ideg, h->k, nr);
     if (h->k > 128) {
-        mml::wrmf_tile_plan(h->udeg, h->ctx->stream, h->uplan, h->ub[rk], h->ub[rk + 1]);
-        mml::wrmf_tile_plan(h->ideg, h->ctx->stream, h->iplan, h->ib[rk], h->ib[rk + 1]);
+        const bool wood = h->p.alpha > 0.0 && !no_woodbury();
+        mml::wrmf_tile_plan(h->udeg, h->ctx->stream, h->uplan, h->ub[rk], h->ub[rk + 1], wood);
+        mml::wrmf_tile_plan(h->ideg, h->ctx->stream, h->iplan, h->ib[rk], h->ib[rk + 1], wood);
     }
     h->shard_nranks = nr;
     h->shard_rank = rk;

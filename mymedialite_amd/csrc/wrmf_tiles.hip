@@ -26,6 +26,7 @@
 // Precision: fp32 with fused multiply-adds (the packed fp64 matrix of the parity path does not fit
 // the LDS at k > 128); the tolerance against the fp64 oracle is stated in tests/test_wrmf_gpu.py.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <vector>
 
@@ -120,54 +121,95 @@ __device__ __forceinline__ void my_tiles(int wave, int nr, int ntile, Tiles& tl)
 // Staging: thread t gathers vector c = t / 32 of the chunk, floats u = t % 32 (+ 32 j) of it (float4
 // when k % 4 == 0); the next chunk's gathers and the index of the one after are in flight while the
 // current chunk's MFMAs run.
+// MODE 1 (Woodbury rows): the "vectors" are the k features f and vector f holds Q[s_i][f] for the
+// row's items i < deg (column i), so the same MFMA loop accumulates C = Q_S Q_S^T (deg x deg).
+template <int MODE>
 __device__ __forceinline__ void gram_accumulate(Smem& sm, f32x16 (&acc)[kSlots], Tiles& tl,
-                                                const int32_t* __restrict__ cols, int64_t b,
-                                                int64_t e, const float* __restrict__ H, int k,
-                                                int hsw) {
+                                                int nslot, const int32_t* __restrict__ cols,
+                                                int64_t b, int64_t e, const float* __restrict__ H,
+                                                int k, int hsw, int kdim) {
     static_assert(kCH * 32 == kThreads, "one staging thread group of 32 per vector");
+    static_assert(kCH * 32 == kThreads && kThreads / 4 >= 128, "MODE 1 staging: 4 threads per item");
     constexpr int kQ = 2;   // float4 per thread (k <= 256)
     constexpr int kS = 8;   // scalars per thread (k <= 256)
     const int t = opaque_tid(), lane = t & 63, q = lane & 31, h = lane >> 5;
-    const int c = t >> 5, u = t & 31;
+    const int c = t >> 5, u = t & 31;      // MODE 0: vector c, floats u + 32 j
+    const int wi = t >> 2, wj = t & 3;     // MODE 1: item column wi, features 4 wj .. 4 wj + 3
     const int kb = hsw - 32;
     const bool vec = (k & 3) == 0;
     float4 p4[kQ];
     float p1[kS];
-    auto fetch = [&](int32_t item, bool live) {
-        const float* src = H + (int64_t)item * k;
-        if (vec) {
+    // MODE 1: this thread's item (fixed for the row), its column in the staged vectors
+    const int64_t deg = MODE == 1 ? (e - b) : 0;
+    const int32_t my_item = (MODE == 1 && wi < deg) ? cols[b + wi] : 0;
+    auto fetch = [&](int32_t item, bool live, int64_t base) {
+        if constexpr (MODE == 0) {
+            const float* src = H + (int64_t)item * k;
+            if (vec) {
 #pragma unroll
-            for (int j = 0; j < kQ; ++j) {
-                const int f = 4 * (u + 32 * j);
-                p4[j] = (live && f < k) ? *reinterpret_cast<const float4*>(src + f)
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int j = 0; j < kQ; ++j) {
+                    const int f = 4 * (u + 32 * j);
+                    p4[j] = (live && f < k) ? *reinterpret_cast<const float4*>(src + f)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < kS; ++j) {
+                    const int f = u + 32 * j;
+                    p1[j] = (live && f < k) ? src[f] : 0.0f;
+                }
             }
         } else {
-#pragma unroll
-            for (int j = 0; j < kS; ++j) {
-                const int f = u + 32 * j;
-                p1[j] = (live && f < k) ? src[f] : 0.0f;
+            const float* src = H + (int64_t)my_item * k;
+            const int f = (int)base + 4 * wj;
+            const bool ok = wi < deg;
+            if (vec) {
+                p4[0] = (ok && f < k) ? *reinterpret_cast<const float4*>(src + f)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                p4[0].x = (ok && f < k) ? src[f] : 0.0f;
+                p4[0].y = (ok && f + 1 < k) ? src[f + 1] : 0.0f;
+                p4[0].z = (ok && f + 2 < k) ? src[f + 2] : 0.0f;
+                p4[0].w = (ok && f + 3 < k) ? src[f + 3] : 0.0f;
             }
+            (void)item; (void)live;
         }
     };
     auto stash = [&](float* buf, bool live) {
-        float* dst = buf + c * kHSW;
-        if (vec) {
+        if constexpr (MODE == 0) {
+            float* dst = buf + c * kHSW;
+            if (vec) {
 #pragma unroll
-            for (int j = 0; j < kQ; ++j) {
-                const int f = 4 * (u + 32 * j);
-                if (f < k) *reinterpret_cast<float4*>(dst + f) = p4[j];
+                for (int j = 0; j < kQ; ++j) {
+                    const int f = 4 * (u + 32 * j);
+                    if (f < k) *reinterpret_cast<float4*>(dst + f) = p4[j];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < kS; ++j) {
+                    const int f = u + 32 * j;
+                    if (f < k) dst[f] = p1[j];
+                }
             }
+            for (int f = k + u; f < hsw; f += 32) dst[f] = (live && f == kb) ? 1.0f : 0.0f;
         } else {
-#pragma unroll
-            for (int j = 0; j < kS; ++j) {
-                const int f = u + 32 * j;
-                if (f < k) dst[f] = p1[j];
+            float* dst = buf + 4 * wj * kHSW;
+            dst[wi] = p4[0].x;
+            dst[kHSW + wi] = p4[0].y;
+            dst[2 * kHSW + wi] = p4[0].z;
+            dst[3 * kHSW + wi] = p4[0].w;
+            if (wi + 128 < hsw) {  // columns beyond the 128 staged items (b-row tile): zero
+                dst[wi + 128] = 0.0f;
+                dst[kHSW + wi + 128] = 0.0f;
+                dst[2 * kHSW + wi + 128] = 0.0f;
+                dst[3 * kHSW + wi + 128] = 0.0f;
             }
+            (void)live;
         }
-        for (int f = k + u; f < hsw; f += 32) dst[f] = (live && f == kb) ? 1.0f : 0.0f;
     };
     if (e <= b) return;
+    const int64_t eb = MODE == 0 ? b : 0;      // entries (MODE 0) or features (MODE 1)
+    const int64_t ee = MODE == 0 ? e : k;
     // per-lane operand offsets of the owned tiles (unused slots read offset 0 with weight 0)
     int offJ[kSlots], offI[kSlots];
     float mJ[kSlots];
@@ -177,35 +219,37 @@ __device__ __forceinline__ void gram_accumulate(Smem& sm, f32x16 (&acc)[kSlots],
         const int cj = 32 * tl.J[s] + q;
         offJ[s] = ok ? cj : 0;
         offI[s] = ok ? 32 * tl.I[s] + q : 0;
-        mJ[s] = (ok && cj < k) ? 1.0f : 0.0f;
+        mJ[s] = (ok && cj < kdim) ? 1.0f : 0.0f;
     }
     auto idx_at = [&](int64_t base) -> int32_t {
-        return base + c < e ? cols[base + c] : 0;
+        if constexpr (MODE == 0) return base + c < ee ? cols[base + c] : 0;
+        return 0;
     };
     int cur = 0;
     __syncthreads();  // the LDS union may still be read by the previous row's last phase
-    int32_t i0 = idx_at(b);
-    int32_t i1 = b + kCH < e ? idx_at(b + kCH) : 0;
-    fetch(i0, b + c < e);
-    stash(sm.u.hs[0], b + c < e);
+    int32_t i0 = idx_at(eb);
+    int32_t i1 = eb + kCH < ee ? idx_at(eb + kCH) : 0;
+    fetch(i0, eb + c < ee, eb);
+    stash(sm.u.hs[0], eb + c < ee);
     __syncthreads();
-    for (int64_t base = b; base < e; base += kCH) {
-        const int nrc = (int)min((int64_t)kCH, e - base);
+    for (int64_t base = eb; base < ee; base += kCH) {
+        const int nrc = (int)min((int64_t)kCH, ee - base);
         const int64_t nb = base + kCH;
-        const bool more = nb < e;
+        const bool more = nb < ee;
         if (more) {
-            fetch(i1, nb + c < e);                            // next chunk: in flight
-            i1 = nb + kCH < e ? idx_at(nb + kCH) : 0;         // the index after it
+            fetch(i1, nb + c < ee, nb);                       // next chunk: in flight
+            i1 = nb + kCH < ee ? idx_at(nb + kCH) : 0;        // the index after it
         }
         const float* buf = sm.u.hs[cur];
         for (int cc = 0; cc < nrc; cc += 2) {
             const float* hr = buf + (cc + h) * kHSW;
 #pragma unroll
             for (int s = 0; s < kSlots; ++s)  // straight line: unused slots multiply by 0
-                acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(hr[offJ[s]] * mJ[s], hr[offI[s]],
-                                                              acc[s], 0, 0, 0);
+                if (s < nslot)
+                    acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(hr[offJ[s]] * mJ[s],
+                                                                  hr[offI[s]], acc[s], 0, 0, 0);
         }
-        if (more) stash(sm.u.hs[cur ^ 1], nb + c < e);
+        if (more) stash(sm.u.hs[cur ^ 1], nb + c < ee);
         __syncthreads();
         cur ^= 1;
     }
@@ -234,7 +278,7 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_gram_kernel(
         for (int s = 0; s < kSlots; ++s)
 #pragma unroll
             for (int g = 0; g < 16; ++g) acc[s][g] = 0.0f;
-        gram_accumulate(sm, acc, tl, cols, sg.b, sg.e, H, k, 32 * nr);
+        gram_accumulate<0>(sm, acc, tl, kSlots, cols, sg.b, sg.e, H, k, 32 * nr, k);
 #pragma unroll
         for (int s = 0; s < kSlots; ++s) {
             if (tl.I[s] < 0) continue;
@@ -267,7 +311,7 @@ __global__ __launch_bounds__(256) void wrmf_tile_hh_kernel(const double* __restr
 // One wave: T = L^{-1} for the diagonal tile the caller wrote to sm.dg (row-major):
 // L = chol(tile) with row q of the tile in lane q (v_readlane broadcasts of the pivot column), then
 // column q of T in lane q from the rows of L broadcast out of LDS.  Writes tT[c][m] = T[m][c].
-__device__ __forceinline__ void diag_factor(Smem& sm, float (*tT)[kTS]) {
+__device__ __forceinline__ void diag_factor(float (*dg)[kDG], float (*tT)[kTS]) {
     const int lane = opaque_tid() & 63, q = lane & 31, h = lane >> 5;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -275,7 +319,7 @@ __device__ __forceinline__ void diag_factor(Smem& sm, float (*tT)[kTS]) {
     float x[32];
 #pragma unroll
     for (int c = 0; c < 32; c += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(&sm.dg[q][c]);
+        const float4 v = *reinterpret_cast<const float4*>(&dg[q][c]);
         x[c] = v.x; x[c + 1] = v.y; x[c + 2] = v.z; x[c + 3] = v.w;
     }
 #pragma unroll
@@ -290,7 +334,7 @@ __device__ __forceinline__ void diag_factor(Smem& sm, float (*tT)[kTS]) {
     if (h == 0)
 #pragma unroll
         for (int c = 0; c < 32; c += 4)
-            *reinterpret_cast<float4*>(&sm.dg[q][c]) = make_float4(x[c], x[c + 1], x[c + 2], x[c + 3]);
+            *reinterpret_cast<float4*>(&dg[q][c]) = make_float4(x[c], x[c + 1], x[c + 2], x[c + 3]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -300,13 +344,13 @@ __device__ __forceinline__ void diag_factor(Smem& sm, float (*tT)[kTS]) {
         float sacc = (m == q) ? 1.0f : 0.0f;
 #pragma unroll
         for (int j4 = 0; j4 < m; j4 += 4) {
-            const float4 l = *reinterpret_cast<const float4*>(&sm.dg[m][j4]);
+            const float4 l = *reinterpret_cast<const float4*>(&dg[m][j4]);
             sacc -= l.x * tc[j4];
             if (j4 + 1 < m) sacc -= l.y * tc[j4 + 1];
             if (j4 + 2 < m) sacc -= l.z * tc[j4 + 2];
             if (j4 + 3 < m) sacc -= l.w * tc[j4 + 3];
         }
-        tc[m] = sacc * __builtin_amdgcn_rcpf(sm.dg[m][m]);
+        tc[m] = sacc * __builtin_amdgcn_rcpf(dg[m][m]);
     }
     if (h == 0)
 #pragma unroll
@@ -328,7 +372,7 @@ __device__ __forceinline__ void factor_tile(Smem& sm, f32x16 (&acc)[kSlots], int
             *reinterpret_cast<float4*>(&sm.park[s][g / 4][lane][0]) =
                 make_float4(acc[s][g], acc[s][g + 1], acc[s][g + 2], acc[s][g + 3]);
     }
-    diag_factor(sm, tT);
+    diag_factor(sm.dg, tT);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -341,15 +385,23 @@ __device__ __forceinline__ void factor_tile(Smem& sm, f32x16 (&acc)[kSlots], int
         }
 }
 
+// MODE 0: the direct row solve (W_u = A_u^{-1} b_u), kdim = k.
+// MODE 1: the Woodbury row solve for rows with deg <= kWood (WRMF.cs:110-156 restated):
+//   A_u = B + alpha H_S^T H_S with B = HH + reg I = L L^T shared by all rows, Q = H L^{-T}:
+//   W_u = ((1 + alpha) / alpha) L^{-T} Q_S^T C^{-1} 1,  C = I / alpha + Q_S Q_S^T  (deg x deg).
+//   The kernel solves C v = 1 on the same tile machinery (kdim = 32 * ceil(deg_max / 32)) and
+//   writes t = Q_S^T v to Tout[list index]; W rows = c t L^{-1} follow as one batched GEMM.
+template <int MODE>
 __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, int32_t* __restrict__ counter,
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols, float* __restrict__ W,
     const float* __restrict__ H, const float* __restrict__ HHt, const double* __restrict__ gram,
-    int32_t k, float alpha, int32_t dbg) {
+    int32_t k, int32_t kdim, float alpha, float* __restrict__ Tout, int32_t dbg) {
     __shared__ Smem sm;
     const int wave = threadIdx.x >> 6;
-    const int nt = (k + 31) >> 5, nr = nt + 1;
+    const int nt = (kdim + 31) >> 5, nr = nt + 1;
     const int ntile = nt * nr - nt * (nt - 1) / 2;
+    const int nslot = (ntile + kWaves - 1) / kWaves;
     const int hsw = 32 * nr;
     Tiles tl;
     my_tiles(wave, nr, ntile, tl);
@@ -365,7 +417,10 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
         const int32_t row = rows[li];
         const int64_t rb = off[row], re = off[row + 1];
         if (re == rb) {  // no entries: A^{-1} 0 = 0 (WRMF.cs:126-155)
-            for (int f = t; f < k; f += kThreads) W[(int64_t)row * k + f] = 0.0f;
+            if (MODE == 0)
+                for (int f = t; f < k; f += kThreads) W[(int64_t)row * k + f] = 0.0f;
+            else
+                for (int f = t; f < k; f += kThreads) Tout[(int64_t)li * k + f] = 0.0f;
             continue;
         }
         f32x16 acc[kSlots];
@@ -374,7 +429,7 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
 #pragma unroll
             for (int g = 0; g < 16; ++g) acc[s][g] = 0.0f;
         // ---- 1. Gram (+ b in row kb)
-        if (gram) {
+        if (MODE == 0 && gram) {
 #pragma unroll
             for (int s = 0; s < kSlots; ++s) {
                 if (tl.I[s] < 0) continue;
@@ -383,20 +438,42 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
                 for (int g = 0; g < 16; ++g) acc[s][g] = (float)src[g * 64];
             }
         } else if (!(dbg & 8)) {
-            gram_accumulate(sm, acc, tl, cols, rb, re, H, k, hsw);
+            gram_accumulate<MODE>(sm, acc, tl, nslot, cols, rb, re, H, k, hsw, kdim);
         }
         // ---- 2. A' = HHt + alpha * S above row kb (HHt = HH + reg I, identity on the padding;
         //         S is 0 on the padding), (1 + alpha) * S on the b-row tile
+        if constexpr (MODE == 0) {
 #pragma unroll
-        for (int s = 0; s < kSlots; ++s) {
-            if (tl.I[s] < 0) continue;
-            if (tl.I[s] < nt) {
-                const float* hh = HHt + tile_id(tl.I[s], tl.J[s], nr) * 1024 + lane;
+            for (int s = 0; s < kSlots; ++s) {
+                if (tl.I[s] < 0) continue;
+                if (tl.I[s] < nt) {
+                    const float* hh = HHt + tile_id(tl.I[s], tl.J[s], nr) * 1024 + lane;
 #pragma unroll
-                for (int g = 0; g < 16; ++g) acc[s][g] = hh[g * 64] + alpha * acc[s][g];
-            } else {
+                    for (int g = 0; g < 16; ++g) acc[s][g] = hh[g * 64] + alpha * acc[s][g];
+                } else {
 #pragma unroll
-                for (int g = 0; g < 16; ++g) acc[s][g] *= 1.0f + alpha;
+                    for (int g = 0; g < 16; ++g) acc[s][g] *= 1.0f + alpha;
+                }
+            }
+        } else {
+            // C' = [I / alpha + Q_S Q_S^T (identity on the padding); b row = 1 on the deg columns]
+            const int deg = (int)(re - rb);
+            const float ainv = 1.0f / alpha;
+#pragma unroll
+            for (int s = 0; s < kSlots; ++s) {
+                if (tl.I[s] < 0) continue;
+                const int r = 32 * tl.I[s] + q;
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const int cc = 32 * tl.J[s] + rho(g, h);
+                    float v = acc[s][g];
+                    if (tl.I[s] < nt) {
+                        if (r == cc) v += cc < deg ? ainv : 1.0f;
+                    } else {
+                        v = (q == 0 && cc < deg) ? 1.0f : 0.0f;
+                    }
+                    acc[s][g] = v;
+                }
             }
         }
         // ---- 3. blocked Cholesky by 32-column panels, with a one-panel lookahead: the owner of
@@ -506,7 +583,361 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
             }
         }
         __syncthreads();
-        for (int f = t; f < k; f += kThreads) W[(int64_t)row * k + f] = sm.wv[f];
+        if constexpr (MODE == 0) {
+            for (int f = t; f < k; f += kThreads) W[(int64_t)row * k + f] = sm.wv[f];
+        } else {
+            // t = Q_S^T v (the item ids staged in LDS first)
+            const int deg = (int)(re - rb);
+            int32_t* ids = reinterpret_cast<int32_t*>(sm.u.red);
+            for (int x = t; x < deg; x += kThreads) ids[x] = cols[rb + x];
+            __syncthreads();
+            for (int f = t; f < k; f += kThreads) {
+                float a0 = 0.0f, a1 = 0.0f;
+                int x = 0;
+                for (; x + 1 < deg; x += 2) {
+                    a0 += sm.wv[x] * H[(int64_t)ids[x] * k + f];
+                    a1 += sm.wv[x + 1] * H[(int64_t)ids[x + 1] * k + f];
+                }
+                if (x < deg) a0 += sm.wv[x] * H[(int64_t)ids[x] * k + f];
+                Tout[(int64_t)li * k + f] = a0 + a1;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Woodbury rows, several per workgroup.  A row with deg <= 32 NT entries has only
+// NT (NT + 1) - NT (NT - 1) / 2 tiles (<= 14), so the 8 waves split into R groups of WPG waves and
+// each group solves its own row: the groups run the same phases in lockstep (shared barriers), so
+// their serial diagonal factorisations run side by side on different waves.  Same math as
+// wrmf_tile_solve_kernel<1>; every group owns a private LDS slice.
+template <int NT>
+struct WoodCfg {
+    static constexpr int R = (NT >= 3) ? 2 : 4;             // rows per workgroup (registers)
+    static constexpr int WPG = kWaves / R;                  // waves per row
+    static constexpr int TG = 64 * WPG;                     // threads per row
+    static constexpr int NR = NT + 1;
+    static constexpr int NTILE = NT * NR - NT * (NT - 1) / 2;
+    static constexpr int SLOTS = (NTILE + WPG - 1) / WPG;
+    static constexpr int ITEMS = 32 * NT;                   // item columns (deg <= ITEMS)
+    static constexpr int HSW = 32 * NR;                     // staged width (+ the b-row tile)
+    static constexpr int F4 = (ITEMS * 4 + TG - 1) / TG;    // float4 staged per thread and chunk
+};
+
+template <int NT>
+struct WoodSmem {
+    using C = WoodCfg<NT>;
+    union {
+        float hs[2][kCH][C::HSW];
+        float pn[NT][32][kPS];
+        float red[NT][32][kDS];
+    } u;
+    float dg[32][kDG];
+    float tT[2][32][kTS];
+    float yv[C::HSW];
+    float wv[C::HSW];
+    float sv[32];
+    float part[NT][32];
+    int32_t ids[C::ITEMS];
+};
+
+template <int NT>
+__global__ __launch_bounds__(kThreads, 2) void wrmf_wood_kernel(
+    const int32_t* __restrict__ rows, int32_t n_list, int32_t* __restrict__ counter,
+    const int64_t* __restrict__ off, const int32_t* __restrict__ cols,
+    const float* __restrict__ Q, int32_t k, float alpha, float* __restrict__ Tout) {
+    using C = WoodCfg<NT>;
+    extern __shared__ __attribute__((aligned(16))) char wood_smem[];
+    __shared__ int32_t base_row;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int grp = wave / C::WPG, wig = wave % C::WPG;
+    WoodSmem<NT>& sm = reinterpret_cast<WoodSmem<NT>*>(wood_smem)[grp];
+    int TI[C::SLOTS], TJ[C::SLOTS];
+#pragma unroll
+    for (int s = 0; s < C::SLOTS; ++s) {
+        const int t = s * C::WPG + wig;
+        int I = -1, J = -1;
+        if (t < C::NTILE) tile_of(t, C::NR, I, J);
+        TI[s] = __builtin_amdgcn_readfirstlane(I);
+        TJ[s] = __builtin_amdgcn_readfirstlane(J);
+    }
+    const float ainv = 1.0f / alpha;
+    const bool vec = (k & 3) == 0;
+    for (;;) {
+        const int tid = opaque_tid(), lane = tid & 63, q = lane & 31, h = lane >> 5;
+        const int tg = tid - grp * C::TG;
+        __syncthreads();
+        if (tid == 0) base_row = atomicAdd(counter, C::R);
+        __syncthreads();
+        const int b0 = base_row;
+        if (b0 >= n_list) break;
+        const int li = b0 + grp;
+        const bool live = li < n_list;
+        const int32_t row = live ? rows[li] : 0;
+        const int64_t rb = live ? off[row] : 0;
+        const int deg = live ? (int)(off[row + 1] - rb) : 0;
+        for (int x = tg; x < C::ITEMS; x += C::TG) sm.ids[x] = x < deg ? cols[rb + x] : 0;
+        f32x16 acc[C::SLOTS];
+#pragma unroll
+        for (int s = 0; s < C::SLOTS; ++s)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) acc[s][g] = 0.0f;
+        // ---- C = Q_S Q_S^T: the k features are the vectors, 16 per LDS chunk, double-buffered
+        float4 p4[C::F4];
+        auto fetch = [&](int f0) {
+#pragma unroll
+            for (int j = 0; j < C::F4; ++j) {
+                const int x = tg + j * C::TG;
+                const int wi = x >> 2, f = f0 + 4 * (x & 3);
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (x < C::ITEMS * 4 && wi < deg) {
+                    const float* src = Q + (int64_t)sm.ids[wi] * k + f;
+                    if (vec) {
+                        if (f < k) v = *reinterpret_cast<const float4*>(src);
+                    } else {
+                        v.x = f < k ? src[0] : 0.f;
+                        v.y = f + 1 < k ? src[1] : 0.f;
+                        v.z = f + 2 < k ? src[2] : 0.f;
+                        v.w = f + 3 < k ? src[3] : 0.f;
+                    }
+                }
+                p4[j] = v;
+            }
+        };
+        auto stash = [&](int buf) {
+#pragma unroll
+            for (int j = 0; j < C::F4; ++j) {
+                const int x = tg + j * C::TG;
+                if (x < C::ITEMS * 4) {
+                    const int wi = x >> 2, r4 = 4 * (x & 3);
+                    sm.u.hs[buf][r4][wi] = p4[j].x;
+                    sm.u.hs[buf][r4 + 1][wi] = p4[j].y;
+                    sm.u.hs[buf][r4 + 2][wi] = p4[j].z;
+                    sm.u.hs[buf][r4 + 3][wi] = p4[j].w;
+                }
+            }
+        };
+        __syncthreads();  // ids visible; the LDS union is free
+        for (int x = tg; x < 2 * kCH * 32; x += C::TG)  // the b-row tile's columns stay 0
+            sm.u.hs[x / (kCH * 32)][(x / 32) % kCH][C::ITEMS + (x & 31)] = 0.0f;
+        fetch(0);
+        stash(0);
+        __syncthreads();
+        int cur = 0;
+        for (int f0 = 0; f0 < k; f0 += kCH) {
+            const bool more = f0 + kCH < k;
+            if (more) fetch(f0 + kCH);
+#pragma unroll
+            for (int cc = 0; cc < kCH; cc += 2) {
+                const float* hr = sm.u.hs[cur][cc + h];
+#pragma unroll
+                for (int s = 0; s < C::SLOTS; ++s) {
+                    const bool ok = TI[s] >= 0;
+                    const float a = ok ? hr[32 * TJ[s] + q] : 0.0f;
+                    const float bb = ok ? hr[32 * TI[s] + q] : 0.0f;
+                    acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc[s], 0, 0, 0);
+                }
+            }
+            if (more) stash(cur ^ 1);
+            __syncthreads();
+            cur ^= 1;
+        }
+        // ---- C' = [I / alpha + C (identity on the padding); b row = 1 on the deg columns]
+#pragma unroll
+        for (int s = 0; s < C::SLOTS; ++s) {
+            if (TI[s] < 0) continue;
+            const int r = 32 * TI[s] + q;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int cc = 32 * TJ[s] + rho(g, h);
+                float v = acc[s][g];
+                if (TI[s] < NT) {
+                    if (r == cc) v += cc < deg ? ainv : 1.0f;
+                } else {
+                    v = (q == 0 && cc < deg) ? 1.0f : 0.0f;
+                }
+                acc[s][g] = v;
+            }
+        }
+        // ---- blocked Cholesky with a one-panel lookahead (as wrmf_tile_solve_kernel)
+        auto factor_owned = [&](int tile, float (*tT)[kTS]) {
+#pragma unroll
+            for (int s = 0; s < C::SLOTS; ++s)
+                if (s * C::WPG + wig == tile)
+#pragma unroll
+                    for (int g = 0; g < 16; ++g) sm.dg[q][rho(g, h)] = acc[s][g];
+            diag_factor(sm.dg, tT);
+        };
+        if (wig == 0) factor_owned(0, sm.tT[0]);
+        __syncthreads();
+#pragma unroll
+        for (int J = 0; J < NT; ++J) {
+            const int tdn = tile_id(J + 1, J + 1, C::NR);
+            float (*tT)[kTS] = sm.tT[J & 1];
+#pragma unroll
+            for (int s = 0; s < C::SLOTS; ++s) {
+                if (TJ[s] != J) continue;
+                if (TI[s] == J) {
+#pragma unroll
+                    for (int g = 0; g < 16; ++g) acc[s][g] = tT[2 * g + h][q];
+                    continue;
+                }
+                f32x16 nv;
+#pragma unroll
+                for (int g = 0; g < 16; ++g) nv[g] = 0.0f;
+#pragma unroll
+                for (int st = 0; st < 16; ++st)
+                    nv = __builtin_amdgcn_mfma_f32_32x32x2f32(tT[rho(st, h)][q], acc[s][st], nv, 0,
+                                                              0, 0);
+                acc[s] = nv;
+                const int pi = TI[s] - J - 1;
+#pragma unroll
+                for (int g = 0; g < 16; ++g) sm.u.pn[pi][q][rho(g, h)] = nv[g];
+                if (TI[s] == NT && q == 0)
+#pragma unroll
+                    for (int g = 0; g < 16; ++g) sm.yv[32 * J + rho(g, h)] = nv[g];
+            }
+            __syncthreads();
+            if (J + 1 < NT) {
+                const bool own_next = (tdn % C::WPG) == wig;
+#pragma unroll
+                for (int s = 0; s < C::SLOTS; ++s) {
+                    if (TI[s] < 0 || TJ[s] <= J) continue;
+                    const bool next = s * C::WPG + wig == tdn;
+                    if (own_next != next && next) continue;
+                    const float* lk = sm.u.pn[TJ[s] - J - 1][q];
+                    const float* lr = sm.u.pn[TI[s] - J - 1][q];
+#pragma unroll
+                    for (int st = 0; st < 16; ++st)
+                        acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(-lk[2 * st + h],
+                                                                      lr[2 * st + h], acc[s], 0, 0,
+                                                                      0);
+                    if (next) factor_owned(tdn, sm.tT[(J + 1) & 1]);
+                }
+            }
+            __syncthreads();
+        }
+        // ---- backward substitution L^T v = y
+#pragma unroll
+        for (int J = NT - 1; J >= 0; --J) {
+#pragma unroll
+            for (int s = 0; s < C::SLOTS; ++s) {
+                if (TJ[s] != J) continue;
+                if (TI[s] == J) {
+#pragma unroll
+                    for (int g = 0; g < 16; ++g) sm.tT[0][2 * g + h][q] = acc[s][g];
+                } else if (TI[s] < NT) {
+                    const float wr = sm.wv[32 * TI[s] + q];
+                    const int pi = TI[s] - J - 1;
+#pragma unroll
+                    for (int g = 0; g < 16; ++g) sm.u.red[pi][rho(g, h)][q] = acc[s][g] * wr;
+                }
+            }
+            __syncthreads();
+            const int nparts = NT - 1 - J;
+            if (tg < 32 * nparts) {
+                const int pi = tg >> 5, c = tg & 31;
+                float sacc = 0.0f;
+#pragma unroll
+                for (int x = 0; x < 32; ++x) sacc += sm.u.red[pi][c][x];
+                sm.part[pi][c] = sacc;
+            }
+            __syncthreads();
+            if (tg < 32) {
+                float sacc = sm.yv[32 * J + tg];
+                for (int pi = 0; pi < nparts; ++pi) sacc -= sm.part[pi][tg];
+                sm.sv[tg] = sacc;
+            }
+            __syncthreads();
+            if (tg < 32) {
+                float w = 0.0f;
+#pragma unroll
+                for (int c = 0; c < 32; ++c) w += (c >= tg) ? sm.tT[0][tg][c] * sm.sv[c] : 0.0f;
+                sm.wv[32 * J + tg] = w;
+            }
+            __syncthreads();
+        }
+        // ---- t = Q_S^T v
+        if (live)
+            for (int f = tg; f < k; f += C::TG) {
+                float a0 = 0.0f, a1 = 0.0f;
+                int x = 0;
+                for (; x + 1 < deg; x += 2) {
+                    a0 += sm.wv[x] * Q[(int64_t)sm.ids[x] * k + f];
+                    a1 += sm.wv[x + 1] * Q[(int64_t)sm.ids[x + 1] * k + f];
+                }
+                if (x < deg) a0 += sm.wv[x] * Q[(int64_t)sm.ids[x] * k + f];
+                Tout[(int64_t)li * k + f] = a0 + a1;
+            }
+    }
+}
+
+template <int NT>
+void launch_wood(hipStream_t st, const int32_t* rows, int32_t n, int32_t* counter,
+                 const int64_t* off, const int32_t* cols, const float* Q, int32_t k, float alpha,
+                 float* Tout) {
+    using C = WoodCfg<NT>;
+    const size_t lds = sizeof(WoodSmem<NT>) * C::R;
+    static const bool attr = [lds] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wrmf_wood_kernel<NT>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        return true;
+    }();
+    (void)attr;
+    MML_HIP(hipMemsetAsync(counter, 0, sizeof(int32_t), st));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + C::R - 1) / C::R, 512));
+    wrmf_wood_kernel<NT><<<grid, kThreads, lds, st>>>(rows, n, counter, off, cols, Q, k, alpha,
+                                                      Tout);
+}
+
+// Y[yrow(r)] = scale * X[xrow(r)] * M for n rows (X, Y row-major [.. x k], M [k x k] row-major,
+// k <= 256; xrows / yrows null = identity).  32 rows per workgroup staged in LDS, 4 waves x 2
+// output tiles of 32 x 32 on v_mfma_f32_32x32x2_f32; M streams from L2.
+constexpr int kGS = 257;  // LDS row stride of the staged rows
+__global__ __launch_bounds__(256) void wrmf_rows_matmul_kernel(
+    const float* __restrict__ X, const int32_t* __restrict__ xrows, int64_t n,
+    const float* __restrict__ M, int32_t k, float scale, float* __restrict__ Y,
+    const int32_t* __restrict__ yrows) {
+    __shared__ float xs[32 * kGS];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, q = lane & 31, h = lane >> 5;
+    const int nct = (k + 31) >> 5;
+    for (int64_t blk = blockIdx.x; blk * 32 < n; blk += gridDim.x) {
+        const int64_t r0 = blk * 32;
+        __syncthreads();
+        for (int x = t; x < 32 * k; x += 256) {
+            const int i = x / k, f = x - i * k;
+            float v = 0.0f;
+            if (r0 + i < n) {
+                const int64_t src = xrows ? xrows[r0 + i] : r0 + i;
+                v = X[src * k + f];
+            }
+            xs[i * kGS + f] = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+            const int J = wave * 2 + jt;
+            if (J >= nct) continue;
+            f32x16 d;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) d[g] = 0.0f;
+            const int col = 32 * J + q;
+            for (int f0 = 0; f0 < k; f0 += 2) {
+                const int f = f0 + h;
+                const float a = f < k ? xs[q * kGS + f] : 0.0f;
+                const float bv = (f < k && col < k) ? M[(int64_t)f * k + col] : 0.0f;
+                d = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, d, 0, 0, 0);
+            }
+            if (col < k)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const int i = rho(g, h);
+                    if (r0 + i < n) {
+                        const int64_t dst = yrows ? yrows[r0 + i] : r0 + i;
+                        Y[dst * k + col] = scale * d[g];
+                    }
+                }
+        }
     }
 }
 
@@ -521,6 +952,7 @@ int debug_mask() {
 }
 
 constexpr int kHeavy = 8192;   // rows with more entries take the split Gram
+constexpr int kWood = 128;     // rows with at most this many entries take the Woodbury solve
 constexpr int kSeg = 8192;     // entries per split-Gram segment
 constexpr int64_t kGramBatchBytes = (int64_t)1 << 30;
 
@@ -529,15 +961,18 @@ constexpr int64_t kGramBatchBytes = (int64_t)1 << 30;
 namespace mml {
 
 void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p, int64_t r0,
-                    int64_t r1) {
+                    int64_t r1, bool woodbury) {
     const int32_t n = (int32_t)deg.size();
     // light rows by degree, descending (longest first: the work queue then ends on short rows)
     std::vector<int32_t> light, heavy;
     std::vector<int64_t> begin(n + 1, 0);
     for (int32_t r = 0; r < n; ++r) begin[r + 1] = begin[r] + deg[r];
     std::vector<int64_t> bucket(kHeavy + 2, 0);
+    std::vector<int32_t> wood[4];
+    auto is_wood = [&](int32_t r) { return woodbury && deg[r] >= 1 && deg[r] <= kWood; };
     for (int32_t r = (int32_t)r0; r < (int32_t)r1; ++r)
-        if (deg[r] <= kHeavy) ++bucket[kHeavy - deg[r]];
+        if (is_wood(r)) wood[(deg[r] - 1) / 32].push_back(r);
+        else if (deg[r] <= kHeavy) ++bucket[kHeavy - deg[r]];
         else heavy.push_back(r);
     int64_t acc = 0;
     for (auto& b : bucket) {
@@ -547,7 +982,14 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
     }
     light.resize(acc);
     for (int32_t r = (int32_t)r0; r < (int32_t)r1; ++r)
-        if (deg[r] <= kHeavy) light[bucket[kHeavy - deg[r]]++] = r;
+        if (!is_wood(r) && deg[r] <= kHeavy) light[bucket[kHeavy - deg[r]]++] = r;
+    for (int g = 0; g < 4; ++g) {
+        p.n_wood[g] = (int32_t)wood[g].size();
+        p.wood[g].alloc(std::max<size_t>(1, wood[g].size()));
+        if (!wood[g].empty())
+            MML_HIP(hipMemcpyAsync(p.wood[g].get(), wood[g].data(),
+                                   sizeof(int32_t) * wood[g].size(), hipMemcpyHostToDevice, st));
+    }
     std::sort(heavy.begin(), heavy.end(), [&](int32_t a, int32_t b) { return deg[a] > deg[b]; });
     std::vector<Seg> segs;
     p.seg_first.assign(heavy.size() + 1, 0);
@@ -576,9 +1018,34 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
     MML_HIP(hipStreamSynchronize(st));
 }
 
-void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, const int64_t* off,
-                     const int32_t* cols, const double* HH, int32_t k, double alpha, double reg,
-                     int& launches) {
+// L^{-1} (lower) of B = HH + reg I by Cholesky in fp64 on the host (k <= 256: ~10 M flops)
+static void chol_inverse(const std::vector<double>& HH, int k, double reg, std::vector<double>& Li) {
+    std::vector<double> L(HH);
+    for (int i = 0; i < k; ++i) L[(size_t)i * k + i] += reg;
+    for (int j = 0; j < k; ++j) {
+        double d = L[(size_t)j * k + j];
+        for (int m = 0; m < j; ++m) d -= L[(size_t)j * k + m] * L[(size_t)j * k + m];
+        MML_REQUIRE(d > 0.0, "HH + reg I is not positive definite");
+        d = std::sqrt(d);
+        L[(size_t)j * k + j] = d;
+        for (int i = j + 1; i < k; ++i) {
+            double v = L[(size_t)i * k + j];
+            for (int m = 0; m < j; ++m) v -= L[(size_t)i * k + m] * L[(size_t)j * k + m];
+            L[(size_t)i * k + j] = v / d;
+        }
+    }
+    Li.assign((size_t)k * k, 0.0);
+    for (int c = 0; c < k; ++c)  // column c of L^{-1}: forward substitution on e_c
+        for (int i = c; i < k; ++i) {
+            double v = (i == c) ? 1.0 : 0.0;
+            for (int m = c; m < i; ++m) v -= L[(size_t)i * k + m] * Li[(size_t)m * k + c];
+            Li[(size_t)i * k + c] = v / L[(size_t)i * k + i];
+        }
+}
+
+void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
+                     const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
+                     double alpha, double reg, int& launches) {
     MML_REQUIRE(k > 128 && k <= 256, "tile solver covers 128 < k <= 256");
     const int nt = (k + 31) >> 5, nr = nt + 1;
     const int ntile = nt * nr - nt * (nt - 1) / 2;
@@ -601,20 +1068,71 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                                                   p.gram.get());
         MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
         const int gs = (int)std::min<int64_t>(h1 - h0, grid_cap);
-        wrmf_tile_solve_kernel<<<gs, kThreads, 0, st>>>(p.heavy_dev.get() + h0, (int32_t)(h1 - h0),
-                                                   p.counter.get(), off, cols, W, H, p.hht.get(),
-                                                   p.gram.get(), k, (float)alpha, debug_mask());
+        wrmf_tile_solve_kernel<0><<<gs, kThreads, 0, st>>>(
+            p.heavy_dev.get() + h0, (int32_t)(h1 - h0), p.counter.get(), off, cols, W, H,
+            p.hht.get(), p.gram.get(), k, k, (float)alpha, nullptr, debug_mask());
         MML_HIP(hipGetLastError());
         launches += 2;
     }
     if (p.n_light > 0) {
         MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
         const int gs = (int)std::min<int64_t>(p.n_light, grid_cap);
-        wrmf_tile_solve_kernel<<<gs, kThreads, 0, st>>>(p.light.get(), p.n_light, p.counter.get(), off,
-                                                   cols, W, H, p.hht.get(), nullptr, k,
-                                                   (float)alpha, debug_mask());
+        wrmf_tile_solve_kernel<0><<<gs, kThreads, 0, st>>>(
+            p.light.get(), p.n_light, p.counter.get(), off, cols, W, H, p.hht.get(), nullptr, k, k,
+            (float)alpha, nullptr, debug_mask());
         MML_HIP(hipGetLastError());
         ++launches;
+    }
+    int64_t nw = 0, nw_max = 0;
+    for (int g = 0; g < 4; ++g) {
+        nw += p.n_wood[g];
+        nw_max = std::max<int64_t>(nw_max, p.n_wood[g]);
+    }
+    if (nw == 0) return;
+    // Woodbury rows: B = HH + reg I = L L^T (host fp64), Q = H L^{-T}, per-row C v = 1 and
+    // t = Q_S^T v on the tiles, then W rows = ((1 + alpha) / alpha) t L^{-1}
+    std::vector<double> hh((size_t)k * k), li;
+    MML_HIP(hipMemcpyAsync(hh.data(), HH, sizeof(double) * hh.size(), hipMemcpyDeviceToHost, st));
+    MML_HIP(hipStreamSynchronize(st));
+    chol_inverse(hh, k, reg, li);
+    std::vector<float> lf((size_t)k * k), ltf((size_t)k * k);
+    for (int i = 0; i < k; ++i)
+        for (int j = 0; j < k; ++j) {
+            lf[(size_t)i * k + j] = (float)li[(size_t)i * k + j];
+            ltf[(size_t)j * k + i] = (float)li[(size_t)i * k + j];
+        }
+    p.linv.alloc(lf.size());
+    p.linvt.alloc(ltf.size());
+    MML_HIP(hipMemcpyAsync(p.linv.get(), lf.data(), sizeof(float) * lf.size(),
+                           hipMemcpyHostToDevice, st));
+    MML_HIP(hipMemcpyAsync(p.linvt.get(), ltf.data(), sizeof(float) * ltf.size(),
+                           hipMemcpyHostToDevice, st));
+    p.qbuf.alloc((size_t)h_rows * k);
+    const int gq = (int)std::min<int64_t>((h_rows + 31) / 32, 8192);
+    wrmf_rows_matmul_kernel<<<gq, 256, 0, st>>>(H, nullptr, h_rows, p.linvt.get(), k, 1.0f,
+                                                p.qbuf.get(), nullptr);
+    p.tbuf.alloc((size_t)nw_max * k);
+    const float cw = (float)((1.0 + alpha) / alpha);
+    launches += 1;
+    for (int g = 0; g < 4; ++g) {
+        if (!p.n_wood[g]) continue;
+        if (debug_mask() & 16) {  // the one-row-per-workgroup MODE 1 kernel (A/B)
+            MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
+            const int gs = (int)std::min<int64_t>(p.n_wood[g], grid_cap);
+            wrmf_tile_solve_kernel<1><<<gs, kThreads, 0, st>>>(
+                p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, W, p.qbuf.get(),
+                nullptr, nullptr, k, 32 * (g + 1), (float)alpha, p.tbuf.get(), debug_mask());
+        } else {
+            auto* L = g == 0 ? &launch_wood<1> : g == 1 ? &launch_wood<2>
+                      : g == 2 ? &launch_wood<3> : &launch_wood<4>;
+            L(st, p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, p.qbuf.get(), k,
+              (float)alpha, p.tbuf.get());
+        }
+        const int gw = (int)std::min<int64_t>((p.n_wood[g] + 31) / 32, 8192);
+        wrmf_rows_matmul_kernel<<<gw, 256, 0, st>>>(p.tbuf.get(), nullptr, p.n_wood[g],
+                                                    p.linv.get(), k, cw, W, p.wood[g].get());
+        MML_HIP(hipGetLastError());
+        launches += 2;
     }
 }
 

@@ -104,3 +104,30 @@ def test_wrmf_with_communicator_matches_single(k):
         out.append((U, V))
     np.testing.assert_array_equal(out[0][0], out[1][0])
     np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("k,alpha", [(160, 1.0), (256, 4.0), (200, 0.0)])
+def test_wrmf_woodbury_and_direct_rows_match_oracle(k, alpha):
+    """128 < k: rows with 1..128 entries take the Woodbury solve (all four 32-column groups),
+    longer rows the direct tile solve; alpha = 0 sends every row to the direct solve.  Enough
+    users (280 > k) that HH + reg I is well conditioned: with fewer rows than factors the fp32 vs
+    fp64 gap grows with cond(HH + reg I) ~ |H|^2 / reg, for any fp32 solver (measured per row on
+    one half-step: Woodbury <= 9e-7, direct <= 6e-6, scripts/diag_wrmf_rows.py)."""
+    rs = np.random.default_rng(k)
+    degs = [1, 5, 31, 32, 33, 64, 65, 96, 97, 127, 128, 129, 200, 300]
+    n_items = 420
+    us, its = [], []
+    for u, d in enumerate(degs * 20):
+        us += [u] * d
+        its += rs.choice(n_items, size=d, replace=False).tolist()
+    u = np.array(us, np.int32)
+    i = np.array(its, np.int32)
+    nu, ni = int(u.max()) + 1, n_items
+    st = O.wrmf_train(u, i, nu, ni, seed=9, k=k, num_iter=2, alpha=alpha)
+    Random.set_seed(9)
+    m = WRMF(NumFactors=k, NumIter=2, Alpha=alpha)
+    m.feedback = PosOnlyFeedback(u, i)
+    m.train()
+    du, dv = _close(m.user_factors, st["U"]), _close(m.item_factors, st["V"])
+    print(f"WRMF k={k} alpha={alpha}: max rel diff U {du:.2e} V {dv:.2e}")
+    assert du <= 2e-3 and dv <= 2e-3
