@@ -133,6 +133,11 @@ mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const int32_t* ite
 /* Device time of the last mml_bmf_iterate's SGD kernels (HIP events on the library stream):
  * out[0] = ms for the whole epoch, out[1] = number of kernel launches in it. */
 mml_status mml_bmf_last_timing(mml_bmf* h, float* out);
+/* BiasedMatrixFactorization.ComputeObjective (:496-552) on the device model and training data:
+ * out[0] = ComputeLoss() (RMSE / MAE / logistic sum per params.loss, double), out[1] = the
+ * complexity term; ComputeObjective = (float)(out[0] + out[1]).  BoldDriver's UpdateLearnRate
+ * (:225-244) compares consecutive values on the host. */
+mml_status mml_bmf_objective(mml_bmf* h, double* out);
 /* Multi-GPU (user shards): in-place RCCL all-reduce of item factors and item
  * biases over the context's communicator, then scale by 1/nranks (model averaging). */
 mml_status mml_bmf_allreduce_items(mml_bmf* h);

@@ -90,6 +90,7 @@ SIGNATURES = {
     "mml_bmf_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
     "mml_bmf_evaluate": (_st, [_vp, _i32p, _i32p, _f32p, ctypes.c_int64, _f32p]),
     "mml_bmf_last_timing": (_st, [_vp, _f32p]),
+    "mml_bmf_objective": (_st, [_vp, _f64p]),
     "mml_bmf_allreduce_items": (_st, [_vp]),
     "mml_bpr_create": (_st, [_vp, ctypes.POINTER(BprParams), ctypes.c_int32, ctypes.c_int32,
                              ctypes.POINTER(_vp)]),

@@ -309,6 +309,84 @@ __global__ __launch_bounds__(256) void bmf_eval_kernel(
     }
 }
 
+// ComputeLoss (:496-514): RMSE.ComputeSquaredErrorSum / MAE.ComputeAbsoluteErrorSum /
+// LogisticLoss.ComputeSum over the training ratings, double sums, per-block partials.
+__global__ __launch_bounds__(256) void bmf_loss_kernel(
+    const int32_t* __restrict__ users, const int32_t* __restrict__ items,
+    const float* __restrict__ values, int64_t n, int32_t n_users, int32_t n_items,
+    const float* __restrict__ U, const float* __restrict__ V, const float* __restrict__ bu,
+    const float* __restrict__ bi, int32_t k, int32_t ld, float gb, float min_rating, float range,
+    int32_t loss_kind, double* __restrict__ partials) {
+    double acc = 0.0;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const float p = bmf_predict1(users[x], items[x], n_users, n_items, U, V, bu, bi, k, ld,
+                                     gb, min_rating, range);
+        if (loss_kind == MML_LOSS_RMSE) {
+            const double d = (double)(p - values[x]);  // float difference, Math.Pow in double
+            acc += d * d;
+        } else if (loss_kind == MML_LOSS_MAE) {
+            acc += fabs((double)(p - values[x]));
+        } else {
+            double pr = ((double)p - (double)min_rating) / (double)range;
+            pr = pr < 0.0 ? 0.0 : (pr > 1.0 ? 1.0 : pr);
+            const double act = (double)((values[x] - min_rating) / range);  // float arithmetic
+            acc -= act * log(pr);
+            acc -= (1 - act) * log(1 - pr);
+        }
+    }
+    __shared__ double sh[256];
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partials[blockIdx.x] = sh[0];
+}
+
+// ComputeObjective's complexity term (:518-550) over the user rows then the item rows:
+// Math.Pow(EuclideanNorm(row), 2) in double; weights count * reg (float, C# int * float) or
+// reg / sqrt(count) with FrequencyRegularization.  One wavefront per row, per-block partials.
+__global__ __launch_bounds__(256) void bmf_complexity_kernel(
+    const float* __restrict__ U, const float* __restrict__ V, const float* __restrict__ bu,
+    const float* __restrict__ bi, const int32_t* __restrict__ cnt_u,
+    const int32_t* __restrict__ cnt_i, int32_t n_users, int32_t n_items, int32_t k, int32_t ld,
+    float reg_u, float reg_i, float bias_reg, int32_t freq, double* __restrict__ partials) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double acc = 0.0;
+    const int64_t rows = (int64_t)n_users + n_items;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < rows; r += (int64_t)gridDim.x * 4) {
+        const bool user = r < n_users;
+        const int64_t row = user ? r : r - n_users;
+        const float* M = (user ? U : V) + row * ld;
+        double sq = 0.0;
+        for (int f = lane; f < k; f += 64) sq += (double)M[f] * (double)M[f];
+        for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+        if (lane == 0) {
+            const double norm2 = pow(sqrt(sq), 2.0);
+            const int32_t c = user ? cnt_u[row] : cnt_i[row];
+            const float reg = user ? reg_u : reg_i;
+            const double b = (double)(user ? bu[row] : bi[row]);
+            if (freq) {
+                if (c > 0) {
+                    const double w = (double)reg / sqrt((double)c);
+                    acc += w * norm2;
+                    acc += w * (double)bias_reg * (b * b);
+                }
+            } else {
+                const float w = (float)c * reg, wb = (float)c * reg * bias_reg;
+                acc += (double)w * norm2;
+                acc += (double)wb * (b * b);
+            }
+        }
+    }
+    __shared__ double sh[4];
+    if (lane == 0) sh[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
 // stream[x] = raw[order[x]] for the three SoA columns
 __global__ __launch_bounds__(256) void gather_stream_kernel(
     const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const float* __restrict__ rr,
@@ -843,6 +921,37 @@ extern "C" mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const i
         }
         out[0] = (float)std::sqrt(se / (double)n);
         out[1] = (float)(ae / (double)n);
+    });
+}
+
+extern "C" mml_status mml_bmf_objective(mml_bmf* h, double* out) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->has_model && h->has_data && out, "model, data and out required");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        const int g1 = grid_for(h->n, 256, 1024);
+        const int g2 = grid_for((int64_t)h->n_users + h->n_items, 4, 1024);
+        h->ev_partials.alloc(g1 + g2);
+        bmf_loss_kernel<<<g1, 256, 0, st>>>(h->su.get(), h->si.get(), h->sr.get(), h->n,
+                                            h->n_users, h->n_items, h->U.get(), h->V.get(),
+                                            h->bu.get(), h->bi.get(), h->k, h->ld, h->gb,
+                                            h->min_rating, h->max_rating - h->min_rating,
+                                            h->p.loss, h->ev_partials.get());
+        bmf_complexity_kernel<<<g2, 256, 0, st>>>(
+            h->U.get(), h->V.get(), h->bu.get(), h->bi.get(), h->cnt_u.get(), h->cnt_i.get(),
+            h->n_users, h->n_items, h->k, h->ld, h->p.reg_u, h->p.reg_i, h->p.bias_reg,
+            h->p.frequency_regularization, h->ev_partials.get() + g1);
+        MML_HIP(hipGetLastError());
+        std::vector<double> part(g1 + g2);
+        MML_HIP(hipMemcpyAsync(part.data(), h->ev_partials.get(), sizeof(double) * part.size(),
+                               hipMemcpyDeviceToHost, st));
+        MML_HIP(hipStreamSynchronize(st));
+        double loss = 0.0, cx = 0.0;
+        for (int b = 0; b < g1; ++b) loss += part[b];
+        for (int b = 0; b < g2; ++b) cx += part[g1 + b];
+        out[0] = loss;
+        out[1] = cx;
     });
 }
 

@@ -14,6 +14,7 @@ Schedule (GPU-only property):
 from __future__ import annotations
 
 import math
+import sys
 
 import numpy as np
 
@@ -114,8 +115,6 @@ class BiasedMatrixFactorization(Recommender):
 
     def init_model(self):
         """InitModel (MatrixFactorization.cs:99-116 + BiasedMatrixFactorization.cs:161-170)."""
-        if self.BoldDriver:
-            raise NotImplementedError("BoldDriver is not supported on the GPU path yet")
         r = self._ratings
         k = int(self.NumFactors)
         nu, ni = self.MaxUserID + 1, self.MaxItemID + 1
@@ -135,14 +134,30 @@ class BiasedMatrixFactorization(Recommender):
         self._h = h
         self._order_uploaded = False
         self._host = dict(U=U, V=V, bu=bu, bi=bi)
+        self._last_loss = -math.inf
+        if self.BoldDriver:
+            # InitModel (:168-169) runs before Train sets global_bias and rating_range_size: the
+            # reference's first objective sees global_bias = 0 and a zero range (predictions =
+            # min_rating), reproduced by uploading max_rating = min_rating for this one call
+            self._upload_model(0.0, range_zero=True)
+            N.check(N.lib().mml_bmf_set_data(self._h, N.ptr(r.users, N._i32p),
+                                             N.ptr(r.items, N._i32p), N.ptr(r.values, N._f32p),
+                                             r.count, None))  # no RNG draw: order is irrelevant
+            self._last_loss = self.compute_objective()
         self._upload_model(0.0)
 
-    def _upload_model(self, global_bias):
+    def _upload_model(self, global_bias, range_zero=False):
         m = self._host
         N.check(N.lib().mml_bmf_set_model(
             self._h, N.ptr(N.f32(m["U"]), N._f32p), N.ptr(N.f32(m["V"]), N._f32p),
             N.ptr(m["bu"], N._f32p), N.ptr(m["bi"], N._f32p), float(global_bias),
-            float(self.min_rating), float(self.max_rating)))
+            float(self.min_rating), float(self.min_rating if range_zero else self.max_rating)))
+
+    def compute_objective(self) -> float:
+        """ComputeObjective (:518-552): (float)(ComputeLoss() + complexity), on the GPU."""
+        out = np.zeros(2, np.float64)
+        N.check(N.lib().mml_bmf_objective(self._h, N.ptr(out, N._f64p)))
+        return float(np.float32(out[0] + out[1]))
 
     def train(self):
         """Train() (:173-194)."""
@@ -215,6 +230,18 @@ class BiasedMatrixFactorization(Recommender):
         self._update_learn_rate()
 
     def _update_learn_rate(self):
+        """UpdateLearnRate (:225-244): bold driver (objective up: x 0.5, down: x 1.05) or decay."""
+        if self.BoldDriver:
+            loss = self.compute_objective()
+            lr = np.float32(self.current_learnrate)
+            if loss > self._last_loss:
+                lr = np.float32(lr * np.float32(0.5))
+            elif loss < self._last_loss:
+                lr = np.float32(lr * np.float32(1.05))
+            self._last_loss = loss
+            self.current_learnrate = float(lr)
+            print(f"objective {loss:.9g} learn_rate {float(lr):.9g} ", file=sys.stderr)
+            return
         self.current_learnrate = float(np.float32(np.float32(self.current_learnrate) *
                                                   np.float32(self.Decay)))
 

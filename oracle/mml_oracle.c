@@ -239,6 +239,62 @@ void ora_rating_eval(const float* predictions, const float* values, int64_t n, f
     out[1] = (float)(mae / (double)n);
 }
 
+/* BiasedMatrixFactorization.ComputeLoss + ComputeObjective (:496-552), RMSE.ComputeSquaredErrorSum
+ * (Eval/Measures/RMSE.cs:32-38), MAE.ComputeAbsoluteErrorSum (MAE.cs:32-38), LogisticLoss.ComputeSum
+ * (LogisticLoss.cs:34-55).  out[0] = loss, out[1] = complexity (both double, unrounded). */
+void ora_bmf_objective(const int32_t* users, const int32_t* items, const float* values, int64_t n,
+                       int32_t n_users, int32_t n_items, int k, const float* U, const float* V,
+                       const float* bu, const float* bi, float global_bias, float min_rating,
+                       float range, int loss_kind, float reg_u, float reg_i, float bias_reg,
+                       int frequency_regularization, const int32_t* cnt_u, const int32_t* cnt_i,
+                       double* out) {
+    double loss = 0.0;
+    for (int64_t x = 0; x < n; x++) {
+        float p = ora_bmf_predict1(users[x], items[x], n_users, n_items, k, U, V, bu, bi,
+                                   global_bias, min_rating, range);
+        if (loss_kind == 0) {
+            double d = (double)(p - values[x]);
+            loss += pow(d, 2.0);
+        } else if (loss_kind == 1) {
+            loss += fabs((double)(p - values[x]));
+        } else {
+            double prediction = ((double)p - (double)min_rating) / (double)range;
+            if (prediction < 0.0) prediction = 0.0;
+            if (prediction > 1.0) prediction = 1.0;
+            double actual = (double)((values[x] - min_rating) / range);
+            loss -= actual * log(prediction);
+            loss -= (1 - actual) * log(1 - prediction);
+        }
+    }
+    double complexity = 0.0;
+    for (int side = 0; side < 2; side++) {
+        int32_t rows = side == 0 ? n_users : n_items;
+        const float* M = side == 0 ? U : V;
+        const float* b = side == 0 ? bu : bi;
+        const int32_t* cnt = side == 0 ? cnt_u : cnt_i;
+        float reg = side == 0 ? reg_u : reg_i;
+        for (int32_t r = 0; r < rows; r++) {
+            double sq = 0.0;
+            for (int f = 0; f < k; f++) sq += pow((double)M[(int64_t)r * k + f], 2.0);
+            double norm2 = pow(sqrt(sq), 2.0);  /* Math.Pow(EuclideanNorm(row), 2) */
+            if (frequency_regularization) {
+                if (cnt[r] > 0) {
+                    double w = (double)reg / sqrt((double)cnt[r]);
+                    complexity += w * norm2;
+                    complexity += w * (double)bias_reg * pow((double)b[r], 2.0);
+                }
+            } else {
+                float w = (float)cnt[r] * reg;           /* int * float -> float in C# */
+                float wb = (float)cnt[r] * reg * bias_reg;
+                complexity += (double)w * norm2;
+                complexity += (double)wb * pow((double)b[r], 2.0);
+            }
+        }
+    }
+    out[0] = loss;
+    out[1] = complexity;
+}
+
 /* MultiCore.PartitionUsersAndItems (MultiCore.cs:43-73).  Produces blocks as a CSR over
  * block id b = ug * G + ig: offsets[G*G+1], indices[n].  Returns G (clipped). */
 int32_t ora_partition_users_and_items(ora_rng* r, const int32_t* users, const int32_t* items,

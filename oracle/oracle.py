@@ -67,6 +67,11 @@ def lib():
                                       ctypes.c_int, _f32p, _f32p, _f32p, _f32p, ctypes.c_float,
                                       ctypes.c_float, ctypes.c_float, _f32p]
         L.ora_rating_eval.argtypes = [_f32p, _f32p, ctypes.c_int64, _f32p]
+        L.ora_bmf_objective.argtypes = [
+            _i32p, _i32p, _f32p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
+            _f32p, _f32p, _f32p, _f32p, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+            ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_int, _i32p,
+            _i32p, _f64p]
         L.ora_partition_users_and_items.argtypes = [
             ctypes.c_void_p, _i32p, _i32p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
             ctypes.c_int32, _i64p, _i32p]
@@ -217,7 +222,7 @@ def bmf_train(users, items, values, n_users, n_items, min_rating, max_rating, *,
               learn_rate=0.01, decay=1.0, reg_u=0.015, reg_i=0.015, bias_reg=0.01,
               bias_learn_rate=1.0, num_iter=30, init_mean=0.0, init_stddev=0.1, loss=0,
               frequency_regularization=False, max_threads=1, naive_parallelization=False,
-              rng=None, callback=None):
+              bold_driver=False, rng=None, callback=None):
     """BiasedMatrixFactorization.Train() (:173-194) and NumIter x Iterate() (:197-222).
 
     Returns a dict with the model and the RNG-derived schedule (so a GPU run can be fed the
@@ -236,6 +241,30 @@ def bmf_train(users, items, values, n_users, n_items, min_rating, max_rating, *,
     bi = np.zeros(n_items, np.float32)
     lr = np.float32(learn_rate)
     state = dict(U=U, V=V, bu=bu, bi=bi, init_U=U.copy(), init_V=V.copy())
+    objectives = []
+    obj_kw = dict(k=k, loss=loss, reg_u=reg_u, reg_i=reg_i, bias_reg=bias_reg,
+                  frequency_regularization=frequency_regularization)
+    last_loss = -math.inf
+    if bold_driver:  # InitModel (:168-169): before Train sets global_bias / rating_range_size
+        last_loss = float(np.float32(sum(bmf_objective(users, items, values, U, V, bu, bi,
+                                                       np.float32(0), np.float32(min_rating),
+                                                       np.float32(0), **obj_kw))))
+        objectives.append(last_loss)
+
+    def update_learn_rate(lr):
+        """UpdateLearnRate (:225-244)."""
+        nonlocal last_loss
+        if not bold_driver:
+            return np.float32(lr * np.float32(decay))
+        o = float(np.float32(sum(bmf_objective(users, items, values, U, V, bu, bi, gb,
+                                               np.float32(min_rating), range_, **obj_kw))))
+        if o > last_loss:
+            lr = np.float32(lr * np.float32(0.5))
+        elif o < last_loss:
+            lr = np.float32(lr * np.float32(1.05))
+        last_loss = o
+        objectives.append(o)
+        return lr
 
     blocks = None
     lists = None
@@ -273,18 +302,34 @@ def bmf_train(users, items, values, n_users, n_items, min_rating, max_rating, *,
                         b = j * G + (i + j) % G
                         bmf_iterate(users, items, values, idx[off[b]:off[b + 1]], U, V, bu, bi,
                                     lr=lr, **common)
-            lr = np.float32(lr * np.float32(decay))  # UpdateLearnRate() at :216
+            lr = update_learn_rate(lr)  # UpdateLearnRate() at :216
         else:
             if random_index is None:
                 random_index = rng.shuffle(np.arange(len(users), dtype=np.int32))
             bmf_iterate(users, items, values, random_index, U, V, bu, bi, lr=lr, **common)
-        lr = np.float32(lr * np.float32(decay))  # UpdateLearnRate() at :221
+        lr = update_learn_rate(lr)  # UpdateLearnRate() at :221
         if callback is not None:
             callback(epoch, state)
     state.update(global_bias=gb, min_rating=np.float32(min_rating), range_=range_,
                  random_index=random_index, blocks=blocks, subepochs=subepochs, lrs=lrs,
-                 current_learnrate=lr, rng=rng)
+                 current_learnrate=lr, rng=rng, objectives=objectives)
     return state
+
+
+def bmf_objective(users, items, values, U, V, bu, bi, gb, min_rating, range_, *, k, loss=0,
+                  reg_u=0.015, reg_i=0.015, bias_reg=0.01, frequency_regularization=False):
+    """ComputeLoss + the complexity term of ComputeObjective (:496-552) -> (loss, complexity)."""
+    users, items, values = i32(users), i32(items), f32(values)
+    cnt_u = np.bincount(users, minlength=U.shape[0]).astype(np.int32)
+    cnt_i = np.bincount(items, minlength=V.shape[0]).astype(np.int32)
+    out = np.zeros(2, np.float64)
+    lib().ora_bmf_objective(_p(users, _i32p), _p(items, _i32p), _p(values, _f32p), len(users),
+                            U.shape[0], V.shape[0], k, _p(f32(U), _f32p), _p(f32(V), _f32p),
+                            _p(f32(bu), _f32p), _p(f32(bi), _f32p), float(gb), float(min_rating),
+                            float(range_), int(loss), float(reg_u), float(reg_i), float(bias_reg),
+                            int(bool(frequency_regularization)), _p(cnt_u, _i32p),
+                            _p(cnt_i, _i32p), _p(out, _f64p))
+    return float(out[0]), float(out[1])
 
 
 def bmf_predict(users, items, U, V, bu, bi, gb, min_rating, range_):

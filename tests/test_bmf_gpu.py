@@ -226,3 +226,47 @@ def test_dsgd_many_groups_exact():
     assert _maxdiff(m.user_factors, st["U"]) <= 1e-5
     assert _maxdiff(m.item_factors, st["V"]) <= 1e-5
     assert _maxdiff(m.item_bias, st["bi"]) <= 1e-5
+
+
+@pytest.mark.parametrize("loss,freq", [("RMSE", False), ("MAE", True), ("LogisticLoss", False)])
+def test_objective_matches_oracle(loss, freq):
+    """ComputeObjective (:496-552) on the device: the loss sum (double sums over bit-identical
+    predictions, another order) and the complexity term within 1e-9 relative of the oracle."""
+    u, i, v = synth_ratings(21, 300, 120, 6000)
+    r = Ratings(u, i, v)
+    m, _ = gpu_train(u, i, v, seed=3, k=12, num_iter=2, Loss=loss,
+                     FrequencyRegularization=freq)
+    import numpy as _np
+    from mymedialite_amd import _native as N
+    out = _np.zeros(2, _np.float64)
+    N.check(N.lib().mml_bmf_objective(m._h, N.ptr(out, N._f64p)))
+    md = m.get_model()
+    ref = O.bmf_objective(u, i, v, md["U"], md["V"], md["bu"], md["bi"], m.global_bias,
+                          r.scale_min, _np.float32(r.scale_max - r.scale_min), k=12,
+                          loss={"RMSE": 0, "MAE": 1, "LogisticLoss": 2}[loss],
+                          frequency_regularization=freq)
+    print(f"objective {loss}: gpu {out} oracle {ref}")
+    assert abs(out[0] - ref[0]) <= 1e-9 * abs(ref[0])
+    assert abs(out[1] - ref[1]) <= 1e-9 * abs(ref[1])
+
+
+def test_bold_driver_matches_oracle():
+    """BoldDriver (UpdateLearnRate :225-244, InitModel :168-169): the ordered schedule is
+    bit-faithful, so every objective (float) and every learn-rate decision matches the oracle."""
+    u, i, v = synth_ratings(23, 200, 80, 4000)
+    r = Ratings(u, i, v)
+    st = O.bmf_train(u, i, v, 200, 80, r.scale_min, r.scale_max, seed=5, k=8, num_iter=6,
+                     bold_driver=True, learn_rate=0.05)
+    Random.set_seed(5)
+    m = BiasedMatrixFactorization(NumFactors=8, NumIter=0, BoldDriver=True, LearnRate=0.05)
+    m.ratings = r
+    m.train()  # InitModel (with its objective) + global bias, no epochs yet
+    objs, lrs = [m._last_loss], [m.current_learnrate]
+    for _ in range(6):
+        m.iterate()
+        objs.append(m._last_loss)
+        lrs.append(m.current_learnrate)
+    print("objectives gpu", objs, "oracle", st["objectives"])
+    np.testing.assert_allclose(objs, st["objectives"], rtol=1e-6)
+    assert [float(np.float32(x)) for x in lrs[:-1]] == [float(np.float32(x)) for x in st["lrs"]]
+    assert np.float32(lrs[-1]) == np.float32(st["current_learnrate"])
