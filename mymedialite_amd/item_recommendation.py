@@ -61,6 +61,43 @@ class _MFBase(Recommender):
     def _auc_symbol(self):
         raise NotImplementedError
 
+    # SaveModel / LoadModel (MF.cs:160-195, BPRMF.cs:434-479): IO/Model.cs text format
+    TYPE_NAME = ""
+
+    def save_model(self, path: str):
+        from .model_io import ModelWriter
+        m = self.get_model()
+        with ModelWriter(path, self.TYPE_NAME) as w:
+            w.write_matrix(m["U"])
+            if "bias" in m:
+                w.write_vector(m["bias"])
+            w.write_matrix(m["V"])
+
+    def load_model(self, path: str):
+        import sys
+        from .model_io import ModelReader
+        with ModelReader(path, self.TYPE_NAME) as r:
+            U = r.read_matrix()
+            bias = r.read_vector() if self._has_bias() else None
+            V = r.read_matrix()
+        if U.shape[1] != V.shape[1]:
+            raise IOError(f"Number of user and item factors must match: {U.shape[1]} != "
+                          f"{V.shape[1]}")
+        if bias is not None and len(bias) != V.shape[0]:
+            raise IOError(f"Number of items must be the same for biases and factors: "
+                          f"{len(bias)} != {V.shape[0]}")
+        self.MaxUserID, self.MaxItemID = U.shape[0] - 1, V.shape[0] - 1
+        if int(self.NumFactors) != U.shape[1]:
+            print(f"Set num_factors to {U.shape[1]}", file=sys.stderr)
+            self.NumFactors = U.shape[1]
+        self._load_device_model(U, V, bias)
+
+    def _has_bias(self) -> bool:
+        return False
+
+    def _load_device_model(self, U, V, bias):
+        raise NotImplementedError
+
     def evaluate_auc(self, test: PosOnlyFeedback, test_users=None, candidate_items=None):
         """Eval.Items.Evaluate (Eval/Items.cs:126-209) restricted to AUC, scored on the GPU.
 
@@ -144,6 +181,26 @@ class BPRMF(_MFBase):
 
     def _auc_symbol(self):
         return "mml_bpr_auc"
+
+    TYPE_NAME = "MyMediaLite.ItemRecommendation.BPRMF"
+
+    def _has_bias(self) -> bool:
+        return True
+
+    def _load_device_model(self, U, V, bias):
+        self._release()
+        self._ctx = N.Context(self.Device)
+        f = lambda x: float(np.float32(x))
+        p = N.BprParams(int(self.NumFactors), self._sampler(), int(bool(self.UpdateJ)),
+                        f(self.LearnRate), f(self.RegU), f(self.RegI), f(self.RegJ),
+                        f(self.BiasReg))
+        h = N._vp()
+        N.check(N.lib().mml_bpr_create(self._ctx.handle, ctypes.byref(p), U.shape[0], V.shape[0],
+                                       ctypes.byref(h)))
+        self._h = h
+        N.check(N.lib().mml_bpr_set_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
+                                          N.ptr(bias, N._f32p)))
+        self._host = dict(U=U, V=V, bias=bias)
 
     def _sampler(self) -> int:
         if self.WithReplacement:
@@ -254,6 +311,19 @@ class WRMF(_MFBase):
 
     def _auc_symbol(self):
         return "mml_wrmf_auc"
+
+    TYPE_NAME = "MyMediaLite.ItemRecommendation.WRMF"
+
+    def _load_device_model(self, U, V, bias):
+        self._release()
+        self._ctx = N.Context(self.Device)
+        p = N.WrmfParams(int(self.NumFactors), 0, float(self.Alpha), float(self.Regularization))
+        h = N._vp()
+        N.check(N.lib().mml_wrmf_create(self._ctx.handle, ctypes.byref(p), U.shape[0], V.shape[0],
+                                        ctypes.byref(h)))
+        self._h = h
+        N.check(N.lib().mml_wrmf_set_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p)))
+        self._host = dict(U=U, V=V)
 
     def init_model(self):
         """MF.InitModel (MF.cs:51-58) + the feedback sets on the device."""

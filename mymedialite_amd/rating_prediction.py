@@ -65,7 +65,7 @@ class BiasedMatrixFactorization(Recommender):
         self._ctx = None
         self._h = None
         self._host = None  # cached host copy of the model
-        self.current_learnrate = float(np.float32(self.LearnRate))
+        self.current_learnrate = 0.0  # set by InitModel (MatrixFactorization.cs:115); 0 before
         self.global_bias = 0.0
         self.min_rating = 0.0
         self.max_rating = 0.0
@@ -126,13 +126,7 @@ class BiasedMatrixFactorization(Recommender):
         bu = np.zeros(nu, np.float32)
         bi = np.zeros(ni, np.float32)
         self.current_learnrate = float(np.float32(self.LearnRate))
-        self._release()
-        self._ctx = N.Context(self.Device)
-        h = N._vp()
-        N.check(N.lib().mml_bmf_create(self._ctx.handle, N.ctypes.byref(self._params()), nu, ni,
-                                       N.ctypes.byref(h)))
-        self._h = h
-        self._order_uploaded = False
+        self._create_handle(nu, ni)
         self._host = dict(U=U, V=V, bu=bu, bi=bi)
         self._last_loss = -math.inf
         if self.BoldDriver:
@@ -145,6 +139,60 @@ class BiasedMatrixFactorization(Recommender):
                                              r.count, None))  # no RNG draw: order is irrelevant
             self._last_loss = self.compute_objective()
         self._upload_model(0.0)
+
+    def _create_handle(self, nu, ni):
+        self._release()
+        self._ctx = N.Context(self.Device)
+        h = N._vp()
+        N.check(N.lib().mml_bmf_create(self._ctx.handle, N.ctypes.byref(self._params()), nu, ni,
+                                       N.ctypes.byref(h)))
+        self._h = h
+        self._order_uploaded = False
+
+    TYPE_NAME = "MyMediaLite.RatingPrediction.BiasedMatrixFactorization"
+
+    def save_model(self, path: str):
+        """SaveModel (:339-351): global bias, min/max rating, user biases, user factors, item
+        biases, item factors (IO/Model.cs text format, 7-digit floats)."""
+        from .model_io import ModelWriter
+        m = self.get_model()
+        with ModelWriter(path, self.TYPE_NAME) as w:
+            w.write_float(self.global_bias)
+            w.write_float(self.min_rating)
+            w.write_float(self.max_rating)
+            w.write_vector(m["bu"])
+            w.write_matrix(m["U"])
+            w.write_vector(m["bi"])
+            w.write_matrix(m["V"])
+
+    def load_model(self, path: str):
+        """LoadModel (:354-401); the model goes to the device.  Like the reference it does not
+        touch current_learnrate (0 on a fresh object: Iterate() after a load leaves the factors
+        unchanged until InitModel / Train sets it)."""
+        import sys
+        from .model_io import ModelReader
+        with ModelReader(path, self.TYPE_NAME) as r:
+            gb, mn, mx = r.read_float(), r.read_float(), r.read_float()
+            bu, U = r.read_vector(), r.read_matrix()
+            bi, V = r.read_vector(), r.read_matrix()
+        if U.shape[1] != V.shape[1]:
+            raise IOError(f"Number of user and item factors must match: {U.shape[1]} != "
+                          f"{V.shape[1]}")
+        if len(bu) != U.shape[0]:
+            raise IOError(f"Number of users must be the same for biases and factors: "
+                          f"{len(bu)} != {U.shape[0]}")
+        if len(bi) != V.shape[0]:
+            raise IOError(f"Number of items must be the same for biases and factors: "
+                          f"{len(bi)} != {V.shape[0]}")
+        self.MaxUserID, self.MaxItemID = U.shape[0] - 1, V.shape[0] - 1
+        if int(self.NumFactors) != U.shape[1]:
+            print(f"Set NumFactors to {U.shape[1]}", file=sys.stderr)
+            self.NumFactors = U.shape[1]
+        self.global_bias, self.min_rating, self.max_rating = float(gb), float(mn), float(mx)
+        self._create_handle(U.shape[0], V.shape[0])
+        self._host = dict(U=U, V=V, bu=bu, bi=bi)
+        self._upload_model(self.global_bias)
+        self._host = None
 
     def _upload_model(self, global_bias, range_zero=False):
         m = self._host

@@ -270,3 +270,22 @@ def test_bold_driver_matches_oracle():
     np.testing.assert_allclose(objs, st["objectives"], rtol=1e-6)
     assert [float(np.float32(x)) for x in lrs[:-1]] == [float(np.float32(x)) for x in st["lrs"]]
     assert np.float32(lrs[-1]) == np.float32(st["current_learnrate"])
+
+
+def test_save_load_model_predictions(tmp_path):
+    """RatingPredictorsTest.TestSaveLoad (:76-108): Predict equal within 1e-4 after a save/load
+    round trip through the IO/Model.cs text format; a fresh object keeps current_learnrate = 0."""
+    u, i, v = synth_ratings(31, 150, 60, 3000)
+    m, _ = gpu_train(u, i, v, seed=2, k=6, num_iter=3)
+    qu = np.array([0, 0, 0, 0, 0, 149, 500], np.int32)
+    qi = np.array([0, 1, 2, 3, 4, 59, 3], np.int32)
+    before = m.predict(qu, qi)
+    path = str(tmp_path / "bmf.model")
+    m.save_model(path)
+    m2 = BiasedMatrixFactorization()
+    m2.load_model(path)
+    after = m2.predict(qu, qi)
+    np.testing.assert_allclose(after, before, atol=1e-4)
+    assert m2.NumFactors == 6 and m2.current_learnrate == 0.0
+    m.load_model(path)  # into the trained object itself (the reference test's form)
+    np.testing.assert_allclose(m.predict(qu, qi), before, atol=1e-4)

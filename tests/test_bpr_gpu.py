@@ -92,3 +92,24 @@ def test_bpr_update_j_false_keeps_negatives():
     # items that are never positive are only ever sampled as j -> unchanged with UpdateJ=false
     assert len(never_pos) == 0 or np.array_equal(V0[never_pos], V1[never_pos])
     assert not np.array_equal(V0, V1)
+
+
+def test_bpr_and_wrmf_save_load_model(tmp_path):
+    """ItemRecommendersTest save/load (:63-103): Predict equal within 1e-4 after a round trip."""
+    from mymedialite_amd import WRMF
+    tr_u, tr_i, _, _ = planted_feedback(4, 120, 50, 8)
+    qu = np.array([0, 1, 2, 119, 5], np.int32)
+    qi = np.array([0, 1, 2, 49, 7], np.int32)
+    for cls in (BPRMF, WRMF):
+        Random.set_seed(3)
+        m = cls(NumFactors=5, NumIter=2)
+        m.feedback = PosOnlyFeedback(tr_u, tr_i)
+        m.train()
+        before = m.predict(qu, qi)
+        path = str(tmp_path / f"{cls.__name__}.model")
+        m.save_model(path)
+        m2 = cls()
+        m2.load_model(path)
+        np.testing.assert_allclose(m2.predict(qu, qi), before, atol=1e-4)
+        assert m2.NumFactors == 5
+        assert open(path).readline().strip() == f"MyMediaLite.ItemRecommendation.{cls.__name__}"

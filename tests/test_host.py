@@ -141,3 +141,37 @@ def test_blank_line_scale_quirk(tmp_path):
     p.write_text("0 0 3\n\n1 1 4\n")
     r = read_ratings(str(p))
     assert r.count == 2 and r.scale_min == 0.0 and r.scale_max == 4.0
+
+
+# ------------------------------------------------------------------ model files (IO/Model.cs)
+def test_float_text_matches_dotnet_invariant_g7():
+    """Single.ToString(CultureInfo.InvariantCulture): 7 significant digits, E+XX / E-XX."""
+    from mymedialite_amd.model_io import format_float
+    cases = {0.1: "0.1", 1.0 / 3: "0.3333333", 1e-5: "1E-05", 123456789.0: "1.234568E+08",
+             -2.5: "-2.5", 0.0: "0", 1234567.0: "1234567", 12345678.0: "1.234568E+07",
+             0.0001: "0.0001", 0.00001234: "1.234E-05", -3.402823466e38: "-3.402823E+38",
+             float("nan"): "NaN", float("inf"): "Infinity"}
+    for x, want in cases.items():
+        assert format_float(x) == want, (x, format_float(x), want)
+
+
+def test_model_text_round_trip(tmp_path):
+    """WriteMatrix / WriteVector (IO/MatrixExtensions.cs:31-89, VectorExtensions.cs:40-60) read
+    back by ReadMatrix / ReadVector: equal up to the 7-digit text, header lines as Model.GetWriter."""
+    from mymedialite_amd.model_io import ModelReader, ModelWriter
+    rs = np.random.default_rng(0)
+    M = (rs.standard_normal((5, 3)) * 10.0 ** rs.integers(-6, 6, (5, 3))).astype(np.float32)
+    v = rs.standard_normal(4).astype(np.float32)
+    p = tmp_path / "m.txt"
+    with ModelWriter(str(p), "MyMediaLite.Test") as w:
+        w.write_float(0.25)
+        w.write_vector(v)
+        w.write_matrix(M)
+    lines = p.read_text().split("\n")
+    assert lines[:4] == ["MyMediaLite.Test", "2.99", "0.25", "4"]
+    assert lines[8] == "5 3" and lines[9].startswith("0 0 ") and lines[24] == ""
+    with ModelReader(str(p), "MyMediaLite.Test") as r:
+        assert r.read_float() == np.float32(0.25)
+        v2, M2 = r.read_vector(), r.read_matrix()
+    np.testing.assert_allclose(v2, v, rtol=1e-6)
+    np.testing.assert_allclose(M2, M, rtol=1e-6)
