@@ -75,6 +75,37 @@ mml_status mml_partition_users_and_items(mml_random* r, const int32_t* users, co
 mml_status mml_balanced_rows(const int64_t* deg, int64_t n, int32_t k, int32_t parts,
                              int64_t* bounds);
 
+/* ------------------------------------------------------------------ rating files (host) */
+/* IO/StaticRatingData.Read (src/MyMediaLite/IO/StaticRatingData.cs:36-117), multi-threaded:
+ * StreamReader.ReadLine lines ("\n", "\r" or "\r\n"; a UTF-8 BOM dropped), empty lines skipped,
+ * String.Split on '\t' ' ' ',' (>= 3 tokens), ids by IdentityMapping (int.Parse) or
+ * Mapping.ToInternalID (first-appearance order, Data/Mapping.cs:75-85) seeded with the ids the
+ * caller's mapping already holds, ratings by float.Parse.  WITHOUT_RATINGS: the
+ * TestRatingFileFormat.WITHOUT_RATINGS variant (>= 2 tokens, rating 0).  ITEM_DATA: ItemData.Read
+ * (IO/ItemData.cs:59-94): >= 2 tokens, lines that Trim() to nothing skipped, values all 0. */
+enum {
+    MML_READ_IGNORE_FIRST_LINE = 1,
+    MML_READ_USER_IDENTITY = 2, /* IdentityMapping for users (else Mapping) */
+    MML_READ_ITEM_IDENTITY = 4,
+    MML_READ_WITHOUT_RATINGS = 8,
+    MML_READ_ITEM_DATA = 16,
+};
+typedef struct mml_rating_file mml_rating_file;
+mml_status mml_rating_file_read(const char* path, int32_t flags, int32_t n_threads,
+                                const char* const* user_seed, int32_t n_user_seed,
+                                const char* const* item_seed, int32_t n_item_seed,
+                                mml_rating_file** out);
+/* n_ratings = entries; n_lines = StaticRatings size (the array length the reference allocates);
+ * n_new_* = external ids the seeded mappings did not hold (internal ids n_seed, n_seed + 1, ...) */
+mml_status mml_rating_file_counts(mml_rating_file* f, int64_t* n_ratings, int64_t* n_lines,
+                                  int32_t* n_new_users, int32_t* n_new_items);
+mml_status mml_rating_file_get(mml_rating_file* f, int32_t* users, int32_t* items, float* values);
+/* which = 0 users, 1 items: all new external ids in internal-id order, each followed by '\n';
+ * *bytes = their total length (cap 0: query only) */
+mml_status mml_rating_file_new_ids(mml_rating_file* f, int32_t which, char* buf, int64_t cap,
+                                   int64_t* bytes);
+mml_status mml_rating_file_destroy(mml_rating_file* f);
+
 /* ------------------------------------------------------------------ BiasedMatrixFactorization */
 enum { MML_LOSS_RMSE = 0, MML_LOSS_MAE = 1, MML_LOSS_LOGISTIC = 2 }; /* OptimizationTarget */
 enum {

@@ -76,6 +76,15 @@ SIGNATURES = {
     "mml_random_shuffle_i32": (_st, [_vp, _i32p, ctypes.c_int64]),
     "mml_partition_users_and_items": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, ctypes.c_int32,
                                             ctypes.c_int32, ctypes.c_int32, _i64p, _i32p, _i32p]),
+    "mml_rating_file_read": (_st, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
+                                   ctypes.POINTER(ctypes.c_char_p), ctypes.c_int32,
+                                   ctypes.POINTER(ctypes.c_char_p), ctypes.c_int32,
+                                   ctypes.POINTER(_vp)]),
+    "mml_rating_file_counts": (_st, [_vp, _i64p, _i64p, _i32p, _i32p]),
+    "mml_rating_file_get": (_st, [_vp, _i32p, _i32p, _f32p]),
+    "mml_rating_file_new_ids": (_st, [_vp, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int64,
+                                      _i64p]),
+    "mml_rating_file_destroy": (_st, [_vp]),
     "mml_balanced_rows": (_st, [_i64p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _i64p]),
     "mml_bmf_create": (_st, [_vp, ctypes.POINTER(BmfParams), ctypes.c_int32, ctypes.c_int32,
                              ctypes.POINTER(_vp)]),
@@ -146,6 +155,10 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+READ_IGNORE_FIRST_LINE, READ_USER_IDENTITY, READ_ITEM_IDENTITY = 1, 2, 4
+READ_WITHOUT_RATINGS, READ_ITEM_DATA = 8, 16
 
 
 def check(status: int):

@@ -877,8 +877,8 @@ void launch_wood(hipStream_t st, const int32_t* rows, int32_t n, int32_t* counte
                  const int64_t* off, const int32_t* cols, const float* Q, int32_t k, float alpha,
                  float* Tout) {
     using C = WoodCfg<NT>;
-    const size_t lds = sizeof(WoodSmem<NT>) * C::R;
-    static const bool attr = [lds] {
+    constexpr size_t lds = sizeof(WoodSmem<NT>) * C::R;
+    static const bool attr = [] {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wrmf_wood_kernel<NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         return true;

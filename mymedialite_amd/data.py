@@ -148,18 +148,91 @@ def _tokens(line: str):
     return _SPLIT.split(line)
 
 
-def read_ratings(path: str, user_mapping=None, item_mapping=None, ignore_first_line=False):
-    """StaticRatingData.Read: arrays sized by the line count, empty lines skipped, >= 3 columns.
+# Char.IsWhiteSpace, which String.Trim strips (ItemData.Read skips lines that Trim to nothing)
+_CS_WHITESPACE = ("\t\n\v\f\r \x85\xa0\u1680" + "".join(chr(c) for c in range(0x2000, 0x200B))
+                  + "\u2028\u2029\u202f\u205f\u3000")
+_READLINE = re.compile(r"\r\n|\r|\n")
+
+
+def _read_lines(path: str, ignore_first_line: bool):
+    """StreamReader.ReadLine over a file: lines end at "\n", "\r" or "\r\n", a UTF-8 BOM is
+    dropped, a last line without a terminator still counts."""
+    with open(path, "r", encoding="utf-8-sig", newline="") as fh:
+        text = fh.read()
+    lines = _READLINE.split(text) if text else []
+    if lines and lines[-1] == "":
+        lines.pop()
+    return lines[1:] if ignore_first_line else lines
+
+
+def _native_read(path, user_mapping, item_mapping, flags, n_threads):
+    """mml_rating_file_read (ratings_file.cpp): the multi-threaded parse; the Mapping objects are
+    seeded into it and receive the new ids in first-appearance order.  Returns (users, items,
+    values, n_lines)."""
+    import ctypes
+    from . import _native as N
+    seeds = []
+    for which, m in ((0, user_mapping), (1, item_mapping)):
+        if isinstance(m, IdentityMapping):
+            flags |= N.READ_USER_IDENTITY if which == 0 else N.READ_ITEM_IDENTITY
+            seeds.append((None, 0))
+        else:
+            arr = (ctypes.c_char_p * max(1, len(m.internal_to_original)))(
+                *[x.encode() for x in m.internal_to_original])
+            seeds.append((arr, len(m.internal_to_original)))
+    h = N._vp()
+    N.check(N.lib().mml_rating_file_read(path.encode(), flags, n_threads, seeds[0][0],
+                                         seeds[0][1], seeds[1][0], seeds[1][1], ctypes.byref(h)))
+    try:
+        nr, nl = ctypes.c_int64(), ctypes.c_int64()
+        nu, ni = ctypes.c_int32(), ctypes.c_int32()
+        N.check(N.lib().mml_rating_file_counts(h, ctypes.byref(nr), ctypes.byref(nl),
+                                               ctypes.byref(nu), ctypes.byref(ni)))
+        users = np.empty(nr.value, np.int32)
+        items = np.empty(nr.value, np.int32)
+        values = np.empty(nr.value, np.float32)
+        N.check(N.lib().mml_rating_file_get(h, N.ptr(users, N._i32p), N.ptr(items, N._i32p),
+                                            N.ptr(values, N._f32p)))
+        for which, m, cnt in ((0, user_mapping, nu.value), (1, item_mapping, ni.value)):
+            if cnt == 0:
+                continue
+            nb = ctypes.c_int64()
+            N.check(N.lib().mml_rating_file_new_ids(h, which, None, 0, ctypes.byref(nb)))
+            buf = ctypes.create_string_buffer(nb.value)
+            N.check(N.lib().mml_rating_file_new_ids(h, which, buf, nb.value, ctypes.byref(nb)))
+            ids = buf.raw[: nb.value].decode().split("\n")[:-1]
+            assert len(ids) == cnt
+            base = len(m.internal_to_original)
+            m.internal_to_original.extend(ids)
+            m.original_to_internal.update(zip(ids, range(base, base + cnt)))
+    finally:
+        N.lib().mml_rating_file_destroy(h)
+    return users, items, values, nl.value
+
+
+def read_ratings(path: str, user_mapping=None, item_mapping=None, ignore_first_line=False,
+                 native=True, n_threads=8, with_ratings=True):
+    """StaticRatingData.Read (IO/StaticRatingData.cs:36-117): arrays sized by the line count,
+    empty lines skipped, >= 3 columns (>= 2 and rating 0 with ``with_ratings=False``, the
+    TestRatingFileFormat.WITHOUT_RATINGS variant).
 
     Quirk kept: the rating scale is built from the whole sized array,
-    so a blank line adds a level 0.
+    so a blank line adds a level 0.  ``native``: the library's multi-threaded reader
+    (mml_rating_file_read); False: this Python restatement (the two are tested equal).
     """
     user_mapping = user_mapping or IdentityMapping()
     item_mapping = item_mapping or IdentityMapping()
-    with open(path, "r", encoding="utf-8") as fh:
-        lines = fh.read().splitlines()
-    if ignore_first_line:
-        lines = lines[1:]
+    want = 3 if with_ratings else 2
+    if native:
+        from . import _native as N
+        flags = (N.READ_IGNORE_FIRST_LINE if ignore_first_line else 0) | \
+            (0 if with_ratings else N.READ_WITHOUT_RATINGS)
+        users, items, values, n_lines = _native_read(path, user_mapping, item_mapping, flags,
+                                                     n_threads)
+        scale = np.zeros(n_lines, np.float32)  # the sized array: blank lines are 0 (quirk above)
+        scale[: len(values)] = values
+        return Ratings(users, items, values, scale_values=scale)
+    lines = _read_lines(path, ignore_first_line)
     size = len(lines)
     users = np.zeros(size, np.int32)
     items = np.zeros(size, np.int32)
@@ -169,30 +242,38 @@ def read_ratings(path: str, user_mapping=None, item_mapping=None, ignore_first_l
         if len(line) == 0:
             continue
         tok = _tokens(line)
-        if len(tok) < 3:
-            raise ValueError("Expected at least 3 columns: " + line)
+        if len(tok) < want:
+            raise ValueError(f"Expected at least {want} columns: " + line)
         users[pos] = user_mapping.to_internal_id(tok[0])
         items[pos] = item_mapping.to_internal_id(tok[1])
-        values[pos] = np.float32(float(tok[2]))
+        values[pos] = np.float32(float(tok[2])) if with_ratings else 0.0
         pos += 1
     return Ratings(users[:pos], items[:pos], values[:pos], scale_values=values)
 
 
-def read_items(path: str, user_mapping=None, item_mapping=None, ignore_first_line=False):
-    """ItemData.Read: user item per line (blank lines skipped, >= 2 columns)."""
+def read_items(path: str, user_mapping=None, item_mapping=None, ignore_first_line=False,
+               native=True, n_threads=8):
+    """ItemData.Read (IO/ItemData.cs:59-94): user item per line, lines that Trim() to nothing
+    skipped, >= 2 columns.  ``native``: mml_rating_file_read with MML_READ_ITEM_DATA."""
     user_mapping = user_mapping or IdentityMapping()
     item_mapping = item_mapping or IdentityMapping()
+    if native:
+        from . import _native as N
+        flags = N.READ_ITEM_DATA | (N.READ_IGNORE_FIRST_LINE if ignore_first_line else 0)
+        users, items, _, _ = _native_read(path, user_mapping, item_mapping, flags, n_threads)
+        return PosOnlyFeedback(users, items)
     users, items = [], []
-    with open(path, "r", encoding="utf-8") as fh:
-        lines = fh.read().splitlines()
-    if ignore_first_line:
-        lines = lines[1:]
-    for line in lines:
-        if len(line.strip()) == 0:
+    for line in _read_lines(path, ignore_first_line):
+        if len(line.strip(_CS_WHITESPACE)) == 0:
             continue
         tok = _tokens(line)
         if len(tok) < 2:
             raise ValueError("Expected at least 2 columns: " + line)
-        users.append(user_mapping.to_internal_id(tok[0]))
-        items.append(item_mapping.to_internal_id(tok[1]))
+        try:
+            u = user_mapping.to_internal_id(tok[0])
+            i = item_mapping.to_internal_id(tok[1])
+        except ValueError:
+            raise ValueError(f"Could not read line '{line}'")
+        users.append(u)
+        items.append(i)
     return PosOnlyFeedback(np.array(users, np.int32), np.array(items, np.int32))

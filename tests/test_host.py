@@ -175,3 +175,144 @@ def test_model_text_round_trip(tmp_path):
         v2, M2 = r.read_vector(), r.read_matrix()
     np.testing.assert_allclose(v2, v, rtol=1e-6)
     np.testing.assert_allclose(M2, M, rtol=1e-6)
+
+
+def test_native_rating_reader_equals_python_restatement(tmp_path):
+    """mml_rating_file_read (multi-threaded) == the sequential StaticRatingData.Read restatement:
+    CRLF, blank lines, ',' / tab / space separators, string ids in first-appearance order across
+    thread chunks, a mapping seeded with ids it already holds, ignore_first_line."""
+    from mymedialite_amd import Mapping
+    rs = np.random.default_rng(4)
+    lines = ["user item rating"]
+    for x in range(5000):
+        sep = ["\t", " ", ","][x % 3]
+        lines.append(f"u{rs.integers(0, 300)}{sep}i{rs.integers(0, 900)}{sep}{rs.integers(1, 6)}"
+                     + (".5" if x % 7 == 0 else ""))
+        if x % 997 == 0:
+            lines.append("")
+    p = tmp_path / "r.txt"
+    p.write_bytes(("\r\n".join(lines) + "\r\n").encode())
+    for threads in (1, 3, 8):
+        got = []
+        for native in (True, False):
+            um, im = Mapping(), Mapping()
+            um.to_internal_id("u7")  # a mapping that already holds ids (train file read first)
+            im.to_internal_id("i_seed")
+            r = read_ratings(str(p), um, im, ignore_first_line=True, native=native,
+                             n_threads=threads)
+            got.append((r, um.internal_to_original, im.internal_to_original))
+        (a, au, ai), (b, bu, bi) = got
+        np.testing.assert_array_equal(a.users, b.users)
+        np.testing.assert_array_equal(a.items, b.items)
+        np.testing.assert_array_equal(a.values, b.values)
+        assert au == bu and ai == bi
+        assert a.scale_min == b.scale_min and a.scale_max == b.scale_max
+
+
+def test_native_rating_reader_identity_and_errors(tmp_path):
+    p = tmp_path / "ok.txt"
+    p.write_text("1 2 3.5\n\n4\t5\t1e0\n7,8,2")  # last line without a newline
+    r = read_ratings(str(p), n_threads=4)
+    np.testing.assert_array_equal(r.users, [1, 4, 7])
+    np.testing.assert_array_equal(r.items, [2, 5, 8])
+    np.testing.assert_array_equal(r.values, np.array([3.5, 1.0, 2.0], np.float32))
+    q = tmp_path / "bad.txt"
+    q.write_text("1 2 3\n1  2\n")  # "1", "", "2": three tokens, empty item id -> int.Parse fails
+    with pytest.raises(Exception):
+        read_ratings(str(q))
+    q.write_text("1 2 3\n12\n")
+    with pytest.raises(Exception, match="at least 3 columns"):
+        read_ratings(str(q))
+
+
+def _random_feedback_text(seed, n, terminators, with_rating=True, blanks=("",)):
+    rs = np.random.default_rng(seed)
+    parts = ["\ufeff"]  # UTF-8 BOM: StreamReader drops it
+    for x in range(n):
+        sep = ["\t", " ", ","][x % 3]
+        line = f"u{rs.integers(0, 200)}{sep}i{rs.integers(0, 500)}"
+        if with_rating:
+            line += f"{sep}{rs.integers(1, 6)}"
+        parts.append(line + terminators[x % len(terminators)])
+        if x % 311 == 0:
+            parts.append(blanks[x % len(blanks)] + terminators[(x + 1) % len(terminators)])
+    return "".join(parts)
+
+
+def test_native_reader_readline_terminators_and_bom(tmp_path):
+    """ReadLine ends lines at "\\n", a lone "\\r" and "\\r\\n" (a "\\r" | "\\n" pair split across
+    thread chunks included); the BOM is dropped; a tiny file read by more threads than bytes."""
+    from mymedialite_amd import Mapping
+    p = tmp_path / "t.txt"
+    p.write_bytes(_random_feedback_text(9, 3000, ["\n", "\r", "\r\n"]).encode())
+    for threads in (1, 2, 7, 16):
+        got = []
+        for native in (True, False):
+            um, im = Mapping(), Mapping()
+            r = read_ratings(str(p), um, im, native=native, n_threads=threads)
+            got.append((r.users, r.items, r.values, r.scale_min, um.internal_to_original,
+                        im.internal_to_original))
+        for x, y in zip(*got):
+            if isinstance(x, np.ndarray):
+                np.testing.assert_array_equal(x, y)
+            else:
+                assert x == y
+        assert got[0][0].shape == (3000,)
+    q = tmp_path / "tiny.txt"
+    for text in ("\ufeff1 2 3", "\ufeff1 2 3\r", "1 2 3\r4 5 1\r\n", "\r\n1 2 3"):
+        q.write_bytes(text.encode())
+        for threads in (1, 8, 64):
+            a = read_ratings(str(q), n_threads=threads)
+            b = read_ratings(str(q), native=False)
+            np.testing.assert_array_equal(a.users, b.users)
+            np.testing.assert_array_equal(a.values, b.values)
+            assert a.scale_min == b.scale_min
+
+
+def test_native_reader_without_ratings(tmp_path):
+    from mymedialite_amd import Mapping
+    p = tmp_path / "t.txt"
+    p.write_bytes(_random_feedback_text(3, 2000, ["\n"], with_rating=False).encode())
+    um, im = Mapping(), Mapping()
+    a = read_ratings(str(p), um, im, with_ratings=False, n_threads=5)
+    b = read_ratings(str(p), Mapping(), Mapping(), with_ratings=False, native=False)
+    np.testing.assert_array_equal(a.users, b.users)
+    np.testing.assert_array_equal(a.items, b.items)
+    assert not a.values.any() and a.count == 2000
+    with pytest.raises(Exception, match="at least 3 columns"):
+        read_ratings(str(p))  # WITH_RATINGS on a two-column file
+
+
+def test_native_item_data_reader_equals_restatement(tmp_path):
+    """ItemData.Read: >= 2 columns, lines that String.Trim() to nothing are skipped (tabs, NBSP,
+    ideographic space), extra columns ignored; identity and string mappings."""
+    from mymedialite_amd import Mapping, read_items
+    p = tmp_path / "f.txt"
+    text = _random_feedback_text(5, 4000, ["\n", "\r\n"], with_rating=False,
+                                 blanks=("", " \t ", "\xa0", "\u3000 ", "\u2003"))
+    p.write_bytes(("uid iid\n" + text.replace("\ufeff", "")).encode())
+    for threads in (1, 8):
+        um, im = Mapping(), Mapping()
+        um.to_internal_id("u3")
+        a = read_items(str(p), um, im, ignore_first_line=True, n_threads=threads)
+        vm, jm = Mapping(), Mapping()
+        vm.to_internal_id("u3")
+        b = read_items(str(p), vm, jm, ignore_first_line=True, native=False)
+        np.testing.assert_array_equal(a.users, b.users)
+        np.testing.assert_array_equal(a.items, b.items)
+        assert um.internal_to_original == vm.internal_to_original
+        assert im.internal_to_original == jm.internal_to_original
+        assert a.count == 4000
+    q = tmp_path / "ids.txt"
+    q.write_text("1 2 9\n\xa0\n3\t4\n5,6\n")
+    a = read_items(str(q), n_threads=3)
+    np.testing.assert_array_equal(a.users, [1, 3, 5])
+    np.testing.assert_array_equal(a.items, [2, 4, 6])
+    q.write_text("1 2\nx 4\n")
+    with pytest.raises(Exception, match="Could not read line 'x 4'"):
+        read_items(str(q))
+    with pytest.raises(Exception, match="Could not read line 'x 4'"):
+        read_items(str(q), native=False)
+    q.write_text("1 2\n34\n")
+    with pytest.raises(Exception, match="at least 2 columns"):
+        read_items(str(q))
