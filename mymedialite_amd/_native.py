@@ -145,10 +145,11 @@ def lib():
             import torch  # noqa: F401
         except ImportError:
             pass
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() "
+        path = os.environ.get("MML_LIB_PATH", LIB_PATH)  # an alternative build, for A/B runs
+        if not os.path.exists(path):
+            raise ImportError(f"{path} is missing: run __graft_entry__.build() "
                               "(hipcc --offload-arch=gfx950); there is no CPU fallback")
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res

@@ -190,18 +190,60 @@ __device__ __forceinline__ void store1(float* p, float v) {
     else *p = v;
 }
 
-// HOGWILD: LPR lanes per rating, one float4 of U_u and of V_i per lane (one 16-B load and store per
-// row per lane), plain racy stores of the new rows and biases (Hogwild!).  A float-atomic variant
-// for item rows (no lost updates) was measured 7.5x slower on C2 (memory-side atomics serialise on
-// hot Zipf items) for no RMSE gain at that scale, so it is not kept.
-template <int LOSS, int LPR, bool COH>
+// Sum over an aligned group of LPR lanes, every lane of the group getting the bit-identical total
+// (each pairwise add is x_self + x_partner, commutative).  Within a 16-lane row the partner comes
+// through DPP (quad_perm xor 1 / xor 2, half-row mirror, row mirror): a VALU operand modifier with
+// no LDS round trip, unlike __shfl_xor (ds_bpermute), which is kept only across rows.
+#define MML_DPP_F32(v, ctrl) \
+    __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
+template <int LPR>
+__device__ __forceinline__ float group_sum(float x) {
+    if constexpr (LPR >= 2) x += MML_DPP_F32(x, 0xB1);   // quad_perm [1,0,3,2]
+    if constexpr (LPR >= 4) x += MML_DPP_F32(x, 0x4E);   // quad_perm [2,3,0,1]
+    if constexpr (LPR >= 8) x += MML_DPP_F32(x, 0x141);  // row_half_mirror
+    if constexpr (LPR >= 16) x += MML_DPP_F32(x, 0x140); // row_mirror
+    if constexpr (LPR >= 32) x += __shfl_xor(x, 16);
+    if constexpr (LPR >= 64) x += __shfl_xor(x, 32);
+    return x;
+}
+
+// value of lane base + (lane / LPR) for a wave-uniform base: v_readlane per group (scalar lane
+// index, no LDS) while a step holds at most 4 groups, ds_bpermute beyond
+template <int LPR, typename T>
+__device__ __forceinline__ T group_fetch(T v, int base, int lane) {
+    constexpr int RPW = 64 / LPR;
+    if constexpr (RPW <= 4) {
+        const int sub = lane / LPR;
+        const int bits = __builtin_bit_cast(int, v);
+        int out = __builtin_amdgcn_readlane(bits, base);
+        if constexpr (RPW >= 2) out = sub == 1 ? __builtin_amdgcn_readlane(bits, base + 1) : out;
+        if constexpr (RPW >= 4) {
+            out = sub == 2 ? __builtin_amdgcn_readlane(bits, base + 2) : out;
+            out = sub == 3 ? __builtin_amdgcn_readlane(bits, base + 3) : out;
+        }
+        return __builtin_bit_cast(T, out);
+    } else {
+        return __shfl(v, base + lane / LPR);
+    }
+}
+
+// HOGWILD: LPR lanes per rating, VPL float4s of U_u and of V_i per lane (float4 q + LPR v of the
+// row, so each load instruction reads 16 LPR contiguous bytes of every row in the step), plain
+// racy stores of the new rows and biases (Hogwild!).  A float-atomic variant for item rows (no lost
+// updates) was measured 7.5x slower on C2 (memory-side atomics serialise on hot Zipf items) for no
+// RMSE gain at that scale, so it is not kept.  VPL > 1 puts more ratings in one wave
+// step (64 / LPR): more rows in flight per wave and the per-rating scalar part (sigmoid, fp64
+// gradient) shared by fewer lanes.
+template <int LOSS, int LPR, int VPL, bool COH>
 __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
     int64_t n, int64_t chunk, float* U, float* V, float* bu, float* bi, int32_t ld4, BmfScalars s,
     const int32_t* __restrict__ cnt_u, const int32_t* __restrict__ cnt_i) {
     constexpr int RPW = 64 / LPR;  // ratings per wave step
     const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    // wave-uniform (SGPR) bounds: the loops' branches stay scalar
+    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + wib;
     const int64_t begin = wave * chunk;
     const int64_t end = min(begin + chunk, n);
     const int sub = lane / LPR, q = lane % LPR;
@@ -214,33 +256,49 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
         const int32_t my_u = in ? su[idx] : 0;
         const int32_t my_i = in ? si[idx] : 0;
         const float my_r = in ? sr[idx] : 0.0f;
+        // consume the three loads here: otherwise the wait for them lands at the top of the
+        // step loop, where the in-order counter makes it a wait for the previous step's stores
+        asm volatile("" ::"v"(my_u), "v"(my_i), "v"(my_r));
         const int cnt = (int)min((int64_t)64, end - base);
         for (int step = 0; step < cnt; step += RPW) {
             const int src = step + sub;
-            const int32_t u = __shfl(my_u, src);
-            const int32_t i = __shfl(my_i, src);
-            const float r = __shfl(my_r, src);
+            // lanes past cnt read lane min(src, 63): a real (loaded or zeroed) entry, unused
+            const int32_t u = group_fetch<LPR>(my_u, step, lane);
+            const int32_t i = group_fetch<LPR>(my_i, step, lane);
+            const float r = group_fetch<LPR>(my_r, step, lane);
             if (src < cnt) {
                 const int64_t ou = (int64_t)u * ld4 + q, oi = (int64_t)i * ld4 + q;
-                const float4 pu = load4<COH>(U4 + ou);
-                const float4 qi = load4<COH>(V4 + oi);
-                float part = pu.x * qi.x;
-                part += pu.y * qi.y;
-                part += pu.z * qi.z;
-                part += pu.w * qi.w;
-                // xor butterfly: every lane of the group ends with the bit-identical sum
+                float4 pu[VPL], qi[VPL];
 #pragma unroll
-                for (int off = LPR / 2; off >= 1; off >>= 1) part += __shfl_xor(part, off);
+                for (int v = 0; v < VPL; ++v) {
+                    pu[v] = load4<COH>(U4 + ou + LPR * v);
+                    qi[v] = load4<COH>(V4 + oi + LPR * v);
+                }
+                float part = 0.0f;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v) {
+                    part += pu[v].x * qi[v].x;
+                    part += pu[v].y * qi[v].y;
+                    part += pu[v].z * qi[v].z;
+                    part += pu[v].w * qi[v].w;
+                }
+                part = group_sum<LPR>(part);
                 const float bu_u = load1<COH>(bu + u), bi_i = load1<COH>(bi + i);
                 const RatingStep<LOSS> st(s, part, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
                 if (q == 0) {
                     store1<COH>(bu + u, st.new_bu);
                     store1<COH>(bi + i, st.new_bi);
                 }
-                store4<COH>(U4 + ou, make_float4(st.new_u(s, pu.x, qi.x), st.new_u(s, pu.y, qi.y),
-                                             st.new_u(s, pu.z, qi.z), st.new_u(s, pu.w, qi.w)));
-                store4<COH>(V4 + oi, make_float4(st.new_i(s, pu.x, qi.x), st.new_i(s, pu.y, qi.y),
-                                             st.new_i(s, pu.z, qi.z), st.new_i(s, pu.w, qi.w)));
+#pragma unroll
+                for (int v = 0; v < VPL; ++v) {
+                    const float4 a = pu[v], c = qi[v];
+                    store4<COH>(U4 + ou + LPR * v,
+                                make_float4(st.new_u(s, a.x, c.x), st.new_u(s, a.y, c.y),
+                                            st.new_u(s, a.z, c.z), st.new_u(s, a.w, c.w)));
+                    store4<COH>(V4 + oi + LPR * v,
+                                make_float4(st.new_i(s, a.x, c.x), st.new_i(s, a.y, c.y),
+                                            st.new_i(s, a.z, c.z), st.new_i(s, a.w, c.w)));
+                }
             }
         }
     }
@@ -571,26 +629,44 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     const int64_t chunk = (n + waves - 1) / waves;
     const int ld4 = h->ld / 4;
     const bool coh = h->p.schedule == MML_SCHEDULE_HOGWILD_COHERENT;
-#define MML_HOG1(LPR, COH)                                                                     \
-    bmf_sgd_hogwild_kernel<LOSS, LPR, COH><<<(int)blocks, 256, 0, st>>>(                     \
+    static const int vpl_env = [] {
+        const char* e = std::getenv("MML_HOGWILD_VPL");
+        return e ? std::atoi(e) : 0;
+    }();
+    // float4s per lane: VPL x LPR = ld / 4 (h->lpr is the VPL = 1 lane count)
+    int vpl = vpl_env == 2 || vpl_env == 4 ? vpl_env : 1;
+#define MML_HOG1(LPR, VPL, COH)                                                                \
+    bmf_sgd_hogwild_kernel<LOSS, LPR, VPL, COH><<<(int)blocks, 256, 0, st>>>(                \
         h->su.get(), h->si.get(), h->sr.get(), n, chunk, h->U.get(), h->V.get(), h->bu.get(),  \
         h->bi.get(), ld4, s, cu, ci)
-#define MML_HOG(LPR)             \
-    if (coh) {                   \
-        MML_HOG1(LPR, true);     \
-    } else {                     \
-        MML_HOG1(LPR, false);    \
+#define MML_HOGV(LPR, VPL)         \
+    if (coh) {                     \
+        MML_HOG1(LPR, VPL, true);  \
+    } else {                       \
+        MML_HOG1(LPR, VPL, false); \
     }
-    switch (h->lpr) {
-        case 1: MML_HOG(1); break;
-        case 2: MML_HOG(2); break;
-        case 4: MML_HOG(4); break;
-        case 8: MML_HOG(8); break;
-        case 16: MML_HOG(16); break;
-        case 32: MML_HOG(32); break;
-        default: MML_HOG(64); break;
+    // VPL > 1 only for 16 < k <= 128 (row lengths 8, 16, 32 float4s)
+    const int row4 = h->lpr;
+    if (vpl > 1 && (row4 < 8 || row4 > 32)) vpl = 1;
+    switch (row4 * 8 + vpl) {
+        case 8 * 8 + 2: MML_HOGV(4, 2); break;
+        case 8 * 8 + 4: MML_HOGV(2, 4); break;
+        case 16 * 8 + 2: MML_HOGV(8, 2); break;
+        case 16 * 8 + 4: MML_HOGV(4, 4); break;
+        case 32 * 8 + 2: MML_HOGV(16, 2); break;
+        case 32 * 8 + 4: MML_HOGV(8, 4); break;
+        default:
+            switch (row4) {
+                case 1: MML_HOGV(1, 1); break;
+                case 2: MML_HOGV(2, 1); break;
+                case 4: MML_HOGV(4, 1); break;
+                case 8: MML_HOGV(8, 1); break;
+                case 16: MML_HOGV(16, 1); break;
+                case 32: MML_HOGV(32, 1); break;
+                default: MML_HOGV(64, 1); break;
+            }
     }
-#undef MML_HOG
+#undef MML_HOGV
 #undef MML_HOG1
     MML_HIP(hipGetLastError());
 }

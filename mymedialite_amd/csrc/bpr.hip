@@ -143,6 +143,131 @@ __global__ __launch_bounds__(256) void bpr_hogwild_kernel(
     }
 }
 
+// Two-phase epoch (default): bpr_sample_kernel draws every triple of the epoch -- the same
+// counter-based draws as the fused kernel, one thread per sample, so the dependent chain
+// eligible -> off -> cols -> rejection search of one sample overlaps with thousands of others --
+// and bpr_update_kernel then streams the triples like the BiasedMF Hogwild kernel (one row-load
+// latency per step instead of the whole sampling chain).  Same triples, same visit order.
+template <bool PAIR>
+__global__ __launch_bounds__(256) void bpr_sample_kernel(
+    const int64_t* __restrict__ off, const int32_t* __restrict__ cols,
+    const int32_t* __restrict__ eligible, int32_t n_eligible, const int32_t* __restrict__ ev_u,
+    const int32_t* __restrict__ ev_i, int64_t n_samples, int32_t n_items, uint64_t seed,
+    int32_t* __restrict__ tu, int32_t* __restrict__ ti, int32_t* __restrict__ tj) {
+    for (int64_t smp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; smp < n_samples;
+         smp += (int64_t)gridDim.x * blockDim.x) {
+        int32_t u, i;
+        if constexpr (PAIR) {
+            u = ev_u[smp];
+            i = ev_i[smp];
+        } else {
+            u = eligible[draw(seed, smp, 0, (uint32_t)n_eligible)];
+            const int64_t b = off[u];
+            const uint32_t deg = (uint32_t)(off[u + 1] - b);
+            i = cols[b + draw(seed, smp, 1, deg)];
+        }
+        const int64_t rb = off[u], re = off[u + 1];
+        int32_t j;
+        for (uint32_t d = 2;; ++d) {
+            j = (int32_t)draw(seed, smp, d, (uint32_t)n_items);
+            int64_t lo = rb, hi = re;  // j in the sorted row?
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (cols[mid] < j) lo = mid + 1;
+                else hi = mid;
+            }
+            if (!(lo < re && cols[lo] == j)) break;
+        }
+        tu[smp] = u;
+        ti[smp] = i;
+        tj[smp] = j;
+    }
+}
+
+// the triple of lane base + lane / LPR: v_readlane per group while a step holds <= 4 groups
+template <int LPR>
+__device__ __forceinline__ int32_t bpr_group_fetch(int32_t v, int base, int lane) {
+    constexpr int RPW = 64 / LPR;
+    if constexpr (RPW <= 4) {
+        const int sub = lane / LPR;
+        int out = __builtin_amdgcn_readlane(v, base);
+        if constexpr (RPW >= 2) out = sub == 1 ? __builtin_amdgcn_readlane(v, base + 1) : out;
+        if constexpr (RPW >= 4) {
+            out = sub == 2 ? __builtin_amdgcn_readlane(v, base + 2) : out;
+            out = sub == 3 ? __builtin_amdgcn_readlane(v, base + 3) : out;
+        }
+        return out;
+    } else {
+        return __shfl(v, base + lane / LPR);
+    }
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void bpr_update_kernel(
+    const int32_t* __restrict__ tu, const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
+    int64_t n_samples, int64_t chunk, float* U, float* V, float* bias, int32_t ld4, BprScalars s) {
+    constexpr int RPW = 64 / LPR;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t begin = wave * chunk;
+    const int64_t end = min(begin + chunk, n_samples);
+    const int sub = lane / LPR, q = lane % LPR;
+    float4* U4 = reinterpret_cast<float4*>(U);
+    float4* V4 = reinterpret_cast<float4*>(V);
+    for (int64_t base = begin; base < end; base += 64) {
+        const int64_t x = base + lane;
+        const bool in = x < end;
+        const int32_t my_u = in ? tu[x] : 0, my_i = in ? ti[x] : 0, my_j = in ? tj[x] : 0;
+        // consume the loads here, not at the top of the step loop (where the in-order counter
+        // would also wait for the previous step's stores)
+        asm volatile("" ::"v"(my_u), "v"(my_i), "v"(my_j));
+        const int cnt = (int)min((int64_t)64, end - base);
+        for (int step = 0; step < cnt; step += RPW) {
+            const int32_t u = bpr_group_fetch<LPR>(my_u, step, lane);
+            const int32_t i = bpr_group_fetch<LPR>(my_i, step, lane);
+            const int32_t j = bpr_group_fetch<LPR>(my_j, step, lane);
+            if (step + sub >= cnt) continue;
+            const int64_t ou = (int64_t)u * ld4 + q, oi = (int64_t)i * ld4 + q,
+                          oj = (int64_t)j * ld4 + q;
+            const float4 w = U4[ou];
+            const float4 hi = V4[oi];
+            const float4 hj = V4[oj];
+            const float bi = bias[i], bj = bias[j];
+            double part = (double)(w.x * (hi.x - hj.x));
+            part += (double)(w.y * (hi.y - hj.y));
+            part += (double)(w.z * (hi.z - hj.z));
+            part += (double)(w.w * (hi.w - hj.w));
+#pragma unroll
+            for (int o = LPR / 2; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+            const double x_uij = (double)(bi - bj) + part;
+            const double e = 1.0 / (1.0 + exp(x_uij));
+            if (q == 0) {
+                bias[i] = bi + (float)((double)s.lr * (e - (double)(s.bias_reg * bi)));
+                if (s.update_j)
+                    bias[j] = bj + (float)((double)s.lr * (-e - (double)(s.bias_reg * bj)));
+            }
+            const double lr = s.lr;
+            auto upd_u = [&](float wf, float hif, float hjf) {
+                return (float)((double)wf + lr * ((double)(hif - hjf) * e - (double)(s.reg_u * wf)));
+            };
+            auto upd_i = [&](float wf, float hif) {
+                return (float)((double)hif + lr * ((double)wf * e - (double)(s.reg_i * hif)));
+            };
+            auto upd_j = [&](float wf, float hjf) {
+                return (float)((double)hjf + lr * ((double)(-wf) * e - (double)(s.reg_j * hjf)));
+            };
+            U4[ou] = make_float4(upd_u(w.x, hi.x, hj.x), upd_u(w.y, hi.y, hj.y),
+                                 upd_u(w.z, hi.z, hj.z), upd_u(w.w, hi.w, hj.w));
+            V4[oi] = make_float4(upd_i(w.x, hi.x), upd_i(w.y, hi.y), upd_i(w.z, hi.z),
+                                 upd_i(w.w, hi.w));
+            if (s.update_j)
+                V4[oj] = make_float4(upd_j(w.x, hj.x), upd_j(w.y, hj.y), upd_j(w.z, hj.z),
+                                     upd_j(w.w, hj.w));
+        }
+    }
+}
+
 // BPRMF.Predict (:425-431): item_bias[i] + RowScalarProduct (float, left to right);
 // float.MinValue for ids beyond the model.  MF.Predict (WRMF) passes bias = nullptr.
 __global__ __launch_bounds__(256) void mf_predict_kernel(
@@ -185,6 +310,7 @@ struct mml_bpr {
     mml::DeviceArray<float> U, V, bias, ev_out;
     mml::DeviceArray<int64_t> off;
     mml::DeviceArray<int32_t> cols, eligible, ev_u, ev_i, q_u, q_i;
+    mml::DeviceArray<int32_t> tri_u, tri_i, tri_j;  // the epoch's triples (two-phase epoch)
     int64_t n_events = 0, nnz = 0;
     int32_t n_eligible = 0;
     bool has_data = false, has_model = false, has_order = false;
@@ -426,13 +552,44 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)16384;
         }();
         int64_t waves = std::min<int64_t>(256 * 32, std::max<int64_t>(1, n / min_chunk));
+        // fewer than 16 waves' worth of samples run as ONE workgroup: one CU, one L2, where 2+
+        // workgroups on different XCDs would each cache the hot item rows and overwrite each
+        // other's updates on write-back (bmf.hip launch_hogwild)
+        if (waves < 16) waves = 4;
         const int64_t blocks = (waves + 3) / 4;
         waves = blocks * 4;
         const int64_t chunk = (n + waves - 1) / waves;
         const bool pair = h->p.sampler == MML_BPR_SAMPLER_UNIFORM_PAIR;
+        static const bool fused = [] {
+            const char* e = std::getenv("MML_BPR_FUSED");
+            return e && std::atoi(e) > 0;
+        }();
+        if (!fused && n > 0 && (int64_t)h->tri_u.count < n) {
+            h->tri_u.alloc(n);
+            h->tri_i.alloc(n);
+            h->tri_j.alloc(n);
+        }
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
+        if (!fused && n > 0) {
+            const int sgrid = (int)std::min<int64_t>(256 * 64, (n + 255) / 256);
+            if (pair)
+                bpr_sample_kernel<true><<<sgrid, 256, 0, st>>>(
+                    h->off.get(), h->cols.get(), h->eligible.get(), h->n_eligible, h->ev_u.get(),
+                    h->ev_i.get(), n, h->n_items, seed, h->tri_u.get(), h->tri_i.get(),
+                    h->tri_j.get());
+            else
+                bpr_sample_kernel<false><<<sgrid, 256, 0, st>>>(
+                    h->off.get(), h->cols.get(), h->eligible.get(), h->n_eligible, h->ev_u.get(),
+                    h->ev_i.get(), n, h->n_items, seed, h->tri_u.get(), h->tri_i.get(),
+                    h->tri_j.get());
+            MML_HIP(hipGetLastError());
+        }
 #define MML_BPR(LPR)                                                                            \
-    if (pair)                                                                                   \
+    if (!fused)                                                                                 \
+        bpr_update_kernel<LPR><<<(int)blocks, 256, 0, st>>>(                                  \
+            h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), n, chunk, h->U.get(), h->V.get(),   \
+            h->bias.get(), h->ld / 4, s);                                                       \
+    else if (pair)                                                                              \
         bpr_hogwild_kernel<LPR, true><<<(int)blocks, 256, 0, st>>>(                           \
             h->off.get(), h->cols.get(), h->eligible.get(), h->n_eligible, h->ev_u.get(),       \
             h->ev_i.get(), n, chunk, h->n_items, seed, h->U.get(), h->V.get(), h->bias.get(),   \
