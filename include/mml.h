@@ -220,6 +220,8 @@ mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed);
 /* BPRMF.Predict (:425-431), batched: float.MinValue for ids beyond the model. */
 mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t n,
                            float* out);
+/* out[0] = the last epoch's device time (ms), out[1] = its update kernel alone (the rest is the
+ * triple sampler) */
 mml_status mml_bpr_last_timing(mml_bpr* h, float* out);
 /* Eval.Items.Evaluate's AUC (Eval/Items.cs:126-209 + Recommender.Recommend n = -1 +
  * Eval/Measures/AUC.cs:42-68) on the device for the eval users: candidates = the already shuffled

@@ -616,8 +616,9 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     // stream in order.  Fewer than 16 waves' worth of work runs as ONE workgroup: a single CU keeps
     // every row in one L1/L2, whereas 2+ workgroups land on different XCDs whose private write-back
     // L2s replicate hot rows ("Hogwild and per-XCD caches"; C1: 4 waves on one CU
-    // RMSE +0.007 vs sequential, 19 waves on 5 CUs +0.12).  Measured on C2: 8,192 waves 21.3 ms,
-    // 6,103 waves 22.9 ms; a software-pipelined variant (rows one step ahead) was not faster.
+    // RMSE +0.007 vs sequential, 19 waves on 5 CUs +0.12).  On C2 the kernel runs at the time of
+    // its bare memory pattern (scripts/ubench/rowrmw.hip: 22.2 ms for the 1,052 B per rating);
+    // VPL 2 equal, VPL 4 10 % slower, item-bucketing the stream per XCD 2 % slower.
     static const int64_t min_chunk = [] {
         const char* e = std::getenv("MML_HOGWILD_MIN_CHUNK");
         return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)12000;

@@ -49,6 +49,7 @@ extern "C" mml_status mml_ctx_create(int32_t device_id, mml_ctx** out) {
             MML_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
             MML_HIP(hipEventCreate(&ctx->ev_begin));
             MML_HIP(hipEventCreate(&ctx->ev_end));
+            MML_HIP(hipEventCreate(&ctx->ev_mid));
         } catch (...) {
             delete ctx;
             throw;
@@ -64,6 +65,7 @@ extern "C" mml_status mml_ctx_destroy(mml_ctx* ctx) {
         if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
         if (ctx->ev_begin) (void)hipEventDestroy(ctx->ev_begin);
         if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
+        if (ctx->ev_mid) (void)hipEventDestroy(ctx->ev_mid);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         delete ctx;
     });

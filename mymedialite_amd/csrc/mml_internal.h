@@ -141,6 +141,6 @@ struct mml_ctx {
     ncclComm_t comm = nullptr;
     int32_t nranks = 1;
     int32_t rank = 0;
-    hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_mid = nullptr;
     void activate() const { MML_HIP(hipSetDevice(device)); }
 };
