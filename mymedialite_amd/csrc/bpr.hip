@@ -148,6 +148,39 @@ __global__ __launch_bounds__(256) void bpr_hogwild_kernel(
 // eligible -> off -> cols -> rejection search of one sample overlaps with thousands of others --
 // and bpr_update_kernel then streams the triples like the BiasedMF Hogwild kernel (one row-load
 // latency per step instead of the whole sampling chain).  Same triples, same visit order.
+// Is j in the sorted row cols[rb, re)?  Rows of up to kScanMax entries are scanned flat: aligned
+// int4 loads that do not depend on each other (one memory round trip instead of the log2(deg)
+// dependent probes of a binary search; the CSR carries 16 entries of padding for the overrun),
+// entries outside [rb, re) masked.  Longer rows fall back to the binary search.
+constexpr int64_t kScanMax = 128;
+__device__ __forceinline__ bool row_has(const int32_t* __restrict__ cols, int64_t rb, int64_t re,
+                                        int32_t j) {
+    if (re - rb <= kScanMax) {
+        const int64_t a = rb & ~(int64_t)3;
+        const int4* p = reinterpret_cast<const int4*>(cols + a);
+        const int n4 = (int)((re - a + 3) >> 2);
+        bool hit = false;
+#pragma unroll 8
+        for (int t = 0; t < n4; ++t) {
+            const int4 v = p[t];
+            const int64_t x = a + 4 * t;
+            hit |= (v.x == j) & (x >= rb) & (x < re);
+            hit |= (v.y == j) & (x + 1 >= rb) & (x + 1 < re);
+            hit |= (v.z == j) & (x + 2 >= rb) & (x + 2 < re);
+            hit |= (v.w == j) & (x + 3 < re);
+        }
+        return hit;
+    }
+    int64_t lo = rb, hi = re;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (cols[mid] < j) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < re && cols[lo] == j;
+}
+
+// eligible == nullptr: every user is eligible (u = the draw itself, no gather)
 template <bool PAIR>
 __global__ __launch_bounds__(256) void bpr_sample_kernel(
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols,
@@ -156,27 +189,20 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
     int32_t* __restrict__ tu, int32_t* __restrict__ ti, int32_t* __restrict__ tj) {
     for (int64_t smp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; smp < n_samples;
          smp += (int64_t)gridDim.x * blockDim.x) {
-        int32_t u, i;
+        int32_t u, i = 0;
         if constexpr (PAIR) {
             u = ev_u[smp];
             i = ev_i[smp];
         } else {
-            u = eligible[draw(seed, smp, 0, (uint32_t)n_eligible)];
-            const int64_t b = off[u];
-            const uint32_t deg = (uint32_t)(off[u + 1] - b);
-            i = cols[b + draw(seed, smp, 1, deg)];
+            const uint32_t du = draw(seed, smp, 0, (uint32_t)n_eligible);
+            u = eligible ? eligible[du] : (int32_t)du;
         }
         const int64_t rb = off[u], re = off[u + 1];
+        if constexpr (!PAIR) i = cols[rb + draw(seed, smp, 1, (uint32_t)(re - rb))];
         int32_t j;
         for (uint32_t d = 2;; ++d) {
             j = (int32_t)draw(seed, smp, d, (uint32_t)n_items);
-            int64_t lo = rb, hi = re;  // j in the sorted row?
-            while (lo < hi) {
-                const int64_t mid = (lo + hi) >> 1;
-                if (cols[mid] < j) lo = mid + 1;
-                else hi = mid;
-            }
-            if (!(lo < re && cols[lo] == j)) break;
+            if (!row_has(cols, rb, re, j)) break;
         }
         tu[smp] = u;
         ti[smp] = i;
@@ -579,7 +605,9 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
                     h->tri_j.get());
             else
                 bpr_sample_kernel<false><<<sgrid, 256, 0, st>>>(
-                    h->off.get(), h->cols.get(), h->eligible.get(), h->n_eligible, h->ev_u.get(),
+                    h->off.get(), h->cols.get(),
+                    h->n_eligible == h->n_users ? nullptr : h->eligible.get(), h->n_eligible,
+                    h->ev_u.get(),
                     h->ev_i.get(), n, h->n_items, seed, h->tri_u.get(), h->tri_i.get(),
                     h->tri_j.get());
             MML_HIP(hipGetLastError());

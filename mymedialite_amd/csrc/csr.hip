@@ -70,7 +70,7 @@ void build_csr_device(const int32_t* rows, const int32_t* cols, int64_t n, int32
     out.deg_host.assign(n_rows, 0);
     if (n == 0) {
         MML_HIP(hipMemsetAsync(out.off.get(), 0, sizeof(int64_t) * (n_rows + 1), st));
-        out.cols.alloc(1);
+        out.cols.alloc(16);
         out.nnz = 0;
         MML_HIP(hipStreamSynchronize(st));
         return;
@@ -106,7 +106,10 @@ void build_csr_device(const int32_t* rows, const int32_t* cols, int64_t n, int32
     int64_t nnz = 0;
     MML_HIP(hipMemcpyAsync(&nnz, nsel.get(), sizeof(int64_t), hipMemcpyDeviceToHost, st));
     MML_HIP(hipStreamSynchronize(st));
-    out.cols.alloc(std::max<int64_t>(1, nnz));
+    // 16 entries of padding: the BPR sampler scans rows with aligned int4 loads that may run up to
+    // 15 entries past the last row (masked, never used)
+    out.cols.alloc(nnz + 16);
+    MML_HIP(hipMemsetAsync(out.cols.get() + nnz, 0xff, sizeof(int32_t) * 16, st));
     deg.alloc(n_rows);
     MML_HIP(hipMemsetAsync(deg.get(), 0, sizeof(int32_t) * n_rows, st));
     unpack_keys_kernel<<<grid_for(nnz), 256, 0, st>>>(keys.get(), nsel.get(), out.cols.get(),
