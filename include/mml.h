@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 1
+#define MML_ABI_VERSION 2
 
 typedef int32_t mml_status;
 enum {
@@ -116,6 +116,16 @@ enum {
                                          cache replicas of hot rows; slower on skewed items */
 };
 
+/* Model family of an mml_bmf handle. */
+enum {
+    MML_MF_BIASED = 0, /* BiasedMatrixFactorization (BiasedMatrixFactorization.cs:77-562) */
+    MML_MF_PLAIN = 1   /* MatrixFactorization (MatrixFactorization.cs:50-418): no biases, score =
+                          global_bias + <U_u, V_i>, err = r - score in float, Regularization for
+                          both sides (pass it as reg_u = reg_i), Predict clipped to [min, max];
+                          loss, frequency_regularization and the bias fields are ignored and
+                          mml_bmf_objective is not defined */
+};
+
 typedef struct {
     int32_t num_factors;              /* NumFactors (MatrixFactorization.cs:71) */
     int32_t loss;                     /* Loss, MML_LOSS_* (BiasedMatrixFactorization.cs:114) */
@@ -125,6 +135,7 @@ typedef struct {
     float bias_reg;                   /* BiasReg (:88) */
     float reg_u;                      /* RegU (:91) */
     float reg_i;                      /* RegI (:94) */
+    int32_t model;                    /* MML_MF_* (ABI 2) */
 } mml_bmf_params;
 
 typedef struct mml_bmf mml_bmf;
@@ -151,11 +162,14 @@ mml_status mml_bmf_set_model(mml_bmf* h, const float* user_factors, const float*
                              float min_rating, float max_rating);
 mml_status mml_bmf_get_model(mml_bmf* h, float* user_factors, float* item_factors,
                              float* user_bias, float* item_bias);
-/* One epoch = BiasedMatrixFactorization.Iterate(IList<int>,bool,bool) (:264-310) over the stored
+/* One epoch = BiasedMatrixFactorization.Iterate(IList<int>,bool,bool) (:264-310) -- for
+ * MML_MF_PLAIN MatrixFactorization.Iterate(IList<int>,bool,bool) (MatrixFactorization.cs:166-196)
+ * without its trailing UpdateLearnRate, which stays on the host -- over the stored
  * order at current_learnrate = learn_rate.  DSGD: subepoch_sequence[G] is the shuffled
  * sub-epoch order of Iterate() (:209-214); NULL otherwise. */
 mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate, const int32_t* subepoch_sequence);
-/* BiasedMatrixFactorization.Predict(int,int) (:313-325), batched; unknown ids allowed. */
+/* BiasedMatrixFactorization.Predict(int,int) (:313-325), batched; unknown ids allowed.
+ * MML_MF_PLAIN: MatrixFactorization.Predict(int,int) (MatrixFactorization.cs:251-258). */
 mml_status mml_bmf_predict(mml_bmf* h, const int32_t* users, const int32_t* items, int64_t n,
                            float* out);
 /* Eval.Ratings.Evaluate (Eval/Ratings.cs:96-139) on device: out[0] = RMSE, out[1] = MAE. */

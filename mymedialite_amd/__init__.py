@@ -6,7 +6,8 @@ include/mml.h); this package is the host-side mirror of the reference's recommen
 from .data import IdentityMapping, Mapping, PosOnlyFeedback, Ratings, read_items, read_ratings
 from .random import Random, SystemRandom
 from .item_recommendation import BPRMF, WRMF
-from .rating_prediction import BiasedMatrixFactorization
+from .rating_prediction import BiasedMatrixFactorization, MatrixFactorization
 
-__all__ = ["BiasedMatrixFactorization", "BPRMF", "WRMF", "Ratings", "PosOnlyFeedback", "Mapping",
-           "IdentityMapping", "read_ratings", "read_items", "Random", "SystemRandom"]
+__all__ = ["BiasedMatrixFactorization", "MatrixFactorization", "BPRMF", "WRMF", "Ratings",
+           "PosOnlyFeedback", "Mapping", "IdentityMapping", "read_ratings", "read_items", "Random",
+           "SystemRandom"]

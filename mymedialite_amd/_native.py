@@ -39,7 +39,10 @@ class BmfParams(ctypes.Structure):
     _fields_ = [("num_factors", ctypes.c_int32), ("loss", ctypes.c_int32),
                 ("frequency_regularization", ctypes.c_int32), ("schedule", ctypes.c_int32),
                 ("bias_learn_rate", ctypes.c_float), ("bias_reg", ctypes.c_float),
-                ("reg_u", ctypes.c_float), ("reg_i", ctypes.c_float)]
+                ("reg_u", ctypes.c_float), ("reg_i", ctypes.c_float), ("model", ctypes.c_int32)]
+
+
+MF_BIASED, MF_PLAIN = 0, 1
 
 
 class BprParams(ctypes.Structure):

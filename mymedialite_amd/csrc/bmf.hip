@@ -95,6 +95,32 @@ struct RatingStep {
     }
 };
 
+// MatrixFactorization (the plain model, MatrixFactorization.cs:166-196) runs on the same kernels
+// as template value kPlainMF in the LOSS slot: no biases; err = r - (global_bias + dot) in float;
+// delta = err * i_f - Regularization * u_f in float, widened to double; Inc adds
+// (float)(current_learnrate * delta).
+constexpr int kPlainMF = 8;
+
+template <>
+struct RatingStep<kPlainMF> {
+    float err, reg_u, reg_i, new_bu, new_bi;
+    __device__ __forceinline__ RatingStep(const BmfScalars& s, float dot, float, float, float r,
+                                          const int32_t*, const int32_t*, int32_t, int32_t) {
+        err = r - (s.gb + dot);
+        reg_u = s.reg_u;
+        reg_i = s.reg_i;
+        new_bu = new_bi = 0.0f;
+    }
+    __device__ __forceinline__ float new_u(const BmfScalars& s, float u_f, float i_f) const {
+        const double delta = (double)(err * i_f - reg_u * u_f);
+        return u_f + (float)((double)s.lr * delta);
+    }
+    __device__ __forceinline__ float new_i(const BmfScalars& s, float u_f, float i_f) const {
+        const double delta = (double)(err * u_f - reg_i * i_f);
+        return i_f + (float)((double)s.lr * delta);
+    }
+};
+
 // ORDERED / DSGD: workgroup = one wavefront; wavefront j walks block (j, (subepoch+j) mod G).
 // KM = factors per lane (k <= 64 * KM).
 template <int LOSS, int KM>
@@ -128,9 +154,10 @@ __global__ __launch_bounds__(64) void bmf_sgd_ordered_kernel(
             const int bits = __float_as_int(prod[m]);
             for (int l = 0; l < lim; ++l) dot += __int_as_float(__builtin_amdgcn_readlane(bits, l));
         }
-        const float bu_u = bu[u], bi_i = bi[i];
+        constexpr bool biased = LOSS != kPlainMF;
+        const float bu_u = biased ? bu[u] : 0.0f, bi_i = biased ? bi[i] : 0.0f;
         const RatingStep<LOSS> st(s, dot, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
-        if (lane == 0) {
+        if (biased && lane == 0) {
             bu[u] = st.new_bu;
             bi[i] = st.new_bi;
         }
@@ -283,9 +310,11 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
                     part += pu[v].w * qi[v].w;
                 }
                 part = group_sum<LPR>(part);
-                const float bu_u = load1<COH>(bu + u), bi_i = load1<COH>(bi + i);
+                constexpr bool biased = LOSS != kPlainMF;
+                const float bu_u = biased ? load1<COH>(bu + u) : 0.0f;
+                const float bi_i = biased ? load1<COH>(bi + i) : 0.0f;
                 const RatingStep<LOSS> st(s, part, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
-                if (q == 0) {
+                if (biased && q == 0) {
                     store1<COH>(bu + u, st.new_bu);
                     store1<COH>(bi + i, st.new_bi);
                 }
@@ -305,21 +334,31 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
 }
 
 // BiasedMatrixFactorization.Predict(int,int) (:313-325): double score, float dot in order.
+// plain: MatrixFactorization.Predict(int,int) (MatrixFactorization.cs:251-258 + :205-217):
+// global_bias for ids beyond the model, else global_bias + dot clipped to [min, max].
 __device__ __forceinline__ float bmf_predict1(int32_t u, int32_t i, int32_t n_users,
                                               int32_t n_items, const float* U, const float* V,
                                               const float* bu, const float* bi, int32_t k,
                                               int32_t ld, float gb, float min_rating,
-                                              float range) {
-    double score = (double)gb;
-    if (u >= 0 && u < n_users) score += (double)bu[u];
-    if (i >= 0 && i < n_items) score += (double)bi[i];
-    if (u >= 0 && u < n_users && i >= 0 && i < n_items) {
+                                              float max_rating, bool plain) {
+    const bool ku = u >= 0 && u < n_users, ki = i >= 0 && i < n_items;
+    float dot = 0.0f;
+    if (ku && ki) {
         const float* a = U + (int64_t)u * ld;
         const float* c = V + (int64_t)i * ld;
-        float dot = 0.0f;
         for (int f = 0; f < k; ++f) dot += a[f] * c[f];
-        score += (double)dot;
     }
+    if (plain) {
+        if (!(ku && ki)) return gb;
+        float r = gb + dot;
+        r = r > max_rating ? max_rating : r;
+        return r < min_rating ? min_rating : r;
+    }
+    double score = (double)gb;
+    if (ku) score += (double)bu[u];
+    if (ki) score += (double)bi[i];
+    if (ku && ki) score += (double)dot;
+    const float range = max_rating - min_rating;
     return (float)((double)min_rating + (1.0 / (1.0 + exp(-score))) * (double)range);
 }
 
@@ -327,11 +366,11 @@ __global__ __launch_bounds__(256) void bmf_predict_kernel(
     const int32_t* __restrict__ users, const int32_t* __restrict__ items, int64_t n,
     int32_t n_users, int32_t n_items, const float* __restrict__ U, const float* __restrict__ V,
     const float* __restrict__ bu, const float* __restrict__ bi, int32_t k, int32_t ld, float gb,
-    float min_rating, float range, float* __restrict__ out) {
+    float min_rating, float max_rating, int32_t plain, float* __restrict__ out) {
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
          x += (int64_t)gridDim.x * blockDim.x)
         out[x] = bmf_predict1(users[x], items[x], n_users, n_items, U, V, bu, bi, k, ld, gb,
-                              min_rating, range);
+                              min_rating, max_rating, plain != 0);
 }
 
 // Eval.Ratings.Evaluate (:96-139): float error, float square, double sums; per-block partials.
@@ -339,13 +378,13 @@ __global__ __launch_bounds__(256) void bmf_eval_kernel(
     const int32_t* __restrict__ users, const int32_t* __restrict__ items,
     const float* __restrict__ values, int64_t n, int32_t n_users, int32_t n_items,
     const float* __restrict__ U, const float* __restrict__ V, const float* __restrict__ bu,
-    const float* __restrict__ bi, int32_t k, int32_t ld, float gb, float min_rating, float range,
-    double* __restrict__ partials) {
+    const float* __restrict__ bi, int32_t k, int32_t ld, float gb, float min_rating,
+    float max_rating, int32_t plain, double* __restrict__ partials) {
     double se = 0.0, ae = 0.0;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
          x += (int64_t)gridDim.x * blockDim.x) {
         const float p = bmf_predict1(users[x], items[x], n_users, n_items, U, V, bu, bi, k, ld,
-                                     gb, min_rating, range);
+                                     gb, min_rating, max_rating, plain != 0);
         const float e = p - values[x];
         se += (double)(e * e);
         ae += (double)fabsf(e);
@@ -373,13 +412,14 @@ __global__ __launch_bounds__(256) void bmf_loss_kernel(
     const int32_t* __restrict__ users, const int32_t* __restrict__ items,
     const float* __restrict__ values, int64_t n, int32_t n_users, int32_t n_items,
     const float* __restrict__ U, const float* __restrict__ V, const float* __restrict__ bu,
-    const float* __restrict__ bi, int32_t k, int32_t ld, float gb, float min_rating, float range,
-    int32_t loss_kind, double* __restrict__ partials) {
+    const float* __restrict__ bi, int32_t k, int32_t ld, float gb, float min_rating,
+    float max_rating, int32_t loss_kind, double* __restrict__ partials) {
+    const float range = max_rating - min_rating;
     double acc = 0.0;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
          x += (int64_t)gridDim.x * blockDim.x) {
         const float p = bmf_predict1(users[x], items[x], n_users, n_items, U, V, bu, bi, k, ld,
-                                     gb, min_rating, range);
+                                     gb, min_rating, max_rating, false);
         if (loss_kind == MML_LOSS_RMSE) {
             const double d = (double)(p - values[x]);  // float difference, Math.Pow in double
             acc += d * d;
@@ -713,6 +753,8 @@ extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params,
                     "num_factors must be in [1, 256]");
         MML_REQUIRE(params->loss >= MML_LOSS_RMSE && params->loss <= MML_LOSS_LOGISTIC,
                     "unknown loss");
+        MML_REQUIRE(params->model == MML_MF_BIASED || params->model == MML_MF_PLAIN,
+                    "unknown model family");
         MML_REQUIRE(params->schedule >= MML_SCHEDULE_ORDERED &&
                         params->schedule <= MML_SCHEDULE_HOGWILD_COHERENT,
                     "unknown schedule");
@@ -915,7 +957,8 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
         s.reg_i = h->p.reg_i;
         hipStream_t st = h->ctx->stream;
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
-        switch (h->p.loss) {
+        switch (h->p.model == MML_MF_PLAIN ? kPlainMF : h->p.loss) {
+            case kPlainMF: run_epoch<kPlainMF>(h, s, subepoch_sequence); break;
             case MML_LOSS_MAE: run_epoch<MML_LOSS_MAE>(h, s, subepoch_sequence); break;
             case MML_LOSS_LOGISTIC: run_epoch<MML_LOSS_LOGISTIC>(h, s, subepoch_sequence); break;
             default: run_epoch<MML_LOSS_RMSE>(h, s, subepoch_sequence); break;
@@ -958,8 +1001,8 @@ extern "C" mml_status mml_bmf_predict(mml_bmf* h, const int32_t* users, const in
         h->ev_out.alloc(n);
         bmf_predict_kernel<<<grid_for(n), 256, 0, st>>>(
             h->ev_u.get(), h->ev_i.get(), n, h->n_users, h->n_items, h->U.get(), h->V.get(),
-            h->bu.get(), h->bi.get(), h->k, h->ld, h->gb, h->min_rating,
-            h->max_rating - h->min_rating, h->ev_out.get());
+            h->bu.get(), h->bi.get(), h->k, h->ld, h->gb, h->min_rating, h->max_rating,
+            (int32_t)(h->p.model == MML_MF_PLAIN), h->ev_out.get());
         MML_HIP(hipGetLastError());
         MML_HIP(hipMemcpyAsync(out, h->ev_out.get(), sizeof(float) * n, hipMemcpyDeviceToHost,
                                st));
@@ -984,7 +1027,8 @@ extern "C" mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const i
         bmf_eval_kernel<<<grid, 256, 0, st>>>(h->ev_u.get(), h->ev_i.get(), h->ev_r.get(), n,
                                               h->n_users, h->n_items, h->U.get(), h->V.get(),
                                               h->bu.get(), h->bi.get(), h->k, h->ld, h->gb,
-                                              h->min_rating, h->max_rating - h->min_rating,
+                                              h->min_rating, h->max_rating,
+                                              (int32_t)(h->p.model == MML_MF_PLAIN),
                                               h->ev_partials.get());
         MML_HIP(hipGetLastError());
         std::vector<double> part(2 * grid);
@@ -1005,6 +1049,8 @@ extern "C" mml_status mml_bmf_objective(mml_bmf* h, double* out) {
     return guard([&] {
         check_handle(h);
         MML_REQUIRE(h->has_model && h->has_data && out, "model, data and out required");
+        MML_REQUIRE(h->p.model == MML_MF_BIASED,
+                    "ComputeObjective is defined for BiasedMatrixFactorization only");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         const int g1 = grid_for(h->n, 256, 1024);
@@ -1013,8 +1059,8 @@ extern "C" mml_status mml_bmf_objective(mml_bmf* h, double* out) {
         bmf_loss_kernel<<<g1, 256, 0, st>>>(h->su.get(), h->si.get(), h->sr.get(), h->n,
                                             h->n_users, h->n_items, h->U.get(), h->V.get(),
                                             h->bu.get(), h->bi.get(), h->k, h->ld, h->gb,
-                                            h->min_rating, h->max_rating - h->min_rating,
-                                            h->p.loss, h->ev_partials.get());
+                                            h->min_rating, h->max_rating, h->p.loss,
+                                            h->ev_partials.get());
         bmf_complexity_kernel<<<g2, 256, 0, st>>>(
             h->U.get(), h->V.get(), h->bu.get(), h->bi.get(), h->cnt_u.get(), h->cnt_i.get(),
             h->n_users, h->n_items, h->k, h->ld, h->p.reg_u, h->p.reg_i, h->p.bias_reg,

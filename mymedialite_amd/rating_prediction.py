@@ -28,7 +28,226 @@ _SCHED = {"ordered": N.SCHEDULE_ORDERED, "dsgd": N.SCHEDULE_DSGD, "hogwild": N.S
           "hogwild_coherent": N.SCHEDULE_HOGWILD_COHERENT}
 
 
-class BiasedMatrixFactorization(Recommender):
+class MatrixFactorization(Recommender):
+    """GPU-backed MyMediaLite.RatingPrediction.MatrixFactorization (MatrixFactorization.cs:50-418):
+    the plain model (no biases) on the BiasedMatrixFactorization kernels (MML_MF_PLAIN).
+
+    Train() = InitModel (:99-116) + global_bias = Ratings.Average + NumIter x Iterate(RandomIndex)
+    (:119-126, LearnFactors :199-203); every Iterate() ends with UpdateLearnRate (:129-132,
+    current_learnrate *= Decay).  Schedule: ``auto``/``ordered`` = the reference's sequential loop
+    (exact), ``hogwild`` / ``hogwild_coherent`` = the lock-free GPU epoch."""
+    PROPERTIES = {
+        "Decay": "float", "Device": "int", "InitMean": "double", "InitStdDev": "double",
+        "LearnRate": "float", "NumFactors": "uint", "NumIter": "uint", "Regularization": "float",
+        "Schedule": "string",
+    }
+    MODEL = N.MF_PLAIN
+    TYPE_NAME = "MyMediaLite.RatingPrediction.MatrixFactorization"
+
+    def __init__(self, **kw):
+        # MatrixFactorization() defaults (:87-96)
+        self.Regularization = 0.015
+        self.LearnRate = 0.01
+        self.Decay = 1.0
+        self.NumIter = 30
+        self.InitMean = 0.0
+        self.InitStdDev = 0.1
+        self.NumFactors = 10
+        self.Schedule = "auto"
+        self.Device = 0
+        for k, v in kw.items():
+            setattr(self, k, v)
+        self._ratings = None
+        self._ctx = None
+        self._h = None
+        self._host = None
+        self.current_learnrate = 0.0
+        self.global_bias = 0.0
+        self.min_rating = 0.0
+        self.max_rating = 0.0
+        self._order_uploaded = False
+
+    @property
+    def ratings(self) -> Ratings:
+        return self._ratings
+
+    @ratings.setter
+    def ratings(self, r: Ratings):
+        """RatingPredictor.Ratings setter (RatingPrediction/RatingPredictor.cs:39-49)."""
+        self._ratings = r
+        self.MaxUserID = r.max_user_id
+        self.MaxItemID = r.max_item_id
+        self.min_rating = r.scale_min
+        self.max_rating = r.scale_max
+
+    def schedule(self) -> str:
+        if self.Schedule == "auto":
+            return "ordered"
+        if self.Schedule not in ("ordered", "hogwild", "hogwild_coherent"):
+            raise ValueError(f"unknown Schedule '{self.Schedule}' for {type(self).__name__}")
+        return self.Schedule
+
+    def _params(self) -> N.BmfParams:
+        reg = float(np.float32(self.Regularization))
+        return N.BmfParams(int(self.NumFactors), N.LOSS_RMSE, 0, _SCHED[self.schedule()], 0.0, 0.0,
+                           reg, reg, self.MODEL)
+
+    def _create_handle(self, nu, ni):
+        self._release()
+        self._ctx = N.Context(self.Device)
+        h = N._vp()
+        N.check(N.lib().mml_bmf_create(self._ctx.handle, N.ctypes.byref(self._params()), nu, ni,
+                                       N.ctypes.byref(h)))
+        self._h = h
+        self._order_uploaded = False
+
+    def init_model(self):
+        """InitModel (:99-116): U fully, then V fully, N(InitMean, InitStdDev); rows of users /
+        items without ratings zeroed; current_learnrate = LearnRate."""
+        r = self._ratings
+        k = int(self.NumFactors)
+        nu, ni = self.MaxUserID + 1, self.MaxItemID + 1
+        rng = Random.get_instance()
+        U = rng.fill_normal(nu * k, self.InitMean, self.InitStdDev).reshape(nu, k)
+        V = rng.fill_normal(ni * k, self.InitMean, self.InitStdDev).reshape(ni, k)
+        U[r.count_by_user == 0] = 0.0
+        V[r.count_by_item == 0] = 0.0
+        self.current_learnrate = float(np.float32(self.LearnRate))
+        self._create_handle(nu, ni)
+        self._host = dict(U=U, V=V)
+        self._upload_model(0.0)
+
+    def _upload_model(self, global_bias):
+        m = self._host
+        bu = np.zeros(m["U"].shape[0], np.float32)
+        bi = np.zeros(m["V"].shape[0], np.float32)
+        N.check(N.lib().mml_bmf_set_model(
+            self._h, N.ptr(N.f32(m["U"]), N._f32p), N.ptr(N.f32(m["V"]), N._f32p),
+            N.ptr(bu, N._f32p), N.ptr(bi, N._f32p), float(global_bias), float(self.min_rating),
+            float(self.max_rating)))
+
+    def train(self):
+        """Train() (:119-126)."""
+        self.init_model()
+        self.global_bias = self._ratings.average  # Ratings.Average, float
+        self._upload_model(self.global_bias)
+        self._host = None
+        for _ in range(int(self.NumIter)):
+            self.iterate()
+
+    def _ensure_data(self):
+        if self._order_uploaded:
+            return
+        r = self._ratings
+        order = r.random_index  # DataSet.RandomIndex: shuffled ONCE, reused every epoch
+        N.check(N.lib().mml_bmf_set_data(self._h, N.ptr(r.users, N._i32p), N.ptr(r.items, N._i32p),
+                                         N.ptr(r.values, N._f32p), r.count,
+                                         N.ptr(order, N._i32p)))
+        self._order_uploaded = True
+
+    def iterate(self):
+        """Iterate() (:135-138) = Iterate(RandomIndex, true, true) (:166-196), which ends with
+        UpdateLearnRate() (:129-132)."""
+        if self._h is None:
+            raise RuntimeError("Train() or init_model() first")
+        self._ensure_data()
+        N.check(N.lib().mml_bmf_iterate(self._h, float(np.float32(self.current_learnrate)), None))
+        self._host = None
+        self.current_learnrate = float(np.float32(np.float32(self.current_learnrate) *
+                                                  np.float32(self.Decay)))
+
+    def last_epoch_ms(self) -> float:
+        out = np.zeros(2, np.float32)
+        N.check(N.lib().mml_bmf_last_timing(self._h, N.ptr(out, N._f32p)))
+        return float(out[0])
+
+    def get_model(self):
+        if self._host is None:
+            k = int(self.NumFactors)
+            nu, ni = self.MaxUserID + 1, self.MaxItemID + 1
+            U = np.empty((nu, k), np.float32)
+            V = np.empty((ni, k), np.float32)
+            N.check(N.lib().mml_bmf_get_model(self._h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
+                                              None, None))
+            self._host = dict(U=U, V=V)
+        return self._host
+
+    @property
+    def user_factors(self):
+        return self.get_model()["U"]
+
+    @property
+    def item_factors(self):
+        return self.get_model()["V"]
+
+    def save_model(self, path: str):
+        """SaveModel (:370-378): global bias, user factors, item factors."""
+        from .model_io import ModelWriter
+        m = self.get_model()
+        with ModelWriter(path, self.TYPE_NAME) as w:
+            w.write_float(self.global_bias)
+            w.write_matrix(m["U"])
+            w.write_matrix(m["V"])
+
+    def load_model(self, path: str):
+        """LoadModel (:381-408); min/max rating stay those of the current Ratings."""
+        from .model_io import ModelReader
+        with ModelReader(path, self.TYPE_NAME) as r:
+            gb = r.read_float()
+            U, V = r.read_matrix(), r.read_matrix()
+        if U.shape[1] != V.shape[1]:
+            raise IOError(f"Number of user and item factors must match: {U.shape[1]} != "
+                          f"{V.shape[1]}")
+        self.MaxUserID, self.MaxItemID = U.shape[0] - 1, V.shape[0] - 1
+        if int(self.NumFactors) != U.shape[1]:
+            print(f"Set NumFactors to {U.shape[1]}", file=sys.stderr)
+            self.NumFactors = U.shape[1]
+        self.global_bias = float(gb)
+        self._create_handle(U.shape[0], V.shape[0])
+        self._host = dict(U=U, V=V)
+        self._upload_model(self.global_bias)
+        self._host = None
+
+    def predict(self, users, items) -> np.ndarray:
+        """Predict(int,int), batched on the GPU."""
+        u, i = N.i32(np.atleast_1d(users)), N.i32(np.atleast_1d(items))
+        out = np.empty(len(u), np.float32)
+        N.check(N.lib().mml_bmf_predict(self._h, N.ptr(u, N._i32p), N.ptr(i, N._i32p), len(u),
+                                        N.ptr(out, N._f32p)))
+        return out
+
+    def evaluate(self, test: Ratings) -> dict:
+        """Eval.Ratings.Evaluate (Eval/Ratings.cs:96-139) on the GPU -> RMSE, MAE, NMAE."""
+        out = np.zeros(2, np.float32)
+        N.check(N.lib().mml_bmf_evaluate(self._h, N.ptr(test.users, N._i32p),
+                                         N.ptr(test.items, N._i32p), N.ptr(test.values, N._f32p),
+                                         test.count, N.ptr(out, N._f32p)))
+        rmse, mae = float(out[0]), float(out[1])
+        nmae = float(np.float32(np.float32(mae) / np.float32(self.max_rating - self.min_rating)))
+        return {"RMSE": rmse, "MAE": mae, "NMAE": nmae}
+
+    def _release(self):
+        if self._h is not None:
+            N.lib().mml_bmf_destroy(self._h)
+            self._h = None
+        if self._ctx is not None:
+            self._ctx.close()
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+    def __str__(self):
+        """ToString() (:411-417)."""
+        return ("{} num_factors={} regularization={} learn_rate={} learn_rate_decay={} "
+                "num_iter={}").format(type(self).__name__, self.NumFactors, _g(self.Regularization),
+                                      _g(self.LearnRate), _g(self.Decay), self.NumIter)
+
+
+class BiasedMatrixFactorization(MatrixFactorization):
     PROPERTIES = {
         "BiasLearnRate": "float", "BiasReg": "float", "BoldDriver": "bool", "Decay": "float",
         "Device": "int", "FrequencyRegularization": "bool", "InitMean": "double",
@@ -83,20 +302,6 @@ class BiasedMatrixFactorization(Recommender):
         self.RegU = v
         self.RegI = v
 
-    # ------------------------------------------------------------------ data
-    @property
-    def ratings(self) -> Ratings:
-        return self._ratings
-
-    @ratings.setter
-    def ratings(self, r: Ratings):
-        """RatingPredictor.Ratings setter (RatingPrediction/RatingPredictor.cs:39-49)."""
-        self._ratings = r
-        self.MaxUserID = r.max_user_id
-        self.MaxItemID = r.max_item_id
-        self.min_rating = r.scale_min
-        self.max_rating = r.scale_max
-
     def schedule(self) -> str:
         if self.Schedule != "auto":
             if self.Schedule not in _SCHED:
@@ -140,15 +345,7 @@ class BiasedMatrixFactorization(Recommender):
             self._last_loss = self.compute_objective()
         self._upload_model(0.0)
 
-    def _create_handle(self, nu, ni):
-        self._release()
-        self._ctx = N.Context(self.Device)
-        h = N._vp()
-        N.check(N.lib().mml_bmf_create(self._ctx.handle, N.ctypes.byref(self._params()), nu, ni,
-                                       N.ctypes.byref(h)))
-        self._h = h
-        self._order_uploaded = False
-
+    MODEL = N.MF_BIASED
     TYPE_NAME = "MyMediaLite.RatingPrediction.BiasedMatrixFactorization"
 
     def save_model(self, path: str):
@@ -293,11 +490,6 @@ class BiasedMatrixFactorization(Recommender):
         self.current_learnrate = float(np.float32(np.float32(self.current_learnrate) *
                                                   np.float32(self.Decay)))
 
-    def last_epoch_ms(self) -> float:
-        out = np.zeros(2, np.float32)
-        N.check(N.lib().mml_bmf_last_timing(self._h, N.ptr(out, N._f32p)))
-        return float(out[0])
-
     # ------------------------------------------------------------------ model access
     def get_model(self):
         if self._host is None:
@@ -313,53 +505,12 @@ class BiasedMatrixFactorization(Recommender):
         return self._host
 
     @property
-    def user_factors(self):
-        return self.get_model()["U"]
-
-    @property
-    def item_factors(self):
-        return self.get_model()["V"]
-
-    @property
     def user_bias(self):
         return self.get_model()["bu"]
 
     @property
     def item_bias(self):
         return self.get_model()["bi"]
-
-    def predict(self, users, items) -> np.ndarray:
-        """Predict(int,int) (:313-325), batched on the GPU."""
-        u, i = N.i32(np.atleast_1d(users)), N.i32(np.atleast_1d(items))
-        out = np.empty(len(u), np.float32)
-        N.check(N.lib().mml_bmf_predict(self._h, N.ptr(u, N._i32p), N.ptr(i, N._i32p), len(u),
-                                        N.ptr(out, N._f32p)))
-        return out
-
-    def evaluate(self, test: Ratings) -> dict:
-        """Eval.Ratings.Evaluate (Eval/Ratings.cs:96-139) on the GPU -> RMSE, MAE, NMAE."""
-        out = np.zeros(2, np.float32)
-        N.check(N.lib().mml_bmf_evaluate(self._h, N.ptr(test.users, N._i32p),
-                                         N.ptr(test.items, N._i32p), N.ptr(test.values, N._f32p),
-                                         test.count, N.ptr(out, N._f32p)))
-        rmse, mae = float(out[0]), float(out[1])
-        nmae = float(np.float32(np.float32(mae) / np.float32(self.max_rating - self.min_rating)))
-        return {"RMSE": rmse, "MAE": mae, "NMAE": nmae}
-
-    # ------------------------------------------------------------------ misc
-    def _release(self):
-        if self._h is not None:
-            N.lib().mml_bmf_destroy(self._h)
-            self._h = None
-        if self._ctx is not None:
-            self._ctx.close()
-            self._ctx = None
-
-    def __del__(self):
-        try:
-            self._release()
-        except Exception:
-            pass
 
     def __str__(self):
         """ToString() (:554-561)."""

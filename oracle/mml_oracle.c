@@ -295,6 +295,57 @@ void ora_bmf_objective(const int32_t* users, const int32_t* items, const float* 
     out[1] = complexity;
 }
 
+/* ----------------------------------------------------------------------------------------
+ * MatrixFactorization (RatingPrediction/MatrixFactorization.cs): the plain model, no biases
+ * ---------------------------------------------------------------------------------------- */
+
+/* MatrixFactorization.Iterate(IList<int>,bool,bool), :166-196, with Predict(u, i, false) :205-217:
+ * err = r - (global_bias + RowScalarProduct) in float; delta = err * i_f - Regularization * u_f
+ * evaluated in float (all operands are float in C#) and widened to double; Inc adds
+ * (float)(current_learnrate * delta).  u_f and i_f are read before either row is written. */
+void ora_mf_iterate(int k, float global_bias, float learn_rate, float regularization,
+                    int update_user, int update_item, const int32_t* users, const int32_t* items,
+                    const float* values, const int32_t* idx, int64_t n_idx, float* U, float* V) {
+    for (int64_t n = 0; n < n_idx; n++) {
+        const int32_t index = idx[n];
+        float* Uu = U + (int64_t)users[index] * k;
+        float* Vi = V + (int64_t)items[index] * k;
+        float dot = 0.0f;
+        for (int c = 0; c < k; c++) dot += Uu[c] * Vi[c];
+        const float err = values[index] - (global_bias + dot);
+        for (int f = 0; f < k; f++) {
+            const float u_f = Uu[f];
+            const float i_f = Vi[f];
+            if (update_user) {
+                const double delta_u = (double)(err * i_f - regularization * u_f);
+                Uu[f] += (float)((double)learn_rate * delta_u);
+            }
+            if (update_item) {
+                const double delta_i = (double)(err * u_f - regularization * i_f);
+                Vi[f] += (float)((double)learn_rate * delta_i);
+            }
+        }
+    }
+}
+
+/* MatrixFactorization.Predict(int,int), :251-258 (+ Predict(u, i, true) :205-217): global_bias for
+ * ids beyond the model, else global_bias + RowScalarProduct clipped to [MinRating, MaxRating]. */
+void ora_mf_predict(const int32_t* users, const int32_t* items, int64_t n, int32_t n_users,
+                    int32_t n_items, int k, const float* U, const float* V, float global_bias,
+                    float min_rating, float max_rating, float* out) {
+    for (int64_t x = 0; x < n; x++) {
+        const int32_t u = users[x], i = items[x];
+        if (u >= n_users || i >= n_items) {
+            out[x] = global_bias;
+            continue;
+        }
+        float r = global_bias + ora_row_scalar_product(U, u, V, i, k);
+        if (r > max_rating) r = max_rating;
+        if (r < min_rating) r = min_rating;
+        out[x] = r;
+    }
+}
+
 /* MultiCore.PartitionUsersAndItems (MultiCore.cs:43-73).  Produces blocks as a CSR over
  * block id b = ug * G + ig: offsets[G*G+1], indices[n].  Returns G (clipped). */
 int32_t ora_partition_users_and_items(ora_rng* r, const int32_t* users, const int32_t* items,

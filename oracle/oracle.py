@@ -10,6 +10,8 @@ tests; the end-to-end trajectory is not runnable against the reference here (C#,
 Drivers below mirror the reference's control flow:
   * ``bmf_train``   -- BiasedMatrixFactorization.Train/Iterate
                        (src/MyMediaLite/RatingPrediction/BiasedMatrixFactorization.cs:173-244)
+  * ``mf_train``    -- MatrixFactorization.Train/Iterate
+                       (src/MyMediaLite/RatingPrediction/MatrixFactorization.cs:99-196)
   * ``bpr_train``   -- BPRMF.Train/Iterate (src/MyMediaLite/ItemRecommendation/BPRMF.cs:129-226)
   * ``wrmf_train``  -- MF.Train + WRMF.Iterate (ItemRecommendation/MF.cs:51-67, WRMF.cs:68-92)
 """
@@ -63,6 +65,12 @@ def lib():
         L.ora_bmf_params_sizeof.restype = ctypes.c_size_t
         L.ora_bmf_iterate.argtypes = [ctypes.c_void_p, _i32p, _i32p, _f32p, _i32p, ctypes.c_int64,
                                       _f32p, _f32p, _f32p, _f32p, _i32p, _i32p]
+        L.ora_mf_iterate.argtypes = [ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                     ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f32p, _i32p,
+                                     ctypes.c_int64, _f32p, _f32p]
+        L.ora_mf_predict.argtypes = [_i32p, _i32p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.c_int, _f32p, _f32p, ctypes.c_float, ctypes.c_float,
+                                     ctypes.c_float, _f32p]
         L.ora_bmf_predict.argtypes = [_i32p, _i32p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                       ctypes.c_int, _f32p, _f32p, _f32p, _f32p, ctypes.c_float,
                                       ctypes.c_float, ctypes.c_float, _f32p]
@@ -314,6 +322,52 @@ def bmf_train(users, items, values, n_users, n_items, min_rating, max_rating, *,
                  random_index=random_index, blocks=blocks, subepochs=subepochs, lrs=lrs,
                  current_learnrate=lr, rng=rng, objectives=objectives)
     return state
+
+
+def mf_iterate(users, items, values, indices, U, V, *, gb, lr, reg, update_user=True,
+               update_item=True):
+    """MatrixFactorization.Iterate(IList<int>,bool,bool) :166-196 -- in place."""
+    idx = i32(indices)
+    lib().ora_mf_iterate(U.shape[1], float(gb), float(lr), float(reg), int(update_user),
+                         int(update_item), _p(users, _i32p), _p(items, _i32p), _p(values, _f32p),
+                         _p(idx, _i32p), idx.size, _p(U, _f32p), _p(V, _f32p))
+
+
+def mf_train(users, items, values, n_users, n_items, *, seed=1, k=10, learn_rate=0.01, decay=1.0,
+             regularization=0.015, num_iter=30, init_mean=0.0, init_stddev=0.1, rng=None,
+             callback=None):
+    """MatrixFactorization.Train() (MatrixFactorization.cs:119-126): InitModel (:99-116, U fully
+    then V fully), global_bias = Ratings.Average (Data/Ratings.cs:76-84, float), then NumIter x
+    Iterate(RandomIndex) (LearnFactors :199-203), each followed by UpdateLearnRate (:129-132)."""
+    users, items, values = i32(users), i32(items), f32(values)
+    rng = rng if rng is not None else Rng(seed)
+    U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
+    V = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
+    U[np.bincount(users, minlength=n_users) == 0] = 0
+    V[np.bincount(items, minlength=n_items) == 0] = 0
+    state = dict(U=U, V=V, init_U=U.copy(), init_V=V.copy())
+    lr = np.float32(learn_rate)
+    s = ratings_average_exact(values) if len(values) <= 200000 else float(
+        np.sum(values, dtype=np.float64))
+    gb = np.float32(np.float32(s) / np.float32(len(values)))
+    random_index = rng.shuffle(np.arange(len(users), dtype=np.int32))
+    for epoch in range(num_iter):
+        mf_iterate(users, items, values, random_index, U, V, gb=gb, lr=lr,
+                   reg=np.float32(regularization))
+        lr = np.float32(lr * np.float32(decay))
+        if callback is not None:
+            callback(epoch, state)
+    state.update(global_bias=gb, random_index=random_index, current_learnrate=lr, rng=rng)
+    return state
+
+
+def mf_predict(users, items, U, V, gb, min_rating, max_rating):
+    users, items = i32(users), i32(items)
+    out = np.empty(len(users), np.float32)
+    lib().ora_mf_predict(_p(users, _i32p), _p(items, _i32p), len(users), U.shape[0], V.shape[0],
+                         U.shape[1], _p(U, _f32p), _p(V, _f32p), float(gb), float(min_rating),
+                         float(max_rating), _p(out, _f32p))
+    return out
 
 
 def bmf_objective(users, items, values, U, V, bu, bi, gb, min_rating, range_, *, k, loss=0,

@@ -113,6 +113,42 @@ def case_bmf_synth_dsgd4():
     return _bmf_case(u, i, v, None, seed=9, k=8, num_iter=2, max_threads=4)
 
 
+def _mf_case(users, items, values, test, *, seed, k, num_iter, **kw):
+    nu, ni = int(users.max()) + 1, int(items.max()) + 1
+    lo, hi = float(np.unique(values)[0]), float(np.unique(values)[-1])
+    snaps = {}
+
+    def cb(epoch, st):
+        snaps[f"U{epoch + 1}"] = st["U"].copy()
+        snaps[f"V{epoch + 1}"] = st["V"].copy()
+
+    st = O.mf_train(users, items, values, nu, ni, seed=seed, k=k, num_iter=num_iter, callback=cb,
+                    **kw)
+    out = dict(users=users, items=items, values=values, init_U=st["init_U"],
+               init_V=st["init_V"], global_bias=np.float32(st["global_bias"]),
+               lr_final=np.float32(st["current_learnrate"]), random_index=st["random_index"],
+               **snaps)
+    tu, ti, tv = test
+    p = O.mf_predict(tu, ti, st["U"], st["V"], st["global_bias"], lo, hi)
+    out["test_pred"] = p
+    out["test_rmse_mae"] = np.array(O.rating_eval(p, tv), np.float32)
+    return out
+
+
+def case_mf_example_k3():
+    """MatrixFactorization on the reference's toy fixture, learn-rate decay 0.5."""
+    return _mf_case(*load_example("example.train"), load_example("example.test"), seed=1, k=3,
+                    num_iter=3, decay=0.5)
+
+
+def case_mf_synth_k10():
+    u, i, v = synth_ratings(13, 60, 40, 2000)
+    tu = np.concatenate([u[:150], np.array([60, 0], np.int32)])  # + an unknown user and item
+    ti = np.concatenate([i[:150], np.array([0, 40], np.int32)])
+    tv = np.concatenate([v[:150], np.array([3, 3], np.float32)])
+    return _mf_case(u, i, v, (tu, ti, tv), seed=6, k=10, num_iter=4, learn_rate=0.02)
+
+
 def case_bpr_small():
     u, i = synth_feedback(21, 30, 20, 8)
     nu, ni = int(u.max()) + 1, int(i.max()) + 1
@@ -135,6 +171,8 @@ CASES = {
     "bmf_example_k10_logistic": case_bmf_example_k10_logistic,
     "bmf_synth_freq": case_bmf_synth_freq,
     "bmf_synth_dsgd4": case_bmf_synth_dsgd4,
+    "mf_example_k3": case_mf_example_k3,
+    "mf_synth_k10": case_mf_synth_k10,
     "bpr_small": case_bpr_small,
     "wrmf_small": case_wrmf_small,
 }

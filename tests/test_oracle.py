@@ -154,3 +154,23 @@ def test_wrmf_oracle_row_solve_is_least_squares():
     b = 2.0 * Hd[cols].sum(0)
     np.testing.assert_allclose(W[0], np.linalg.solve(A, b), rtol=1e-5, atol=1e-6)
     assert np.all(W[1] == 0)
+
+
+def test_mf_learn_rate_decay():
+    # MatrixFactorizationTest.TestDefaultBehaviorIsNoDecay / TestDecay (:40-61) on the oracle
+    u, i, v = _tiny_ratings()
+    st = O.mf_train(u, i, v, 1, 1, seed=1, learn_rate=1.1, num_iter=10)
+    assert st["current_learnrate"] == np.float32(1.1)
+    st = O.mf_train(u, i, v, 1, 1, seed=1, learn_rate=1.0, decay=0.5, num_iter=1)
+    assert st["current_learnrate"] == np.float32(0.5)
+    st = O.mf_train(u, i, v, 1, 1, seed=1, learn_rate=1.0, decay=0.5, num_iter=2)
+    assert st["current_learnrate"] == np.float32(0.25)
+
+
+def test_mf_oracle_predict_bounds_and_unknown_ids():
+    # Predict(int,int) (MatrixFactorization.cs:251-258): global bias for unknown ids, else clipped
+    U = np.array([[3.0, 0.0], [0.0, -3.0]], np.float32)
+    V = np.array([[1.0, 1.0], [0.5, 0.5]], np.float32)
+    out = O.mf_predict(np.array([0, 1, 1, 2, 0], np.int32), np.array([0, 0, 1, 0, 7], np.int32),
+                       U, V, 2.5, 1.0, 5.0)
+    np.testing.assert_array_equal(out, np.float32([5.0, 1.0, 1.0, 2.5, 2.5]))
