@@ -190,8 +190,23 @@ mml_status mml_bmf_allreduce_items(mml_bmf* h);
 /* ------------------------------------------------------------------ BPRMF */
 enum {
     MML_BPR_SAMPLER_UNIFORM_USER = 0, /* default: IterateWithoutReplacementUniformUser (BPRMF.cs:216-226) */
-    MML_BPR_SAMPLER_UNIFORM_PAIR = 1  /* IterateWithoutReplacementUniformPair over the visit order
+    MML_BPR_SAMPLER_UNIFORM_PAIR = 1, /* IterateWithoutReplacementUniformPair over the visit order
                                          (:248-268; MultiCoreBPRMF's sampler, MultiCoreBPRMF.cs:49-63) */
+    MML_BPR_SAMPLER_WEIGHTED = 2      /* WeightedBPRMF.SampleTriple (WeightedBPRMF.cs:55-67): (u, i) a
+                                         uniform event, j the item of a uniform event, not in S_u */
+};
+/* How an epoch's sampled triples are applied (ABI 2) */
+enum {
+    MML_BPR_SCHEDULE_AUTO = 0,    /* ORDERED for epochs under 262,144 samples, else HOGWILD */
+    MML_BPR_SCHEDULE_HOGWILD = 1, /* lock-free: thousands of wavefronts, LPR lanes per triple */
+    MML_BPR_SCHEDULE_ORDERED = 2  /* one wavefront applies the triples in sample order, exactly as
+                                     the reference's loop (mml_bpr_apply_triples' kernel) */
+};
+/* UpdateFactors of the model family (ABI 2) */
+enum {
+    MML_BPR_MODEL_BPR = 0,        /* BPRMF.UpdateFactors (BPRMF.cs:330-374) */
+    MML_BPR_MODEL_SOFT_MARGIN = 1 /* SoftMarginRankingMF.UpdateFactors (SoftMarginRankingMF.cs:66-113):
+                                     hinge loss, no update when x_uij > 0 */
 };
 
 typedef struct {
@@ -203,6 +218,8 @@ typedef struct {
     float reg_i;         /* RegI (:94) */
     float reg_j;         /* RegJ (:97) */
     float bias_reg;      /* BiasReg (:85) */
+    int32_t model;       /* MML_BPR_MODEL_* (ABI 2) */
+    int32_t schedule;    /* MML_BPR_SCHEDULE_* (ABI 2) */
 } mml_bpr_params;
 
 typedef struct mml_bpr mml_bpr;
@@ -231,6 +248,11 @@ mml_status mml_bpr_init_model(mml_bpr* h, uint64_t seed, double mean, double std
 /* One epoch = BPRMF.Iterate() (:160-178): Feedback.Count sampled triples, each followed by
  * UpdateFactors (:330-374).  seed keys the counter-based sampler (e.g. drawn from the host RNG). */
 mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed);
+/* UpdateFactors(u[x], i[x], j[x], true, true, UpdateJ) for x = 0 .. n-1 strictly in order, with
+ * the reference's arithmetic and summation order (bit-faithful to the managed loop): the exact
+ * path for a host that draws its own triples (e.g. the C# SampleTriple on System.Random). */
+mml_status mml_bpr_apply_triples(mml_bpr* h, const int32_t* users, const int32_t* items,
+                                 const int32_t* other_items, int64_t n);
 /* BPRMF.Predict (:425-431), batched: float.MinValue for ids beyond the model. */
 mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t n,
                            float* out);

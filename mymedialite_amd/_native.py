@@ -50,10 +50,13 @@ class BprParams(ctypes.Structure):
     _fields_ = [("num_factors", ctypes.c_int32), ("sampler", ctypes.c_int32),
                 ("update_j", ctypes.c_int32), ("learn_rate", ctypes.c_float),
                 ("reg_u", ctypes.c_float), ("reg_i", ctypes.c_float), ("reg_j", ctypes.c_float),
-                ("bias_reg", ctypes.c_float)]
+                ("bias_reg", ctypes.c_float), ("model", ctypes.c_int32),
+                ("schedule", ctypes.c_int32)]
 
 
-BPR_SAMPLER_UNIFORM_USER, BPR_SAMPLER_UNIFORM_PAIR = 0, 1
+BPR_SAMPLER_UNIFORM_USER, BPR_SAMPLER_UNIFORM_PAIR, BPR_SAMPLER_WEIGHTED = 0, 1, 2
+BPR_MODEL_BPR, BPR_MODEL_SOFT_MARGIN = 0, 1
+BPR_SCHEDULE_AUTO, BPR_SCHEDULE_HOGWILD, BPR_SCHEDULE_ORDERED = 0, 1, 2
 
 
 class WrmfParams(ctypes.Structure):
@@ -114,6 +117,7 @@ SIGNATURES = {
     "mml_bpr_init_model": (_st, [_vp, ctypes.c_uint64, ctypes.c_double, ctypes.c_double]),
     "mml_bpr_iterate": (_st, [_vp, ctypes.c_uint64]),
     "mml_bpr_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
+    "mml_bpr_apply_triples": (_st, [_vp, _i32p, _i32p, _i32p, ctypes.c_int64]),
     "mml_bpr_last_timing": (_st, [_vp, _f32p]),
     "mml_bpr_auc": (_st, [_vp, _i32p, ctypes.c_int32, _i32p, ctypes.c_int32, _i64p, _i32p,
                           _f64p]),

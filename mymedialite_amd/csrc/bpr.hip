@@ -37,6 +37,40 @@ struct BprScalars {
     int32_t update_j;
 };
 
+// UpdateFactors after x_uij: BPRMF.UpdateFactors (BPRMF.cs:330-374) or, SOFT,
+// SoftMarginRankingMF.UpdateFactors (SoftMarginRankingMF.cs:66-113), whose update expressions are
+// float arithmetic (float operands, the int literal 1) widened to double for the learn-rate step
+// and which skips the triple when x_uij > 0.
+template <bool SOFT>
+struct TripleStep {
+    double e = 0.0, lr;
+    bool skip = false;
+    __device__ __forceinline__ TripleStep(const BprScalars& s, double x_uij) : lr(s.lr) {
+        if constexpr (SOFT) skip = x_uij > 0;
+        else e = 1.0 / (1.0 + exp(x_uij));
+    }
+    __device__ __forceinline__ float bias_i(const BprScalars& s, float bi) const {
+        if constexpr (SOFT) return bi + (float)(lr * (double)(1.0f - s.bias_reg * bi));
+        else return bi + (float)(lr * (e - (double)(s.bias_reg * bi)));
+    }
+    __device__ __forceinline__ float bias_j(const BprScalars& s, float bj) const {
+        if constexpr (SOFT) return bj + (float)(lr * (double)(-1.0f - s.bias_reg * bj));
+        else return bj + (float)(lr * (-e - (double)(s.bias_reg * bj)));
+    }
+    __device__ __forceinline__ float u(const BprScalars& s, float wf, float hif, float hjf) const {
+        if constexpr (SOFT) return (float)((double)wf + lr * (double)(hif - hjf - s.reg_u * wf));
+        else return (float)((double)wf + lr * ((double)(hif - hjf) * e - (double)(s.reg_u * wf)));
+    }
+    __device__ __forceinline__ float i(const BprScalars& s, float wf, float hif) const {
+        if constexpr (SOFT) return (float)((double)hif + lr * (double)(wf - s.reg_i * hif));
+        else return (float)((double)hif + lr * ((double)wf * e - (double)(s.reg_i * hif)));
+    }
+    __device__ __forceinline__ float j(const BprScalars& s, float wf, float hjf) const {
+        if constexpr (SOFT) return (float)((double)hjf + lr * (double)(-wf - s.reg_j * hjf));
+        else return (float)((double)hjf + lr * ((double)(-wf) * e - (double)(s.reg_j * hjf)));
+    }
+};
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -180,29 +214,52 @@ __device__ __forceinline__ bool row_has(const int32_t* __restrict__ cols, int64_
     return lo < re && cols[lo] == j;
 }
 
-// eligible == nullptr: every user is eligible (u = the draw itself, no gather)
-template <bool PAIR>
+// SAMPLER: MML_BPR_SAMPLER_*.  eligible == nullptr: every user is eligible (u = the draw itself,
+// no gather).  WEIGHTED (WeightedBPRMF.SampleTriple): (u, i) = event draw 0, j = the item of event
+// draw d until j is not in S_u -- capped at kMaxWeightedDraws, after which the sample is flagged
+// (*fail) instead of looping for ever on a user whose items carry all the event mass.
+constexpr uint32_t kMaxWeightedDraws = 1u << 16;
+// MML_BPR_SCHEDULE_AUTO applies epochs below this many samples in order (one wavefront)
+constexpr int64_t kAutoOrderedBelow = 16 * 16384;
+template <int SAMPLER>
 __global__ __launch_bounds__(256) void bpr_sample_kernel(
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols,
     const int32_t* __restrict__ eligible, int32_t n_eligible, const int32_t* __restrict__ ev_u,
     const int32_t* __restrict__ ev_i, int64_t n_samples, int32_t n_items, uint64_t seed,
-    int32_t* __restrict__ tu, int32_t* __restrict__ ti, int32_t* __restrict__ tj) {
+    int32_t* __restrict__ tu, int32_t* __restrict__ ti, int32_t* __restrict__ tj,
+    int32_t* __restrict__ fail) {
     for (int64_t smp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; smp < n_samples;
          smp += (int64_t)gridDim.x * blockDim.x) {
-        int32_t u, i = 0;
-        if constexpr (PAIR) {
+        int32_t u, i = 0, j = 0;
+        if constexpr (SAMPLER == MML_BPR_SAMPLER_UNIFORM_PAIR) {
             u = ev_u[smp];
             i = ev_i[smp];
+        } else if constexpr (SAMPLER == MML_BPR_SAMPLER_WEIGHTED) {
+            const uint32_t e = draw(seed, smp, 0, (uint32_t)n_samples);
+            u = ev_u[e];
+            i = ev_i[e];
         } else {
             const uint32_t du = draw(seed, smp, 0, (uint32_t)n_eligible);
             u = eligible ? eligible[du] : (int32_t)du;
         }
         const int64_t rb = off[u], re = off[u + 1];
-        if constexpr (!PAIR) i = cols[rb + draw(seed, smp, 1, (uint32_t)(re - rb))];
-        int32_t j;
-        for (uint32_t d = 2;; ++d) {
-            j = (int32_t)draw(seed, smp, d, (uint32_t)n_items);
-            if (!row_has(cols, rb, re, j)) break;
+        if constexpr (SAMPLER == MML_BPR_SAMPLER_UNIFORM_USER)
+            i = cols[rb + draw(seed, smp, 1, (uint32_t)(re - rb))];
+        if constexpr (SAMPLER == MML_BPR_SAMPLER_WEIGHTED) {
+            uint32_t d = 1;
+            for (; d <= kMaxWeightedDraws; ++d) {
+                j = ev_i[draw(seed, smp, d, (uint32_t)n_samples)];
+                if (!row_has(cols, rb, re, j)) break;
+            }
+            if (d > kMaxWeightedDraws) {
+                atomicOr(fail, 1);
+                j = i;
+            }
+        } else {
+            for (uint32_t d = 2;; ++d) {
+                j = (int32_t)draw(seed, smp, d, (uint32_t)n_items);
+                if (!row_has(cols, rb, re, j)) break;
+            }
         }
         tu[smp] = u;
         ti[smp] = i;
@@ -228,7 +285,7 @@ __device__ __forceinline__ int32_t bpr_group_fetch(int32_t v, int base, int lane
     }
 }
 
-template <int LPR>
+template <int LPR, bool SOFT>
 __global__ __launch_bounds__(256) void bpr_update_kernel(
     const int32_t* __restrict__ tu, const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
     int64_t n_samples, int64_t chunk, float* U, float* V, float* bias, int32_t ld4, BprScalars s) {
@@ -266,30 +323,72 @@ __global__ __launch_bounds__(256) void bpr_update_kernel(
             part += (double)(w.w * (hi.w - hj.w));
 #pragma unroll
             for (int o = LPR / 2; o >= 1; o >>= 1) part += __shfl_xor(part, o);
-            const double x_uij = (double)(bi - bj) + part;
-            const double e = 1.0 / (1.0 + exp(x_uij));
-            if (q == 0) {
-                bias[i] = bi + (float)((double)s.lr * (e - (double)(s.bias_reg * bi)));
-                if (s.update_j)
-                    bias[j] = bj + (float)((double)s.lr * (-e - (double)(s.bias_reg * bj)));
+            // every lane of the group holds the bit-identical sum: `skip` is group-uniform
+            const TripleStep<SOFT> t(s, (double)(bi - bj) + part);
+            if (t.skip) continue;
+            if (q == 0) {  // i == j: the reference re-reads item_bias[j] after writing [i]
+                const float nbi = t.bias_i(s, bi);
+                bias[i] = nbi;
+                if (s.update_j) bias[j] = t.bias_j(s, i == j ? nbi : bj);
             }
-            const double lr = s.lr;
-            auto upd_u = [&](float wf, float hif, float hjf) {
-                return (float)((double)wf + lr * ((double)(hif - hjf) * e - (double)(s.reg_u * wf)));
-            };
-            auto upd_i = [&](float wf, float hif) {
-                return (float)((double)hif + lr * ((double)wf * e - (double)(s.reg_i * hif)));
-            };
-            auto upd_j = [&](float wf, float hjf) {
-                return (float)((double)hjf + lr * ((double)(-wf) * e - (double)(s.reg_j * hjf)));
-            };
-            U4[ou] = make_float4(upd_u(w.x, hi.x, hj.x), upd_u(w.y, hi.y, hj.y),
-                                 upd_u(w.z, hi.z, hj.z), upd_u(w.w, hi.w, hj.w));
-            V4[oi] = make_float4(upd_i(w.x, hi.x), upd_i(w.y, hi.y), upd_i(w.z, hi.z),
-                                 upd_i(w.w, hi.w));
+            U4[ou] = make_float4(t.u(s, w.x, hi.x, hj.x), t.u(s, w.y, hi.y, hj.y),
+                                 t.u(s, w.z, hi.z, hj.z), t.u(s, w.w, hi.w, hj.w));
+            V4[oi] = make_float4(t.i(s, w.x, hi.x), t.i(s, w.y, hi.y), t.i(s, w.z, hi.z),
+                                 t.i(s, w.w, hi.w));
             if (s.update_j)
-                V4[oj] = make_float4(upd_j(w.x, hj.x), upd_j(w.y, hj.y), upd_j(w.z, hj.z),
-                                     upd_j(w.w, hj.w));
+                V4[oj] = make_float4(t.j(s, w.x, hj.x), t.j(s, w.y, hj.y), t.j(s, w.z, hj.z),
+                                     t.j(s, w.w, hj.w));
+        }
+    }
+}
+
+// mml_bpr_apply_triples: UpdateFactors for a given triple list strictly in order -- one
+// wavefront, lane f owns factors f, f + 64, ... (KM per lane); x_uij summed left to right in
+// double through v_readlane exactly as RowScalarProductWithRowDifference
+// (DataType/MatrixExtensions.cs:276-298), so the result is bit-faithful to the managed loop.
+template <bool SOFT, int KM>
+__global__ __launch_bounds__(64) void bpr_apply_ordered_kernel(
+    const int32_t* __restrict__ tu, const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
+    int64_t n, float* U, float* V, float* bias, int32_t k, int32_t ld, BprScalars s) {
+    const int lane = threadIdx.x;
+    for (int64_t x = 0; x < n; ++x) {
+        const int32_t u = tu[x], i = ti[x], j = tj[x];
+        float* Wu = U + (int64_t)u * ld;
+        float* Hi = V + (int64_t)i * ld;
+        float* Hj = V + (int64_t)j * ld;
+        float w[KM], hi[KM], hj[KM], prod[KM];
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int f = lane + 64 * m;
+            w[m] = f < k ? Wu[f] : 0.0f;
+            hi[m] = f < k ? Hi[f] : 0.0f;
+            hj[m] = f < k ? Hj[f] : 0.0f;
+            prod[m] = w[m] * (hi[m] - hj[m]);
+        }
+        double dot = 0.0;
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int lim = min(64, k - 64 * m);
+            const int bits = __float_as_int(prod[m]);
+            for (int l = 0; l < lim; ++l)
+                dot += (double)__int_as_float(__builtin_amdgcn_readlane(bits, l));
+        }
+        const float bi = bias[i], bj = bias[j];
+        const TripleStep<SOFT> t(s, (double)(bi - bj) + dot);
+        if (t.skip) continue;
+        if (lane == 0) {  // i == j: the reference re-reads item_bias[j] after writing [i]
+            const float nbi = t.bias_i(s, bi);
+            bias[i] = nbi;
+            if (s.update_j) bias[j] = t.bias_j(s, i == j ? nbi : bj);
+        }
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int f = lane + 64 * m;
+            if (f < k) {
+                Wu[f] = t.u(s, w[m], hi[m], hj[m]);
+                Hi[f] = t.i(s, w[m], hi[m]);
+                if (s.update_j) Hj[f] = t.j(s, w[m], hj[m]);
+            }
         }
     }
 }
@@ -337,6 +436,7 @@ struct mml_bpr {
     mml::DeviceArray<int64_t> off;
     mml::DeviceArray<int32_t> cols, eligible, ev_u, ev_i, q_u, q_i;
     mml::DeviceArray<int32_t> tri_u, tri_i, tri_j;  // the epoch's triples (two-phase epoch)
+    mml::DeviceArray<int32_t> fail;                 // WEIGHTED sampler: a sample ran out of draws
     int64_t n_events = 0, nnz = 0;
     int32_t n_eligible = 0;
     bool has_data = false, has_model = false, has_order = false;
@@ -370,8 +470,15 @@ extern "C" mml_status mml_bpr_create(mml_ctx* ctx, const mml_bpr_params* params,
         MML_REQUIRE(params->num_factors >= 1 && params->num_factors <= 256,
                     "num_factors must be in [1, 256]");
         MML_REQUIRE(params->sampler == MML_BPR_SAMPLER_UNIFORM_USER ||
-                        params->sampler == MML_BPR_SAMPLER_UNIFORM_PAIR,
+                        params->sampler == MML_BPR_SAMPLER_UNIFORM_PAIR ||
+                        params->sampler == MML_BPR_SAMPLER_WEIGHTED,
                     "unknown sampler");
+        MML_REQUIRE(params->model == MML_BPR_MODEL_BPR ||
+                        params->model == MML_BPR_MODEL_SOFT_MARGIN,
+                    "unknown model family");
+        MML_REQUIRE(params->schedule >= MML_BPR_SCHEDULE_AUTO &&
+                        params->schedule <= MML_BPR_SCHEDULE_ORDERED,
+                    "unknown schedule");
         ctx->activate();
         auto* h = new mml_bpr();
         try {
@@ -436,7 +543,7 @@ void bpr_ingest(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t 
     h->eligible.alloc(elig.size());
     MML_HIP(hipMemcpyAsync(h->eligible.get(), elig.data(), sizeof(int32_t) * elig.size(),
                            hipMemcpyHostToDevice, st));
-    if (h->p.sampler == MML_BPR_SAMPLER_UNIFORM_PAIR) {
+    if (h->p.sampler != MML_BPR_SAMPLER_UNIFORM_USER) {  // PAIR: visit order; WEIGHTED: any order
         h->ev_u.alloc(n);
         h->ev_i.alloc(n);
         bpr_gather_events_kernel<<<grid_for(n), 256, 0, st>>>(users, items, order, n,
@@ -480,8 +587,8 @@ extern "C" mml_status mml_bpr_set_data_device(mml_bpr* h, const int32_t* users,
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
         MML_REQUIRE(n >= 1 && users && items, "need >= 1 event");
-        MML_REQUIRE(!order || h->p.sampler == MML_BPR_SAMPLER_UNIFORM_PAIR,
-                    "a device order is only used by the UNIFORM_PAIR sampler");
+        MML_REQUIRE(!order || h->p.sampler != MML_BPR_SAMPLER_UNIFORM_USER,
+                    "a device order is not used by the UNIFORM_USER sampler");
         h->ctx->activate();
         h->has_data = false;
         bpr_ingest(h, users, items, n, order);
@@ -559,6 +666,46 @@ extern "C" mml_status mml_bpr_get_model(mml_bpr* h, float* U, float* V, float* i
     });
 }
 
+namespace {
+
+// one wavefront applies n triples in order (bpr_apply_ordered_kernel), k <= 256
+void launch_apply_ordered(mml_bpr* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
+                          int64_t n, const BprScalars& s, hipStream_t st) {
+    const int km = (h->k + 63) / 64;
+    const bool soft = h->p.model == MML_BPR_MODEL_SOFT_MARGIN;
+#define MML_APPLY(SOFT, KM)                                                                    \
+    bpr_apply_ordered_kernel<SOFT, KM><<<1, 64, 0, st>>>(tu, ti, tj, n, h->U.get(), h->V.get(), \
+                                                         h->bias.get(), h->k, h->ld, s)
+#define MML_APPLY_K(SOFT)                   \
+    switch (km) {                           \
+        case 1: MML_APPLY(SOFT, 1); break;  \
+        case 2: MML_APPLY(SOFT, 2); break;  \
+        case 3: MML_APPLY(SOFT, 3); break;  \
+        default: MML_APPLY(SOFT, 4); break; \
+    }
+    if (soft) {
+        MML_APPLY_K(true);
+    } else {
+        MML_APPLY_K(false);
+    }
+#undef MML_APPLY_K
+#undef MML_APPLY
+    MML_HIP(hipGetLastError());
+}
+
+BprScalars scalars_of(const mml_bpr* h) {
+    BprScalars s;
+    s.lr = h->p.learn_rate;
+    s.reg_u = h->p.reg_u;
+    s.reg_i = h->p.reg_i;
+    s.reg_j = h->p.reg_j;
+    s.bias_reg = h->p.bias_reg;
+    s.update_j = h->p.update_j;
+    return s;
+}
+
+}  // namespace
+
 extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
@@ -586,10 +733,18 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         waves = blocks * 4;
         const int64_t chunk = (n + waves - 1) / waves;
         const bool pair = h->p.sampler == MML_BPR_SAMPLER_UNIFORM_PAIR;
-        static const bool fused = [] {
+        const bool soft = h->p.model == MML_BPR_MODEL_SOFT_MARGIN;
+        const bool weighted = h->p.sampler == MML_BPR_SAMPLER_WEIGHTED;
+        static const bool fused_env = [] {
             const char* e = std::getenv("MML_BPR_FUSED");
             return e && std::atoi(e) > 0;
         }();
+        // ORDERED (or AUTO on a small epoch): the sampled triples are applied in sample order by
+        // one wavefront -- the reference's sequential loop on the device's triples
+        const bool ordered = h->p.schedule == MML_BPR_SCHEDULE_ORDERED ||
+                             (h->p.schedule == MML_BPR_SCHEDULE_AUTO && n < kAutoOrderedBelow);
+        // the fused single-kernel epoch exists for the BPRMF update with the uniform samplers
+        const bool fused = fused_env && !soft && !weighted && !ordered;
         if (!fused && n > 0 && (int64_t)h->tri_u.count < n) {
             h->tri_u.alloc(n);
             h->tri_i.alloc(n);
@@ -598,24 +753,44 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
         if (!fused && n > 0) {
             const int sgrid = (int)std::min<int64_t>(256 * 64, (n + 255) / 256);
-            if (pair)
-                bpr_sample_kernel<true><<<sgrid, 256, 0, st>>>(
-                    h->off.get(), h->cols.get(), h->eligible.get(), h->n_eligible, h->ev_u.get(),
-                    h->ev_i.get(), n, h->n_items, seed, h->tri_u.get(), h->tri_i.get(),
-                    h->tri_j.get());
+            if (weighted) {
+                h->fail.alloc(1);
+                MML_HIP(hipMemsetAsync(h->fail.get(), 0, sizeof(int32_t), st));
+            }
+#define MML_SMP(KIND, ELIG)                                                                     \
+    bpr_sample_kernel<KIND><<<sgrid, 256, 0, st>>>(                                            \
+        h->off.get(), h->cols.get(), ELIG, h->n_eligible, h->ev_u.get(), h->ev_i.get(), n,    \
+        h->n_items, seed, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), h->fail.get())
+            if (pair) MML_SMP(MML_BPR_SAMPLER_UNIFORM_PAIR, h->eligible.get());
+            else if (weighted) MML_SMP(MML_BPR_SAMPLER_WEIGHTED, nullptr);
             else
-                bpr_sample_kernel<false><<<sgrid, 256, 0, st>>>(
-                    h->off.get(), h->cols.get(),
-                    h->n_eligible == h->n_users ? nullptr : h->eligible.get(), h->n_eligible,
-                    h->ev_u.get(),
-                    h->ev_i.get(), n, h->n_items, seed, h->tri_u.get(), h->tri_i.get(),
-                    h->tri_j.get());
+                MML_SMP(MML_BPR_SAMPLER_UNIFORM_USER,
+                        h->n_eligible == h->n_users ? nullptr : h->eligible.get());
+#undef MML_SMP
             MML_HIP(hipGetLastError());
+            if (weighted) {
+                int32_t bad = 0;
+                MML_HIP(hipMemcpyAsync(&bad, h->fail.get(), sizeof(int32_t),
+                                       hipMemcpyDeviceToHost, st));
+                MML_HIP(hipStreamSynchronize(st));
+                if (bad)
+                    mml::fail(MML_ERR_STATE,
+                              "WeightedBPRMF: a user's items hold (nearly) all the event mass; no "
+                              "negative item found in 65536 draws (the reference loops for ever)");
+            }
         }
         MML_HIP(hipEventRecord(h->ctx->ev_mid, st));
+        if (ordered && n > 0)
+            launch_apply_ordered(h, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), n, s, st);
 #define MML_BPR(LPR)                                                                            \
-    if (!fused)                                                                                 \
-        bpr_update_kernel<LPR><<<(int)blocks, 256, 0, st>>>(                                  \
+    if (ordered)                                                                                \
+        ;                                                                                       \
+    else if (!fused && soft)                                                                         \
+        bpr_update_kernel<LPR, true><<<(int)blocks, 256, 0, st>>>(                            \
+            h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), n, chunk, h->U.get(), h->V.get(),   \
+            h->bias.get(), h->ld / 4, s);                                                       \
+    else if (!fused)                                                                            \
+        bpr_update_kernel<LPR, false><<<(int)blocks, 256, 0, st>>>(                           \
             h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), n, chunk, h->U.get(), h->V.get(),   \
             h->bias.get(), h->ld / 4, s);                                                       \
     else if (pair)                                                                              \
@@ -643,6 +818,34 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         MML_HIP(hipEventSynchronize(h->ctx->ev_end));
         MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));
         MML_HIP(hipEventElapsedTime(&h->last_update_ms, h->ctx->ev_mid, h->ctx->ev_end));
+    });
+}
+
+extern "C" mml_status mml_bpr_apply_triples(mml_bpr* h, const int32_t* users,
+                                             const int32_t* items, const int32_t* other_items,
+                                             int64_t n) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(n >= 0 && (n == 0 || (users && items && other_items)), "bad arguments");
+        for (int64_t x = 0; x < n; ++x)
+            MML_REQUIRE(users[x] >= 0 && users[x] < h->n_users && items[x] >= 0 &&
+                            items[x] < h->n_items && other_items[x] >= 0 &&
+                            other_items[x] < h->n_items,
+                        "triple id out of range");
+        if (n == 0) return;
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        mml::DeviceArray<int32_t> du, di, dj;
+        du.alloc(n);
+        di.alloc(n);
+        dj.alloc(n);
+        MML_HIP(hipMemcpyAsync(du.get(), users, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(di.get(), items, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(dj.get(), other_items, sizeof(int32_t) * n, hipMemcpyHostToDevice,
+                               st));
+        launch_apply_ordered(h, du.get(), di.get(), dj.get(), n, scalars_of(h), st);
+        MML_HIP(hipStreamSynchronize(st));
     });
 }
 

@@ -161,8 +161,8 @@ class BPRMF(_MFBase):
     PROPERTIES = {
         "BiasReg": "float", "Device": "int", "InitMean": "double", "InitStdDev": "double",
         "LearnRate": "float", "NumFactors": "uint", "NumIter": "uint", "RegI": "float",
-        "RegJ": "float", "RegU": "float", "UniformUserSampling": "bool", "UpdateJ": "bool",
-        "WithReplacement": "bool",
+        "RegJ": "float", "RegU": "float", "Schedule": "string", "UniformUserSampling": "bool",
+        "UpdateJ": "bool", "WithReplacement": "bool",
     }
 
     def __init__(self, **kw):
@@ -176,6 +176,9 @@ class BPRMF(_MFBase):
         self.RegI = 0.0025
         self.RegJ = 0.00025
         self.UpdateJ = True
+        # GPU: "auto" (in-order application below 262,144 samples per epoch, else Hogwild),
+        # "hogwild" or "ordered" (MML_BPR_SCHEDULE_*)
+        self.Schedule = "auto"
         for k, v in kw.items():
             setattr(self, k, v)
 
@@ -190,10 +193,7 @@ class BPRMF(_MFBase):
     def _load_device_model(self, U, V, bias):
         self._release()
         self._ctx = N.Context(self.Device)
-        f = lambda x: float(np.float32(x))
-        p = N.BprParams(int(self.NumFactors), self._sampler(), int(bool(self.UpdateJ)),
-                        f(self.LearnRate), f(self.RegU), f(self.RegI), f(self.RegJ),
-                        f(self.BiasReg))
+        p = self._params()
         h = N._vp()
         N.check(N.lib().mml_bpr_create(self._ctx.handle, ctypes.byref(p), U.shape[0], V.shape[0],
                                        ctypes.byref(h)))
@@ -201,6 +201,26 @@ class BPRMF(_MFBase):
         N.check(N.lib().mml_bpr_set_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
                                           N.ptr(bias, N._f32p)))
         self._host = dict(U=U, V=V, bias=bias)
+
+    MODEL = N.BPR_MODEL_BPR
+
+    def _params(self) -> N.BprParams:
+        f = lambda x: float(np.float32(x))
+        sched = {"auto": N.BPR_SCHEDULE_AUTO, "hogwild": N.BPR_SCHEDULE_HOGWILD,
+                 "ordered": N.BPR_SCHEDULE_ORDERED}
+        if self.Schedule not in sched:
+            raise ValueError(f"unknown Schedule '{self.Schedule}'")
+        return N.BprParams(int(self.NumFactors), self._sampler(), int(bool(self.UpdateJ)),
+                           f(self.LearnRate), f(self.RegU), f(self.RegI), f(self.RegJ),
+                           f(self.BiasReg), self.MODEL, sched[self.Schedule])
+
+    def apply_triples(self, users, items, other_items):
+        """UpdateFactors(u, i, j, true, true, UpdateJ) (:330-374) for the given triples strictly in
+        order on the GPU (bit-faithful): the exact path for triples drawn by the host."""
+        u, i, j = N.i32(users), N.i32(items), N.i32(other_items)
+        N.check(N.lib().mml_bpr_apply_triples(self._h, N.ptr(u, N._i32p), N.ptr(i, N._i32p),
+                                              N.ptr(j, N._i32p), len(u)))
+        self._host = None
 
     def _sampler(self) -> int:
         if self.WithReplacement:
@@ -215,10 +235,7 @@ class BPRMF(_MFBase):
         bias = np.zeros(self.MaxItemID + 1, np.float32)
         self._release()
         self._ctx = N.Context(self.Device)
-        f = lambda x: float(np.float32(x))
-        p = N.BprParams(int(self.NumFactors), self._sampler(), int(bool(self.UpdateJ)),
-                        f(self.LearnRate), f(self.RegU), f(self.RegI), f(self.RegJ),
-                        f(self.BiasReg))
+        p = self._params()
         h = N._vp()
         N.check(N.lib().mml_bpr_create(self._ctx.handle, ctypes.byref(p), self.MaxUserID + 1,
                                        self.MaxItemID + 1, ctypes.byref(h)))
@@ -288,11 +305,53 @@ class BPRMF(_MFBase):
     def __str__(self):
         """BPRMF.ToString() (BPRMF.cs:540-551)."""
         g = lambda x: f"{float(np.float32(x)):.7g}"
-        return (f"BPRMF num_factors={self.NumFactors} bias_reg={g(self.BiasReg)} "
+        return (f"{type(self).__name__} num_factors={self.NumFactors} bias_reg={g(self.BiasReg)} "
                 f"reg_u={g(self.RegU)} reg_i={g(self.RegI)} reg_j={g(self.RegJ)} "
                 f"num_iter={self.NumIter} LearnRate={g(self.LearnRate)} "
                 f"uniform_user_sampling={self.UniformUserSampling} "
                 f"with_replacement={self.WithReplacement} update_j={self.UpdateJ}")
+
+
+class WeightedBPRMF(BPRMF):
+    """WeightedBPRMF (ItemRecommendation/WeightedBPRMF.cs:32-77): BPR-MF with frequency-adjusted
+    sampling -- (u, i) a uniformly drawn event, j the item of another uniformly drawn event, redrawn
+    while j is in S_u (SampleTriple :55-67; MML_BPR_SAMPLER_WEIGHTED).  WithReplacement = false and
+    UniformUserSampling = true are forced in the constructor and in Train() (:35-53)."""
+    TYPE_NAME = "MyMediaLite.ItemRecommendation.WeightedBPRMF"
+
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self.WithReplacement = False
+        self.UniformUserSampling = True
+
+    def _sampler(self) -> int:
+        return N.BPR_SAMPLER_WEIGHTED
+
+    def train(self):
+        self.WithReplacement = False
+        self.UniformUserSampling = True
+        super().train()
+
+    def __str__(self):
+        """WeightedBPRMF.ToString() (:70-76)."""
+        g = lambda x: f"{float(np.float32(x)):.7g}"
+        return (f"WeightedBPRMF num_factors={self.NumFactors} bias_reg={g(self.BiasReg)} "
+                f"reg_u={g(self.RegU)} reg_i={g(self.RegI)} reg_j={g(self.RegJ)} "
+                f"num_iter={self.NumIter} learn_rate={g(self.LearnRate)}")
+
+
+class SoftMarginRankingMF(BPRMF):
+    """SoftMarginRankingMF (ItemRecommendation/SoftMarginRankingMF.cs:51-126): BPRMF's samplers
+    with a soft-margin (hinge) UpdateFactors (:66-113, MML_BPR_MODEL_SOFT_MARGIN); LearnRate
+    defaults to 0.1 (:53-56)."""
+    TYPE_NAME = "MyMediaLite.ItemRecommendation.SoftMarginRankingMF"
+    MODEL = N.BPR_MODEL_SOFT_MARGIN
+
+    def __init__(self, **kw):
+        super().__init__()
+        self.LearnRate = 0.1
+        for k, v in kw.items():
+            setattr(self, k, v)
 
 
 class WRMF(_MFBase):

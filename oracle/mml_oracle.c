@@ -391,6 +391,11 @@ typedef struct {
     int32_t update_u, update_i, update_j;
     float learn_rate, reg_u, reg_i, reg_j, bias_reg;
     int32_t max_user_id, max_item_id;
+    int32_t model;   /* 0 BPRMF, 1 SoftMarginRankingMF (UpdateFactors) */
+    int32_t sampler; /* 0 SampleTriple of BPRMF, 2 WeightedBPRMF.SampleTriple */
+    const int32_t* ev_users; /* Feedback.Users / Feedback.Items (event order), sampler 2 */
+    const int32_t* ev_items;
+    int64_t n_events;
 } ora_bpr_params;
 
 size_t ora_bpr_params_sizeof(void) { return sizeof(ora_bpr_params); }
@@ -405,9 +410,23 @@ static int ora_row_contains(const int64_t* off, const int32_t* sorted, int32_t u
     return lo < off[u + 1] && sorted[lo] == item;
 }
 
-/* SampleUser :300-310, SampleItemPair :290-296, SampleTriple :316-321 */
+/* SampleUser :300-310, SampleItemPair :290-296, SampleTriple :316-321; sampler 2:
+ * WeightedBPRMF.SampleTriple (ItemRecommendation/WeightedBPRMF.cs:55-67): (u, i) = the event at
+ * Next(Feedback.Count), j = Feedback.Items[Next(Feedback.Count)] until j is not in S_u. */
 void ora_bpr_sample_triple(ora_rng* r, const ora_bpr_params* p, const int64_t* off,
                            const int32_t* rows, const int32_t* sorted, int32_t* out) {
+    if (p->sampler == 2) {
+        const int32_t n = (int32_t)p->n_events;
+        const int32_t index = ora_rng_next(r, n);
+        const int32_t wu = p->ev_users[index], wi = p->ev_items[index];
+        int32_t wj;
+        do wj = p->ev_items[ora_rng_next(r, n)];
+        while (ora_row_contains(off, sorted, wu, wj));
+        out[0] = wu;
+        out[1] = wi;
+        out[2] = wj;
+        return;
+    }
     int32_t u;
     for (;;) {
         u = ora_rng_next(r, p->max_user_id + 1);
@@ -425,7 +444,39 @@ void ora_bpr_sample_triple(ora_rng* r, const ora_bpr_params* p, const int64_t* o
     out[2] = j;
 }
 
-/* BPRMF.UpdateFactors(u,i,j,...) :330-374 */
+/* SoftMarginRankingMF.UpdateFactors (ItemRecommendation/SoftMarginRankingMF.cs:66-113): no
+ * update when x_uij > 0; otherwise the hinge gradient -- all the update expressions are float
+ * arithmetic in C# (float operands, int literal 1) widened to double before the learn-rate step. */
+static void ora_soft_margin_update(const ora_bpr_params* p, int32_t i, int32_t j, float* w,
+                                   float* hi, float* hj, float* bias, double x_uij) {
+    if (x_uij > 0) return;
+    const double lr = (double)p->learn_rate;
+    if (p->update_i) {
+        const double bias_update = (double)(1.0f - p->bias_reg * bias[i]);
+        bias[i] += (float)(lr * bias_update);
+    }
+    if (p->update_j) {
+        const double bias_update = (double)(-1.0f - p->bias_reg * bias[j]);
+        bias[j] += (float)(lr * bias_update);
+    }
+    for (int f = 0; f < p->k; f++) {
+        const float w_uf = w[f], h_if = hi[f], h_jf = hj[f];
+        if (p->update_u) {
+            const double uf_update = (double)(h_if - h_jf - p->reg_u * w_uf);
+            w[f] = (float)((double)w_uf + lr * uf_update);
+        }
+        if (p->update_i) {
+            const double if_update = (double)(w_uf - p->reg_i * h_if);
+            hi[f] = (float)((double)h_if + lr * if_update);
+        }
+        if (p->update_j) {
+            const double jf_update = (double)(-w_uf - p->reg_j * h_jf);
+            hj[f] = (float)((double)h_jf + lr * jf_update);
+        }
+    }
+}
+
+/* BPRMF.UpdateFactors(u,i,j,...) :330-374 (model 1: SoftMarginRankingMF's override) */
 void ora_bpr_update(const ora_bpr_params* p, int32_t u, int32_t i, int32_t j, float* U, float* V,
                     float* bias) {
     const int k = p->k;
@@ -434,6 +485,10 @@ void ora_bpr_update(const ora_bpr_params* p, int32_t u, int32_t i, int32_t j, fl
     float* hj = V + (int64_t)j * k;
     double x_uij = (double)(bias[i] - bias[j]) +
                    ora_row_scalar_product_with_row_difference(U, u, V, i, V, j, k);
+    if (p->model == 1) {
+        ora_soft_margin_update(p, i, j, w, hi, hj, bias, x_uij);
+        return;
+    }
     double e = 1.0 / (1.0 + exp(x_uij));
     if (p->update_i) {
         double update = e - (double)(p->bias_reg * bias[i]);

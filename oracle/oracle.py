@@ -409,7 +409,13 @@ class _BprParams(ctypes.Structure):
                 ("update_j", ctypes.c_int32), ("learn_rate", ctypes.c_float),
                 ("reg_u", ctypes.c_float), ("reg_i", ctypes.c_float), ("reg_j", ctypes.c_float),
                 ("bias_reg", ctypes.c_float), ("max_user_id", ctypes.c_int32),
-                ("max_item_id", ctypes.c_int32)]
+                ("max_item_id", ctypes.c_int32), ("model", ctypes.c_int32),
+                ("sampler", ctypes.c_int32), ("ev_users", ctypes.c_void_p),
+                ("ev_items", ctypes.c_void_p), ("n_events", ctypes.c_int64)]
+
+
+BPR_MODEL = {"BPRMF": 0, "SoftMarginRankingMF": 1}
+BPR_SAMPLER = {"uniform_user": 0, "weighted": 2}
 
 
 def insertion_order_rows(rows_of, cols_of, n_rows):
@@ -436,8 +442,11 @@ def sorted_rows(off, cols):
 
 def bpr_train(users, items, n_users, n_items, *, seed=1, k=10, num_iter=30, learn_rate=0.05,
               reg_u=0.0025, reg_i=0.0025, reg_j=0.00025, bias_reg=0.0, update_j=True,
-              init_mean=0.0, init_stddev=0.1, rng=None, trace_epochs=0, callback=None):
-    """BPRMF.Train (:129-154) with the default IterateWithoutReplacementUniformUser (:216-226)."""
+              init_mean=0.0, init_stddev=0.1, rng=None, trace_epochs=0, callback=None,
+              model="BPRMF", sampler="uniform_user"):
+    """BPRMF.Train (:129-154) with the default IterateWithoutReplacementUniformUser (:216-226).
+    model="SoftMarginRankingMF": its UpdateFactors (SoftMarginRankingMF.cs:66-113); sampler=
+    "weighted": WeightedBPRMF.SampleTriple (WeightedBPRMF.cs:55-67), also in the loss-sample burn."""
     users, items = i32(users), i32(items)
     rng = rng if rng is not None else Rng(seed)
     U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
@@ -447,7 +456,8 @@ def bpr_train(users, items, n_users, n_items, *, seed=1, k=10, num_iter=30, lear
     off, rows = insertion_order_rows(users, items, n_users)
     srt = sorted_rows(off, rows)
     p = _BprParams(k, 1, 1, int(update_j), learn_rate, reg_u, reg_i, reg_j, bias_reg, n_users - 1,
-                   n_items - 1)
+                   n_items - 1, BPR_MODEL[model], BPR_SAMPLER[sampler], users.ctypes.data,
+                   items.ctypes.data, len(users))
     L = lib()
     num_burn = int(math.sqrt(n_users - 1)) * 100
     L.ora_bpr_burn(rng._buf, ctypes.byref(p), _p(off, _i64p), _p(rows, _i32p), _p(srt, _i32p),
@@ -468,9 +478,12 @@ def bpr_train(users, items, n_users, n_items, *, seed=1, k=10, num_iter=30, lear
 
 
 def bpr_update(u, i, j, U, V, bias, *, learn_rate=0.05, reg_u=0.0025, reg_i=0.0025,
-               reg_j=0.00025, bias_reg=0.0, update_u=True, update_i=True, update_j=True):
+               reg_j=0.00025, bias_reg=0.0, update_u=True, update_i=True, update_j=True,
+               model="BPRMF"):
+    """BPRMF.UpdateFactors (BPRMF.cs:330-374) / SoftMarginRankingMF's (:66-113) -- in place."""
     p = _BprParams(U.shape[1], int(update_u), int(update_i), int(update_j), learn_rate, reg_u,
-                   reg_i, reg_j, bias_reg, U.shape[0] - 1, V.shape[0] - 1)
+                   reg_i, reg_j, bias_reg, U.shape[0] - 1, V.shape[0] - 1, BPR_MODEL[model], 0,
+                   None, None, 0)
     lib().ora_bpr_update(ctypes.byref(p), u, i, j, _p(U, _f32p), _p(V, _f32p), _p(bias, _f32p))
 
 

@@ -157,6 +157,21 @@ def case_bpr_small():
                 V=st["V"], bias=st["bias"], trace0=st["traces"][0])
 
 
+def case_bpr_soft_margin_small():
+    u, i = synth_feedback(22, 30, 20, 8)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    st = O.bpr_train(u, i, nu, ni, seed=4, k=5, num_iter=2, trace_epochs=1, learn_rate=0.1,
+                     model="SoftMarginRankingMF")
+    return dict(users=u, items=i, U=st["U"], V=st["V"], bias=st["bias"], trace0=st["traces"][0])
+
+
+def case_bpr_weighted_small():
+    u, i = synth_feedback(23, 30, 20, 8)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    st = O.bpr_train(u, i, nu, ni, seed=6, k=5, num_iter=2, trace_epochs=1, sampler="weighted")
+    return dict(users=u, items=i, U=st["U"], V=st["V"], bias=st["bias"], trace0=st["traces"][0])
+
+
 def case_wrmf_small():
     u, i = synth_feedback(31, 30, 20, 8)
     nu, ni = int(u.max()) + 1, int(i.max()) + 1
@@ -174,6 +189,8 @@ CASES = {
     "mf_example_k3": case_mf_example_k3,
     "mf_synth_k10": case_mf_synth_k10,
     "bpr_small": case_bpr_small,
+    "bpr_soft_margin_small": case_bpr_soft_margin_small,
+    "bpr_weighted_small": case_bpr_weighted_small,
     "wrmf_small": case_wrmf_small,
 }
 

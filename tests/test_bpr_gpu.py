@@ -42,22 +42,24 @@ def auc_of(U, V, bias, tr_u, tr_i, te_u, te_i, seed=99):
     return O.item_eval_auc(U, V, bias, tr_u, tr_i, te_u, te_i, candidates=cand)
 
 
+@pytest.mark.parametrize("schedule", ["ordered", "hogwild"])
 @pytest.mark.parametrize("sampling", ["uniform_user", "uniform_pair"])
-def test_bpr_auc_parity(sampling):
+def test_bpr_auc_parity(sampling, schedule):
     tr_u, tr_i, te_u, te_i = planted_feedback(1, 4000, 600, 25)
     nu, ni = int(tr_u.max()) + 1, int(tr_i.max()) + 1
     k, iters = 16, 20
     st = O.bpr_train(tr_u, tr_i, nu, ni, seed=5, k=k, num_iter=iters)
     auc_ref, n_ref = auc_of(st["U"], st["V"], st["bias"], tr_u, tr_i, te_u, te_i)
     Random.set_seed(5)
-    m = BPRMF(NumFactors=k, NumIter=iters, UniformUserSampling=(sampling == "uniform_user"))
+    m = BPRMF(NumFactors=k, NumIter=iters, UniformUserSampling=(sampling == "uniform_user"),
+              Schedule=schedule)
     m.feedback = PosOnlyFeedback(tr_u, tr_i)
     m.init_model()
     np.testing.assert_array_equal(m.user_factors, st["init_U"])  # same host RNG init
     for _ in range(iters):
         m.iterate()
     auc_gpu, n_gpu = auc_of(m.user_factors, m.item_factors, m.item_bias, tr_u, tr_i, te_u, te_i)
-    print(f"BPR {sampling}: AUC gpu {auc_gpu:.5f} oracle {auc_ref:.5f} users {n_gpu}")
+    print(f"BPR {sampling} {schedule}: AUC gpu {auc_gpu:.5f} oracle {auc_ref:.5f} users {n_gpu}")
     assert n_gpu == n_ref
     assert auc_ref > 0.75
     assert abs(auc_gpu - auc_ref) <= 0.01

@@ -174,3 +174,28 @@ def test_mf_oracle_predict_bounds_and_unknown_ids():
     out = O.mf_predict(np.array([0, 1, 1, 2, 0], np.int32), np.array([0, 0, 1, 0, 7], np.int32),
                        U, V, 2.5, 1.0, 5.0)
     np.testing.assert_array_equal(out, np.float32([5.0, 1.0, 1.0, 2.5, 2.5]))
+
+
+def test_soft_margin_update_hinge():
+    # SoftMarginRankingMF.UpdateFactors (:66-113): no update when x_uij > 0, else the hinge step
+    U = np.array([[1.0, 0.5]], np.float32)
+    V = np.array([[1.0, 1.0], [0.0, 0.0]], np.float32)
+    b = np.zeros(2, np.float32)
+    U0, V0 = U.copy(), V.copy()
+    O.bpr_update(0, 0, 1, U, V, b, model="SoftMarginRankingMF", learn_rate=0.1)  # x = 1.5 > 0
+    assert np.array_equal(U, U0) and np.array_equal(V, V0) and not b.any()
+    O.bpr_update(0, 1, 0, U, V, b, model="SoftMarginRankingMF", learn_rate=0.1, bias_reg=0.0,
+                 reg_u=0.0, reg_i=0.0, reg_j=0.0)  # x = -1.5: w += lr (h_i - h_j), b_i += lr
+    np.testing.assert_array_equal(U, np.float32([[0.9, 0.4]]))
+    np.testing.assert_array_equal(V, np.float32([[0.9, 0.95], [0.1, 0.05]]))
+    np.testing.assert_array_equal(b, np.float32([-0.1, 0.1]))
+
+
+def test_weighted_sampler_draws_event_items():
+    # WeightedBPRMF.SampleTriple (:55-67): j is always the item of some event and never in S_u
+    g = golden()
+    u, i = g["bpr_weighted_small/users"], g["bpr_weighted_small/items"]
+    tr = g["bpr_weighted_small/trace0"]
+    pos = set(zip(u.tolist(), i.tolist()))
+    assert all((a, b) in pos for a, b, _ in tr.tolist())
+    assert all((a, c) not in pos and c in set(i.tolist()) for a, _, c in tr.tolist())
