@@ -212,10 +212,23 @@ def main():
         torch.distributed.destroy_process_group()
 
 
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: the process's CPU share, at most 16 (the GPU box gives
+    one GPU job 16 cores; os.cpu_count() there reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def cpu_baseline(h, k, n_users, n_items, gb, seconds, sample):
-    """Oracle Iterate() (single thread, exact reference arithmetic) on a bounded sample of the
-    same workload: a prefix of the very ratings stream the GPU trains on, applied to the GPU
-    model's current state, sized for ~`seconds` of CPU work."""
+    """The oracle (C restatement of BiasedMatrixFactorization.cs:264-310) on a bounded sample of
+    the same workload -- a prefix of the very ratings stream the GPU trains on, applied to the GPU
+    model's current state:
+      * value: the reference's own multi-core schedule, MaxThreads = T DSGD (:205-215; blocks from
+        MultiCore.PartitionUsersAndItems, one sub-epoch's blocks on T threads), one epoch;
+      * single_thread: the sequential Iterate(), sized for ~`seconds` of CPU work."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -235,10 +248,23 @@ def cpu_baseline(h, k, n_users, n_items, gb, seconds, sample):
     t0 = time.perf_counter()
     O.bmf_iterate(u, i, v, np.arange(probe, probe + n, dtype=np.int32), U, V, bu, bi, **kw)
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "rating-updates/s", "cores": 1, "kind": "port",
-            "sample": f"{n} ratings of the C2 stream itself (the GPU's training data), k={k}, "
-                      f"oracle Iterate() = C restatement of BiasedMatrixFactorization.cs:264-310, "
-                      f"single thread, {dt:.1f} s"}
+    single = {"value": n / dt, "unit": "rating-updates/s", "cores": 1, "kind": "port",
+              "sample": f"{n} ratings of the C2 stream itself (the GPU's training data), k={k}, "
+                        f"oracle Iterate() = C restatement of BiasedMatrixFactorization.cs:"
+                        f"264-310, single thread, {dt:.1f} s"}
+    T = cpu_threads()
+    rng = O.Rng(1)
+    blocks = O.partition_users_and_items(rng, u, i, n_users - 1, n_items - 1, T)
+    seq = rng.shuffle(np.arange(blocks[0], dtype=np.int32))
+    t0 = time.perf_counter()
+    O.bmf_dsgd_epoch_mt(u, i, v, blocks, seq, T, U, V, bu, bi, **kw)
+    dt_mt = time.perf_counter() - t0
+    return {"value": len(u) / dt_mt, "unit": "rating-updates/s", "cores": T, "kind": "port",
+            "sample": f"one DSGD epoch (MaxThreads={T}: {blocks[0]}x{blocks[0]} user x item "
+                      f"blocks, BiasedMatrixFactorization.cs:205-215) over the first {len(u)} "
+                      f"ratings of the C2 stream, k={k}, oracle C restatement on {T} threads, "
+                      f"{dt_mt:.1f} s",
+            "single_thread": single}
 
 
 def bench_bpr(args):

@@ -16,6 +16,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -379,6 +380,51 @@ int32_t ora_partition_users_and_items(ora_rng* r, const int32_t* users, const in
     free(up);
     free(ip);
     return G;
+}
+
+/* BiasedMatrixFactorization.Iterate() with MaxThreads = G (:205-215): per sub-epoch i of the
+ * shuffled sequence, Parallel.For over j runs block (j, (i + j) % G) -- blocks of one sub-epoch
+ * share no user and no item -- on up to n_threads threads, then joins (the CPU baseline of the
+ * reference's own multi-core DSGD).  Blocks as produced by ora_partition_users_and_items. */
+typedef struct {
+    const ora_bmf_params* p;
+    const int32_t *users, *items, *idx, *cu, *ci;
+    const float* values;
+    const int64_t* off;
+    float *U, *V, *bu, *bi;
+    int32_t G, sub, t, T;
+} ora_dsgd_job;
+
+static void* ora_dsgd_worker(void* arg) {
+    const ora_dsgd_job* j = (const ora_dsgd_job*)arg;
+    for (int32_t x = j->t; x < j->G; x += j->T) {
+        const int64_t b = (int64_t)x * j->G + (j->sub + x) % j->G;
+        ora_bmf_iterate(j->p, j->users, j->items, j->values, j->idx + j->off[b],
+                        j->off[b + 1] - j->off[b], j->U, j->V, j->bu, j->bi, j->cu, j->ci);
+    }
+    return NULL;
+}
+
+void ora_bmf_dsgd_epoch_mt(const ora_bmf_params* p, const int32_t* users, const int32_t* items,
+                           const float* values, const int64_t* offsets, const int32_t* indices,
+                           int32_t G, const int32_t* subepochs, int32_t n_threads, float* U,
+                           float* V, float* bu, float* bi, const int32_t* count_by_user,
+                           const int32_t* count_by_item) {
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > G) n_threads = G;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)n_threads);
+    ora_dsgd_job* jobs = (ora_dsgd_job*)malloc(sizeof(ora_dsgd_job) * (size_t)n_threads);
+    for (int32_t s = 0; s < G; s++) {
+        for (int32_t t = 0; t < n_threads; t++) {
+            ora_dsgd_job jb = {p, users, items, indices, count_by_user, count_by_item, values,
+                               offsets, U, V, bu, bi, G, subepochs[s], t, n_threads};
+            jobs[t] = jb;
+            pthread_create(&th[t], NULL, ora_dsgd_worker, &jobs[t]);
+        }
+        for (int32_t t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+    }
+    free(jobs);
+    free(th);
 }
 
 /* ------------------------------------------------------------------------------------------

@@ -65,6 +65,9 @@ def lib():
         L.ora_bmf_params_sizeof.restype = ctypes.c_size_t
         L.ora_bmf_iterate.argtypes = [ctypes.c_void_p, _i32p, _i32p, _f32p, _i32p, ctypes.c_int64,
                                       _f32p, _f32p, _f32p, _f32p, _i32p, _i32p]
+        L.ora_bmf_dsgd_epoch_mt.argtypes = [ctypes.c_void_p, _i32p, _i32p, _f32p, _i64p, _i32p,
+                                            ctypes.c_int32, _i32p, ctypes.c_int32, _f32p, _f32p,
+                                            _f32p, _f32p, _i32p, _i32p]
         L.ora_mf_iterate.argtypes = [ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                      ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f32p, _i32p,
                                      ctypes.c_int64, _f32p, _f32p]
@@ -114,6 +117,10 @@ def _p(a, t):
 
 def i32(a):
     return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def i64(a):
+    return np.ascontiguousarray(a, dtype=np.int64)
 
 
 def f32(a):
@@ -206,6 +213,25 @@ def bmf_iterate(users, items, values, indices, U, V, bu, bi, *, gb, min_rating, 
     lib().ora_bmf_iterate(ctypes.byref(p), _p(users, _i32p), _p(items, _i32p), _p(values, _f32p),
                           _p(idx, _i32p), idx.size, _p(U, _f32p), _p(V, _f32p), _p(bu, _f32p),
                           _p(bi, _f32p), _p(cu, _i32p), _p(ci, _i32p))
+
+
+def bmf_dsgd_epoch_mt(users, items, values, blocks, subepochs, n_threads, U, V, bu, bi, *, gb,
+                      min_rating, range_, lr, bias_lr=1.0, bias_reg=0.01, reg_u=0.015,
+                      reg_i=0.015, loss=0, freq_reg=False, count_by_user=None,
+                      count_by_item=None):
+    """One DSGD epoch (BiasedMatrixFactorization.cs:205-215, MaxThreads = G) with the blocks of a
+    sub-epoch on ``n_threads`` pthreads -- in place; equal to the sequential block order."""
+    G, off, idx = blocks
+    k = U.shape[1]
+    p = _BmfParams(k, loss, int(freq_reg), 1, 1, gb, min_rating, range_, lr, bias_lr, bias_reg,
+                   reg_u, reg_i)
+    cu = i32(count_by_user) if count_by_user is not None else None
+    ci = i32(count_by_item) if count_by_item is not None else None
+    seq = i32(subepochs)
+    lib().ora_bmf_dsgd_epoch_mt(ctypes.byref(p), _p(users, _i32p), _p(items, _i32p),
+                                _p(values, _f32p), _p(i64(off), _i64p), _p(i32(idx), _i32p), G,
+                                _p(seq, _i32p), int(n_threads), _p(U, _f32p), _p(V, _f32p),
+                                _p(bu, _f32p), _p(bi, _f32p), _p(cu, _i32p), _p(ci, _i32p))
 
 
 def partition_users_and_items(rng: Rng, users, items, max_user_id, max_item_id, num_groups):

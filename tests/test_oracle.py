@@ -199,3 +199,21 @@ def test_weighted_sampler_draws_event_items():
     pos = set(zip(u.tolist(), i.tolist()))
     assert all((a, b) in pos for a, b, _ in tr.tolist())
     assert all((a, c) not in pos and c in set(i.tolist()) for a, _, c in tr.tolist())
+
+
+def test_multithreaded_dsgd_equals_sequential_blocks():
+    # MaxThreads = G DSGD: blocks of one sub-epoch are disjoint, so the threaded epoch (the CPU
+    # baseline of bench.py) equals the sequential block order bit for bit
+    from golden_cases import synth_ratings
+    u, i, v = synth_ratings(14, 200, 150, 20000)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    st = O.bmf_train(u, i, v, nu, ni, 1.0, 5.0, seed=3, k=8, num_iter=1, max_threads=6)
+    U, V = st["init_U"].copy(), st["init_V"].copy()
+    bu, bi = np.zeros(nu, np.float32), np.zeros(ni, np.float32)
+    O.bmf_dsgd_epoch_mt(u, i, v, st["blocks"], st["subepochs"][0], 6, U, V, bu, bi,
+                        gb=st["global_bias"], min_rating=np.float32(1), range_=st["range_"],
+                        lr=np.float32(0.01), count_by_user=np.bincount(u, minlength=nu),
+                        count_by_item=np.bincount(i, minlength=ni))
+    np.testing.assert_array_equal(U, st["U"])
+    np.testing.assert_array_equal(V, st["V"])
+    np.testing.assert_array_equal(bu, st["bu"])
