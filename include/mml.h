@@ -186,6 +186,26 @@ mml_status mml_bmf_objective(mml_bmf* h, double* out);
 /* Multi-GPU (user shards): in-place RCCL all-reduce of item factors and item
  * biases over the context's communicator, then scale by 1/nranks (model averaging). */
 mml_status mml_bmf_allreduce_items(mml_bmf* h);
+/* IFoldInRatingPredictor.ScoreItems' FoldIn (RatingPrediction/IFoldInRatingPredictor.cs:42-48):
+ * BiasedMatrixFactorization.FoldIn (:447-492) -- MML_MF_PLAIN: MatrixFactorization.FoldIn
+ * (MatrixFactorization.cs:326-351) -- for n_fold new users at once against the trained item side,
+ * one wavefront each.  User x's ratings are rated_items/rated_values[rated_off[x] ..
+ * rated_off[x+1]) in visiting order (the host has shuffled them, Utils.Shuffle) and
+ * init_factors[x * k ..] are its InitNormal draws (drawn before the shuffle).  num_iter = NumIter,
+ * learn_rate = LearnRate, decay = Decay (MML_MF_PLAIN only; BiasedMatrixFactorization.FoldIn does
+ * not decay).  out_vectors: [n_fold x (k + 1)] = (user bias, factors) for MML_MF_BIASED
+ * (FOLD_IN_BIAS_INDEX = 0, :80-82), [n_fold x k] for MML_MF_PLAIN. */
+mml_status mml_bmf_fold_in(mml_bmf* h, int32_t n_fold, const int64_t* rated_off,
+                           const int32_t* rated_items, const float* rated_values,
+                           const float* init_factors, int32_t num_iter, float learn_rate,
+                           float decay, float* out_vectors);
+/* Predict(float[] user_vector, int item_id) (BiasedMatrixFactorization.cs:327-335; MML_MF_PLAIN:
+ * MatrixFactorization.cs:222-241, bound) for n (vector, item) pairs: vectors as mml_bmf_fold_in
+ * writes them, vector_index[x] selects the vector of pair x.  MML_MF_PLAIN rejects items beyond the
+ * model (the reference's RowScalarProduct throws). */
+mml_status mml_bmf_predict_vectors(mml_bmf* h, int32_t n_vectors, const float* vectors,
+                                   const int32_t* vector_index, const int32_t* items, int64_t n,
+                                   float* out);
 
 /* ------------------------------------------------------------------ BPRMF */
 enum {

@@ -102,6 +102,10 @@ SIGNATURES = {
                                 ctypes.c_float]),
     "mml_bmf_get_model": (_st, [_vp, _f32p, _f32p, _f32p, _f32p]),
     "mml_bmf_iterate": (_st, [_vp, ctypes.c_float, _i32p]),
+    "mml_bmf_fold_in": (_st, [_vp, ctypes.c_int32, _i64p, _i32p, _f32p, _f32p, ctypes.c_int32,
+                              ctypes.c_float, ctypes.c_float, _f32p]),
+    "mml_bmf_predict_vectors": (_st, [_vp, ctypes.c_int32, _f32p, _i32p, _i32p, ctypes.c_int64,
+                                      _f32p]),
     "mml_bmf_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
     "mml_bmf_evaluate": (_st, [_vp, _i32p, _i32p, _f32p, ctypes.c_int64, _f32p]),
     "mml_bmf_last_timing": (_st, [_vp, _f32p]),

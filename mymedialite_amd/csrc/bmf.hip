@@ -485,6 +485,112 @@ __global__ __launch_bounds__(256) void bmf_complexity_kernel(
     if (threadIdx.x == 0) partials[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
+// ---------------------------------------------------------------- fold-in (IFoldInRatingPredictor)
+struct FoldScalars {
+    float gb, min_rating, range, lr, blr, bias_reg, reg_u, decay;
+    int32_t freq;
+};
+
+// BiasedMatrixFactorization.FoldIn (:447-492) / MatrixFactorization.FoldIn (MatrixFactorization.cs:
+// 326-351, LOSS = kPlainMF) for fold-in user blockIdx.x: one wavefront, lane f owns factors
+// f, f + 64, ...; the item-row dot is summed left to right via v_readlane (RowScalarProduct,
+// DataType/MatrixExtensions.cs:183-196); the bias step and factor deltas are the reference's float
+// expressions.  out: (bias, factors) rows of k + 1 (biased) or factor rows of k (plain).
+template <int LOSS, int KM>
+__global__ __launch_bounds__(64) void bmf_fold_in_kernel(
+    const int64_t* __restrict__ off, const int32_t* __restrict__ items,
+    const float* __restrict__ values, int32_t num_iter, const float* __restrict__ V,
+    const float* __restrict__ bi, int32_t k, int32_t ld, FoldScalars s,
+    const float* __restrict__ init, float* __restrict__ out) {
+    constexpr bool plain = LOSS == kPlainMF;
+    const int lane = threadIdx.x;
+    const int64_t b = blockIdx.x;
+    const int64_t begin = off[b], end = off[b + 1];
+    float fac[KM];
+#pragma unroll
+    for (int m = 0; m < KM; ++m) {
+        const int f = lane + 64 * m;
+        fac[m] = f < k ? init[b * k + f] : 0.0f;
+    }
+    const float reg_weight =
+        (!plain && s.freq) ? (float)((double)s.reg_u / sqrt((double)(end - begin))) : s.reg_u;
+    float ub = 0.0f;
+    double lr = (double)s.lr;
+    for (int32_t it = 0; it < num_iter; ++it) {
+        for (int64_t x = begin; x < end; ++x) {
+            const int32_t i = items[x];
+            const float* Vi = V + (int64_t)i * ld;
+            float vi[KM];
+            float dot = 0.0f;
+#pragma unroll
+            for (int m = 0; m < KM; ++m) {
+                const int f = lane + 64 * m;
+                vi[m] = f < k ? Vi[f] : 0.0f;
+                const int bits = __float_as_int(vi[m] * fac[m]);
+                const int lim = min(64, k - 64 * m);
+                for (int l = 0; l < lim; ++l)
+                    dot += __int_as_float(__builtin_amdgcn_readlane(bits, l));
+            }
+            if constexpr (plain) {
+                const float err = values[x] - (s.gb + dot);
+#pragma unroll
+                for (int m = 0; m < KM; ++m)
+                    fac[m] += (float)(lr * (double)(err * vi[m] - s.reg_u * fac[m]));
+            } else {
+                const double score = (double)(((s.gb + ub) + bi[i]) + dot);
+                const double sig = 1.0 / (1.0 + exp(-score));
+                const double err =
+                    (double)values[x] - ((double)s.min_rating + sig * (double)s.range);
+                const float g = gradient_common<LOSS>(sig, err, s.range);
+                ub += s.blr * (g - s.bias_reg * reg_weight * ub);
+#pragma unroll
+                for (int m = 0; m < KM; ++m)
+                    fac[m] += (float)(lr * (double)(g * vi[m] - reg_weight * fac[m]));
+            }
+        }
+        if constexpr (plain) lr *= (double)s.decay;
+    }
+    const int64_t w = plain ? k : k + 1;
+    float* o = out + b * w + (plain ? 0 : 1);
+    if (!plain && lane == 0) out[b * w] = ub;
+#pragma unroll
+    for (int m = 0; m < KM; ++m) {
+        const int f = lane + 64 * m;
+        if (f < k) o[f] = fac[m];
+    }
+}
+
+// Predict(float[] user_vector, int item_id) for (vector, item) pairs: BiasedMatrixFactorization
+// (:327-335) or, plain, MatrixFactorization's bound form (MatrixFactorization.cs:222-241).
+__global__ __launch_bounds__(256) void bmf_predict_vectors_kernel(
+    const float* __restrict__ vec, const int32_t* __restrict__ vidx,
+    const int32_t* __restrict__ items, int64_t n, int32_t n_items, const float* __restrict__ V,
+    const float* __restrict__ bi, int32_t k, int32_t ld, float gb, float min_rating,
+    float max_rating, int32_t plain, float* __restrict__ out) {
+    const int64_t w = plain ? k : k + 1;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const float* uv = vec + (int64_t)vidx[x] * w;
+        const int32_t i = items[x];
+        if (plain) {
+            float dot = 0.0f;
+            for (int f = 0; f < k; ++f) dot += V[(int64_t)i * ld + f] * uv[f];
+            float r = gb + dot;
+            r = r > max_rating ? max_rating : r;
+            out[x] = r < min_rating ? min_rating : r;
+            continue;
+        }
+        double score = (double)(gb + uv[0]);
+        if (i < n_items) {
+            float dot = 0.0f;
+            for (int f = 0; f < k; ++f) dot += V[(int64_t)i * ld + f] * uv[1 + f];
+            score += (double)(bi[i] + dot);
+        }
+        const float range = max_rating - min_rating;
+        out[x] = (float)((double)min_rating + 1.0 / (1.0 + exp(-score)) * (double)range);
+    }
+}
+
 // stream[x] = raw[order[x]] for the three SoA columns
 __global__ __launch_bounds__(256) void gather_stream_kernel(
     const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const float* __restrict__ rr,
@@ -1097,6 +1203,132 @@ extern "C" mml_status mml_bmf_allreduce_items(mml_bmf* h) {
         scale_kernel<<<grid_for((int64_t)nv), 256, 0, st>>>(h->V.get(), (int64_t)nv, f);
         scale_kernel<<<grid_for(h->n_items), 256, 0, st>>>(h->bi.get(), h->n_items, f);
         MML_HIP(hipGetLastError());
+        MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+namespace {
+template <int LOSS>
+void launch_fold_in(mml_bmf* h, int32_t n_fold, const int64_t* off, const int32_t* items,
+                    const float* values, int32_t num_iter, const FoldScalars& fs,
+                    const float* init, float* out) {
+    hipStream_t st = h->ctx->stream;
+    const int km = (h->k + 63) / 64;
+#define MML_FOLD(KM)                                                                            \
+    bmf_fold_in_kernel<LOSS, KM><<<n_fold, 64, 0, st>>>(off, items, values, num_iter, h->V.get(), \
+                                                        h->bi.get(), h->k, h->ld, fs, init, out)
+    switch (km) {
+        case 1: MML_FOLD(1); break;
+        case 2: MML_FOLD(2); break;
+        case 3: MML_FOLD(3); break;
+        default: MML_FOLD(4); break;
+    }
+#undef MML_FOLD
+    MML_HIP(hipGetLastError());
+}
+}  // namespace
+
+extern "C" mml_status mml_bmf_fold_in(mml_bmf* h, int32_t n_fold, const int64_t* rated_off,
+                                      const int32_t* rated_items, const float* rated_values,
+                                      const float* init_factors, int32_t num_iter,
+                                      float learn_rate, float decay, float* out_vectors) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(n_fold >= 0 && num_iter >= 0, "negative sizes");
+        if (n_fold == 0) return;
+        MML_REQUIRE(rated_off && init_factors && out_vectors, "null arguments");
+        MML_REQUIRE(rated_off[0] == 0, "rated_off[0] must be 0");
+        for (int32_t x = 0; x < n_fold; ++x)
+            MML_REQUIRE(rated_off[x + 1] >= rated_off[x], "rated_off must be non-decreasing");
+        const int64_t nr = rated_off[n_fold];
+        MML_REQUIRE(nr == 0 || (rated_items && rated_values), "null rated arrays");
+        for (int64_t x = 0; x < nr; ++x)
+            MML_REQUIRE(rated_items[x] >= 0 && rated_items[x] < h->n_items,
+                        "fold-in item id beyond the model");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        const bool plain = h->p.model == MML_MF_PLAIN;
+        const int64_t w = plain ? h->k : h->k + 1;
+        mml::DeviceArray<int64_t> doff;
+        mml::DeviceArray<int32_t> ditems;
+        mml::DeviceArray<float> dvals, dinit, dout;
+        doff.alloc(n_fold + 1);
+        ditems.alloc(std::max<int64_t>(1, nr));
+        dvals.alloc(std::max<int64_t>(1, nr));
+        dinit.alloc((size_t)n_fold * h->k);
+        dout.alloc((size_t)n_fold * w);
+        MML_HIP(hipMemcpyAsync(doff.get(), rated_off, sizeof(int64_t) * (n_fold + 1),
+                               hipMemcpyHostToDevice, st));
+        if (nr > 0) {
+            MML_HIP(hipMemcpyAsync(ditems.get(), rated_items, sizeof(int32_t) * nr,
+                                   hipMemcpyHostToDevice, st));
+            MML_HIP(hipMemcpyAsync(dvals.get(), rated_values, sizeof(float) * nr,
+                                   hipMemcpyHostToDevice, st));
+        }
+        MML_HIP(hipMemcpyAsync(dinit.get(), init_factors, sizeof(float) * n_fold * h->k,
+                               hipMemcpyHostToDevice, st));
+        FoldScalars fs;
+        fs.gb = h->gb;
+        fs.min_rating = h->min_rating;
+        fs.range = h->max_rating - h->min_rating;
+        fs.lr = learn_rate;
+        fs.blr = h->p.bias_learn_rate * learn_rate;
+        fs.bias_reg = h->p.bias_reg;
+        fs.reg_u = h->p.reg_u;
+        fs.decay = decay;
+        fs.freq = h->p.frequency_regularization;
+#define MML_FOLD_ARGS h, n_fold, doff.get(), ditems.get(), dvals.get(), num_iter, fs, dinit.get(), \
+                      dout.get()
+        switch (plain ? kPlainMF : h->p.loss) {
+            case kPlainMF: launch_fold_in<kPlainMF>(MML_FOLD_ARGS); break;
+            case MML_LOSS_MAE: launch_fold_in<MML_LOSS_MAE>(MML_FOLD_ARGS); break;
+            case MML_LOSS_LOGISTIC: launch_fold_in<MML_LOSS_LOGISTIC>(MML_FOLD_ARGS); break;
+            default: launch_fold_in<MML_LOSS_RMSE>(MML_FOLD_ARGS); break;
+        }
+#undef MML_FOLD_ARGS
+        MML_HIP(hipMemcpyAsync(out_vectors, dout.get(), sizeof(float) * n_fold * w,
+                               hipMemcpyDeviceToHost, st));
+        MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+extern "C" mml_status mml_bmf_predict_vectors(mml_bmf* h, int32_t n_vectors, const float* vectors,
+                                              const int32_t* vector_index, const int32_t* items,
+                                              int64_t n, float* out) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(n_vectors >= 0 && n >= 0, "negative sizes");
+        if (n == 0) return;
+        MML_REQUIRE(vectors && vector_index && items && out, "null arguments");
+        const bool plain = h->p.model == MML_MF_PLAIN;
+        for (int64_t x = 0; x < n; ++x) {
+            MML_REQUIRE(vector_index[x] >= 0 && vector_index[x] < n_vectors,
+                        "vector index out of range");
+            MML_REQUIRE(items[x] >= 0 && (!plain || items[x] < h->n_items),
+                        "item id beyond the model");
+        }
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        const int64_t w = plain ? h->k : h->k + 1;
+        mml::DeviceArray<float> dvec, dout;
+        mml::DeviceArray<int32_t> dvi, dit;
+        dvec.alloc((size_t)std::max<int64_t>(1, (int64_t)n_vectors * w));
+        dvi.alloc(n);
+        dit.alloc(n);
+        dout.alloc(n);
+        if (n_vectors > 0)
+            MML_HIP(hipMemcpyAsync(dvec.get(), vectors, sizeof(float) * n_vectors * w,
+                                   hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(dvi.get(), vector_index, sizeof(int32_t) * n,
+                               hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(dit.get(), items, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+        bmf_predict_vectors_kernel<<<grid_for(n), 256, 0, st>>>(
+            dvec.get(), dvi.get(), dit.get(), n, h->n_items, h->V.get(), h->bi.get(), h->k, h->ld,
+            h->gb, h->min_rating, h->max_rating, (int32_t)plain, dout.get());
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipMemcpyAsync(out, dout.get(), sizeof(float) * n, hipMemcpyDeviceToHost, st));
         MML_HIP(hipStreamSynchronize(st));
     });
 }

@@ -208,6 +208,66 @@ class MatrixFactorization(Recommender):
         self._upload_model(self.global_bias)
         self._host = None
 
+    # ------------------------------------------------------------------ fold-in
+    def fold_in_batch(self, rated_lists) -> np.ndarray:
+        """FoldIn for several new users (IFoldInRatingPredictor; BiasedMatrixFactorization.cs:
+        447-492, MatrixFactorization.cs:326-351), one GPU wavefront each.  ``rated_lists``: per user
+        a list of (item_id, rating).  The host RNG draws in the reference's order, user by user:
+        InitNormal of the factors, then rated_items.Shuffle().  Returns the user vectors:
+        (bias, factors) rows for BiasedMatrixFactorization, factor rows for MatrixFactorization."""
+        if self._h is None:
+            raise RuntimeError("Train() or load_model() first")
+        k = int(self.NumFactors)
+        rng = Random.get_instance()
+        inits, its, vals, off = [], [], [], [0]
+        for rated in rated_lists:
+            inits.append(rng.fill_normal(k, self.InitMean, self.InitStdDev))
+            perm = rng.shuffle(np.arange(len(rated), dtype=np.int32))
+            rated = [rated[p] for p in perm.tolist()]
+            its += [int(t[0]) for t in rated]
+            vals += [float(t[1]) for t in rated]
+            off.append(len(its))
+        n = len(rated_lists)
+        w = k if self.MODEL == N.MF_PLAIN else k + 1
+        out = np.empty((n, w), np.float32)
+        init = N.f32(np.concatenate(inits)) if n else np.zeros(0, np.float32)
+        off_a, it_a, va_a = N.i64(off), N.i32(its), N.f32(vals)
+        N.check(N.lib().mml_bmf_fold_in(
+            self._h, n, N.ptr(off_a, N._i64p), N.ptr(it_a, N._i32p), N.ptr(va_a, N._f32p),
+            N.ptr(init, N._f32p), int(self.NumIter), float(np.float32(self.LearnRate)),
+            float(np.float32(getattr(self, "Decay", 1.0))), N.ptr(out, N._f32p)))
+        return out
+
+    def fold_in(self, rated_items) -> np.ndarray:
+        return self.fold_in_batch([rated_items])[0]
+
+    def predict_vectors(self, vectors, vector_index, items) -> np.ndarray:
+        """Predict(float[] user_vector, int item_id) for (vector, item) pairs on the GPU."""
+        v = N.f32(vectors)
+        vi, it = N.i32(vector_index), N.i32(items)
+        out = np.empty(len(it), np.float32)
+        N.check(N.lib().mml_bmf_predict_vectors(self._h, v.shape[0], N.ptr(v, N._f32p),
+                                                N.ptr(vi, N._i32p), N.ptr(it, N._i32p), len(it),
+                                                N.ptr(out, N._f32p)))
+        return out
+
+    def score_items(self, rated_items, candidate_items=None):
+        """IFoldInRatingPredictor.ScoreItems (MatrixFactorization.cs:355-366): fold in, then score
+        the candidates; without candidates, FoldInRatingPredictorExtensions.ScoreItems' range
+        0 .. MaxItemID - 2 (FoldInRatingPredictorExtensions.cs:63-67, quirk kept)."""
+        if candidate_items is None:
+            candidate_items = np.arange(0, max(0, self.MaxItemID - 1), dtype=np.int32)
+        cand = N.i32(candidate_items)
+        v = self.fold_in(rated_items)
+        sc = self.predict_vectors(v[None, :], np.zeros(len(cand), np.int32), cand)
+        return list(zip(cand.tolist(), sc.tolist()))
+
+    def recommend_items(self, rated_items, n, candidate_items=None):
+        """FoldInRatingPredictorExtensions.RecommendItems (:35-52): ScoreItems, stable
+        OrderByDescending on the score, Take(n)."""
+        scored = self.score_items(rated_items, candidate_items)
+        return sorted(scored, key=lambda t: -t[1])[:n]
+
     def predict(self, users, items) -> np.ndarray:
         """Predict(int,int), batched on the GPU."""
         u, i = N.i32(np.atleast_1d(users)), N.i32(np.atleast_1d(items))

@@ -296,6 +296,64 @@ void ora_bmf_objective(const int32_t* users, const int32_t* items, const float* 
     out[1] = complexity;
 }
 
+/* BiasedMatrixFactorization.FoldIn (:447-492) for one user, its rated_items already shuffled and
+ * `factors` already drawn (InitNormal, then Shuffle, on the host RNG).  Uses LearnRate (not the
+ * decayed current rate), no decay; the bias step and the factor delta are float expressions (float
+ * operands), widened to double for the factor step.  out[0] = user bias, out[1..k] = factors. */
+void ora_bmf_fold_in(const ora_bmf_params* p, int64_t n, const int32_t* items, const float* values,
+                     int32_t num_iter, const float* V, const float* bi, const float* init_factors,
+                     float* out) {
+    const int k = p->k;
+    float* factors = out + 1;
+    for (int f = 0; f < k; f++) factors[f] = init_factors[f];
+    float user_bias = 0.0f;
+    const float reg_weight = p->frequency_regularization
+                                 ? (float)((double)p->reg_u / sqrt((double)n))
+                                 : p->reg_u;
+    for (int32_t it = 0; it < num_iter; it++)
+        for (int64_t x = 0; x < n; x++) {
+            const int32_t item = items[x];
+            const float* Vi = V + (int64_t)item * k;
+            float dot = 0.0f;
+            for (int f = 0; f < k; f++) dot += Vi[f] * factors[f];
+            const double score = (double)(((p->global_bias + user_bias) + bi[item]) + dot);
+            const double sig = 1.0 / (1.0 + exp(-score));
+            const double prediction = (double)p->min_rating + sig * (double)p->rating_range_size;
+            const double err = (double)values[x] - prediction;
+            float g;
+            if (p->loss == ORA_LOSS_MAE) {
+                const double sgn = (err > 0) ? 1.0 : ((err < 0) ? -1.0 : 0.0);
+                g = (float)(sgn * sig * (1.0 - sig) * (double)p->rating_range_size);
+            } else if (p->loss == ORA_LOSS_LOGISTIC) {
+                g = (float)err;
+            } else {
+                g = (float)(err * sig * (1.0 - sig) * (double)p->rating_range_size);
+            }
+            user_bias += p->bias_learn_rate * p->learn_rate *
+                         (g - p->bias_reg * reg_weight * user_bias);
+            for (int f = 0; f < k; f++) {
+                const float u_f = factors[f];
+                const float i_f = Vi[f];
+                const double delta_u = (double)(g * i_f - reg_weight * u_f);
+                factors[f] += (float)((double)p->learn_rate * delta_u);
+            }
+        }
+    out[0] = user_bias;
+}
+
+/* BiasedMatrixFactorization.Predict(float[] user_vector, int item_id) (:327-335) */
+float ora_bmf_predict_vector(const ora_bmf_params* p, const float* user_vector, int32_t item,
+                             int32_t n_items, const float* V, const float* bi) {
+    double score = (double)(p->global_bias + user_vector[0]);
+    if (item < n_items) {
+        float dot = 0.0f;
+        for (int f = 0; f < p->k; f++) dot += V[(int64_t)item * p->k + f] * user_vector[1 + f];
+        score += (double)(bi[item] + dot);
+    }
+    return (float)((double)p->min_rating +
+                   1.0 / (1.0 + exp(-score)) * (double)p->rating_range_size);
+}
+
 /* ----------------------------------------------------------------------------------------
  * MatrixFactorization (RatingPrediction/MatrixFactorization.cs): the plain model, no biases
  * ---------------------------------------------------------------------------------------- */
@@ -327,6 +385,41 @@ void ora_mf_iterate(int k, float global_bias, float learn_rate, float regulariza
             }
         }
     }
+}
+
+/* MatrixFactorization.FoldIn (:326-351) for one user (rated_items shuffled, user_vector drawn by
+ * the host): double lr = LearnRate, multiplied by Decay after every pass; err and delta in float. */
+void ora_mf_fold_in(int k, float global_bias, float learn_rate, float decay, float regularization,
+                    int64_t n, const int32_t* items, const float* values, int32_t num_iter,
+                    const float* V, const float* init_factors, float* out) {
+    for (int f = 0; f < k; f++) out[f] = init_factors[f];
+    double lr = (double)learn_rate;
+    for (int32_t it = 0; it < num_iter; it++) {
+        for (int64_t x = 0; x < n; x++) {
+            const float* Vi = V + (int64_t)items[x] * k;
+            float dot = 0.0f;
+            for (int f = 0; f < k; f++) dot += Vi[f] * out[f];
+            const float err = values[x] - (global_bias + dot);
+            for (int f = 0; f < k; f++) {
+                const float u_f = out[f];
+                const float i_f = Vi[f];
+                const double delta_u = (double)(err * i_f - regularization * u_f);
+                out[f] += (float)(lr * delta_u);
+            }
+        }
+        lr *= (double)decay;
+    }
+}
+
+/* MatrixFactorization.Predict(float[] user_vector, int item_id) (:222-241), bound */
+float ora_mf_predict_vector(int k, float global_bias, float min_rating, float max_rating,
+                           const float* user_vector, int32_t item, const float* V) {
+    float dot = 0.0f;
+    for (int f = 0; f < k; f++) dot += V[(int64_t)item * k + f] * user_vector[f];
+    float r = global_bias + dot;
+    if (r > max_rating) r = max_rating;
+    if (r < min_rating) r = min_rating;
+    return r;
 }
 
 /* MatrixFactorization.Predict(int,int), :251-258 (+ Predict(u, i, true) :205-217): global_bias for

@@ -68,6 +68,17 @@ def lib():
         L.ora_bmf_dsgd_epoch_mt.argtypes = [ctypes.c_void_p, _i32p, _i32p, _f32p, _i64p, _i32p,
                                             ctypes.c_int32, _i32p, ctypes.c_int32, _f32p, _f32p,
                                             _f32p, _f32p, _i32p, _i32p]
+        L.ora_bmf_fold_in.argtypes = [ctypes.c_void_p, ctypes.c_int64, _i32p, _f32p, ctypes.c_int32,
+                                      _f32p, _f32p, _f32p, _f32p]
+        L.ora_bmf_predict_vector.restype = ctypes.c_float
+        L.ora_bmf_predict_vector.argtypes = [ctypes.c_void_p, _f32p, ctypes.c_int32, ctypes.c_int32,
+                                             _f32p, _f32p]
+        L.ora_mf_fold_in.argtypes = [ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                     ctypes.c_float, ctypes.c_int64, _i32p, _f32p, ctypes.c_int32,
+                                     _f32p, _f32p, _f32p]
+        L.ora_mf_predict_vector.restype = ctypes.c_float
+        L.ora_mf_predict_vector.argtypes = [ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                            ctypes.c_float, _f32p, ctypes.c_int32, _f32p]
         L.ora_mf_iterate.argtypes = [ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                      ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f32p, _i32p,
                                      ctypes.c_int64, _f32p, _f32p]
@@ -385,6 +396,48 @@ def mf_train(users, items, values, n_users, n_items, *, seed=1, k=10, learn_rate
             callback(epoch, state)
     state.update(global_bias=gb, random_index=random_index, current_learnrate=lr, rng=rng)
     return state
+
+
+def fold_in_draws(rng: Rng, k, rated_items, rated_values, init_mean=0.0, init_stddev=0.1):
+    """FoldIn's host RNG order (BiasedMatrixFactorization.cs:453-459, MatrixFactorization.cs:
+    328-330): factors.InitNormal, then rated_items.Shuffle() (Utils.cs:52-64)."""
+    init = rng.fill_normal(k, init_mean, init_stddev)
+    perm = rng.shuffle(np.arange(len(rated_items), dtype=np.int32))
+    return init, i32(np.asarray(rated_items)[perm]), f32(np.asarray(rated_values)[perm])
+
+
+def bmf_score_items(rng, rated_items, rated_values, candidates, V, bi, *, gb, min_rating, range_,
+                    k, num_iter=30, learn_rate=0.01, bias_learn_rate=1.0, bias_reg=0.01,
+                    reg_u=0.015, loss=0, freq_reg=False, init_mean=0.0, init_stddev=0.1):
+    """IFoldInRatingPredictor.ScoreItems for BiasedMatrixFactorization: FoldIn (:447-492) then
+    Predict(user_vector, item) (:327-335) per candidate -> (user_vector, scores)."""
+    init, it, va = fold_in_draws(rng, k, rated_items, rated_values, init_mean, init_stddev)
+    p = _BmfParams(k, loss, int(freq_reg), 1, 0, gb, min_rating, range_, learn_rate,
+                   bias_learn_rate, bias_reg, reg_u, reg_u)
+    out = np.zeros(k + 1, np.float32)
+    L = lib()
+    L.ora_bmf_fold_in(ctypes.byref(p), len(it), _p(it, _i32p), _p(va, _f32p), int(num_iter),
+                      _p(V, _f32p), _p(bi, _f32p), _p(init, _f32p), _p(out, _f32p))
+    sc = np.array([L.ora_bmf_predict_vector(ctypes.byref(p), _p(out, _f32p), int(c), V.shape[0],
+                                            _p(V, _f32p), _p(bi, _f32p)) for c in candidates],
+                  np.float32)
+    return out, sc
+
+
+def mf_score_items(rng, rated_items, rated_values, candidates, V, *, gb, min_rating, max_rating,
+                   k, num_iter=30, learn_rate=0.01, decay=1.0, regularization=0.015,
+                   init_mean=0.0, init_stddev=0.1):
+    """MatrixFactorization.ScoreItems (:355-366): FoldIn (:326-351) + bound Predict per item."""
+    init, it, va = fold_in_draws(rng, k, rated_items, rated_values, init_mean, init_stddev)
+    out = np.zeros(k, np.float32)
+    L = lib()
+    L.ora_mf_fold_in(k, float(gb), float(learn_rate), float(decay), float(regularization),
+                     len(it), _p(it, _i32p), _p(va, _f32p), int(num_iter), _p(V, _f32p),
+                     _p(init, _f32p), _p(out, _f32p))
+    sc = np.array([L.ora_mf_predict_vector(k, float(gb), float(min_rating), float(max_rating),
+                                           _p(out, _f32p), int(c), _p(V, _f32p))
+                   for c in candidates], np.float32)
+    return out, sc
 
 
 def mf_predict(users, items, U, V, gb, min_rating, max_rating):
