@@ -119,11 +119,18 @@ enum {
 /* Model family of an mml_bmf handle. */
 enum {
     MML_MF_BIASED = 0, /* BiasedMatrixFactorization (BiasedMatrixFactorization.cs:77-562) */
-    MML_MF_PLAIN = 1   /* MatrixFactorization (MatrixFactorization.cs:50-418): no biases, score =
+    MML_MF_PLAIN = 1,  /* MatrixFactorization (MatrixFactorization.cs:50-418): no biases, score =
                           global_bias + <U_u, V_i>, err = r - score in float, Regularization for
                           both sides (pass it as reg_u = reg_i), Predict clipped to [min, max];
                           loss, frequency_regularization and the bias fields are ignored and
                           mml_bmf_objective is not defined */
+    MML_MF_SOCIAL = 2  /* SocialMF (SocialMF.cs:43-254): BiasedMatrixFactorization trained by
+                          full-batch gradient descent with a social-network regulariser
+                          (IterateBatch :77-194) over the user relation of
+                          mml_bmf_set_user_relation; mml_bmf_iterate's learn_rate is LearnRate
+                          (the batch step never reads current_learnrate); the schedule field is
+                          ignored (the batch step is order-independent up to the per-row
+                          accumulation order, which follows the stored visit order) */
 };
 
 typedef struct {
@@ -136,6 +143,7 @@ typedef struct {
     float reg_u;                      /* RegU (:91) */
     float reg_i;                      /* RegI (:94) */
     int32_t model;                    /* MML_MF_* (ABI 2) */
+    float social_regularization;      /* SocialRegularization (SocialMF.cs:46), MML_MF_SOCIAL */
 } mml_bmf_params;
 
 typedef struct mml_bmf mml_bmf;
@@ -186,6 +194,12 @@ mml_status mml_bmf_objective(mml_bmf* h, double* out);
 /* Multi-GPU (user shards): in-place RCCL all-reduce of item factors and item
  * biases over the context's communicator, then scale by 1/nranks (model averaging). */
 mml_status mml_bmf_allreduce_items(mml_bmf* h);
+/* SocialMF.UserRelation (SocialMF.cs:50): rows [0, n_rows) of the user_connections
+ * SparseBooleanMatrix as CSR (offsets[n_rows + 1], cols = the rows' HashSet enumeration order, no
+ * duplicates within a row, ids < n_users); the library builds the Transpose() the batch step walks
+ * (SparseBooleanMatrix.cs:200-207).  MML_MF_SOCIAL handles only. */
+mml_status mml_bmf_set_user_relation(mml_bmf* h, int32_t n_rows, const int64_t* offsets,
+                                     const int32_t* cols);
 /* IFoldInRatingPredictor.ScoreItems' FoldIn (RatingPrediction/IFoldInRatingPredictor.cs:42-48):
  * BiasedMatrixFactorization.FoldIn (:447-492) -- MML_MF_PLAIN: MatrixFactorization.FoldIn
  * (MatrixFactorization.cs:326-351) -- for n_fold new users at once against the trained item side,

@@ -39,10 +39,11 @@ class BmfParams(ctypes.Structure):
     _fields_ = [("num_factors", ctypes.c_int32), ("loss", ctypes.c_int32),
                 ("frequency_regularization", ctypes.c_int32), ("schedule", ctypes.c_int32),
                 ("bias_learn_rate", ctypes.c_float), ("bias_reg", ctypes.c_float),
-                ("reg_u", ctypes.c_float), ("reg_i", ctypes.c_float), ("model", ctypes.c_int32)]
+                ("reg_u", ctypes.c_float), ("reg_i", ctypes.c_float), ("model", ctypes.c_int32),
+                ("social_regularization", ctypes.c_float)]
 
 
-MF_BIASED, MF_PLAIN = 0, 1
+MF_BIASED, MF_PLAIN, MF_SOCIAL = 0, 1, 2
 
 
 class BprParams(ctypes.Structure):
@@ -102,6 +103,7 @@ SIGNATURES = {
                                 ctypes.c_float]),
     "mml_bmf_get_model": (_st, [_vp, _f32p, _f32p, _f32p, _f32p]),
     "mml_bmf_iterate": (_st, [_vp, ctypes.c_float, _i32p]),
+    "mml_bmf_set_user_relation": (_st, [_vp, ctypes.c_int32, _i64p, _i32p]),
     "mml_bmf_fold_in": (_st, [_vp, ctypes.c_int32, _i64p, _i32p, _f32p, _f32p, ctypes.c_int32,
                               ctypes.c_float, ctypes.c_float, _f32p]),
     "mml_bmf_predict_vectors": (_st, [_vp, ctypes.c_int32, _f32p, _i32p, _i32p, ctypes.c_int64,

@@ -27,6 +27,8 @@
 //            per rating (float4 each), 64/LPR ratings per wave step, dot product by xor-shuffle
 //            reduction, plain (racy) stores of the updated rows -- Hogwild! semantics.
 //   HOGWILD_COHERENT  the same with sc1 (agent-coherent) row and bias accesses, see load4 below.
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
@@ -591,6 +593,181 @@ __global__ __launch_bounds__(256) void bmf_predict_vectors_kernel(
     }
 }
 
+// ---------------------------------------------------------------- SocialMF (IterateBatch)
+// SocialMF.IterateBatch (SocialMF.cs:77-194) restated as a deterministic device batch step: every
+// gradient element accumulates in the reference's order (ratings in visit order per user / item,
+// then L2, then the social terms), so the step is bit-faithful up to libm-vs-ocml exp rounding.
+
+// I.1 (:89-102): per rating of the stream, the loss gradient g[x] (float score, float
+// prediction, error = prediction - rating)
+template <int LOSS>
+__global__ __launch_bounds__(256) void smf_error_kernel(
+    const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
+    int64_t n, const float* __restrict__ U, const float* __restrict__ V,
+    const float* __restrict__ bu, const float* __restrict__ bi, int32_t k, int32_t ld, float gb,
+    float min_rating, float range, float* __restrict__ g) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t u = su[x], i = si[x];
+        float score = (gb + bu[u]) + bi[i];
+        const float* a = U + (int64_t)u * ld;
+        const float* c = V + (int64_t)i * ld;
+        float dot = 0.0f;
+        for (int f = 0; f < k; ++f) dot += a[f] * c[f];
+        score += dot;
+        const double sig = 1.0 / (1.0 + exp(-(double)score));
+        const float prediction = (float)((double)min_rating + sig * (double)range);
+        g[x] = gradient_common<LOSS>(sig, (double)(prediction - sr[x]), range);
+    }
+}
+
+__device__ __forceinline__ int64_t smf_row_len(const int64_t* off, int32_t n_rows, int32_t r) {
+    return r < n_rows ? off[r + 1] - off[r] : 0;
+}
+
+// User gradient, one wavefront per user, lane f owns factors f, f + 64, ... (KM per lane):
+// I.1 over the user's ratings in visit order (pos CSR), I.2 (:119-126), I.3 (:133-177).
+template <int KM>
+__global__ __launch_bounds__(64) void smf_user_grad_kernel(
+    const int64_t* __restrict__ pos_off, const int32_t* __restrict__ pos,
+    const int32_t* __restrict__ si, const float* __restrict__ g, const float* __restrict__ U,
+    const float* __restrict__ V, const float* __restrict__ bu, int32_t k, int32_t ld,
+    float reg_u, float bias_reg, float soc, const int64_t* __restrict__ conn_off,
+    const int32_t* __restrict__ conn_cols, int32_t n_conn, const int64_t* __restrict__ rev_off,
+    const int32_t* __restrict__ rev_cols, int32_t n_rev, float* __restrict__ Ug,
+    float* __restrict__ bug) {
+    const int lane = threadIdx.x;
+    const int32_t u = blockIdx.x;
+    float acc[KM], tmp[KM];
+    float bacc = 0.0f;
+#pragma unroll
+    for (int m = 0; m < KM; ++m) acc[m] = 0.0f;
+    auto row = [&](const float* M, int32_t r, int m) {
+        const int f = lane + 64 * m;
+        return f < k ? M[(int64_t)r * ld + f] : 0.0f;
+    };
+    for (int64_t p = pos_off[u]; p < pos_off[u + 1]; ++p) {
+        const int32_t x = pos[p];
+        const float gx = g[x];
+        const int32_t i = si[x];
+        bacc += gx;
+#pragma unroll
+        for (int m = 0; m < KM; ++m) acc[m] += gx * row(V, i, m);
+    }
+    bacc += bu[u] * reg_u * bias_reg;
+#pragma unroll
+    for (int m = 0; m < KM; ++m) acc[m] += row(U, u, m) * reg_u;
+    if (soc != 0.0f) {
+        const int64_t num = smf_row_len(conn_off, n_conn, u);
+        float bsum = 0.0f;
+#pragma unroll
+        for (int m = 0; m < KM; ++m) tmp[m] = 0.0f;
+        for (int64_t x = 0; x < num; ++x) {
+            const int32_t v = conn_cols[conn_off[u] + x];
+            bsum += bu[v];
+#pragma unroll
+            for (int m = 0; m < KM; ++m) tmp[m] += row(U, v, m);
+        }
+        if (num != 0) {
+            bacc += soc * (bu[u] - bsum / (float)num);
+#pragma unroll
+            for (int m = 0; m < KM; ++m) acc[m] += soc * (row(U, u, m) - tmp[m] / (float)num);
+        }
+        const int64_t nrev = smf_row_len(rev_off, n_rev, u);
+        for (int64_t y = 0; y < nrev; ++y) {
+            const int32_t v = rev_cols[rev_off[u] + y];
+            const int64_t cv = smf_row_len(conn_off, n_conn, v);
+            const float trust = 1.0f / (float)cv;
+            const float neg = -soc * trust;
+            float bd = 0.0f;
+#pragma unroll
+            for (int m = 0; m < KM; ++m) tmp[m] = 0.0f;
+            for (int64_t x = 0; x < cv; ++x) {
+                const int32_t w = conn_cols[conn_off[v] + x];
+                bd -= bu[w];
+#pragma unroll
+                for (int m = 0; m < KM; ++m) tmp[m] -= row(U, w, m);
+            }
+            bd *= trust;
+            bd += bu[v];
+            bacc += neg * bd;
+#pragma unroll
+            for (int m = 0; m < KM; ++m) {
+                tmp[m] *= trust;
+                tmp[m] += row(U, v, m);
+                acc[m] += neg * tmp[m];
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < KM; ++m) {
+        const int f = lane + 64 * m;
+        if (f < k) Ug[(int64_t)u * ld + f] = acc[m];
+    }
+    if (lane == 0) bug[u] = bacc;
+}
+
+// Item gradient, one wavefront per item: I.1 in visit order, then I.2 (:121-130)
+template <int KM>
+__global__ __launch_bounds__(64) void smf_item_grad_kernel(
+    const int64_t* __restrict__ pos_off, const int32_t* __restrict__ pos,
+    const int32_t* __restrict__ su, const float* __restrict__ g, const float* __restrict__ U,
+    const float* __restrict__ V, const float* __restrict__ bi, int32_t k, int32_t ld,
+    float reg_i, float bias_reg, float* __restrict__ Vg, float* __restrict__ big) {
+    const int lane = threadIdx.x;
+    const int32_t i = blockIdx.x;
+    float acc[KM];
+    float bacc = 0.0f;
+#pragma unroll
+    for (int m = 0; m < KM; ++m) acc[m] = 0.0f;
+    for (int64_t p = pos_off[i]; p < pos_off[i + 1]; ++p) {
+        const int32_t x = pos[p];
+        const float gx = g[x];
+        const int32_t u = su[x];
+        bacc += gx;
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int f = lane + 64 * m;
+            acc[m] += gx * (f < k ? U[(int64_t)u * ld + f] : 0.0f);
+        }
+    }
+    bacc += bi[i] * reg_i * bias_reg;
+#pragma unroll
+    for (int m = 0; m < KM; ++m) {
+        const int f = lane + 64 * m;
+        if (f < k) Vg[(int64_t)i * ld + f] = acc[m] + V[(int64_t)i * ld + f] * reg_i;
+    }
+    if (lane == 0) big[i] = bacc;
+}
+
+// II (:180-193): M += G * (-LearnRate) (Multiply then Inc), b -= g * LearnRate * BiasLearnRate
+__global__ __launch_bounds__(256) void smf_apply_kernel(float* __restrict__ M,
+                                                        const float* __restrict__ G, int64_t n,
+                                                        float* __restrict__ b,
+                                                        const float* __restrict__ gb, int64_t nb,
+                                                        float lr, float blr) {
+    const float neg = -lr;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (int64_t)gridDim.x * blockDim.x)
+        M[e] += G[e] * neg;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nb;
+         e += (int64_t)gridDim.x * blockDim.x)
+        b[e] -= gb[e] * lr * blr;
+}
+
+__global__ __launch_bounds__(256) void smf_iota_kernel(int32_t* __restrict__ a, int64_t n) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x)
+        a[x] = (int32_t)x;
+}
+
+__global__ __launch_bounds__(256) void smf_widen_kernel(const int32_t* __restrict__ c, int32_t n,
+                                                        int64_t* __restrict__ out) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x)
+        out[x] = c[x];
+}
+
 // stream[x] = raw[order[x]] for the three SoA columns
 __global__ __launch_bounds__(256) void gather_stream_kernel(
     const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const float* __restrict__ rr,
@@ -669,6 +846,13 @@ struct mml_bmf {
     float gb = 0.0f, min_rating = 0.0f, max_rating = 0.0f;
     float last_ms = 0.0f;
     int32_t last_launches = 0;
+    // SocialMF: the relation and its transpose, the stream positions per user / item in visit
+    // order, the per-rating gradient and the batch gradients
+    mml::DeviceArray<int64_t> conn_off, rev_off, upos_off, ipos_off;
+    mml::DeviceArray<int32_t> conn_cols, rev_cols, upos, ipos;
+    mml::DeviceArray<float> gerr, Ug, Vg, bug, big;
+    int32_t n_conn = 0, n_rev = 0;
+    bool has_positions = false;
 };
 
 namespace {
@@ -731,7 +915,94 @@ void finish_data(mml_bmf* h, const int32_t* order_dev) {
     MML_HIP(hipMemcpyAsync(h->whole_off.get(), off, sizeof(off), hipMemcpyHostToDevice, st));
     MML_HIP(hipStreamSynchronize(st));
     h->G = 0;
+    h->has_positions = false;
     h->has_data = true;
+}
+
+// stream positions grouped by key (users or items) in visit order: stable radix sort of
+// (key, position) pairs, offsets from the per-key counts
+void build_positions(mml_bmf* h, const int32_t* keys, const int32_t* cnt, int32_t n_keys,
+                     mml::DeviceArray<int64_t>& off, mml::DeviceArray<int32_t>& pos) {
+    hipStream_t st = h->ctx->stream;
+    const int64_t n = h->n;
+    off.alloc((size_t)n_keys + 1);
+    pos.alloc(std::max<int64_t>(1, n));
+    MML_HIP(hipMemsetAsync(off.get(), 0, sizeof(int64_t) * (n_keys + 1), st));
+    if (n == 0 || n_keys == 0) return;
+    mml::DeviceArray<int32_t> iota, ksorted;
+    mml::DeviceArray<int64_t> wide;
+    iota.alloc(n);
+    ksorted.alloc(n);
+    wide.alloc(n_keys);
+    smf_iota_kernel<<<grid_for(n), 256, 0, st>>>(iota.get(), n);
+    smf_widen_kernel<<<grid_for(n_keys), 256, 0, st>>>(cnt, n_keys, wide.get());
+    MML_HIP(hipGetLastError());
+    int end_bit = 1;
+    while (end_bit < 31 && (1 << end_bit) < n_keys) ++end_bit;
+    size_t b1 = 0, b2 = 0;
+    MML_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, keys, ksorted.get(), iota.get(),
+                                               pos.get(), (int)n, 0, end_bit, st));
+    MML_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, b2, wide.get(), off.get() + 1, n_keys, st));
+    mml::DeviceArray<uint8_t> tmp;
+    tmp.alloc(std::max(b1, b2));
+    MML_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.get(), b1, keys, ksorted.get(), iota.get(),
+                                               pos.get(), (int)n, 0, end_bit, st));
+    MML_HIP(hipcub::DeviceScan::InclusiveSum(tmp.get(), b2, wide.get(), off.get() + 1, n_keys,
+                                             st));
+    MML_HIP(hipStreamSynchronize(st));
+}
+
+template <int LOSS, int KM>
+void social_epoch_km(mml_bmf* h, const BmfScalars& s) {
+    hipStream_t st = h->ctx->stream;
+    const int64_t n = h->n;
+    if (n > 0) {
+        smf_error_kernel<LOSS><<<grid_for(n), 256, 0, st>>>(
+            h->su.get(), h->si.get(), h->sr.get(), n, h->U.get(), h->V.get(), h->bu.get(),
+            h->bi.get(), h->k, h->ld, s.gb, s.min_rating, s.range, h->gerr.get());
+        MML_HIP(hipGetLastError());
+    }
+    if (h->n_users > 0)
+        smf_user_grad_kernel<KM><<<h->n_users, 64, 0, st>>>(
+            h->upos_off.get(), h->upos.get(), h->si.get(), h->gerr.get(), h->U.get(), h->V.get(),
+            h->bu.get(), h->k, h->ld, s.reg_u, s.bias_reg, h->p.social_regularization,
+            h->conn_off.get(), h->conn_cols.get(), h->n_conn, h->rev_off.get(),
+            h->rev_cols.get(), h->n_rev, h->Ug.get(), h->bug.get());
+    if (h->n_items > 0)
+        smf_item_grad_kernel<KM><<<h->n_items, 64, 0, st>>>(
+            h->ipos_off.get(), h->ipos.get(), h->su.get(), h->gerr.get(), h->U.get(), h->V.get(),
+            h->bi.get(), h->k, h->ld, s.reg_i, s.bias_reg, h->Vg.get(), h->big.get());
+    MML_HIP(hipGetLastError());
+    const float blr = h->p.bias_learn_rate;
+    smf_apply_kernel<<<grid_for((int64_t)h->n_users * h->ld), 256, 0, st>>>(
+        h->U.get(), h->Ug.get(), (int64_t)h->n_users * h->ld, h->bu.get(), h->bug.get(),
+        h->n_users, s.lr, blr);
+    smf_apply_kernel<<<grid_for((int64_t)h->n_items * h->ld), 256, 0, st>>>(
+        h->V.get(), h->Vg.get(), (int64_t)h->n_items * h->ld, h->bi.get(), h->big.get(),
+        h->n_items, s.lr, blr);
+    MML_HIP(hipGetLastError());
+}
+
+// SocialMF.Iterate(IList<int>,bool,bool) -> IterateBatch (SocialMF.cs:72-194), one batch step
+template <int LOSS>
+void social_epoch(mml_bmf* h, const BmfScalars& s) {
+    if (!h->has_positions) {
+        build_positions(h, h->su.get(), h->cnt_u.get(), h->n_users, h->upos_off, h->upos);
+        build_positions(h, h->si.get(), h->cnt_i.get(), h->n_items, h->ipos_off, h->ipos);
+        h->gerr.alloc(std::max<int64_t>(1, h->n));
+        h->Ug.alloc(std::max<size_t>(1, (size_t)h->n_users * h->ld));
+        h->Vg.alloc(std::max<size_t>(1, (size_t)h->n_items * h->ld));
+        h->bug.alloc(std::max<int32_t>(1, h->n_users));
+        h->big.alloc(std::max<int32_t>(1, h->n_items));
+        h->has_positions = true;
+    }
+    switch ((h->k + 63) / 64) {
+        case 1: social_epoch_km<LOSS, 1>(h, s); break;
+        case 2: social_epoch_km<LOSS, 2>(h, s); break;
+        case 3: social_epoch_km<LOSS, 3>(h, s); break;
+        default: social_epoch_km<LOSS, 4>(h, s); break;
+    }
+    h->last_launches = 5;
 }
 
 template <int LOSS>
@@ -859,7 +1130,8 @@ extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params,
                     "num_factors must be in [1, 256]");
         MML_REQUIRE(params->loss >= MML_LOSS_RMSE && params->loss <= MML_LOSS_LOGISTIC,
                     "unknown loss");
-        MML_REQUIRE(params->model == MML_MF_BIASED || params->model == MML_MF_PLAIN,
+        MML_REQUIRE(params->model == MML_MF_BIASED || params->model == MML_MF_PLAIN ||
+                        params->model == MML_MF_SOCIAL,
                     "unknown model family");
         MML_REQUIRE(params->schedule >= MML_SCHEDULE_ORDERED &&
                         params->schedule <= MML_SCHEDULE_HOGWILD_COHERENT,
@@ -1044,7 +1316,7 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
     return guard([&] {
         check_handle(h);
         MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
-        if (h->p.schedule == MML_SCHEDULE_DSGD) {
+        if (h->p.schedule == MML_SCHEDULE_DSGD && h->p.model != MML_MF_SOCIAL) {
             MML_REQUIRE(h->G > 0, "DSGD schedule needs set_blocks");
             MML_REQUIRE(subepoch_sequence, "DSGD schedule needs a sub-epoch sequence");
             for (int32_t x = 0; x < h->G; ++x)
@@ -1063,7 +1335,13 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
         s.reg_i = h->p.reg_i;
         hipStream_t st = h->ctx->stream;
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
-        switch (h->p.model == MML_MF_PLAIN ? kPlainMF : h->p.loss) {
+        if (h->p.model == MML_MF_SOCIAL) {
+            switch (h->p.loss) {
+                case MML_LOSS_MAE: social_epoch<MML_LOSS_MAE>(h, s); break;
+                case MML_LOSS_LOGISTIC: social_epoch<MML_LOSS_LOGISTIC>(h, s); break;
+                default: social_epoch<MML_LOSS_RMSE>(h, s); break;
+            }
+        } else switch (h->p.model == MML_MF_PLAIN ? kPlainMF : h->p.loss) {
             case kPlainMF: run_epoch<kPlainMF>(h, s, subepoch_sequence); break;
             case MML_LOSS_MAE: run_epoch<MML_LOSS_MAE>(h, s, subepoch_sequence); break;
             case MML_LOSS_LOGISTIC: run_epoch<MML_LOSS_LOGISTIC>(h, s, subepoch_sequence); break;
@@ -1330,5 +1608,53 @@ extern "C" mml_status mml_bmf_predict_vectors(mml_bmf* h, int32_t n_vectors, con
         MML_HIP(hipGetLastError());
         MML_HIP(hipMemcpyAsync(out, dout.get(), sizeof(float) * n, hipMemcpyDeviceToHost, st));
         MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+extern "C" mml_status mml_bmf_set_user_relation(mml_bmf* h, int32_t n_rows, const int64_t* offsets,
+                                                const int32_t* cols) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->p.model == MML_MF_SOCIAL, "the user relation belongs to SocialMF handles");
+        MML_REQUIRE(n_rows >= 0 && n_rows <= h->n_users, "relation rows beyond the users");
+        MML_REQUIRE(n_rows == 0 || offsets, "null offsets");
+        const int64_t nnz = n_rows ? offsets[n_rows] : 0;
+        MML_REQUIRE(n_rows == 0 || offsets[0] == 0, "offsets[0] must be 0");
+        for (int32_t r = 0; r < n_rows; ++r)
+            MML_REQUIRE(offsets[r + 1] >= offsets[r], "offsets must be non-decreasing");
+        MML_REQUIRE(nnz == 0 || cols, "null cols");
+        int32_t n_rev = 0;
+        for (int64_t x = 0; x < nnz; ++x) {
+            MML_REQUIRE(cols[x] >= 0 && cols[x] < h->n_users, "relation id beyond the users");
+            n_rev = std::max(n_rev, cols[x] + 1);
+        }
+        // Transpose() (SparseBooleanMatrix.cs:200-207): rows filled by ascending source row
+        std::vector<int64_t> roff((size_t)n_rev + 1, 0);
+        for (int64_t x = 0; x < nnz; ++x) ++roff[(size_t)cols[x] + 1];
+        for (int32_t r = 0; r < n_rev; ++r) roff[r + 1] += roff[r];
+        std::vector<int32_t> rcols((size_t)std::max<int64_t>(1, nnz));
+        std::vector<int64_t> fill(roff.begin(), roff.end() - 1);
+        for (int32_t r = 0; r < n_rows; ++r)
+            for (int64_t x = offsets[r]; x < offsets[r + 1]; ++x) rcols[fill[cols[x]]++] = r;
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        h->conn_off.alloc((size_t)n_rows + 1);
+        h->conn_cols.alloc((size_t)std::max<int64_t>(1, nnz));
+        h->rev_off.alloc((size_t)n_rev + 1);
+        h->rev_cols.alloc((size_t)std::max<int64_t>(1, nnz));
+        if (n_rows)
+            MML_HIP(hipMemcpyAsync(h->conn_off.get(), offsets, sizeof(int64_t) * (n_rows + 1),
+                                   hipMemcpyHostToDevice, st));
+        if (nnz) {
+            MML_HIP(hipMemcpyAsync(h->conn_cols.get(), cols, sizeof(int32_t) * nnz,
+                                   hipMemcpyHostToDevice, st));
+            MML_HIP(hipMemcpyAsync(h->rev_cols.get(), rcols.data(), sizeof(int32_t) * nnz,
+                                   hipMemcpyHostToDevice, st));
+        }
+        MML_HIP(hipMemcpyAsync(h->rev_off.get(), roff.data(), sizeof(int64_t) * (n_rev + 1),
+                               hipMemcpyHostToDevice, st));
+        MML_HIP(hipStreamSynchronize(st));
+        h->n_conn = n_rows;
+        h->n_rev = n_rev;
     });
 }

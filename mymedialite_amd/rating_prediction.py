@@ -110,8 +110,8 @@ class MatrixFactorization(Recommender):
         rng = Random.get_instance()
         U = rng.fill_normal(nu * k, self.InitMean, self.InitStdDev).reshape(nu, k)
         V = rng.fill_normal(ni * k, self.InitMean, self.InitStdDev).reshape(ni, k)
-        U[r.count_by_user == 0] = 0.0
-        V[r.count_by_item == 0] = 0.0
+        U[np.flatnonzero(r.count_by_user == 0)] = 0.0
+        V[np.flatnonzero(r.count_by_item == 0)] = 0.0
         self.current_learnrate = float(np.float32(self.LearnRate))
         self._create_handle(nu, ni)
         self._host = dict(U=U, V=V)
@@ -376,7 +376,8 @@ class BiasedMatrixFactorization(MatrixFactorization):
         f = lambda x: float(np.float32(x))
         return N.BmfParams(int(self.NumFactors), _LOSS[self.Loss], int(self.FrequencyRegularization),
                            _SCHED[self.schedule()], f(self.BiasLearnRate), f(self.BiasReg),
-                           f(self.RegU), f(self.RegI))
+                           f(self.RegU), f(self.RegI), self.MODEL,
+                           f(getattr(self, "SocialRegularization", 0.0)))
 
     def init_model(self):
         """InitModel (MatrixFactorization.cs:99-116 + BiasedMatrixFactorization.cs:161-170)."""
@@ -386,8 +387,8 @@ class BiasedMatrixFactorization(MatrixFactorization):
         rng = Random.get_instance()
         U = rng.fill_normal(nu * k, self.InitMean, self.InitStdDev).reshape(nu, k)
         V = rng.fill_normal(ni * k, self.InitMean, self.InitStdDev).reshape(ni, k)
-        U[r.count_by_user == 0] = 0.0
-        V[r.count_by_item == 0] = 0.0
+        U[np.flatnonzero(r.count_by_user == 0)] = 0.0
+        V[np.flatnonzero(r.count_by_item == 0)] = 0.0
         bu = np.zeros(nu, np.float32)
         bi = np.zeros(ni, np.float32)
         self.current_learnrate = float(np.float32(self.LearnRate))
@@ -581,6 +582,87 @@ class BiasedMatrixFactorization(MatrixFactorization):
             self.FrequencyRegularization, _g(self.LearnRate), _g(self.BiasLearnRate),
             _g(self.Decay), self.NumIter, self.BoldDriver, self.Loss, self.MaxThreads,
             self.NaiveParallelization)
+
+
+class SocialMF(BiasedMatrixFactorization):
+    """GPU-backed MyMediaLite.RatingPrediction.SocialMF (SocialMF.cs:43-254): BiasedMatrixFactorization
+    trained by full-batch gradient descent with a social-network regulariser (IterateBatch
+    :77-194, MML_MF_SOCIAL).  Every gradient element accumulates in the reference's order, so the
+    batch step matches the oracle bit for bit (up to exp rounding).
+
+    ``user_relation``: the UserRelation SparseBooleanMatrix as a list of rows (each row the user's
+    connections in insertion order) or as (offsets, cols).  The batch step uses LearnRate; like the
+    reference, Iterate() still decays current_learnrate, which the step never reads.  BoldDriver
+    (SocialMF's own ComputeObjective, :197-243) and MaxThreads > 1 are not on the GPU path."""
+    PROPERTIES = dict(BiasedMatrixFactorization.PROPERTIES, SocialRegularization="float")
+    MODEL = N.MF_SOCIAL
+    TYPE_NAME = "MyMediaLite.RatingPrediction.SocialMF"
+
+    def __init__(self, **kw):
+        self.SocialRegularization = 1.0  # :47
+        self._relation = (np.zeros(1, np.int64), np.zeros(0, np.int32), 0)
+        super().__init__(**kw)
+
+    @property
+    def user_relation(self):
+        return self._relation
+
+    @user_relation.setter
+    def user_relation(self, rel):
+        if isinstance(rel, tuple):
+            off, cols = np.ascontiguousarray(rel[0], np.int64), np.ascontiguousarray(rel[1], np.int32)
+            self._relation = (off, cols, len(off) - 1)
+            return
+        rows = [list(dict.fromkeys(int(c) for c in r)) for r in rel]  # HashSet: first insertion
+        off = np.zeros(len(rows) + 1, np.int64)
+        off[1:] = np.cumsum([len(r) for r in rows])
+        cols = np.array([c for r in rows for c in r], np.int32)
+        self._relation = (off, cols, len(rows))
+
+    @property
+    def NumUsers(self):
+        return self.MaxUserID + 1
+
+    def init_model(self):
+        """SocialMF.InitModel (:57-69): MaxUserID widened to the relation's rows and columns, then
+        BiasedMatrixFactorization.InitModel."""
+        if self.BoldDriver:
+            raise NotImplementedError("SocialMF with BoldDriver (its own ComputeObjective, "
+                                      ":197-243) is not on the GPU path")
+        if self.MaxThreads > 1:
+            raise NotImplementedError("SocialMF with MaxThreads > 1 is not on the GPU path")
+        off, cols, n_rows = self._relation
+        self.MaxUserID = max(self.MaxUserID, n_rows - 1,
+                             int(cols.max()) if len(cols) else -1)
+        super().init_model()
+
+    def _create_handle(self, nu, ni):
+        super()._create_handle(nu, ni)
+        off, cols, n_rows = self._relation
+        n_rows = min(n_rows, nu)
+        N.check(N.lib().mml_bmf_set_user_relation(self._h, n_rows, N.ptr(off, N._i64p),
+                                                  N.ptr(cols, N._i32p)))
+
+    def schedule(self) -> str:
+        return "ordered"
+
+    def iterate(self):
+        """BiasedMatrixFactorization.Iterate() (:197-222) -> Iterate(RandomIndex, true, true) =
+        IterateBatch (SocialMF.cs:72-194) with LearnRate, then UpdateLearnRate()."""
+        if self._h is None:
+            raise RuntimeError("Train() or init_model() first")
+        self._ensure_data()
+        N.check(N.lib().mml_bmf_iterate(self._h, float(np.float32(self.LearnRate)), None))
+        self._host = None
+        self._update_learn_rate()
+
+    def __str__(self):
+        """ToString() (:246-252)."""
+        return ("SocialMF num_factors={} reg_u={} reg_i={} bias_reg={} social_regularization={} "
+                "learn_rate={} bias_learn_rate={} num_iter={} bold_driver={} loss={}").format(
+            self.NumFactors, _g(self.RegU), _g(self.RegI), _g(self.BiasReg),
+            _g(self.SocialRegularization), _g(self.LearnRate), _g(self.BiasLearnRate),
+            self.NumIter, self.BoldDriver, self.Loss)
 
 
 def _g(x):

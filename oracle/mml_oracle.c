@@ -440,6 +440,117 @@ void ora_mf_predict(const int32_t* users, const int32_t* items, int64_t n, int32
     }
 }
 
+/* ----------------------------------------------------------------------------------------
+ * SocialMF (RatingPrediction/SocialMF.cs): BiasedMatrixFactorization with a social-network
+ * regulariser, trained by full-batch gradient descent (Iterate(IList...) -> IterateBatch :77-194).
+ * user_connections rows (HashSet enumeration = insertion order) as conn CSR over n_conn rows;
+ * rev = its Transpose() (SparseBooleanMatrix.cs:200-207: rows filled by ascending source row).
+ * p->learn_rate = LearnRate (IterateBatch never reads current_learnrate).
+ * ---------------------------------------------------------------------------------------- */
+static int64_t ora_row_len(const int64_t* off, int32_t n_rows, int32_t r) {
+    return r < n_rows ? off[r + 1] - off[r] : 0;
+}
+
+void ora_socialmf_iterate(const ora_bmf_params* p, float social_reg, const int32_t* users,
+                          const int32_t* items, const float* values, const int32_t* idx,
+                          int64_t n_idx, int32_t n_users, int32_t n_items, const int64_t* conn_off,
+                          const int32_t* conn_cols, int32_t n_conn, const int64_t* rev_off,
+                          const int32_t* rev_cols, int32_t n_rev, float* U, float* V, float* bu,
+                          float* bi) {
+    const int k = p->k;
+    float* Ug = (float*)calloc((size_t)n_users * k, sizeof(float));
+    float* Vg = (float*)calloc((size_t)n_items * k, sizeof(float));
+    float* bug = (float*)calloc((size_t)n_users, sizeof(float));
+    float* big = (float*)calloc((size_t)n_items, sizeof(float));
+    float* sum = (float*)malloc(sizeof(float) * (size_t)k);
+    /* I.1 prediction error (:89-115): float score, float prediction, error = prediction - r */
+    for (int64_t n = 0; n < n_idx; n++) {
+        const int32_t index = idx[n];
+        const int32_t u = users[index], i = items[index];
+        float score = (p->global_bias + bu[u]) + bi[i];
+        score += ora_row_scalar_product(U, u, V, i, k);
+        const double sig = 1.0 / (1.0 + exp(-(double)score));
+        const float prediction = (float)((double)p->min_rating + sig * (double)p->rating_range_size);
+        const double err = (double)(prediction - values[index]);
+        float g;
+        if (p->loss == ORA_LOSS_MAE) {
+            const double sgn = (err > 0) ? 1.0 : ((err < 0) ? -1.0 : 0.0);
+            g = (float)(sgn * sig * (1.0 - sig) * (double)p->rating_range_size);
+        } else if (p->loss == ORA_LOSS_LOGISTIC) {
+            g = (float)err;
+        } else {
+            g = (float)(err * sig * (1.0 - sig) * (double)p->rating_range_size);
+        }
+        bug[u] += g;
+        big[i] += g;
+        for (int f = 0; f < k; f++) {
+            Ug[(int64_t)u * k + f] += g * V[(int64_t)i * k + f];
+            Vg[(int64_t)i * k + f] += g * U[(int64_t)u * k + f];
+        }
+    }
+    /* I.2 L2 regularisation (:119-130) */
+    for (int32_t u = 0; u < n_users; u++) bug[u] += bu[u] * p->reg_u * p->bias_reg;
+    for (int32_t i = 0; i < n_items; i++) big[i] += bi[i] * p->reg_i * p->bias_reg;
+    for (int64_t e = 0; e < (int64_t)n_users * k; e++) Ug[e] += U[e] * p->reg_u;
+    for (int64_t e = 0; e < (int64_t)n_items * k; e++) Vg[e] += V[e] * p->reg_i;
+    /* I.3 social regularisation, eq. (13) of the paper (:133-177) */
+    if (social_reg != 0.0f)
+        for (int32_t u = 0; u < n_users; u++) {
+            float bias_sum = 0.0f;
+            for (int f = 0; f < k; f++) sum[f] = 0.0f;
+            const int64_t num = ora_row_len(conn_off, n_conn, u);
+            for (int64_t x = 0; x < num; x++) {
+                const int32_t v = conn_cols[conn_off[u] + x];
+                bias_sum += bu[v];
+                for (int f = 0; f < k; f++) sum[f] += U[(int64_t)v * k + f];
+            }
+            if (num != 0) {
+                bug[u] += social_reg * (bu[u] - bias_sum / (float)num);
+                for (int f = 0; f < k; f++)
+                    Ug[(int64_t)u * k + f] +=
+                        social_reg * (U[(int64_t)u * k + f] - sum[f] / (float)num);
+            }
+            const int64_t nrev = ora_row_len(rev_off, n_rev, u);
+            for (int64_t y = 0; y < nrev; y++) {
+                const int32_t v = rev_cols[rev_off[u] + y];
+                const int64_t cv = ora_row_len(conn_off, n_conn, v);
+                const float trust_v = 1.0f / (float)cv;
+                const float neg_trust_times_reg = -social_reg * trust_v;
+                float bias_diff = 0.0f;
+                for (int f = 0; f < k; f++) sum[f] = 0.0f; /* factor_diffs */
+                for (int64_t x = 0; x < cv; x++) {
+                    const int32_t w = conn_cols[conn_off[v] + x];
+                    bias_diff -= bu[w];
+                    for (int f = 0; f < k; f++) sum[f] -= U[(int64_t)w * k + f];
+                }
+                bias_diff *= trust_v;
+                bias_diff += bu[v];
+                bug[u] += neg_trust_times_reg * bias_diff;
+                for (int f = 0; f < k; f++) {
+                    sum[f] *= trust_v;
+                    sum[f] += U[(int64_t)v * k + f];
+                    Ug[(int64_t)u * k + f] += neg_trust_times_reg * sum[f];
+                }
+            }
+        }
+    /* II. gradient step with LearnRate (:180-193) */
+    if (p->update_user) {
+        for (int32_t u = 0; u < n_users; u++)
+            bu[u] -= bug[u] * p->learn_rate * p->bias_learn_rate;
+        for (int64_t e = 0; e < (int64_t)n_users * k; e++) U[e] += Ug[e] * -p->learn_rate;
+    }
+    if (p->update_item) {
+        for (int32_t i = 0; i < n_items; i++)
+            bi[i] -= big[i] * p->learn_rate * p->bias_learn_rate;
+        for (int64_t e = 0; e < (int64_t)n_items * k; e++) V[e] += Vg[e] * -p->learn_rate;
+    }
+    free(Ug);
+    free(Vg);
+    free(bug);
+    free(big);
+    free(sum);
+}
+
 /* MultiCore.PartitionUsersAndItems (MultiCore.cs:43-73).  Produces blocks as a CSR over
  * block id b = ug * G + ig: offsets[G*G+1], indices[n].  Returns G (clipped). */
 int32_t ora_partition_users_and_items(ora_rng* r, const int32_t* users, const int32_t* items,

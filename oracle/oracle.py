@@ -79,6 +79,10 @@ def lib():
         L.ora_mf_predict_vector.restype = ctypes.c_float
         L.ora_mf_predict_vector.argtypes = [ctypes.c_int, ctypes.c_float, ctypes.c_float,
                                             ctypes.c_float, _f32p, ctypes.c_int32, _f32p]
+        L.ora_socialmf_iterate.argtypes = [ctypes.c_void_p, ctypes.c_float, _i32p, _i32p, _f32p,
+                                           _i32p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                           _i64p, _i32p, ctypes.c_int32, _i64p, _i32p,
+                                           ctypes.c_int32, _f32p, _f32p, _f32p, _f32p]
         L.ora_mf_iterate.argtypes = [ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                      ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f32p, _i32p,
                                      ctypes.c_int64, _f32p, _f32p]
@@ -395,6 +399,69 @@ def mf_train(users, items, values, n_users, n_items, *, seed=1, k=10, learn_rate
         if callback is not None:
             callback(epoch, state)
     state.update(global_bias=gb, random_index=random_index, current_learnrate=lr, rng=rng)
+    return state
+
+
+def relation_csr(rows):
+    """SparseBooleanMatrix rows (HashSet<int> per row, enumeration = first-insertion order) given
+    as a list of lists -> (off, cols, n_rows); and its Transpose() (SparseBooleanMatrix.cs:200-207):
+    rows filled by ascending source row."""
+    seen = [list(dict.fromkeys(r)) for r in rows]
+    off = np.zeros(len(seen) + 1, np.int64)
+    off[1:] = np.cumsum([len(r) for r in seen])
+    cols = np.array([c for r in seen for c in r], np.int32)
+    n_t = int(cols.max()) + 1 if len(cols) else 0
+    t = [[] for _ in range(n_t)]
+    for src, r in enumerate(seen):
+        for c in r:
+            t[c].append(src)
+    toff = np.zeros(n_t + 1, np.int64)
+    toff[1:] = np.cumsum([len(r) for r in t])
+    tcols = np.array([c for r in t for c in r], np.int32)
+    return (off, cols, len(seen)), (toff, tcols, n_t)
+
+
+def socialmf_train(users, items, values, n_users, n_items, min_rating, max_rating, relation, *,
+                   seed=1, k=10, learn_rate=0.01, decay=1.0, reg_u=0.015, reg_i=0.015,
+                   bias_reg=0.01, bias_learn_rate=1.0, social_reg=1.0, num_iter=30,
+                   init_mean=0.0, init_stddev=0.1, loss=0, callback=None):
+    """SocialMF.Train: InitModel (SocialMF.cs:57-69: MaxUserID widened by the relation, then
+    BiasedMatrixFactorization.InitModel), the global bias of BiasedMatrixFactorization.Train
+    (:173-194), then NumIter x Iterate() -> IterateBatch over RandomIndex (SocialMF.cs:72-194)
+    with LearnRate; UpdateLearnRate still decays current_learnrate (unused by the batch step)."""
+    users, items, values = i32(users), i32(items), f32(values)
+    (coff, ccols, nconn), (roff, rcols, nrev) = relation_csr(relation)
+    n_users = max(n_users, nconn, nrev)
+    rng = Rng(seed)
+    U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
+    V = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
+    cu = np.bincount(users, minlength=int(users.max()) + 1)
+    ci = np.bincount(items, minlength=n_items)
+    U[np.flatnonzero(cu == 0)] = 0
+    V[np.flatnonzero(ci == 0)] = 0
+    bu = np.zeros(n_users, np.float32)
+    bi = np.zeros(n_items, np.float32)
+    state = dict(U=U, V=V, bu=bu, bi=bi, init_U=U.copy(), init_V=V.copy())
+    range_ = np.float32(np.float32(max_rating) - np.float32(min_rating))
+    s = ratings_average_exact(values)
+    avg_f = np.float32(np.float32(s) / np.float32(len(values)))
+    avg = np.float32(np.float32(avg_f - np.float32(min_rating)) / range_)
+    gb = np.float32(math.log(float(avg) / (1.0 - float(avg))))
+    p = _BmfParams(k, loss, 0, 1, 1, gb, min_rating, range_, learn_rate, bias_learn_rate,
+                   bias_reg, reg_u, reg_i)
+    random_index = rng.shuffle(np.arange(len(users), dtype=np.int32))
+    lr = np.float32(learn_rate)
+    for epoch in range(num_iter):
+        lib().ora_socialmf_iterate(ctypes.byref(p), float(social_reg), _p(users, _i32p),
+                                   _p(items, _i32p), _p(values, _f32p), _p(random_index, _i32p),
+                                   len(random_index), n_users, n_items, _p(coff, _i64p),
+                                   _p(ccols, _i32p), nconn, _p(roff, _i64p), _p(rcols, _i32p),
+                                   nrev, _p(U, _f32p), _p(V, _f32p), _p(bu, _f32p), _p(bi, _f32p))
+        lr = np.float32(lr * np.float32(decay))
+        if callback is not None:
+            callback(epoch, state)
+    state.update(global_bias=gb, range_=range_, random_index=random_index, current_learnrate=lr,
+                 n_users=n_users)
     return state
 
 

@@ -149,6 +149,28 @@ def case_mf_synth_k10():
     return _mf_case(u, i, v, (tu, ti, tv), seed=6, k=10, num_iter=4, learn_rate=0.02)
 
 
+def social_relation(seed, n_rows, n_ids, max_deg=5):
+    """A user relation (rows of connections in insertion order) incl. users only in the relation."""
+    rs = np.random.default_rng(seed)
+    return [[int(c) for c in rs.choice(n_ids, size=int(rs.integers(0, max_deg + 1)),
+                                       replace=False)] for _ in range(n_rows)]
+
+
+def case_socialmf_small():
+    u, i, v = synth_ratings(61, 60, 40, 1500)
+    rel = social_relation(3, 62, 65)
+    snaps = {}
+
+    def cb(epoch, st):
+        for key in ("U", "V", "bu", "bi"):
+            snaps[f"{key}{epoch + 1}"] = st[key].copy()
+
+    st = O.socialmf_train(u, i, v, 60, 40, 1.0, 5.0, rel, seed=2, k=6, num_iter=3, callback=cb)
+    off, cols, _ = O.relation_csr(rel)[0]
+    return dict(users=u, items=i, values=v, rel_off=off, rel_cols=cols, init_U=st["init_U"],
+                init_V=st["init_V"], global_bias=np.float32(st["global_bias"]), **snaps)
+
+
 def case_bpr_small():
     u, i = synth_feedback(21, 30, 20, 8)
     nu, ni = int(u.max()) + 1, int(i.max()) + 1
@@ -188,6 +210,7 @@ CASES = {
     "bmf_synth_dsgd4": case_bmf_synth_dsgd4,
     "mf_example_k3": case_mf_example_k3,
     "mf_synth_k10": case_mf_synth_k10,
+    "socialmf_small": case_socialmf_small,
     "bpr_small": case_bpr_small,
     "bpr_soft_margin_small": case_bpr_soft_margin_small,
     "bpr_weighted_small": case_bpr_weighted_small,
