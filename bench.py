@@ -63,6 +63,10 @@ def main():
     ap.add_argument("--schedule", default="hogwild", choices=["hogwild", "ordered"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--sampler", default="uniform_user",
+                    choices=["uniform_user", "uniform_pair", "user_replacement",
+                             "pair_replacement"],
+                    help="C3 only: BPRMF's Iterate() variant (BPRMF.cs:160-268)")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
                     help="c2 (default; N>1 = C4 weak scaling): BiasedMF; c3: BPRMF k=128; "
                          "c5: WRMF k=256")
@@ -293,7 +297,11 @@ def bench_bpr(args):
         x = torch.rand(e - s0, generator=g, device=dev, dtype=torch.float64)
         items[s0:e] = perm[torch.searchsorted(cdf, x).clamp_(max=n_items - 1)].to(torch.int32)
     torch.cuda.synchronize()
-    p = N.BprParams(k, N.BPR_SAMPLER_UNIFORM_USER, 1, 0.05, 0.0025, 0.0025, 0.00025, 0.0)
+    sampler = {"uniform_user": N.BPR_SAMPLER_UNIFORM_USER,
+               "uniform_pair": N.BPR_SAMPLER_UNIFORM_PAIR,
+               "user_replacement": N.BPR_SAMPLER_USER_REPLACEMENT,
+               "pair_replacement": N.BPR_SAMPLER_PAIR_REPLACEMENT}[args.sampler]
+    p = N.BprParams(k, sampler, 1, 0.05, 0.0025, 0.0025, 0.00025, 0.0)
     h = N._vp()
     N.check(N.lib().mml_bpr_create(ctx.handle, ctypes.byref(p), n_users, n_items,
                                    ctypes.byref(h)))
@@ -331,7 +339,9 @@ def bench_bpr(args):
         "data": "synthetic (users uniform, items Zipf(0.8), generated in HBM)",
         "config": {"workload": "C3: BPRMF 10M users x 1M items, 500M positives, k=128",
                    "num_factors": k, "events": n, "users": n_users, "items": n_items,
-                   "sampler": "uniform_user (BPRMF default)", "device_ingest_s": ingest_s},
+                   "sampler": args.sampler + (" (BPRMF default)" if args.sampler ==
+                                              "uniform_user" else ""),
+                   "device_ingest_s": ingest_s},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": f"bpr_update_kernel<{max(1, (k + 3) // 4)}>",

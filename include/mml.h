@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 2
+#define MML_ABI_VERSION 3
 
 typedef int32_t mml_status;
 enum {
@@ -226,8 +226,14 @@ enum {
     MML_BPR_SAMPLER_UNIFORM_USER = 0, /* default: IterateWithoutReplacementUniformUser (BPRMF.cs:216-226) */
     MML_BPR_SAMPLER_UNIFORM_PAIR = 1, /* IterateWithoutReplacementUniformPair over the visit order
                                          (:248-268; MultiCoreBPRMF's sampler, MultiCoreBPRMF.cs:49-63) */
-    MML_BPR_SAMPLER_WEIGHTED = 2      /* WeightedBPRMF.SampleTriple (WeightedBPRMF.cs:55-67): (u, i) a
+    MML_BPR_SAMPLER_WEIGHTED = 2,     /* WeightedBPRMF.SampleTriple (WeightedBPRMF.cs:55-67): (u, i) a
                                          uniform event, j the item of a uniform event, not in S_u */
+    MML_BPR_SAMPLER_USER_REPLACEMENT = 3, /* IterateWithReplacementUniformUser (BPRMF.cs:183-211):
+                                         u uniform; i drawn WITHOUT repetition from the user's
+                                         remaining items of this epoch, the set refilled when
+                                         exhausted; j uniform outside S_u (ABI 3) */
+    MML_BPR_SAMPLER_PAIR_REPLACEMENT = 4  /* IterateWithReplacementUniformPair (:231-243): (u, i) the
+                                         event at a uniform index, j = SampleOtherItem (ABI 3) */
 };
 /* How an epoch's sampled triples are applied (ABI 2) */
 enum {
@@ -293,6 +299,10 @@ mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const int32_t* item
 /* out[0] = the last epoch's device time (ms), out[1] = its update kernel alone (the rest is the
  * triple sampler) */
 mml_status mml_bpr_last_timing(mml_bpr* h, float* out);
+/* The last epoch's sampled triples in sample order (n = Feedback.Count), e.g. for BPRMF's
+ * loss_sample_* arrays (BPRMF.cs:136-150) or to check a sampler's distribution (ABI 3). */
+mml_status mml_bpr_last_triples(mml_bpr* h, int32_t* users, int32_t* items, int32_t* other_items,
+                                int64_t n);
 /* Eval.Items.Evaluate's AUC (Eval/Items.cs:126-209 + Recommender.Recommend n = -1 +
  * Eval/Measures/AUC.cs:42-68) on the device for the eval users: candidates = the already shuffled
  * candidate list (Items.Candidates, :62-96), the users' test items as CSR (test_off[n_users + 1],

@@ -56,6 +56,7 @@ class BprParams(ctypes.Structure):
 
 
 BPR_SAMPLER_UNIFORM_USER, BPR_SAMPLER_UNIFORM_PAIR, BPR_SAMPLER_WEIGHTED = 0, 1, 2
+BPR_SAMPLER_USER_REPLACEMENT, BPR_SAMPLER_PAIR_REPLACEMENT = 3, 4
 BPR_MODEL_BPR, BPR_MODEL_SOFT_MARGIN = 0, 1
 BPR_SCHEDULE_AUTO, BPR_SCHEDULE_HOGWILD, BPR_SCHEDULE_ORDERED = 0, 1, 2
 
@@ -125,6 +126,7 @@ SIGNATURES = {
     "mml_bpr_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
     "mml_bpr_apply_triples": (_st, [_vp, _i32p, _i32p, _i32p, ctypes.c_int64]),
     "mml_bpr_last_timing": (_st, [_vp, _f32p]),
+    "mml_bpr_last_triples": (_st, [_vp, _i32p, _i32p, _i32p, ctypes.c_int64]),
     "mml_bpr_auc": (_st, [_vp, _i32p, ctypes.c_int32, _i32p, ctypes.c_int32, _i64p, _i32p,
                           _f64p]),
     "mml_bpr_allreduce_items": (_st, [_vp]),

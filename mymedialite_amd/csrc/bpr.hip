@@ -21,9 +21,20 @@
 //   j ~ Uniform(I \ S_u)       == SampleItemPair / SampleOtherItem's rejection loop
 // Parity is therefore statistical (AUC, tests/test_bpr_gpu.py).
 //
+// The WithReplacement = true samplers (:183-211, :231-243; MML_BPR_SAMPLER_*_REPLACEMENT):
+//   PAIR_REPLACEMENT  (u, i) = the event at a uniform index, j as above
+//   USER_REPLACEMENT  u as above; i = the next item of the user's current round: the reference
+//                     removes each drawn item from an epoch-local copy of S_u and refills the copy
+//                     once it is empty, so a user's k-th sample of the epoch takes position k mod
+//                     |S_u| of round floor(k / |S_u|), each round a fresh keyed permutation of S_u.
+//                     k (the sample's rank among its user's samples, in sample order) comes from a
+//                     stable radix sort of (u << 32 | s).
+//
 // Update (Hogwild!, LPR lanes per triple, one float4 per lane of U_u, V_i, V_j): the reference's
 // float/double arithmetic -- x_uij = (b_i - b_j) + sum_f (double)(w_f * (h_if - h_jf)), double
 // sigmoid, double deltas, float stores -- with the f-sum as per-lane partials + xor butterfly.
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
@@ -82,6 +93,28 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 __device__ __forceinline__ uint32_t draw(uint64_t seed, uint64_t s, uint32_t d, uint32_t n) {
     const uint64_t x = splitmix64(seed ^ (s * 0xD1B54A32D192ED03ull + d));
     return (uint32_t)(((x >> 32) * (uint64_t)n) >> 32);
+}
+
+// A keyed bijection of [0, n): three rounds of xor / odd multiply / xorshift on the next power of
+// two, cycle-walked back into [0, n) (the walk from x < n stays on x's cycle, < 2 steps expected).
+__device__ __forceinline__ uint32_t keyed_perm(uint32_t x, uint32_t n, uint64_t key) {
+    if (n <= 1) return 0;
+    const int b = 32 - __clz(n - 1);
+    const uint32_t mask = b >= 32 ? 0xffffffffu : ((1u << b) - 1u);
+    const int sh = b > 1 ? b / 2 : 1;
+    const uint64_t k1 = splitmix64(key), k2 = splitmix64(k1), k3 = splitmix64(k2);
+    auto rounds = [&](uint32_t v) {
+        v = ((v ^ (uint32_t)k1) * ((uint32_t)(k1 >> 32) | 1u)) & mask;
+        v ^= v >> sh;
+        v = ((v ^ (uint32_t)k2) * ((uint32_t)(k2 >> 32) | 1u)) & mask;
+        v ^= v >> sh;
+        v = ((v ^ (uint32_t)k3) * ((uint32_t)(k3 >> 32) | 1u)) & mask;
+        v ^= v >> sh;
+        return v;
+    };
+    uint32_t y = rounds(x);
+    while (y >= n) y = rounds(y);
+    return y;
 }
 
 // is item j in the sorted row [b, e)?  The LPR lanes of a group test a window of LPR entries per
@@ -227,14 +260,15 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
     const int32_t* __restrict__ eligible, int32_t n_eligible, const int32_t* __restrict__ ev_u,
     const int32_t* __restrict__ ev_i, int64_t n_samples, int32_t n_items, uint64_t seed,
     int32_t* __restrict__ tu, int32_t* __restrict__ ti, int32_t* __restrict__ tj,
-    int32_t* __restrict__ fail) {
+    int32_t* __restrict__ fail, uint64_t* __restrict__ user_keys) {
     for (int64_t smp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; smp < n_samples;
          smp += (int64_t)gridDim.x * blockDim.x) {
         int32_t u, i = 0, j = 0;
         if constexpr (SAMPLER == MML_BPR_SAMPLER_UNIFORM_PAIR) {
             u = ev_u[smp];
             i = ev_i[smp];
-        } else if constexpr (SAMPLER == MML_BPR_SAMPLER_WEIGHTED) {
+        } else if constexpr (SAMPLER == MML_BPR_SAMPLER_WEIGHTED ||
+                             SAMPLER == MML_BPR_SAMPLER_PAIR_REPLACEMENT) {
             const uint32_t e = draw(seed, smp, 0, (uint32_t)n_samples);
             u = ev_u[e];
             i = ev_i[e];
@@ -245,6 +279,9 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
         const int64_t rb = off[u], re = off[u + 1];
         if constexpr (SAMPLER == MML_BPR_SAMPLER_UNIFORM_USER)
             i = cols[rb + draw(seed, smp, 1, (uint32_t)(re - rb))];
+        // USER_REPLACEMENT: i is resolved after the epoch's samples are ranked per user
+        if constexpr (SAMPLER == MML_BPR_SAMPLER_USER_REPLACEMENT)
+            user_keys[smp] = ((uint64_t)(uint32_t)u << 32) | (uint32_t)smp;
         if constexpr (SAMPLER == MML_BPR_SAMPLER_WEIGHTED) {
             uint32_t d = 1;
             for (; d <= kMaxWeightedDraws; ++d) {
@@ -262,8 +299,40 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
             }
         }
         tu[smp] = u;
-        ti[smp] = i;
+        if constexpr (SAMPLER != MML_BPR_SAMPLER_USER_REPLACEMENT) ti[smp] = i;
         tj[smp] = j;
+    }
+}
+
+// USER_REPLACEMENT, after a stable sort of the keys (u << 32 | s) by u: head[u] = the position
+// of user u's first sample, so sample s's rank among its user's samples is its position - head[u]
+__global__ __launch_bounds__(256) void bpr_user_heads_kernel(const uint64_t* __restrict__ sorted,
+                                                             int64_t n, int64_t* __restrict__ head) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
+         p += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t u = (uint32_t)(sorted[p] >> 32);
+        if (p == 0 || (uint32_t)(sorted[p - 1] >> 32) != u) head[u] = p;
+    }
+}
+
+// i of every USER_REPLACEMENT sample: rank r -> round r / deg, position r mod deg of that round's
+// keyed permutation of S_u (IterateWithReplacementUniformUser, BPRMF.cs:190-203: draw from the
+// remaining items, forget the drawn one, refill the user's copy when it is empty)
+__global__ __launch_bounds__(256) void bpr_resolve_user_replacement_kernel(
+    const uint64_t* __restrict__ sorted, int64_t n, const int64_t* __restrict__ head,
+    const int64_t* __restrict__ off, const int32_t* __restrict__ cols, uint64_t seed,
+    int32_t* __restrict__ ti) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
+         p += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t key = sorted[p];
+        const uint32_t u = (uint32_t)(key >> 32), s = (uint32_t)key;
+        const uint32_t r = (uint32_t)(p - head[u]);
+        const int64_t b = off[u];
+        const uint32_t deg = (uint32_t)(off[u + 1] - b);
+        const uint32_t round = r / deg, pos = r - round * deg;
+        const uint64_t rk = splitmix64(seed ^ ((uint64_t)u * 0x9E3779B97F4A7C15ull) ^
+                                       ((uint64_t)round << 40) ^ 0x2545F4914F6CDD1Dull);
+        ti[s] = cols[b + keyed_perm(pos, deg, rk)];
     }
 }
 
@@ -437,9 +506,12 @@ struct mml_bpr {
     mml::DeviceArray<int32_t> cols, eligible, ev_u, ev_i, q_u, q_i;
     mml::DeviceArray<int32_t> tri_u, tri_i, tri_j;  // the epoch's triples (two-phase epoch)
     mml::DeviceArray<int32_t> fail;                 // WEIGHTED sampler: a sample ran out of draws
+    mml::DeviceArray<uint64_t> rank_keys, rank_sorted;  // USER_REPLACEMENT: (u << 32 | s)
+    mml::DeviceArray<int64_t> rank_head;                // USER_REPLACEMENT: first position per user
+    mml::DeviceArray<uint8_t> rank_tmp;                 // its radix-sort scratch
     int64_t n_events = 0, nnz = 0;
     int32_t n_eligible = 0;
-    bool has_data = false, has_model = false, has_order = false;
+    bool has_data = false, has_model = false, has_order = false, has_triples = false;
     float last_ms = 0.0f, last_update_ms = 0.0f;
 };
 
@@ -469,9 +541,8 @@ extern "C" mml_status mml_bpr_create(mml_ctx* ctx, const mml_bpr_params* params,
         MML_REQUIRE(n_users >= 1 && n_items >= 2, "need >= 1 user and >= 2 items");
         MML_REQUIRE(params->num_factors >= 1 && params->num_factors <= 256,
                     "num_factors must be in [1, 256]");
-        MML_REQUIRE(params->sampler == MML_BPR_SAMPLER_UNIFORM_USER ||
-                        params->sampler == MML_BPR_SAMPLER_UNIFORM_PAIR ||
-                        params->sampler == MML_BPR_SAMPLER_WEIGHTED,
+        MML_REQUIRE(params->sampler >= MML_BPR_SAMPLER_UNIFORM_USER &&
+                        params->sampler <= MML_BPR_SAMPLER_PAIR_REPLACEMENT,
                     "unknown sampler");
         MML_REQUIRE(params->model == MML_BPR_MODEL_BPR ||
                         params->model == MML_BPR_MODEL_SOFT_MARGIN,
@@ -543,7 +614,12 @@ void bpr_ingest(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t 
     h->eligible.alloc(elig.size());
     MML_HIP(hipMemcpyAsync(h->eligible.get(), elig.data(), sizeof(int32_t) * elig.size(),
                            hipMemcpyHostToDevice, st));
-    if (h->p.sampler != MML_BPR_SAMPLER_UNIFORM_USER) {  // PAIR: visit order; WEIGHTED: any order
+    MML_REQUIRE(h->p.sampler != MML_BPR_SAMPLER_USER_REPLACEMENT || n <= (int64_t)UINT32_MAX,
+                "USER_REPLACEMENT ranks samples with 32-bit indices: at most 2^32 - 1 events");
+    h->has_triples = false;
+    // PAIR: visit order; WEIGHTED / PAIR_REPLACEMENT: any order (events drawn by index)
+    if (h->p.sampler != MML_BPR_SAMPLER_UNIFORM_USER &&
+        h->p.sampler != MML_BPR_SAMPLER_USER_REPLACEMENT) {
         h->ev_u.alloc(n);
         h->ev_i.alloc(n);
         bpr_gather_events_kernel<<<grid_for(n), 256, 0, st>>>(users, items, order, n,
@@ -587,8 +663,9 @@ extern "C" mml_status mml_bpr_set_data_device(mml_bpr* h, const int32_t* users,
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
         MML_REQUIRE(n >= 1 && users && items, "need >= 1 event");
-        MML_REQUIRE(!order || h->p.sampler != MML_BPR_SAMPLER_UNIFORM_USER,
-                    "a device order is not used by the UNIFORM_USER sampler");
+        MML_REQUIRE(!order || (h->p.sampler != MML_BPR_SAMPLER_UNIFORM_USER &&
+                               h->p.sampler != MML_BPR_SAMPLER_USER_REPLACEMENT),
+                    "a device order is not used by the user-sampling samplers");
         h->ctx->activate();
         h->has_data = false;
         bpr_ingest(h, users, items, n, order);
@@ -735,6 +812,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         const bool pair = h->p.sampler == MML_BPR_SAMPLER_UNIFORM_PAIR;
         const bool soft = h->p.model == MML_BPR_MODEL_SOFT_MARGIN;
         const bool weighted = h->p.sampler == MML_BPR_SAMPLER_WEIGHTED;
+        const bool user_repl = h->p.sampler == MML_BPR_SAMPLER_USER_REPLACEMENT;
         static const bool fused_env = [] {
             const char* e = std::getenv("MML_BPR_FUSED");
             return e && std::atoi(e) > 0;
@@ -744,11 +822,29 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         const bool ordered = h->p.schedule == MML_BPR_SCHEDULE_ORDERED ||
                              (h->p.schedule == MML_BPR_SCHEDULE_AUTO && n < kAutoOrderedBelow);
         // the fused single-kernel epoch exists for the BPRMF update with the uniform samplers
-        const bool fused = fused_env && !soft && !weighted && !ordered;
+        const bool fused = fused_env && !soft && !ordered &&
+                           (pair || h->p.sampler == MML_BPR_SAMPLER_UNIFORM_USER);
         if (!fused && n > 0 && (int64_t)h->tri_u.count < n) {
             h->tri_u.alloc(n);
             h->tri_i.alloc(n);
             h->tri_j.alloc(n);
+        }
+        // USER_REPLACEMENT: rank keys, their sorted copy, per-user heads and the sort's scratch
+        int rank_end_bit = 0;
+        size_t rank_tmp_bytes = 0;
+        if (user_repl && n > 0) {
+            if ((int64_t)h->rank_keys.count < n) {
+                h->rank_keys.alloc(n);
+                h->rank_sorted.alloc(n);
+            }
+            h->rank_head.alloc(h->n_users);
+            int ub = 0;
+            while (ub < 32 && ((uint32_t)(h->n_users - 1) >> ub) != 0) ++ub;
+            rank_end_bit = 32 + std::max(ub, 1);
+            MML_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, rank_tmp_bytes, h->rank_keys.get(),
+                                                      h->rank_sorted.get(), n, 32, rank_end_bit,
+                                                      st));
+            if (h->rank_tmp.count < rank_tmp_bytes) h->rank_tmp.alloc(rank_tmp_bytes);
         }
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
         if (!fused && n > 0) {
@@ -760,14 +856,35 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
 #define MML_SMP(KIND, ELIG)                                                                     \
     bpr_sample_kernel<KIND><<<sgrid, 256, 0, st>>>(                                            \
         h->off.get(), h->cols.get(), ELIG, h->n_eligible, h->ev_u.get(), h->ev_i.get(), n,    \
-        h->n_items, seed, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), h->fail.get())
-            if (pair) MML_SMP(MML_BPR_SAMPLER_UNIFORM_PAIR, h->eligible.get());
-            else if (weighted) MML_SMP(MML_BPR_SAMPLER_WEIGHTED, nullptr);
-            else
-                MML_SMP(MML_BPR_SAMPLER_UNIFORM_USER,
-                        h->n_eligible == h->n_users ? nullptr : h->eligible.get());
+        h->n_items, seed, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), h->fail.get(),       \
+        h->rank_keys.get())
+            int32_t* elig = h->n_eligible == h->n_users ? nullptr : h->eligible.get();
+            switch (h->p.sampler) {
+                case MML_BPR_SAMPLER_UNIFORM_PAIR:
+                    MML_SMP(MML_BPR_SAMPLER_UNIFORM_PAIR, h->eligible.get());
+                    break;
+                case MML_BPR_SAMPLER_WEIGHTED: MML_SMP(MML_BPR_SAMPLER_WEIGHTED, nullptr); break;
+                case MML_BPR_SAMPLER_USER_REPLACEMENT:
+                    MML_SMP(MML_BPR_SAMPLER_USER_REPLACEMENT, elig);
+                    break;
+                case MML_BPR_SAMPLER_PAIR_REPLACEMENT:
+                    MML_SMP(MML_BPR_SAMPLER_PAIR_REPLACEMENT, nullptr);
+                    break;
+                default: MML_SMP(MML_BPR_SAMPLER_UNIFORM_USER, elig); break;
+            }
 #undef MML_SMP
             MML_HIP(hipGetLastError());
+            if (user_repl) {
+                MML_HIP(hipcub::DeviceRadixSort::SortKeys(h->rank_tmp.get(), rank_tmp_bytes,
+                                                          h->rank_keys.get(), h->rank_sorted.get(),
+                                                          n, 32, rank_end_bit, st));
+                bpr_user_heads_kernel<<<sgrid, 256, 0, st>>>(h->rank_sorted.get(), n,
+                                                             h->rank_head.get());
+                bpr_resolve_user_replacement_kernel<<<sgrid, 256, 0, st>>>(
+                    h->rank_sorted.get(), n, h->rank_head.get(), h->off.get(), h->cols.get(), seed,
+                    h->tri_i.get());
+                MML_HIP(hipGetLastError());
+            }
             if (weighted) {
                 int32_t bad = 0;
                 MML_HIP(hipMemcpyAsync(&bad, h->fail.get(), sizeof(int32_t),
@@ -818,6 +935,27 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         MML_HIP(hipEventSynchronize(h->ctx->ev_end));
         MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));
         MML_HIP(hipEventElapsedTime(&h->last_update_ms, h->ctx->ev_mid, h->ctx->ev_end));
+        h->has_triples = !fused && n > 0;
+    });
+}
+
+extern "C" mml_status mml_bpr_last_triples(mml_bpr* h, int32_t* users, int32_t* items,
+                                           int32_t* other_items, int64_t n) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(h->has_triples, "no sampled epoch to report (run mml_bpr_iterate first; the "
+                                    "MML_BPR_FUSED epoch keeps no triples)");
+        MML_REQUIRE(n == h->n_events && users && items && other_items,
+                    "n must equal the epoch's sample count (Feedback.Count)");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        MML_HIP(hipMemcpyAsync(users, h->tri_u.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost,
+                               st));
+        MML_HIP(hipMemcpyAsync(items, h->tri_i.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost,
+                               st));
+        MML_HIP(hipMemcpyAsync(other_items, h->tri_j.get(), sizeof(int32_t) * n,
+                               hipMemcpyDeviceToHost, st));
+        MML_HIP(hipStreamSynchronize(st));
     });
 }
 

@@ -223,11 +223,20 @@ class BPRMF(_MFBase):
         self._host = None
 
     def _sampler(self) -> int:
-        if self.WithReplacement:
-            raise NotImplementedError(
-                "WithReplacement=true samplers (BPRMF.cs:183-211, :231-243) are not on the GPU path")
-        return N.BPR_SAMPLER_UNIFORM_USER if self.UniformUserSampling else \
+        """Iterate()'s dispatch (BPRMF.cs:160-178) on UniformUserSampling x WithReplacement."""
+        if self.UniformUserSampling:
+            return N.BPR_SAMPLER_USER_REPLACEMENT if self.WithReplacement else \
+                N.BPR_SAMPLER_UNIFORM_USER
+        return N.BPR_SAMPLER_PAIR_REPLACEMENT if self.WithReplacement else \
             N.BPR_SAMPLER_UNIFORM_PAIR
+
+    def last_triples(self):
+        """The last epoch's sampled (u, i, j) triples in sample order (mml_bpr_last_triples)."""
+        n = self._feedback.count
+        u, i, j = (np.empty(n, np.int32) for _ in range(3))
+        N.check(N.lib().mml_bpr_last_triples(self._h, N.ptr(u, N._i32p), N.ptr(i, N._i32p),
+                                             N.ptr(j, N._i32p), n))
+        return u, i, j
 
     def init_model(self):
         """InitModel (BPRMF.cs:121-126): MF factors + zero item biases; data to the device."""
@@ -242,7 +251,7 @@ class BPRMF(_MFBase):
         self._h = h
         fb = self._feedback
         order = None
-        if not self.UniformUserSampling:  # Feedback.RandomIndex (:250), shuffled once
+        if self._sampler() == N.BPR_SAMPLER_UNIFORM_PAIR:  # Feedback.RandomIndex (:250), once
             order = Random.get_instance().shuffle(np.arange(fb.count, dtype=np.int32))
         N.check(N.lib().mml_bpr_set_data(h, N.ptr(fb.users, N._i32p), N.ptr(fb.items, N._i32p),
                                          fb.count, N.ptr(order, N._i32p)))

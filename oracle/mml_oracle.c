@@ -642,7 +642,8 @@ typedef struct {
     float learn_rate, reg_u, reg_i, reg_j, bias_reg;
     int32_t max_user_id, max_item_id;
     int32_t model;   /* 0 BPRMF, 1 SoftMarginRankingMF (UpdateFactors) */
-    int32_t sampler; /* 0 SampleTriple of BPRMF, 2 WeightedBPRMF.SampleTriple */
+    int32_t sampler; /* 0 SampleTriple of BPRMF, 2 WeightedBPRMF.SampleTriple,
+                        3 IterateWithReplacementUniformUser, 4 IterateWithReplacementUniformPair */
     const int32_t* ev_users; /* Feedback.Users / Feedback.Items (event order), sampler 2 */
     const int32_t* ev_items;
     int64_t n_events;
@@ -772,14 +773,72 @@ void ora_bpr_burn(ora_rng* r, const ora_bpr_params* p, const int64_t* off, const
     for (int64_t c = 0; c < count; c++) ora_bpr_sample_triple(r, p, off, rows, sorted, t);
 }
 
-/* IterateWithoutReplacementUniformUser :216-226 -- num_events triples, each sampled then applied.
- * If trace != NULL, the triples are recorded (3 * num_events ints). */
+/* SampleUser :300-310 */
+static int32_t ora_bpr_sample_user(ora_rng* r, const ora_bpr_params* p, const int64_t* off) {
+    for (;;) {
+        int32_t u = ora_rng_next(r, p->max_user_id + 1);
+        int64_t cnt = off[u + 1] - off[u];
+        if (cnt == 0 || cnt == (int64_t)p->max_item_id + 1) continue;
+        return u;
+    }
+}
+
+/* One epoch of num_events triples, each sampled then applied; if trace != NULL the triples are
+ * recorded (3 * num_events ints).
+ *   sampler 0 / 2: IterateWithoutReplacementUniformUser :216-226 (SampleTriple per event)
+ *   sampler 3: IterateWithReplacementUniformUser :183-211.  user_matrix = GetUserMatrixCopy()
+ *     (Data/PosOnlyFeedback.cs:68-74) once per epoch: each row a HashSet filled in event order.
+ *     ElementAt(Next(Count)) enumerates the set's slots in index order and Remove (the `= false`
+ *     setter) frees one slot without moving the others, so the remaining items keep their insertion
+ *     order; removing the last one leaves an empty set (count 0, lastIndex 0), which the reset at
+ *     :198-200 refills with Feedback.UserMatrix[u] in its enumeration order -- the full row again.
+ *     The negative is drawn against the full set, Feedback.UserMatrix[u] (:204-206).
+ *   sampler 4: IterateWithReplacementUniformPair :231-243: the event at Next(Count), then
+ *     SampleOtherItem :275-284 (the given item is positive, so j is redrawn while in S_u). */
 void ora_bpr_epoch(ora_rng* r, const ora_bpr_params* p, const int64_t* off, const int32_t* rows,
                    const int32_t* sorted, int64_t num_events, float* U, float* V, float* bias,
                    int32_t* trace) {
     int32_t t[3];
+    int32_t* rem = NULL;  /* sampler 3: each user's remaining items, insertion order */
+    int64_t* left = NULL; /* sampler 3: how many remain */
+    if (p->sampler == 3) {
+        const int64_t n_rows = (int64_t)p->max_user_id + 1, nnz = off[n_rows];
+        rem = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nnz > 0 ? nnz : 1));
+        left = (int64_t*)malloc(sizeof(int64_t) * (size_t)n_rows);
+        memcpy(rem, rows, sizeof(int32_t) * (size_t)nnz);
+        for (int64_t u = 0; u < n_rows; u++) left[u] = off[u + 1] - off[u];
+    }
     for (int64_t c = 0; c < num_events; c++) {
-        ora_bpr_sample_triple(r, p, off, rows, sorted, t);
+        if (p->sampler == 3) {
+            const int32_t u = ora_bpr_sample_user(r, p, off);
+            int32_t* row = rem + off[u];
+            if (left[u] == 0) { /* reset: refill from Feedback.UserMatrix[u] */
+                left[u] = off[u + 1] - off[u];
+                memcpy(row, rows + off[u], sizeof(int32_t) * (size_t)left[u]);
+            }
+            const int32_t x = ora_rng_next(r, (int32_t)left[u]);
+            const int32_t i = row[x];
+            memmove(row + x, row + x + 1, sizeof(int32_t) * (size_t)(left[u] - x - 1));
+            left[u]--;
+            int32_t j;
+            do j = ora_rng_next(r, p->max_item_id + 1);
+            while (ora_row_contains(off, sorted, u, j));
+            t[0] = u;
+            t[1] = i;
+            t[2] = j;
+        } else if (p->sampler == 4) {
+            const int32_t index = ora_rng_next(r, (int32_t)p->n_events);
+            const int32_t u = p->ev_users[index], i = p->ev_items[index];
+            const int item_is_positive = ora_row_contains(off, sorted, u, i);
+            int32_t j;
+            do j = ora_rng_next(r, p->max_item_id + 1);
+            while (ora_row_contains(off, sorted, u, j) == item_is_positive);
+            t[0] = u;
+            t[1] = i;
+            t[2] = j;
+        } else {
+            ora_bpr_sample_triple(r, p, off, rows, sorted, t);
+        }
         if (trace) {
             trace[3 * c] = t[0];
             trace[3 * c + 1] = t[1];
@@ -787,6 +846,8 @@ void ora_bpr_epoch(ora_rng* r, const ora_bpr_params* p, const int64_t* off, cons
         }
         ora_bpr_update(p, t[0], t[1], t[2], U, V, bias);
     }
+    free(rem);
+    free(left);
 }
 
 /* ------------------------------------------------------------------------------------------

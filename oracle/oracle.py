@@ -561,7 +561,7 @@ class _BprParams(ctypes.Structure):
 
 
 BPR_MODEL = {"BPRMF": 0, "SoftMarginRankingMF": 1}
-BPR_SAMPLER = {"uniform_user": 0, "weighted": 2}
+BPR_SAMPLER = {"uniform_user": 0, "weighted": 2, "user_replacement": 3, "pair_replacement": 4}
 
 
 def insertion_order_rows(rows_of, cols_of, n_rows):
@@ -592,7 +592,10 @@ def bpr_train(users, items, n_users, n_items, *, seed=1, k=10, num_iter=30, lear
               model="BPRMF", sampler="uniform_user"):
     """BPRMF.Train (:129-154) with the default IterateWithoutReplacementUniformUser (:216-226).
     model="SoftMarginRankingMF": its UpdateFactors (SoftMarginRankingMF.cs:66-113); sampler=
-    "weighted": WeightedBPRMF.SampleTriple (WeightedBPRMF.cs:55-67), also in the loss-sample burn."""
+    "weighted": WeightedBPRMF.SampleTriple (WeightedBPRMF.cs:55-67), also in the loss-sample burn;
+    "user_replacement" / "pair_replacement": WithReplacement = true with UniformUserSampling = true
+    (IterateWithReplacementUniformUser :183-211) / false (IterateWithReplacementUniformPair
+    :231-243); their loss-sample burn is BPRMF.SampleTriple."""
     users, items = i32(users), i32(items)
     rng = rng if rng is not None else Rng(seed)
     U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)

@@ -187,6 +187,26 @@ def case_bpr_soft_margin_small():
     return dict(users=u, items=i, U=st["U"], V=st["V"], bias=st["bias"], trace0=st["traces"][0])
 
 
+def case_bpr_user_replacement_small():
+    # IterateWithReplacementUniformUser (BPRMF.cs:183-211): ~deg(u) samples per user per epoch,
+    # so rounds run out and refill
+    u, i = synth_feedback(24, 30, 20, 8)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    st = O.bpr_train(u, i, nu, ni, seed=7, k=5, num_iter=2, trace_epochs=2,
+                     sampler="user_replacement")
+    return dict(users=u, items=i, U=st["U"], V=st["V"], bias=st["bias"], trace0=st["traces"][0],
+                trace1=st["traces"][1])
+
+
+def case_bpr_pair_replacement_small():
+    # IterateWithReplacementUniformPair (BPRMF.cs:231-243)
+    u, i = synth_feedback(25, 30, 20, 8)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    st = O.bpr_train(u, i, nu, ni, seed=8, k=5, num_iter=2, trace_epochs=1,
+                     sampler="pair_replacement")
+    return dict(users=u, items=i, U=st["U"], V=st["V"], bias=st["bias"], trace0=st["traces"][0])
+
+
 def case_bpr_weighted_small():
     u, i = synth_feedback(23, 30, 20, 8)
     nu, ni = int(u.max()) + 1, int(i.max()) + 1
@@ -214,6 +234,8 @@ CASES = {
     "bpr_small": case_bpr_small,
     "bpr_soft_margin_small": case_bpr_soft_margin_small,
     "bpr_weighted_small": case_bpr_weighted_small,
+    "bpr_user_replacement_small": case_bpr_user_replacement_small,
+    "bpr_pair_replacement_small": case_bpr_pair_replacement_small,
     "wrmf_small": case_wrmf_small,
 }
 

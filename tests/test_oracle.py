@@ -217,3 +217,79 @@ def test_multithreaded_dsgd_equals_sequential_blocks():
     np.testing.assert_array_equal(U, st["U"])
     np.testing.assert_array_equal(V, st["V"])
     np.testing.assert_array_equal(bu, st["bu"])
+
+
+def _rounds_are_permutations(users, items, triples):
+    """IterateWithReplacementUniformUser (BPRMF.cs:183-211): a user's samples of one epoch, in
+    sample order and cut into runs of |S_u|, never repeat an item within a run (each drawn item is
+    forgotten until the user's copy is refilled); every complete run is S_u; j is never in S_u."""
+    import collections
+    S = collections.defaultdict(set)
+    for a, b in zip(users.tolist(), items.tolist()):
+        S[a].add(b)
+    seq = collections.defaultdict(list)
+    for a, b, c in triples.tolist():
+        assert c not in S[a]
+        seq[a].append(b)
+    refills = 0
+    for a, run in seq.items():
+        d = len(S[a])
+        refills += len(run) > d
+        for c in range(0, len(run), d):
+            chunk = run[c:c + d]
+            assert len(set(chunk)) == len(chunk) and set(chunk) <= S[a]
+            assert len(chunk) < d or set(chunk) == S[a]
+    return refills
+
+
+def test_user_replacement_sampler_draws_rounds_without_repetition():
+    g = golden()
+    u, i = g["bpr_user_replacement_small/users"], g["bpr_user_replacement_small/items"]
+    for t in ("trace0", "trace1"):  # the per-epoch copy restarts every user at a full set
+        assert _rounds_are_permutations(u, i, g[f"bpr_user_replacement_small/{t}"]) > 0
+
+
+def test_user_replacement_removal_keeps_insertion_order():
+    # ElementAt over a HashSet after Remove: the remaining slots keep their insertion order.  One
+    # user, items inserted as 7, 3, 9: the oracle's i must be remaining[Next(count)] of that order.
+    users = np.array([0, 0, 0, 1], np.int32)
+    items = np.array([7, 3, 9, 0], np.int32)
+    st = O.bpr_train(users, items, 2, 12, seed=11, k=2, num_iter=1, trace_epochs=1,
+                     sampler="user_replacement")
+    rng = O.Rng(11)
+    rng.fill_normal(2 * 2, 0.0, 0.1), rng.fill_normal(12 * 2, 0.0, 0.1)
+    sets = {0: [7, 3, 9], 1: [0]}
+    for _ in range(int(np.sqrt(1)) * 100):  # loss-sample burn: BPRMF.SampleTriple
+        while True:
+            uu = rng.next(2)
+            if 0 < len(sets[uu]) < 12:
+                break
+        rng.next(len(sets[uu]))
+        while rng.next(12) in sets[uu]:
+            pass
+    rem = {0: [7, 3, 9], 1: [0]}
+    for uu, ii, jj in st["traces"][0].tolist():
+        while True:
+            cand = rng.next(2)
+            if 0 < len(sets[cand]) < 12:
+                break
+        assert cand == uu
+        if not rem[uu]:
+            rem[uu] = list(sets[uu])
+        assert ii == rem[uu].pop(rng.next(len(rem[uu])))
+        while True:
+            j = rng.next(12)
+            if j not in sets[uu]:
+                break
+        assert jj == j
+
+
+def test_pair_replacement_sampler_draws_events():
+    # IterateWithReplacementUniformPair (:231-243): (u, i) is an event, j not in S_u; events are
+    # drawn with replacement, so some repeat within the epoch
+    g = golden()
+    u, i = g["bpr_pair_replacement_small/users"], g["bpr_pair_replacement_small/items"]
+    tr = g["bpr_pair_replacement_small/trace0"]
+    pos = set(zip(u.tolist(), i.tolist()))
+    assert all((a, b) in pos and (a, c) not in pos for a, b, c in tr.tolist())
+    assert len({(a, b) for a, b, _ in tr.tolist()}) < len(tr)
