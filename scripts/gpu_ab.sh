@@ -10,5 +10,5 @@ run() {  # tag, lib
   tail -1 gpurun_out/ab_$1.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d.get('roofline') or {}; print('$1', '%.4g' % d['value'], d['ms_per_step'], r.get('kernel_avg_ms'), d.get('final_rmse'))"
 }
 run base "" || exit 1
-for v in "$@"; do run $v build/variants/$v/libmml_hip.so || exit 1; done
+for v in "$@"; do case $v in base*) run $v "" || exit 1; continue;; esac; run $v ${VARIANT_DIR:-build/variants}/$v/libmml_hip.so || exit 1; done
 run base2 "" || exit 1
