@@ -150,3 +150,56 @@ def test_replacement_auc_parity(sampler, schedule):
     assert auc_ref > 0.75
     lo, hi = (-0.01, 0.01) if schedule == "ordered" else (-0.01, 0.025)
     assert lo <= auc_gpu - auc_ref <= hi
+
+
+def _splitmix64(x):
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def _draw(seed, s, d, n):
+    """bpr.hip draw(): Lemire multiply-shift of the high 32 bits of splitmix64(seed ^ (s C + d))."""
+    with np.errstate(over="ignore"):
+        x = _splitmix64(np.uint64(seed) ^ (s.astype(np.uint64) * np.uint64(0xD1B54A32D192ED03) +
+                                           np.uint64(d)))
+        return (((x >> np.uint64(32)) * np.asarray(n, np.uint64)) >> np.uint64(32)).astype(np.int64)
+
+
+def test_uniform_user_sampler_triples_exact_at_5m_events():
+    """The default sampler's triples (counter-based, a pure function of (seed, sample)) restated in
+    numpy and compared exactly at 5M events."""
+    from mymedialite_amd import _native as N
+    rs = np.random.default_rng(9)
+    n_users, n_items, n = 200_000, 20_000, 5_000_000
+    users = rs.integers(0, n_users, n).astype(np.int32)
+    items = (rs.zipf(1.6, n) % n_items).astype(np.int32)
+    Random.set_seed(3)
+    m = BPRMF(NumFactors=16, NumIter=1, Schedule="hogwild")
+    m.feedback = PosOnlyFeedback(users, items)
+    m.init_model()
+    seed = 0x1234_5678_9ABC
+    N.check(N.lib().mml_bpr_iterate(m._h, seed))
+    tu, ti, tj = m.last_triples()
+    off, cols = _csr(users, items, n_users)
+    deg = np.diff(off)
+    elig = np.flatnonzero((deg > 0) & (deg < n_items))
+    s = np.arange(n, dtype=np.int64)
+    du = _draw(seed, s, 0, len(elig))
+    u = du if len(elig) == n_users else elig[du]
+    i = cols[off[u] + _draw(seed, s, 1, deg[u])]
+    w = np.int64(n_items)
+    members = np.repeat(np.arange(n_users, dtype=np.int64), deg) * w + cols
+    j = np.full(n, -1, np.int64)
+    todo = np.arange(n)
+    d = 2
+    while len(todo):
+        cand = _draw(seed, todo, d, n_items)
+        ok = ~np.isin(u[todo] * w + cand, members)
+        j[todo[ok]] = cand[ok]
+        todo = todo[~ok]
+        d += 1
+    np.testing.assert_array_equal(tu, u)
+    np.testing.assert_array_equal(ti, i)
+    np.testing.assert_array_equal(tj, j)
