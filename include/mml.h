@@ -124,13 +124,18 @@ enum {
                           both sides (pass it as reg_u = reg_i), Predict clipped to [min, max];
                           loss, frequency_regularization and the bias fields are ignored and
                           mml_bmf_objective is not defined */
-    MML_MF_SOCIAL = 2  /* SocialMF (SocialMF.cs:43-254): BiasedMatrixFactorization trained by
+    MML_MF_SOCIAL = 2, /* SocialMF (SocialMF.cs:43-254): BiasedMatrixFactorization trained by
                           full-batch gradient descent with a social-network regulariser
                           (IterateBatch :77-194) over the user relation of
                           mml_bmf_set_user_relation; mml_bmf_iterate's learn_rate is LearnRate
                           (the batch step never reads current_learnrate); the schedule field is
                           ignored (the batch step is order-independent up to the per-row
                           accumulation order, which follows the stored visit order) */
+    MML_MF_ITEM_ASYM = 3 /* SigmoidItemAsymmetricFactorModel (SigmoidItemAsymmetricFactorModel.cs:
+                            43-344): a BiasedMatrixFactorization whose user vector is y summed over
+                            the items the user rated (training + AdditionalFeedback) / sqrt(count);
+                            mml_bmf_set_item_feedback before iterate; ORDERED (bit-faithful) or
+                            HOGWILD (ABI 3) */
 };
 
 typedef struct {
@@ -220,6 +225,16 @@ mml_status mml_bmf_fold_in(mml_bmf* h, int32_t n_fold, const int64_t* rated_off,
 mml_status mml_bmf_predict_vectors(mml_bmf* h, int32_t n_vectors, const float* vectors,
                                    const int32_t* vector_index, const int32_t* items, int64_t n,
                                    float* out);
+
+/* MML_MF_ITEM_ASYM: the items_rated_by_user CSR (ITransductiveRatingPredictor.ItemsRatedByUser,
+ * ITransductiveRatingPredictor.cs:63-79: per user the training items in rating-index order, then
+ * AdditionalFeedback's, distinct; n_rows = n_users), y [n_items x k] (InitModel :290-301) and
+ * y_reg [n_items] (Train :72-77).  U then holds PrecomputeUserFactors (:305-331), refreshed after
+ * every epoch, so Predict / evaluate read the reference's user_factors (ABI 3). */
+mml_status mml_bmf_set_item_feedback(mml_bmf* h, int32_t n_rows, const int64_t* offsets,
+                                     const int32_t* items, const float* y, const float* y_reg);
+/* y [n_items x k] (SaveModel writes it, :150-162) */
+mml_status mml_bmf_get_item_feedback_factors(mml_bmf* h, float* y);
 
 /* ------------------------------------------------------------------ BPRMF */
 enum {

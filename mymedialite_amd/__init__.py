@@ -6,9 +6,11 @@ include/mml.h); this package is the host-side mirror of the reference's recommen
 from .data import IdentityMapping, Mapping, PosOnlyFeedback, Ratings, read_items, read_ratings
 from .random import Random, SystemRandom
 from .item_recommendation import BPRMF, WRMF, SoftMarginRankingMF, WeightedBPRMF
-from .rating_prediction import BiasedMatrixFactorization, MatrixFactorization, SocialMF
+from .rating_prediction import (BiasedMatrixFactorization, MatrixFactorization,
+                                SigmoidItemAsymmetricFactorModel, SocialMF)
 
-__all__ = ["BiasedMatrixFactorization", "MatrixFactorization", "SocialMF", "BPRMF", "WRMF",
+__all__ = ["BiasedMatrixFactorization", "MatrixFactorization", "SocialMF",
+           "SigmoidItemAsymmetricFactorModel", "BPRMF", "WRMF",
            "SoftMarginRankingMF", "WeightedBPRMF", "Ratings",
            "PosOnlyFeedback", "Mapping", "IdentityMapping", "read_ratings", "read_items", "Random",
            "SystemRandom"]

@@ -829,6 +829,134 @@ inline int lanes_per_rating(int k) {
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------------
+// SigmoidItemAsymmetricFactorModel (MML_MF_ITEM_ASYM; RatingPrediction/
+// SigmoidItemAsymmetricFactorModel.cs:43-344).  The user is represented by y summed over the
+// items they rated (training + AdditionalFeedback, the items_rated_by_user CSR), / sqrt(count).
+// One wavefront per rating at a time, lane f owns factors f, f + 64, ... (KM per lane), so every
+// per-factor sum and update runs in the reference's order.  ORDERED = one wavefront over the
+// whole stream (bit-faithful); HOGWILD = many wavefronts on chunks of it.
+
+// the user vector: SumOfRows (DataType/MatrixExtensions.cs:125-135, float, list order),
+// / sqrt(count) in double, cast to float (Iterate :104-107, PrecomputeUserFactors :316-331)
+template <int KM>
+__device__ __forceinline__ double iafm_user_vector(const float* __restrict__ Y, int32_t k,
+                                                   int32_t ld, const int64_t* __restrict__ roff,
+                                                   const int32_t* __restrict__ ritems, int32_t u,
+                                                   int lane, float (&vec)[KM]) {
+    const int64_t b = roff[u], e = roff[u + 1];
+#pragma unroll
+    for (int m = 0; m < KM; ++m) vec[m] = 0.0f;
+    for (int64_t t = b; t < e; ++t) {
+        const float* row = Y + (int64_t)ritems[t] * ld;
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int f = lane + 64 * m;
+            vec[m] += f < k ? row[f] : 0.0f;
+        }
+    }
+    const double norm = sqrt((double)(e - b));
+#pragma unroll
+    for (int m = 0; m < KM; ++m) vec[m] = (float)((double)vec[m] / norm);
+    return norm;
+}
+
+template <int LOSS, int KM>
+__global__ __launch_bounds__(64) void iafm_sgd_kernel(
+    const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
+    int64_t n, int64_t chunk, float* Y, float* V, float* bu, float* bi, int32_t k, int32_t ld,
+    BmfScalars s, const int32_t* __restrict__ cnt_u, const int32_t* __restrict__ cnt_i,
+    const int64_t* __restrict__ roff, const int32_t* __restrict__ ritems,
+    const float* __restrict__ y_reg) {
+    const int lane = threadIdx.x;
+    const int64_t begin = (int64_t)blockIdx.x * chunk;
+    const int64_t end = min(begin + chunk, n);
+    for (int64_t x = begin; x < end; ++x) {
+        const int32_t u = su[x], i = si[x];
+        const float r = sr[x];
+        float vec[KM], qi[KM], prod[KM];
+        const double norm = iafm_user_vector<KM>(Y, k, ld, roff, ritems, u, lane, vec);
+        float* Vi = V + (int64_t)i * ld;
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int f = lane + 64 * m;
+            qi[m] = f < k ? Vi[f] : 0.0f;
+            prod[m] = qi[m] * vec[m];
+        }
+        // RowScalarProduct(i, IList<float>) (MatrixExtensions.cs:183-196): float, left to right
+        float dot = 0.0f;
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int lim = min(64, k - 64 * m);
+            const int bits = __float_as_int(prod[m]);
+            for (int l = 0; l < lim; ++l) dot += __int_as_float(__builtin_amdgcn_readlane(bits, l));
+        }
+        const float bu_u = bu[u], bi_i = bi[i];
+        // score = global_bias + user_bias + item_bias in float, then + dot in double (:103-109)
+        const double score = (double)((s.gb + bu_u) + bi_i) + (double)dot;
+        const double sig = 1.0 / (1.0 + exp(-score));
+        const double err = (double)r - ((double)s.min_rating + sig * (double)s.range);
+        const float g = gradient_common<LOSS>(sig, err, s.range);
+        float reg_u = s.reg_u, reg_i = s.reg_i;
+        if (cnt_u) {  // FrequencyRegularization (:115-116)
+            reg_u = (float)((double)s.reg_u / sqrt((double)cnt_u[u]));
+            reg_i = (float)((double)s.reg_i / sqrt((double)cnt_i[i]));
+        }
+        if (lane == 0) {  // :120-123
+            bu[u] = bu_u + s.blr * (g - (s.bias_reg * reg_u) * bu_u);
+            bi[i] = bi_i + s.blr * (g - (s.bias_reg * reg_i) * bi_i);
+        }
+        const double ngc = (double)g / norm;  // normalized_gradient_common (:126)
+        double common[KM];
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int f = lane + 64 * m;
+            const float i_f = qi[m];
+            // delta_i is a float expression widened to double; Inc adds (float)(lr * delta)
+            const double delta_i = (double)(g * vec[m] - reg_i * i_f);
+            if (f < k) Vi[f] = i_f + (float)((double)s.lr * delta_i);
+            common[m] = ngc * (double)i_f;
+        }
+        // y rows of every item the user rated (:137-142), list order per factor
+        const int64_t b = roff[u], e = roff[u + 1];
+        for (int64_t t = b; t < e; ++t) {
+            const int32_t j = ritems[t];
+            const float yr = y_reg[j];
+            float* row = Y + (int64_t)j * ld;
+#pragma unroll
+            for (int m = 0; m < KM; ++m) {
+                const int f = lane + 64 * m;
+                if (f < k) {
+                    const float y = row[f];
+                    row[f] = y + (float)((double)s.lr * (common[m] - (double)(yr * y)));
+                }
+            }
+        }
+    }
+}
+
+// PrecomputeUserFactors (:305-331): U[u] = the user vector; users without items get zeros
+template <int KM>
+__global__ __launch_bounds__(64) void iafm_user_factors_kernel(
+    const float* __restrict__ Y, int32_t k, int32_t ld, const int64_t* __restrict__ roff,
+    const int32_t* __restrict__ ritems, int32_t n_users, float* __restrict__ U) {
+    const int lane = threadIdx.x;
+    for (int32_t u = blockIdx.x; u < n_users; u += gridDim.x) {
+        float vec[KM];
+        if (roff[u + 1] > roff[u]) {
+            iafm_user_vector<KM>(Y, k, ld, roff, ritems, u, lane, vec);
+        } else {
+#pragma unroll
+            for (int m = 0; m < KM; ++m) vec[m] = 0.0f;
+        }
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int f = lane + 64 * m;
+            if (f < k) U[(int64_t)u * ld + f] = vec[m];
+        }
+    }
+}
+
 struct mml_bmf {
     mml_ctx* ctx = nullptr;
     mml_bmf_params p{};
@@ -853,6 +981,11 @@ struct mml_bmf {
     mml::DeviceArray<float> gerr, Ug, Vg, bug, big;
     int32_t n_conn = 0, n_rev = 0;
     bool has_positions = false;
+    // SigmoidItemAsymmetricFactorModel: items_rated_by_user (CSR), y, y_reg
+    mml::DeviceArray<int64_t> rated_off;
+    mml::DeviceArray<int32_t> rated_items;
+    mml::DeviceArray<float> Y, y_reg;
+    bool has_item_feedback = false;
 };
 
 namespace {
@@ -1089,6 +1222,57 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     MML_HIP(hipGetLastError());
 }
 
+// U <- PrecomputeUserFactors (the representation Predict and the evaluators read)
+void iafm_user_factors(mml_bmf* h) {
+    const int km = (h->k + 63) / 64;
+    const int grid = std::max(1, std::min(h->n_users, 65536));
+    hipStream_t st = h->ctx->stream;
+#define MML_IUF(KM)                                                                            \
+    iafm_user_factors_kernel<KM><<<grid, 64, 0, st>>>(h->Y.get(), h->k, h->ld,                 \
+                                                      h->rated_off.get(), h->rated_items.get(), \
+                                                      h->n_users, h->U.get())
+    switch (km) {
+        case 1: MML_IUF(1); break;
+        case 2: MML_IUF(2); break;
+        case 3: MML_IUF(3); break;
+        default: MML_IUF(4); break;
+    }
+#undef MML_IUF
+    MML_HIP(hipGetLastError());
+}
+
+template <int LOSS>
+void iafm_epoch(mml_bmf* h, const BmfScalars& s) {
+    const int32_t* cu = h->p.frequency_regularization ? h->cnt_u.get() : nullptr;
+    const int32_t* ci = h->p.frequency_regularization ? h->cnt_i.get() : nullptr;
+    const int64_t n = h->n;
+    hipStream_t st = h->ctx->stream;
+    if (n > 0) {
+        // ORDERED: one wavefront, the whole stream in order.  HOGWILD: a wavefront per >= 2,048
+        // ratings (a rating reads and writes all |items(u)| y rows), at most 256 CUs x 8
+        int64_t waves = 1;
+        if (h->p.schedule != MML_SCHEDULE_ORDERED)
+            waves = std::min<int64_t>(256 * 8, std::max<int64_t>(1, n / 2048));
+        const int64_t chunk = (n + waves - 1) / waves;
+        const int km = (h->k + 63) / 64;
+#define MML_IAFM(KM)                                                                           \
+    iafm_sgd_kernel<LOSS, KM><<<(int)waves, 64, 0, st>>>(                                      \
+        h->su.get(), h->si.get(), h->sr.get(), n, chunk, h->Y.get(), h->V.get(), h->bu.get(),  \
+        h->bi.get(), h->k, h->ld, s, cu, ci, h->rated_off.get(), h->rated_items.get(),          \
+        h->y_reg.get())
+        switch (km) {
+            case 1: MML_IAFM(1); break;
+            case 2: MML_IAFM(2); break;
+            case 3: MML_IAFM(3); break;
+            default: MML_IAFM(4); break;
+        }
+#undef MML_IAFM
+        MML_HIP(hipGetLastError());
+    }
+    iafm_user_factors(h);
+    h->last_launches = 1;
+}
+
 template <int LOSS>
 void run_epoch(mml_bmf* h, const BmfScalars& s, const int32_t* seq) {
     const int32_t* cu = h->p.frequency_regularization ? h->cnt_u.get() : nullptr;
@@ -1130,8 +1314,7 @@ extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params,
                     "num_factors must be in [1, 256]");
         MML_REQUIRE(params->loss >= MML_LOSS_RMSE && params->loss <= MML_LOSS_LOGISTIC,
                     "unknown loss");
-        MML_REQUIRE(params->model == MML_MF_BIASED || params->model == MML_MF_PLAIN ||
-                        params->model == MML_MF_SOCIAL,
+        MML_REQUIRE(params->model >= MML_MF_BIASED && params->model <= MML_MF_ITEM_ASYM,
                     "unknown model family");
         MML_REQUIRE(params->schedule >= MML_SCHEDULE_ORDERED &&
                         params->schedule <= MML_SCHEDULE_HOGWILD_COHERENT,
@@ -1316,7 +1499,14 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
     return guard([&] {
         check_handle(h);
         MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
-        if (h->p.schedule == MML_SCHEDULE_DSGD && h->p.model != MML_MF_SOCIAL) {
+        if (h->p.model == MML_MF_ITEM_ASYM) {
+            MML_REQUIRE(h->has_item_feedback, "set_item_feedback must precede iterate");
+            MML_REQUIRE(h->p.schedule == MML_SCHEDULE_ORDERED ||
+                            h->p.schedule == MML_SCHEDULE_HOGWILD,
+                        "the item-asymmetric model runs the ORDERED or HOGWILD schedule");
+        }
+        if (h->p.schedule == MML_SCHEDULE_DSGD && h->p.model != MML_MF_SOCIAL &&
+            h->p.model != MML_MF_ITEM_ASYM) {
             MML_REQUIRE(h->G > 0, "DSGD schedule needs set_blocks");
             MML_REQUIRE(subepoch_sequence, "DSGD schedule needs a sub-epoch sequence");
             for (int32_t x = 0; x < h->G; ++x)
@@ -1335,7 +1525,13 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
         s.reg_i = h->p.reg_i;
         hipStream_t st = h->ctx->stream;
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
-        if (h->p.model == MML_MF_SOCIAL) {
+        if (h->p.model == MML_MF_ITEM_ASYM) {
+            switch (h->p.loss) {
+                case MML_LOSS_MAE: iafm_epoch<MML_LOSS_MAE>(h, s); break;
+                case MML_LOSS_LOGISTIC: iafm_epoch<MML_LOSS_LOGISTIC>(h, s); break;
+                default: iafm_epoch<MML_LOSS_RMSE>(h, s); break;
+            }
+        } else if (h->p.model == MML_MF_SOCIAL) {
             switch (h->p.loss) {
                 case MML_LOSS_MAE: social_epoch<MML_LOSS_MAE>(h, s); break;
                 case MML_LOSS_LOGISTIC: social_epoch<MML_LOSS_LOGISTIC>(h, s); break;
@@ -1469,6 +1665,8 @@ extern "C" mml_status mml_bmf_allreduce_items(mml_bmf* h) {
         mml_ctx* c = h->ctx;
         if (c->nranks <= 1) return;
         MML_REQUIRE(c->comm, "context has no communicator (mml_ctx_comm_init)");
+        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM,
+                    "the item-asymmetric model's y is not averaged across ranks");
         c->activate();
         hipStream_t st = c->stream;
         const size_t nv = (size_t)h->n_items * h->ld;
@@ -1513,6 +1711,8 @@ extern "C" mml_status mml_bmf_fold_in(mml_bmf* h, int32_t n_fold, const int64_t*
     return guard([&] {
         check_handle(h);
         MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM,
+                    "SigmoidItemAsymmetricFactorModel has its own FoldIn (not on the GPU path)");
         MML_REQUIRE(n_fold >= 0 && num_iter >= 0, "negative sizes");
         if (n_fold == 0) return;
         MML_REQUIRE(rated_off && init_factors && out_vectors, "null arguments");
@@ -1577,6 +1777,8 @@ extern "C" mml_status mml_bmf_predict_vectors(mml_bmf* h, int32_t n_vectors, con
     return guard([&] {
         check_handle(h);
         MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM,
+                    "SigmoidItemAsymmetricFactorModel has its own FoldIn (not on the GPU path)");
         MML_REQUIRE(n_vectors >= 0 && n >= 0, "negative sizes");
         if (n == 0) return;
         MML_REQUIRE(vectors && vector_index && items && out, "null arguments");
@@ -1656,5 +1858,54 @@ extern "C" mml_status mml_bmf_set_user_relation(mml_bmf* h, int32_t n_rows, cons
         MML_HIP(hipStreamSynchronize(st));
         h->n_conn = n_rows;
         h->n_rev = n_rev;
+    });
+}
+
+extern "C" mml_status mml_bmf_set_item_feedback(mml_bmf* h, int32_t n_rows, const int64_t* offsets,
+                                                const int32_t* items, const float* y,
+                                                const float* y_reg) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->p.model == MML_MF_ITEM_ASYM,
+                    "item feedback belongs to SigmoidItemAsymmetricFactorModel handles");
+        MML_REQUIRE(n_rows == h->n_users, "one row of rated items per user (n_rows = n_users)");
+        MML_REQUIRE(offsets && y && y_reg, "null argument");
+        MML_REQUIRE(offsets[0] == 0, "offsets[0] must be 0");
+        for (int32_t u = 0; u < n_rows; ++u)
+            MML_REQUIRE(offsets[u + 1] >= offsets[u], "offsets must not decrease");
+        const int64_t nnz = offsets[n_rows];
+        MML_REQUIRE(nnz == 0 || items, "null items");
+        for (int64_t x = 0; x < nnz; ++x)
+            MML_REQUIRE(items[x] >= 0 && items[x] < h->n_items, "rated item id out of range");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        h->has_item_feedback = false;
+        h->rated_off.alloc((size_t)n_rows + 1);
+        h->rated_items.alloc((size_t)std::max<int64_t>(1, nnz));
+        h->Y.alloc((size_t)std::max<int64_t>(1, (int64_t)h->n_items * h->ld));
+        h->y_reg.alloc((size_t)std::max(1, h->n_items));
+        MML_HIP(hipMemcpyAsync(h->rated_off.get(), offsets, sizeof(int64_t) * (n_rows + 1),
+                               hipMemcpyHostToDevice, st));
+        if (nnz)
+            MML_HIP(hipMemcpyAsync(h->rated_items.get(), items, sizeof(int32_t) * nnz,
+                                   hipMemcpyHostToDevice, st));
+        upload_padded(h, h->Y.get(), y, h->n_items);
+        if (h->n_items)
+            MML_HIP(hipMemcpyAsync(h->y_reg.get(), y_reg, sizeof(float) * h->n_items,
+                                   hipMemcpyHostToDevice, st));
+        if (h->n_users) iafm_user_factors(h);
+        MML_HIP(hipStreamSynchronize(st));
+        h->has_item_feedback = true;
+    });
+}
+
+extern "C" mml_status mml_bmf_get_item_feedback_factors(mml_bmf* h, float* y) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->has_item_feedback, "no item feedback factors (set_item_feedback first)");
+        MML_REQUIRE(y, "null argument");
+        h->ctx->activate();
+        download_padded(h, y, h->Y.get(), h->n_items);
+        MML_HIP(hipStreamSynchronize(h->ctx->stream));
     });
 }

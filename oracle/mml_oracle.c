@@ -207,6 +207,94 @@ void ora_bmf_iterate(const ora_bmf_params* p, const int32_t* users, const int32_
     }
 }
 
+/* y summed over the user's rated items (MatrixExtensions.SumOfRows, DataType/MatrixExtensions.cs:
+ * 125-135: float accumulation in list order), / sqrt(count) in double, cast to float -- the user
+ * vector of SigmoidItemAsymmetricFactorModel (Iterate :104-107, PrecomputeUserFactors :316-331) */
+static void ora_iafm_user_vector(const float* Y, int k, const int64_t* rated_off,
+                                 const int32_t* rated_items, int32_t u, float* vec, double* norm) {
+    const int64_t b = rated_off[u], e = rated_off[u + 1];
+    for (int f = 0; f < k; f++) vec[f] = 0.0f;
+    for (int64_t t = b; t < e; t++) {
+        const float* row = Y + (int64_t)rated_items[t] * k;
+        for (int f = 0; f < k; f++) vec[f] += row[f];
+    }
+    *norm = sqrt((double)(e - b));
+    for (int f = 0; f < k; f++) vec[f] = (float)((double)vec[f] / *norm);
+}
+
+/* SigmoidItemAsymmetricFactorModel.Iterate(IList<int>,bool,bool)
+ * (RatingPrediction/SigmoidItemAsymmetricFactorModel.cs:91-147).  rated_off / rated_items: the
+ * items_rated_by_user CSR (ITransductiveRatingPredictor.ItemsRatedByUser, :63-79: training items
+ * in rating-index order, then AdditionalFeedback's, distinct); y_reg per item (Train :72-77).
+ * vec: k floats of scratch. */
+void ora_iafm_iterate(const ora_bmf_params* p, const int32_t* users, const int32_t* items,
+                      const float* values, const int32_t* idx, int64_t n_idx, float* Y, float* V,
+                      float* bu, float* bi, const int32_t* count_by_user,
+                      const int32_t* count_by_item, const int64_t* rated_off,
+                      const int32_t* rated_items, const float* y_reg, float* vec) {
+    const int k = p->k;
+    const float lr = p->learn_rate;
+    for (int64_t n = 0; n < n_idx; n++) {
+        const int32_t index = idx[n];
+        const int32_t u = users[index], i = items[index];
+        float* Vi = V + (int64_t)i * k;
+        double norm;
+        ora_iafm_user_vector(Y, k, rated_off, rated_items, u, vec, &norm);
+        double score = (double)((p->global_bias + bu[u]) + bi[i]); /* float sum, :103 */
+        float dot = 0.0f; /* RowScalarProduct(i, IList<float>) :183-196, float acc */
+        for (int f = 0; f < k; f++) dot += Vi[f] * vec[f];
+        score += (double)dot;
+        const double sig = 1.0 / (1.0 + exp(-score));
+        const double prediction = (double)p->min_rating + sig * (double)p->rating_range_size;
+        const double err = (double)values[index] - prediction;
+        float g;
+        if (p->loss == ORA_LOSS_MAE) {
+            double sgn = (err > 0) ? 1.0 : ((err < 0) ? -1.0 : 0.0);
+            g = (float)(sgn * sig * (1.0 - sig) * (double)p->rating_range_size);
+        } else if (p->loss == ORA_LOSS_LOGISTIC) {
+            g = (float)err;
+        } else {
+            g = (float)(err * sig * (1.0 - sig) * (double)p->rating_range_size);
+        }
+        float reg_u = p->reg_u, reg_i = p->reg_i;
+        if (p->frequency_regularization) {
+            reg_u = (float)((double)p->reg_u / sqrt((double)count_by_user[u]));
+            reg_i = (float)((double)p->reg_i / sqrt((double)count_by_item[i]));
+        }
+        const float blr = p->bias_learn_rate * lr;
+        if (p->update_user) bu[u] += blr * (g - (p->bias_reg * reg_u) * bu[u]);
+        if (p->update_item) bi[i] += blr * (g - (p->bias_reg * reg_i) * bi[i]);
+        const double ngc = (double)g / norm; /* normalized_gradient_common :126 */
+        const int64_t b = rated_off[u], e = rated_off[u + 1];
+        for (int f = 0; f < k; f++) {
+            const float i_f = Vi[f];
+            if (!p->update_item) continue;
+            const double delta_i = (double)(g * vec[f] - reg_i * i_f); /* float expression */
+            Vi[f] += (float)((double)lr * delta_i);
+            const double common = ngc * (double)i_f;
+            for (int64_t t = b; t < e; t++) {
+                const int32_t j = rated_items[t];
+                float* yj = Y + (int64_t)j * k + f;
+                const double delta_oi = common - (double)(y_reg[j] * *yj);
+                *yj += (float)((double)lr * delta_oi);
+            }
+        }
+    }
+}
+
+/* PrecomputeUserFactors (:305-331): U[u] = the user vector; users without items keep zeros */
+void ora_iafm_user_factors(const float* Y, int k, int32_t n_users, const int64_t* rated_off,
+                           const int32_t* rated_items, float* U) {
+    for (int32_t u = 0; u < n_users; u++) {
+        double norm;
+        if (rated_off[u + 1] == rated_off[u]) {
+            for (int f = 0; f < k; f++) U[(int64_t)u * k + f] = 0.0f;
+            continue;
+        }
+        ora_iafm_user_vector(Y, k, rated_off, rated_items, u, U + (int64_t)u * k, &norm);
+    }
+}
+
 /* BiasedMatrixFactorization.Predict(int,int), :313-325 (score accumulated in double) */
 float ora_bmf_predict1(int32_t u, int32_t i, int32_t n_users, int32_t n_items, int k,
                        const float* U, const float* V, const float* bu, const float* bi,

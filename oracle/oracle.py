@@ -111,6 +111,11 @@ def lib():
                                    ctypes.c_int64]
         L.ora_bpr_epoch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _i64p, _i32p, _i32p,
                                     ctypes.c_int64, _f32p, _f32p, _f32p, _i32p]
+        L.ora_iafm_iterate.argtypes = [
+            ctypes.c_void_p, _i32p, _i32p, _f32p, _i32p, ctypes.c_int64, _f32p, _f32p, _f32p,
+            _f32p, _i32p, _i32p, _i64p, _i32p, _f32p, _f32p]
+        L.ora_iafm_user_factors.argtypes = [_f32p, ctypes.c_int, ctypes.c_int32, _i64p, _i32p,
+                                            _f32p]
         L.ora_wrmf_square.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f64p]
         L.ora_wrmf_optimize_rows.argtypes = [_i64p, _i32p, ctypes.c_int64, ctypes.c_int64,
                                              ctypes.c_int64, _f32p, _f32p, _f64p, ctypes.c_int,
@@ -400,6 +405,87 @@ def mf_train(users, items, values, n_users, n_items, *, seed=1, k=10, learn_rate
             callback(epoch, state)
     state.update(global_bias=gb, random_index=random_index, current_learnrate=lr, rng=rng)
     return state
+
+
+def items_rated_by_user(users, items, n_users, add_users=None, add_items=None):
+    """ITransductiveRatingPredictor.ItemsRatedByUser (ITransductiveRatingPredictor.cs:63-79): per
+    user the training items in rating-index order (Ratings.ByUser), then AdditionalFeedback's, as a
+    Union (distinct, first appearance).  Returns the CSR (offsets, items)."""
+    rows = [[] for _ in range(n_users)]
+    seen = [set() for _ in range(n_users)]
+    pairs = list(zip(i32(users).tolist(), i32(items).tolist()))
+    if add_users is not None:
+        pairs += list(zip(i32(add_users).tolist(), i32(add_items).tolist()))
+    for u, i in pairs:
+        if i not in seen[u]:
+            seen[u].add(i)
+            rows[u].append(i)
+    off = np.zeros(n_users + 1, np.int64)
+    off[1:] = np.cumsum([len(r) for r in rows])
+    return off, np.array([i for r in rows for i in r], np.int32)
+
+
+def iafm_train(users, items, values, n_users, n_items, min_rating, max_rating, *, seed=1, k=10,
+               learn_rate=0.001, decay=1.0, reg_u=0.015, reg_i=0.015, bias_reg=0.33,
+               bias_learn_rate=0.7, num_iter=30, init_mean=0.0, init_stddev=0.1, loss=0,
+               frequency_regularization=False, add_users=None, add_items=None, callback=None):
+    """SigmoidItemAsymmetricFactorModel.Train (SigmoidItemAsymmetricFactorModel.cs:66-80) ->
+    BiasedMatrixFactorization.Train (:173-194) with InitModel (:290-301: y, then U, then V) and
+    NumIter x Iterate(RandomIndex) (:91-147) + UpdateLearnRate.  n_users / n_items cover the
+    AdditionalFeedback ids.  Defaults are the model's (:56-63)."""
+    users, items, values = i32(users), i32(items), f32(values)
+    rng = Rng(seed)
+    cnt_u = np.bincount(users, minlength=int(users.max()) + 1).astype(np.int32)
+    cnt_i = np.bincount(items, minlength=int(items.max()) + 1).astype(np.int32)
+    off, rated = items_rated_by_user(users, items, n_users, add_users, add_items)
+    fb_i = np.bincount(items, minlength=n_items)
+    if add_items is not None:
+        fb_i = fb_i + np.bincount(i32(add_items), minlength=n_items)
+    y_reg = np.zeros(n_items, np.float32)
+    for it in range(n_items):  # Train :72-77
+        if fb_i[it] > 0:
+            y_reg[it] = np.float32(reg_i / math.sqrt(fb_i[it])) if frequency_regularization \
+                else np.float32(reg_i)
+    Y = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
+    Y[[x for x in range(n_items) if x >= len(cnt_i) or cnt_i[x] == 0]] = 0
+    U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
+    V = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
+    U[np.flatnonzero(cnt_u == 0)] = 0
+    V[np.flatnonzero(cnt_i == 0)] = 0
+    init = dict(Y=Y.copy(), U=U.copy(), V=V.copy())
+    bu = np.zeros(n_users, np.float32)
+    bi = np.zeros(n_items, np.float32)
+    range_ = np.float32(np.float32(max_rating) - np.float32(min_rating))
+    avg_f = np.float32(np.float32(ratings_average_exact(values)) / np.float32(len(values)))
+    avg = np.float32(np.float32(avg_f - np.float32(min_rating)) / range_)
+    gb = np.float32(math.log(float(avg) / (1.0 - float(avg))))
+    cu = np.zeros(n_users, np.int32)
+    cu[:len(cnt_u)] = cnt_u
+    ci = np.zeros(n_items, np.int32)
+    ci[:len(cnt_i)] = cnt_i
+    lr = np.float32(learn_rate)
+    random_index = None
+    vec = np.zeros(k, np.float32)
+    L = lib()
+    for epoch in range(num_iter):
+        if random_index is None:
+            random_index = rng.shuffle(np.arange(len(users), dtype=np.int32))
+        p = _BmfParams(k, loss, int(frequency_regularization), 1, 1, gb, np.float32(min_rating),
+                       range_, lr, bias_learn_rate, bias_reg, reg_u, reg_i)
+        L.ora_iafm_iterate(ctypes.byref(p), _p(users, _i32p), _p(items, _i32p),
+                           _p(values, _f32p), _p(random_index, _i32p), random_index.size,
+                           _p(Y, _f32p), _p(V, _f32p), _p(bu, _f32p), _p(bi, _f32p),
+                           _p(cu, _i32p), _p(ci, _i32p), _p(off, _i64p), _p(rated, _i32p),
+                           _p(y_reg, _f32p), _p(vec, _f32p))
+        lr = np.float32(lr * np.float32(decay))
+        if callback is not None:
+            callback(epoch, dict(Y=Y, V=V, bu=bu, bi=bi))
+    Uf = np.zeros((n_users, k), np.float32)
+    L.ora_iafm_user_factors(_p(Y, _f32p), k, n_users, _p(off, _i64p), _p(rated, _i32p),
+                            _p(Uf, _f32p))
+    return dict(Y=Y, U=Uf, V=V, bu=bu, bi=bi, init=init, global_bias=gb, range_=range_,
+                random_index=random_index, rated_off=off, rated_items=rated, y_reg=y_reg,
+                current_learnrate=lr)
 
 
 def relation_csr(rows):

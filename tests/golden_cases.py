@@ -187,6 +187,29 @@ def case_bpr_soft_margin_small():
     return dict(users=u, items=i, U=st["U"], V=st["V"], bias=st["bias"], trace0=st["traces"][0])
 
 
+def iafm_case_data():
+    # ratings plus AdditionalFeedback (test pairs, some for users / items beyond the training ids)
+    u, i, v = synth_ratings(41, 40, 30, 600)
+    rs = np.random.default_rng(42)
+    au = rs.integers(0, 44, 80).astype(np.int32)
+    ai = rs.integers(0, 33, 80).astype(np.int32)
+    return u, i, v, au, ai
+
+
+def case_iafm_small():
+    # SigmoidItemAsymmetricFactorModel (SigmoidItemAsymmetricFactorModel.cs:66-147)
+    u, i, v, au, ai = iafm_case_data()
+    nu = max(int(u.max()), int(au.max())) + 1
+    ni = max(int(i.max()), int(ai.max())) + 1
+    snaps = {}
+    st = O.iafm_train(u, i, v, nu, ni, 1.0, 5.0, seed=9, k=5, num_iter=3, learn_rate=0.01,
+                      add_users=au, add_items=ai,
+                      callback=lambda e, m: snaps.update({f"Y{e}": m["Y"].copy()}))
+    return dict(users=u, items=i, values=v, add_users=au, add_items=ai, init_Y=st["init"]["Y"],
+                Y=st["Y"], U=st["U"], V=st["V"], bu=st["bu"], bi=st["bi"],
+                rated_off=st["rated_off"], rated_items=st["rated_items"], **snaps)
+
+
 def case_bpr_user_replacement_small():
     # IterateWithReplacementUniformUser (BPRMF.cs:183-211): ~deg(u) samples per user per epoch,
     # so rounds run out and refill
@@ -235,6 +258,7 @@ CASES = {
     "bpr_soft_margin_small": case_bpr_soft_margin_small,
     "bpr_weighted_small": case_bpr_weighted_small,
     "bpr_user_replacement_small": case_bpr_user_replacement_small,
+    "iafm_small": case_iafm_small,
     "bpr_pair_replacement_small": case_bpr_pair_replacement_small,
     "wrmf_small": case_wrmf_small,
 }

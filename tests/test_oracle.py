@@ -293,3 +293,39 @@ def test_pair_replacement_sampler_draws_events():
     pos = set(zip(u.tolist(), i.tolist()))
     assert all((a, b) in pos and (a, c) not in pos for a, b, c in tr.tolist())
     assert len({(a, b) for a, b, _ in tr.tolist()}) < len(tr)
+
+
+def test_iafm_user_factors_are_the_normalised_y_sums():
+    # PrecomputeUserFactors (SigmoidItemAsymmetricFactorModel.cs:305-331): U[u] = (float)(
+    # SumOfRows(y, items(u)) / sqrt(|items(u)|)), the float sum in list order; zeros without items
+    g = golden()
+    Y, U = g["iafm_small/Y"], g["iafm_small/U"]
+    off, items = g["iafm_small/rated_off"], g["iafm_small/rated_items"]
+    for u in range(len(off) - 1):
+        rows = items[off[u]:off[u + 1]]
+        acc = np.zeros(Y.shape[1], np.float32)
+        for j in rows:
+            acc = (acc + Y[j]).astype(np.float32)
+        want = (acc.astype(np.float64) / np.sqrt(len(rows))).astype(np.float32) if len(rows) \
+            else np.zeros(Y.shape[1], np.float32)
+        np.testing.assert_array_equal(U[u], want)
+
+
+def test_iafm_items_rated_by_user_union_order():
+    # ItemsRatedByUser (ITransductiveRatingPredictor.cs:63-79): training items in rating-index
+    # order, then the additional feedback's, each once
+    g = golden()
+    u, i = g["iafm_small/users"], g["iafm_small/items"]
+    au, ai = g["iafm_small/add_users"], g["iafm_small/add_items"]
+    off, items = g["iafm_small/rated_off"], g["iafm_small/rated_items"]
+    for x in range(len(off) - 1):
+        want = list(dict.fromkeys(i[u == x].tolist() + ai[au == x].tolist()))
+        assert items[off[x]:off[x + 1]].tolist() == want
+    from mymedialite_amd import Ratings, SigmoidItemAsymmetricFactorModel
+    m = SigmoidItemAsymmetricFactorModel()
+    m.ratings = Ratings(u, i, g["iafm_small/values"])
+    m.additional_feedback = Ratings(au, ai, np.ones(len(au), np.float32))
+    m.MaxUserID, m.MaxItemID = len(off) - 2, int(max(i.max(), ai.max()))
+    o2, it2 = m._items_rated_by_user()
+    np.testing.assert_array_equal(o2, off)
+    np.testing.assert_array_equal(it2, items)
