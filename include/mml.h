@@ -131,11 +131,15 @@ enum {
                           (the batch step never reads current_learnrate); the schedule field is
                           ignored (the batch step is order-independent up to the per-row
                           accumulation order, which follows the stored visit order) */
-    MML_MF_ITEM_ASYM = 3 /* SigmoidItemAsymmetricFactorModel (SigmoidItemAsymmetricFactorModel.cs:
+    MML_MF_ITEM_ASYM = 3, /* SigmoidItemAsymmetricFactorModel (SigmoidItemAsymmetricFactorModel.cs:
                             43-344): a BiasedMatrixFactorization whose user vector is y summed over
                             the items the user rated (training + AdditionalFeedback) / sqrt(count);
-                            mml_bmf_set_item_feedback before iterate; ORDERED (bit-faithful) or
-                            HOGWILD (ABI 3) */
+                            mml_bmf_set_implicit_feedback before iterate; ORDERED (bit-faithful)
+                            or HOGWILD (ABI 3) */
+    MML_MF_USER_ASYM = 4 /* SigmoidUserAsymmetricFactorModel (SigmoidUserAsymmetricFactorModel.cs:
+                            43-309): the mirror -- the item vector is x summed over the users who
+                            rated the item / sqrt(count), each rating trains U_u and those x rows
+                            (ABI 3) */
 };
 
 typedef struct {
@@ -226,15 +230,21 @@ mml_status mml_bmf_predict_vectors(mml_bmf* h, int32_t n_vectors, const float* v
                                    const int32_t* vector_index, const int32_t* items, int64_t n,
                                    float* out);
 
-/* MML_MF_ITEM_ASYM: the items_rated_by_user CSR (ITransductiveRatingPredictor.ItemsRatedByUser,
- * ITransductiveRatingPredictor.cs:63-79: per user the training items in rating-index order, then
- * AdditionalFeedback's, distinct; n_rows = n_users), y [n_items x k] (InitModel :290-301) and
- * y_reg [n_items] (Train :72-77).  U then holds PrecomputeUserFactors (:305-331), refreshed after
- * every epoch, so Predict / evaluate read the reference's user_factors (ABI 3). */
-mml_status mml_bmf_set_item_feedback(mml_bmf* h, int32_t n_rows, const int64_t* offsets,
-                                     const int32_t* items, const float* y, const float* y_reg);
-/* y [n_items x k] (SaveModel writes it, :150-162) */
-mml_status mml_bmf_get_item_feedback_factors(mml_bmf* h, float* y);
+/* The asymmetric models' implicit feedback (ABI 3).
+ * MML_MF_ITEM_ASYM: lists = the items_rated_by_user CSR (ITransductiveRatingPredictor.
+ *   ItemsRatedByUser, ITransductiveRatingPredictor.cs:63-79: per user the training items in
+ *   rating-index order, then AdditionalFeedback's, distinct; n_rows = n_users), factors = y
+ *   [n_items x k] (InitModel, SigmoidItemAsymmetricFactorModel.cs:290-301), reg = y_reg [n_items]
+ *   (Train :72-77).  U then holds PrecomputeUserFactors (:305-331), refreshed after every epoch.
+ * MML_MF_USER_ASYM: lists = UsersWhoRated (:40-55; n_rows = n_items), factors = x [n_users x k]
+ *   (SigmoidUserAsymmetricFactorModel.cs:252-263), reg = x_reg [n_users] (Train :66-80); V then
+ *   holds PrecomputeItemFactors (:265-296).
+ * Predict / evaluate therefore read the reference's precomputed factors. */
+mml_status mml_bmf_set_implicit_feedback(mml_bmf* h, int32_t n_rows, const int64_t* offsets,
+                                         const int32_t* ids, const float* factors,
+                                         const float* reg);
+/* y [n_items x k] / x [n_users x k] (SaveModel writes it) */
+mml_status mml_bmf_get_implicit_factors(mml_bmf* h, float* factors);
 
 /* ------------------------------------------------------------------ BPRMF */
 enum {

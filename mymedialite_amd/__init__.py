@@ -7,10 +7,11 @@ from .data import IdentityMapping, Mapping, PosOnlyFeedback, Ratings, read_items
 from .random import Random, SystemRandom
 from .item_recommendation import BPRMF, WRMF, SoftMarginRankingMF, WeightedBPRMF
 from .rating_prediction import (BiasedMatrixFactorization, MatrixFactorization,
-                                SigmoidItemAsymmetricFactorModel, SocialMF)
+                                SigmoidItemAsymmetricFactorModel,
+                                SigmoidUserAsymmetricFactorModel, SocialMF)
 
 __all__ = ["BiasedMatrixFactorization", "MatrixFactorization", "SocialMF",
-           "SigmoidItemAsymmetricFactorModel", "BPRMF", "WRMF",
+           "SigmoidItemAsymmetricFactorModel", "SigmoidUserAsymmetricFactorModel", "BPRMF", "WRMF",
            "SoftMarginRankingMF", "WeightedBPRMF", "Ratings",
            "PosOnlyFeedback", "Mapping", "IdentityMapping", "read_ratings", "read_items", "Random",
            "SystemRandom"]

@@ -830,12 +830,16 @@ inline int lanes_per_rating(int k) {
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
-// SigmoidItemAsymmetricFactorModel (MML_MF_ITEM_ASYM; RatingPrediction/
-// SigmoidItemAsymmetricFactorModel.cs:43-344).  The user is represented by y summed over the
-// items they rated (training + AdditionalFeedback, the items_rated_by_user CSR), / sqrt(count).
-// One wavefront per rating at a time, lane f owns factors f, f + 64, ... (KM per lane), so every
-// per-factor sum and update runs in the reference's order.  ORDERED = one wavefront over the
-// whole stream (bit-faithful); HOGWILD = many wavefronts on chunks of it.
+// The asymmetric factor models.  SigmoidItemAsymmetricFactorModel (MML_MF_ITEM_ASYM;
+// RatingPrediction/SigmoidItemAsymmetricFactorModel.cs:43-344): the user is y summed over the
+// items they rated (training + AdditionalFeedback, the items_rated_by_user CSR) / sqrt(count), and
+// each rating trains the item's factors and those y rows.  SigmoidUserAsymmetricFactorModel
+// (MML_MF_USER_ASYM, SigmoidUserAsymmetricFactorModel.cs:43-309) is its mirror (USERS = true):
+// the item is x summed over the users who rated it, and each rating trains the user's factors
+// and those x rows.  X = the implicit factor matrix (y or x), lists = the CSR keyed by the
+// represented side.  One wavefront per rating at a time, lane f owns factors f, f + 64, ... (KM
+// per lane), so every per-factor sum and update runs in the reference's order.  ORDERED = one
+// wavefront over the whole stream (bit-faithful); HOGWILD = many wavefronts on chunks of it.
 
 // the user vector: SumOfRows (DataType/MatrixExtensions.cs:125-135, float, list order),
 // / sqrt(count) in double, cast to float (Iterate :104-107, PrecomputeUserFactors :316-331)
@@ -861,10 +865,10 @@ __device__ __forceinline__ double iafm_user_vector(const float* __restrict__ Y, 
     return norm;
 }
 
-template <int LOSS, int KM>
+template <int LOSS, int KM, bool USERS>
 __global__ __launch_bounds__(64) void iafm_sgd_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
-    int64_t n, int64_t chunk, float* Y, float* V, float* bu, float* bi, int32_t k, int32_t ld,
+    int64_t n, int64_t chunk, float* Y, float* T, float* bu, float* bi, int32_t k, int32_t ld,
     BmfScalars s, const int32_t* __restrict__ cnt_u, const int32_t* __restrict__ cnt_i,
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ritems,
     const float* __restrict__ y_reg) {
@@ -875,8 +879,9 @@ __global__ __launch_bounds__(64) void iafm_sgd_kernel(
         const int32_t u = su[x], i = si[x];
         const float r = sr[x];
         float vec[KM], qi[KM], prod[KM];
-        const double norm = iafm_user_vector<KM>(Y, k, ld, roff, ritems, u, lane, vec);
-        float* Vi = V + (int64_t)i * ld;
+        const int32_t key = USERS ? i : u;  // the represented side
+        const double norm = iafm_user_vector<KM>(Y, k, ld, roff, ritems, key, lane, vec);
+        float* Vi = T + (int64_t)(USERS ? u : i) * ld;  // the trained row: U_u or V_i
 #pragma unroll
         for (int m = 0; m < KM; ++m) {
             const int f = lane + 64 * m;
@@ -913,12 +918,12 @@ __global__ __launch_bounds__(64) void iafm_sgd_kernel(
             const int f = lane + 64 * m;
             const float i_f = qi[m];
             // delta_i is a float expression widened to double; Inc adds (float)(lr * delta)
-            const double delta_i = (double)(g * vec[m] - reg_i * i_f);
+            const double delta_i = (double)(g * vec[m] - (USERS ? reg_u : reg_i) * i_f);
             if (f < k) Vi[f] = i_f + (float)((double)s.lr * delta_i);
             common[m] = ngc * (double)i_f;
         }
         // y rows of every item the user rated (:137-142), list order per factor
-        const int64_t b = roff[u], e = roff[u + 1];
+        const int64_t b = roff[key], e = roff[key + 1];
         for (int64_t t = b; t < e; ++t) {
             const int32_t j = ritems[t];
             const float yr = y_reg[j];
@@ -935,7 +940,8 @@ __global__ __launch_bounds__(64) void iafm_sgd_kernel(
     }
 }
 
-// PrecomputeUserFactors (:305-331): U[u] = the user vector; users without items get zeros
+// PrecomputeUserFactors (:305-331) / PrecomputeItemFactors (SigmoidUserAsymmetricFactorModel.cs:
+// 265-296): row r of U (or V) = the represented vector of r; rows with an empty list get zeros
 template <int KM>
 __global__ __launch_bounds__(64) void iafm_user_factors_kernel(
     const float* __restrict__ Y, int32_t k, int32_t ld, const int64_t* __restrict__ roff,
@@ -985,7 +991,7 @@ struct mml_bmf {
     mml::DeviceArray<int64_t> rated_off;
     mml::DeviceArray<int32_t> rated_items;
     mml::DeviceArray<float> Y, y_reg;
-    bool has_item_feedback = false;
+    bool has_implicit = false;
 };
 
 namespace {
@@ -1222,15 +1228,18 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     MML_HIP(hipGetLastError());
 }
 
-// U <- PrecomputeUserFactors (the representation Predict and the evaluators read)
+// U (or V) <- PrecomputeUserFactors / PrecomputeItemFactors (what Predict and the evaluators read)
 void iafm_user_factors(mml_bmf* h) {
     const int km = (h->k + 63) / 64;
-    const int grid = std::max(1, std::min(h->n_users, 65536));
+    const bool users = h->p.model == MML_MF_USER_ASYM;
+    const int32_t rows = users ? h->n_items : h->n_users;
+    if (rows == 0) return;
+    const int grid = std::max(1, std::min(rows, 65536));
     hipStream_t st = h->ctx->stream;
 #define MML_IUF(KM)                                                                            \
     iafm_user_factors_kernel<KM><<<grid, 64, 0, st>>>(h->Y.get(), h->k, h->ld,                 \
                                                       h->rated_off.get(), h->rated_items.get(), \
-                                                      h->n_users, h->U.get())
+                                                      rows, users ? h->V.get() : h->U.get())
     switch (km) {
         case 1: MML_IUF(1); break;
         case 2: MML_IUF(2); break;
@@ -1255,17 +1264,25 @@ void iafm_epoch(mml_bmf* h, const BmfScalars& s) {
             waves = std::min<int64_t>(256 * 8, std::max<int64_t>(1, n / 2048));
         const int64_t chunk = (n + waves - 1) / waves;
         const int km = (h->k + 63) / 64;
-#define MML_IAFM(KM)                                                                           \
-    iafm_sgd_kernel<LOSS, KM><<<(int)waves, 64, 0, st>>>(                                      \
-        h->su.get(), h->si.get(), h->sr.get(), n, chunk, h->Y.get(), h->V.get(), h->bu.get(),  \
-        h->bi.get(), h->k, h->ld, s, cu, ci, h->rated_off.get(), h->rated_items.get(),          \
-        h->y_reg.get())
-        switch (km) {
-            case 1: MML_IAFM(1); break;
-            case 2: MML_IAFM(2); break;
-            case 3: MML_IAFM(3); break;
-            default: MML_IAFM(4); break;
+        const bool users = h->p.model == MML_MF_USER_ASYM;
+#define MML_IAFM(KM, USERS)                                                                    \
+    iafm_sgd_kernel<LOSS, KM, USERS><<<(int)waves, 64, 0, st>>>(                               \
+        h->su.get(), h->si.get(), h->sr.get(), n, chunk, h->Y.get(),                           \
+        USERS ? h->U.get() : h->V.get(), h->bu.get(), h->bi.get(), h->k, h->ld, s, cu, ci,     \
+        h->rated_off.get(), h->rated_items.get(), h->y_reg.get())
+#define MML_IAFM_K(USERS)                    \
+    switch (km) {                            \
+        case 1: MML_IAFM(1, USERS); break;   \
+        case 2: MML_IAFM(2, USERS); break;   \
+        case 3: MML_IAFM(3, USERS); break;   \
+        default: MML_IAFM(4, USERS); break;  \
+    }
+        if (users) {
+            MML_IAFM_K(true);
+        } else {
+            MML_IAFM_K(false);
         }
+#undef MML_IAFM_K
 #undef MML_IAFM
         MML_HIP(hipGetLastError());
     }
@@ -1314,7 +1331,7 @@ extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params,
                     "num_factors must be in [1, 256]");
         MML_REQUIRE(params->loss >= MML_LOSS_RMSE && params->loss <= MML_LOSS_LOGISTIC,
                     "unknown loss");
-        MML_REQUIRE(params->model >= MML_MF_BIASED && params->model <= MML_MF_ITEM_ASYM,
+        MML_REQUIRE(params->model >= MML_MF_BIASED && params->model <= MML_MF_USER_ASYM,
                     "unknown model family");
         MML_REQUIRE(params->schedule >= MML_SCHEDULE_ORDERED &&
                         params->schedule <= MML_SCHEDULE_HOGWILD_COHERENT,
@@ -1499,14 +1516,14 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
     return guard([&] {
         check_handle(h);
         MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
-        if (h->p.model == MML_MF_ITEM_ASYM) {
-            MML_REQUIRE(h->has_item_feedback, "set_item_feedback must precede iterate");
+        const bool asym = h->p.model == MML_MF_ITEM_ASYM || h->p.model == MML_MF_USER_ASYM;
+        if (asym) {
+            MML_REQUIRE(h->has_implicit, "set_implicit_feedback must precede iterate");
             MML_REQUIRE(h->p.schedule == MML_SCHEDULE_ORDERED ||
                             h->p.schedule == MML_SCHEDULE_HOGWILD,
-                        "the item-asymmetric model runs the ORDERED or HOGWILD schedule");
+                        "the asymmetric models run the ORDERED or HOGWILD schedule");
         }
-        if (h->p.schedule == MML_SCHEDULE_DSGD && h->p.model != MML_MF_SOCIAL &&
-            h->p.model != MML_MF_ITEM_ASYM) {
+        if (h->p.schedule == MML_SCHEDULE_DSGD && h->p.model != MML_MF_SOCIAL && !asym) {
             MML_REQUIRE(h->G > 0, "DSGD schedule needs set_blocks");
             MML_REQUIRE(subepoch_sequence, "DSGD schedule needs a sub-epoch sequence");
             for (int32_t x = 0; x < h->G; ++x)
@@ -1525,7 +1542,7 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
         s.reg_i = h->p.reg_i;
         hipStream_t st = h->ctx->stream;
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
-        if (h->p.model == MML_MF_ITEM_ASYM) {
+        if (asym) {
             switch (h->p.loss) {
                 case MML_LOSS_MAE: iafm_epoch<MML_LOSS_MAE>(h, s); break;
                 case MML_LOSS_LOGISTIC: iafm_epoch<MML_LOSS_LOGISTIC>(h, s); break;
@@ -1665,8 +1682,8 @@ extern "C" mml_status mml_bmf_allreduce_items(mml_bmf* h) {
         mml_ctx* c = h->ctx;
         if (c->nranks <= 1) return;
         MML_REQUIRE(c->comm, "context has no communicator (mml_ctx_comm_init)");
-        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM,
-                    "the item-asymmetric model's y is not averaged across ranks");
+        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM && h->p.model != MML_MF_USER_ASYM,
+                    "the asymmetric models' implicit factors are not averaged across ranks");
         c->activate();
         hipStream_t st = c->stream;
         const size_t nv = (size_t)h->n_items * h->ld;
@@ -1711,8 +1728,8 @@ extern "C" mml_status mml_bmf_fold_in(mml_bmf* h, int32_t n_fold, const int64_t*
     return guard([&] {
         check_handle(h);
         MML_REQUIRE(h->has_model, "no model");
-        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM,
-                    "SigmoidItemAsymmetricFactorModel has its own FoldIn (not on the GPU path)");
+        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM && h->p.model != MML_MF_USER_ASYM,
+                    "the asymmetric models have their own FoldIn (not on the GPU path)");
         MML_REQUIRE(n_fold >= 0 && num_iter >= 0, "negative sizes");
         if (n_fold == 0) return;
         MML_REQUIRE(rated_off && init_factors && out_vectors, "null arguments");
@@ -1777,8 +1794,8 @@ extern "C" mml_status mml_bmf_predict_vectors(mml_bmf* h, int32_t n_vectors, con
     return guard([&] {
         check_handle(h);
         MML_REQUIRE(h->has_model, "no model");
-        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM,
-                    "SigmoidItemAsymmetricFactorModel has its own FoldIn (not on the GPU path)");
+        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM && h->p.model != MML_MF_USER_ASYM,
+                    "the asymmetric models have their own FoldIn (not on the GPU path)");
         MML_REQUIRE(n_vectors >= 0 && n >= 0, "negative sizes");
         if (n == 0) return;
         MML_REQUIRE(vectors && vector_index && items && out, "null arguments");
@@ -1861,14 +1878,19 @@ extern "C" mml_status mml_bmf_set_user_relation(mml_bmf* h, int32_t n_rows, cons
     });
 }
 
-extern "C" mml_status mml_bmf_set_item_feedback(mml_bmf* h, int32_t n_rows, const int64_t* offsets,
+extern "C" mml_status mml_bmf_set_implicit_feedback(mml_bmf* h, int32_t n_rows, const int64_t* offsets,
                                                 const int32_t* items, const float* y,
                                                 const float* y_reg) {
     return guard([&] {
         check_handle(h);
-        MML_REQUIRE(h->p.model == MML_MF_ITEM_ASYM,
-                    "item feedback belongs to SigmoidItemAsymmetricFactorModel handles");
-        MML_REQUIRE(n_rows == h->n_users, "one row of rated items per user (n_rows = n_users)");
+        const bool users = h->p.model == MML_MF_USER_ASYM;
+        MML_REQUIRE(h->p.model == MML_MF_ITEM_ASYM || users,
+                    "implicit feedback belongs to the asymmetric models' handles");
+        // ITEM_ASYM: a row of rated items per user, y [n_items x k]; USER_ASYM: a row of users
+        // per item, x [n_users x k]
+        const int32_t n_list = users ? h->n_items : h->n_users;
+        const int32_t n_x = users ? h->n_users : h->n_items;
+        MML_REQUIRE(n_rows == n_list, "one list per user (ITEM_ASYM) / per item (USER_ASYM)");
         MML_REQUIRE(offsets && y && y_reg, "null argument");
         MML_REQUIRE(offsets[0] == 0, "offsets[0] must be 0");
         for (int32_t u = 0; u < n_rows; ++u)
@@ -1876,36 +1898,37 @@ extern "C" mml_status mml_bmf_set_item_feedback(mml_bmf* h, int32_t n_rows, cons
         const int64_t nnz = offsets[n_rows];
         MML_REQUIRE(nnz == 0 || items, "null items");
         for (int64_t x = 0; x < nnz; ++x)
-            MML_REQUIRE(items[x] >= 0 && items[x] < h->n_items, "rated item id out of range");
+            MML_REQUIRE(items[x] >= 0 && items[x] < n_x, "list id out of range");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
-        h->has_item_feedback = false;
+        h->has_implicit = false;
         h->rated_off.alloc((size_t)n_rows + 1);
         h->rated_items.alloc((size_t)std::max<int64_t>(1, nnz));
-        h->Y.alloc((size_t)std::max<int64_t>(1, (int64_t)h->n_items * h->ld));
-        h->y_reg.alloc((size_t)std::max(1, h->n_items));
+        h->Y.alloc((size_t)std::max<int64_t>(1, (int64_t)n_x * h->ld));
+        h->y_reg.alloc((size_t)std::max(1, n_x));
         MML_HIP(hipMemcpyAsync(h->rated_off.get(), offsets, sizeof(int64_t) * (n_rows + 1),
                                hipMemcpyHostToDevice, st));
         if (nnz)
             MML_HIP(hipMemcpyAsync(h->rated_items.get(), items, sizeof(int32_t) * nnz,
                                    hipMemcpyHostToDevice, st));
-        upload_padded(h, h->Y.get(), y, h->n_items);
-        if (h->n_items)
-            MML_HIP(hipMemcpyAsync(h->y_reg.get(), y_reg, sizeof(float) * h->n_items,
+        upload_padded(h, h->Y.get(), y, n_x);
+        if (n_x)
+            MML_HIP(hipMemcpyAsync(h->y_reg.get(), y_reg, sizeof(float) * n_x,
                                    hipMemcpyHostToDevice, st));
-        if (h->n_users) iafm_user_factors(h);
+        iafm_user_factors(h);
         MML_HIP(hipStreamSynchronize(st));
-        h->has_item_feedback = true;
+        h->has_implicit = true;
     });
 }
 
-extern "C" mml_status mml_bmf_get_item_feedback_factors(mml_bmf* h, float* y) {
+extern "C" mml_status mml_bmf_get_implicit_factors(mml_bmf* h, float* y) {
     return guard([&] {
         check_handle(h);
-        MML_REQUIRE(h->has_item_feedback, "no item feedback factors (set_item_feedback first)");
+        MML_REQUIRE(h->has_implicit, "no implicit factors (set_implicit_feedback first)");
         MML_REQUIRE(y, "null argument");
         h->ctx->activate();
-        download_padded(h, y, h->Y.get(), h->n_items);
+        download_padded(h, y, h->Y.get(),
+                        h->p.model == MML_MF_USER_ASYM ? h->n_users : h->n_items);
         MML_HIP(hipStreamSynchronize(h->ctx->stream));
     });
 }

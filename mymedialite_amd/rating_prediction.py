@@ -665,21 +665,19 @@ class SocialMF(BiasedMatrixFactorization):
             self.NumIter, self.BoldDriver, self.Loss)
 
 
-class SigmoidItemAsymmetricFactorModel(BiasedMatrixFactorization):
-    """GPU-backed MyMediaLite.RatingPrediction.SigmoidItemAsymmetricFactorModel
-    (SigmoidItemAsymmetricFactorModel.cs:43-344, ITransductiveRatingPredictor): a
-    BiasedMatrixFactorization whose user vector is y summed over the items the user rated (training
-    and ``additional_feedback``) / sqrt(count); every rating updates the item's factors and the y
-    rows of all the user's items (Iterate :91-147, MML_MF_ITEM_ASYM).  ``ordered`` (default) is
-    the reference's sequential loop bit for bit; ``hogwild`` runs many wavefronts.  BoldDriver
-    (its own ComputeObjective :211-243), MaxThreads > 1 and FoldIn are not on the GPU path."""
+class _AsymmetricFactorModel(BiasedMatrixFactorization):
+    """The Sigmoid*AsymmetricFactorModels (ITransductiveRatingPredictor): a BiasedMatrixFactorization
+    in which one side is represented by implicit factors summed over its feedback list (training
+    and ``additional_feedback``) / sqrt(count).  ``ordered`` (default) is the reference's sequential
+    loop bit for bit; ``hogwild`` runs many wavefronts.  BoldDriver (their own ComputeObjective),
+    MaxThreads > 1 and FoldIn are not on the GPU path."""
     PROPERTIES = dict(BiasedMatrixFactorization.PROPERTIES)
-    MODEL = N.MF_ITEM_ASYM
-    TYPE_NAME = "MyMediaLite.RatingPrediction.SigmoidItemAsymmetricFactorModel"
+    USER_SIDE = False  # False: y per item, lists per user; True: x per user, lists per item
 
     def __init__(self, **kw):
         super().__init__()
-        # SigmoidItemAsymmetricFactorModel() (:56-63)
+        # the models' constructors (SigmoidItemAsymmetricFactorModel.cs:56-63,
+        # SigmoidUserAsymmetricFactorModel.cs:56-63)
         self.Regularization = 0.015
         self.LearnRate = 0.001
         self.BiasLearnRate = 0.7
@@ -694,65 +692,88 @@ class SigmoidItemAsymmetricFactorModel(BiasedMatrixFactorization):
             raise ValueError(f"unknown Schedule '{self.Schedule}' for {type(self).__name__}")
         return s
 
-    def _items_rated_by_user(self):
-        """ItemsRatedByUser (ITransductiveRatingPredictor.cs:63-79): per user the training items in
-        rating-index order (ByUser), then AdditionalFeedback's, distinct (Union) -- as CSR."""
+    def _feedback_lists(self):
+        """ItemsRatedByUser / UsersWhoRated (ITransductiveRatingPredictor.cs:40-79): per key the
+        training partners in rating-index order (ByUser / ByItem), then AdditionalFeedback's,
+        distinct (Union) -- as CSR."""
         r, a = self._ratings, self.additional_feedback
-        nu, ni = self.MaxUserID + 1, self.MaxItemID + 1
         us, its = [N.i32(r.users)], [N.i32(r.items)]
         if a is not None and len(a.users):
             us.append(N.i32(a.users))
             its.append(N.i32(a.items))
         u = np.concatenate(us).astype(np.int64)
         i = np.concatenate(its).astype(np.int64)
-        seq = np.arange(len(u))
-        key = u * ni + i
-        _, first = np.unique(key, return_index=True)  # first appearance of each (user, item)
-        first = first[np.lexsort((seq[first], u[first]))]  # by user, then appearance
-        off = np.zeros(nu + 1, np.int64)
-        np.cumsum(np.bincount(u[first], minlength=nu), out=off[1:])
-        return off, N.i32(i[first])
+        keys, vals = (i, u) if self.USER_SIDE else (u, i)
+        n_keys = self.MaxItemID + 1 if self.USER_SIDE else self.MaxUserID + 1
+        n_vals = self.MaxUserID + 1 if self.USER_SIDE else self.MaxItemID + 1
+        seq = np.arange(len(keys))
+        _, first = np.unique(keys * n_vals + vals, return_index=True)  # first appearance
+        first = first[np.lexsort((seq[first], keys[first]))]  # by key, then appearance
+        off = np.zeros(n_keys + 1, np.int64)
+        np.cumsum(np.bincount(keys[first], minlength=n_keys), out=off[1:])
+        return off, N.i32(vals[first])
 
     def init_model(self):
-        """Train (:66-80) sizes and y_reg, then InitModel (:290-301): y (rows of items without
-        training ratings zeroed), then BiasedMatrixFactorization.InitModel (U, V, biases)."""
+        """Train (sizes and the implicit factors' regularisation, :66-80), then InitModel: the
+        implicit factors (rows without training ratings zeroed), then BiasedMatrixFactorization's
+        InitModel (U, V, biases)."""
+        name = type(self).__name__
         if self.BoldDriver:
-            raise NotImplementedError("SigmoidItemAsymmetricFactorModel with BoldDriver (its own "
-                                      "ComputeObjective, :211-243) is not on the GPU path")
+            raise NotImplementedError(f"{name} with BoldDriver (its own ComputeObjective) is not "
+                                      "on the GPU path")
         if self.MaxThreads > 1:
-            raise NotImplementedError("SigmoidItemAsymmetricFactorModel with MaxThreads > 1 is "
-                                      "not on the GPU path")
+            raise NotImplementedError(f"{name} with MaxThreads > 1 is not on the GPU path")
         r, a = self._ratings, self.additional_feedback
         if a is not None and len(a.users):
             self.MaxUserID = max(r.max_user_id, int(np.max(a.users)))
             self.MaxItemID = max(r.max_item_id, int(np.max(a.items)))
         k = int(self.NumFactors)
-        ni = self.MaxItemID + 1
-        fb = np.bincount(N.i32(r.items), minlength=ni)
+        side = N.i32(r.users) if self.USER_SIDE else N.i32(r.items)
+        n_x = self.MaxUserID + 1 if self.USER_SIDE else self.MaxItemID + 1
+        fb = np.bincount(side, minlength=n_x)  # UserFeedbackCounts / ItemFeedbackCounts
         if a is not None and len(a.users):
-            fb = fb + np.bincount(N.i32(a.items), minlength=ni)
-        reg_i = float(np.float32(self.RegI))
-        y_reg = np.zeros(ni, np.float32)
+            fb = fb + np.bincount(N.i32(a.users if self.USER_SIDE else a.items), minlength=n_x)
+        reg = float(np.float32(self.RegU if self.USER_SIDE else self.RegI))
+        x_reg = np.zeros(n_x, np.float32)
         nz = fb > 0
-        y_reg[nz] = (np.float32(reg_i / np.sqrt(fb[nz].astype(np.float64)))
-                     if self.FrequencyRegularization else np.float32(reg_i))
+        x_reg[nz] = (np.float32(reg / np.sqrt(fb[nz].astype(np.float64)))
+                     if self.FrequencyRegularization else np.float32(reg))
         rng = Random.get_instance()
-        y = rng.fill_normal(ni * k, self.InitMean, self.InitStdDev).reshape(ni, k)
-        trained = np.zeros(ni, bool)
-        trained[:len(r.count_by_item)] = r.count_by_item > 0
-        y[~trained] = 0.0
+        x = rng.fill_normal(n_x * k, self.InitMean, self.InitStdDev).reshape(n_x, k)
+        cnt = r.count_by_user if self.USER_SIDE else r.count_by_item
+        trained = np.zeros(n_x, bool)
+        trained[:len(cnt)] = cnt > 0
+        x[~trained] = 0.0
         super().init_model()
-        off, items = self._items_rated_by_user()
-        N.check(N.lib().mml_bmf_set_item_feedback(
-            self._h, self.MaxUserID + 1, N.ptr(off, N._i64p), N.ptr(items, N._i32p),
-            N.ptr(N.f32(y), N._f32p), N.ptr(y_reg, N._f32p)))
+        off, ids = self._feedback_lists()
+        N.check(N.lib().mml_bmf_set_implicit_feedback(
+            self._h, len(off) - 1, N.ptr(off, N._i64p), N.ptr(ids, N._i32p),
+            N.ptr(N.f32(x), N._f32p), N.ptr(x_reg, N._f32p)))
+
+    def _implicit_factors(self):
+        n_x = self.MaxUserID + 1 if self.USER_SIDE else self.MaxItemID + 1
+        out = np.empty((n_x, int(self.NumFactors)), np.float32)
+        N.check(N.lib().mml_bmf_get_implicit_factors(self._h, N.ptr(out, N._f32p)))
+        return out
+
+    def load_model(self, path: str):
+        raise NotImplementedError(f"{type(self).__name__}.LoadModel needs the training data to "
+                                  "rebuild the precomputed factors; not on the GPU path")
+
+
+class SigmoidItemAsymmetricFactorModel(_AsymmetricFactorModel):
+    """GPU-backed MyMediaLite.RatingPrediction.SigmoidItemAsymmetricFactorModel
+    (SigmoidItemAsymmetricFactorModel.cs:43-344): the user vector is y summed over the items the
+    user rated / sqrt(count); every rating updates the item's factors and the y rows of all the
+    user's items (Iterate :91-147, MML_MF_ITEM_ASYM).  user_factors = PrecomputeUserFactors."""
+    MODEL = N.MF_ITEM_ASYM
+    TYPE_NAME = "MyMediaLite.RatingPrediction.SigmoidItemAsymmetricFactorModel"
+    USER_SIDE = False
 
     @property
     def y(self):
         """y [n_items x k], the item factors that express the users (:49-50)."""
-        out = np.empty((self.MaxItemID + 1, int(self.NumFactors)), np.float32)
-        N.check(N.lib().mml_bmf_get_item_feedback_factors(self._h, N.ptr(out, N._f32p)))
-        return out
+        return self._implicit_factors()
 
     def save_model(self, path: str):
         """SaveModel (:150-162): global bias, min/max rating, user biases, item biases, y, item
@@ -768,10 +789,6 @@ class SigmoidItemAsymmetricFactorModel(BiasedMatrixFactorization):
             w.write_matrix(self.y)
             w.write_matrix(m["V"])
 
-    def load_model(self, path: str):
-        raise NotImplementedError("SigmoidItemAsymmetricFactorModel.LoadModel needs the training "
-                                  "data to rebuild the user vectors; not on the GPU path")
-
     def __str__(self):
         """ToString() (:335-341) with its placeholder slip kept: num_iter= repeats {7} (Decay) and
         loss= prints {8} (NumIter)."""
@@ -781,6 +798,44 @@ class SigmoidItemAsymmetricFactorModel(BiasedMatrixFactorization):
             self.NumFactors, _g(self.Regularization), _g(self.BiasReg),
             self.FrequencyRegularization, _g(self.LearnRate), _g(self.BiasLearnRate),
             _g(self.Decay), _g(self.Decay), self.NumIter)
+
+
+class SigmoidUserAsymmetricFactorModel(_AsymmetricFactorModel):
+    """GPU-backed MyMediaLite.RatingPrediction.SigmoidUserAsymmetricFactorModel
+    (SigmoidUserAsymmetricFactorModel.cs:43-309): the item vector is x summed over the users who
+    rated the item / sqrt(count); every rating updates the user's factors and the x rows of all
+    the item's users (Iterate :91-144, MML_MF_USER_ASYM).  item_factors = PrecomputeItemFactors."""
+    MODEL = N.MF_USER_ASYM
+    TYPE_NAME = "MyMediaLite.RatingPrediction.SigmoidUserAsymmetricFactorModel"
+    USER_SIDE = True
+
+    @property
+    def x(self):
+        """x [n_users x k], the user factors that express the items (:49-50)."""
+        return self._implicit_factors()
+
+    def save_model(self, path: str):
+        """SaveModel (:147-159): global bias, min/max rating, user biases, item biases, x, user
+        factors (version line "3.00")."""
+        from .model_io import ModelWriter
+        m = self.get_model()
+        with ModelWriter(path, self.TYPE_NAME, "3.00") as w:
+            w.write_float(self.global_bias)
+            w.write_float(self.min_rating)
+            w.write_float(self.max_rating)
+            w.write_vector(m["bu"])
+            w.write_vector(m["bi"])
+            w.write_matrix(self.x)
+            w.write_matrix(m["U"])
+
+    def __str__(self):
+        """ToString() (:298-305)."""
+        return ("SigmoidUserAsymmetricFactorModel num_factors={} regularization={} bias_reg={} "
+                "frequency_regularization={} learn_rate={} bias_learn_rate={} "
+                "learn_rate_decay={} num_iter={} loss={}").format(
+            self.NumFactors, _g(self.Regularization), _g(self.BiasReg),
+            self.FrequencyRegularization, _g(self.LearnRate), _g(self.BiasLearnRate),
+            _g(self.Decay), self.NumIter, self.Loss)
 
 
 def _g(x):

@@ -226,20 +226,24 @@ static void ora_iafm_user_vector(const float* Y, int k, const int64_t* rated_off
  * (RatingPrediction/SigmoidItemAsymmetricFactorModel.cs:91-147).  rated_off / rated_items: the
  * items_rated_by_user CSR (ITransductiveRatingPredictor.ItemsRatedByUser, :63-79: training items
  * in rating-index order, then AdditionalFeedback's, distinct); y_reg per item (Train :72-77).
- * vec: k floats of scratch. */
+ * user_side = 1: SigmoidUserAsymmetricFactorModel.Iterate (SigmoidUserAsymmetricFactorModel.cs:
+ * 91-144), the mirror -- Y = x, the lists = UsersWhoRated per item (:40-55), V = the user factors
+ * U it trains, y_reg = x_reg per user.  vec: k floats of scratch. */
 void ora_iafm_iterate(const ora_bmf_params* p, const int32_t* users, const int32_t* items,
                       const float* values, const int32_t* idx, int64_t n_idx, float* Y, float* V,
                       float* bu, float* bi, const int32_t* count_by_user,
                       const int32_t* count_by_item, const int64_t* rated_off,
-                      const int32_t* rated_items, const float* y_reg, float* vec) {
+                      const int32_t* rated_items, const float* y_reg, float* vec,
+                      int32_t user_side) {
     const int k = p->k;
     const float lr = p->learn_rate;
     for (int64_t n = 0; n < n_idx; n++) {
         const int32_t index = idx[n];
         const int32_t u = users[index], i = items[index];
-        float* Vi = V + (int64_t)i * k;
+        const int32_t key = user_side ? i : u;
+        float* Vi = V + (int64_t)(user_side ? u : i) * k;
         double norm;
-        ora_iafm_user_vector(Y, k, rated_off, rated_items, u, vec, &norm);
+        ora_iafm_user_vector(Y, k, rated_off, rated_items, key, vec, &norm);
         double score = (double)((p->global_bias + bu[u]) + bi[i]); /* float sum, :103 */
         float dot = 0.0f; /* RowScalarProduct(i, IList<float>) :183-196, float acc */
         for (int f = 0; f < k; f++) dot += Vi[f] * vec[f];
@@ -265,11 +269,11 @@ void ora_iafm_iterate(const ora_bmf_params* p, const int32_t* users, const int32
         if (p->update_user) bu[u] += blr * (g - (p->bias_reg * reg_u) * bu[u]);
         if (p->update_item) bi[i] += blr * (g - (p->bias_reg * reg_i) * bi[i]);
         const double ngc = (double)g / norm; /* normalized_gradient_common :126 */
-        const int64_t b = rated_off[u], e = rated_off[u + 1];
+        const int64_t b = rated_off[key], e = rated_off[key + 1];
         for (int f = 0; f < k; f++) {
             const float i_f = Vi[f];
-            if (!p->update_item) continue;
-            const double delta_i = (double)(g * vec[f] - reg_i * i_f); /* float expression */
+            if (!(user_side ? p->update_user : p->update_item)) continue;
+            const double delta_i = (double)(g * vec[f] - (user_side ? reg_u : reg_i) * i_f);
             Vi[f] += (float)((double)lr * delta_i);
             const double common = ngc * (double)i_f;
             for (int64_t t = b; t < e; t++) {

@@ -113,7 +113,7 @@ def lib():
                                     ctypes.c_int64, _f32p, _f32p, _f32p, _i32p]
         L.ora_iafm_iterate.argtypes = [
             ctypes.c_void_p, _i32p, _i32p, _f32p, _i32p, ctypes.c_int64, _f32p, _f32p, _f32p,
-            _f32p, _i32p, _i32p, _i64p, _i32p, _f32p, _f32p]
+            _f32p, _i32p, _i32p, _i64p, _i32p, _f32p, _f32p, ctypes.c_int32]
         L.ora_iafm_user_factors.argtypes = [_f32p, ctypes.c_int, ctypes.c_int32, _i64p, _i32p,
                                             _f32p]
         L.ora_wrmf_square.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f64p]
@@ -425,29 +425,39 @@ def items_rated_by_user(users, items, n_users, add_users=None, add_items=None):
     return off, np.array([i for r in rows for i in r], np.int32)
 
 
-def iafm_train(users, items, values, n_users, n_items, min_rating, max_rating, *, seed=1, k=10,
-               learn_rate=0.001, decay=1.0, reg_u=0.015, reg_i=0.015, bias_reg=0.33,
+def asym_train(users, items, values, n_users, n_items, min_rating, max_rating, *, side="item",
+               seed=1, k=10, learn_rate=0.001, decay=1.0, reg_u=0.015, reg_i=0.015, bias_reg=0.33,
                bias_learn_rate=0.7, num_iter=30, init_mean=0.0, init_stddev=0.1, loss=0,
                frequency_regularization=False, add_users=None, add_items=None, callback=None):
-    """SigmoidItemAsymmetricFactorModel.Train (SigmoidItemAsymmetricFactorModel.cs:66-80) ->
-    BiasedMatrixFactorization.Train (:173-194) with InitModel (:290-301: y, then U, then V) and
-    NumIter x Iterate(RandomIndex) (:91-147) + UpdateLearnRate.  n_users / n_items cover the
-    AdditionalFeedback ids.  Defaults are the model's (:56-63)."""
+    """side="item": SigmoidItemAsymmetricFactorModel.Train (SigmoidItemAsymmetricFactorModel.cs:
+    66-80) -> BiasedMatrixFactorization.Train (:173-194) with InitModel (:290-301: y, then U, then
+    V) and NumIter x Iterate(RandomIndex) (:91-147) + UpdateLearnRate; U = PrecomputeUserFactors.
+    side="user": SigmoidUserAsymmetricFactorModel (SigmoidUserAsymmetricFactorModel.cs:66-296),
+    the mirror: x per user, lists = UsersWhoRated, trains U, V = PrecomputeItemFactors.
+    n_users / n_items cover the AdditionalFeedback ids.  Defaults are the models' (:56-63)."""
     users, items, values = i32(users), i32(items), f32(values)
+    user_side = side == "user"
     rng = Rng(seed)
     cnt_u = np.bincount(users, minlength=int(users.max()) + 1).astype(np.int32)
     cnt_i = np.bincount(items, minlength=int(items.max()) + 1).astype(np.int32)
-    off, rated = items_rated_by_user(users, items, n_users, add_users, add_items)
-    fb_i = np.bincount(items, minlength=n_items)
-    if add_items is not None:
-        fb_i = fb_i + np.bincount(i32(add_items), minlength=n_items)
-    y_reg = np.zeros(n_items, np.float32)
-    for it in range(n_items):  # Train :72-77
-        if fb_i[it] > 0:
-            y_reg[it] = np.float32(reg_i / math.sqrt(fb_i[it])) if frequency_regularization \
-                else np.float32(reg_i)
-    Y = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
-    Y[[x for x in range(n_items) if x >= len(cnt_i) or cnt_i[x] == 0]] = 0
+    if user_side:  # UsersWhoRated: the same Union construction keyed by item
+        off, rated = items_rated_by_user(items, users, n_items, add_items, add_users)
+        n_x, keys, cnt_x, reg_x = n_users, users, cnt_u, reg_u
+        adds = add_users
+    else:
+        off, rated = items_rated_by_user(users, items, n_users, add_users, add_items)
+        n_x, keys, cnt_x, reg_x = n_items, items, cnt_i, reg_i
+        adds = add_items
+    fb = np.bincount(keys, minlength=n_x)  # UserFeedbackCounts / ItemFeedbackCounts
+    if adds is not None:
+        fb = fb + np.bincount(i32(adds), minlength=n_x)
+    x_reg = np.zeros(n_x, np.float32)
+    for it in range(n_x):  # Train :72-77
+        if fb[it] > 0:
+            x_reg[it] = np.float32(reg_x / math.sqrt(fb[it])) if frequency_regularization \
+                else np.float32(reg_x)
+    Y = rng.fill_normal(n_x * k, init_mean, init_stddev).reshape(n_x, k)
+    Y[[x for x in range(n_x) if x >= len(cnt_x) or cnt_x[x] == 0]] = 0
     U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
     V = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
     U[np.flatnonzero(cnt_u == 0)] = 0
@@ -466,6 +476,7 @@ def iafm_train(users, items, values, n_users, n_items, min_rating, max_rating, *
     lr = np.float32(learn_rate)
     random_index = None
     vec = np.zeros(k, np.float32)
+    T = U if user_side else V  # the factors Iterate trains
     L = lib()
     for epoch in range(num_iter):
         if random_index is None:
@@ -474,18 +485,28 @@ def iafm_train(users, items, values, n_users, n_items, min_rating, max_rating, *
                        range_, lr, bias_learn_rate, bias_reg, reg_u, reg_i)
         L.ora_iafm_iterate(ctypes.byref(p), _p(users, _i32p), _p(items, _i32p),
                            _p(values, _f32p), _p(random_index, _i32p), random_index.size,
-                           _p(Y, _f32p), _p(V, _f32p), _p(bu, _f32p), _p(bi, _f32p),
+                           _p(Y, _f32p), _p(T, _f32p), _p(bu, _f32p), _p(bi, _f32p),
                            _p(cu, _i32p), _p(ci, _i32p), _p(off, _i64p), _p(rated, _i32p),
-                           _p(y_reg, _f32p), _p(vec, _f32p))
+                           _p(x_reg, _f32p), _p(vec, _f32p), int(user_side))
         lr = np.float32(lr * np.float32(decay))
         if callback is not None:
-            callback(epoch, dict(Y=Y, V=V, bu=bu, bi=bi))
-    Uf = np.zeros((n_users, k), np.float32)
-    L.ora_iafm_user_factors(_p(Y, _f32p), k, n_users, _p(off, _i64p), _p(rated, _i32p),
-                            _p(Uf, _f32p))
-    return dict(Y=Y, U=Uf, V=V, bu=bu, bi=bi, init=init, global_bias=gb, range_=range_,
-                random_index=random_index, rated_off=off, rated_items=rated, y_reg=y_reg,
+            callback(epoch, dict(Y=Y, U=U, V=V, bu=bu, bi=bi))
+    n_rows = n_items if user_side else n_users
+    P = np.zeros((n_rows, k), np.float32)  # PrecomputeItemFactors / PrecomputeUserFactors
+    L.ora_iafm_user_factors(_p(Y, _f32p), k, n_rows, _p(off, _i64p), _p(rated, _i32p),
+                            _p(P, _f32p))
+    if user_side:
+        U_out, V_out = U, P
+    else:
+        U_out, V_out = P, V
+    return dict(Y=Y, U=U_out, V=V_out, bu=bu, bi=bi, init=init, global_bias=gb, range_=range_,
+                random_index=random_index, rated_off=off, rated_items=rated, y_reg=x_reg,
                 current_learnrate=lr)
+
+
+def iafm_train(*a, **kw):
+    """SigmoidItemAsymmetricFactorModel (asym_train side="item")."""
+    return asym_train(*a, side="item", **kw)
 
 
 def relation_csr(rows):

@@ -210,6 +210,19 @@ def case_iafm_small():
                 rated_off=st["rated_off"], rated_items=st["rated_items"], **snaps)
 
 
+def case_uafm_small():
+    # SigmoidUserAsymmetricFactorModel (SigmoidUserAsymmetricFactorModel.cs:66-144)
+    u, i, v, au, ai = iafm_case_data()
+    nu = max(int(u.max()), int(au.max())) + 1
+    ni = max(int(i.max()), int(ai.max())) + 1
+    snaps = {}
+    st = O.asym_train(u, i, v, nu, ni, 1.0, 5.0, side="user", seed=10, k=5, num_iter=3,
+                      learn_rate=0.01, add_users=au, add_items=ai,
+                      callback=lambda e, m: snaps.update({f"X{e}": m["Y"].copy()}))
+    return dict(init_X=st["init"]["Y"], X=st["Y"], U=st["U"], V=st["V"], bu=st["bu"],
+                bi=st["bi"], rated_off=st["rated_off"], rated_items=st["rated_items"], **snaps)
+
+
 def case_bpr_user_replacement_small():
     # IterateWithReplacementUniformUser (BPRMF.cs:183-211): ~deg(u) samples per user per epoch,
     # so rounds run out and refill
@@ -259,6 +272,7 @@ CASES = {
     "bpr_weighted_small": case_bpr_weighted_small,
     "bpr_user_replacement_small": case_bpr_user_replacement_small,
     "iafm_small": case_iafm_small,
+    "uafm_small": case_uafm_small,
     "bpr_pair_replacement_small": case_bpr_pair_replacement_small,
     "wrmf_small": case_wrmf_small,
 }
