@@ -136,9 +136,13 @@ enum {
                             the items the user rated (training + AdditionalFeedback) / sqrt(count);
                             mml_bmf_set_implicit_feedback before iterate; ORDERED (bit-faithful)
                             or HOGWILD (ABI 3) */
-    MML_MF_USER_ASYM = 4 /* SigmoidUserAsymmetricFactorModel (SigmoidUserAsymmetricFactorModel.cs:
+    MML_MF_USER_ASYM = 4, /* SigmoidUserAsymmetricFactorModel (SigmoidUserAsymmetricFactorModel.cs:
                             43-309): the mirror -- the item vector is x summed over the users who
                             rated the item / sqrt(count), each rating trains U_u and those x rows
+                            (ABI 3) */
+    MML_MF_COMBINED_ASYM = 5 /* SigmoidCombinedAsymmetricFactorModel
+                            (SigmoidCombinedAsymmetricFactorModel.cs:46-382): both -- user vector
+                            from y, item vector from x, each rating trains those x and y rows
                             (ABI 3) */
 };
 
@@ -230,21 +234,22 @@ mml_status mml_bmf_predict_vectors(mml_bmf* h, int32_t n_vectors, const float* v
                                    const int32_t* vector_index, const int32_t* items, int64_t n,
                                    float* out);
 
-/* The asymmetric models' implicit feedback (ABI 3).
- * MML_MF_ITEM_ASYM: lists = the items_rated_by_user CSR (ITransductiveRatingPredictor.
- *   ItemsRatedByUser, ITransductiveRatingPredictor.cs:63-79: per user the training items in
- *   rating-index order, then AdditionalFeedback's, distinct; n_rows = n_users), factors = y
- *   [n_items x k] (InitModel, SigmoidItemAsymmetricFactorModel.cs:290-301), reg = y_reg [n_items]
- *   (Train :72-77).  U then holds PrecomputeUserFactors (:305-331), refreshed after every epoch.
- * MML_MF_USER_ASYM: lists = UsersWhoRated (:40-55; n_rows = n_items), factors = x [n_users x k]
- *   (SigmoidUserAsymmetricFactorModel.cs:252-263), reg = x_reg [n_users] (Train :66-80); V then
- *   holds PrecomputeItemFactors (:265-296).
- * Predict / evaluate therefore read the reference's precomputed factors. */
-mml_status mml_bmf_set_implicit_feedback(mml_bmf* h, int32_t n_rows, const int64_t* offsets,
-                                         const int32_t* ids, const float* factors,
-                                         const float* reg);
-/* y [n_items x k] / x [n_users x k] (SaveModel writes it) */
-mml_status mml_bmf_get_implicit_factors(mml_bmf* h, float* factors);
+/* The asymmetric models' implicit feedback (ABI 3), one call per side the model uses.
+ * side 0 (MML_MF_ITEM_ASYM, MML_MF_COMBINED_ASYM): lists = the items_rated_by_user CSR
+ *   (ITransductiveRatingPredictor.ItemsRatedByUser, ITransductiveRatingPredictor.cs:63-79: per
+ *   user the training items in rating-index order, then AdditionalFeedback's, distinct;
+ *   n_rows = n_users), factors = y [n_items x k] (e.g. SigmoidItemAsymmetricFactorModel.cs:
+ *   290-301), reg = y_reg [n_items] (Train :72-77).  U then holds PrecomputeUserFactors.
+ * side 1 (MML_MF_USER_ASYM, MML_MF_COMBINED_ASYM): lists = UsersWhoRated (:40-55;
+ *   n_rows = n_items), factors = x [n_users x k], reg = x_reg [n_users].  V then holds
+ *   PrecomputeItemFactors.
+ * The precomputed factors are refreshed after every epoch, so Predict / evaluate read the
+ * reference's user_factors / item_factors. */
+mml_status mml_bmf_set_implicit_feedback(mml_bmf* h, int32_t side, int32_t n_rows,
+                                         const int64_t* offsets, const int32_t* ids,
+                                         const float* factors, const float* reg);
+/* y [n_items x k] (side 0) / x [n_users x k] (side 1), e.g. for SaveModel */
+mml_status mml_bmf_get_implicit_factors(mml_bmf* h, int32_t side, float* factors);
 
 /* ------------------------------------------------------------------ BPRMF */
 enum {

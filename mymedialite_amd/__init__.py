@@ -8,10 +8,12 @@ from .random import Random, SystemRandom
 from .item_recommendation import BPRMF, WRMF, SoftMarginRankingMF, WeightedBPRMF
 from .rating_prediction import (BiasedMatrixFactorization, MatrixFactorization,
                                 SigmoidItemAsymmetricFactorModel,
-                                SigmoidUserAsymmetricFactorModel, SocialMF)
+                                SigmoidUserAsymmetricFactorModel, SocialMF,
+                                SigmoidCombinedAsymmetricFactorModel)
 
 __all__ = ["BiasedMatrixFactorization", "MatrixFactorization", "SocialMF",
-           "SigmoidItemAsymmetricFactorModel", "SigmoidUserAsymmetricFactorModel", "BPRMF", "WRMF",
+           "SigmoidItemAsymmetricFactorModel", "SigmoidUserAsymmetricFactorModel",
+           "SigmoidCombinedAsymmetricFactorModel", "BPRMF", "WRMF",
            "SoftMarginRankingMF", "WeightedBPRMF", "Ratings",
            "PosOnlyFeedback", "Mapping", "IdentityMapping", "read_ratings", "read_items", "Random",
            "SystemRandom"]

@@ -830,29 +830,36 @@ inline int lanes_per_rating(int k) {
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
-// The asymmetric factor models.  SigmoidItemAsymmetricFactorModel (MML_MF_ITEM_ASYM;
-// RatingPrediction/SigmoidItemAsymmetricFactorModel.cs:43-344): the user is y summed over the
-// items they rated (training + AdditionalFeedback, the items_rated_by_user CSR) / sqrt(count), and
-// each rating trains the item's factors and those y rows.  SigmoidUserAsymmetricFactorModel
-// (MML_MF_USER_ASYM, SigmoidUserAsymmetricFactorModel.cs:43-309) is its mirror (USERS = true):
-// the item is x summed over the users who rated it, and each rating trains the user's factors
-// and those x rows.  X = the implicit factor matrix (y or x), lists = the CSR keyed by the
-// represented side.  One wavefront per rating at a time, lane f owns factors f, f + 64, ... (KM
-// per lane), so every per-factor sum and update runs in the reference's order.  ORDERED = one
-// wavefront over the whole stream (bit-faithful); HOGWILD = many wavefronts on chunks of it.
+// The asymmetric factor models (ITransductiveRatingPredictor).  Two implicit-feedback slots:
+//   slot 0: per user the items rated (training + AdditionalFeedback, ItemsRatedByUser) over y
+//           [n_items x k]: the user vector = y summed over the user's items / sqrt(count)
+//   slot 1: per item the users who rated it (UsersWhoRated) over x [n_users x k]: the item vector
+//           = x summed over the item's users / sqrt(count)
+// MODE kAsymItem (SigmoidItemAsymmetricFactorModel.cs:91-147): slot 0; trains V_i and y.
+// MODE kAsymUser (SigmoidUserAsymmetricFactorModel.cs:91-144): slot 1; trains U_u and x.
+// MODE kAsymCombined (SigmoidCombinedAsymmetricFactorModel.cs:108-182): both; trains x and y.
+// One wavefront per rating at a time, lane f owns factors f, f + 64, ... (KM per lane), so every
+// per-factor sum and update runs in the reference's order.  ORDERED = one wavefront over the
+// whole stream (bit-faithful); HOGWILD = many wavefronts on chunks of it.
+constexpr int kAsymItem = 0, kAsymUser = 1, kAsymCombined = 2;
 
-// the user vector: SumOfRows (DataType/MatrixExtensions.cs:125-135, float, list order),
-// / sqrt(count) in double, cast to float (Iterate :104-107, PrecomputeUserFactors :316-331)
+struct AsymSlot {
+    float* X;                         // the implicit factors (y or x)
+    const int64_t* __restrict__ off;  // the lists (CSR)
+    const int32_t* __restrict__ ids;
+    const float* __restrict__ reg;    // y_reg / x_reg
+};
+
+// the represented vector of row `key`: SumOfRows (DataType/MatrixExtensions.cs:125-135: float,
+// list order), / sqrt(count) in double, cast to float (e.g. :104-107, PrecomputeUserFactors)
 template <int KM>
-__device__ __forceinline__ double iafm_user_vector(const float* __restrict__ Y, int32_t k,
-                                                   int32_t ld, const int64_t* __restrict__ roff,
-                                                   const int32_t* __restrict__ ritems, int32_t u,
-                                                   int lane, float (&vec)[KM]) {
-    const int64_t b = roff[u], e = roff[u + 1];
+__device__ __forceinline__ double asym_vector(const AsymSlot& sl, int32_t k, int32_t ld,
+                                              int32_t key, int lane, float (&vec)[KM]) {
+    const int64_t b = sl.off[key], e = sl.off[key + 1];
 #pragma unroll
     for (int m = 0; m < KM; ++m) vec[m] = 0.0f;
     for (int64_t t = b; t < e; ++t) {
-        const float* row = Y + (int64_t)ritems[t] * ld;
+        const float* row = sl.X + (int64_t)sl.ids[t] * ld;
 #pragma unroll
         for (int m = 0; m < KM; ++m) {
             const int f = lane + 64 * m;
@@ -865,92 +872,120 @@ __device__ __forceinline__ double iafm_user_vector(const float* __restrict__ Y, 
     return norm;
 }
 
-template <int LOSS, int KM, bool USERS>
-__global__ __launch_bounds__(64) void iafm_sgd_kernel(
+// x.Inc / y.Inc over the list of `key`: X[t, f] += (float)(lr * (common_f - reg[t] * X[t, f]))
+template <int KM>
+__device__ __forceinline__ void asym_list_step(const AsymSlot& sl, int32_t k, int32_t ld,
+                                               int32_t key, int lane, float lr,
+                                               const double (&common)[KM]) {
+    const int64_t b = sl.off[key], e = sl.off[key + 1];
+    for (int64_t t = b; t < e; ++t) {
+        const int32_t j = sl.ids[t];
+        const float rg = sl.reg[j];
+        float* row = sl.X + (int64_t)j * ld;
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            const int f = lane + 64 * m;
+            if (f < k) {
+                const float y = row[f];
+                row[f] = y + (float)((double)lr * (common[m] - (double)(rg * y)));
+            }
+        }
+    }
+}
+
+template <int LOSS, int KM, int MODE>
+__global__ __launch_bounds__(64) void asym_sgd_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
-    int64_t n, int64_t chunk, float* Y, float* T, float* bu, float* bi, int32_t k, int32_t ld,
-    BmfScalars s, const int32_t* __restrict__ cnt_u, const int32_t* __restrict__ cnt_i,
-    const int64_t* __restrict__ roff, const int32_t* __restrict__ ritems,
-    const float* __restrict__ y_reg) {
+    int64_t n, int64_t chunk, AsymSlot s0, AsymSlot s1, float* U, float* V, float* bu, float* bi,
+    int32_t k, int32_t ld, BmfScalars s, const int32_t* __restrict__ cnt_u,
+    const int32_t* __restrict__ cnt_i) {
     const int lane = threadIdx.x;
     const int64_t begin = (int64_t)blockIdx.x * chunk;
     const int64_t end = min(begin + chunk, n);
     for (int64_t x = begin; x < end; ++x) {
         const int32_t u = su[x], i = si[x];
         const float r = sr[x];
-        float vec[KM], qi[KM], prod[KM];
-        const int32_t key = USERS ? i : u;  // the represented side
-        const double norm = iafm_user_vector<KM>(Y, k, ld, roff, ritems, key, lane, vec);
-        float* Vi = T + (int64_t)(USERS ? u : i) * ld;  // the trained row: U_u or V_i
+        // a = the user side, c = the item side of the score
+        float a[KM], c[KM], prod[KM];
+        double norm_u = 1.0, norm_i = 1.0;
+        float* trained = nullptr;  // kAsymItem: V_i, kAsymUser: U_u
+        if constexpr (MODE != kAsymUser) norm_u = asym_vector<KM>(s0, k, ld, u, lane, a);
+        if constexpr (MODE != kAsymItem) norm_i = asym_vector<KM>(s1, k, ld, i, lane, c);
+        if constexpr (MODE == kAsymItem) trained = V + (int64_t)i * ld;
+        if constexpr (MODE == kAsymUser) trained = U + (int64_t)u * ld;
 #pragma unroll
         for (int m = 0; m < KM; ++m) {
             const int f = lane + 64 * m;
-            qi[m] = f < k ? Vi[f] : 0.0f;
-            prod[m] = qi[m] * vec[m];
+            if constexpr (MODE == kAsymItem) c[m] = f < k ? trained[f] : 0.0f;
+            if constexpr (MODE == kAsymUser) a[m] = f < k ? trained[f] : 0.0f;
+            prod[m] = a[m] * c[m];
         }
-        // RowScalarProduct(i, IList<float>) (MatrixExtensions.cs:183-196): float, left to right
+        // kAsymItem / kAsymUser: RowScalarProduct(row, IList<float>) (MatrixExtensions.cs:183-196),
+        // float accumulation; kAsymCombined: VectorExtensions.ScalarProduct (VectorExtensions.cs:
+        // 30-38), double accumulation of the float products, cast to float
         float dot = 0.0f;
+        double dotd = 0.0;
 #pragma unroll
         for (int m = 0; m < KM; ++m) {
             const int lim = min(64, k - 64 * m);
             const int bits = __float_as_int(prod[m]);
-            for (int l = 0; l < lim; ++l) dot += __int_as_float(__builtin_amdgcn_readlane(bits, l));
+            for (int l = 0; l < lim; ++l) {
+                const float p = __int_as_float(__builtin_amdgcn_readlane(bits, l));
+                if constexpr (MODE == kAsymCombined) dotd += (double)p;
+                else dot += p;
+            }
         }
+        if constexpr (MODE == kAsymCombined) dot = (float)dotd;
         const float bu_u = bu[u], bi_i = bi[i];
-        // score = global_bias + user_bias + item_bias in float, then + dot in double (:103-109)
+        // score = global_bias + user_bias + item_bias in float, then + dot in double
         const double score = (double)((s.gb + bu_u) + bi_i) + (double)dot;
         const double sig = 1.0 / (1.0 + exp(-score));
         const double err = (double)r - ((double)s.min_rating + sig * (double)s.range);
         const float g = gradient_common<LOSS>(sig, err, s.range);
         float reg_u = s.reg_u, reg_i = s.reg_i;
-        if (cnt_u) {  // FrequencyRegularization (:115-116)
+        if (cnt_u) {  // FrequencyRegularization
             reg_u = (float)((double)s.reg_u / sqrt((double)cnt_u[u]));
             reg_i = (float)((double)s.reg_i / sqrt((double)cnt_i[i]));
         }
-        if (lane == 0) {  // :120-123
+        if (lane == 0) {
             bu[u] = bu_u + s.blr * (g - (s.bias_reg * reg_u) * bu_u);
             bi[i] = bi_i + s.blr * (g - (s.bias_reg * reg_i) * bi_i);
         }
-        const double ngc = (double)g / norm;  // normalized_gradient_common (:126)
-        double common[KM];
+        double cu[KM], ci[KM];  // common updates of the slot-0 and the slot-1 lists
 #pragma unroll
         for (int m = 0; m < KM; ++m) {
             const int f = lane + 64 * m;
-            const float i_f = qi[m];
-            // delta_i is a float expression widened to double; Inc adds (float)(lr * delta)
-            const double delta_i = (double)(g * vec[m] - (USERS ? reg_u : reg_i) * i_f);
-            if (f < k) Vi[f] = i_f + (float)((double)s.lr * delta_i);
-            common[m] = ngc * (double)i_f;
-        }
-        // y rows of every item the user rated (:137-142), list order per factor
-        const int64_t b = roff[key], e = roff[key + 1];
-        for (int64_t t = b; t < e; ++t) {
-            const int32_t j = ritems[t];
-            const float yr = y_reg[j];
-            float* row = Y + (int64_t)j * ld;
-#pragma unroll
-            for (int m = 0; m < KM; ++m) {
-                const int f = lane + 64 * m;
-                if (f < k) {
-                    const float y = row[f];
-                    row[f] = y + (float)((double)s.lr * (common[m] - (double)(yr * y)));
-                }
+            if constexpr (MODE == kAsymItem) {  // :127-143: V_i step, y's common from old i_f
+                const float i_f = c[m];
+                const double delta = (double)(g * a[m] - reg_i * i_f);  // float expression
+                if (f < k) trained[f] = i_f + (float)((double)s.lr * delta);
+                cu[m] = ((double)g / norm_u) * (double)i_f;
+            } else if constexpr (MODE == kAsymUser) {  // :127-142: U_u step, x's from old u_f
+                const float u_f = a[m];
+                const double delta = (double)(g * c[m] - reg_u * u_f);
+                if (f < k) trained[f] = u_f + (float)((double)s.lr * delta);
+                ci[m] = ((double)g / norm_i) * (double)u_f;
+            } else {  // :151-180: x from the user vector, y from the item vector
+                ci[m] = ((double)g / norm_i) * (double)a[m];
+                cu[m] = ((double)g / norm_u) * (double)c[m];
             }
         }
+        if constexpr (MODE != kAsymItem) asym_list_step<KM>(s1, k, ld, i, lane, s.lr, ci);
+        if constexpr (MODE != kAsymUser) asym_list_step<KM>(s0, k, ld, u, lane, s.lr, cu);
     }
 }
 
-// PrecomputeUserFactors (:305-331) / PrecomputeItemFactors (SigmoidUserAsymmetricFactorModel.cs:
-// 265-296): row r of U (or V) = the represented vector of r; rows with an empty list get zeros
+// PrecomputeUserFactors / PrecomputeItemFactors: row r of `out` = the represented vector of r;
+// rows with an empty list get zeros (the reference assigns a fresh zero matrix)
 template <int KM>
-__global__ __launch_bounds__(64) void iafm_user_factors_kernel(
-    const float* __restrict__ Y, int32_t k, int32_t ld, const int64_t* __restrict__ roff,
-    const int32_t* __restrict__ ritems, int32_t n_users, float* __restrict__ U) {
+__global__ __launch_bounds__(64) void asym_precompute_kernel(AsymSlot sl, int32_t k, int32_t ld,
+                                                             int32_t n_rows,
+                                                             float* __restrict__ out) {
     const int lane = threadIdx.x;
-    for (int32_t u = blockIdx.x; u < n_users; u += gridDim.x) {
+    for (int32_t r = blockIdx.x; r < n_rows; r += gridDim.x) {
         float vec[KM];
-        if (roff[u + 1] > roff[u]) {
-            iafm_user_vector<KM>(Y, k, ld, roff, ritems, u, lane, vec);
+        if (sl.off[r + 1] > sl.off[r]) {
+            asym_vector<KM>(sl, k, ld, r, lane, vec);
         } else {
 #pragma unroll
             for (int m = 0; m < KM; ++m) vec[m] = 0.0f;
@@ -958,7 +993,7 @@ __global__ __launch_bounds__(64) void iafm_user_factors_kernel(
 #pragma unroll
         for (int m = 0; m < KM; ++m) {
             const int f = lane + 64 * m;
-            if (f < k) U[(int64_t)u * ld + f] = vec[m];
+            if (f < k) out[(int64_t)r * ld + f] = vec[m];
         }
     }
 }
@@ -987,11 +1022,11 @@ struct mml_bmf {
     mml::DeviceArray<float> gerr, Ug, Vg, bug, big;
     int32_t n_conn = 0, n_rev = 0;
     bool has_positions = false;
-    // SigmoidItemAsymmetricFactorModel: items_rated_by_user (CSR), y, y_reg
-    mml::DeviceArray<int64_t> rated_off;
-    mml::DeviceArray<int32_t> rated_items;
-    mml::DeviceArray<float> Y, y_reg;
-    bool has_implicit = false;
+    // the asymmetric models' implicit-feedback slots (0: lists per user over y, 1: per item over x)
+    mml::DeviceArray<int64_t> asym_off[2];
+    mml::DeviceArray<int32_t> asym_ids[2];
+    mml::DeviceArray<float> asym_x[2], asym_reg[2];
+    bool has_slot[2] = {false, false};
 };
 
 namespace {
@@ -1228,65 +1263,85 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     MML_HIP(hipGetLastError());
 }
 
-// U (or V) <- PrecomputeUserFactors / PrecomputeItemFactors (what Predict and the evaluators read)
-void iafm_user_factors(mml_bmf* h) {
+bool is_asym(const mml_bmf* h) {
+    return h->p.model == MML_MF_ITEM_ASYM || h->p.model == MML_MF_USER_ASYM ||
+           h->p.model == MML_MF_COMBINED_ASYM;
+}
+int asym_mode(const mml_bmf* h) {
+    return h->p.model == MML_MF_ITEM_ASYM ? kAsymItem
+           : h->p.model == MML_MF_USER_ASYM ? kAsymUser
+                                            : kAsymCombined;
+}
+AsymSlot asym_slot(mml_bmf* h, int side) {
+    return AsymSlot{h->asym_x[side].get(), h->asym_off[side].get(), h->asym_ids[side].get(),
+                    h->asym_reg[side].get()};
+}
+bool asym_ready(const mml_bmf* h) {
+    const int mode = asym_mode(h);
+    return (mode == kAsymUser || h->has_slot[0]) && (mode == kAsymItem || h->has_slot[1]);
+}
+
+// U <- PrecomputeUserFactors (slot 0) and / or V <- PrecomputeItemFactors (slot 1): what Predict
+// and the evaluators read
+void asym_precompute(mml_bmf* h) {
     const int km = (h->k + 63) / 64;
-    const bool users = h->p.model == MML_MF_USER_ASYM;
-    const int32_t rows = users ? h->n_items : h->n_users;
-    if (rows == 0) return;
-    const int grid = std::max(1, std::min(rows, 65536));
+    const int mode = asym_mode(h);
     hipStream_t st = h->ctx->stream;
-#define MML_IUF(KM)                                                                            \
-    iafm_user_factors_kernel<KM><<<grid, 64, 0, st>>>(h->Y.get(), h->k, h->ld,                 \
-                                                      h->rated_off.get(), h->rated_items.get(), \
-                                                      rows, users ? h->V.get() : h->U.get())
-    switch (km) {
-        case 1: MML_IUF(1); break;
-        case 2: MML_IUF(2); break;
-        case 3: MML_IUF(3); break;
-        default: MML_IUF(4); break;
+    for (int side = 0; side < 2; ++side) {
+        if ((side == 0 && mode == kAsymUser) || (side == 1 && mode == kAsymItem)) continue;
+        const int32_t rows = side == 0 ? h->n_users : h->n_items;
+        if (rows == 0) continue;
+        const int grid = std::max(1, std::min(rows, 65536));
+        float* out = side == 0 ? h->U.get() : h->V.get();
+        const AsymSlot sl = asym_slot(h, side);
+#define MML_PRE(KM) asym_precompute_kernel<KM><<<grid, 64, 0, st>>>(sl, h->k, h->ld, rows, out)
+        switch (km) {
+            case 1: MML_PRE(1); break;
+            case 2: MML_PRE(2); break;
+            case 3: MML_PRE(3); break;
+            default: MML_PRE(4); break;
+        }
+#undef MML_PRE
+        MML_HIP(hipGetLastError());
     }
-#undef MML_IUF
-    MML_HIP(hipGetLastError());
 }
 
 template <int LOSS>
-void iafm_epoch(mml_bmf* h, const BmfScalars& s) {
+void asym_epoch(mml_bmf* h, const BmfScalars& s) {
     const int32_t* cu = h->p.frequency_regularization ? h->cnt_u.get() : nullptr;
     const int32_t* ci = h->p.frequency_regularization ? h->cnt_i.get() : nullptr;
     const int64_t n = h->n;
     hipStream_t st = h->ctx->stream;
     if (n > 0) {
         // ORDERED: one wavefront, the whole stream in order.  HOGWILD: a wavefront per >= 2,048
-        // ratings (a rating reads and writes all |items(u)| y rows), at most 256 CUs x 8
+        // ratings (a rating reads and writes whole lists of implicit rows), at most 256 CUs x 8
         int64_t waves = 1;
         if (h->p.schedule != MML_SCHEDULE_ORDERED)
             waves = std::min<int64_t>(256 * 8, std::max<int64_t>(1, n / 2048));
         const int64_t chunk = (n + waves - 1) / waves;
         const int km = (h->k + 63) / 64;
-        const bool users = h->p.model == MML_MF_USER_ASYM;
-#define MML_IAFM(KM, USERS)                                                                    \
-    iafm_sgd_kernel<LOSS, KM, USERS><<<(int)waves, 64, 0, st>>>(                               \
-        h->su.get(), h->si.get(), h->sr.get(), n, chunk, h->Y.get(),                           \
-        USERS ? h->U.get() : h->V.get(), h->bu.get(), h->bi.get(), h->k, h->ld, s, cu, ci,     \
-        h->rated_off.get(), h->rated_items.get(), h->y_reg.get())
-#define MML_IAFM_K(USERS)                    \
-    switch (km) {                            \
-        case 1: MML_IAFM(1, USERS); break;   \
-        case 2: MML_IAFM(2, USERS); break;   \
-        case 3: MML_IAFM(3, USERS); break;   \
-        default: MML_IAFM(4, USERS); break;  \
+        const AsymSlot s0 = asym_slot(h, 0), s1 = asym_slot(h, 1);
+#define MML_ASYM(KM, MODE)                                                                     \
+    asym_sgd_kernel<LOSS, KM, MODE><<<(int)waves, 64, 0, st>>>(                                \
+        h->su.get(), h->si.get(), h->sr.get(), n, chunk, s0, s1, h->U.get(), h->V.get(),       \
+        h->bu.get(), h->bi.get(), h->k, h->ld, s, cu, ci)
+#define MML_ASYM_K(MODE)                    \
+    switch (km) {                           \
+        case 1: MML_ASYM(1, MODE); break;   \
+        case 2: MML_ASYM(2, MODE); break;   \
+        case 3: MML_ASYM(3, MODE); break;   \
+        default: MML_ASYM(4, MODE); break;  \
     }
-        if (users) {
-            MML_IAFM_K(true);
-        } else {
-            MML_IAFM_K(false);
+        switch (asym_mode(h)) {
+            case kAsymItem: MML_ASYM_K(kAsymItem); break;
+            case kAsymUser: MML_ASYM_K(kAsymUser); break;
+            default: MML_ASYM_K(kAsymCombined); break;
         }
-#undef MML_IAFM_K
-#undef MML_IAFM
+#undef MML_ASYM_K
+#undef MML_ASYM
         MML_HIP(hipGetLastError());
     }
-    iafm_user_factors(h);
+    asym_precompute(h);
     h->last_launches = 1;
 }
 
@@ -1331,7 +1386,7 @@ extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params,
                     "num_factors must be in [1, 256]");
         MML_REQUIRE(params->loss >= MML_LOSS_RMSE && params->loss <= MML_LOSS_LOGISTIC,
                     "unknown loss");
-        MML_REQUIRE(params->model >= MML_MF_BIASED && params->model <= MML_MF_USER_ASYM,
+        MML_REQUIRE(params->model >= MML_MF_BIASED && params->model <= MML_MF_COMBINED_ASYM,
                     "unknown model family");
         MML_REQUIRE(params->schedule >= MML_SCHEDULE_ORDERED &&
                         params->schedule <= MML_SCHEDULE_HOGWILD_COHERENT,
@@ -1516,9 +1571,10 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
     return guard([&] {
         check_handle(h);
         MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
-        const bool asym = h->p.model == MML_MF_ITEM_ASYM || h->p.model == MML_MF_USER_ASYM;
+        const bool asym = is_asym(h);
         if (asym) {
-            MML_REQUIRE(h->has_implicit, "set_implicit_feedback must precede iterate");
+            MML_REQUIRE(asym_ready(h), "set_implicit_feedback (each side the model uses) must "
+                                       "precede iterate");
             MML_REQUIRE(h->p.schedule == MML_SCHEDULE_ORDERED ||
                             h->p.schedule == MML_SCHEDULE_HOGWILD,
                         "the asymmetric models run the ORDERED or HOGWILD schedule");
@@ -1544,9 +1600,9 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
         if (asym) {
             switch (h->p.loss) {
-                case MML_LOSS_MAE: iafm_epoch<MML_LOSS_MAE>(h, s); break;
-                case MML_LOSS_LOGISTIC: iafm_epoch<MML_LOSS_LOGISTIC>(h, s); break;
-                default: iafm_epoch<MML_LOSS_RMSE>(h, s); break;
+                case MML_LOSS_MAE: asym_epoch<MML_LOSS_MAE>(h, s); break;
+                case MML_LOSS_LOGISTIC: asym_epoch<MML_LOSS_LOGISTIC>(h, s); break;
+                default: asym_epoch<MML_LOSS_RMSE>(h, s); break;
             }
         } else if (h->p.model == MML_MF_SOCIAL) {
             switch (h->p.loss) {
@@ -1682,8 +1738,7 @@ extern "C" mml_status mml_bmf_allreduce_items(mml_bmf* h) {
         mml_ctx* c = h->ctx;
         if (c->nranks <= 1) return;
         MML_REQUIRE(c->comm, "context has no communicator (mml_ctx_comm_init)");
-        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM && h->p.model != MML_MF_USER_ASYM,
-                    "the asymmetric models' implicit factors are not averaged across ranks");
+        MML_REQUIRE(!is_asym(h), "the asymmetric models' implicit factors are not averaged across ranks");
         c->activate();
         hipStream_t st = c->stream;
         const size_t nv = (size_t)h->n_items * h->ld;
@@ -1728,8 +1783,7 @@ extern "C" mml_status mml_bmf_fold_in(mml_bmf* h, int32_t n_fold, const int64_t*
     return guard([&] {
         check_handle(h);
         MML_REQUIRE(h->has_model, "no model");
-        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM && h->p.model != MML_MF_USER_ASYM,
-                    "the asymmetric models have their own FoldIn (not on the GPU path)");
+        MML_REQUIRE(!is_asym(h), "the asymmetric models have their own FoldIn (not on the GPU path)");
         MML_REQUIRE(n_fold >= 0 && num_iter >= 0, "negative sizes");
         if (n_fold == 0) return;
         MML_REQUIRE(rated_off && init_factors && out_vectors, "null arguments");
@@ -1794,8 +1848,7 @@ extern "C" mml_status mml_bmf_predict_vectors(mml_bmf* h, int32_t n_vectors, con
     return guard([&] {
         check_handle(h);
         MML_REQUIRE(h->has_model, "no model");
-        MML_REQUIRE(h->p.model != MML_MF_ITEM_ASYM && h->p.model != MML_MF_USER_ASYM,
-                    "the asymmetric models have their own FoldIn (not on the GPU path)");
+        MML_REQUIRE(!is_asym(h), "the asymmetric models have their own FoldIn (not on the GPU path)");
         MML_REQUIRE(n_vectors >= 0 && n >= 0, "negative sizes");
         if (n == 0) return;
         MML_REQUIRE(vectors && vector_index && items && out, "null arguments");
@@ -1878,57 +1931,59 @@ extern "C" mml_status mml_bmf_set_user_relation(mml_bmf* h, int32_t n_rows, cons
     });
 }
 
-extern "C" mml_status mml_bmf_set_implicit_feedback(mml_bmf* h, int32_t n_rows, const int64_t* offsets,
-                                                const int32_t* items, const float* y,
-                                                const float* y_reg) {
+extern "C" mml_status mml_bmf_set_implicit_feedback(mml_bmf* h, int32_t side, int32_t n_rows,
+                                                    const int64_t* offsets, const int32_t* ids,
+                                                    const float* factors, const float* reg) {
     return guard([&] {
         check_handle(h);
-        const bool users = h->p.model == MML_MF_USER_ASYM;
-        MML_REQUIRE(h->p.model == MML_MF_ITEM_ASYM || users,
-                    "implicit feedback belongs to the asymmetric models' handles");
-        // ITEM_ASYM: a row of rated items per user, y [n_items x k]; USER_ASYM: a row of users
-        // per item, x [n_users x k]
-        const int32_t n_list = users ? h->n_items : h->n_users;
-        const int32_t n_x = users ? h->n_users : h->n_items;
-        MML_REQUIRE(n_rows == n_list, "one list per user (ITEM_ASYM) / per item (USER_ASYM)");
-        MML_REQUIRE(offsets && y && y_reg, "null argument");
+        MML_REQUIRE(is_asym(h), "implicit feedback belongs to the asymmetric models' handles");
+        MML_REQUIRE(side == 0 || side == 1, "side must be 0 (lists per user) or 1 (per item)");
+        const int mode = asym_mode(h);
+        MML_REQUIRE(!(side == 0 && mode == kAsymUser) && !(side == 1 && mode == kAsymItem),
+                    "this model does not use that side");
+        // side 0: a list of items per user, factors y [n_items x k]; side 1: a list of users per
+        // item, factors x [n_users x k]
+        const int32_t n_list = side == 0 ? h->n_users : h->n_items;
+        const int32_t n_x = side == 0 ? h->n_items : h->n_users;
+        MML_REQUIRE(n_rows == n_list, "one list per user (side 0) / per item (side 1)");
+        MML_REQUIRE(offsets && factors && reg, "null argument");
         MML_REQUIRE(offsets[0] == 0, "offsets[0] must be 0");
-        for (int32_t u = 0; u < n_rows; ++u)
-            MML_REQUIRE(offsets[u + 1] >= offsets[u], "offsets must not decrease");
+        for (int32_t r = 0; r < n_rows; ++r)
+            MML_REQUIRE(offsets[r + 1] >= offsets[r], "offsets must not decrease");
         const int64_t nnz = offsets[n_rows];
-        MML_REQUIRE(nnz == 0 || items, "null items");
+        MML_REQUIRE(nnz == 0 || ids, "null ids");
         for (int64_t x = 0; x < nnz; ++x)
-            MML_REQUIRE(items[x] >= 0 && items[x] < n_x, "list id out of range");
+            MML_REQUIRE(ids[x] >= 0 && ids[x] < n_x, "list id out of range");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
-        h->has_implicit = false;
-        h->rated_off.alloc((size_t)n_rows + 1);
-        h->rated_items.alloc((size_t)std::max<int64_t>(1, nnz));
-        h->Y.alloc((size_t)std::max<int64_t>(1, (int64_t)n_x * h->ld));
-        h->y_reg.alloc((size_t)std::max(1, n_x));
-        MML_HIP(hipMemcpyAsync(h->rated_off.get(), offsets, sizeof(int64_t) * (n_rows + 1),
+        h->has_slot[side] = false;
+        h->asym_off[side].alloc((size_t)n_rows + 1);
+        h->asym_ids[side].alloc((size_t)std::max<int64_t>(1, nnz));
+        h->asym_x[side].alloc((size_t)std::max<int64_t>(1, (int64_t)n_x * h->ld));
+        h->asym_reg[side].alloc((size_t)std::max(1, n_x));
+        MML_HIP(hipMemcpyAsync(h->asym_off[side].get(), offsets, sizeof(int64_t) * (n_rows + 1),
                                hipMemcpyHostToDevice, st));
         if (nnz)
-            MML_HIP(hipMemcpyAsync(h->rated_items.get(), items, sizeof(int32_t) * nnz,
+            MML_HIP(hipMemcpyAsync(h->asym_ids[side].get(), ids, sizeof(int32_t) * nnz,
                                    hipMemcpyHostToDevice, st));
-        upload_padded(h, h->Y.get(), y, n_x);
+        upload_padded(h, h->asym_x[side].get(), factors, n_x);
         if (n_x)
-            MML_HIP(hipMemcpyAsync(h->y_reg.get(), y_reg, sizeof(float) * n_x,
+            MML_HIP(hipMemcpyAsync(h->asym_reg[side].get(), reg, sizeof(float) * n_x,
                                    hipMemcpyHostToDevice, st));
-        iafm_user_factors(h);
+        h->has_slot[side] = true;
+        if (asym_ready(h)) asym_precompute(h);
         MML_HIP(hipStreamSynchronize(st));
-        h->has_implicit = true;
     });
 }
 
-extern "C" mml_status mml_bmf_get_implicit_factors(mml_bmf* h, float* y) {
+extern "C" mml_status mml_bmf_get_implicit_factors(mml_bmf* h, int32_t side, float* factors) {
     return guard([&] {
         check_handle(h);
-        MML_REQUIRE(h->has_implicit, "no implicit factors (set_implicit_feedback first)");
-        MML_REQUIRE(y, "null argument");
+        MML_REQUIRE(side == 0 || side == 1, "side must be 0 or 1");
+        MML_REQUIRE(h->has_slot[side], "no implicit factors on that side");
+        MML_REQUIRE(factors, "null argument");
         h->ctx->activate();
-        download_padded(h, y, h->Y.get(),
-                        h->p.model == MML_MF_USER_ASYM ? h->n_users : h->n_items);
+        download_padded(h, factors, h->asym_x[side].get(), side == 0 ? h->n_items : h->n_users);
         MML_HIP(hipStreamSynchronize(h->ctx->stream));
     });
 }

@@ -667,17 +667,18 @@ class SocialMF(BiasedMatrixFactorization):
 
 class _AsymmetricFactorModel(BiasedMatrixFactorization):
     """The Sigmoid*AsymmetricFactorModels (ITransductiveRatingPredictor): a BiasedMatrixFactorization
-    in which one side is represented by implicit factors summed over its feedback list (training
-    and ``additional_feedback``) / sqrt(count).  ``ordered`` (default) is the reference's sequential
-    loop bit for bit; ``hogwild`` runs many wavefronts.  BoldDriver (their own ComputeObjective),
-    MaxThreads > 1 and FoldIn are not on the GPU path."""
+    in which users and / or items are represented by implicit factors summed over their feedback
+    lists (training and ``additional_feedback``) / sqrt(count).  Side 0 = y over the items each
+    user rated, side 1 = x over the users who rated each item.  ``ordered`` (default) is the
+    reference's sequential loop bit for bit; ``hogwild`` runs many wavefronts.  BoldDriver (their
+    own ComputeObjective), MaxThreads > 1 and FoldIn are not on the GPU path."""
     PROPERTIES = dict(BiasedMatrixFactorization.PROPERTIES)
-    USER_SIDE = False  # False: y per item, lists per user; True: x per user, lists per item
+    SIDES = ()          # the implicit sides the model uses
+    INIT_FIRST = True   # InitModel draws the implicit factors before (True) or after U, V
 
     def __init__(self, **kw):
         super().__init__()
-        # the models' constructors (SigmoidItemAsymmetricFactorModel.cs:56-63,
-        # SigmoidUserAsymmetricFactorModel.cs:56-63)
+        # the models' constructors (e.g. SigmoidItemAsymmetricFactorModel.cs:56-63)
         self.Regularization = 0.015
         self.LearnRate = 0.001
         self.BiasLearnRate = 0.7
@@ -692,20 +693,22 @@ class _AsymmetricFactorModel(BiasedMatrixFactorization):
             raise ValueError(f"unknown Schedule '{self.Schedule}' for {type(self).__name__}")
         return s
 
-    def _feedback_lists(self):
-        """ItemsRatedByUser / UsersWhoRated (ITransductiveRatingPredictor.cs:40-79): per key the
-        training partners in rating-index order (ByUser / ByItem), then AdditionalFeedback's,
-        distinct (Union) -- as CSR."""
+    def _pairs(self):
         r, a = self._ratings, self.additional_feedback
         us, its = [N.i32(r.users)], [N.i32(r.items)]
         if a is not None and len(a.users):
             us.append(N.i32(a.users))
             its.append(N.i32(a.items))
-        u = np.concatenate(us).astype(np.int64)
-        i = np.concatenate(its).astype(np.int64)
-        keys, vals = (i, u) if self.USER_SIDE else (u, i)
-        n_keys = self.MaxItemID + 1 if self.USER_SIDE else self.MaxUserID + 1
-        n_vals = self.MaxUserID + 1 if self.USER_SIDE else self.MaxItemID + 1
+        return np.concatenate(us).astype(np.int64), np.concatenate(its).astype(np.int64)
+
+    def _feedback_lists(self, side=0):
+        """ItemsRatedByUser (side 0) / UsersWhoRated (side 1) (ITransductiveRatingPredictor.cs:
+        40-79): per key the training partners in rating-index order (ByUser / ByItem), then
+        AdditionalFeedback's, distinct (Union) -- as CSR."""
+        u, i = self._pairs()
+        keys, vals = (i, u) if side else (u, i)
+        n_keys = self.MaxItemID + 1 if side else self.MaxUserID + 1
+        n_vals = self.MaxUserID + 1 if side else self.MaxItemID + 1
         seq = np.arange(len(keys))
         _, first = np.unique(keys * n_vals + vals, return_index=True)  # first appearance
         first = first[np.lexsort((seq[first], keys[first]))]  # by key, then appearance
@@ -713,10 +716,31 @@ class _AsymmetricFactorModel(BiasedMatrixFactorization):
         np.cumsum(np.bincount(keys[first], minlength=n_keys), out=off[1:])
         return off, N.i32(vals[first])
 
+    def _implicit_init(self, side):
+        """x (side 1) / y (side 0): N(InitMean, InitStdDev), rows without training ratings zeroed
+        (e.g. SigmoidItemAsymmetricFactorModel.cs:290-301), and x_reg / y_reg (Train :66-80)."""
+        r, a = self._ratings, self.additional_feedback
+        k = int(self.NumFactors)
+        n_x = self.MaxUserID + 1 if side else self.MaxItemID + 1
+        fb = np.bincount(N.i32(r.users if side else r.items), minlength=n_x)  # *FeedbackCounts
+        if a is not None and len(a.users):
+            fb = fb + np.bincount(N.i32(a.users if side else a.items), minlength=n_x)
+        reg = float(np.float32(self.RegU if side else self.RegI))
+        x_reg = np.zeros(n_x, np.float32)
+        nz = fb > 0
+        x_reg[nz] = (np.float32(reg / np.sqrt(fb[nz].astype(np.float64)))
+                     if self.FrequencyRegularization else np.float32(reg))
+        x = Random.get_instance().fill_normal(n_x * k, self.InitMean,
+                                              self.InitStdDev).reshape(n_x, k)
+        cnt = r.count_by_user if side else r.count_by_item
+        trained = np.zeros(n_x, bool)
+        trained[:len(cnt)] = cnt > 0
+        x[~trained] = 0.0
+        return x, x_reg
+
     def init_model(self):
-        """Train (sizes and the implicit factors' regularisation, :66-80), then InitModel: the
-        implicit factors (rows without training ratings zeroed), then BiasedMatrixFactorization's
-        InitModel (U, V, biases)."""
+        """Train (sizes, :66-80), then InitModel: the implicit factors before (item / user
+        models) or after (combined model) BiasedMatrixFactorization's InitModel (U, V, biases)."""
         name = type(self).__name__
         if self.BoldDriver:
             raise NotImplementedError(f"{name} with BoldDriver (its own ComputeObjective) is not "
@@ -727,33 +751,26 @@ class _AsymmetricFactorModel(BiasedMatrixFactorization):
         if a is not None and len(a.users):
             self.MaxUserID = max(r.max_user_id, int(np.max(a.users)))
             self.MaxItemID = max(r.max_item_id, int(np.max(a.items)))
-        k = int(self.NumFactors)
-        side = N.i32(r.users) if self.USER_SIDE else N.i32(r.items)
-        n_x = self.MaxUserID + 1 if self.USER_SIDE else self.MaxItemID + 1
-        fb = np.bincount(side, minlength=n_x)  # UserFeedbackCounts / ItemFeedbackCounts
-        if a is not None and len(a.users):
-            fb = fb + np.bincount(N.i32(a.users if self.USER_SIDE else a.items), minlength=n_x)
-        reg = float(np.float32(self.RegU if self.USER_SIDE else self.RegI))
-        x_reg = np.zeros(n_x, np.float32)
-        nz = fb > 0
-        x_reg[nz] = (np.float32(reg / np.sqrt(fb[nz].astype(np.float64)))
-                     if self.FrequencyRegularization else np.float32(reg))
-        rng = Random.get_instance()
-        x = rng.fill_normal(n_x * k, self.InitMean, self.InitStdDev).reshape(n_x, k)
-        cnt = r.count_by_user if self.USER_SIDE else r.count_by_item
-        trained = np.zeros(n_x, bool)
-        trained[:len(cnt)] = cnt > 0
-        x[~trained] = 0.0
+        implicit = {}
+        if self.INIT_FIRST:
+            for side in self.SIDES:
+                implicit[side] = self._implicit_init(side)
         super().init_model()
-        off, ids = self._feedback_lists()
-        N.check(N.lib().mml_bmf_set_implicit_feedback(
-            self._h, len(off) - 1, N.ptr(off, N._i64p), N.ptr(ids, N._i32p),
-            N.ptr(N.f32(x), N._f32p), N.ptr(x_reg, N._f32p)))
+        if not self.INIT_FIRST:
+            for side in self.SIDES:
+                implicit[side] = self._implicit_init(side)
+        for side in self.SIDES:
+            off, ids = self._feedback_lists(side)
+            x, x_reg = implicit[side]
+            N.check(N.lib().mml_bmf_set_implicit_feedback(
+                self._h, side, len(off) - 1, N.ptr(off, N._i64p), N.ptr(ids, N._i32p),
+                N.ptr(N.f32(x), N._f32p), N.ptr(x_reg, N._f32p)))
 
-    def _implicit_factors(self):
-        n_x = self.MaxUserID + 1 if self.USER_SIDE else self.MaxItemID + 1
+    def _implicit_factors(self, side=None):
+        side = self.SIDES[0] if side is None else side
+        n_x = self.MaxUserID + 1 if side else self.MaxItemID + 1
         out = np.empty((n_x, int(self.NumFactors)), np.float32)
-        N.check(N.lib().mml_bmf_get_implicit_factors(self._h, N.ptr(out, N._f32p)))
+        N.check(N.lib().mml_bmf_get_implicit_factors(self._h, side, N.ptr(out, N._f32p)))
         return out
 
     def load_model(self, path: str):
@@ -768,12 +785,12 @@ class SigmoidItemAsymmetricFactorModel(_AsymmetricFactorModel):
     user's items (Iterate :91-147, MML_MF_ITEM_ASYM).  user_factors = PrecomputeUserFactors."""
     MODEL = N.MF_ITEM_ASYM
     TYPE_NAME = "MyMediaLite.RatingPrediction.SigmoidItemAsymmetricFactorModel"
-    USER_SIDE = False
+    SIDES = (0,)
 
     @property
     def y(self):
         """y [n_items x k], the item factors that express the users (:49-50)."""
-        return self._implicit_factors()
+        return self._implicit_factors(0)
 
     def save_model(self, path: str):
         """SaveModel (:150-162): global bias, min/max rating, user biases, item biases, y, item
@@ -807,12 +824,12 @@ class SigmoidUserAsymmetricFactorModel(_AsymmetricFactorModel):
     the item's users (Iterate :91-144, MML_MF_USER_ASYM).  item_factors = PrecomputeItemFactors."""
     MODEL = N.MF_USER_ASYM
     TYPE_NAME = "MyMediaLite.RatingPrediction.SigmoidUserAsymmetricFactorModel"
-    USER_SIDE = True
+    SIDES = (1,)
 
     @property
     def x(self):
         """x [n_users x k], the user factors that express the items (:49-50)."""
-        return self._implicit_factors()
+        return self._implicit_factors(1)
 
     def save_model(self, path: str):
         """SaveModel (:147-159): global bias, min/max rating, user biases, item biases, x, user
@@ -831,6 +848,48 @@ class SigmoidUserAsymmetricFactorModel(_AsymmetricFactorModel):
     def __str__(self):
         """ToString() (:298-305)."""
         return ("SigmoidUserAsymmetricFactorModel num_factors={} regularization={} bias_reg={} "
+                "frequency_regularization={} learn_rate={} bias_learn_rate={} "
+                "learn_rate_decay={} num_iter={} loss={}").format(
+            self.NumFactors, _g(self.Regularization), _g(self.BiasReg),
+            self.FrequencyRegularization, _g(self.LearnRate), _g(self.BiasLearnRate),
+            _g(self.Decay), self.NumIter, self.Loss)
+
+
+class SigmoidCombinedAsymmetricFactorModel(_AsymmetricFactorModel):
+    """GPU-backed MyMediaLite.RatingPrediction.SigmoidCombinedAsymmetricFactorModel
+    (SigmoidCombinedAsymmetricFactorModel.cs:46-382): users from y over their items, items from x
+    over their users, score = ScalarProduct of the two; every rating updates the x rows of the
+    item's users and the y rows of the user's items (Iterate :108-182, MML_MF_COMBINED_ASYM).
+    InitModel draws U, V, then x, then y (:291-306); both factor matrices are precomputed."""
+    MODEL = N.MF_COMBINED_ASYM
+    TYPE_NAME = "MyMediaLite.RatingPrediction.SigmoidCombinedAsymmetricFactorModel"
+    SIDES = (1, 0)
+    INIT_FIRST = False
+
+    @property
+    def x(self):
+        return self._implicit_factors(1)
+
+    @property
+    def y(self):
+        return self._implicit_factors(0)
+
+    def save_model(self, path: str):
+        """SaveModel (:185-197): global bias, min/max rating, user biases, item biases, x, y."""
+        from .model_io import ModelWriter
+        m = self.get_model()
+        with ModelWriter(path, self.TYPE_NAME, "3.00") as w:
+            w.write_float(self.global_bias)
+            w.write_float(self.min_rating)
+            w.write_float(self.max_rating)
+            w.write_vector(m["bu"])
+            w.write_vector(m["bi"])
+            w.write_matrix(self.x)
+            w.write_matrix(self.y)
+
+    def __str__(self):
+        """ToString() (:373-379)."""
+        return ("SigmoidCombinedAsymmetricFactorModel num_factors={} regularization={} bias_reg={} "
                 "frequency_regularization={} learn_rate={} bias_learn_rate={} "
                 "learn_rate_decay={} num_iter={} loss={}").format(
             self.NumFactors, _g(self.Regularization), _g(self.BiasReg),

@@ -222,32 +222,49 @@ static void ora_iafm_user_vector(const float* Y, int k, const int64_t* rated_off
     for (int f = 0; f < k; f++) vec[f] = (float)((double)vec[f] / *norm);
 }
 
-/* SigmoidItemAsymmetricFactorModel.Iterate(IList<int>,bool,bool)
- * (RatingPrediction/SigmoidItemAsymmetricFactorModel.cs:91-147).  rated_off / rated_items: the
- * items_rated_by_user CSR (ITransductiveRatingPredictor.ItemsRatedByUser, :63-79: training items
- * in rating-index order, then AdditionalFeedback's, distinct); y_reg per item (Train :72-77).
- * user_side = 1: SigmoidUserAsymmetricFactorModel.Iterate (SigmoidUserAsymmetricFactorModel.cs:
- * 91-144), the mirror -- Y = x, the lists = UsersWhoRated per item (:40-55), V = the user factors
- * U it trains, y_reg = x_reg per user.  vec: k floats of scratch. */
-void ora_iafm_iterate(const ora_bmf_params* p, const int32_t* users, const int32_t* items,
-                      const float* values, const int32_t* idx, int64_t n_idx, float* Y, float* V,
+/* The asymmetric models' Iterate(IList<int>,bool,bool).  Slot 0: per user the items rated
+ * (ITransductiveRatingPredictor.ItemsRatedByUser, :63-79: training items in rating-index order,
+ * then AdditionalFeedback's, distinct) over Y = y [n_items x k] with y_reg; slot 1: per item the
+ * users who rated it (UsersWhoRated, :40-55) over X = x [n_users x k] with x_reg.
+ *   mode 0 SigmoidItemAsymmetricFactorModel (SigmoidItemAsymmetricFactorModel.cs:91-147):
+ *          user vector from y; trains V_i (RowScalarProduct, float) and y
+ *   mode 1 SigmoidUserAsymmetricFactorModel (SigmoidUserAsymmetricFactorModel.cs:91-144):
+ *          item vector from x; trains U_u and x
+ *   mode 2 SigmoidCombinedAsymmetricFactorModel (SigmoidCombinedAsymmetricFactorModel.cs:
+ *          108-182): both vectors; VectorExtensions.ScalarProduct (double sum, VectorExtensions.cs:
+ *          30-38); trains x (from the user vector) and y (from the item vector)
+ * vu, vi: k floats of scratch each. */
+void ora_asym_iterate(const ora_bmf_params* p, const int32_t* users, const int32_t* items,
+                      const float* values, const int32_t* idx, int64_t n_idx, float* U, float* V,
                       float* bu, float* bi, const int32_t* count_by_user,
-                      const int32_t* count_by_item, const int64_t* rated_off,
-                      const int32_t* rated_items, const float* y_reg, float* vec,
-                      int32_t user_side) {
+                      const int32_t* count_by_item, float* Y, const int64_t* off_u,
+                      const int32_t* ids_u, const float* y_reg, float* X, const int64_t* off_i,
+                      const int32_t* ids_i, const float* x_reg, float* vu, float* vi,
+                      int32_t mode) {
     const int k = p->k;
     const float lr = p->learn_rate;
     for (int64_t n = 0; n < n_idx; n++) {
         const int32_t index = idx[n];
         const int32_t u = users[index], i = items[index];
-        const int32_t key = user_side ? i : u;
-        float* Vi = V + (int64_t)(user_side ? u : i) * k;
-        double norm;
-        ora_iafm_user_vector(Y, k, rated_off, rated_items, key, vec, &norm);
-        double score = (double)((p->global_bias + bu[u]) + bi[i]); /* float sum, :103 */
-        float dot = 0.0f; /* RowScalarProduct(i, IList<float>) :183-196, float acc */
-        for (int f = 0; f < k; f++) dot += Vi[f] * vec[f];
-        score += (double)dot;
+        double norm_u = 1.0, norm_i = 1.0;
+        if (mode != 1) ora_iafm_user_vector(Y, k, off_u, ids_u, u, vu, &norm_u);
+        if (mode != 0) ora_iafm_user_vector(X, k, off_i, ids_i, i, vi, &norm_i);
+        float* Ui = U + (int64_t)u * k;
+        float* Vi = V + (int64_t)i * k;
+        double score = (double)((p->global_bias + bu[u]) + bi[i]); /* float sum */
+        if (mode == 0) {        /* item_factors.RowScalarProduct(i, u_plus_y_sum_vector) */
+            float dot = 0.0f;
+            for (int f = 0; f < k; f++) dot += Vi[f] * vu[f];
+            score += (double)dot;
+        } else if (mode == 1) { /* user_factors.RowScalarProduct(u, x_sum) */
+            float dot = 0.0f;
+            for (int f = 0; f < k; f++) dot += Ui[f] * vi[f];
+            score += (double)dot;
+        } else {                /* ScalarProduct(y_sum, x_sum) */
+            double dot = 0.0;
+            for (int f = 0; f < k; f++) dot += (double)(vu[f] * vi[f]);
+            score += (double)(float)dot;
+        }
         const double sig = 1.0 / (1.0 + exp(-score));
         const double prediction = (double)p->min_rating + sig * (double)p->rating_range_size;
         const double err = (double)values[index] - prediction;
@@ -268,19 +285,44 @@ void ora_iafm_iterate(const ora_bmf_params* p, const int32_t* users, const int32
         const float blr = p->bias_learn_rate * lr;
         if (p->update_user) bu[u] += blr * (g - (p->bias_reg * reg_u) * bu[u]);
         if (p->update_item) bi[i] += blr * (g - (p->bias_reg * reg_i) * bi[i]);
-        const double ngc = (double)g / norm; /* normalized_gradient_common :126 */
-        const int64_t b = rated_off[key], e = rated_off[key + 1];
+        const double ngc_u = (double)g / norm_u, ngc_i = (double)g / norm_i;
         for (int f = 0; f < k; f++) {
-            const float i_f = Vi[f];
-            if (!(user_side ? p->update_user : p->update_item)) continue;
-            const double delta_i = (double)(g * vec[f] - (user_side ? reg_u : reg_i) * i_f);
-            Vi[f] += (float)((double)lr * delta_i);
-            const double common = ngc * (double)i_f;
-            for (int64_t t = b; t < e; t++) {
-                const int32_t j = rated_items[t];
-                float* yj = Y + (int64_t)j * k + f;
-                const double delta_oi = common - (double)(y_reg[j] * *yj);
-                *yj += (float)((double)lr * delta_oi);
+            if (mode == 0) {
+                const float i_f = Vi[f];
+                if (!p->update_item) continue;
+                const double delta_i = (double)(g * vu[f] - reg_i * i_f); /* float expression */
+                Vi[f] += (float)((double)lr * delta_i);
+                const double common = ngc_u * (double)i_f;
+                for (int64_t t = off_u[u]; t < off_u[u + 1]; t++) {
+                    float* yj = Y + (int64_t)ids_u[t] * k + f;
+                    *yj += (float)((double)lr * (common - (double)(y_reg[ids_u[t]] * *yj)));
+                }
+            } else if (mode == 1) {
+                const float u_f = Ui[f];
+                if (!p->update_user) continue;
+                const double delta_u = (double)(g * vi[f] - reg_u * u_f);
+                Ui[f] += (float)((double)lr * delta_u);
+                const double common = ngc_i * (double)u_f;
+                for (int64_t t = off_i[i]; t < off_i[i + 1]; t++) {
+                    float* xo = X + (int64_t)ids_i[t] * k + f;
+                    *xo += (float)((double)lr * (common - (double)(x_reg[ids_i[t]] * *xo)));
+                }
+            } else {
+                const float u_f = vu[f], i_f = vi[f];
+                if (p->update_user) {
+                    const double common = ngc_i * (double)u_f;
+                    for (int64_t t = off_i[i]; t < off_i[i + 1]; t++) {
+                        float* xo = X + (int64_t)ids_i[t] * k + f;
+                        *xo += (float)((double)lr * (common - (double)(x_reg[ids_i[t]] * *xo)));
+                    }
+                }
+                if (p->update_item) {
+                    const double common = ngc_u * (double)i_f;
+                    for (int64_t t = off_u[u]; t < off_u[u + 1]; t++) {
+                        float* yj = Y + (int64_t)ids_u[t] * k + f;
+                        *yj += (float)((double)lr * (common - (double)(y_reg[ids_u[t]] * *yj)));
+                    }
+                }
             }
         }
     }

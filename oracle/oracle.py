@@ -111,9 +111,10 @@ def lib():
                                    ctypes.c_int64]
         L.ora_bpr_epoch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _i64p, _i32p, _i32p,
                                     ctypes.c_int64, _f32p, _f32p, _f32p, _i32p]
-        L.ora_iafm_iterate.argtypes = [
+        L.ora_asym_iterate.argtypes = [
             ctypes.c_void_p, _i32p, _i32p, _f32p, _i32p, ctypes.c_int64, _f32p, _f32p, _f32p,
-            _f32p, _i32p, _i32p, _i64p, _i32p, _f32p, _f32p, ctypes.c_int32]
+            _f32p, _i32p, _i32p, _f32p, _i64p, _i32p, _f32p, _f32p, _i64p, _i32p, _f32p, _f32p,
+            _f32p, ctypes.c_int32]
         L.ora_iafm_user_factors.argtypes = [_f32p, ctypes.c_int, ctypes.c_int32, _i64p, _i32p,
                                             _f32p]
         L.ora_wrmf_square.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f64p]
@@ -429,40 +430,62 @@ def asym_train(users, items, values, n_users, n_items, min_rating, max_rating, *
                seed=1, k=10, learn_rate=0.001, decay=1.0, reg_u=0.015, reg_i=0.015, bias_reg=0.33,
                bias_learn_rate=0.7, num_iter=30, init_mean=0.0, init_stddev=0.1, loss=0,
                frequency_regularization=False, add_users=None, add_items=None, callback=None):
-    """side="item": SigmoidItemAsymmetricFactorModel.Train (SigmoidItemAsymmetricFactorModel.cs:
-    66-80) -> BiasedMatrixFactorization.Train (:173-194) with InitModel (:290-301: y, then U, then
-    V) and NumIter x Iterate(RandomIndex) (:91-147) + UpdateLearnRate; U = PrecomputeUserFactors.
-    side="user": SigmoidUserAsymmetricFactorModel (SigmoidUserAsymmetricFactorModel.cs:66-296),
-    the mirror: x per user, lists = UsersWhoRated, trains U, V = PrecomputeItemFactors.
-    n_users / n_items cover the AdditionalFeedback ids.  Defaults are the models' (:56-63)."""
+    """The asymmetric factor models' Train -> BiasedMatrixFactorization.Train (:173-194):
+    InitModel, NumIter x Iterate(RandomIndex) + UpdateLearnRate, then the precomputed factors.
+      side="item": SigmoidItemAsymmetricFactorModel (SigmoidItemAsymmetricFactorModel.cs:66-331):
+        InitModel = y, then U, V (:290-301); U = PrecomputeUserFactors
+      side="user": SigmoidUserAsymmetricFactorModel (SigmoidUserAsymmetricFactorModel.cs:66-296):
+        x, then U, V; V = PrecomputeItemFactors
+      side="combined": SigmoidCombinedAsymmetricFactorModel (SigmoidCombinedAsymmetricFactorModel
+        .cs:74-371): U, V, then x, then y (:291-306); both precomputed
+    n_users / n_items cover the AdditionalFeedback ids.  Defaults are the models' (:56-63).
+    Returns Y (y) and X (x) as they exist for the side."""
     users, items, values = i32(users), i32(items), f32(values)
-    user_side = side == "user"
+    mode = {"item": 0, "user": 1, "combined": 2}[side]
     rng = Rng(seed)
     cnt_u = np.bincount(users, minlength=int(users.max()) + 1).astype(np.int32)
     cnt_i = np.bincount(items, minlength=int(items.max()) + 1).astype(np.int32)
-    if user_side:  # UsersWhoRated: the same Union construction keyed by item
-        off, rated = items_rated_by_user(items, users, n_items, add_items, add_users)
-        n_x, keys, cnt_x, reg_x = n_users, users, cnt_u, reg_u
-        adds = add_users
+    off_u, ids_u = items_rated_by_user(users, items, n_users, add_users, add_items)
+    off_i, ids_i = items_rated_by_user(items, users, n_items, add_items, add_users)  # UsersWhoRated
+
+    def implicit_reg(n_x, keys, adds, reg):
+        fb = np.bincount(keys, minlength=n_x)  # UserFeedbackCounts / ItemFeedbackCounts
+        if adds is not None:
+            fb = fb + np.bincount(i32(adds), minlength=n_x)
+        out = np.zeros(n_x, np.float32)
+        for it in range(n_x):
+            if fb[it] > 0:
+                out[it] = np.float32(reg / math.sqrt(fb[it])) if frequency_regularization \
+                    else np.float32(reg)
+        return out
+
+    def implicit_init(n_x, cnt):
+        M = rng.fill_normal(n_x * k, init_mean, init_stddev).reshape(n_x, k)
+        M[[x for x in range(n_x) if x >= len(cnt) or cnt[x] == 0]] = 0
+        return M
+
+    def mf_init():
+        U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
+        V = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
+        U[np.flatnonzero(cnt_u == 0)] = 0
+        V[np.flatnonzero(cnt_i == 0)] = 0
+        return U, V
+
+    y_reg = implicit_reg(n_items, items, add_items, reg_i)
+    x_reg = implicit_reg(n_users, users, add_users, reg_u)
+    Y = np.zeros((n_items, k), np.float32)
+    X = np.zeros((n_users, k), np.float32)
+    if mode == 0:
+        Y = implicit_init(n_items, cnt_i)
+        U, V = mf_init()
+    elif mode == 1:
+        X = implicit_init(n_users, cnt_u)
+        U, V = mf_init()
     else:
-        off, rated = items_rated_by_user(users, items, n_users, add_users, add_items)
-        n_x, keys, cnt_x, reg_x = n_items, items, cnt_i, reg_i
-        adds = add_items
-    fb = np.bincount(keys, minlength=n_x)  # UserFeedbackCounts / ItemFeedbackCounts
-    if adds is not None:
-        fb = fb + np.bincount(i32(adds), minlength=n_x)
-    x_reg = np.zeros(n_x, np.float32)
-    for it in range(n_x):  # Train :72-77
-        if fb[it] > 0:
-            x_reg[it] = np.float32(reg_x / math.sqrt(fb[it])) if frequency_regularization \
-                else np.float32(reg_x)
-    Y = rng.fill_normal(n_x * k, init_mean, init_stddev).reshape(n_x, k)
-    Y[[x for x in range(n_x) if x >= len(cnt_x) or cnt_x[x] == 0]] = 0
-    U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
-    V = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
-    U[np.flatnonzero(cnt_u == 0)] = 0
-    V[np.flatnonzero(cnt_i == 0)] = 0
-    init = dict(Y=Y.copy(), U=U.copy(), V=V.copy())
+        U, V = mf_init()
+        X = implicit_init(n_users, cnt_u)
+        Y = implicit_init(n_items, cnt_i)
+    init = dict(Y=Y.copy(), X=X.copy(), U=U.copy(), V=V.copy())
     bu = np.zeros(n_users, np.float32)
     bi = np.zeros(n_items, np.float32)
     range_ = np.float32(np.float32(max_rating) - np.float32(min_rating))
@@ -475,33 +498,34 @@ def asym_train(users, items, values, n_users, n_items, min_rating, max_rating, *
     ci[:len(cnt_i)] = cnt_i
     lr = np.float32(learn_rate)
     random_index = None
-    vec = np.zeros(k, np.float32)
-    T = U if user_side else V  # the factors Iterate trains
+    vu, vi = np.zeros(k, np.float32), np.zeros(k, np.float32)
     L = lib()
     for epoch in range(num_iter):
         if random_index is None:
             random_index = rng.shuffle(np.arange(len(users), dtype=np.int32))
         p = _BmfParams(k, loss, int(frequency_regularization), 1, 1, gb, np.float32(min_rating),
                        range_, lr, bias_learn_rate, bias_reg, reg_u, reg_i)
-        L.ora_iafm_iterate(ctypes.byref(p), _p(users, _i32p), _p(items, _i32p),
+        L.ora_asym_iterate(ctypes.byref(p), _p(users, _i32p), _p(items, _i32p),
                            _p(values, _f32p), _p(random_index, _i32p), random_index.size,
-                           _p(Y, _f32p), _p(T, _f32p), _p(bu, _f32p), _p(bi, _f32p),
-                           _p(cu, _i32p), _p(ci, _i32p), _p(off, _i64p), _p(rated, _i32p),
-                           _p(x_reg, _f32p), _p(vec, _f32p), int(user_side))
+                           _p(U, _f32p), _p(V, _f32p), _p(bu, _f32p), _p(bi, _f32p),
+                           _p(cu, _i32p), _p(ci, _i32p), _p(Y, _f32p), _p(off_u, _i64p),
+                           _p(ids_u, _i32p), _p(y_reg, _f32p), _p(X, _f32p), _p(off_i, _i64p),
+                           _p(ids_i, _i32p), _p(x_reg, _f32p), _p(vu, _f32p), _p(vi, _f32p),
+                           mode)
         lr = np.float32(lr * np.float32(decay))
         if callback is not None:
-            callback(epoch, dict(Y=Y, U=U, V=V, bu=bu, bi=bi))
-    n_rows = n_items if user_side else n_users
-    P = np.zeros((n_rows, k), np.float32)  # PrecomputeItemFactors / PrecomputeUserFactors
-    L.ora_iafm_user_factors(_p(Y, _f32p), k, n_rows, _p(off, _i64p), _p(rated, _i32p),
-                            _p(P, _f32p))
-    if user_side:
-        U_out, V_out = U, P
-    else:
-        U_out, V_out = P, V
-    return dict(Y=Y, U=U_out, V=V_out, bu=bu, bi=bi, init=init, global_bias=gb, range_=range_,
-                random_index=random_index, rated_off=off, rated_items=rated, y_reg=x_reg,
-                current_learnrate=lr)
+            callback(epoch, dict(Y=Y, X=X, U=U, V=V, bu=bu, bi=bi))
+    if mode != 1:  # PrecomputeUserFactors
+        U = np.zeros((n_users, k), np.float32)
+        L.ora_iafm_user_factors(_p(Y, _f32p), k, n_users, _p(off_u, _i64p), _p(ids_u, _i32p),
+                                _p(U, _f32p))
+    if mode != 0:  # PrecomputeItemFactors
+        V = np.zeros((n_items, k), np.float32)
+        L.ora_iafm_user_factors(_p(X, _f32p), k, n_items, _p(off_i, _i64p), _p(ids_i, _i32p),
+                                _p(V, _f32p))
+    return dict(Y=Y, X=X, U=U, V=V, bu=bu, bi=bi, init=init, global_bias=gb, range_=range_,
+                random_index=random_index, rated_off=off_u, rated_items=ids_u, users_off=off_i,
+                users_ids=ids_i, y_reg=y_reg, x_reg=x_reg, current_learnrate=lr)
 
 
 def iafm_train(*a, **kw):

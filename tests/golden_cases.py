@@ -218,9 +218,23 @@ def case_uafm_small():
     snaps = {}
     st = O.asym_train(u, i, v, nu, ni, 1.0, 5.0, side="user", seed=10, k=5, num_iter=3,
                       learn_rate=0.01, add_users=au, add_items=ai,
-                      callback=lambda e, m: snaps.update({f"X{e}": m["Y"].copy()}))
-    return dict(init_X=st["init"]["Y"], X=st["Y"], U=st["U"], V=st["V"], bu=st["bu"],
-                bi=st["bi"], rated_off=st["rated_off"], rated_items=st["rated_items"], **snaps)
+                      callback=lambda e, m: snaps.update({f"X{e}": m["X"].copy()}))
+    return dict(init_X=st["init"]["X"], X=st["X"], U=st["U"], V=st["V"], bu=st["bu"],
+                bi=st["bi"], users_off=st["users_off"], users_ids=st["users_ids"], **snaps)
+
+
+def case_cafm_small():
+    # SigmoidCombinedAsymmetricFactorModel (SigmoidCombinedAsymmetricFactorModel.cs:74-182)
+    u, i, v, au, ai = iafm_case_data()
+    nu = max(int(u.max()), int(au.max())) + 1
+    ni = max(int(i.max()), int(ai.max())) + 1
+    snaps = {}
+    st = O.asym_train(u, i, v, nu, ni, 1.0, 5.0, side="combined", seed=11, k=5, num_iter=3,
+                      learn_rate=0.01, add_users=au, add_items=ai,
+                      callback=lambda e, m: snaps.update({f"X{e}": m["X"].copy(),
+                                                         f"Y{e}": m["Y"].copy()}))
+    return dict(init_X=st["init"]["X"], init_Y=st["init"]["Y"], X=st["X"], Y=st["Y"], U=st["U"],
+                V=st["V"], bu=st["bu"], bi=st["bi"], **snaps)
 
 
 def case_bpr_user_replacement_small():
@@ -273,6 +287,7 @@ CASES = {
     "bpr_user_replacement_small": case_bpr_user_replacement_small,
     "iafm_small": case_iafm_small,
     "uafm_small": case_uafm_small,
+    "cafm_small": case_cafm_small,
     "bpr_pair_replacement_small": case_bpr_pair_replacement_small,
     "wrmf_small": case_wrmf_small,
 }

@@ -1,5 +1,5 @@
-"""SigmoidItemAsymmetricFactorModel and SigmoidUserAsymmetricFactorModel on the MI355X vs the CPU
-oracle (RatingPrediction/Sigmoid{Item,User}AsymmetricFactorModel.cs; MML_MF_ITEM_ASYM / USER_ASYM).
+"""The Sigmoid{Item,User,Combined}AsymmetricFactorModels on the MI355X vs the CPU oracle
+(RatingPrediction/Sigmoid*AsymmetricFactorModel.cs; MML_MF_ITEM_ASYM / USER_ASYM / COMBINED_ASYM).
 
 * ORDERED: one wavefront in the reference's visit order; the implicit factors (y / x), the trained
   factors, biases and the precomputed factors after every epoch equal the oracle's within 1e-5 (golden fixture with AdditionalFeedback,
@@ -13,15 +13,16 @@ import pytest
 
 import oracle as O
 from golden_cases import golden, iafm_case_data, synth_ratings
-from mymedialite_amd import (Random, Ratings, SigmoidItemAsymmetricFactorModel,
-                             SigmoidUserAsymmetricFactorModel)
+from mymedialite_amd import (Random, Ratings, SigmoidCombinedAsymmetricFactorModel,
+                             SigmoidItemAsymmetricFactorModel, SigmoidUserAsymmetricFactorModel)
 
 pytestmark = pytest.mark.gpu
 
 LOSS = {0: "RMSE", 1: "MAE", 2: "LogisticLoss"}
 
 
-CLS = {"item": SigmoidItemAsymmetricFactorModel, "user": SigmoidUserAsymmetricFactorModel}
+CLS = {"item": SigmoidItemAsymmetricFactorModel, "user": SigmoidUserAsymmetricFactorModel,
+       "combined": SigmoidCombinedAsymmetricFactorModel}
 
 
 def _model(u, i, v, au, ai, side="item", **kw):
@@ -67,7 +68,26 @@ def test_user_model_ordered_matches_golden():
     print("uafm golden max |dX|", float(np.abs(m.x - g["uafm_small/X"]).max()))
 
 
-@pytest.mark.parametrize("side", ["item", "user"])
+def test_combined_model_ordered_matches_golden():
+    g = golden()
+    u, i, v, au, ai = iafm_case_data()
+    Random.set_seed(11)
+    m = _model(u, i, v, au, ai, side="combined", NumFactors=5, NumIter=0, LearnRate=0.01)
+    m.train()
+    np.testing.assert_array_equal(m.x, g["cafm_small/init_X"])
+    np.testing.assert_array_equal(m.y, g["cafm_small/init_Y"])
+    for e in range(3):
+        m.iterate()
+        np.testing.assert_allclose(m.x, g[f"cafm_small/X{e}"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(m.y, g[f"cafm_small/Y{e}"], rtol=0, atol=1e-5)
+    for key, got in (("U", m.user_factors), ("V", m.item_factors), ("bu", m.user_bias),
+                     ("bi", m.item_bias)):
+        np.testing.assert_allclose(got, g[f"cafm_small/{key}"], rtol=0, atol=1e-5)
+    print("cafm golden max |dX|, |dY|", float(np.abs(m.x - g["cafm_small/X"]).max()),
+          float(np.abs(m.y - g["cafm_small/Y"]).max()))
+
+
+@pytest.mark.parametrize("side", ["item", "user", "combined"])
 @pytest.mark.parametrize("loss,freq,k", [(0, False, 64), (1, True, 5), (2, False, 130)])
 def test_ordered_matches_oracle(loss, freq, k, side):
     u, i, v = synth_ratings(43, 120, 80, 3000)
@@ -82,8 +102,9 @@ def test_ordered_matches_oracle(loss, freq, k, side):
     m = _model(u, i, v, au, ai, side=side, NumFactors=k, NumIter=2, LearnRate=0.01,
                Loss=LOSS[loss], FrequencyRegularization=freq)
     m.train()
-    d = max(float(np.abs(m._implicit_factors() - st["Y"]).max()),
-            float(np.abs(m.item_factors - st["V"]).max()),
+    implicit = [float(np.abs(m._implicit_factors(sd) - st["X" if sd else "Y"]).max())
+                for sd in m.SIDES]
+    d = max(*implicit, float(np.abs(m.item_factors - st["V"]).max()),
             float(np.abs(m.user_factors - st["U"]).max()),
             float(np.abs(m.user_bias - st["bu"]).max()),
             float(np.abs(m.item_bias - st["bi"]).max()))
@@ -97,7 +118,7 @@ def test_ordered_matches_oracle(loss, freq, k, side):
     np.testing.assert_allclose(m.predict(qu, qi), want, rtol=0, atol=1e-5)
 
 
-@pytest.mark.parametrize("side", ["item", "user"])
+@pytest.mark.parametrize("side", ["item", "user", "combined"])
 def test_hogwild_statistical_parity(side):
     u, i, v = synth_ratings(45, 1500, 400, 20000)
     tu, ti, tv = synth_ratings(46, 1500, 400, 4000)

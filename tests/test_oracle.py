@@ -326,6 +326,6 @@ def test_iafm_items_rated_by_user_union_order():
     m.ratings = Ratings(u, i, g["iafm_small/values"])
     m.additional_feedback = Ratings(au, ai, np.ones(len(au), np.float32))
     m.MaxUserID, m.MaxItemID = len(off) - 2, int(max(i.max(), ai.max()))
-    o2, it2 = m._feedback_lists()
+    o2, it2 = m._feedback_lists(0)
     np.testing.assert_array_equal(o2, off)
     np.testing.assert_array_equal(it2, items)
