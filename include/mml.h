@@ -140,10 +140,15 @@ enum {
                             43-309): the mirror -- the item vector is x summed over the users who
                             rated the item / sqrt(count), each rating trains U_u and those x rows
                             (ABI 3) */
-    MML_MF_COMBINED_ASYM = 5 /* SigmoidCombinedAsymmetricFactorModel
+    MML_MF_COMBINED_ASYM = 5, /* SigmoidCombinedAsymmetricFactorModel
                             (SigmoidCombinedAsymmetricFactorModel.cs:46-382): both -- user vector
                             from y, item vector from x, each rating trains those x and y rows
                             (ABI 3) */
+    MML_MF_SVDPP = 6,    /* SVDPlusPlus (SVDPlusPlus.cs:43-423): a MatrixFactorization with biases;
+                            user vector = y summed over the user's items / sqrt(count) + p_u;
+                            Predict without sigmoid, clipped (ABI 3) */
+    MML_MF_SIGMOID_SVDPP = 7 /* SigmoidSVDPlusPlus (SigmoidSVDPlusPlus.cs:42-269): the same with
+                            the sigmoid link and the loss variants (ABI 3) */
 };
 
 typedef struct {
@@ -250,6 +255,10 @@ mml_status mml_bmf_set_implicit_feedback(mml_bmf* h, int32_t side, int32_t n_row
                                          const float* factors, const float* reg);
 /* y [n_items x k] (side 0) / x [n_users x k] (side 1), e.g. for SaveModel */
 mml_status mml_bmf_get_implicit_factors(mml_bmf* h, int32_t side, float* factors);
+/* SVD++: the free user factors p [n_users x k] (SVDPlusPlus.InitModel, SVDPlusPlus.cs:129-155);
+ * together with side 0 they form the precomputed user factors (PrecomputeFactors :230-246) */
+mml_status mml_bmf_set_user_offsets(mml_bmf* h, const float* p);
+mml_status mml_bmf_get_user_offsets(mml_bmf* h, float* p);
 
 /* ------------------------------------------------------------------ BPRMF */
 enum {

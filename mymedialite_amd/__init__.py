@@ -9,11 +9,12 @@ from .item_recommendation import BPRMF, WRMF, SoftMarginRankingMF, WeightedBPRMF
 from .rating_prediction import (BiasedMatrixFactorization, MatrixFactorization,
                                 SigmoidItemAsymmetricFactorModel,
                                 SigmoidUserAsymmetricFactorModel, SocialMF,
-                                SigmoidCombinedAsymmetricFactorModel)
+                                SigmoidCombinedAsymmetricFactorModel, SigmoidSVDPlusPlus,
+                                SVDPlusPlus)
 
 __all__ = ["BiasedMatrixFactorization", "MatrixFactorization", "SocialMF",
            "SigmoidItemAsymmetricFactorModel", "SigmoidUserAsymmetricFactorModel",
-           "SigmoidCombinedAsymmetricFactorModel", "BPRMF", "WRMF",
+           "SigmoidCombinedAsymmetricFactorModel", "SVDPlusPlus", "SigmoidSVDPlusPlus", "BPRMF", "WRMF",
            "SoftMarginRankingMF", "WeightedBPRMF", "Ratings",
            "PosOnlyFeedback", "Mapping", "IdentityMapping", "read_ratings", "read_items", "Random",
            "SystemRandom"]

@@ -44,6 +44,7 @@ class BmfParams(ctypes.Structure):
 
 
 MF_BIASED, MF_PLAIN, MF_SOCIAL, MF_ITEM_ASYM, MF_USER_ASYM, MF_COMBINED_ASYM = 0, 1, 2, 3, 4, 5
+MF_SVDPP, MF_SIGMOID_SVDPP = 6, 7
 
 
 class BprParams(ctypes.Structure):
@@ -129,6 +130,8 @@ SIGNATURES = {
     "mml_bmf_set_implicit_feedback": (_st, [_vp, ctypes.c_int32, ctypes.c_int32, _i64p, _i32p,
                                             _f32p, _f32p]),
     "mml_bmf_get_implicit_factors": (_st, [_vp, ctypes.c_int32, _f32p]),
+    "mml_bmf_set_user_offsets": (_st, [_vp, _f32p]),
+    "mml_bmf_get_user_offsets": (_st, [_vp, _f32p]),
     "mml_bpr_last_triples": (_st, [_vp, _i32p, _i32p, _i32p, ctypes.c_int64]),
     "mml_bpr_auc": (_st, [_vp, _i32p, ctypes.c_int32, _i32p, ctypes.c_int32, _i64p, _i32p,
                           _f64p]),

@@ -342,7 +342,8 @@ __device__ __forceinline__ float bmf_predict1(int32_t u, int32_t i, int32_t n_us
                                               int32_t n_items, const float* U, const float* V,
                                               const float* bu, const float* bi, int32_t k,
                                               int32_t ld, float gb, float min_rating,
-                                              float max_rating, bool plain) {
+                                              float max_rating, int kind) {
+    const bool plain = kind == 1;
     const bool ku = u >= 0 && u < n_users, ki = i >= 0 && i < n_items;
     float dot = 0.0f;
     if (ku && ki) {
@@ -360,6 +361,11 @@ __device__ __forceinline__ float bmf_predict1(int32_t u, int32_t i, int32_t n_us
     if (ku) score += (double)bu[u];
     if (ki) score += (double)bi[i];
     if (ku && ki) score += (double)dot;
+    if (kind == 2) {  // SVDPlusPlus.Predict (SVDPlusPlus.cs:106-126): no sigmoid, clamped
+        if (score > (double)max_rating) return max_rating;
+        if (score < (double)min_rating) return min_rating;
+        return (float)score;
+    }
     const float range = max_rating - min_rating;
     return (float)((double)min_rating + (1.0 / (1.0 + exp(-score))) * (double)range);
 }
@@ -372,7 +378,7 @@ __global__ __launch_bounds__(256) void bmf_predict_kernel(
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
          x += (int64_t)gridDim.x * blockDim.x)
         out[x] = bmf_predict1(users[x], items[x], n_users, n_items, U, V, bu, bi, k, ld, gb,
-                              min_rating, max_rating, plain != 0);
+                              min_rating, max_rating, plain);
 }
 
 // Eval.Ratings.Evaluate (:96-139): float error, float square, double sums; per-block partials.
@@ -386,7 +392,7 @@ __global__ __launch_bounds__(256) void bmf_eval_kernel(
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
          x += (int64_t)gridDim.x * blockDim.x) {
         const float p = bmf_predict1(users[x], items[x], n_users, n_items, U, V, bu, bi, k, ld,
-                                     gb, min_rating, max_rating, plain != 0);
+                                     gb, min_rating, max_rating, plain);
         const float e = p - values[x];
         se += (double)(e * e);
         ae += (double)fabsf(e);
@@ -838,10 +844,14 @@ inline int lanes_per_rating(int k) {
 // MODE kAsymItem (SigmoidItemAsymmetricFactorModel.cs:91-147): slot 0; trains V_i and y.
 // MODE kAsymUser (SigmoidUserAsymmetricFactorModel.cs:91-144): slot 1; trains U_u and x.
 // MODE kAsymCombined (SigmoidCombinedAsymmetricFactorModel.cs:108-182): both; trains x and y.
+// MODE kSvdpp (SVDPlusPlus.cs:157-212, a MatrixFactorization: no sigmoid, err drives the steps)
+// and kSigmoidSvdpp (SigmoidSVDPlusPlus.cs:111-173): slot 0 plus the free user offset p
+// [n_users x k]: user vector = y sum / sqrt(count) + p_u (double, cast to float); trains p_u,
+// V_i and y.
 // One wavefront per rating at a time, lane f owns factors f, f + 64, ... (KM per lane), so every
 // per-factor sum and update runs in the reference's order.  ORDERED = one wavefront over the
 // whole stream (bit-faithful); HOGWILD = many wavefronts on chunks of it.
-constexpr int kAsymItem = 0, kAsymUser = 1, kAsymCombined = 2;
+constexpr int kAsymItem = 0, kAsymUser = 1, kAsymCombined = 2, kSvdpp = 3, kSigmoidSvdpp = 4;
 
 struct AsymSlot {
     float* X;                         // the implicit factors (y or x)
@@ -898,7 +908,8 @@ __global__ __launch_bounds__(64) void asym_sgd_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
     int64_t n, int64_t chunk, AsymSlot s0, AsymSlot s1, float* U, float* V, float* bu, float* bi,
     int32_t k, int32_t ld, BmfScalars s, const int32_t* __restrict__ cnt_u,
-    const int32_t* __restrict__ cnt_i) {
+    const int32_t* __restrict__ cnt_i, float* P) {
+    constexpr bool svdpp = MODE == kSvdpp || MODE == kSigmoidSvdpp;
     const int lane = threadIdx.x;
     const int64_t begin = (int64_t)blockIdx.x * chunk;
     const int64_t end = min(begin + chunk, n);
@@ -909,14 +920,38 @@ __global__ __launch_bounds__(64) void asym_sgd_kernel(
         float a[KM], c[KM], prod[KM];
         double norm_u = 1.0, norm_i = 1.0;
         float* trained = nullptr;  // kAsymItem: V_i, kAsymUser: U_u
-        if constexpr (MODE != kAsymUser) norm_u = asym_vector<KM>(s0, k, ld, u, lane, a);
-        if constexpr (MODE != kAsymItem) norm_i = asym_vector<KM>(s1, k, ld, i, lane, c);
-        if constexpr (MODE == kAsymItem) trained = V + (int64_t)i * ld;
+        float pu[KM];  // svdpp: p_u
+        if constexpr (svdpp) {
+            // p_plus_y_sum_vector[f] = (float)(y_sum[f] / norm + p[u, f]) (SVDPlusPlus.cs:166-170)
+            float* Pu = P + (int64_t)u * ld;
+            const int64_t b = s0.off[u], e = s0.off[u + 1];
+#pragma unroll
+            for (int m = 0; m < KM; ++m) a[m] = 0.0f;
+            for (int64_t t = b; t < e; ++t) {
+                const float* row = s0.X + (int64_t)s0.ids[t] * ld;
+#pragma unroll
+                for (int m = 0; m < KM; ++m) {
+                    const int f = lane + 64 * m;
+                    a[m] += f < k ? row[f] : 0.0f;
+                }
+            }
+            norm_u = sqrt((double)(e - b));
+#pragma unroll
+            for (int m = 0; m < KM; ++m) {
+                const int f = lane + 64 * m;
+                pu[m] = f < k ? Pu[f] : 0.0f;
+                a[m] = (float)((double)a[m] / norm_u + (double)pu[m]);
+            }
+        } else if constexpr (MODE != kAsymUser) {
+            norm_u = asym_vector<KM>(s0, k, ld, u, lane, a);
+        }
+        if constexpr (MODE != kAsymItem && !svdpp) norm_i = asym_vector<KM>(s1, k, ld, i, lane, c);
+        if constexpr (MODE == kAsymItem || svdpp) trained = V + (int64_t)i * ld;
         if constexpr (MODE == kAsymUser) trained = U + (int64_t)u * ld;
 #pragma unroll
         for (int m = 0; m < KM; ++m) {
             const int f = lane + 64 * m;
-            if constexpr (MODE == kAsymItem) c[m] = f < k ? trained[f] : 0.0f;
+            if constexpr (MODE == kAsymItem || svdpp) c[m] = f < k ? trained[f] : 0.0f;
             if constexpr (MODE == kAsymUser) a[m] = f < k ? trained[f] : 0.0f;
             prod[m] = a[m] * c[m];
         }
@@ -939,9 +974,16 @@ __global__ __launch_bounds__(64) void asym_sgd_kernel(
         const float bu_u = bu[u], bi_i = bi[i];
         // score = global_bias + user_bias + item_bias in float, then + dot in double
         const double score = (double)((s.gb + bu_u) + bi_i) + (double)dot;
-        const double sig = 1.0 / (1.0 + exp(-score));
-        const double err = (double)r - ((double)s.min_rating + sig * (double)s.range);
-        const float g = gradient_common<LOSS>(sig, err, s.range);
+        double err;
+        float g;
+        if constexpr (MODE == kSvdpp) {  // prediction = score, no sigmoid; biases step on (float)err
+            err = (double)r - score;
+            g = (float)err;
+        } else {
+            const double sig = 1.0 / (1.0 + exp(-score));
+            err = (double)r - ((double)s.min_rating + sig * (double)s.range);
+            g = gradient_common<LOSS>(sig, err, s.range);
+        }
         float reg_u = s.reg_u, reg_i = s.reg_i;
         if (cnt_u) {  // FrequencyRegularization
             reg_u = (float)((double)s.reg_u / sqrt((double)cnt_u[u]));
@@ -960,6 +1002,24 @@ __global__ __launch_bounds__(64) void asym_sgd_kernel(
                 const double delta = (double)(g * a[m] - reg_i * i_f);  // float expression
                 if (f < k) trained[f] = i_f + (float)((double)s.lr * delta);
                 cu[m] = ((double)g / norm_u) * (double)i_f;
+            } else if constexpr (MODE == kSvdpp) {  // SVDPlusPlus.cs:186-209: double err drives
+                const float i_f = c[m];
+                const double delta_u = err * (double)i_f - (double)(reg_u * pu[m]);
+                const double delta_i = err * (double)a[m] - (double)(reg_i * i_f);
+                if (f < k) {
+                    P[(int64_t)u * ld + f] = pu[m] + (float)((double)s.lr * delta_u);
+                    trained[f] = i_f + (float)((double)s.lr * delta_i);
+                }
+                cu[m] = (err / norm_u) * (double)i_f;
+            } else if constexpr (MODE == kSigmoidSvdpp) {  // SigmoidSVDPlusPlus.cs:152-170
+                const float i_f = c[m];
+                const double delta_u = (double)(g * i_f - reg_u * pu[m]);  // float expressions
+                const double delta_i = (double)(g * a[m] - reg_i * i_f);
+                if (f < k) {
+                    P[(int64_t)u * ld + f] = pu[m] + (float)((double)s.lr * delta_u);
+                    trained[f] = i_f + (float)((double)s.lr * delta_i);
+                }
+                cu[m] = ((double)g / norm_u) * (double)i_f;
             } else if constexpr (MODE == kAsymUser) {  // :127-142: U_u step, x's from old u_f
                 const float u_f = a[m];
                 const double delta = (double)(g * c[m] - reg_u * u_f);
@@ -970,21 +1030,42 @@ __global__ __launch_bounds__(64) void asym_sgd_kernel(
                 cu[m] = ((double)g / norm_u) * (double)c[m];
             }
         }
-        if constexpr (MODE != kAsymItem) asym_list_step<KM>(s1, k, ld, i, lane, s.lr, ci);
+        if constexpr (MODE == kAsymUser || MODE == kAsymCombined)
+            asym_list_step<KM>(s1, k, ld, i, lane, s.lr, ci);
         if constexpr (MODE != kAsymUser) asym_list_step<KM>(s0, k, ld, u, lane, s.lr, cu);
     }
 }
 
 // PrecomputeUserFactors / PrecomputeItemFactors: row r of `out` = the represented vector of r;
 // rows with an empty list get zeros (the reference assigns a fresh zero matrix)
+// P != nullptr (SVD++ PrecomputeFactors, SVDPlusPlus.cs:230-246): + p_r before the cast
 template <int KM>
 __global__ __launch_bounds__(64) void asym_precompute_kernel(AsymSlot sl, int32_t k, int32_t ld,
                                                              int32_t n_rows,
+                                                             const float* __restrict__ P,
                                                              float* __restrict__ out) {
     const int lane = threadIdx.x;
     for (int32_t r = blockIdx.x; r < n_rows; r += gridDim.x) {
         float vec[KM];
-        if (sl.off[r + 1] > sl.off[r]) {
+        if (sl.off[r + 1] > sl.off[r] && P) {
+            const int64_t b = sl.off[r], e = sl.off[r + 1];
+#pragma unroll
+            for (int m = 0; m < KM; ++m) vec[m] = 0.0f;
+            for (int64_t t = b; t < e; ++t) {
+                const float* row = sl.X + (int64_t)sl.ids[t] * ld;
+#pragma unroll
+                for (int m = 0; m < KM; ++m) {
+                    const int f = lane + 64 * m;
+                    vec[m] += f < k ? row[f] : 0.0f;
+                }
+            }
+            const double norm = sqrt((double)(e - b));
+#pragma unroll
+            for (int m = 0; m < KM; ++m) {
+                const int f = lane + 64 * m;
+                vec[m] = (float)((double)vec[m] / norm + (double)(f < k ? P[(int64_t)r * ld + f] : 0.0f));
+            }
+        } else if (sl.off[r + 1] > sl.off[r]) {
             asym_vector<KM>(sl, k, ld, r, lane, vec);
         } else {
 #pragma unroll
@@ -1027,11 +1108,19 @@ struct mml_bmf {
     mml::DeviceArray<int32_t> asym_ids[2];
     mml::DeviceArray<float> asym_x[2], asym_reg[2];
     bool has_slot[2] = {false, false};
+    mml::DeviceArray<float> P;  // SVD++: the free user offsets p [n_users x ld]
+    bool has_p = false;
 };
 
 namespace {
 
 void check_handle(mml_bmf* h) { MML_REQUIRE(h && h->ctx, "null handle"); }
+
+// bmf_predict1's kind: 0 BiasedMatrixFactorization (sigmoid), 1 MatrixFactorization (plain,
+// clipped), 2 SVDPlusPlus (biases, clipped)
+int32_t predict_kind(const mml_bmf* h) {
+    return h->p.model == MML_MF_PLAIN ? 1 : h->p.model == MML_MF_SVDPP ? 2 : 0;
+}
 
 // upload / download a [rows x k] host matrix into a [rows x ld] zero-padded device matrix
 void upload_padded(mml_bmf* h, float* dst, const float* src, int64_t rows) {
@@ -1264,21 +1353,32 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
 }
 
 bool is_asym(const mml_bmf* h) {
-    return h->p.model == MML_MF_ITEM_ASYM || h->p.model == MML_MF_USER_ASYM ||
-           h->p.model == MML_MF_COMBINED_ASYM;
+    return h->p.model >= MML_MF_ITEM_ASYM && h->p.model <= MML_MF_SIGMOID_SVDPP;
 }
 int asym_mode(const mml_bmf* h) {
-    return h->p.model == MML_MF_ITEM_ASYM ? kAsymItem
-           : h->p.model == MML_MF_USER_ASYM ? kAsymUser
-                                            : kAsymCombined;
+    switch (h->p.model) {
+        case MML_MF_ITEM_ASYM: return kAsymItem;
+        case MML_MF_USER_ASYM: return kAsymUser;
+        case MML_MF_SVDPP: return kSvdpp;
+        case MML_MF_SIGMOID_SVDPP: return kSigmoidSvdpp;
+        default: return kAsymCombined;
+    }
+}
+bool is_svdpp(const mml_bmf* h) {
+    return h->p.model == MML_MF_SVDPP || h->p.model == MML_MF_SIGMOID_SVDPP;
 }
 AsymSlot asym_slot(mml_bmf* h, int side) {
     return AsymSlot{h->asym_x[side].get(), h->asym_off[side].get(), h->asym_ids[side].get(),
                     h->asym_reg[side].get()};
 }
-bool asym_ready(const mml_bmf* h) {
+// the sides a model reads: slot 0 for all but the user model, slot 1 for the user / combined ones
+bool uses_side(const mml_bmf* h, int side) {
     const int mode = asym_mode(h);
-    return (mode == kAsymUser || h->has_slot[0]) && (mode == kAsymItem || h->has_slot[1]);
+    return side == 0 ? mode != kAsymUser : (mode == kAsymUser || mode == kAsymCombined);
+}
+bool asym_ready(const mml_bmf* h) {
+    return (!uses_side(h, 0) || h->has_slot[0]) && (!uses_side(h, 1) || h->has_slot[1]) &&
+           (!is_svdpp(h) || h->has_p);
 }
 
 // U <- PrecomputeUserFactors (slot 0) and / or V <- PrecomputeItemFactors (slot 1): what Predict
@@ -1287,14 +1387,17 @@ void asym_precompute(mml_bmf* h) {
     const int km = (h->k + 63) / 64;
     const int mode = asym_mode(h);
     hipStream_t st = h->ctx->stream;
+    (void)mode;
     for (int side = 0; side < 2; ++side) {
-        if ((side == 0 && mode == kAsymUser) || (side == 1 && mode == kAsymItem)) continue;
+        if (!uses_side(h, side)) continue;
         const int32_t rows = side == 0 ? h->n_users : h->n_items;
         if (rows == 0) continue;
         const int grid = std::max(1, std::min(rows, 65536));
         float* out = side == 0 ? h->U.get() : h->V.get();
         const AsymSlot sl = asym_slot(h, side);
-#define MML_PRE(KM) asym_precompute_kernel<KM><<<grid, 64, 0, st>>>(sl, h->k, h->ld, rows, out)
+        const float* pp = side == 0 && is_svdpp(h) ? h->P.get() : nullptr;
+#define MML_PRE(KM) \
+    asym_precompute_kernel<KM><<<grid, 64, 0, st>>>(sl, h->k, h->ld, rows, pp, out)
         switch (km) {
             case 1: MML_PRE(1); break;
             case 2: MML_PRE(2); break;
@@ -1324,7 +1427,7 @@ void asym_epoch(mml_bmf* h, const BmfScalars& s) {
 #define MML_ASYM(KM, MODE)                                                                     \
     asym_sgd_kernel<LOSS, KM, MODE><<<(int)waves, 64, 0, st>>>(                                \
         h->su.get(), h->si.get(), h->sr.get(), n, chunk, s0, s1, h->U.get(), h->V.get(),       \
-        h->bu.get(), h->bi.get(), h->k, h->ld, s, cu, ci)
+        h->bu.get(), h->bi.get(), h->k, h->ld, s, cu, ci, h->P.get())
 #define MML_ASYM_K(MODE)                    \
     switch (km) {                           \
         case 1: MML_ASYM(1, MODE); break;   \
@@ -1335,6 +1438,8 @@ void asym_epoch(mml_bmf* h, const BmfScalars& s) {
         switch (asym_mode(h)) {
             case kAsymItem: MML_ASYM_K(kAsymItem); break;
             case kAsymUser: MML_ASYM_K(kAsymUser); break;
+            case kSvdpp: MML_ASYM_K(kSvdpp); break;
+            case kSigmoidSvdpp: MML_ASYM_K(kSigmoidSvdpp); break;
             default: MML_ASYM_K(kAsymCombined); break;
         }
 #undef MML_ASYM_K
@@ -1386,7 +1491,7 @@ extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params,
                     "num_factors must be in [1, 256]");
         MML_REQUIRE(params->loss >= MML_LOSS_RMSE && params->loss <= MML_LOSS_LOGISTIC,
                     "unknown loss");
-        MML_REQUIRE(params->model >= MML_MF_BIASED && params->model <= MML_MF_COMBINED_ASYM,
+        MML_REQUIRE(params->model >= MML_MF_BIASED && params->model <= MML_MF_SIGMOID_SVDPP,
                     "unknown model family");
         MML_REQUIRE(params->schedule >= MML_SCHEDULE_ORDERED &&
                         params->schedule <= MML_SCHEDULE_HOGWILD_COHERENT,
@@ -1655,7 +1760,7 @@ extern "C" mml_status mml_bmf_predict(mml_bmf* h, const int32_t* users, const in
         bmf_predict_kernel<<<grid_for(n), 256, 0, st>>>(
             h->ev_u.get(), h->ev_i.get(), n, h->n_users, h->n_items, h->U.get(), h->V.get(),
             h->bu.get(), h->bi.get(), h->k, h->ld, h->gb, h->min_rating, h->max_rating,
-            (int32_t)(h->p.model == MML_MF_PLAIN), h->ev_out.get());
+            predict_kind(h), h->ev_out.get());
         MML_HIP(hipGetLastError());
         MML_HIP(hipMemcpyAsync(out, h->ev_out.get(), sizeof(float) * n, hipMemcpyDeviceToHost,
                                st));
@@ -1681,7 +1786,7 @@ extern "C" mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const i
                                               h->n_users, h->n_items, h->U.get(), h->V.get(),
                                               h->bu.get(), h->bi.get(), h->k, h->ld, h->gb,
                                               h->min_rating, h->max_rating,
-                                              (int32_t)(h->p.model == MML_MF_PLAIN),
+                                              predict_kind(h),
                                               h->ev_partials.get());
         MML_HIP(hipGetLastError());
         std::vector<double> part(2 * grid);
@@ -1938,9 +2043,7 @@ extern "C" mml_status mml_bmf_set_implicit_feedback(mml_bmf* h, int32_t side, in
         check_handle(h);
         MML_REQUIRE(is_asym(h), "implicit feedback belongs to the asymmetric models' handles");
         MML_REQUIRE(side == 0 || side == 1, "side must be 0 (lists per user) or 1 (per item)");
-        const int mode = asym_mode(h);
-        MML_REQUIRE(!(side == 0 && mode == kAsymUser) && !(side == 1 && mode == kAsymItem),
-                    "this model does not use that side");
+        MML_REQUIRE(uses_side(h, side), "this model does not use that side");
         // side 0: a list of items per user, factors y [n_items x k]; side 1: a list of users per
         // item, factors x [n_users x k]
         const int32_t n_list = side == 0 ? h->n_users : h->n_items;
@@ -1984,6 +2087,31 @@ extern "C" mml_status mml_bmf_get_implicit_factors(mml_bmf* h, int32_t side, flo
         MML_REQUIRE(factors, "null argument");
         h->ctx->activate();
         download_padded(h, factors, h->asym_x[side].get(), side == 0 ? h->n_items : h->n_users);
+        MML_HIP(hipStreamSynchronize(h->ctx->stream));
+    });
+}
+
+extern "C" mml_status mml_bmf_set_user_offsets(mml_bmf* h, const float* p) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(is_svdpp(h), "user offsets belong to SVD++ handles");
+        MML_REQUIRE(p, "null argument");
+        h->ctx->activate();
+        h->P.alloc((size_t)std::max<int64_t>(1, (int64_t)h->n_users * h->ld));
+        upload_padded(h, h->P.get(), p, h->n_users);
+        h->has_p = true;
+        if (asym_ready(h)) asym_precompute(h);
+        MML_HIP(hipStreamSynchronize(h->ctx->stream));
+    });
+}
+
+extern "C" mml_status mml_bmf_get_user_offsets(mml_bmf* h, float* p) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(h->has_p, "no user offsets (set_user_offsets first)");
+        MML_REQUIRE(p, "null argument");
+        h->ctx->activate();
+        download_padded(h, p, h->P.get(), h->n_users);
         MML_HIP(hipStreamSynchronize(h->ctx->stream));
     });
 }

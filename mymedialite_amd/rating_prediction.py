@@ -897,5 +897,119 @@ class SigmoidCombinedAsymmetricFactorModel(_AsymmetricFactorModel):
             _g(self.Decay), self.NumIter, self.Loss)
 
 
+class SVDPlusPlus(_AsymmetricFactorModel):
+    """GPU-backed MyMediaLite.RatingPrediction.SVDPlusPlus (SVDPlusPlus.cs:43-423): a
+    MatrixFactorization with biases whose user vector is y summed over the user's items (training
+    and ``additional_feedback``) / sqrt(count) + p_u; each rating trains p_u, V_i and the y rows
+    of the user's items (Iterate :157-212, MML_MF_SVDPP).  Train() sets global_bias =
+    Ratings.Average (MatrixFactorization.Train :119-126); Predict has no sigmoid and is clipped to
+    the rating scale (:106-126).  user_factors = PrecomputeFactors (:216-246)."""
+    PROPERTIES = {
+        "BiasLearnRate": "float", "BiasReg": "float", "Decay": "float", "Device": "int",
+        "FrequencyRegularization": "bool", "InitMean": "double", "InitStdDev": "double",
+        "LearnRate": "float", "NumFactors": "uint", "NumIter": "uint", "Regularization": "float",
+        "Schedule": "string",
+    }
+    MODEL = N.MF_SVDPP
+    TYPE_NAME = "MyMediaLite.RatingPrediction.SVDPlusPlus"
+    SIDES = (0,)
+
+    def init_model(self):
+        """Train (:87-104: sizes, y_reg from Regularization), then InitModel (:129-155): U, V
+        (MatrixFactorization), p, y; rows of items / users beyond the training ids zeroed (V too)."""
+        r, a = self._ratings, self.additional_feedback
+        if a is not None and len(a.users):
+            self.MaxUserID = max(r.max_user_id, int(np.max(a.users)))
+            self.MaxItemID = max(r.max_item_id, int(np.max(a.items)))
+        k = int(self.NumFactors)
+        nu, ni = self.MaxUserID + 1, self.MaxItemID + 1
+        fb = np.bincount(N.i32(r.items), minlength=ni)  # ItemFeedbackCounts
+        if a is not None and len(a.users):
+            fb = fb + np.bincount(N.i32(a.items), minlength=ni)
+        reg = float(np.float32(self.Regularization))
+        y_reg = np.zeros(ni, np.float32)
+        nz = fb > 0
+        y_reg[nz] = (np.float32(reg / np.sqrt(fb[nz].astype(np.float64)))
+                     if self.FrequencyRegularization else np.float32(reg))
+        rng = Random.get_instance()
+        U = rng.fill_normal(nu * k, self.InitMean, self.InitStdDev).reshape(nu, k)
+        V = rng.fill_normal(ni * k, self.InitMean, self.InitStdDev).reshape(ni, k)
+        cu, ci = r.count_by_user, r.count_by_item
+        U[np.flatnonzero(cu == 0)] = 0.0
+        V[np.flatnonzero(ci == 0)] = 0.0
+        P = rng.fill_normal(nu * k, self.InitMean, self.InitStdDev).reshape(nu, k)
+        y = rng.fill_normal(ni * k, self.InitMean, self.InitStdDev).reshape(ni, k)
+        y[np.flatnonzero(ci == 0)] = 0.0
+        y[len(ci):] = 0.0
+        V[len(ci):] = 0.0
+        P[len(cu):] = 0.0
+        self.current_learnrate = float(np.float32(self.LearnRate))
+        self._create_handle(nu, ni)
+        self._host = dict(U=U, V=V, bu=np.zeros(nu, np.float32), bi=np.zeros(ni, np.float32))
+        self._upload_model(0.0)
+        off, ids = self._feedback_lists(0)
+        N.check(N.lib().mml_bmf_set_implicit_feedback(
+            self._h, 0, len(off) - 1, N.ptr(off, N._i64p), N.ptr(ids, N._i32p),
+            N.ptr(N.f32(y), N._f32p), N.ptr(y_reg, N._f32p)))
+        N.check(N.lib().mml_bmf_set_user_offsets(self._h, N.ptr(N.f32(P), N._f32p)))
+
+    def train(self):
+        """MatrixFactorization.Train (:119-126): InitModel, global_bias = Ratings.Average,
+        NumIter x Iterate (each ending with UpdateLearnRate, SVDPlusPlus.cs:211)."""
+        self.init_model()
+        self.global_bias = self._ratings.average
+        self._upload_model(self.global_bias)
+        self._host = None
+        for _ in range(int(self.NumIter)):
+            self.iterate()
+
+    @property
+    def y(self):
+        return self._implicit_factors(0)
+
+    @property
+    def p(self):
+        out = np.empty((self.MaxUserID + 1, int(self.NumFactors)), np.float32)
+        N.check(N.lib().mml_bmf_get_user_offsets(self._h, N.ptr(out, N._f32p)))
+        return out
+
+    def save_model(self, path: str):
+        """SaveModel (:272-285): global bias, min/max rating, user biases, item biases, p, y,
+        item factors."""
+        from .model_io import ModelWriter
+        m = self.get_model()
+        with ModelWriter(path, self.TYPE_NAME) as w:
+            w.write_float(self.global_bias)
+            w.write_float(self.min_rating)
+            w.write_float(self.max_rating)
+            w.write_vector(m["bu"])
+            w.write_vector(m["bi"])
+            w.write_matrix(self.p)
+            w.write_matrix(self.y)
+            w.write_matrix(m["V"])
+
+    def __str__(self):
+        """ToString() (:414-420)."""
+        return ("{} num_factors={} regularization={} bias_reg={} frequency_regularization={} "
+                "learn_rate={} bias_learn_rate={} learn_rate_decay={} num_iter={}").format(
+            type(self).__name__, self.NumFactors, _g(self.Regularization), _g(self.BiasReg),
+            self.FrequencyRegularization, _g(self.LearnRate), _g(self.BiasLearnRate),
+            _g(self.Decay), self.NumIter)
+
+
+class SigmoidSVDPlusPlus(SVDPlusPlus):
+    """GPU-backed MyMediaLite.RatingPrediction.SigmoidSVDPlusPlus (SigmoidSVDPlusPlus.cs:42-269):
+    SVDPlusPlus with the sigmoid link and the loss variants (Iterate :111-173,
+    MML_MF_SIGMOID_SVDPP).  Its Train computes the logit global bias, which
+    MatrixFactorization.Train then overwrites with Ratings.Average (kept, :62-71)."""
+    PROPERTIES = dict(SVDPlusPlus.PROPERTIES, Loss=tuple(_LOSS))
+    MODEL = N.MF_SIGMOID_SVDPP
+    TYPE_NAME = "MyMediaLite.RatingPrediction.SigmoidSVDPlusPlus"
+
+    def __str__(self):
+        """ToString() (:260-266)."""
+        return super().__str__() + f" loss={self.Loss}"
+
+
 def _g(x):
     return f"{float(np.float32(x)):.7g}"

@@ -233,26 +233,41 @@ static void ora_iafm_user_vector(const float* Y, int k, const int64_t* rated_off
  *   mode 2 SigmoidCombinedAsymmetricFactorModel (SigmoidCombinedAsymmetricFactorModel.cs:
  *          108-182): both vectors; VectorExtensions.ScalarProduct (double sum, VectorExtensions.cs:
  *          30-38); trains x (from the user vector) and y (from the item vector)
- * vu, vi: k floats of scratch each. */
+ *   mode 3 SVDPlusPlus (SVDPlusPlus.cs:157-212): user vector = (float)(y sum / norm + p_u); no
+ *          sigmoid: err = r - prediction drives the (float)err bias steps and the double p_u,
+ *          V_i and y steps
+ *   mode 4 SigmoidSVDPlusPlus (SigmoidSVDPlusPlus.cs:111-173): the same vector with the sigmoid
+ *          link and gradient_common (float update expressions)
+ * P: p [n_users x k] (modes 3, 4).  vu, vi: k floats of scratch each. */
 void ora_asym_iterate(const ora_bmf_params* p, const int32_t* users, const int32_t* items,
                       const float* values, const int32_t* idx, int64_t n_idx, float* U, float* V,
                       float* bu, float* bi, const int32_t* count_by_user,
                       const int32_t* count_by_item, float* Y, const int64_t* off_u,
                       const int32_t* ids_u, const float* y_reg, float* X, const int64_t* off_i,
                       const int32_t* ids_i, const float* x_reg, float* vu, float* vi,
-                      int32_t mode) {
+                      int32_t mode, float* P) {
     const int k = p->k;
     const float lr = p->learn_rate;
     for (int64_t n = 0; n < n_idx; n++) {
         const int32_t index = idx[n];
         const int32_t u = users[index], i = items[index];
         double norm_u = 1.0, norm_i = 1.0;
-        if (mode != 1) ora_iafm_user_vector(Y, k, off_u, ids_u, u, vu, &norm_u);
-        if (mode != 0) ora_iafm_user_vector(X, k, off_i, ids_i, i, vi, &norm_i);
+        if (mode >= 3) { /* p_plus_y_sum_vector (SVDPlusPlus.cs:166-170) */
+            const int64_t b = off_u[u], e = off_u[u + 1];
+            for (int f = 0; f < k; f++) vu[f] = 0.0f;
+            for (int64_t t = b; t < e; t++)
+                for (int f = 0; f < k; f++) vu[f] += Y[(int64_t)ids_u[t] * k + f];
+            norm_u = sqrt((double)(e - b));
+            for (int f = 0; f < k; f++)
+                vu[f] = (float)((double)vu[f] / norm_u + (double)P[(int64_t)u * k + f]);
+        } else if (mode != 1) {
+            ora_iafm_user_vector(Y, k, off_u, ids_u, u, vu, &norm_u);
+        }
+        if (mode == 1 || mode == 2) ora_iafm_user_vector(X, k, off_i, ids_i, i, vi, &norm_i);
         float* Ui = U + (int64_t)u * k;
         float* Vi = V + (int64_t)i * k;
         double score = (double)((p->global_bias + bu[u]) + bi[i]); /* float sum */
-        if (mode == 0) {        /* item_factors.RowScalarProduct(i, u_plus_y_sum_vector) */
+        if (mode == 0 || mode >= 3) { /* item_factors.RowScalarProduct(i, vector) */
             float dot = 0.0f;
             for (int f = 0; f < k; f++) dot += Vi[f] * vu[f];
             score += (double)dot;
@@ -265,11 +280,18 @@ void ora_asym_iterate(const ora_bmf_params* p, const int32_t* users, const int32
             for (int f = 0; f < k; f++) dot += (double)(vu[f] * vi[f]);
             score += (double)(float)dot;
         }
-        const double sig = 1.0 / (1.0 + exp(-score));
-        const double prediction = (double)p->min_rating + sig * (double)p->rating_range_size;
-        const double err = (double)values[index] - prediction;
+        double sig = 0.0, err;
         float g;
-        if (p->loss == ORA_LOSS_MAE) {
+        if (mode == 3) {
+            err = (double)values[index] - score;
+        } else {
+            sig = 1.0 / (1.0 + exp(-score));
+            err = (double)values[index] -
+                  ((double)p->min_rating + sig * (double)p->rating_range_size);
+        }
+        if (mode == 3) {
+            g = (float)err;
+        } else if (p->loss == ORA_LOSS_MAE) {
             double sgn = (err > 0) ? 1.0 : ((err < 0) ? -1.0 : 0.0);
             g = (float)(sgn * sig * (1.0 - sig) * (double)p->rating_range_size);
         } else if (p->loss == ORA_LOSS_LOGISTIC) {
@@ -287,7 +309,25 @@ void ora_asym_iterate(const ora_bmf_params* p, const int32_t* users, const int32
         if (p->update_item) bi[i] += blr * (g - (p->bias_reg * reg_i) * bi[i]);
         const double ngc_u = (double)g / norm_u, ngc_i = (double)g / norm_i;
         for (int f = 0; f < k; f++) {
-            if (mode == 0) {
+            if (mode >= 3) {
+                const float i_f = Vi[f];
+                float* pf = P + (int64_t)u * k + f;
+                if (p->update_user) {
+                    const double delta_u = mode == 3 ? err * (double)i_f - (double)(reg_u * *pf)
+                                                     : (double)(g * i_f - reg_u * *pf);
+                    *pf += (float)((double)lr * delta_u);
+                }
+                if (p->update_item) {
+                    const double delta_i = mode == 3 ? err * (double)vu[f] - (double)(reg_i * i_f)
+                                                     : (double)(g * vu[f] - reg_i * i_f);
+                    Vi[f] += (float)((double)lr * delta_i);
+                    const double common = (mode == 3 ? err / norm_u : ngc_u) * (double)i_f;
+                    for (int64_t t = off_u[u]; t < off_u[u + 1]; t++) {
+                        float* yj = Y + (int64_t)ids_u[t] * k + f;
+                        *yj += (float)((double)lr * (common - (double)(y_reg[ids_u[t]] * *yj)));
+                    }
+                }
+            } else if (mode == 0) {
                 const float i_f = Vi[f];
                 if (!p->update_item) continue;
                 const double delta_i = (double)(g * vu[f] - reg_i * i_f); /* float expression */
@@ -328,16 +368,28 @@ void ora_asym_iterate(const ora_bmf_params* p, const int32_t* users, const int32
     }
 }
 
-/* PrecomputeUserFactors (:305-331): U[u] = the user vector; users without items keep zeros */
+/* PrecomputeUserFactors (:305-331): U[u] = the user vector; users without items keep zeros.
+ * P != NULL: SVDPlusPlus.PrecomputeFactors (SVDPlusPlus.cs:230-246), (float)(sum / norm + p) */
 void ora_iafm_user_factors(const float* Y, int k, int32_t n_users, const int64_t* rated_off,
-                           const int32_t* rated_items, float* U) {
+                           const int32_t* rated_items, float* U, const float* P) {
     for (int32_t u = 0; u < n_users; u++) {
         double norm;
-        if (rated_off[u + 1] == rated_off[u]) {
-            for (int f = 0; f < k; f++) U[(int64_t)u * k + f] = 0.0f;
+        float* row = U + (int64_t)u * k;
+        const int64_t b = rated_off[u], e = rated_off[u + 1];
+        if (e == b) {
+            for (int f = 0; f < k; f++) row[f] = 0.0f;
             continue;
         }
-        ora_iafm_user_vector(Y, k, rated_off, rated_items, u, U + (int64_t)u * k, &norm);
+        if (!P) {
+            ora_iafm_user_vector(Y, k, rated_off, rated_items, u, row, &norm);
+            continue;
+        }
+        for (int f = 0; f < k; f++) row[f] = 0.0f;
+        for (int64_t t = b; t < e; t++)
+            for (int f = 0; f < k; f++) row[f] += Y[(int64_t)rated_items[t] * k + f];
+        norm = sqrt((double)(e - b));
+        for (int f = 0; f < k; f++)
+            row[f] = (float)((double)row[f] / norm + (double)P[(int64_t)u * k + f]);
     }
 }
 

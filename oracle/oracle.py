@@ -114,9 +114,9 @@ def lib():
         L.ora_asym_iterate.argtypes = [
             ctypes.c_void_p, _i32p, _i32p, _f32p, _i32p, ctypes.c_int64, _f32p, _f32p, _f32p,
             _f32p, _i32p, _i32p, _f32p, _i64p, _i32p, _f32p, _f32p, _i64p, _i32p, _f32p, _f32p,
-            _f32p, ctypes.c_int32]
+            _f32p, ctypes.c_int32, _f32p]
         L.ora_iafm_user_factors.argtypes = [_f32p, ctypes.c_int, ctypes.c_int32, _i64p, _i32p,
-                                            _f32p]
+                                            _f32p, _f32p]
         L.ora_wrmf_square.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f64p]
         L.ora_wrmf_optimize_rows.argtypes = [_i64p, _i32p, ctypes.c_int64, ctypes.c_int64,
                                              ctypes.c_int64, _f32p, _f32p, _f64p, ctypes.c_int,
@@ -438,10 +438,15 @@ def asym_train(users, items, values, n_users, n_items, min_rating, max_rating, *
         x, then U, V; V = PrecomputeItemFactors
       side="combined": SigmoidCombinedAsymmetricFactorModel (SigmoidCombinedAsymmetricFactorModel
         .cs:74-371): U, V, then x, then y (:291-306); both precomputed
+      side="svdpp" / "sigmoid_svdpp": SVDPlusPlus (SVDPlusPlus.cs:87-246) / SigmoidSVDPlusPlus
+        (SigmoidSVDPlusPlus.cs:62-173): U, V, then p, then y (:129-155); y_reg from
+        Regularization (pass reg_u = reg_i = Regularization); global_bias = Ratings.Average
+        (MatrixFactorization.Train :119-126 -- it also overwrites SigmoidSVDPlusPlus's logit);
+        U = PrecomputeFactors (y sum / norm + p)
     n_users / n_items cover the AdditionalFeedback ids.  Defaults are the models' (:56-63).
     Returns Y (y) and X (x) as they exist for the side."""
     users, items, values = i32(users), i32(items), f32(values)
-    mode = {"item": 0, "user": 1, "combined": 2}[side]
+    mode = {"item": 0, "user": 1, "combined": 2, "svdpp": 3, "sigmoid_svdpp": 4}[side]
     rng = Rng(seed)
     cnt_u = np.bincount(users, minlength=int(users.max()) + 1).astype(np.int32)
     cnt_i = np.bincount(items, minlength=int(items.max()) + 1).astype(np.int32)
@@ -475,7 +480,16 @@ def asym_train(users, items, values, n_users, n_items, min_rating, max_rating, *
     x_reg = implicit_reg(n_users, users, add_users, reg_u)
     Y = np.zeros((n_items, k), np.float32)
     X = np.zeros((n_users, k), np.float32)
-    if mode == 0:
+    P = np.zeros((n_users, k), np.float32)
+    if mode >= 3:  # SVDPlusPlus.InitModel (:129-155)
+        U, V = mf_init()
+        P = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
+        Y = rng.fill_normal(n_items * k, init_mean, init_stddev).reshape(n_items, k)
+        Y[np.flatnonzero(cnt_i == 0)] = 0
+        Y[len(cnt_i):] = 0
+        V[len(cnt_i):] = 0
+        P[len(cnt_u):] = 0
+    elif mode == 0:
         Y = implicit_init(n_items, cnt_i)
         U, V = mf_init()
     elif mode == 1:
@@ -485,13 +499,15 @@ def asym_train(users, items, values, n_users, n_items, min_rating, max_rating, *
         U, V = mf_init()
         X = implicit_init(n_users, cnt_u)
         Y = implicit_init(n_items, cnt_i)
-    init = dict(Y=Y.copy(), X=X.copy(), U=U.copy(), V=V.copy())
+    init = dict(Y=Y.copy(), X=X.copy(), U=U.copy(), V=V.copy(), P=P.copy())
     bu = np.zeros(n_users, np.float32)
     bi = np.zeros(n_items, np.float32)
     range_ = np.float32(np.float32(max_rating) - np.float32(min_rating))
     avg_f = np.float32(np.float32(ratings_average_exact(values)) / np.float32(len(values)))
     avg = np.float32(np.float32(avg_f - np.float32(min_rating)) / range_)
     gb = np.float32(math.log(float(avg) / (1.0 - float(avg))))
+    if mode >= 3:
+        gb = avg_f  # global_bias = ratings.Average (MatrixFactorization.Train)
     cu = np.zeros(n_users, np.int32)
     cu[:len(cnt_u)] = cnt_u
     ci = np.zeros(n_items, np.int32)
@@ -511,19 +527,19 @@ def asym_train(users, items, values, n_users, n_items, min_rating, max_rating, *
                            _p(cu, _i32p), _p(ci, _i32p), _p(Y, _f32p), _p(off_u, _i64p),
                            _p(ids_u, _i32p), _p(y_reg, _f32p), _p(X, _f32p), _p(off_i, _i64p),
                            _p(ids_i, _i32p), _p(x_reg, _f32p), _p(vu, _f32p), _p(vi, _f32p),
-                           mode)
+                           mode, _p(P, _f32p))
         lr = np.float32(lr * np.float32(decay))
         if callback is not None:
-            callback(epoch, dict(Y=Y, X=X, U=U, V=V, bu=bu, bi=bi))
-    if mode != 1:  # PrecomputeUserFactors
+            callback(epoch, dict(Y=Y, X=X, U=U, V=V, bu=bu, bi=bi, P=P))
+    if mode != 1:  # PrecomputeUserFactors (SVD++: + p)
         U = np.zeros((n_users, k), np.float32)
         L.ora_iafm_user_factors(_p(Y, _f32p), k, n_users, _p(off_u, _i64p), _p(ids_u, _i32p),
-                                _p(U, _f32p))
-    if mode != 0:  # PrecomputeItemFactors
+                                _p(U, _f32p), _p(P if mode >= 3 else None, _f32p))
+    if mode in (1, 2):  # PrecomputeItemFactors
         V = np.zeros((n_items, k), np.float32)
         L.ora_iafm_user_factors(_p(X, _f32p), k, n_items, _p(off_i, _i64p), _p(ids_i, _i32p),
-                                _p(V, _f32p))
-    return dict(Y=Y, X=X, U=U, V=V, bu=bu, bi=bi, init=init, global_bias=gb, range_=range_,
+                                _p(V, _f32p), None)
+    return dict(Y=Y, X=X, P=P, U=U, V=V, bu=bu, bi=bi, init=init, global_bias=gb, range_=range_,
                 random_index=random_index, rated_off=off_u, rated_items=ids_u, users_off=off_i,
                 users_ids=ids_i, y_reg=y_reg, x_reg=x_reg, current_learnrate=lr)
 

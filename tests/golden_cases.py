@@ -237,6 +237,22 @@ def case_cafm_small():
                 V=st["V"], bu=st["bu"], bi=st["bi"], **snaps)
 
 
+def case_svdpp_small(side, seed):
+    # SVDPlusPlus (SVDPlusPlus.cs:87-246) / SigmoidSVDPlusPlus (SigmoidSVDPlusPlus.cs:62-173):
+    # Regularization = 0.015 for reg_u, reg_i and y_reg
+    u, i, v, au, ai = iafm_case_data()
+    nu = max(int(u.max()), int(au.max())) + 1
+    ni = max(int(i.max()), int(ai.max())) + 1
+    snaps = {}
+    st = O.asym_train(u, i, v, nu, ni, 1.0, 5.0, side=side, seed=seed, k=5, num_iter=3,
+                      learn_rate=0.01, add_users=au, add_items=ai,
+                      callback=lambda e, m: snaps.update({f"Y{e}": m["Y"].copy(),
+                                                         f"P{e}": m["P"].copy()}))
+    return dict(init_Y=st["init"]["Y"], init_P=st["init"]["P"], init_V=st["init"]["V"],
+                Y=st["Y"], P=st["P"], U=st["U"], V=st["V"], bu=st["bu"], bi=st["bi"],
+                global_bias=np.float32(st["global_bias"]), **snaps)
+
+
 def case_bpr_user_replacement_small():
     # IterateWithReplacementUniformUser (BPRMF.cs:183-211): ~deg(u) samples per user per epoch,
     # so rounds run out and refill
@@ -288,6 +304,8 @@ CASES = {
     "iafm_small": case_iafm_small,
     "uafm_small": case_uafm_small,
     "cafm_small": case_cafm_small,
+    "svdpp_small": lambda: case_svdpp_small("svdpp", 12),
+    "sigmoid_svdpp_small": lambda: case_svdpp_small("sigmoid_svdpp", 13),
     "bpr_pair_replacement_small": case_bpr_pair_replacement_small,
     "wrmf_small": case_wrmf_small,
 }
