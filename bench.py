@@ -67,7 +67,7 @@ def main():
                     choices=["uniform_user", "uniform_pair", "user_replacement",
                              "pair_replacement"],
                     help="C3 only: BPRMF's Iterate() variant (BPRMF.cs:160-268)")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5", "svdpp"],
                     help="c2 (default; N>1 = C4 weak scaling): BiasedMF; c3: BPRMF k=128; "
                          "c5: WRMF k=256")
     args = ap.parse_args()
@@ -75,6 +75,8 @@ def main():
         return bench_bpr(args)
     if args.workload == "c5":
         return bench_wrmf(args)
+    if args.workload == "svdpp":
+        return bench_svdpp(args)
 
     world, rank, local = env_rank()
     init_host_group(world)  # gloo, host coordination only; the data path is RCCL
@@ -461,6 +463,88 @@ def cpu_baseline_wrmf(k, seconds, n_users, n_items, per_user):
             "sample": f"{rows} row solves (deg {per_user}, k={k}) of the oracle's fp64 "
                       f"WRMF.Optimize(u) = {dt * 1e3:.1f} ms/row, extrapolated to "
                       f"{n_users + n_items} rows per iteration (HH not included)"}
+
+
+def svdpp_data(n_users, n_items, n, seed=7):
+    """100-ish ratings per user, Zipf(0.8) items, planted-signal ratings (host arrays)."""
+    from mymedialite_amd.synthetic import zipf_cdf
+    rs = np.random.default_rng(seed)
+    u = rs.integers(0, n_users, n).astype(np.int32)
+    i = np.searchsorted(zipf_cdf(n_items, 0.8), rs.random(n)).clip(max=n_items - 1)
+    i = rs.permutation(n_items)[i].astype(np.int32)
+    pu = rs.normal(0, 0.5, (n_users, 4)).astype(np.float32)
+    qi = rs.normal(0, 0.5, (n_items, 4)).astype(np.float32)
+    r = 3.5 + (pu[u] * qi[i]).sum(1) + rs.normal(0, 0.5, n)
+    return u, i, np.clip(np.round(r), 1, 5).astype(np.float32)
+
+
+def bench_svdpp(args):
+    """SVDPlusPlus (SVDPlusPlus.cs:157-212) Hogwild epochs, k = 64, on 100k users x 20k items x
+    10M ratings (~100 per user).  One step = one Iterate().  A rating reads the y rows of all the
+    user's items (the sum), then rewrites them: algorithmic bytes per rating = 8k deg(u) (y read +
+    write) + 4 deg(u) (the list) + 16k (p_u, V_i read + write) + 12 (stream) + 16 (biases)."""
+    from mymedialite_amd import Random, Ratings, SVDPlusPlus
+    world, rank, local = env_rank()
+    if world != 1:
+        raise SystemExit("the SVD++ workload is a single-GPU configuration")
+    k = args.k
+    n_users, n_items = args.users or 100_000, 20_000
+    n = args.ratings or 10_000_000
+    u, i, v = svdpp_data(n_users, n_items, n)
+    Random.set_seed(1)
+    m = SVDPlusPlus(NumFactors=k, NumIter=0, LearnRate=0.001, Schedule="hogwild",
+                    Device=local)
+    m.ratings = Ratings(u, i, v)
+    t0 = time.perf_counter()
+    m.train()
+    setup_s = time.perf_counter() - t0
+    off, _ = m._feedback_lists(0)
+    deg = np.diff(off).astype(np.float64)
+    cnt = np.bincount(u, minlength=n_users).astype(np.float64)
+    total_bytes = float((cnt * (8 * k * deg + 4 * deg)).sum() + n * (16 * k + 28))
+    for _ in range(args.warmup):
+        m.iterate()
+    torch.cuda.synchronize()
+    ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m.iterate()
+        ms.append(m.last_epoch_ms())
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    avg_ms = float(np.mean(ms))
+    achieved = total_bytes / (avg_ms * 1e-3) / 1e9
+    cpu = None
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        # all the ratings of the first 3,000 users (their full item lists), one epoch, 1 thread
+        sel = u < 3000
+        ns = int(sel.sum())
+        t1 = time.perf_counter()
+        O.asym_train(u[sel], i[sel], v[sel], 3000, n_items, 1.0, 5.0, side="svdpp", seed=1,
+                     k=k, num_iter=1, learn_rate=0.001)
+        dt = time.perf_counter() - t1
+        cpu = {"value": ns / dt, "unit": "rating-updates/s", "cores": 1, "kind": "port",
+               "sample": f"SVDPlusPlus.Train with 1 iteration on the {ns} ratings of the first "
+                         f"3000 users of the same stream (full item lists), k={k}, oracle C "
+                         f"restatement of SVDPlusPlus.cs:157-212, {dt:.1f} s incl. init"}
+    line = {
+        "metric": "SVD++ rating-updates/sec, SVDPlusPlus k=64 Hogwild", "value": n * args.steps /
+        elapsed, "unit": "rating-updates/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (planted rank-4 model, Zipf(0.8) items; host-generated)",
+        "config": {"workload": f"SVDPlusPlus {n_users} users x {n_items} items, {n} ratings",
+                   "num_factors": k, "mean_items_per_user": float(deg.mean()),
+                   "setup_s": setup_s},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "asym_sgd_kernel<RMSE,1,kSvdpp>", "kernel_avg_ms": avg_ms,
+                     "bytes_per_epoch": total_bytes},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
 
 
 def cpu_baseline_bpr(k, seconds):

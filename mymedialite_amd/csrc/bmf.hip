@@ -862,20 +862,44 @@ struct AsymSlot {
 
 // the represented vector of row `key`: SumOfRows (DataType/MatrixExtensions.cs:125-135: float,
 // list order), / sqrt(count) in double, cast to float (e.g. :104-107, PrecomputeUserFactors)
+// The list is read 64 ids at a time (one coalesced load, then v_readlane per id) and its rows
+// kAsymBatch at a time, so kAsymBatch row loads are in flight before the in-order adds.
+constexpr int kAsymBatch = 8;
+
+template <int KM>
+__device__ __forceinline__ void asym_sum(const AsymSlot& sl, int32_t k, int32_t ld, int64_t b,
+                                         int64_t e, int lane, float (&vec)[KM]) {
+#pragma unroll
+    for (int m = 0; m < KM; ++m) vec[m] = 0.0f;
+    for (int64_t base = b; base < e; base += 64) {
+        const int cnt = (int)min((int64_t)64, e - base);
+        const int32_t my_id = lane < cnt ? sl.ids[base + lane] : 0;
+        for (int t = 0; t < cnt; t += kAsymBatch) {
+            float v[kAsymBatch][KM];
+#pragma unroll
+            for (int q = 0; q < kAsymBatch; ++q) {
+                const int32_t j = __builtin_amdgcn_readlane(my_id, min(t + q, cnt - 1));
+                const float* row = sl.X + (int64_t)j * ld;
+#pragma unroll
+                for (int m = 0; m < KM; ++m) {
+                    const int f = lane + 64 * m;
+                    v[q][m] = (t + q < cnt && f < k) ? row[f] : 0.0f;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kAsymBatch; ++q)
+                if (t + q < cnt)
+#pragma unroll
+                    for (int m = 0; m < KM; ++m) vec[m] += v[q][m];  // list order
+        }
+    }
+}
+
 template <int KM>
 __device__ __forceinline__ double asym_vector(const AsymSlot& sl, int32_t k, int32_t ld,
                                               int32_t key, int lane, float (&vec)[KM]) {
     const int64_t b = sl.off[key], e = sl.off[key + 1];
-#pragma unroll
-    for (int m = 0; m < KM; ++m) vec[m] = 0.0f;
-    for (int64_t t = b; t < e; ++t) {
-        const float* row = sl.X + (int64_t)sl.ids[t] * ld;
-#pragma unroll
-        for (int m = 0; m < KM; ++m) {
-            const int f = lane + 64 * m;
-            vec[m] += f < k ? row[f] : 0.0f;
-        }
-    }
+    asym_sum<KM>(sl, k, ld, b, e, lane, vec);
     const double norm = sqrt((double)(e - b));
 #pragma unroll
     for (int m = 0; m < KM; ++m) vec[m] = (float)((double)vec[m] / norm);
@@ -888,16 +912,35 @@ __device__ __forceinline__ void asym_list_step(const AsymSlot& sl, int32_t k, in
                                                int32_t key, int lane, float lr,
                                                const double (&common)[KM]) {
     const int64_t b = sl.off[key], e = sl.off[key + 1];
-    for (int64_t t = b; t < e; ++t) {
-        const int32_t j = sl.ids[t];
-        const float rg = sl.reg[j];
-        float* row = sl.X + (int64_t)j * ld;
+    for (int64_t base = b; base < e; base += 64) {
+        const int cnt = (int)min((int64_t)64, e - base);
+        const int32_t my_id = lane < cnt ? sl.ids[base + lane] : 0;
+        for (int t = 0; t < cnt; t += kAsymBatch) {
+            float y[kAsymBatch][KM], rg[kAsymBatch];
+            int32_t j[kAsymBatch];
 #pragma unroll
-        for (int m = 0; m < KM; ++m) {
-            const int f = lane + 64 * m;
-            if (f < k) {
-                const float y = row[f];
-                row[f] = y + (float)((double)lr * (common[m] - (double)(rg * y)));
+            for (int q = 0; q < kAsymBatch; ++q) {
+                j[q] = __builtin_amdgcn_readlane(my_id, min(t + q, cnt - 1));
+                rg[q] = sl.reg[j[q]];
+                const float* row = sl.X + (int64_t)j[q] * ld;
+#pragma unroll
+                for (int m = 0; m < KM; ++m) {
+                    const int f = lane + 64 * m;
+                    y[q][m] = (t + q < cnt && f < k) ? row[f] : 0.0f;
+                }
+            }
+            // the ids of a list are distinct, so the rows of a batch never alias
+#pragma unroll
+            for (int q = 0; q < kAsymBatch; ++q) {
+                if (t + q >= cnt) continue;
+                float* row = sl.X + (int64_t)j[q] * ld;
+#pragma unroll
+                for (int m = 0; m < KM; ++m) {
+                    const int f = lane + 64 * m;
+                    if (f < k)
+                        row[f] = y[q][m] +
+                                 (float)((double)lr * (common[m] - (double)(rg[q] * y[q][m])));
+                }
             }
         }
     }
@@ -925,16 +968,7 @@ __global__ __launch_bounds__(64) void asym_sgd_kernel(
             // p_plus_y_sum_vector[f] = (float)(y_sum[f] / norm + p[u, f]) (SVDPlusPlus.cs:166-170)
             float* Pu = P + (int64_t)u * ld;
             const int64_t b = s0.off[u], e = s0.off[u + 1];
-#pragma unroll
-            for (int m = 0; m < KM; ++m) a[m] = 0.0f;
-            for (int64_t t = b; t < e; ++t) {
-                const float* row = s0.X + (int64_t)s0.ids[t] * ld;
-#pragma unroll
-                for (int m = 0; m < KM; ++m) {
-                    const int f = lane + 64 * m;
-                    a[m] += f < k ? row[f] : 0.0f;
-                }
-            }
+            asym_sum<KM>(s0, k, ld, b, e, lane, a);
             norm_u = sqrt((double)(e - b));
 #pragma unroll
             for (int m = 0; m < KM; ++m) {
@@ -1049,16 +1083,7 @@ __global__ __launch_bounds__(64) void asym_precompute_kernel(AsymSlot sl, int32_
         float vec[KM];
         if (sl.off[r + 1] > sl.off[r] && P) {
             const int64_t b = sl.off[r], e = sl.off[r + 1];
-#pragma unroll
-            for (int m = 0; m < KM; ++m) vec[m] = 0.0f;
-            for (int64_t t = b; t < e; ++t) {
-                const float* row = sl.X + (int64_t)sl.ids[t] * ld;
-#pragma unroll
-                for (int m = 0; m < KM; ++m) {
-                    const int f = lane + 64 * m;
-                    vec[m] += f < k ? row[f] : 0.0f;
-                }
-            }
+            asym_sum<KM>(sl, k, ld, b, e, lane, vec);
             const double norm = sqrt((double)(e - b));
 #pragma unroll
             for (int m = 0; m < KM; ++m) {
@@ -1416,11 +1441,15 @@ void asym_epoch(mml_bmf* h, const BmfScalars& s) {
     const int64_t n = h->n;
     hipStream_t st = h->ctx->stream;
     if (n > 0) {
-        // ORDERED: one wavefront, the whole stream in order.  HOGWILD: a wavefront per >= 2,048
-        // ratings (a rating reads and writes whole lists of implicit rows), at most 256 CUs x 8
+        // ORDERED: one wavefront, the whole stream in order.  HOGWILD: a wavefront per >= 1,024
+        // ratings (a rating reads and writes whole lists of implicit rows), at most 256 CUs x 32
+        static const int64_t cap = [] {
+            const char* e = std::getenv("MML_ASYM_WAVES");
+            return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)256 * 32;
+        }();
         int64_t waves = 1;
         if (h->p.schedule != MML_SCHEDULE_ORDERED)
-            waves = std::min<int64_t>(256 * 8, std::max<int64_t>(1, n / 2048));
+            waves = std::min<int64_t>(cap, std::max<int64_t>(1, n / 1024));
         const int64_t chunk = (n + waves - 1) / waves;
         const int km = (h->k + 63) / 64;
         const AsymSlot s0 = asym_slot(h, 0), s1 = asym_slot(h, 1);
