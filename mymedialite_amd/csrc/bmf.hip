@@ -866,11 +866,10 @@ struct AsymSlot {
 // kAsymBatch at a time, so kAsymBatch row loads are in flight before the in-order adds.
 constexpr int kAsymBatch = 8;
 
+// adds rows [b, e) of the list onto vec, in list order
 template <int KM>
-__device__ __forceinline__ void asym_sum(const AsymSlot& sl, int32_t k, int32_t ld, int64_t b,
-                                         int64_t e, int lane, float (&vec)[KM]) {
-#pragma unroll
-    for (int m = 0; m < KM; ++m) vec[m] = 0.0f;
+__device__ __forceinline__ void asym_sum_add(const AsymSlot& sl, int32_t k, int32_t ld, int64_t b,
+                                             int64_t e, int lane, float (&vec)[KM]) {
     for (int64_t base = b; base < e; base += 64) {
         const int cnt = (int)min((int64_t)64, e - base);
         const int32_t my_id = lane < cnt ? sl.ids[base + lane] : 0;
@@ -896,6 +895,14 @@ __device__ __forceinline__ void asym_sum(const AsymSlot& sl, int32_t k, int32_t 
 }
 
 template <int KM>
+__device__ __forceinline__ void asym_sum(const AsymSlot& sl, int32_t k, int32_t ld, int64_t b,
+                                         int64_t e, int lane, float (&vec)[KM]) {
+#pragma unroll
+    for (int m = 0; m < KM; ++m) vec[m] = 0.0f;
+    asym_sum_add<KM>(sl, k, ld, b, e, lane, vec);
+}
+
+template <int KM>
 __device__ __forceinline__ double asym_vector(const AsymSlot& sl, int32_t k, int32_t ld,
                                               int32_t key, int lane, float (&vec)[KM]) {
     const int64_t b = sl.off[key], e = sl.off[key + 1];
@@ -908,10 +915,9 @@ __device__ __forceinline__ double asym_vector(const AsymSlot& sl, int32_t k, int
 
 // x.Inc / y.Inc over the list of `key`: X[t, f] += (float)(lr * (common_f - reg[t] * X[t, f]))
 template <int KM>
-__device__ __forceinline__ void asym_list_step(const AsymSlot& sl, int32_t k, int32_t ld,
-                                               int32_t key, int lane, float lr,
-                                               const double (&common)[KM]) {
-    const int64_t b = sl.off[key], e = sl.off[key + 1];
+__device__ __forceinline__ void asym_list_step_range(const AsymSlot& sl, int32_t k, int32_t ld,
+                                                     int64_t b, int64_t e, int lane, float lr,
+                                                     const double (&common)[KM]) {
     for (int64_t base = b; base < e; base += 64) {
         const int cnt = (int)min((int64_t)64, e - base);
         const int32_t my_id = lane < cnt ? sl.ids[base + lane] : 0;
@@ -946,13 +952,90 @@ __device__ __forceinline__ void asym_list_step(const AsymSlot& sl, int32_t k, in
     }
 }
 
-template <int LOSS, int KM, int MODE>
+template <int KM>
+__device__ __forceinline__ void asym_list_step(const AsymSlot& sl, int32_t k, int32_t ld,
+                                               int32_t key, int lane, float lr,
+                                               const double (&common)[KM]) {
+    asym_list_step_range<KM>(sl, k, ld, sl.off[key], sl.off[key + 1], lane, lr, common);
+}
+
+// k <= 64: the first C rows of a rating's list stay in registers (one float per lane and row)
+// from the sum to the step.  Between the two passes a rating writes only its trained row, p and
+// the biases, never a row of its own list, so the step's y is exactly the value the sum read
+// (ORDERED stays bit-faithful) and the step issues no loads for those rows.  All C row loads are
+// issued before the in-order adds.  Rows past C are read and re-read as before.
+template <int C>
+struct AsymRowCache {
+    float row[C];
+    int32_t id;    // lane l: the list's l-th id (l < cnt)
+    float reg;     // lane l: reg[id]
+    int cnt;       // rows held (wave-uniform)
+    int64_t b, e;  // the list
+};
+
+template <int C>
+__device__ __forceinline__ void asym_sum_cached(const AsymSlot& sl, int32_t k, int32_t ld,
+                                                int64_t b, int64_t e, int lane, float& acc,
+                                                AsymRowCache<C>& rc) {
+    static_assert(C % kAsymBatch == 0 && C <= 64, "cache rows");
+    const int cnt = (int)min((int64_t)C, e - b);
+    rc.cnt = cnt;
+    rc.b = b;
+    rc.e = e;
+    rc.id = lane < cnt ? sl.ids[b + lane] : 0;
+    rc.reg = lane < cnt ? sl.reg[rc.id] : 0.0f;
+    const bool act = lane < k;
+#pragma unroll
+    for (int t = 0; t < C; t += kAsymBatch)
+        if (t < cnt)
+#pragma unroll
+            for (int q = 0; q < kAsymBatch; ++q) {
+                const int32_t j = __builtin_amdgcn_readlane(rc.id, min(t + q, cnt - 1));
+                rc.row[t + q] = (t + q < cnt && act) ? sl.X[(int64_t)j * ld + lane] : 0.0f;
+            }
+    float vec[1] = {0.0f};
+#pragma unroll
+    for (int t = 0; t < C; t += kAsymBatch)
+        if (t < cnt)
+#pragma unroll
+            for (int q = 0; q < kAsymBatch; ++q)
+                if (t + q < cnt) vec[0] += rc.row[t + q];  // list order
+    asym_sum_add<1>(sl, k, ld, b + cnt, e, lane, vec);
+    acc = vec[0];
+}
+
+template <int C>
+__device__ __forceinline__ void asym_list_step_cached(const AsymSlot& sl, int32_t k, int32_t ld,
+                                                      int lane, float lr,
+                                                      const double (&common)[1],
+                                                      const AsymRowCache<C>& rc) {
+    const int cnt = rc.cnt;
+    const bool act = lane < k;
+#pragma unroll
+    for (int t = 0; t < C; t += kAsymBatch)
+        if (t < cnt)
+#pragma unroll
+            for (int q = 0; q < kAsymBatch; ++q)
+                if (t + q < cnt) {
+                    const int32_t j = __builtin_amdgcn_readlane(rc.id, t + q);
+                    const float rg =
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rc.reg), t + q));
+                    const float y = rc.row[t + q];
+                    if (act)
+                        sl.X[(int64_t)j * ld + lane] =
+                            y + (float)((double)lr * (common[0] - (double)(rg * y)));
+                }
+    asym_list_step_range<1>(sl, k, ld, rc.b + cnt, rc.e, lane, lr, common);
+}
+
+template <int LOSS, int KM, int MODE, int CACHE>
 __global__ __launch_bounds__(64) void asym_sgd_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
     int64_t n, int64_t chunk, AsymSlot s0, AsymSlot s1, float* U, float* V, float* bu, float* bi,
     int32_t k, int32_t ld, BmfScalars s, const int32_t* __restrict__ cnt_u,
     const int32_t* __restrict__ cnt_i, float* P) {
     constexpr bool svdpp = MODE == kSvdpp || MODE == kSigmoidSvdpp;
+    constexpr bool kCached = CACHE > 0 && KM == 1 && MODE != kAsymUser;  // slot 0's rows
     const int lane = threadIdx.x;
     const int64_t begin = (int64_t)blockIdx.x * chunk;
     const int64_t end = min(begin + chunk, n);
@@ -964,11 +1047,14 @@ __global__ __launch_bounds__(64) void asym_sgd_kernel(
         double norm_u = 1.0, norm_i = 1.0;
         float* trained = nullptr;  // kAsymItem: V_i, kAsymUser: U_u
         float pu[KM];  // svdpp: p_u
+        AsymRowCache<kCached ? CACHE : kAsymBatch> rc;  // kCached: the list's first rows
+        (void)rc;
         if constexpr (svdpp) {
             // p_plus_y_sum_vector[f] = (float)(y_sum[f] / norm + p[u, f]) (SVDPlusPlus.cs:166-170)
             float* Pu = P + (int64_t)u * ld;
             const int64_t b = s0.off[u], e = s0.off[u + 1];
-            asym_sum<KM>(s0, k, ld, b, e, lane, a);
+            if constexpr (kCached) asym_sum_cached<CACHE>(s0, k, ld, b, e, lane, a[0], rc);
+            else asym_sum<KM>(s0, k, ld, b, e, lane, a);
             norm_u = sqrt((double)(e - b));
 #pragma unroll
             for (int m = 0; m < KM; ++m) {
@@ -976,6 +1062,11 @@ __global__ __launch_bounds__(64) void asym_sgd_kernel(
                 pu[m] = f < k ? Pu[f] : 0.0f;
                 a[m] = (float)((double)a[m] / norm_u + (double)pu[m]);
             }
+        } else if constexpr (kCached) {  // asym_vector through the row cache
+            const int64_t b = s0.off[u], e = s0.off[u + 1];
+            asym_sum_cached<CACHE>(s0, k, ld, b, e, lane, a[0], rc);
+            norm_u = sqrt((double)(e - b));
+            a[0] = (float)((double)a[0] / norm_u);
         } else if constexpr (MODE != kAsymUser) {
             norm_u = asym_vector<KM>(s0, k, ld, u, lane, a);
         }
@@ -1066,7 +1157,8 @@ __global__ __launch_bounds__(64) void asym_sgd_kernel(
         }
         if constexpr (MODE == kAsymUser || MODE == kAsymCombined)
             asym_list_step<KM>(s1, k, ld, i, lane, s.lr, ci);
-        if constexpr (MODE != kAsymUser) asym_list_step<KM>(s0, k, ld, u, lane, s.lr, cu);
+        if constexpr (kCached) asym_list_step_cached<CACHE>(s0, k, ld, lane, s.lr, cu, rc);
+        else if constexpr (MODE != kAsymUser) asym_list_step<KM>(s0, k, ld, u, lane, s.lr, cu);
     }
 }
 
@@ -1434,6 +1526,13 @@ void asym_precompute(mml_bmf* h) {
     }
 }
 
+// MML_ASYM_CACHE: rows of a list kept in registers from the sum to the step at k <= 64 (0 / 32 /
+// 64, default 64); read per epoch so a test can switch it
+static int asym_cache_rows() {
+    const char* e = std::getenv("MML_ASYM_CACHE");
+    return e ? std::atoi(e) : 64;
+}
+
 template <int LOSS>
 void asym_epoch(mml_bmf* h, const BmfScalars& s) {
     const int32_t* cu = h->p.frequency_regularization ? h->cnt_u.get() : nullptr;
@@ -1453,16 +1552,23 @@ void asym_epoch(mml_bmf* h, const BmfScalars& s) {
         const int64_t chunk = (n + waves - 1) / waves;
         const int km = (h->k + 63) / 64;
         const AsymSlot s0 = asym_slot(h, 0), s1 = asym_slot(h, 1);
-#define MML_ASYM(KM, MODE)                                                                     \
-    asym_sgd_kernel<LOSS, KM, MODE><<<(int)waves, 64, 0, st>>>(                                \
+        const int cache_rows = asym_cache_rows();
+#define MML_ASYM_KM1(MODE)                                        \
+    do {                                                          \
+        if (cache_rows >= 64) MML_ASYM(1, MODE, 64);              \
+        else if (cache_rows >= 32) MML_ASYM(1, MODE, 32);         \
+        else MML_ASYM(1, MODE, 0);                                \
+    } while (0)
+#define MML_ASYM(KM, MODE, C)                                                                     \
+    asym_sgd_kernel<LOSS, KM, MODE, C><<<(int)waves, 64, 0, st>>>(                                \
         h->su.get(), h->si.get(), h->sr.get(), n, chunk, s0, s1, h->U.get(), h->V.get(),       \
         h->bu.get(), h->bi.get(), h->k, h->ld, s, cu, ci, h->P.get())
 #define MML_ASYM_K(MODE)                    \
     switch (km) {                           \
-        case 1: MML_ASYM(1, MODE); break;   \
-        case 2: MML_ASYM(2, MODE); break;   \
-        case 3: MML_ASYM(3, MODE); break;   \
-        default: MML_ASYM(4, MODE); break;  \
+        case 1: MML_ASYM_KM1(MODE); break;   \
+        case 2: MML_ASYM(2, MODE, 0); break;   \
+        case 3: MML_ASYM(3, MODE, 0); break;   \
+        default: MML_ASYM(4, MODE, 0); break;  \
     }
         switch (asym_mode(h)) {
             case kAsymItem: MML_ASYM_K(kAsymItem); break;
@@ -1472,6 +1578,7 @@ void asym_epoch(mml_bmf* h, const BmfScalars& s) {
             default: MML_ASYM_K(kAsymCombined); break;
         }
 #undef MML_ASYM_K
+#undef MML_ASYM_KM1
 #undef MML_ASYM
         MML_HIP(hipGetLastError());
     }

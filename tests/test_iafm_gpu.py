@@ -193,3 +193,33 @@ def test_hogwild_statistical_parity(side):
     # through the bias steps, which Hogwild's concurrent waves partly lose on hot items: measured
     # +0.12 on this noise-only set (ORDERED is exact and the default)
     assert abs(rmse_gpu - rmse_ref) <= (0.15 if side == "sigmoid_svdpp" else 0.02)
+
+
+@pytest.mark.parametrize("cache", ["0", "32", "64"])
+@pytest.mark.parametrize("side", ["item", "combined", "svdpp", "sigmoid_svdpp"])
+def test_ordered_long_lists_row_cache(side, cache, monkeypatch):
+    """k <= 64 keeps the first MML_ASYM_CACHE rows of a rating's list in registers from the sum to
+    the step and re-reads the rest: with lists of well over 128 items (past the cache and past
+    one 64-id load) ORDERED still equals the oracle."""
+    monkeypatch.setenv("MML_ASYM_CACHE", cache)
+    rs = np.random.default_rng(48)
+    n_users, n_items, n = 20, 300, 4000
+    u = rs.integers(0, n_users, n).astype(np.int32)
+    i = rs.integers(0, n_items, n).astype(np.int32)
+    v = rs.integers(1, 6, n).astype(np.float32)
+    u[0], i[0] = n_users - 1, n_items - 1
+    longest = max(len(np.unique(i[u == x])) for x in range(n_users))
+    assert longest > 128
+    st = O.asym_train(u, i, v, n_users, n_items, 1.0, 5.0, side=side, seed=5, k=48, num_iter=2,
+                      learn_rate=0.01)
+    Random.set_seed(5)
+    m = _model(u, i, v, None, None, side=side, NumFactors=48, NumIter=2, LearnRate=0.01)
+    m.train()
+    got = [(m._implicit_factors(sd), st["X" if sd else "Y"]) for sd in m.SIDES]
+    got += [(m.item_factors, st["V"]), (m.user_factors, st["U"]), (m.user_bias, st["bu"]),
+            (m.item_bias, st["bi"])]
+    if side in ("svdpp", "sigmoid_svdpp"):
+        got.append((m.p, st["P"]))
+    d = max(float(np.abs(a - b).max()) for a, b in got)
+    print(f"{side} long lists, MML_ASYM_CACHE={cache}: max |d| {d:.3g} (longest list {longest})")
+    assert d <= 1e-5
