@@ -529,6 +529,17 @@ def bench_svdpp(args):
                "sample": f"SVDPlusPlus.Train with 1 iteration on the {ns} ratings of the first "
                          f"3000 users of the same stream (full item lists), k={k}, oracle C "
                          f"restatement of SVDPlusPlus.cs:157-212, {dt:.1f} s incl. init"}
+    # PMC FETCH_SIZE / WRITE_SIZE of this kernel at this workload (scripts/gpu_pmc_svdpp.sh)
+    traffic, traffic_note = None, None
+    tf = os.path.join(ROOT, "profiles", "svdpp_traffic.json")
+    if os.path.exists(tf) and k == 64 and n == 10_000_000:
+        t = json.load(open(tf))
+        traffic = t["traffic_bytes_per_launch"] / (avg_ms * 1e-3) / 1e9
+        traffic_note = (f"{t['traffic_bytes_per_launch'] / 1e9:.1f} GB per launch at L2 <-> "
+                        f"fabric (PMC, calibrated: {tf[len(ROOT) + 1:]}) vs "
+                        f"{total_bytes / 1e9:.1f} GB algorithmic; y ({n_items} x {k} floats) "
+                        f"stays in L2 / the Infinity Cache, so most algorithmic bytes are cache "
+                        f"hits and frac is not an HBM utilisation")
     line = {
         "metric": "SVD++ rating-updates/sec, SVDPlusPlus k=64 Hogwild", "value": n * args.steps /
         elapsed, "unit": "rating-updates/s", "n_gpus": 1, "steps": args.steps,
@@ -539,7 +550,8 @@ def bench_svdpp(args):
                    "num_factors": k, "mean_items_per_user": float(deg.mean()),
                    "setup_s": setup_s},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_note": traffic_note,
                      "kernel": "asym_sgd_kernel<RMSE,1,kSvdpp>", "kernel_avg_ms": avg_ms,
                      "bytes_per_epoch": total_bytes},
         "cpu_baseline": cpu,
