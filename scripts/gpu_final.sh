@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round-end rehearsal on freshly built libraries: the full GPU suite, smoke(), the default bench
+# line (C2) and rocprofv3 kernel stats of it. Each GPU step has its own time limit; the first
+# failure ends the call.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${1:-r1f}
+step() {  # step <name> <seconds> <command...>
+    local name=$1 secs=$2
+    shift 2
+    timeout -k 10 "$secs" "$@" > "gpurun_out/${name}_$TAG.log" 2>&1
+    local rc=$?
+    echo "$name rc=$rc"
+    tail -2 "gpurun_out/${name}_$TAG.log"
+    [ $rc -eq 0 ] || exit $rc
+}
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()'
+step bench_c2 600 python bench.py
+step prof_c2 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c2_$TAG -o c2 -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline
