@@ -1029,15 +1029,17 @@ __device__ __forceinline__ void asym_list_step_cached(const AsymSlot& sl, int32_
 }
 
 template <int LOSS, int KM, int MODE, int CACHE>
-__global__ __launch_bounds__(64) void asym_sgd_kernel(
+__global__ __launch_bounds__(256) void asym_sgd_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
     int64_t n, int64_t chunk, AsymSlot s0, AsymSlot s1, float* U, float* V, float* bu, float* bi,
     int32_t k, int32_t ld, BmfScalars s, const int32_t* __restrict__ cnt_u,
     const int32_t* __restrict__ cnt_i, float* P) {
     constexpr bool svdpp = MODE == kSvdpp || MODE == kSigmoidSvdpp;
     constexpr bool kCached = CACHE > 0 && KM == 1 && MODE != kAsymUser;  // slot 0's rows
-    const int lane = threadIdx.x;
-    const int64_t begin = (int64_t)blockIdx.x * chunk;
+    // one wavefront per chunk; a workgroup is 1 wave (large sets) or 4 waves on one CU (small sets)
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t begin = wave * chunk;
     const int64_t end = min(begin + chunk, n);
     for (int64_t x = begin; x < end; ++x) {
         const int32_t u = su[x], i = si[x];
@@ -1549,7 +1551,18 @@ void asym_epoch(mml_bmf* h, const BmfScalars& s) {
         int64_t waves = 1;
         if (h->p.schedule != MML_SCHEDULE_ORDERED)
             waves = std::min<int64_t>(cap, std::max<int64_t>(1, n / 1024));
+        // launch_hogwild's small-set rule: a set of fewer than 64 waves' worth of work (65,536
+        // ratings) runs as ONE workgroup of 4 waves, so every row stays in one CU's L1 and one
+        // XCD's L2 (spread over XCDs, their private write-back L2s replicate the hot rows and lose
+        // updates: sigmoid SVD++ on 20 k ratings measured +0.12..0.15 RMSE with 19 one-wave
+        // workgroups)
+        int wg = 64;
+        if (waves > 1 && waves < 64) {
+            waves = 4;
+            wg = 256;
+        }
         const int64_t chunk = (n + waves - 1) / waves;
+        const int64_t blocks = waves / (wg / 64);
         const int km = (h->k + 63) / 64;
         const AsymSlot s0 = asym_slot(h, 0), s1 = asym_slot(h, 1);
         const int cache_rows = asym_cache_rows();
@@ -1560,7 +1573,7 @@ void asym_epoch(mml_bmf* h, const BmfScalars& s) {
         else MML_ASYM(1, MODE, 0);                                \
     } while (0)
 #define MML_ASYM(KM, MODE, C)                                                                     \
-    asym_sgd_kernel<LOSS, KM, MODE, C><<<(int)waves, 64, 0, st>>>(                                \
+    asym_sgd_kernel<LOSS, KM, MODE, C><<<(int)blocks, wg, 0, st>>>(                                \
         h->su.get(), h->si.get(), h->sr.get(), n, chunk, s0, s1, h->U.get(), h->V.get(),       \
         h->bu.get(), h->bi.get(), h->k, h->ld, s, cu, ci, h->P.get())
 #define MML_ASYM_K(MODE)                    \

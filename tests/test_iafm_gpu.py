@@ -8,7 +8,7 @@ SIGMOID_SVDPP).
   losses RMSE / MAE / LogisticLoss, frequency regularisation, k = 5 / 64 / 130).
 * Predict and Eval.Ratings RMSE from the GPU model equal the oracle's formula.
 * HOGWILD: many wavefronts, statistical parity -- test RMSE after 3 epochs within 0.02 of the
-  sequential oracle's on a 20,000-rating set (SigmoidSVDPlusPlus: 0.15, see the test).
+  sequential oracle's on a 20,000-rating set.
 """
 import numpy as np
 import pytest
@@ -188,11 +188,11 @@ def test_hogwild_statistical_parity(side):
     m.train()
     rmse_gpu = m.evaluate(Ratings(tu, ti, tv))["RMSE"]
     print(f"{side} asym hogwild: test RMSE gpu {rmse_gpu:.5f} oracle {rmse_ref:.5f}")
-    # SigmoidSVDPlusPlus keeps the reference's global bias quirk (the Average, not the logit:
-    # MatrixFactorization.Train overwrites it), so its sigmoid starts saturated and learning runs
-    # through the bias steps, which Hogwild's concurrent waves partly lose on hot items: measured
-    # +0.12 on this noise-only set (ORDERED is exact and the default)
-    assert abs(rmse_gpu - rmse_ref) <= (0.15 if side == "sigmoid_svdpp" else 0.02)
+    # 20,000 ratings is under the asym small-set rule (65,536), so the Hogwild waves share one CU
+    # and one XCD's L2; spread over 19 one-wave workgroups on several XCDs, the per-XCD write-back
+    # L2s lost updates of the hot rows and biases (SigmoidSVDPlusPlus, whose saturated sigmoid
+    # learns through the bias steps, measured +0.12..0.15 that way)
+    assert abs(rmse_gpu - rmse_ref) <= 0.02
 
 
 @pytest.mark.parametrize("cache", ["0", "32", "64"])
