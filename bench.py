@@ -9,10 +9,10 @@ RCCL all-reduce of item factors and item biases (model averaging, SURVEY.md 8(e)
 
 Workloads (BASELINE.json configs, synthetic data generated in HBM, inputs resident before timing):
   N = 1 : C2 -- 1M users x 100k items, 100M ratings, k = 64 fp32.
-  N > 1 : C4 weak scaling -- per GPU a user shard of 1.25M users and 125M ratings over the shared
-          100k items (N = 8 is C4: 10M users, 1B ratings).
+  N > 1 : C4 strong scaling -- 1B ratings, 10M users x 100k items, user shards of equal rating
+          count (the same data set at every N; --workload c4 runs its N = 1 point).
 The line carries the roofline of the SGD kernel (algorithmic bytes 16k+28 per update)
-and the CPU oracle's single-thread Iterate() on a bounded sample (rank 0, N = 1 only).
+and the CPU oracle's Iterate() and MaxThreads = T DSGD, one full epoch each (rank 0, N = 1 only).
 """
 from __future__ import annotations
 
@@ -67,36 +67,37 @@ def main():
                     choices=["uniform_user", "uniform_pair", "user_replacement",
                              "pair_replacement"],
                     help="C3 only: BPRMF's Iterate() variant (BPRMF.cs:160-268)")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5", "svdpp"],
-                    help="c2 (default; N>1 = C4 weak scaling): BiasedMF; c3: BPRMF k=128; "
+    ap.add_argument("--workload", default=None, choices=["c2", "c3", "c4", "c5", "svdpp"],
+                    help="default: c2 at N = 1, c4 at N > 1 (BiasedMF k=64); c3: BPRMF k=128 "
+                         "(N > 1: user shards); c4: BiasedMF 1B ratings, strong scaling; "
                          "c5: WRMF k=256")
     args = ap.parse_args()
-    if args.workload == "c3":
+    world = env_rank()[0]
+    workload = args.workload or ("c2" if world == 1 else "c4")
+    if workload == "c3":
         return bench_bpr(args)
-    if args.workload == "c5":
+    if workload == "c4":
+        return bench_c4(args)
+    if workload == "c5":
         return bench_wrmf(args)
-    if args.workload == "svdpp":
+    if workload == "svdpp":
         return bench_svdpp(args)
+    if world > 1:
+        raise SystemExit("C2 is the single-GPU configuration; N > 1 runs C4 (--workload c4)")
+    return bench_c2(args)
 
-    world, rank, local = env_rank()
-    init_host_group(world)  # gloo, host coordination only; the data path is RCCL
+
+def bench_c2(args):
+    """C2: 1M users x 100k items, 100M ratings, BiasedMF k=64, Hogwild SGD, one GPU."""
+    world, rank, local = 1, 0, env_rank()[2]
     k = args.k
-    if world == 1:
-        n_local = args.ratings or 100_000_000
-        users_local = args.users or 1_000_000
-        workload = "C2: 1M users x 100k items, 100M ratings, BiasedMF k=64, Hogwild SGD"
-    else:
-        n_local = args.ratings or 125_000_000
-        users_local = args.users or 1_250_000
-        workload = (f"C4 weak scaling: per GPU {users_local} users / {n_local} ratings, "
-                    f"{args.items} shared items, BiasedMF k=64, per-epoch RCCL all-reduce")
-    n_users_total = users_local * world
+    n_local = args.ratings or 100_000_000
+    users_local = args.users or 1_000_000
+    workload = "C2: 1M users x 100k items, 100M ratings, BiasedMF k=64, Hogwild SGD"
+    n_users_total = users_local
     n_items = args.items
 
     ctx = N.Context(local)
-    if world > 1:
-        ctx.comm_init(share_unique_id(rank, N.Context.unique_id), world, rank)
-
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     lo = rank * users_local
@@ -128,10 +129,10 @@ def main():
                                             values.data_ptr(), n_local, None))
     N.check(N.lib().mml_bmf_set_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
                                       N.ptr(bu, N._f32p), N.ptr(bi, N._f32p), gb, 1.0, 5.0))
-    # bounded host sample of the same workload for the CPU baseline (rank 0, N = 1)
-    n_cpu = min(n_local, 40_000_000)
-    cpu_sample = (users[:n_cpu].cpu().numpy(), items[:n_cpu].cpu().numpy(),
-                  values[:n_cpu].cpu().numpy()) if (rank == 0 and world == 1) else None
+    # the same workload on the host for the CPU baseline: the whole stream (one full epoch each
+    # leg)
+    cpu_sample = None if args.no_cpu_baseline else (
+        users.cpu().numpy(), items.cpu().numpy(), values.cpu().numpy())
     del users, items, values
     tus, tis, tvs = tu.cpu().numpy(), ti.cpu().numpy(), tv.cpu().numpy()
     lr = 0.01
@@ -228,13 +229,23 @@ def cpu_threads() -> int:
     return max(1, min(16, n))
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(h, k, n_users, n_items, gb, seconds, sample):
-    """The oracle (C restatement of BiasedMatrixFactorization.cs:264-310) on a bounded sample of
-    the same workload -- a prefix of the very ratings stream the GPU trains on, applied to the GPU
-    model's current state:
+    """The oracle (C restatement of BiasedMatrixFactorization.cs:264-310) on the same workload --
+    the very ratings stream the GPU trains on, applied to the GPU model's current state, one FULL
+    epoch per leg:
       * value: the reference's own multi-core schedule, MaxThreads = T DSGD (:205-215; blocks from
-        MultiCore.PartitionUsersAndItems, one sub-epoch's blocks on T threads), one epoch;
-      * single_thread: the sequential Iterate(), sized for ~`seconds` of CPU work."""
+        MultiCore.PartitionUsersAndItems, one sub-epoch's blocks on T threads);
+      * single_thread: the sequential Iterate() (MaxThreads = 1)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -245,19 +256,16 @@ def cpu_baseline(h, k, n_users, n_items, gb, seconds, sample):
     N.check(N.lib().mml_bmf_get_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
                                       N.ptr(bu, N._f32p), N.ptr(bi, N._f32p)))
     u, i, v = sample
+    n = len(u)
     kw = dict(gb=np.float32(gb), min_rating=np.float32(1), range_=np.float32(4), lr=0.01)
-    probe = 200_000
+    host = {"cpu_model": cpu_model(), "nproc": os.cpu_count(), "process_cpus": cpu_threads()}
     t0 = time.perf_counter()
-    O.bmf_iterate(u, i, v, np.arange(probe, dtype=np.int32), U, V, bu, bi, **kw)
-    dt = time.perf_counter() - t0
-    n = int(min(len(u) - probe, max(probe, seconds / max(dt, 1e-9) * probe)))
-    t0 = time.perf_counter()
-    O.bmf_iterate(u, i, v, np.arange(probe, probe + n, dtype=np.int32), U, V, bu, bi, **kw)
+    O.bmf_iterate(u, i, v, np.arange(n, dtype=np.int32), U, V, bu, bi, **kw)
     dt = time.perf_counter() - t0
     single = {"value": n / dt, "unit": "rating-updates/s", "cores": 1, "kind": "port",
-              "sample": f"{n} ratings of the C2 stream itself (the GPU's training data), k={k}, "
-                        f"oracle Iterate() = C restatement of BiasedMatrixFactorization.cs:"
-                        f"264-310, single thread, {dt:.1f} s"}
+              "sample": f"one full epoch: all {n} ratings of the C2 stream (the GPU's training "
+                        f"data), k={k}, oracle Iterate() = C restatement of "
+                        f"BiasedMatrixFactorization.cs:264-310, single thread, {dt:.1f} s", **host}
     T = cpu_threads()
     rng = O.Rng(1)
     blocks = O.partition_users_and_items(rng, u, i, n_users - 1, n_items - 1, T)
@@ -265,39 +273,214 @@ def cpu_baseline(h, k, n_users, n_items, gb, seconds, sample):
     t0 = time.perf_counter()
     O.bmf_dsgd_epoch_mt(u, i, v, blocks, seq, T, U, V, bu, bi, **kw)
     dt_mt = time.perf_counter() - t0
-    return {"value": len(u) / dt_mt, "unit": "rating-updates/s", "cores": T, "kind": "port",
-            "sample": f"one DSGD epoch (MaxThreads={T}: {blocks[0]}x{blocks[0]} user x item "
-                      f"blocks, BiasedMatrixFactorization.cs:205-215) over the first {len(u)} "
-                      f"ratings of the C2 stream, k={k}, oracle C restatement on {T} threads, "
-                      f"{dt_mt:.1f} s",
-            "single_thread": single}
+    return {"value": n / dt_mt, "unit": "rating-updates/s", "cores": T, "kind": "port",
+            "sample": f"one full DSGD epoch (MaxThreads={T}: {blocks[0]}x{blocks[0]} user x item "
+                      f"blocks, BiasedMatrixFactorization.cs:205-215) over all {n} ratings of "
+                      f"the C2 stream, k={k}, oracle C restatement on {T} threads, {dt_mt:.1f} s",
+            **host, "single_thread": single}
+
+
+def c4_shard(rank, world, n_total, n_users, n_items, n_test, device, chunks=64):
+    """C4's data set as 64 user-range chunks (chunk c: users [c U/64, (c+1) U/64), n_total/64
+    ratings, seed 4000 + c; test ratings seed 5000 + c), so that the whole data set is the same
+    for every world size and rank r of N holds chunks [r 64/N, (r+1) 64/N): user shards of equal
+    rating count, disjoint users."""
+    from mymedialite_amd.synthetic import planted_ratings_torch
+    assert chunks % world == 0, "world size must divide 64"
+    per = n_total // chunks
+    mine = range(rank * chunks // world, (rank + 1) * chunks // world)
+    n_local = per * len(mine)
+    t_per = max(1, n_test // chunks)
+    out = [torch.empty(n_local, dtype=t, device=device)
+           for t in (torch.int32, torch.int32, torch.float32)]
+    test = [torch.empty(t_per * len(mine), dtype=t, device=device)
+            for t in (torch.int32, torch.int32, torch.float32)]
+    for x, c in enumerate(mine):
+        rng_ = (c * n_users // chunks, (c + 1) * n_users // chunks)
+        for dst, cnt, seed in ((out, per, 4000 + c), (test, t_per, 5000 + c)):
+            part = planted_ratings_torch(n_users, n_items, cnt, seed=seed, device=device,
+                                         user_range=rng_)
+            for d, p_ in zip(dst, part):
+                d[x * cnt:(x + 1) * cnt] = p_
+            del part
+    return out, test, (mine[0] * n_users // chunks, (mine[-1] + 1) * n_users // chunks)
+
+
+def bench_c4(args):
+    """C4: BiasedMF k=64, 1B ratings, 10M users x 100k items (Zipf 0.8), strong scaling over N
+    GPUs: rank r owns a user range with 1/N of the ratings (U, b_u local), runs its Hogwild epoch,
+    then one in-place RCCL all-reduce of V || b_i averages the item side.  One step =
+    one epoch over all 1B ratings + the all-reduce.  The global bias is computed over every rank's
+    ratings; the test RMSE is reduced over every rank's test ratings."""
+    world, rank, local = env_rank()
+    init_host_group(world)
+    k = args.k
+    n_total = args.ratings or 1_000_000_000
+    n_users = args.users or 10_000_000
+    n_items = args.items
+    ctx = N.Context(local)
+    if world > 1:
+        ctx.comm_init(share_unique_id(rank, N.Context.unique_id), world, rank)
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    t0 = time.perf_counter()
+    (users, items, values), (tu, ti, tv), (u_lo, u_hi) = c4_shard(
+        rank, world, n_total, n_users, n_items, 1_000_000, dev)
+    n_local = len(users)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t0
+    # Train(): global_bias from Ratings.Average over ALL ratings (BiasedMatrixFactorization.cs:
+    # 186-190): sum and count reduced over ranks
+    tot = torch.tensor([float(values.double().sum().item()), float(n_local)], dtype=torch.float64)
+    if world > 1:
+        torch.distributed.all_reduce(tot)
+    mean = float(np.float32(tot[0].item() / tot[1].item()))
+    avg = np.float32((np.float32(mean) - np.float32(1.0)) / np.float32(4.0))
+    gb = float(np.float32(np.log(avg / (1 - avg))))
+    params = N.BmfParams(k, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
+    h = N._vp()
+    N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(params), n_users, n_items,
+                                   ctypes.byref(h)))
+    t0 = time.perf_counter()
+    N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
+                                            values.data_ptr(), n_local, None))
+    ingest_s = time.perf_counter() - t0
+    del users, items, values
+    torch.cuda.empty_cache()
+    # InitModel on the device (640M normals at N = 1); rows of other ranks' users stay 0.  The
+    # item side starts identical on every rank (same seed), as after a broadcast.
+    N.check(N.lib().mml_bmf_init_model(h, 4, 0.0, 0.1, gb, 1.0, 5.0))
+    tus, tis, tvs = tu.cpu().numpy(), ti.cpu().numpy(), tv.cpu().numpy()
+    lr = 0.01
+
+    def evaluate():
+        out = np.zeros(2, np.float32)
+        N.check(N.lib().mml_bmf_evaluate(h, N.ptr(tus, N._i32p), N.ptr(tis, N._i32p),
+                                         N.ptr(tvs, N._f32p), len(tus), N.ptr(out, N._f32p)))
+        sse = torch.tensor([float(out[0]) ** 2 * len(tus), float(len(tus))], dtype=torch.float64)
+        if world > 1:
+            torch.distributed.all_reduce(sse)
+        return float(np.sqrt(sse[0].item() / sse[1].item()))
+
+    rmse0 = evaluate()
+    timing = np.zeros(2, np.float32)
+    ar_ms = []
+
+    def step():
+        N.check(N.lib().mml_bmf_iterate(h, lr, None))
+        N.lib().mml_bmf_last_timing(h, N.ptr(timing, N._f32p))
+        if world > 1:
+            t1 = time.perf_counter()
+            N.check(N.lib().mml_bmf_allreduce_items(h))
+            ar_ms.append((time.perf_counter() - t1) * 1e3)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    kernel_ms = []
+    ar_ms.clear()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kernel_ms.append(float(timing[0]))
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    rmse = evaluate()
+    value = n_total * args.steps / elapsed
+    avg_kernel_ms = float(np.mean(kernel_ms))
+    bpu = bytes_per_update(k)
+    achieved = n_local * bpu / (avg_kernel_ms * 1e-3) / 1e9
+    if rank == 0:
+        line = {
+            "metric": "SGD rating-updates/sec + final RMSE, BiasedMF k=64 at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "rating-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (planted rank-8 model, Zipf(0.8) items, 64 seeded user-range "
+                    "chunks generated in HBM; identical data set at every N)",
+            "config": {"workload": f"C4: BiasedMF k={k}, {n_total} ratings, {n_users} users x "
+                                   f"{n_items} items, equal-rating user shards, per-epoch RCCL "
+                                   f"all-reduce of V||b_i (model averaging)",
+                       "num_factors": k, "ratings_total": n_total, "ratings_per_gpu": n_local,
+                       "users": n_users, "items": n_items, "schedule": "hogwild",
+                       "parallelism": f"user-shard x{world}", "generate_s": gen_s,
+                       "device_ingest_s": ingest_s},
+            "final_rmse": rmse,
+            "initial_rmse": rmse0,
+            "epochs_trained": args.warmup + args.steps,
+            "allreduce_ms": float(np.mean(ar_ms)) if ar_ms else None,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": f"bmf_sgd_hogwild_kernel<RMSE,{max(1, (k + 3) // 4)}>",
+                         "kernel_avg_ms": avg_kernel_ms, "bytes_per_update": bpu,
+                         "per": "GPU (rank 0's shard)"},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(line), flush=True)
+    N.lib().mml_bmf_destroy(h)
+    ctx.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def c3_shard(rank, world, n_total, n_users, n_items, device, chunks=64):
+    """C3's events as 64 user-range chunks (chunk c: users [c U/64, (c+1) U/64) uniform, items
+    Zipf(0.8) over one shared permutation, n_total/64 events, seed 2000 + c); rank r of N holds
+    chunks [r 64/N, (r+1) 64/N), so the data set is the same at every N."""
+    from mymedialite_amd.synthetic import zipf_cdf
+    assert chunks % world == 0, "world size must divide 64"
+    per = n_total // chunks
+    mine = range(rank * chunks // world, (rank + 1) * chunks // world)
+    gp = torch.Generator(device=device)
+    gp.manual_seed(2)
+    perm = torch.randperm(n_items, generator=gp, device=device)
+    cdf = torch.from_numpy(zipf_cdf(n_items, 0.8)).to(device)
+    users = torch.empty(per * len(mine), dtype=torch.int32, device=device)
+    items = torch.empty(per * len(mine), dtype=torch.int32, device=device)
+    for x, c in enumerate(mine):
+        g = torch.Generator(device=device)
+        g.manual_seed(2000 + c)
+        lo, hi = c * n_users // chunks, (c + 1) * n_users // chunks
+        for s0 in range(0, per, 1 << 26):
+            e = min(per, s0 + (1 << 26))
+            o = x * per
+            users[o + s0:o + e] = torch.randint(lo, hi, (e - s0,), generator=g, device=device,
+                                                dtype=torch.int32)
+            r = torch.rand(e - s0, generator=g, device=device, dtype=torch.float64)
+            items[o + s0:o + e] = perm[torch.searchsorted(cdf, r).clamp_(max=n_items - 1)].to(
+                torch.int32)
+    return users, items
 
 
 def bench_bpr(args):
-    """C3: BPRMF, 10M users x 1M items, 500M positive events, k = 128, one GPU.  One step = one
-    BPRMF.Iterate() = Feedback.Count sampled triples (BPRMF.cs:160-226)."""
+    """C3: BPRMF, 10M users x 1M items, 500M positive events, k = 128.  One step = one
+    BPRMF.Iterate() = Feedback.Count sampled triples (BPRMF.cs:160-226).  N > 1: user shards of
+    equal event count (negatives drawn over all items), one in-place RCCL all-reduce of V || b
+    per epoch (model averaging; MultiCoreBPRMF.cs:49-63 is the reference's parallel form),
+    strong scaling over the fixed 500M events."""
     world, rank, local = env_rank()
-    if world != 1:
-        raise SystemExit("the C3 workload is a single-GPU configuration")
+    init_host_group(world)
     k = 128 if args.k == 64 else args.k
     n_users, n_items = args.users or 10_000_000, 1_000_000
-    n = args.ratings or 500_000_000
+    n_total = args.ratings or 500_000_000
     ctx = N.Context(local)
+    if world > 1:
+        ctx.comm_init(share_unique_id(rank, N.Context.unique_id), world, rank)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
-    g = torch.Generator(device=dev)
-    g.manual_seed(2)
-    from mymedialite_amd.synthetic import zipf_cdf
-    cdf = torch.from_numpy(zipf_cdf(n_items, 0.8)).to(dev)
-    perm = torch.randperm(n_items, generator=g, device=dev)
-    users = torch.empty(n, dtype=torch.int32, device=dev)
-    items = torch.empty(n, dtype=torch.int32, device=dev)
-    for s0 in range(0, n, 1 << 26):
-        e = min(n, s0 + (1 << 26))
-        users[s0:e] = torch.randint(0, n_users, (e - s0,), generator=g, device=dev,
-                                    dtype=torch.int32)
-        x = torch.rand(e - s0, generator=g, device=dev, dtype=torch.float64)
-        items[s0:e] = perm[torch.searchsorted(cdf, x).clamp_(max=n_items - 1)].to(torch.int32)
+    users, items = c3_shard(rank, world, n_total, n_users, n_items, dev)
+    n = len(users)
     torch.cuda.synchronize()
     sampler = {"uniform_user": N.BPR_SAMPLER_UNIFORM_USER,
                "uniform_pair": N.BPR_SAMPLER_UNIFORM_PAIR,
@@ -312,49 +495,76 @@ def bench_bpr(args):
     ingest_s = time.perf_counter() - t0
     del users, items
     torch.cuda.empty_cache()
-    N.check(N.lib().mml_bpr_init_model(h, 2, 0.0, 0.1))
+    N.check(N.lib().mml_bpr_init_model(h, 2, 0.0, 0.1))  # same seed: V identical on every rank
     timing = np.zeros(2, np.float32)
-    for w in range(args.warmup):
-        N.check(N.lib().mml_bpr_iterate(h, 1000 + w))
-    torch.cuda.synchronize()
-    ms, ums = [], []
-    t0 = time.perf_counter()
-    for step in range(args.steps):
-        N.check(N.lib().mml_bpr_iterate(h, 2000 + step))
+    ar_ms = []
+
+    def step(seed):
+        N.check(N.lib().mml_bpr_iterate(h, seed))
         N.lib().mml_bpr_last_timing(h, N.ptr(timing, N._f32p))
+        if world > 1:
+            t1 = time.perf_counter()
+            N.check(N.lib().mml_bpr_allreduce_items(h))
+            ar_ms.append((time.perf_counter() - t1) * 1e3)
+
+    for w in range(args.warmup):
+        step(1000 + 97 * w + rank)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    ms, ums = [], []
+    ar_ms.clear()
+    t0 = time.perf_counter()
+    for st_ in range(args.steps):
+        step(2000 + 97 * st_ + rank)
         ms.append(float(timing[0]))
         ums.append(float(timing[1]))
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     # the dominant kernel is bpr_update_kernel: U_u, V_i, V_j read + write (24k), b_i, b_j read +
     # write (16), the triple (12); the sampler kernel (the rest of the epoch) is reported beside it
     bpu = 24 * k + 28
     avg_ms = float(np.mean(ms))
     upd_ms = float(np.mean(ums))
     achieved = n * bpu / (upd_ms * 1e-3) / 1e9
-    cpu = None if args.no_cpu_baseline else cpu_baseline_bpr(k, args.cpu_seconds)
+    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_bpr(k, args.cpu_seconds)
     line = {
-        "metric": "BPR triple-updates/sec, BPRMF k=128 (C3)", "value": n * args.steps / elapsed,
-        "unit": "triple-updates/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "metric": "BPR triple-updates/sec, BPRMF k=128 (C3)",
+        "value": n_total * args.steps / elapsed,
+        "unit": "triple-updates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (users uniform, items Zipf(0.8), generated in HBM)",
         "config": {"workload": "C3: BPRMF 10M users x 1M items, 500M positives, k=128",
-                   "num_factors": k, "events": n, "users": n_users, "items": n_items,
+                   "num_factors": k, "events": n_total, "events_per_gpu": n,
+                   "users": n_users, "items": n_items,
                    "sampler": args.sampler + (" (BPRMF default)" if args.sampler ==
                                               "uniform_user" else ""),
+                   "parallelism": f"user-shard x{world}" + (
+                       ", per-epoch RCCL all-reduce of V||b" if world > 1 else ""),
                    "device_ingest_s": ingest_s},
+        "allreduce_ms": float(np.mean(ar_ms)) if ar_ms else None,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": f"bpr_update_kernel<{max(1, (k + 3) // 4)}>",
                      "kernel_avg_ms": upd_ms, "bytes_per_update": bpu,
                      "epoch_device_ms": avg_ms,
-                     "sampler_ms": avg_ms - upd_ms},
+                     "sampler_ms": avg_ms - upd_ms,
+                     "frac_epoch": n * bpu / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "frac_note": "frac = the update kernel alone; frac_epoch = the same bytes "
+                                  "over the whole device epoch (sampler + XCD partition + "
+                                  "update)"},
         "cpu_baseline": cpu,
     }
-    print(json.dumps(line), flush=True)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     N.lib().mml_bpr_destroy(h)
     ctx.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 def bench_wrmf(args):

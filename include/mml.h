@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 3
+#define MML_ABI_VERSION 4
 
 typedef int32_t mml_status;
 enum {
@@ -45,10 +45,24 @@ typedef struct mml_ctx mml_ctx;
 /* One context per recommender instance, bound to one GPU (one process per GPU for multi-GPU). */
 mml_status mml_ctx_create(int32_t device_id, mml_ctx** out);
 mml_status mml_ctx_destroy(mml_ctx* ctx);
+/* One context over n GPUs driven from ONE process (ABI 4) -- the shape of the reference's
+ * single-process front end (RatingPrediction.cs:161-331): an ncclCommInitAll communicator, one
+ * stream per device.  Handles created on it shard the work over the devices: mml_bmf / mml_bpr
+ * split the ratings into user ranges of equal rating count and average V || item biases with one
+ * RCCL all-reduce after every epoch; mml_wrmf solves row shards and all-gathers
+ * them after each half-step.  Each call drives the devices from one host thread per device and
+ * returns when all have finished.  On such handles the exact schedules (ORDERED / DSGD), the
+ * _device data setters and the sibling-model extras return MML_ERR_STATE. */
+mml_status mml_ctx_create_multi(const int32_t* device_ids, int32_t n_devices, mml_ctx** out);
 /* RCCL communicator across processes (one rank per GPU): rank 0 creates the 128-byte id, the host
  * broadcasts it (e.g. torch.distributed / MPI), then every rank calls mml_ctx_comm_init. */
 mml_status mml_comm_unique_id(uint8_t out_id[128]);
 mml_status mml_ctx_comm_init(mml_ctx* ctx, const uint8_t id[128], int32_t nranks, int32_t rank);
+/* Item groups the Hogwild schedules split the stream into (ABI 4): 8 when the device deals the
+ * blocks of a grid round-robin over its 8 XCDs (probed once per context by reading each block's
+ * XCC id), so each group's item rows are only cached in one XCD's L2; else 1.  No reference
+ * counterpart (the managed Hogwild has one coherent cache hierarchy). */
+mml_status mml_ctx_xcd_groups(mml_ctx* ctx, int32_t* out);
 
 /* ------------------------------------------------------------------ host RNG (MyMediaLite.Random)
  * System.Random(seed)-compatible generator for hosts without the .NET BCL; the C# front end keeps
@@ -188,6 +202,12 @@ mml_status mml_bmf_set_model(mml_bmf* h, const float* user_factors, const float*
                              float min_rating, float max_rating);
 mml_status mml_bmf_get_model(mml_bmf* h, float* user_factors, float* item_factors,
                              float* user_bias, float* item_bias);
+/* InitModel on the device for models too large for the host RNG chain (C4: 640 M normals), after
+ * set_data: N(mean, stddev) from a counter-based generator keyed by seed, rows of users / items
+ * without training ratings 0 (MatrixFactorization.cs:99-116), biases 0.  Statistically, not
+ * bitwise, equal to the MathNet draws; MML_MF_BIASED / MML_MF_PLAIN (ABI 4). */
+mml_status mml_bmf_init_model(mml_bmf* h, uint64_t seed, double mean, double stddev,
+                              float global_bias, float min_rating, float max_rating);
 /* One epoch = BiasedMatrixFactorization.Iterate(IList<int>,bool,bool) (:264-310) -- for
  * MML_MF_PLAIN MatrixFactorization.Iterate(IList<int>,bool,bool) (MatrixFactorization.cs:166-196)
  * without its trailing UpdateLearnRate, which stays on the host -- over the stored

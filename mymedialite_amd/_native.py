@@ -74,8 +74,10 @@ SIGNATURES = {
     "mml_device_count": (_st, [_i32p]),
     "mml_ctx_create": (_st, [ctypes.c_int32, ctypes.POINTER(_vp)]),
     "mml_ctx_destroy": (_st, [_vp]),
+    "mml_ctx_create_multi": (_st, [_i32p, ctypes.c_int32, ctypes.POINTER(_vp)]),
     "mml_comm_unique_id": (_st, [_u8p]),
     "mml_ctx_comm_init": (_st, [_vp, _u8p, ctypes.c_int32, ctypes.c_int32]),
+    "mml_ctx_xcd_groups": (_st, [_vp, _i32p]),
     "mml_random_create": (_st, [ctypes.c_int32, ctypes.POINTER(_vp)]),
     "mml_random_destroy": (_st, [_vp]),
     "mml_random_next": (_st, [_vp, ctypes.c_int32, _i32p]),
@@ -104,6 +106,8 @@ SIGNATURES = {
     "mml_bmf_set_model": (_st, [_vp, _f32p, _f32p, _f32p, _f32p, ctypes.c_float, ctypes.c_float,
                                 ctypes.c_float]),
     "mml_bmf_get_model": (_st, [_vp, _f32p, _f32p, _f32p, _f32p]),
+    "mml_bmf_init_model": (_st, [_vp, ctypes.c_uint64, ctypes.c_double, ctypes.c_double,
+                                 ctypes.c_float, ctypes.c_float, ctypes.c_float]),
     "mml_bmf_iterate": (_st, [_vp, ctypes.c_float, _i32p]),
     "mml_bmf_set_user_relation": (_st, [_vp, ctypes.c_int32, _i64p, _i32p]),
     "mml_bmf_fold_in": (_st, [_vp, ctypes.c_int32, _i64p, _i32p, _f32p, _f32p, ctypes.c_int32,
@@ -208,6 +212,15 @@ def f32(a):
     return np.ascontiguousarray(a, dtype=np.float32)
 
 
+def device_arg(rec):
+    """The Context argument of a recommender: its ``Gpus`` property (comma-separated device ids:
+    one multi-device context, user / row shards) when set, else its ``Device`` index."""
+    g = str(getattr(rec, "Gpus", "") or "").strip()
+    if g:
+        return [int(x) for x in g.replace(";", ",").split(",") if x.strip()]
+    return int(getattr(rec, "Device", 0))
+
+
 def device_count() -> int:
     n = ctypes.c_int32(0)
     check(lib().mml_device_count(ctypes.byref(n)))
@@ -217,12 +230,19 @@ def device_count() -> int:
 class Context:
     """mml_ctx: one GPU + one HIP stream (+ RCCL communicator for multi-GPU)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device=0):
+        """device: a GPU index, or a sequence of GPU indices for one multi-device context
+        (mml_ctx_create_multi: user / row shards over the devices, driven from this process)."""
         h = _vp()
-        check(lib().mml_ctx_create(int(device), ctypes.byref(h)))
+        if isinstance(device, (list, tuple)):
+            ids = np.ascontiguousarray(device, dtype=np.int32)
+            check(lib().mml_ctx_create_multi(ptr(ids, _i32p), len(ids), ctypes.byref(h)))
+            self.nranks = len(ids)
+        else:
+            check(lib().mml_ctx_create(int(device), ctypes.byref(h)))
+            self.nranks = 1
         self.handle = h
         self.device = device
-        self.nranks = 1
         self.rank = 0
 
     @staticmethod
@@ -235,6 +255,12 @@ class Context:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(lib().mml_ctx_comm_init(self.handle, buf, int(nranks), int(rank)))
         self.nranks, self.rank = nranks, rank
+
+    def xcd_groups(self) -> int:
+        """Item groups of the Hogwild schedules (8 = one per XCD, probed on the device)."""
+        n = ctypes.c_int32(0)
+        check(lib().mml_ctx_xcd_groups(self.handle, ctypes.byref(n)))
+        return n.value
 
     def close(self):
         if getattr(self, "handle", None):

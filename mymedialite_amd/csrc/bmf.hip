@@ -33,6 +33,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "mml_device.h"
 #include "mml_internal.h"
 
 namespace {
@@ -263,21 +264,33 @@ __device__ __forceinline__ T group_fetch(T v, int base, int lane) {
 // RMSE gain at that scale, so it is not kept.  VPL > 1 puts more ratings in one wave
 // step (64 / LPR): more rows in flight per wave and the per-rating scalar part (sigmoid, fp64
 // gradient) shared by fewer lanes.
-template <int LOSS, int LPR, int VPL, bool COH>
+// Access modes of the Hogwild kernel's rows and biases
+constexpr int kAccPlain = 0;     // plain loads / stores
+constexpr int kAccCoherent = 1;  // every row / bias access agent-coherent (sc1), HOGWILD_COHERENT
+constexpr int kAccItemL2 = 2;    // XCD-owned item groups: item rows / biases loaded sc1 (L2-served,
+                                 // past the CU's stale L1), stored plain (kept in the owning L2)
+
+// The stream is split into ng group spans goff[g] .. goff[g + 1] (mml_device.h group_wave): ng = 8
+// for XCD-owned item groups (block b serves group b % 8, one XCD per group), ng = 1 for one span.
+// waves_per_group waves divide a span into contiguous chunks.
+template <int LOSS, int LPR, int VPL, int AM>
 __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
-    int64_t n, int64_t chunk, float* U, float* V, float* bu, float* bi, int32_t ld4, BmfScalars s,
+    const int64_t* __restrict__ goff, int32_t ng, int32_t waves_per_group, float* U, float* V,
+    float* bu, float* bi, int32_t ld4, uint32_t v_bytes, uint32_t bi_bytes, BmfScalars s,
     const int32_t* __restrict__ cnt_u, const int32_t* __restrict__ cnt_i) {
     constexpr int RPW = 64 / LPR;  // ratings per wave step
+    constexpr bool COH = AM == kAccCoherent;
     const int lane = threadIdx.x & 63;
     // wave-uniform (SGPR) bounds: the loops' branches stay scalar
     const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + wib;
-    const int64_t begin = wave * chunk;
-    const int64_t end = min(begin + chunk, n);
+    const mml::GroupWave gw = mml::group_wave(goff, ng, waves_per_group, wib, blockDim.x >> 6);
+    const int64_t begin = gw.begin, end = gw.end;
     const int sub = lane / LPR, q = lane % LPR;
     float4* U4 = reinterpret_cast<float4*>(U);
     float4* V4 = reinterpret_cast<float4*>(V);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t vrs = mml::buffer_rsrc(V, v_bytes);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t brs = mml::buffer_rsrc(bi, bi_bytes);
     for (int64_t base = begin; base < end; base += 64) {
         // 64 ratings of the stream: three coalesced 256-B loads, then broadcast per group
         const int64_t idx = base + lane;
@@ -301,7 +314,10 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
 #pragma unroll
                 for (int v = 0; v < VPL; ++v) {
                     pu[v] = load4<COH>(U4 + ou + LPR * v);
-                    qi[v] = load4<COH>(V4 + oi + LPR * v);
+                    if constexpr (AM == kAccItemL2)
+                        qi[v] = mml::load4_l2(vrs, (uint32_t)(oi + LPR * v) * 16u);
+                    else
+                        qi[v] = load4<COH>(V4 + oi + LPR * v);
                 }
                 float part = 0.0f;
 #pragma unroll
@@ -314,7 +330,11 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
                 part = group_sum<LPR>(part);
                 constexpr bool biased = LOSS != kPlainMF;
                 const float bu_u = biased ? load1<COH>(bu + u) : 0.0f;
-                const float bi_i = biased ? load1<COH>(bi + i) : 0.0f;
+                float bi_i = 0.0f;
+                if constexpr (biased) {
+                    if constexpr (AM == kAccItemL2) bi_i = mml::load1_l2(brs, (uint32_t)i * 4u);
+                    else bi_i = load1<COH>(bi + i);
+                }
                 const RatingStep<LOSS> st(s, part, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
                 if (biased && q == 0) {
                     store1<COH>(bu + u, st.new_bu);
@@ -1229,6 +1249,15 @@ struct mml_bmf {
     bool has_slot[2] = {false, false};
     mml::DeviceArray<float> P;  // SVD++: the free user offsets p [n_users x ld]
     bool has_p = false;
+    // HOGWILD on XCD-owned item groups (xcd.hip): the stream partitioned by item group, visit
+    // order kept within a group; built on the first Hogwild epoch after set_data
+    mml::XcdSplit xs;
+    mml::DeviceArray<int32_t> xu, xi, xr;  // xr holds the float ratings' bits
+    bool has_xstream = false;
+    // multi-device context: one single-device handle per GPU over a user range ub[d] .. ub[d + 1]
+    // (U, b_u trained there; V, b_i replicated and averaged after every epoch)
+    std::vector<mml_bmf*> shards;
+    std::vector<int32_t> ub;
 };
 
 namespace {
@@ -1298,6 +1327,7 @@ void finish_data(mml_bmf* h, const int32_t* order_dev) {
     MML_HIP(hipStreamSynchronize(st));
     h->G = 0;
     h->has_positions = false;
+    h->has_xstream = false;
     h->has_data = true;
 }
 
@@ -1407,64 +1437,98 @@ void launch_ordered(mml_bmf* h, const int64_t* off, int32_t G, int32_t sub, int 
     MML_HIP(hipGetLastError());
 }
 
+// The XCD-partitioned copy of the visit-order stream (built once per data set): items dealt into 8
+// groups of equal rating count (cnt_i), ratings stably partitioned by their item's group.
+void ensure_xstream(mml_bmf* h) {
+    if (h->has_xstream) return;
+    hipStream_t st = h->ctx->stream;
+    std::vector<int32_t> ci(h->n_items);
+    if (h->n_items > 0)
+        MML_HIP(hipMemcpyAsync(ci.data(), h->cnt_i.get(), sizeof(int32_t) * h->n_items,
+                               hipMemcpyDeviceToHost, st));
+    MML_HIP(hipStreamSynchronize(st));
+    h->xs.set_groups(st, std::vector<int64_t>(ci.begin(), ci.end()), 8);
+    h->xu.alloc(h->n);
+    h->xi.alloc(h->n);
+    h->xr.alloc(h->n);
+    const int32_t* in[3] = {h->su.get(), h->si.get(), reinterpret_cast<const int32_t*>(h->sr.get())};
+    int32_t* out[3] = {h->xu.get(), h->xi.get(), h->xr.get()};
+    h->xs.partition(st, h->si.get(), h->n, 3, in, out);
+    MML_HIP(hipStreamSynchronize(st));
+    h->has_xstream = true;
+}
+
+// MML_HOGWILD_XCD: 1 (default) = XCD-owned item groups with L2-served item loads, 2 = the groups
+// with plain loads, 0 = one span over all XCDs (the round-1 kernel)
+static int hogwild_xcd_mode() {
+    static const int m = [] {
+        const char* e = std::getenv("MML_HOGWILD_XCD");
+        return e ? std::atoi(e) : 1;
+    }();
+    return m;
+}
+
 template <int LOSS>
 void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const int32_t* ci) {
     hipStream_t st = h->ctx->stream;
     const int64_t n = h->n;
     // waves: up to 256 CUs x 32 (all resident at once), each walking >= min_chunk ratings of the
     // stream in order.  Fewer than 16 waves' worth of work runs as ONE workgroup: a single CU keeps
-    // every row in one L1/L2, whereas 2+ workgroups land on different XCDs whose private write-back
-    // L2s replicate hot rows ("Hogwild and per-XCD caches"; C1: 4 waves on one CU
-    // RMSE +0.007 vs sequential, 19 waves on 5 CUs +0.12).  On C2 the kernel runs at the time of
-    // its bare memory pattern (scripts/ubench/rowrmw.hip: 22.2 ms for the 1,052 B per rating);
-    // VPL 2 equal, VPL 4 10 % slower, item-bucketing the stream per XCD 2 % slower.
+    // every row in one L1/L2 and bounds the updates in flight (C1: 4 waves on one CU RMSE +0.007 vs
+    // sequential, 19 waves on 5 CUs +0.12).  Larger sets run on XCD-owned item groups (xcd.hip):
+    // group g's ratings on the blocks b % 8 == g of one XCD, so a hot item's row lives in one L2
+    // instead of 8 replicas whose write-backs overwrite each other's updates.
     static const int64_t min_chunk = [] {
         const char* e = std::getenv("MML_HOGWILD_MIN_CHUNK");
         return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)12000;
     }();
     int64_t waves = std::min<int64_t>(256 * 32, std::max<int64_t>(1, n / min_chunk));
-    if (waves < 16) waves = 4;
-    const int64_t blocks = (waves + 3) / 4;
-    waves = blocks * 4;
-    const int64_t chunk = (n + waves - 1) / waves;
-    const int ld4 = h->ld / 4;
     const bool coh = h->p.schedule == MML_SCHEDULE_HOGWILD_COHERENT;
-    static const int vpl_env = [] {
-        const char* e = std::getenv("MML_HOGWILD_VPL");
-        return e ? std::atoi(e) : 0;
-    }();
-    // float4s per lane: VPL x LPR = ld / 4 (h->lpr is the VPL = 1 lane count)
-    int vpl = vpl_env == 2 || vpl_env == 4 ? vpl_env : 1;
-#define MML_HOG1(LPR, VPL, COH)                                                                \
-    bmf_sgd_hogwild_kernel<LOSS, LPR, VPL, COH><<<(int)blocks, 256, 0, st>>>(                \
-        h->su.get(), h->si.get(), h->sr.get(), n, chunk, h->U.get(), h->V.get(), h->bu.get(),  \
-        h->bi.get(), ld4, s, cu, ci)
-#define MML_HOGV(LPR, VPL)         \
-    if (coh) {                     \
-        MML_HOG1(LPR, VPL, true);  \
-    } else {                       \
-        MML_HOG1(LPR, VPL, false); \
+    const int xmode = hogwild_xcd_mode();
+    const uint64_t v_bytes = (uint64_t)h->n_items * h->ld * sizeof(float);
+    int32_t ng = 1;
+    const int64_t* goff = h->whole_off.get();
+    const int32_t *su = h->su.get(), *si = h->si.get();
+    const float* sr = h->sr.get();
+    int am = coh ? kAccCoherent : kAccPlain;
+    if (waves < 16) {
+        waves = 4;
+    } else if (!coh && xmode > 0 && v_bytes < (1ull << 32) && mml::xcd_groups(h->ctx) == 8) {
+        ensure_xstream(h);
+        ng = 8;
+        goff = h->xs.goff.get();
+        su = h->xu.get();
+        si = h->xi.get();
+        sr = reinterpret_cast<const float*>(h->xr.get());
+        if (xmode == 1) am = kAccItemL2;
     }
-    // VPL > 1 only for 16 < k <= 128 (row lengths 8, 16, 32 float4s)
-    const int row4 = h->lpr;
-    if (vpl > 1 && (row4 < 8 || row4 > 32)) vpl = 1;
-    switch (row4 * 8 + vpl) {
-        case 8 * 8 + 2: MML_HOGV(4, 2); break;
-        case 8 * 8 + 4: MML_HOGV(2, 4); break;
-        case 16 * 8 + 2: MML_HOGV(8, 2); break;
-        case 16 * 8 + 4: MML_HOGV(4, 4); break;
-        case 32 * 8 + 2: MML_HOGV(16, 2); break;
-        case 32 * 8 + 4: MML_HOGV(8, 4); break;
-        default:
-            switch (row4) {
-                case 1: MML_HOGV(1, 1); break;
-                case 2: MML_HOGV(2, 1); break;
-                case 4: MML_HOGV(4, 1); break;
-                case 8: MML_HOGV(8, 1); break;
-                case 16: MML_HOGV(16, 1); break;
-                case 32: MML_HOGV(32, 1); break;
-                default: MML_HOGV(64, 1); break;
-            }
+    int64_t blocks = (waves + 3) / 4;
+    blocks = (blocks + ng - 1) / ng * ng;
+    const int32_t wpg = (int32_t)(blocks / ng * 4);
+    const int ld4 = h->ld / 4;
+    const uint32_t vb = (uint32_t)std::min<uint64_t>(v_bytes, 0xFFFFFFFFull);
+    const uint32_t bb = (uint32_t)((uint64_t)h->n_items * sizeof(float));
+#define MML_HOG1(LPR, VPL, AM)                                                                  \
+    bmf_sgd_hogwild_kernel<LOSS, LPR, VPL, AM><<<(int)blocks, 256, 0, st>>>(                  \
+        su, si, sr, goff, ng, wpg, h->U.get(), h->V.get(), h->bu.get(), h->bi.get(), ld4, vb, bb, \
+        s, cu, ci)
+#define MML_HOGV(LPR, VPL)                                       \
+    if (am == kAccCoherent) {                                    \
+        MML_HOG1(LPR, VPL, kAccCoherent);                        \
+    } else if (am == kAccItemL2) {                               \
+        MML_HOG1(LPR, VPL, kAccItemL2);                          \
+    } else {                                                     \
+        MML_HOG1(LPR, VPL, kAccPlain);                           \
+    }
+    // one float4 of U_u and of V_i per lane (VPL 2 measured equal, VPL 4 10 % slower on C2)
+    switch (h->lpr) {
+        case 1: MML_HOGV(1, 1); break;
+        case 2: MML_HOGV(2, 1); break;
+        case 4: MML_HOGV(4, 1); break;
+        case 8: MML_HOGV(8, 1); break;
+        case 16: MML_HOGV(16, 1); break;
+        case 32: MML_HOGV(32, 1); break;
+        default: MML_HOGV(64, 1); break;
     }
 #undef MML_HOGV
 #undef MML_HOG1
@@ -1631,6 +1695,151 @@ void run_epoch(mml_bmf* h, const BmfScalars& s, const int32_t* seq) {
 
 using mml::guard;
 
+// ------------------------------------------------------------------ multi-device handles
+// A handle on a multi-device context (mml_ctx_create_multi) is the one-process form of SURVEY
+// 8(e)'s user shards: the ratings are split into contiguous user ranges of equal rating count
+// (visit order kept within a shard), one single-device handle per GPU trains its range with the
+// Hogwild schedule, and after every epoch one RCCL all-reduce of V || b_i over the devices
+// (ncclCommInitAll communicator, one host thread per device) averages the item side.
+namespace {
+
+void single_device_only(const mml_bmf* h) {
+    if (h->ctx->multi())
+        mml::fail(MML_ERR_STATE, "not available on a multi-device context (user-sharded Hogwild "
+                                 "training, Predict and Evaluate only)");
+}
+
+void multi_create(mml_ctx* ctx, const mml_bmf_params* params, int32_t n_users, int32_t n_items,
+                  mml_bmf* h) {
+    MML_REQUIRE(params->model == MML_MF_BIASED || params->model == MML_MF_PLAIN,
+                "a multi-device context trains MML_MF_BIASED / MML_MF_PLAIN");
+    MML_REQUIRE(params->schedule == MML_SCHEDULE_HOGWILD ||
+                    params->schedule == MML_SCHEDULE_HOGWILD_COHERENT,
+                "a multi-device context trains with the HOGWILD schedules (user shards)");
+    h->ctx = ctx;
+    h->p = *params;
+    h->n_users = n_users;
+    h->n_items = n_items;
+    h->k = params->num_factors;
+    h->shards.assign(ctx->sub.size(), nullptr);
+    for (size_t d = 0; d < ctx->sub.size(); ++d) {
+        const mml_status st = mml_bmf_create(ctx->sub[d], params, n_users, n_items, &h->shards[d]);
+        if (st != MML_OK) mml::fail(st, mml_last_error());
+    }
+    h->ub.assign(ctx->sub.size() + 1, n_users);
+    h->ub[0] = 0;
+}
+
+void multi_set_data(mml_bmf* h, const int32_t* users, const int32_t* items, const float* values,
+                    int64_t n, const int32_t* order) {
+    const int32_t nd = (int32_t)h->shards.size();
+    for (int64_t x = 0; x < n; ++x) {
+        MML_REQUIRE(users[x] >= 0 && users[x] < h->n_users && items[x] >= 0 &&
+                        items[x] < h->n_items,
+                    "rating user/item id or order index out of range");
+        if (order) MML_REQUIRE(order[x] >= 0 && order[x] < n, "order index out of range");
+    }
+    h->ub = mml::balanced_user_bounds(users, n, h->n_users, nd);
+    std::vector<std::vector<int32_t>> su(nd), si(nd);
+    std::vector<std::vector<float>> sr(nd);
+    for (int64_t x = 0; x < n; ++x) {  // visit order, split by the owner of the user
+        const int64_t o = order ? order[x] : x;
+        const int32_t d = mml::owner_of(h->ub, users[o]);
+        su[d].push_back(users[o]);
+        si[d].push_back(items[o]);
+        sr[d].push_back(values[o]);
+    }
+    mml::on_devices(h->ctx, [&](int32_t d) {
+        return mml_bmf_set_data(h->shards[d], su[d].data(), si[d].data(), sr[d].data(),
+                                (int64_t)su[d].size(), nullptr);
+    });
+    h->n = n;
+    h->has_data = true;
+}
+
+// per-device index lists of (user-routed) queries: unknown users go to device 0
+std::vector<std::vector<int64_t>> route_users(const mml_bmf* h, const int32_t* users, int64_t n) {
+    std::vector<std::vector<int64_t>> r(h->shards.size());
+    for (int64_t x = 0; x < n; ++x) {
+        const int32_t u = users[x];
+        r[u >= 0 && u < h->n_users ? mml::owner_of(h->ub, u) : 0].push_back(x);
+    }
+    return r;
+}
+
+void multi_predict(mml_bmf* h, const int32_t* users, const int32_t* items, int64_t n,
+                   float* out) {
+    const auto r = route_users(h, users, n);
+    mml::on_devices(h->ctx, [&](int32_t d) {
+        const auto& ix = r[d];
+        if (ix.empty()) return (mml_status)MML_OK;
+        std::vector<int32_t> u(ix.size()), i(ix.size());
+        std::vector<float> o(ix.size());
+        for (size_t x = 0; x < ix.size(); ++x) {
+            u[x] = users[ix[x]];
+            i[x] = items[ix[x]];
+        }
+        const mml_status st = mml_bmf_predict(h->shards[d], u.data(), i.data(),
+                                              (int64_t)ix.size(), o.data());
+        for (size_t x = 0; st == MML_OK && x < ix.size(); ++x) out[ix[x]] = o[x];
+        return st;
+    });
+}
+
+void multi_evaluate(mml_bmf* h, const int32_t* users, const int32_t* items, const float* values,
+                    int64_t n, float* out) {
+    const auto r = route_users(h, users, n);
+    const size_t nd = h->shards.size();
+    std::vector<double> sse(nd, 0.0), sae(nd, 0.0);
+    mml::on_devices(h->ctx, [&](int32_t d) {
+        const auto& ix = r[d];
+        if (ix.empty()) return (mml_status)MML_OK;
+        std::vector<int32_t> u(ix.size()), i(ix.size());
+        std::vector<float> v(ix.size());
+        for (size_t x = 0; x < ix.size(); ++x) {
+            u[x] = users[ix[x]];
+            i[x] = items[ix[x]];
+            v[x] = values[ix[x]];
+        }
+        float o[2] = {0.0f, 0.0f};
+        const mml_status st = mml_bmf_evaluate(h->shards[d], u.data(), i.data(), v.data(),
+                                               (int64_t)ix.size(), o);
+        sse[d] = (double)o[0] * o[0] * (double)ix.size();
+        sae[d] = (double)o[1] * (double)ix.size();
+        return st;
+    });
+    double a = 0.0, b = 0.0;
+    for (size_t d = 0; d < nd; ++d) {
+        a += sse[d];
+        b += sae[d];
+    }
+    out[0] = n > 0 ? (float)std::sqrt(a / (double)n) : 0.0f;
+    out[1] = n > 0 ? (float)(b / (double)n) : 0.0f;
+}
+
+void multi_get_model(mml_bmf* h, float* U, float* V, float* bu, float* bi) {
+    mml::on_devices(h->ctx, [&](int32_t d) {
+        return mml::guard([&] {
+            mml_bmf* s = h->shards[d];
+            s->ctx->activate();
+            const int64_t lo = h->ub[d], rows = h->ub[d + 1] - h->ub[d];
+            if (U && rows > 0) download_padded(s, U + lo * h->k, s->U.get() + lo * s->ld, rows);
+            if (bu && rows > 0)
+                MML_HIP(hipMemcpyAsync(bu + lo, s->bu.get() + lo, sizeof(float) * rows,
+                                       hipMemcpyDeviceToHost, s->ctx->stream));
+            if (d == 0) {
+                if (V) download_padded(s, V, s->V.get(), h->n_items);
+                if (bi && h->n_items)
+                    MML_HIP(hipMemcpyAsync(bi, s->bi.get(), sizeof(float) * h->n_items,
+                                           hipMemcpyDeviceToHost, s->ctx->stream));
+            }
+            MML_HIP(hipStreamSynchronize(s->ctx->stream));
+        });
+    });
+}
+
+}  // namespace
+
 extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params, int32_t n_users,
                                      int32_t n_items, mml_bmf** out) {
     return guard([&] {
@@ -1645,6 +1854,17 @@ extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params,
         MML_REQUIRE(params->schedule >= MML_SCHEDULE_ORDERED &&
                         params->schedule <= MML_SCHEDULE_HOGWILD_COHERENT,
                     "unknown schedule");
+        if (ctx->multi()) {
+            auto* h = new mml_bmf();
+            try {
+                multi_create(ctx, params, n_users, n_items, h);
+            } catch (...) {
+                mml_bmf_destroy(h);
+                throw;
+            }
+            *out = h;
+            return;
+        }
         ctx->activate();
         auto* h = new mml_bmf();
         try {
@@ -1670,6 +1890,12 @@ extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params,
 extern "C" mml_status mml_bmf_destroy(mml_bmf* h) {
     return guard([&] {
         if (!h) return;
+        if (!h->shards.empty() || (h->ctx && h->ctx->multi())) {
+            for (mml_bmf* s : h->shards)
+                if (s) mml_bmf_destroy(s);
+            delete h;
+            return;
+        }
         (void)hipSetDevice(h->ctx->device);
         (void)hipStreamSynchronize(h->ctx->stream);
         delete h;
@@ -1682,6 +1908,7 @@ extern "C" mml_status mml_bmf_set_data(mml_bmf* h, const int32_t* users, const i
         check_handle(h);
         MML_REQUIRE(n >= 0 && n <= INT32_MAX, "rating count out of range");
         MML_REQUIRE(n == 0 || (users && items && values), "null rating arrays");
+        if (h->ctx->multi()) return multi_set_data(h, users, items, values, n, order);
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         h->has_data = false;
@@ -1712,6 +1939,7 @@ extern "C" mml_status mml_bmf_set_data_device(mml_bmf* h, const int32_t* users,
                                               int64_t n, const int32_t* order) {
     return guard([&] {
         check_handle(h);
+        single_device_only(h);
         MML_REQUIRE(n >= 0 && n <= INT32_MAX, "rating count out of range");
         MML_REQUIRE(n == 0 || (users && items && values), "null rating arrays");
         h->ctx->activate();
@@ -1737,6 +1965,7 @@ extern "C" mml_status mml_bmf_set_blocks(mml_bmf* h, int32_t num_groups, const i
                                          const int32_t* indices) {
     return guard([&] {
         check_handle(h);
+        single_device_only(h);
         MML_REQUIRE(h->has_data, "set_data must precede set_blocks");
         MML_REQUIRE(num_groups >= 1 && offsets, "bad block arguments");
         const int64_t nb = (int64_t)num_groups * num_groups;
@@ -1782,6 +2011,14 @@ extern "C" mml_status mml_bmf_set_model(mml_bmf* h, const float* U, const float*
                                         float min_rating, float max_rating) {
     return guard([&] {
         check_handle(h);
+        if (h->ctx->multi()) {
+            mml::on_devices(h->ctx, [&](int32_t d) {
+                return mml_bmf_set_model(h->shards[d], U, V, bu, bi, global_bias, min_rating,
+                                         max_rating);
+            });
+            h->has_model = true;
+            return;
+        }
         MML_REQUIRE((h->n_users == 0 || (U && bu)) && (h->n_items == 0 || (V && bi)),
                     "null model arrays");
         h->ctx->activate();
@@ -1802,9 +2039,67 @@ extern "C" mml_status mml_bmf_set_model(mml_bmf* h, const float* U, const float*
     });
 }
 
+namespace {
+// InitModel on the device: N(mean, stddev) in the first k columns of each row (padding 0), rows
+// with no training rating zero (MatrixFactorization.cs:108-113)
+__global__ __launch_bounds__(256) void bmf_init_normal_kernel(float* __restrict__ M, int64_t rows,
+                                                              int32_t k, int32_t ld, uint64_t seed,
+                                                              double mean, double stddev,
+                                                              const int32_t* __restrict__ cnt) {
+    const int64_t total = rows * ld;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = e / ld;
+        const int32_t c = (int32_t)(e - r * ld);
+        M[e] = c < k && cnt[r] > 0
+                   ? (float)(mean + stddev * mml::counter_normal(seed, (uint64_t)(r * k + c)))
+                   : 0.0f;
+    }
+}
+}  // namespace
+
+extern "C" mml_status mml_bmf_init_model(mml_bmf* h, uint64_t seed, double mean, double stddev,
+                                         float global_bias, float min_rating, float max_rating) {
+    return guard([&] {
+        check_handle(h);
+        if (h->ctx->multi()) {  // same seed on every device: one item side, users by range
+            MML_REQUIRE(h->has_data, "set_data must precede init_model");
+            mml::on_devices(h->ctx, [&](int32_t d) {
+                return mml_bmf_init_model(h->shards[d], seed, mean, stddev, global_bias,
+                                          min_rating, max_rating);
+            });
+            h->has_model = true;
+            return;
+        }
+        MML_REQUIRE(h->has_data, "set_data must precede init_model (rows without ratings stay 0)");
+        MML_REQUIRE(h->p.model <= MML_MF_PLAIN, "device init covers MML_MF_BIASED / MML_MF_PLAIN");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        if (h->n_users > 0)
+            bmf_init_normal_kernel<<<8192, 256, 0, st>>>(h->U.get(), h->n_users, h->k, h->ld, seed,
+                                                         mean, stddev, h->cnt_u.get());
+        if (h->n_items > 0)
+            bmf_init_normal_kernel<<<8192, 256, 0, st>>>(h->V.get(), h->n_items, h->k, h->ld,
+                                                         seed ^ 0x5DEECE66Dull, mean, stddev,
+                                                         h->cnt_i.get());
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipMemsetAsync(h->bu.get(), 0, sizeof(float) * h->n_users, st));
+        MML_HIP(hipMemsetAsync(h->bi.get(), 0, sizeof(float) * h->n_items, st));
+        MML_HIP(hipStreamSynchronize(st));
+        h->gb = global_bias;
+        h->min_rating = min_rating;
+        h->max_rating = max_rating;
+        h->has_model = true;
+    });
+}
+
 extern "C" mml_status mml_bmf_get_model(mml_bmf* h, float* U, float* V, float* bu, float* bi) {
     return guard([&] {
         check_handle(h);
+        if (h->ctx->multi()) {
+            MML_REQUIRE(h->has_model, "no model");
+            return multi_get_model(h, U, V, bu, bi);
+        }
         MML_REQUIRE(h->has_model, "no model (set_model first)");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
@@ -1824,6 +2119,19 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
                                       const int32_t* subepoch_sequence) {
     return guard([&] {
         check_handle(h);
+        if (h->ctx->multi()) {  // every device's epoch, then the item all-reduce (its thread)
+            MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
+            std::vector<float> ms(h->shards.size(), 0.0f);
+            mml::on_devices(h->ctx, [&](int32_t d) {
+                mml_status st = mml_bmf_iterate(h->shards[d], learn_rate, nullptr);
+                if (st == MML_OK) ms[d] = h->shards[d]->last_ms;
+                if (st == MML_OK) st = mml_bmf_allreduce_items(h->shards[d]);
+                return st;
+            });
+            h->last_ms = *std::max_element(ms.begin(), ms.end());
+            h->last_launches = h->shards[0]->last_launches;
+            return;
+        }
         MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
         const bool asym = is_asym(h);
         if (asym) {
@@ -1899,6 +2207,11 @@ extern "C" mml_status mml_bmf_predict(mml_bmf* h, const int32_t* users, const in
                                       int64_t n, float* out) {
     return guard([&] {
         check_handle(h);
+        if (h->ctx->multi()) {
+            MML_REQUIRE(n >= 0 && (n == 0 || (users && items && out)), "null arrays");
+            MML_REQUIRE(h->has_model, "no model");
+            return multi_predict(h, users, items, n, out);
+        }
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(n >= 0 && (n == 0 || (users && items && out)), "bad arguments");
         if (n == 0) return;
@@ -1921,6 +2234,11 @@ extern "C" mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const i
                                        const float* values, int64_t n, float* out) {
     return guard([&] {
         check_handle(h);
+        if (h->ctx->multi()) {
+            MML_REQUIRE(n >= 0 && (n == 0 || (users && items && values)) && out, "null arrays");
+            MML_REQUIRE(h->has_model, "no model");
+            return multi_evaluate(h, users, items, values, n, out);
+        }
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(n > 0 && users && items && values && out, "bad arguments");
         h->ctx->activate();
@@ -1955,6 +2273,7 @@ extern "C" mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const i
 extern "C" mml_status mml_bmf_objective(mml_bmf* h, double* out) {
     return guard([&] {
         check_handle(h);
+        single_device_only(h);
         MML_REQUIRE(h->has_model && h->has_data && out, "model, data and out required");
         MML_REQUIRE(h->p.model == MML_MF_BIASED,
                     "ComputeObjective is defined for BiasedMatrixFactorization only");
@@ -1988,9 +2307,10 @@ extern "C" mml_status mml_bmf_objective(mml_bmf* h, double* out) {
 extern "C" mml_status mml_bmf_allreduce_items(mml_bmf* h) {
     return guard([&] {
         check_handle(h);
+        single_device_only(h);
         MML_REQUIRE(h->has_model, "no model");
         mml_ctx* c = h->ctx;
-        if (c->nranks <= 1) return;
+        if (c->nranks <= 1 && !c->comm) return;  // no communicator: nothing to average
         MML_REQUIRE(c->comm, "context has no communicator (mml_ctx_comm_init)");
         MML_REQUIRE(!is_asym(h), "the asymmetric models' implicit factors are not averaged across ranks");
         c->activate();
@@ -2001,10 +2321,12 @@ extern "C" mml_status mml_bmf_allreduce_items(mml_bmf* h) {
         MML_RCCL(ncclAllReduce(h->bi.get(), h->bi.get(), (size_t)h->n_items, ncclFloat, ncclSum,
                                c->comm, st));
         MML_RCCL(ncclGroupEnd());
-        const float f = 1.0f / (float)c->nranks;
-        scale_kernel<<<grid_for((int64_t)nv), 256, 0, st>>>(h->V.get(), (int64_t)nv, f);
-        scale_kernel<<<grid_for(h->n_items), 256, 0, st>>>(h->bi.get(), h->n_items, f);
-        MML_HIP(hipGetLastError());
+        if (c->nranks > 1) {
+            const float f = 1.0f / (float)c->nranks;
+            scale_kernel<<<grid_for((int64_t)nv), 256, 0, st>>>(h->V.get(), (int64_t)nv, f);
+            scale_kernel<<<grid_for(h->n_items), 256, 0, st>>>(h->bi.get(), h->n_items, f);
+            MML_HIP(hipGetLastError());
+        }
         MML_HIP(hipStreamSynchronize(st));
     });
 }
@@ -2036,6 +2358,7 @@ extern "C" mml_status mml_bmf_fold_in(mml_bmf* h, int32_t n_fold, const int64_t*
                                       float learn_rate, float decay, float* out_vectors) {
     return guard([&] {
         check_handle(h);
+        single_device_only(h);
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(!is_asym(h), "the asymmetric models have their own FoldIn (not on the GPU path)");
         MML_REQUIRE(n_fold >= 0 && num_iter >= 0, "negative sizes");
@@ -2101,6 +2424,7 @@ extern "C" mml_status mml_bmf_predict_vectors(mml_bmf* h, int32_t n_vectors, con
                                               int64_t n, float* out) {
     return guard([&] {
         check_handle(h);
+        single_device_only(h);
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(!is_asym(h), "the asymmetric models have their own FoldIn (not on the GPU path)");
         MML_REQUIRE(n_vectors >= 0 && n >= 0, "negative sizes");
@@ -2141,6 +2465,7 @@ extern "C" mml_status mml_bmf_set_user_relation(mml_bmf* h, int32_t n_rows, cons
                                                 const int32_t* cols) {
     return guard([&] {
         check_handle(h);
+        single_device_only(h);
         MML_REQUIRE(h->p.model == MML_MF_SOCIAL, "the user relation belongs to SocialMF handles");
         MML_REQUIRE(n_rows >= 0 && n_rows <= h->n_users, "relation rows beyond the users");
         MML_REQUIRE(n_rows == 0 || offsets, "null offsets");
@@ -2190,6 +2515,7 @@ extern "C" mml_status mml_bmf_set_implicit_feedback(mml_bmf* h, int32_t side, in
                                                     const float* factors, const float* reg) {
     return guard([&] {
         check_handle(h);
+        single_device_only(h);
         MML_REQUIRE(is_asym(h), "implicit feedback belongs to the asymmetric models' handles");
         MML_REQUIRE(side == 0 || side == 1, "side must be 0 (lists per user) or 1 (per item)");
         MML_REQUIRE(uses_side(h, side), "this model does not use that side");
@@ -2231,6 +2557,7 @@ extern "C" mml_status mml_bmf_set_implicit_feedback(mml_bmf* h, int32_t side, in
 extern "C" mml_status mml_bmf_get_implicit_factors(mml_bmf* h, int32_t side, float* factors) {
     return guard([&] {
         check_handle(h);
+        single_device_only(h);
         MML_REQUIRE(side == 0 || side == 1, "side must be 0 or 1");
         MML_REQUIRE(h->has_slot[side], "no implicit factors on that side");
         MML_REQUIRE(factors, "null argument");
@@ -2243,6 +2570,7 @@ extern "C" mml_status mml_bmf_get_implicit_factors(mml_bmf* h, int32_t side, flo
 extern "C" mml_status mml_bmf_set_user_offsets(mml_bmf* h, const float* p) {
     return guard([&] {
         check_handle(h);
+        single_device_only(h);
         MML_REQUIRE(is_svdpp(h), "user offsets belong to SVD++ handles");
         MML_REQUIRE(p, "null argument");
         h->ctx->activate();
@@ -2257,6 +2585,7 @@ extern "C" mml_status mml_bmf_set_user_offsets(mml_bmf* h, const float* p) {
 extern "C" mml_status mml_bmf_get_user_offsets(mml_bmf* h, float* p) {
     return guard([&] {
         check_handle(h);
+        single_device_only(h);
         MML_REQUIRE(h->has_p, "no user offsets (set_user_offsets first)");
         MML_REQUIRE(p, "null argument");
         h->ctx->activate();

@@ -39,6 +39,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "mml_device.h"
 #include "mml_internal.h"
 
 namespace {
@@ -354,19 +355,28 @@ __device__ __forceinline__ int32_t bpr_group_fetch(int32_t v, int base, int lane
     }
 }
 
-template <int LPR, bool SOFT>
+// Access flags of the update kernel's item rows and biases (AM, a bit mask)
+constexpr int kBprLdL2 = 1;   // V_i, V_j, b_i, b_j loaded sc1: L2-served, past the CU's stale L1
+constexpr int kBprJThru = 2;  // V_j / b_j stored sc1: write-through, dropped from this XCD's L2
+constexpr int kBprIThru = 4;  // V_i / b_i stored sc1 as well: every item row lives memory-side
+
+// Triples split into ng group spans by the XCD group of i (mml_device.h group_wave); ng = 1: one span
+template <int LPR, bool SOFT, int AM>
 __global__ __launch_bounds__(256) void bpr_update_kernel(
     const int32_t* __restrict__ tu, const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
-    int64_t n_samples, int64_t chunk, float* U, float* V, float* bias, int32_t ld4, BprScalars s) {
+    const int64_t* __restrict__ goff, int32_t ng, int32_t waves_per_group, float* U, float* V,
+    float* bias, int32_t ld4, uint32_t v_bytes, uint32_t b_bytes, BprScalars s) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) +
-                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t begin = wave * chunk;
-    const int64_t end = min(begin + chunk, n_samples);
+    const mml::GroupWave gw = mml::group_wave(goff, ng, waves_per_group,
+                                              __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+                                              blockDim.x >> 6);
+    const int64_t begin = gw.begin, end = gw.end;
     const int sub = lane / LPR, q = lane % LPR;
     float4* U4 = reinterpret_cast<float4*>(U);
     float4* V4 = reinterpret_cast<float4*>(V);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t vrs = mml::buffer_rsrc(V, v_bytes);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t brs = mml::buffer_rsrc(bias, b_bytes);
     for (int64_t base = begin; base < end; base += 64) {
         const int64_t x = base + lane;
         const bool in = x < end;
@@ -383,9 +393,19 @@ __global__ __launch_bounds__(256) void bpr_update_kernel(
             const int64_t ou = (int64_t)u * ld4 + q, oi = (int64_t)i * ld4 + q,
                           oj = (int64_t)j * ld4 + q;
             const float4 w = U4[ou];
-            const float4 hi = V4[oi];
-            const float4 hj = V4[oj];
-            const float bi = bias[i], bj = bias[j];
+            float4 hi, hj;
+            float bi, bj;
+            if constexpr (!(AM & kBprLdL2)) {
+                hi = V4[oi];
+                hj = V4[oj];
+                bi = bias[i];
+                bj = bias[j];
+            } else {
+                hi = mml::load4_l2(vrs, (uint32_t)oi * 16u);
+                hj = mml::load4_l2(vrs, (uint32_t)oj * 16u);
+                bi = mml::load1_l2(brs, (uint32_t)i * 4u);
+                bj = mml::load1_l2(brs, (uint32_t)j * 4u);
+            }
             double part = (double)(w.x * (hi.x - hj.x));
             part += (double)(w.y * (hi.y - hj.y));
             part += (double)(w.z * (hi.z - hj.z));
@@ -397,16 +417,40 @@ __global__ __launch_bounds__(256) void bpr_update_kernel(
             if (t.skip) continue;
             if (q == 0) {  // i == j: the reference re-reads item_bias[j] after writing [i]
                 const float nbi = t.bias_i(s, bi);
-                bias[i] = nbi;
-                if (s.update_j) bias[j] = t.bias_j(s, i == j ? nbi : bj);
+                if constexpr ((AM & kBprIThru) != 0)
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, nbi), brs,
+                                                          (uint32_t)i * 4u, 0, 16);
+                else
+                    bias[i] = nbi;
+                if (s.update_j) {
+                    const float nbj = t.bias_j(s, i == j ? nbi : bj);
+                    if constexpr ((AM & kBprJThru) != 0)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, nbj),
+                                                              brs, (uint32_t)j * 4u, 0, 16);
+                    else
+                        bias[j] = nbj;
+                }
             }
             U4[ou] = make_float4(t.u(s, w.x, hi.x, hj.x), t.u(s, w.y, hi.y, hj.y),
                                  t.u(s, w.z, hi.z, hj.z), t.u(s, w.w, hi.w, hj.w));
-            V4[oi] = make_float4(t.i(s, w.x, hi.x), t.i(s, w.y, hi.y), t.i(s, w.z, hi.z),
-                                 t.i(s, w.w, hi.w));
-            if (s.update_j)
-                V4[oj] = make_float4(t.j(s, w.x, hj.x), t.j(s, w.y, hj.y), t.j(s, w.z, hj.z),
-                                     t.j(s, w.w, hj.w));
+            const float4 ni = make_float4(t.i(s, w.x, hi.x), t.i(s, w.y, hi.y),
+                                          t.i(s, w.z, hi.z), t.i(s, w.w, hi.w));
+            if constexpr ((AM & kBprIThru) != 0)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, ni), vrs,
+                    (uint32_t)oi * 16u, 0, 16);
+            else
+                V4[oi] = ni;
+            if (s.update_j) {
+                const float4 nj = make_float4(t.j(s, w.x, hj.x), t.j(s, w.y, hj.y),
+                                              t.j(s, w.z, hj.z), t.j(s, w.w, hj.w));
+                if constexpr ((AM & kBprJThru) != 0)
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, nj), vrs,
+                        (uint32_t)oj * 16u, 0, 16);
+                else
+                    V4[oj] = nj;
+            }
         }
     }
 }
@@ -509,6 +553,15 @@ struct mml_bpr {
     mml::DeviceArray<uint64_t> rank_keys, rank_sorted;  // USER_REPLACEMENT: (u << 32 | s)
     mml::DeviceArray<int64_t> rank_head;                // USER_REPLACEMENT: first position per user
     mml::DeviceArray<uint8_t> rank_tmp;                 // its radix-sort scratch
+    // Hogwild on XCD-owned item groups (xcd.hip): the epoch's triples partitioned by the group of
+    // i (stable), xt_* = the partitioned copy; span1 = {0, n} for the one-span launch
+    mml::XcdSplit xs;
+    mml::DeviceArray<int32_t> xt_u, xt_i, xt_j;
+    mml::DeviceArray<int64_t> span1;
+    bool has_groups = false;
+    // multi-device context: one single-device handle per GPU over a user range ub[d] .. ub[d + 1]
+    std::vector<mml_bpr*> shards;
+    std::vector<int32_t> ub;
     int64_t n_events = 0, nnz = 0;
     int32_t n_eligible = 0;
     bool has_data = false, has_model = false, has_order = false, has_triples = false;
@@ -534,6 +587,30 @@ void download_padded(mml_bpr* h, float* dst, const float* src, int64_t rows) {
 
 using mml::guard;
 
+// ------------------------------------------------------------------ multi-device handles
+// The one-process form of user-sharded BPRMF (the reference's parallel form is
+// MultiCoreBPRMF, MultiCoreBPRMF.cs:49-63): events split into contiguous user ranges of equal
+// event count, each device samples and updates its range (negatives over all items), and after
+// every epoch one RCCL all-reduce of V || b averages the item side.
+namespace {
+
+void bpr_single_device_only(const mml_bpr* h) {
+    if (h->ctx->multi())
+        mml::fail(MML_ERR_STATE, "not available on a multi-device context (user-sharded "
+                                 "Hogwild training, Predict and AUC only)");
+}
+
+std::vector<std::vector<int64_t>> bpr_route(const mml_bpr* h, const int32_t* users, int64_t n) {
+    std::vector<std::vector<int64_t>> r(h->shards.size());
+    for (int64_t x = 0; x < n; ++x) {
+        const int32_t u = users[x];
+        r[u >= 0 && u < h->n_users ? mml::owner_of(h->ub, u) : 0].push_back(x);
+    }
+    return r;
+}
+
+}  // namespace
+
 extern "C" mml_status mml_bpr_create(mml_ctx* ctx, const mml_bpr_params* params, int32_t n_users,
                                      int32_t n_items, mml_bpr** out) {
     return guard([&] {
@@ -550,6 +627,30 @@ extern "C" mml_status mml_bpr_create(mml_ctx* ctx, const mml_bpr_params* params,
         MML_REQUIRE(params->schedule >= MML_BPR_SCHEDULE_AUTO &&
                         params->schedule <= MML_BPR_SCHEDULE_ORDERED,
                     "unknown schedule");
+        if (ctx->multi()) {
+            MML_REQUIRE(params->schedule != MML_BPR_SCHEDULE_ORDERED,
+                        "a multi-device context trains with the HOGWILD / AUTO schedules");
+            auto* h = new mml_bpr();
+            h->ctx = ctx;
+            h->p = *params;
+            h->n_users = n_users;
+            h->n_items = n_items;
+            h->k = params->num_factors;
+            h->shards.assign(ctx->sub.size(), nullptr);
+            h->ub.assign(ctx->sub.size() + 1, n_users);
+            h->ub[0] = 0;
+            for (size_t d = 0; d < ctx->sub.size(); ++d) {
+                const mml_status st =
+                    mml_bpr_create(ctx->sub[d], params, n_users, n_items, &h->shards[d]);
+                if (st != MML_OK) {
+                    const std::string m = mml_last_error();
+                    mml_bpr_destroy(h);
+                    mml::fail(st, m);
+                }
+            }
+            *out = h;
+            return;
+        }
         ctx->activate();
         auto* h = new mml_bpr();
         try {
@@ -574,6 +675,12 @@ extern "C" mml_status mml_bpr_create(mml_ctx* ctx, const mml_bpr_params* params,
 extern "C" mml_status mml_bpr_destroy(mml_bpr* h) {
     return guard([&] {
         if (!h) return;
+        if (h->ctx && h->ctx->multi()) {
+            for (mml_bpr* s : h->shards)
+                if (s) mml_bpr_destroy(s);
+            delete h;
+            return;
+        }
         (void)hipSetDevice(h->ctx->device);
         (void)hipStreamSynchronize(h->ctx->stream);
         delete h;
@@ -617,6 +724,10 @@ void bpr_ingest(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t 
     MML_REQUIRE(h->p.sampler != MML_BPR_SAMPLER_USER_REPLACEMENT || n <= (int64_t)UINT32_MAX,
                 "USER_REPLACEMENT ranks samples with 32-bit indices: at most 2^32 - 1 events");
     h->has_triples = false;
+    h->has_groups = false;
+    h->span1.alloc(2);
+    const int64_t span[2] = {0, n};
+    MML_HIP(hipMemcpyAsync(h->span1.get(), span, sizeof(span), hipMemcpyHostToDevice, st));
     // PAIR: visit order; WEIGHTED / PAIR_REPLACEMENT: any order (events drawn by index)
     if (h->p.sampler != MML_BPR_SAMPLER_UNIFORM_USER &&
         h->p.sampler != MML_BPR_SAMPLER_USER_REPLACEMENT) {
@@ -637,6 +748,31 @@ extern "C" mml_status mml_bpr_set_data(mml_bpr* h, const int32_t* users, const i
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
         MML_REQUIRE(n >= 1 && users && items, "need >= 1 event");
+        if (h->ctx->multi()) {
+            if (order)
+                for (int64_t x = 0; x < n; ++x)
+                    MML_REQUIRE(order[x] >= 0 && order[x] < n, "order index out of range");
+            for (int64_t x = 0; x < n; ++x)
+                MML_REQUIRE(users[x] >= 0 && users[x] < h->n_users, "user id out of range");
+            const int32_t nd = (int32_t)h->shards.size();
+            h->ub = mml::balanced_user_bounds(users, n, h->n_users, nd);
+            std::vector<std::vector<int32_t>> su(nd), si(nd);
+            for (int64_t x = 0; x < n; ++x) {  // visit order (UNIFORM_PAIR), split by user owner
+                const int64_t o = order ? order[x] : x;
+                const int32_t d = mml::owner_of(h->ub, users[o]);
+                su[d].push_back(users[o]);
+                si[d].push_back(items[o]);
+            }
+            for (int32_t d = 0; d < nd; ++d)
+                MML_REQUIRE(!su[d].empty(), "a device's user range holds no event");
+            mml::on_devices(h->ctx, [&](int32_t d) {
+                return mml_bpr_set_data(h->shards[d], su[d].data(), si[d].data(),
+                                        (int64_t)su[d].size(), nullptr);
+            });
+            h->n_events = n;
+            h->has_data = true;
+            return;
+        }
         if (order)
             for (int64_t x = 0; x < n; ++x)
                 MML_REQUIRE(order[x] >= 0 && order[x] < n, "order index out of range");
@@ -662,6 +798,7 @@ extern "C" mml_status mml_bpr_set_data_device(mml_bpr* h, const int32_t* users,
                                               const int32_t* order) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        bpr_single_device_only(h);
         MML_REQUIRE(n >= 1 && users && items, "need >= 1 event");
         MML_REQUIRE(!order || (h->p.sampler != MML_BPR_SAMPLER_UNIFORM_USER &&
                                h->p.sampler != MML_BPR_SAMPLER_USER_REPLACEMENT),
@@ -676,6 +813,13 @@ extern "C" mml_status mml_bpr_set_model(mml_bpr* h, const float* U, const float*
                                         const float* item_bias) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) {
+            mml::on_devices(h->ctx, [&](int32_t d) {
+                return mml_bpr_set_model(h->shards[d], U, V, item_bias);
+            });
+            h->has_model = true;
+            return;
+        }
         MML_REQUIRE(U && V && item_bias, "null model arrays");
         h->ctx->activate();
         upload_padded(h, h->U.get(), U, h->n_users);
@@ -716,6 +860,13 @@ __global__ __launch_bounds__(256) void init_normal_kernel(float* __restrict__ M,
 extern "C" mml_status mml_bpr_init_model(mml_bpr* h, uint64_t seed, double mean, double stddev) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) {  // same seed on every device: one initial model
+            mml::on_devices(h->ctx, [&](int32_t d) {
+                return mml_bpr_init_model(h->shards[d], seed, mean, stddev);
+            });
+            h->has_model = true;
+            return;
+        }
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         init_normal_kernel<<<8192, 256, 0, st>>>(h->U.get(), h->n_users, h->k, h->ld, seed, mean,
@@ -732,6 +883,27 @@ extern "C" mml_status mml_bpr_init_model(mml_bpr* h, uint64_t seed, double mean,
 extern "C" mml_status mml_bpr_get_model(mml_bpr* h, float* U, float* V, float* item_bias) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) {
+            MML_REQUIRE(h->has_model, "no model");
+            mml::on_devices(h->ctx, [&](int32_t d) {
+                return mml::guard([&] {
+                    mml_bpr* s = h->shards[d];
+                    s->ctx->activate();
+                    const int64_t lo = h->ub[d], rows = h->ub[d + 1] - h->ub[d];
+                    if (U && rows > 0)
+                        download_padded(s, U + lo * h->k, s->U.get() + lo * s->ld, rows);
+                    if (d == 0) {
+                        if (V) download_padded(s, V, s->V.get(), h->n_items);
+                        if (item_bias)
+                            MML_HIP(hipMemcpyAsync(item_bias, s->bias.get(),
+                                                   sizeof(float) * h->n_items,
+                                                   hipMemcpyDeviceToHost, s->ctx->stream));
+                    }
+                    MML_HIP(hipStreamSynchronize(s->ctx->stream));
+                });
+            });
+            return;
+        }
         MML_REQUIRE(h->has_model, "no model");
         h->ctx->activate();
         if (U) download_padded(h, U, h->U.get(), h->n_users);
@@ -781,11 +953,95 @@ BprScalars scalars_of(const mml_bpr* h) {
     return s;
 }
 
+// How the Hogwild update kernel splits and accesses the item side (MML_BPR_XCD = 0 .. 4):
+//   0  one span over all XCDs, plain accesses (the round-1 kernel)
+//   1  XCD-owned groups of i, item loads sc1, plain stores
+//   2  the same, V_j / b_j stored write-through (sc1)
+//   3  the same, V_i / b_i stored write-through too
+//   4  one span, item loads sc1 and all item stores write-through (no owner: coherent item side)
+// Measured on the C3 replica (100k x 10k, tests/test_bpr_c3_replica_gpu.py): mode 1
+// collapses (AUC 0.60 vs 0.78: a foreign XCD's plain j store leaves a dirty, stale copy of a hot
+// row whose write-back reverts the owner's updates); modes 0 / 2 land +0.010 / +0.008 above the
+// sequential AUC (foreign XCDs read hot j rows as of the owner's last write-back).
+struct BprXcdMode {
+    bool partition;
+    int am;
+};
+BprXcdMode bpr_xcd_mode(int sampler) {
+    static const int env = [] {
+        const char* e = std::getenv("MML_BPR_XCD");
+        return e ? std::atoi(e) : -1;
+    }();
+    // WeightedBPRMF draws j by popularity: most j rows are hot rows of another XCD's group, so
+    // the groups do not apply (mid replica: mode 2 +0.114 AUC, mode 0 -0.004)
+    const int m = env >= 0 ? env : (sampler == MML_BPR_SAMPLER_WEIGHTED ? 0 : 2);
+    switch (m) {
+        case 1: return {true, kBprLdL2};
+        case 2: return {true, kBprLdL2 | kBprJThru};
+        case 3: return {true, kBprLdL2 | kBprJThru | kBprIThru};
+        case 4: return {false, kBprLdL2 | kBprJThru | kBprIThru};
+        default: return {false, 0};
+    }
+}
+
+template <int LPR, bool SOFT>
+void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff, const int32_t* tu,
+                       const int32_t* ti, const int32_t* tj, int64_t blocks, int wpb,
+                       const BprScalars& s, hipStream_t st) {
+    const int32_t wpg = (int32_t)(blocks / ng * wpb);
+    const uint32_t vb = (uint32_t)std::min<uint64_t>((uint64_t)h->n_items * h->ld * 4, 0xFFFFFFFFull);
+    const uint32_t bb = (uint32_t)((uint64_t)h->n_items * 4);
+#define MML_UPD(AM)                                                                             \
+    bpr_update_kernel<LPR, SOFT, AM><<<(int)blocks, 64 * wpb, 0, st>>>(                        \
+        tu, ti, tj, goff, ng, wpg, h->U.get(), h->V.get(), h->bias.get(), h->ld / 4, vb, bb, s)
+    switch (am) {
+        case kBprLdL2: MML_UPD(kBprLdL2); break;
+        case kBprLdL2 | kBprJThru: MML_UPD(kBprLdL2 | kBprJThru); break;
+        case kBprLdL2 | kBprJThru | kBprIThru: MML_UPD(kBprLdL2 | kBprJThru | kBprIThru); break;
+        default: MML_UPD(0); break;
+    }
+#undef MML_UPD
+}
+
+void launch_update(mml_bpr* h, bool soft, int am, int32_t ng, const int64_t* goff,
+                   const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t blocks,
+                   int wpb, const BprScalars& s, hipStream_t st) {
+#define MML_UPL(LPR)                                                                        \
+    if (soft) launch_update_lpr<LPR, true>(h, am, ng, goff, tu, ti, tj, blocks, wpb, s, st); \
+    else launch_update_lpr<LPR, false>(h, am, ng, goff, tu, ti, tj, blocks, wpb, s, st)
+    switch (h->lpr) {
+        case 1: MML_UPL(1); break;
+        case 2: MML_UPL(2); break;
+        case 4: MML_UPL(4); break;
+        case 8: MML_UPL(8); break;
+        case 16: MML_UPL(16); break;
+        case 32: MML_UPL(32); break;
+        default: MML_UPL(64); break;
+    }
+#undef MML_UPL
+    MML_HIP(hipGetLastError());
+}
+
 }  // namespace
 
 extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) {  // every device's epoch (its own sample stream), then the average
+            MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
+            const size_t nd = h->shards.size();
+            std::vector<float> ms(nd, 0.0f), ums(nd, 0.0f);
+            mml::on_devices(h->ctx, [&](int32_t d) {
+                mml_status st = mml_bpr_iterate(h->shards[d], seed + 0x9E3779B97F4A7C15ull * d);
+                ms[d] = h->shards[d]->last_ms;
+                ums[d] = h->shards[d]->last_update_ms;
+                if (st == MML_OK) st = mml_bpr_allreduce_items(h->shards[d]);
+                return st;
+            });
+            h->last_ms = *std::max_element(ms.begin(), ms.end());
+            h->last_update_ms = *std::max_element(ums.begin(), ums.end());
+            return;
+        }
         MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
@@ -805,9 +1061,14 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         // fewer than 16 waves' worth of samples run as ONE workgroup: one CU, one L2, where 2+
         // workgroups on different XCDs would each cache the hot item rows and overwrite each
         // other's updates on write-back (bmf.hip launch_hogwild)
-        if (waves < 16) waves = 4;
-        const int64_t blocks = (waves + 3) / 4;
-        waves = blocks * 4;
+        static const int64_t small_waves = [] {
+            const char* e = std::getenv("MML_BPR_SMALL_WAVES");
+            return e ? std::max<int64_t>(1, std::min<int64_t>(4, std::atoll(e))) : (int64_t)4;
+        }();
+        if (waves < 16) waves = small_waves;
+        // larger epochs: a multiple of 8 blocks, so each XCD group gets the same number of blocks
+        const int64_t blocks = waves < 16 ? 1 : (waves + 31) / 32 * 8;
+        if (blocks > 1) waves = blocks * 4;
         const int64_t chunk = (n + waves - 1) / waves;
         const bool pair = h->p.sampler == MML_BPR_SAMPLER_UNIFORM_PAIR;
         const bool soft = h->p.model == MML_BPR_MODEL_SOFT_MARGIN;
@@ -896,21 +1157,47 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
                               "negative item found in 65536 draws (the reference loops for ever)");
             }
         }
+        // XCD-owned item groups: the triples partitioned by the group of i (stable; part of the
+        // sampling phase), so that every access to V_i comes from the XCD that owns i
+        int32_t ng = 1;
+        const int64_t* goff = h->span1.get();
+        const int32_t *tu = h->tri_u.get(), *ti = h->tri_i.get(), *tj = h->tri_j.get();
+        const BprXcdMode xm = bpr_xcd_mode(h->p.sampler);
+        const bool v_fits = (uint64_t)h->n_items * h->ld * sizeof(float) < (1ull << 32);
+        const bool part = !ordered && !fused && n > 0 && waves >= 16 && xm.partition && v_fits &&
+                          mml::xcd_groups(h->ctx) == 8;
+        // the access flags need the buffer resource (V < 4 GiB) and, for the owner modes, the
+        // groups; a one-workgroup epoch keeps plain accesses (one CU, one L2)
+        const int am = v_fits && waves >= 16 && (part || !xm.partition) ? xm.am : 0;
+        if (part) {
+            if (!h->has_groups) {
+                h->xs.set_groups(st, mml::device_id_counts(st, h->cols.get(), h->nnz, h->n_items),
+                                 8);
+                h->has_groups = true;
+            }
+            if ((int64_t)h->xt_u.count < n) {
+                h->xt_u.alloc(n);
+                h->xt_i.alloc(n);
+                h->xt_j.alloc(n);
+            }
+            const int32_t* in[3] = {tu, ti, tj};
+            int32_t* out[3] = {h->xt_u.get(), h->xt_i.get(), h->xt_j.get()};
+            h->xs.partition(st, ti, n, 3, in, out);
+            ng = 8;
+            goff = h->xs.goff.get();
+            tu = h->xt_u.get();
+            ti = h->xt_i.get();
+            tj = h->xt_j.get();
+        }
         MML_HIP(hipEventRecord(h->ctx->ev_mid, st));
         if (ordered && n > 0)
             launch_apply_ordered(h, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), n, s, st);
+        if (!ordered && !fused && n > 0) {
+            launch_update(h, soft, am, ng, goff, tu, ti, tj, blocks, blocks == 1 ? (int)waves : 4,
+                          s, st);
+        } else if (fused) {
 #define MML_BPR(LPR)                                                                            \
-    if (ordered)                                                                                \
-        ;                                                                                       \
-    else if (!fused && soft)                                                                         \
-        bpr_update_kernel<LPR, true><<<(int)blocks, 256, 0, st>>>(                            \
-            h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), n, chunk, h->U.get(), h->V.get(),   \
-            h->bias.get(), h->ld / 4, s);                                                       \
-    else if (!fused)                                                                            \
-        bpr_update_kernel<LPR, false><<<(int)blocks, 256, 0, st>>>(                           \
-            h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), n, chunk, h->U.get(), h->V.get(),   \
-            h->bias.get(), h->ld / 4, s);                                                       \
-    else if (pair)                                                                              \
+    if (pair)                                                                                   \
         bpr_hogwild_kernel<LPR, true><<<(int)blocks, 256, 0, st>>>(                           \
             h->off.get(), h->cols.get(), h->eligible.get(), h->n_eligible, h->ev_u.get(),       \
             h->ev_i.get(), n, chunk, h->n_items, seed, h->U.get(), h->V.get(), h->bias.get(),   \
@@ -920,16 +1207,17 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             h->off.get(), h->cols.get(), h->eligible.get(), h->n_eligible, h->ev_u.get(),       \
             h->ev_i.get(), n, chunk, h->n_items, seed, h->U.get(), h->V.get(), h->bias.get(),   \
             h->ld / 4, s)
-        switch (h->lpr) {
-            case 1: MML_BPR(1); break;
-            case 2: MML_BPR(2); break;
-            case 4: MML_BPR(4); break;
-            case 8: MML_BPR(8); break;
-            case 16: MML_BPR(16); break;
-            case 32: MML_BPR(32); break;
-            default: MML_BPR(64); break;
-        }
+            switch (h->lpr) {
+                case 1: MML_BPR(1); break;
+                case 2: MML_BPR(2); break;
+                case 4: MML_BPR(4); break;
+                case 8: MML_BPR(8); break;
+                case 16: MML_BPR(16); break;
+                case 32: MML_BPR(32); break;
+                default: MML_BPR(64); break;
+            }
 #undef MML_BPR
+        }
         MML_HIP(hipGetLastError());
         MML_HIP(hipEventRecord(h->ctx->ev_end, st));
         MML_HIP(hipEventSynchronize(h->ctx->ev_end));
@@ -943,6 +1231,7 @@ extern "C" mml_status mml_bpr_last_triples(mml_bpr* h, int32_t* users, int32_t* 
                                            int32_t* other_items, int64_t n) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        bpr_single_device_only(h);
         MML_REQUIRE(h->has_triples, "no sampled epoch to report (run mml_bpr_iterate first; the "
                                     "MML_BPR_FUSED epoch keeps no triples)");
         MML_REQUIRE(n == h->n_events && users && items && other_items,
@@ -964,6 +1253,7 @@ extern "C" mml_status mml_bpr_apply_triples(mml_bpr* h, const int32_t* users,
                                              int64_t n) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        bpr_single_device_only(h);
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(n >= 0 && (n == 0 || (users && items && other_items)), "bad arguments");
         for (int64_t x = 0; x < n; ++x)
@@ -999,6 +1289,26 @@ extern "C" mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const in
                                       int64_t n, float* out) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) {
+            MML_REQUIRE(h->has_model, "no model");
+            MML_REQUIRE(n >= 0 && (n == 0 || (users && items && out)), "bad arguments");
+            const auto r = bpr_route(h, users, n);
+            mml::on_devices(h->ctx, [&](int32_t d) {
+                const auto& ix = r[d];
+                if (ix.empty()) return (mml_status)MML_OK;
+                std::vector<int32_t> u(ix.size()), i(ix.size());
+                std::vector<float> o(ix.size());
+                for (size_t x = 0; x < ix.size(); ++x) {
+                    u[x] = users[ix[x]];
+                    i[x] = items[ix[x]];
+                }
+                const mml_status st = mml_bpr_predict(h->shards[d], u.data(), i.data(),
+                                                      (int64_t)ix.size(), o.data());
+                for (size_t x = 0; st == MML_OK && x < ix.size(); ++x) out[ix[x]] = o[x];
+                return st;
+            });
+            return;
+        }
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(n >= 0 && (n == 0 || (users && items && out)), "bad arguments");
         if (n == 0) return;
@@ -1032,8 +1342,9 @@ __global__ __launch_bounds__(256) void bpr_scale_kernel(float* __restrict__ a, i
 extern "C" mml_status mml_bpr_allreduce_items(mml_bpr* h) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        bpr_single_device_only(h);
         mml_ctx* c = h->ctx;
-        if (c->nranks <= 1) return;
+        if (c->nranks <= 1 && !c->comm) return;  // no communicator: nothing to average
         MML_REQUIRE(c->comm, "context has no communicator (mml_ctx_comm_init)");
         c->activate();
         hipStream_t st = c->stream;
@@ -1043,10 +1354,13 @@ extern "C" mml_status mml_bpr_allreduce_items(mml_bpr* h) {
         MML_RCCL(ncclAllReduce(h->bias.get(), h->bias.get(), (size_t)h->n_items, ncclFloat,
                                ncclSum, c->comm, st));
         MML_RCCL(ncclGroupEnd());
-        const float f = 1.0f / (float)c->nranks;
-        bpr_scale_kernel<<<grid_for((int64_t)nv), 256, 0, st>>>(h->V.get(), (int64_t)nv, f);
-        bpr_scale_kernel<<<grid_for(h->n_items), 256, 0, st>>>(h->bias.get(), h->n_items, f);
-        MML_HIP(hipGetLastError());
+        if (c->nranks > 1) {
+            const float f = 1.0f / (float)c->nranks;
+            bpr_scale_kernel<<<grid_for((int64_t)nv), 256, 0, st>>>(h->V.get(), (int64_t)nv, f);
+            bpr_scale_kernel<<<grid_for(h->n_items), 256, 0, st>>>(h->bias.get(), h->n_items,
+                                                                    f);
+            MML_HIP(hipGetLastError());
+        }
         MML_HIP(hipStreamSynchronize(st));
     });
 }
@@ -1056,6 +1370,32 @@ extern "C" mml_status mml_bpr_auc(mml_bpr* h, const int32_t* candidates, int32_t
                                   const int32_t* test_items, double* out_auc) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) {  // each eval user on the device that holds its training items
+            MML_REQUIRE(h->has_model && h->has_data, "model and training data required");
+            MML_REQUIRE(n_users >= 0 && (n_users == 0 || (users && test_off && out_auc)),
+                        "bad arguments");
+            const auto r = bpr_route(h, users, n_users);
+            mml::on_devices(h->ctx, [&](int32_t d) {
+                const auto& ix = r[d];
+                if (ix.empty()) return (mml_status)MML_OK;
+                std::vector<int32_t> u(ix.size()), items;
+                std::vector<int64_t> off(ix.size() + 1, 0);
+                for (size_t x = 0; x < ix.size(); ++x) {
+                    u[x] = users[ix[x]];
+                    for (int64_t t = test_off[ix[x]]; t < test_off[ix[x] + 1]; ++t)
+                        items.push_back(test_items[t]);
+                    off[x + 1] = (int64_t)items.size();
+                }
+                std::vector<double> a(ix.size());
+                const mml_status st = mml_bpr_auc(h->shards[d], candidates, n_candidates,
+                                                  u.data(), (int32_t)ix.size(), off.data(),
+                                                  items.empty() ? nullptr : items.data(),
+                                                  a.data());
+                for (size_t x = 0; st == MML_OK && x < ix.size(); ++x) out_auc[ix[x]] = a[x];
+                return st;
+            });
+            return;
+        }
         MML_REQUIRE(h->has_model && h->has_data, "model and training data required");
         h->ctx->activate();
         mml::item_auc(h->ctx->stream, h->U.get(), h->ld, h->n_users, h->V.get(), h->ld, h->n_items,

@@ -58,9 +58,49 @@ extern "C" mml_status mml_ctx_create(int32_t device_id, mml_ctx** out) {
     });
 }
 
+extern "C" mml_status mml_ctx_create_multi(const int32_t* device_ids, int32_t n_devices,
+                                           mml_ctx** out) {
+    return guard([&] {
+        MML_REQUIRE(out && device_ids && n_devices >= 1, "need >= 1 device id");
+        for (int32_t a = 0; a < n_devices; ++a)
+            for (int32_t b = a + 1; b < n_devices; ++b)
+                MML_REQUIRE(device_ids[a] != device_ids[b], "duplicate device id");
+        auto* ctx = new mml_ctx();
+        try {
+            for (int32_t d = 0; d < n_devices; ++d) {
+                mml_ctx* s = nullptr;
+                const mml_status st = mml_ctx_create(device_ids[d], &s);
+                if (st != MML_OK) mml::fail(st, mml_last_error());
+                ctx->sub.push_back(s);
+            }
+            // one communicator over the devices, driven from this process (no unique-id exchange)
+            std::vector<ncclComm_t> comms(n_devices);
+            MML_RCCL(ncclCommInitAll(comms.data(), n_devices, device_ids));
+            for (int32_t d = 0; d < n_devices; ++d) {
+                ctx->sub[d]->comm = comms[d];
+                ctx->sub[d]->nranks = n_devices;
+                ctx->sub[d]->rank = d;
+            }
+            ctx->device = ctx->sub[0]->device;
+            ctx->stream = ctx->sub[0]->stream;
+            ctx->nranks = n_devices;
+        } catch (...) {
+            for (mml_ctx* s : ctx->sub) mml_ctx_destroy(s);
+            delete ctx;
+            throw;
+        }
+        *out = ctx;
+    });
+}
+
 extern "C" mml_status mml_ctx_destroy(mml_ctx* ctx) {
     return guard([&] {
         if (!ctx) return;
+        if (ctx->multi()) {
+            for (mml_ctx* s : ctx->sub) mml_ctx_destroy(s);
+            delete ctx;
+            return;
+        }
         (void)hipSetDevice(ctx->device);
         if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
         if (ctx->ev_begin) (void)hipEventDestroy(ctx->ev_begin);
@@ -70,6 +110,25 @@ extern "C" mml_status mml_ctx_destroy(mml_ctx* ctx) {
         delete ctx;
     });
 }
+
+namespace mml {
+std::vector<int32_t> balanced_user_bounds(const int32_t* users, int64_t n, int32_t n_users,
+                                          int32_t parts) {
+    std::vector<int64_t> c((size_t)n_users + 1, 0);
+    for (int64_t x = 0; x < n; ++x) c[(size_t)users[x] + 1]++;
+    for (int32_t u = 0; u < n_users; ++u) c[u + 1] += c[u];  // c[u] = ratings of users < u
+    std::vector<int32_t> b(parts + 1, n_users);
+    b[0] = 0;
+    for (int32_t r = 1; r < parts; ++r) {
+        // first user boundary whose prefix reaches r/parts of the ratings
+        const double target = (double)n * r / parts;
+        b[r] = (int32_t)(std::lower_bound(c.begin(), c.end(), (int64_t)std::ceil(target)) -
+                         c.begin());
+        b[r] = std::min(std::max(b[r], b[r - 1]), n_users);
+    }
+    return b;
+}
+}  // namespace mml
 
 extern "C" mml_status mml_comm_unique_id(uint8_t out_id[128]) {
     return guard([&] {

@@ -5,10 +5,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <exception>
 #include <new>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -133,14 +135,77 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                      const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
                      double alpha, double reg, int& launches);
 
+// XCD-owned item groups (xcd.hip): items dealt into 8 groups of equal weight, a stream partitioned
+// (stable) by the group of its item; group g's span goff[g] .. goff[g + 1] is served by blocks
+// b % 8 == g, which share one XCD and therefore one L2.
+struct XcdSplit {
+    int32_t ng = 1, n_items = 0;
+    DeviceArray<uint8_t> group;  // [n_items]
+    DeviceArray<int64_t> goff;   // [9], device
+    DeviceArray<int64_t> cnt, base;
+    DeviceArray<uint8_t> tmp;
+    void set_groups(hipStream_t st, const std::vector<int64_t>& weight, int32_t groups);
+    // out[c][...] = in[c][...] reordered by group(key[x]), stable; goff written on the device
+    void partition(hipStream_t st, const int32_t* key, int64_t n, int32_t npay,
+                   const int32_t* const* in, int32_t* const* out);
+};
+std::vector<uint8_t> balanced_item_groups(const std::vector<int64_t>& weight, int32_t ng);
+// occurrences of each id in [0, n_ids) of a device id array, on the host
+std::vector<int64_t> device_id_counts(hipStream_t st, const int32_t* ids, int64_t n,
+                                      int32_t n_ids);
+
+}  // namespace mml
+
+struct mml_ctx;
+namespace mml {
+// 8 when blocks b and b + 8 run on one XCD for every b of a 2,048-block grid (probed once per
+// context on the device; MML_XCD_GROUPS=1 forces 1), else 1
+int32_t xcd_groups(mml_ctx* ctx);
 }  // namespace mml
 
 struct mml_ctx {
+    // multi-device context (mml_ctx_create_multi): one single-device sub-context per GPU, each
+    // holding rank d of one ncclCommInitAll communicator; the fields below are sub[0]'s copies
+    std::vector<mml_ctx*> sub;
+    bool multi() const { return !sub.empty(); }
     int32_t device = 0;
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;
     int32_t nranks = 1;
     int32_t rank = 0;
+    int32_t xcd_groups = 0;  // mml::xcd_groups, 0 = not probed yet
     hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_mid = nullptr;
     void activate() const { MML_HIP(hipSetDevice(device)); }
 };
+
+namespace mml {
+// Runs f(d) -> mml_status for every device d of a multi-device context, each on a host thread of
+// its own (rank d drives its device and its communicator rank, so collectives inside f meet),
+// and turns the first failure into an exception carrying that thread's message.
+template <class F>
+void on_devices(const mml_ctx* ctx, F&& f) {
+    const size_t n = ctx->sub.size();
+    std::vector<mml_status> st(n, MML_OK);
+    std::vector<std::string> msg(n);
+    std::vector<std::thread> th;
+    th.reserve(n);
+    for (size_t d = 0; d < n; ++d)
+        th.emplace_back([&, d] {
+            st[d] = f((int32_t)d);
+            if (st[d] != MML_OK) msg[d] = mml_last_error();
+        });
+    for (auto& t : th) t.join();
+    for (size_t d = 0; d < n; ++d)
+        if (st[d] != MML_OK)
+            fail(st[d], "device " + std::to_string(ctx->sub[d]->device) + ": " + msg[d]);
+}
+
+// contiguous user ranges [b[d], b[d + 1]) with balanced rating counts (the multi-device shards;
+// distributed.balanced_user_shards's rule)
+std::vector<int32_t> balanced_user_bounds(const int32_t* users, int64_t n, int32_t n_users,
+                                          int32_t parts);
+inline int32_t owner_of(const std::vector<int32_t>& b, int32_t u) {
+    int32_t d = (int32_t)(std::upper_bound(b.begin(), b.end(), u) - b.begin()) - 1;
+    return d < 0 ? 0 : (d >= (int32_t)b.size() - 1 ? (int32_t)b.size() - 2 : d);
+}
+}  // namespace mml

@@ -544,6 +544,10 @@ struct mml_wrmf {
     // [ib[r], ib[r+1]) of V; the halves are exchanged by an all-gather (grouped broadcasts)
     std::vector<int64_t> udeg, ideg, ub, ib;
     int32_t shard_nranks = 0, shard_rank = -1;
+    // multi-device context: one single-device handle per GPU, each holding the whole data set
+    // and solving its row shards (rank d of the context's communicator); after every half-step
+    // the shards are all-gathered, so every device ends an iteration with the full model
+    std::vector<mml_wrmf*> shards;
 };
 
 namespace {
@@ -666,6 +670,26 @@ extern "C" mml_status mml_wrmf_create(mml_ctx* ctx, const mml_wrmf_params* param
         MML_REQUIRE(n_users >= 1 && n_items >= 1, "need >= 1 user and item");
         MML_REQUIRE(params->num_factors >= 1 && params->num_factors <= 256,
                     "num_factors must be in [1, 256]");
+        if (ctx->multi()) {
+            auto* h = new mml_wrmf();
+            h->ctx = ctx;
+            h->p = *params;
+            h->n_users = n_users;
+            h->n_items = n_items;
+            h->k = params->num_factors;
+            h->shards.assign(ctx->sub.size(), nullptr);
+            for (size_t d = 0; d < ctx->sub.size(); ++d) {
+                const mml_status st =
+                    mml_wrmf_create(ctx->sub[d], params, n_users, n_items, &h->shards[d]);
+                if (st != MML_OK) {
+                    const std::string m = mml_last_error();
+                    mml_wrmf_destroy(h);
+                    mml::fail(st, m);
+                }
+            }
+            *out = h;
+            return;
+        }
         ctx->activate();
         auto* h = new mml_wrmf();
         try {
@@ -692,6 +716,12 @@ extern "C" mml_status mml_wrmf_create(mml_ctx* ctx, const mml_wrmf_params* param
 extern "C" mml_status mml_wrmf_destroy(mml_wrmf* h) {
     return guard([&] {
         if (!h) return;
+        if (h->ctx && h->ctx->multi()) {
+            for (mml_wrmf* s : h->shards)
+                if (s) mml_wrmf_destroy(s);
+            delete h;
+            return;
+        }
         (void)hipSetDevice(h->ctx->device);
         (void)hipStreamSynchronize(h->ctx->stream);
         delete h;
@@ -702,6 +732,11 @@ extern "C" mml_status mml_wrmf_set_data(mml_wrmf* h, const int32_t* users, const
                                         int64_t n) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) {
+            mml::on_devices(h->ctx, [&](int32_t d) { return mml_wrmf_set_data(h->shards[d], users, items, n); });
+            h->has_data = true;
+            return;
+        }
         MML_REQUIRE(n >= 0 && (n == 0 || (users && items)), "bad event arrays");
         for (int64_t x = 0; x < n; ++x)
             MML_REQUIRE(users[x] >= 0 && users[x] < h->n_users && items[x] >= 0 &&
@@ -740,6 +775,7 @@ extern "C" mml_status mml_wrmf_set_data_device(mml_wrmf* h, const int32_t* users
                                                const int32_t* items, int64_t n) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(!h->ctx->multi(), "a multi-device context takes host arrays (set_data)");
         MML_REQUIRE(n >= 0 && (n == 0 || (users && items)), "bad event arrays");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
@@ -782,6 +818,11 @@ extern "C" mml_status mml_wrmf_init_model(mml_wrmf* h, uint64_t seed, double mea
                                           double stddev) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) {
+            mml::on_devices(h->ctx, [&](int32_t d) { return mml_wrmf_init_model(h->shards[d], seed, mean, stddev); });
+            h->has_model = true;
+            return;
+        }
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         wrmf_init_normal_kernel<<<8192, 256, 0, st>>>(h->U.get(), (int64_t)h->n_users * h->k, seed,
@@ -797,6 +838,11 @@ extern "C" mml_status mml_wrmf_init_model(mml_wrmf* h, uint64_t seed, double mea
 extern "C" mml_status mml_wrmf_set_model(mml_wrmf* h, const float* U, const float* V) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx && U && V, "null argument");
+        if (h->ctx->multi()) {
+            mml::on_devices(h->ctx, [&](int32_t d) { return mml_wrmf_set_model(h->shards[d], U, V); });
+            h->has_model = true;
+            return;
+        }
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         MML_HIP(hipMemcpyAsync(h->U.get(), U, sizeof(float) * h->n_users * h->k,
@@ -811,6 +857,9 @@ extern "C" mml_status mml_wrmf_set_model(mml_wrmf* h, const float* U, const floa
 extern "C" mml_status mml_wrmf_get_model(mml_wrmf* h, float* U, float* V) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) return (void)mml::on_devices(h->ctx, [&](int32_t d) {
+            return d == 0 ? mml_wrmf_get_model(h->shards[0], U, V) : (mml_status)MML_OK;
+        });
         MML_REQUIRE(h->has_model, "no model");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
@@ -827,6 +876,17 @@ extern "C" mml_status mml_wrmf_get_model(mml_wrmf* h, float* U, float* V) {
 extern "C" mml_status mml_wrmf_iterate(mml_wrmf* h) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) {  // every device solves its row shards; all-gathers inside
+            std::vector<float> ms(h->shards.size(), 0.0f);
+            mml::on_devices(h->ctx, [&](int32_t d) {
+                const mml_status st = mml_wrmf_iterate(h->shards[d]);
+                ms[d] = h->shards[d]->last_ms;
+                return st;
+            });
+            h->last_ms = *std::max_element(ms.begin(), ms.end());
+            h->last_launches = h->shards[0]->last_launches;
+            return;
+        }
         MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
@@ -861,6 +921,10 @@ extern "C" mml_status mml_wrmf_predict(mml_wrmf* h, const int32_t* users, const 
                                        int64_t n, float* out) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) return (void)mml::on_devices(h->ctx, [&](int32_t d) {
+            return d == 0 ? mml_wrmf_predict(h->shards[0], users, items, n, out)
+                          : (mml_status)MML_OK;
+        });
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(n >= 0 && (n == 0 || (users && items && out)), "bad arguments");
         if (n == 0) return;
@@ -889,6 +953,11 @@ extern "C" mml_status mml_wrmf_auc(mml_wrmf* h, const int32_t* candidates, int32
                                    const int32_t* test_items, double* out_auc) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) return (void)mml::on_devices(h->ctx, [&](int32_t d) {
+            return d == 0 ? mml_wrmf_auc(h->shards[0], candidates, n_candidates, users, n_users,
+                                         test_off, test_items, out_auc)
+                          : (mml_status)MML_OK;
+        });
         MML_REQUIRE(h->has_model && h->has_data, "model and training data required");
         h->ctx->activate();
         mml::item_auc(h->ctx->stream, h->U.get(), h->k, h->n_users, h->V.get(), h->k, h->n_items,

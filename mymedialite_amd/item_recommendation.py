@@ -159,7 +159,7 @@ class _MFBase(Recommender):
 
 class BPRMF(_MFBase):
     PROPERTIES = {
-        "BiasReg": "float", "Device": "int", "InitMean": "double", "InitStdDev": "double",
+        "BiasReg": "float", "Device": "int", "Gpus": "string", "InitMean": "double", "InitStdDev": "double",
         "LearnRate": "float", "NumFactors": "uint", "NumIter": "uint", "RegI": "float",
         "RegJ": "float", "RegU": "float", "Schedule": "string", "UniformUserSampling": "bool",
         "UpdateJ": "bool", "WithReplacement": "bool",
@@ -192,7 +192,7 @@ class BPRMF(_MFBase):
 
     def _load_device_model(self, U, V, bias):
         self._release()
-        self._ctx = N.Context(self.Device)
+        self._ctx = N.Context(N.device_arg(self))
         p = self._params()
         h = N._vp()
         N.check(N.lib().mml_bpr_create(self._ctx.handle, ctypes.byref(p), U.shape[0], V.shape[0],
@@ -243,7 +243,7 @@ class BPRMF(_MFBase):
         U, V = self._init_factors()
         bias = np.zeros(self.MaxItemID + 1, np.float32)
         self._release()
-        self._ctx = N.Context(self.Device)
+        self._ctx = N.Context(N.device_arg(self))
         p = self._params()
         h = N._vp()
         N.check(N.lib().mml_bpr_create(self._ctx.handle, ctypes.byref(p), self.MaxUserID + 1,
@@ -365,7 +365,7 @@ class SoftMarginRankingMF(BPRMF):
 
 class WRMF(_MFBase):
     PROPERTIES = {
-        "Alpha": "double", "Device": "int", "InitMean": "double", "InitStdDev": "double",
+        "Alpha": "double", "Device": "int", "Gpus": "string", "InitMean": "double", "InitStdDev": "double",
         "NumFactors": "uint", "NumIter": "uint", "Regularization": "double",
     }
 
@@ -384,7 +384,7 @@ class WRMF(_MFBase):
 
     def _load_device_model(self, U, V, bias):
         self._release()
-        self._ctx = N.Context(self.Device)
+        self._ctx = N.Context(N.device_arg(self))
         p = N.WrmfParams(int(self.NumFactors), 0, float(self.Alpha), float(self.Regularization))
         h = N._vp()
         N.check(N.lib().mml_wrmf_create(self._ctx.handle, ctypes.byref(p), U.shape[0], V.shape[0],
@@ -397,7 +397,7 @@ class WRMF(_MFBase):
         """MF.InitModel (MF.cs:51-58) + the feedback sets on the device."""
         U, V = self._init_factors()
         self._release()
-        self._ctx = N.Context(self.Device)
+        self._ctx = N.Context(N.device_arg(self))
         p = N.WrmfParams(int(self.NumFactors), 0, float(self.Alpha), float(self.Regularization))
         h = N._vp()
         N.check(N.lib().mml_wrmf_create(self._ctx.handle, ctypes.byref(p), self.MaxUserID + 1,

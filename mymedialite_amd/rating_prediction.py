@@ -37,7 +37,7 @@ class MatrixFactorization(Recommender):
     current_learnrate *= Decay).  Schedule: ``auto``/``ordered`` = the reference's sequential loop
     (exact), ``hogwild`` / ``hogwild_coherent`` = the lock-free GPU epoch."""
     PROPERTIES = {
-        "Decay": "float", "Device": "int", "InitMean": "double", "InitStdDev": "double",
+        "Decay": "float", "Device": "int", "Gpus": "string", "InitMean": "double", "InitStdDev": "double",
         "LearnRate": "float", "NumFactors": "uint", "NumIter": "uint", "Regularization": "float",
         "Schedule": "string",
     }
@@ -94,7 +94,7 @@ class MatrixFactorization(Recommender):
 
     def _create_handle(self, nu, ni):
         self._release()
-        self._ctx = N.Context(self.Device)
+        self._ctx = N.Context(N.device_arg(self))
         h = N._vp()
         N.check(N.lib().mml_bmf_create(self._ctx.handle, N.ctypes.byref(self._params()), nu, ni,
                                        N.ctypes.byref(h)))
@@ -310,7 +310,7 @@ class MatrixFactorization(Recommender):
 class BiasedMatrixFactorization(MatrixFactorization):
     PROPERTIES = {
         "BiasLearnRate": "float", "BiasReg": "float", "BoldDriver": "bool", "Decay": "float",
-        "Device": "int", "FrequencyRegularization": "bool", "InitMean": "double",
+        "Device": "int", "Gpus": "string", "FrequencyRegularization": "bool", "InitMean": "double",
         "InitStdDev": "double", "LearnRate": "float", "Loss": tuple(_LOSS), "MaxThreads": "int",
         "NaiveParallelization": "bool", "NumFactors": "uint", "NumIter": "uint",
         "RegI": "float", "RegU": "float", "Regularization": "float", "Schedule": "string",

@@ -773,6 +773,24 @@ def bpr_train(users, items, n_users, n_items, *, seed=1, k=10, num_iter=30, lear
                 num_burn=num_burn, off=off, rows=rows)
 
 
+def bpr_epoch(rng: Rng, users, items, n_users, n_items, U, V, bias, *, learn_rate=0.05,
+              reg_u=0.0025, reg_i=0.0025, reg_j=0.00025, bias_reg=0.0, update_j=True,
+              model="BPRMF", sampler="uniform_user"):
+    """One BPRMF.Iterate() (BPRMF.cs:160-178) on (users, items) from the given model state and
+    RNG, in place: Feedback.Count samples (e.g. one rank's user shard of MultiCoreBPRMF-style
+    data parallelism, MultiCoreBPRMF.cs:49-63)."""
+    users, items = i32(users), i32(items)
+    k = U.shape[1]
+    off, rows = insertion_order_rows(users, items, n_users)
+    srt = sorted_rows(off, rows)
+    p = _BprParams(k, 1, 1, int(update_j), learn_rate, reg_u, reg_i, reg_j, bias_reg, n_users - 1,
+                   n_items - 1, BPR_MODEL[model], BPR_SAMPLER[sampler], users.ctypes.data,
+                   items.ctypes.data, len(users))
+    lib().ora_bpr_epoch(rng._buf, ctypes.byref(p), _p(off, _i64p), _p(rows, _i32p),
+                        _p(srt, _i32p), len(users), _p(U, _f32p), _p(V, _f32p), _p(bias, _f32p),
+                        None)
+
+
 def bpr_update(u, i, j, U, V, bias, *, learn_rate=0.05, reg_u=0.0025, reg_i=0.0025,
                reg_j=0.00025, bias_reg=0.0, update_u=True, update_i=True, update_j=True,
                model="BPRMF"):

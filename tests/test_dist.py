@@ -102,6 +102,26 @@ def test_two_rank_user_shards_with_item_averaging(tmp_path):
                        np.float32(4))
     assert rm2 < O.rating_eval(p0, v)[0]
     assert bnd[1] > 0
+    # ... and equals the same decomposition emulated in one process, bit for bit
+    r = O.Rng(1)
+    U0 = r.fill_normal(400 * 8, 0, 0.1).reshape(400, 8)
+    V0 = r.fill_normal(120 * 8, 0, 0.1).reshape(120, 8)
+    st = [(U0.copy(), V0.copy(), np.zeros(400, np.float32), np.zeros(120, np.float32))
+          for _ in range(2)]
+    kw = dict(gb=gb, min_rating=np.float32(1), range_=np.float32(4), lr=np.float32(0.01))
+    for _ in range(3):
+        for x, (Ux, Vx, bux, bix) in enumerate(st):
+            su, si, sv = shard_ratings(u, i, v, bnd, x)
+            O.bmf_iterate(su, si, sv, np.arange(len(su), dtype=np.int32), Ux, Vx, bux, bix, **kw)
+        Vm = (st[0][1] + st[1][1]) / np.float32(2)
+        bm = (st[0][3] + st[1][3]) / np.float32(2)
+        for _, Vx, _, bix in st:
+            Vx[:] = Vm
+            bix[:] = bm
+    np.testing.assert_array_equal(V, st[0][1])
+    np.testing.assert_array_equal(bi, st[0][3])
+    np.testing.assert_array_equal(U[:bnd[1]], st[0][0][:bnd[1]])
+    np.testing.assert_array_equal(U[bnd[1]:], st[1][0][bnd[1]:])
 
 
 # ------------------------------------------------------------------ WRMF row shards + all-gather
@@ -179,3 +199,96 @@ def test_two_rank_wrmf_row_shards_equal_single_process(tmp_path):
     u, i = synth_feedback(9, 300, 140, 25)
     st = O.wrmf_train(u, i, 300, 140, seed=4, k=6, num_iter=2)
     np.testing.assert_array_equal(a, np.concatenate([st["U"].ravel(), st["V"].ravel()]))
+
+
+# ------------------------------------------------------------------ BPRMF user shards + averaging
+def _bpr_shard_epochs(rank, world, U, V, b, epochs, allreduce):
+    """rank's part of user-sharded BPRMF (bench.py --workload c3 at N > 1): BPRMF.Iterate() over
+    the rank's events (negatives over all items; SampleUser only finds the rank's users), then
+    V || b averaged over the ranks (mml_bpr_allreduce_items)."""
+    import oracle as O
+    from golden_cases import synth_feedback
+    from mymedialite_amd.distributed import balanced_user_shards
+    u, i = synth_feedback(11, 240, 90, 20)
+    nu, ni = 240, 90
+    bnd = balanced_user_shards(np.bincount(u, minlength=nu), world)
+    m = (u >= bnd[rank]) & (u < bnd[rank + 1])
+    rng = O.Rng(100 + rank)
+    for _ in range(epochs):
+        O.bpr_epoch(rng, u[m], i[m], nu, ni, U, V, b)
+        allreduce(V, b)
+    return bnd
+
+
+def _bpr_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tests")]
+    import torch
+    import torch.distributed as dist
+
+    import oracle as O
+    from mymedialite_amd.distributed import init_host_group
+
+    init_host_group(world)
+    r = O.Rng(3)
+    U = r.fill_normal(240 * 6, 0, 0.1).reshape(240, 6)
+    V = r.fill_normal(90 * 6, 0, 0.1).reshape(90, 6)
+    b = np.zeros(90, np.float32)
+
+    def allreduce(V, b):
+        t = torch.from_numpy(np.concatenate([V.ravel(), b]))
+        dist.all_reduce(t)
+        t /= world
+        V[:] = t[: V.size].numpy().reshape(V.shape)
+        b[:] = t[V.size:].numpy()
+
+    bnd = _bpr_shard_epochs(rank, world, U, V, b, 3, allreduce)
+    lo, hi = bnd[rank], bnd[rank + 1]
+    np.save(os.path.join(out_dir, f"b{rank}.npy"),
+            np.concatenate([V.ravel(), b, U[lo:hi].ravel()]).astype(np.float32))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_bpr_user_shards_equal_emulation(tmp_path):
+    """User-sharded BPRMF with per-epoch item averaging over 2 gloo ranks equals the same
+    decomposition emulated in one process bit for bit (the sum of two floats halved is exact and
+    order-free), and the averaged model ranks held-in positives above random items."""
+    world = 2
+    mp.spawn(_bpr_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    a, c = np.load(tmp_path / "b0.npy"), np.load(tmp_path / "b1.npy")
+    nv = 90 * 6 + 90
+    np.testing.assert_array_equal(a[:nv], c[:nv])  # one item side on every rank
+
+    import oracle as O
+    r = O.Rng(3)
+    U0 = r.fill_normal(240 * 6, 0, 0.1).reshape(240, 6)
+    V0 = r.fill_normal(90 * 6, 0, 0.1).reshape(90, 6)
+    states = [(U0.copy(), V0.copy(), np.zeros(90, np.float32)) for _ in range(world)]
+    rngs = [O.Rng(100 + x) for x in range(world)]
+    from golden_cases import synth_feedback
+    from mymedialite_amd.distributed import balanced_user_shards
+    u, i = synth_feedback(11, 240, 90, 20)
+    bnd = balanced_user_shards(np.bincount(u, minlength=240), world)
+    for _ in range(3):
+        for x, (U, V, b) in enumerate(states):
+            m = (u >= bnd[x]) & (u < bnd[x + 1])
+            O.bpr_epoch(rngs[x], u[m], i[m], 240, 90, U, V, b)
+        Vm = (states[0][1] + states[1][1]) / np.float32(2)
+        bm = (states[0][2] + states[1][2]) / np.float32(2)
+        for U, V, b in states:
+            V[:] = Vm
+            b[:] = bm
+    np.testing.assert_array_equal(a[:90 * 6], states[0][1].ravel())
+    np.testing.assert_array_equal(a[90 * 6:nv], states[0][2])
+    U = np.concatenate([a[nv:], c[nv:]]).reshape(240, 6)
+    np.testing.assert_array_equal(U[:bnd[1]], states[0][0][:bnd[1]])
+    np.testing.assert_array_equal(U[bnd[1]:], states[1][0][bnd[1]:])
+    # learned something: training positives score above the average item for most users
+    V = states[0][1]
+    s = U @ V.T + states[0][2]
+    pos = s[u, i].mean()
+    assert pos > s.mean() + 0.01

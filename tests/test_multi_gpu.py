@@ -1,0 +1,145 @@
+"""Multi-device contexts and the library's RCCL call paths on the GPU box.
+
+The box has one GPU, so the collectives run on 1-rank communicators: the RCCL calls inside
+mml_bmf_allreduce_items / mml_bpr_allreduce_items / the WRMF row all-gather execute (an all-reduce
+over one rank is the identity), and the one-process multi-device handles (mml_ctx_create_multi,
+``Gpus=0``) run their shard / route / gather logic over one shard.  The N > 1 decompositions are
+covered by the gloo tests in tests/test_dist.py and run on 8 GPUs in the driver's scaling bench.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_cases import synth_feedback, synth_ratings
+from mymedialite_amd import (BPRMF, WRMF, BiasedMatrixFactorization, PosOnlyFeedback, Random,
+                             Ratings)
+from mymedialite_amd import _native as N
+from test_bpr_gpu import planted_feedback
+
+pytestmark = pytest.mark.gpu
+
+
+def test_xcd_groups_probe():
+    """Blocks b and b + 8 of a 2,048-block grid share an XCD on the MI355X, so the Hogwild
+    kernels' XCD-owned item groups apply (mml_ctx_xcd_groups)."""
+    ctx = N.Context(0)
+    assert ctx.xcd_groups() == 8
+
+
+def _one_rank_ctx():
+    ctx = N.Context(0)
+    ctx.comm_init(N.Context.unique_id(), 1, 0)
+    return ctx
+
+
+def test_bmf_allreduce_items_one_rank_communicator():
+    """mml_bmf_allreduce_items through a real (1-rank) RCCL communicator: the call path runs and
+    the item side is unchanged (sum over one rank, no 1/N scaling)."""
+    u, i, v = synth_ratings(3, 300, 120, 8000)
+    ctx = _one_rank_ctx()
+    k = 16
+    p = N.BmfParams(k, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
+    h = N._vp()
+    N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(p), 300, 120, ctypes.byref(h)))
+    N.check(N.lib().mml_bmf_set_data(h, N.ptr(u, N._i32p), N.ptr(i, N._i32p),
+                                     N.ptr(v, N._f32p), len(u), None))
+    N.check(N.lib().mml_bmf_init_model(h, 3, 0.0, 0.1, 0.2, 1.0, 5.0))
+    N.check(N.lib().mml_bmf_iterate(h, 0.01, None))
+    got = [np.zeros(s, np.float32) for s in (300 * k, 120 * k, 300, 120)]
+    N.check(N.lib().mml_bmf_get_model(h, *[N.ptr(a, N._f32p) for a in got]))
+    N.check(N.lib().mml_bmf_allreduce_items(h))
+    after = [np.zeros(s, np.float32) for s in (300 * k, 120 * k, 300, 120)]
+    N.check(N.lib().mml_bmf_get_model(h, *[N.ptr(a, N._f32p) for a in after]))
+    for a, b in zip(got, after):
+        np.testing.assert_array_equal(a, b)
+    # init_model: users / items without ratings keep zero rows
+    assert np.all(got[0].reshape(300, k)[np.bincount(u, minlength=300) == 0] == 0)
+    N.lib().mml_bmf_destroy(h)
+
+
+def test_bpr_allreduce_items_one_rank_communicator():
+    tr_u, tr_i, _, _ = planted_feedback(2, 500, 80, 10)
+    ctx = _one_rank_ctx()
+    p = N.BprParams(8, N.BPR_SAMPLER_UNIFORM_USER, 1, 0.05, 0.0025, 0.0025, 0.00025, 0.0, 0,
+                    N.BPR_SCHEDULE_HOGWILD)
+    h = N._vp()
+    N.check(N.lib().mml_bpr_create(ctx.handle, ctypes.byref(p), 500, 80, ctypes.byref(h)))
+    N.check(N.lib().mml_bpr_set_data(h, N.ptr(tr_u, N._i32p), N.ptr(tr_i, N._i32p), len(tr_u),
+                                     None))
+    N.check(N.lib().mml_bpr_init_model(h, 5, 0.0, 0.1))
+    N.check(N.lib().mml_bpr_iterate(h, 11))
+    V0, b0 = np.zeros(80 * 8, np.float32), np.zeros(80, np.float32)
+    N.check(N.lib().mml_bpr_get_model(h, None, N.ptr(V0, N._f32p), N.ptr(b0, N._f32p)))
+    N.check(N.lib().mml_bpr_allreduce_items(h))
+    V1, b1 = np.zeros(80 * 8, np.float32), np.zeros(80, np.float32)
+    N.check(N.lib().mml_bpr_get_model(h, None, N.ptr(V1, N._f32p), N.ptr(b1, N._f32p)))
+    np.testing.assert_array_equal(V0, V1)
+    np.testing.assert_array_equal(b0, b1)
+    N.lib().mml_bpr_destroy(h)
+
+
+def test_bmf_multi_device_context_one_shard():
+    """BiasedMatrixFactorization with Gpus=0 (mml_ctx_create_multi over one device): the user-
+    shard path trains, Predict / Evaluate route through the shard, and the model gathered from it
+    predicts exactly what a single-device handle with that model predicts."""
+    u, i, v = synth_ratings(5, 2000, 300, 120_000)
+    tu, ti, tv = synth_ratings(6, 2000, 300, 5000)
+    res = {}
+    for name, props in (("single", dict(Device=0)), ("multi", dict(Gpus="0"))):
+        Random.set_seed(4)
+        m = BiasedMatrixFactorization(NumFactors=16, NumIter=3, Schedule="hogwild", **props)
+        m.ratings = Ratings(u, i, v)
+        m.train()
+        res[name] = (m, m.evaluate(Ratings(tu, ti, tv))["RMSE"])
+    m, rmse = res["multi"]
+    assert m._ctx.nranks == 1
+    assert abs(rmse - res["single"][1]) < 5e-3, (rmse, res["single"][1])
+    md = m.get_model()
+    q = BiasedMatrixFactorization(NumFactors=16, NumIter=0, Schedule="hogwild")
+    q.ratings = Ratings(u, i, v)
+    q.train()
+    N.check(N.lib().mml_bmf_set_model(q._h, N.ptr(md["U"], N._f32p), N.ptr(md["V"], N._f32p),
+                                      N.ptr(md["bu"], N._f32p), N.ptr(md["bi"], N._f32p),
+                                      m.global_bias, float(m.ratings.scale_min),
+                                      float(m.ratings.scale_max)))
+    qu = np.concatenate([tu[:500], [2500]]).astype(np.int32)  # + an unknown user
+    qi = np.concatenate([ti[:500], [3]]).astype(np.int32)
+    np.testing.assert_array_equal(m.predict(qu, qi), q.predict(qu, qi))
+    # the exact schedules are single-device only
+    with pytest.raises(N.MMLError, match="HOGWILD"):
+        m2 = BiasedMatrixFactorization(NumFactors=4, NumIter=1, Schedule="ordered", Gpus="0")
+        m2.ratings = Ratings(u, i, v)
+        m2.train()
+
+
+def test_bpr_multi_device_context_one_shard():
+    tr_u, tr_i, te_u, te_i = planted_feedback(1, 3000, 400, 20)
+    aucs = {}
+    for name, props in (("single", dict(Device=0)), ("multi", dict(Gpus="0"))):
+        Random.set_seed(5)
+        m = BPRMF(NumFactors=16, NumIter=10, Schedule="hogwild", **props)
+        m.feedback = PosOnlyFeedback(tr_u, tr_i)
+        m.train()
+        aucs[name] = m.evaluate_auc(PosOnlyFeedback(te_u, te_i))["AUC"]
+    print("BPR AUC single / multi(1 shard):", aucs)
+    assert aucs["multi"] > 0.6
+    assert abs(aucs["multi"] - aucs["single"]) < 0.02
+
+
+def test_wrmf_multi_device_context_equals_single():
+    """WRMF is deterministic: one shard of a multi-device context solves every row exactly as the
+    single-device handle does (rows are independent within a half-step)."""
+    u, i = synth_feedback(9, 300, 140, 25)
+    out = {}
+    for name, props in (("single", dict(Device=0)), ("multi", dict(Gpus="0"))):
+        Random.set_seed(4)
+        m = WRMF(NumFactors=6, NumIter=2, **props)
+        m.feedback = PosOnlyFeedback(u, i)
+        m.train()
+        out[name] = (m.user_factors.copy(), m.item_factors.copy())
+    np.testing.assert_array_equal(out["multi"][0], out["single"][0])
+    np.testing.assert_array_equal(out["multi"][1], out["single"][1])
+    st = O.wrmf_train(u, i, 300, 140, seed=4, k=6, num_iter=2)
+    assert np.max(np.abs(out["multi"][0] - st["U"])) <= 1e-5 * (1 + np.max(np.abs(st["U"])))
