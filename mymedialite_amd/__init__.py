@@ -5,7 +5,10 @@ include/mml.h); this package is the host-side mirror of the reference's recommen
 """
 from .data import IdentityMapping, Mapping, PosOnlyFeedback, Ratings, read_items, read_ratings
 from .random import Random, SystemRandom
-from .item_recommendation import BPRMF, WRMF, SoftMarginRankingMF, WeightedBPRMF
+from .recommender import (create_item_recommender, create_rating_predictor, create_recommender,
+                          list_recommenders)
+from .item_recommendation import (BPRMF, WRMF, MultiCoreBPRMF, SoftMarginRankingMF,
+                                  WeightedBPRMF)
 from .rating_prediction import (BiasedMatrixFactorization, MatrixFactorization,
                                 SigmoidItemAsymmetricFactorModel,
                                 SigmoidUserAsymmetricFactorModel, SocialMF,
@@ -15,6 +18,7 @@ from .rating_prediction import (BiasedMatrixFactorization, MatrixFactorization,
 __all__ = ["BiasedMatrixFactorization", "MatrixFactorization", "SocialMF",
            "SigmoidItemAsymmetricFactorModel", "SigmoidUserAsymmetricFactorModel",
            "SigmoidCombinedAsymmetricFactorModel", "SVDPlusPlus", "SigmoidSVDPlusPlus", "BPRMF", "WRMF",
-           "SoftMarginRankingMF", "WeightedBPRMF", "Ratings",
+           "SoftMarginRankingMF", "WeightedBPRMF", "MultiCoreBPRMF", "Ratings",
            "PosOnlyFeedback", "Mapping", "IdentityMapping", "read_ratings", "read_items", "Random",
-           "SystemRandom"]
+           "SystemRandom", "create_rating_predictor", "create_item_recommender",
+           "create_recommender", "list_recommenders"]

@@ -264,11 +264,16 @@ __device__ __forceinline__ T group_fetch(T v, int base, int lane) {
 // RMSE gain at that scale, so it is not kept.  VPL > 1 puts more ratings in one wave
 // step (64 / LPR): more rows in flight per wave and the per-rating scalar part (sigmoid, fp64
 // gradient) shared by fewer lanes.
-// Access modes of the Hogwild kernel's rows and biases
+// Access flags of the Hogwild kernel's rows and biases (AM, a bit mask)
 constexpr int kAccPlain = 0;     // plain loads / stores
 constexpr int kAccCoherent = 1;  // every row / bias access agent-coherent (sc1), HOGWILD_COHERENT
 constexpr int kAccItemL2 = 2;    // XCD-owned item groups: item rows / biases loaded sc1 (L2-served,
                                  // past the CU's stale L1), stored plain (kept in the owning L2)
+constexpr int kAccUserThru = 4;  // user rows / biases loaded sc1 and stored sc1 (write-through,
+                                 // dropped from this XCD's L2): a user's next rating, on any XCD,
+                                 // reads the row from memory instead of a stale L2 copy
+constexpr int kAccFlush = 8;     // one wave per XCD writes its L2's dirty lines back after every
+                                 // 64 ratings it applies (agent release fence = buffer_wbl2)
 
 // The stream is split into ng group spans goff[g] .. goff[g + 1] (mml_device.h group_wave): ng = 8
 // for XCD-owned item groups (block b serves group b % 8, one XCD per group), ng = 1 for one span.
@@ -277,10 +282,12 @@ template <int LOSS, int LPR, int VPL, int AM>
 __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
     const int64_t* __restrict__ goff, int32_t ng, int32_t waves_per_group, float* U, float* V,
-    float* bu, float* bi, int32_t ld4, uint32_t v_bytes, uint32_t bi_bytes, BmfScalars s,
-    const int32_t* __restrict__ cnt_u, const int32_t* __restrict__ cnt_i) {
+    float* bu, float* bi, int32_t ld4, uint32_t v_bytes, uint32_t bi_bytes, uint32_t u_bytes,
+    uint32_t bu_bytes, int32_t flush_every, BmfScalars s, const int32_t* __restrict__ cnt_u,
+    const int32_t* __restrict__ cnt_i) {
     constexpr int RPW = 64 / LPR;  // ratings per wave step
     constexpr bool COH = AM == kAccCoherent;
+    constexpr bool IL2 = (AM & kAccItemL2) != 0, UTH = (AM & kAccUserThru) != 0;
     const int lane = threadIdx.x & 63;
     // wave-uniform (SGPR) bounds: the loops' branches stay scalar
     const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -291,7 +298,14 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
     float4* V4 = reinterpret_cast<float4*>(V);
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t vrs = mml::buffer_rsrc(V, v_bytes);
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t brs = mml::buffer_rsrc(bi, bi_bytes);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t urs = mml::buffer_rsrc(U, u_bytes);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t burs = mml::buffer_rsrc(bu, bu_bytes);
+    // the flushing waves: wave 0 of every flush_every-th block of each XCD's group
+    [[maybe_unused]] const bool flusher = (AM & kAccFlush) != 0 && (threadIdx.x >> 6) == 0 &&
+                                          (blockIdx.x >> 3) % (uint32_t)flush_every == 0;
     for (int64_t base = begin; base < end; base += 64) {
+        if constexpr ((AM & kAccFlush) != 0)
+            if (flusher) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         // 64 ratings of the stream: three coalesced 256-B loads, then broadcast per group
         const int64_t idx = base + lane;
         const bool in = idx < end;
@@ -313,8 +327,11 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
                 float4 pu[VPL], qi[VPL];
 #pragma unroll
                 for (int v = 0; v < VPL; ++v) {
-                    pu[v] = load4<COH>(U4 + ou + LPR * v);
-                    if constexpr (AM == kAccItemL2)
+                    if constexpr (UTH)
+                        pu[v] = mml::load4_l2(urs, (uint32_t)(ou + LPR * v) * 16u);
+                    else
+                        pu[v] = load4<COH>(U4 + ou + LPR * v);
+                    if constexpr (IL2)
                         qi[v] = mml::load4_l2(vrs, (uint32_t)(oi + LPR * v) * 16u);
                     else
                         qi[v] = load4<COH>(V4 + oi + LPR * v);
@@ -329,23 +346,33 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
                 }
                 part = group_sum<LPR>(part);
                 constexpr bool biased = LOSS != kPlainMF;
-                const float bu_u = biased ? load1<COH>(bu + u) : 0.0f;
-                float bi_i = 0.0f;
+                float bu_u = 0.0f, bi_i = 0.0f;
                 if constexpr (biased) {
-                    if constexpr (AM == kAccItemL2) bi_i = mml::load1_l2(brs, (uint32_t)i * 4u);
+                    if constexpr (UTH) bu_u = mml::load1_l2(burs, (uint32_t)u * 4u);
+                    else bu_u = load1<COH>(bu + u);
+                    if constexpr (IL2) bi_i = mml::load1_l2(brs, (uint32_t)i * 4u);
                     else bi_i = load1<COH>(bi + i);
                 }
                 const RatingStep<LOSS> st(s, part, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
                 if (biased && q == 0) {
-                    store1<COH>(bu + u, st.new_bu);
+                    if constexpr (UTH)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, st.new_bu),
+                                                              burs, (uint32_t)u * 4u, 0, 16);
+                    else
+                        store1<COH>(bu + u, st.new_bu);
                     store1<COH>(bi + i, st.new_bi);
                 }
 #pragma unroll
                 for (int v = 0; v < VPL; ++v) {
                     const float4 a = pu[v], c = qi[v];
-                    store4<COH>(U4 + ou + LPR * v,
-                                make_float4(st.new_u(s, a.x, c.x), st.new_u(s, a.y, c.y),
-                                            st.new_u(s, a.z, c.z), st.new_u(s, a.w, c.w)));
+                    const float4 nu = make_float4(st.new_u(s, a.x, c.x), st.new_u(s, a.y, c.y),
+                                                  st.new_u(s, a.z, c.z), st.new_u(s, a.w, c.w));
+                    if constexpr (UTH)
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, nu),
+                            urs, (uint32_t)(ou + LPR * v) * 16u, 0, 16);
+                    else
+                        store4<COH>(U4 + ou + LPR * v, nu);
                     store4<COH>(V4 + oi + LPR * v,
                                 make_float4(st.new_i(s, a.x, c.x), st.new_i(s, a.y, c.y),
                                             st.new_i(s, a.z, c.z), st.new_i(s, a.w, c.w)));
@@ -1458,12 +1485,14 @@ void ensure_xstream(mml_bmf* h) {
     h->has_xstream = true;
 }
 
-// MML_HOGWILD_XCD: 1 (default) = XCD-owned item groups with L2-served item loads, 2 = the groups
-// with plain loads, 0 = one span over all XCDs (the round-1 kernel)
+// MML_HOGWILD_XCD: 4 (default) = XCD-owned item groups with L2-served item loads, user rows written
+// through and flushing waves; 1 = the groups with L2-served item loads only, 2 = the groups
+// with plain loads, 3 = 1 + user rows written through, 4 = 3 + flushing waves (mml::flush_every),
+// 5 = 1 + the flushing waves, 0 = one span over all XCDs (the round-1 kernel)
 static int hogwild_xcd_mode() {
     static const int m = [] {
         const char* e = std::getenv("MML_HOGWILD_XCD");
-        return e ? std::atoi(e) : 1;
+        return e ? std::atoi(e) : 4;
     }();
     return m;
 }
@@ -1500,7 +1529,15 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
         su = h->xu.get();
         si = h->xi.get();
         sr = reinterpret_cast<const float*>(h->xr.get());
-        if (xmode == 1) am = kAccItemL2;
+        const bool u_fits = (uint64_t)h->n_users * h->ld * sizeof(float) < (1ull << 32);
+        switch (xmode) {
+            case 2: am = kAccPlain; break;
+            case 3: am = u_fits ? kAccItemL2 | kAccUserThru : kAccItemL2; break;
+            case 4: am = u_fits ? kAccItemL2 | kAccUserThru | kAccFlush : kAccItemL2 | kAccFlush;
+                break;
+            case 5: am = kAccItemL2 | kAccFlush; break;
+            default: am = kAccItemL2; break;
+        }
     }
     int64_t blocks = (waves + 3) / 4;
     blocks = (blocks + ng - 1) / ng * ng;
@@ -1508,17 +1545,23 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     const int ld4 = h->ld / 4;
     const uint32_t vb = (uint32_t)std::min<uint64_t>(v_bytes, 0xFFFFFFFFull);
     const uint32_t bb = (uint32_t)((uint64_t)h->n_items * sizeof(float));
+    const uint32_t ub = (uint32_t)std::min<uint64_t>((uint64_t)h->n_users * h->ld * sizeof(float),
+                                                     0xFFFFFFFFull);
+    const uint32_t bub = (uint32_t)((uint64_t)h->n_users * sizeof(float));
 #define MML_HOG1(LPR, VPL, AM)                                                                  \
     bmf_sgd_hogwild_kernel<LOSS, LPR, VPL, AM><<<(int)blocks, 256, 0, st>>>(                  \
         su, si, sr, goff, ng, wpg, h->U.get(), h->V.get(), h->bu.get(), h->bi.get(), ld4, vb, bb, \
-        s, cu, ci)
-#define MML_HOGV(LPR, VPL)                                       \
-    if (am == kAccCoherent) {                                    \
-        MML_HOG1(LPR, VPL, kAccCoherent);                        \
-    } else if (am == kAccItemL2) {                               \
-        MML_HOG1(LPR, VPL, kAccItemL2);                          \
-    } else {                                                     \
-        MML_HOG1(LPR, VPL, kAccPlain);                           \
+        ub, bub, mml::flush_every(), s, cu, ci)
+#define MML_HOGV(LPR, VPL)                                                       \
+    switch (am) {                                                                \
+        case kAccCoherent: MML_HOG1(LPR, VPL, kAccCoherent); break;              \
+        case kAccItemL2: MML_HOG1(LPR, VPL, kAccItemL2); break;                  \
+        case kAccItemL2 | kAccUserThru:                                          \
+            MML_HOG1(LPR, VPL, kAccItemL2 | kAccUserThru); break;                \
+        case kAccItemL2 | kAccUserThru | kAccFlush:                              \
+            MML_HOG1(LPR, VPL, kAccItemL2 | kAccUserThru | kAccFlush); break;    \
+        case kAccItemL2 | kAccFlush: MML_HOG1(LPR, VPL, kAccItemL2 | kAccFlush); break; \
+        default: MML_HOG1(LPR, VPL, kAccPlain); break;                           \
     }
     // one float4 of U_u and of V_i per lane (VPL 2 measured equal, VPL 4 10 % slower on C2)
     switch (h->lpr) {
@@ -1890,6 +1933,10 @@ extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params,
 extern "C" mml_status mml_bmf_destroy(mml_bmf* h) {
     return guard([&] {
         if (!h) return;
+        if (!h->ctx) {  // a create that failed before binding the context
+            delete h;
+            return;
+        }
         if (!h->shards.empty() || (h->ctx && h->ctx->multi())) {
             for (mml_bmf* s : h->shards)
                 if (s) mml_bmf_destroy(s);

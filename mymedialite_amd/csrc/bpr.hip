@@ -359,13 +359,20 @@ __device__ __forceinline__ int32_t bpr_group_fetch(int32_t v, int base, int lane
 constexpr int kBprLdL2 = 1;   // V_i, V_j, b_i, b_j loaded sc1: L2-served, past the CU's stale L1
 constexpr int kBprJThru = 2;  // V_j / b_j stored sc1: write-through, dropped from this XCD's L2
 constexpr int kBprIThru = 4;  // V_i / b_i stored sc1 as well: every item row lives memory-side
+constexpr int kBprUThru = 16;  // U_u loaded sc1 and stored sc1 (write-through): no stale user
+                               // rows in any XCD's L2 (U < 4 GiB only: buffer addressing)
+constexpr int kBprFlush = 8;  // one wave per XCD writes its L2's dirty lines back after every 64
+                              // triples it applies (agent release fence = buffer_wbl2): the owner's
+                              // hot rows reach memory, where the other XCDs read them as j, within
+                              // one batch instead of at the end of the launch
 
 // Triples split into ng group spans by the XCD group of i (mml_device.h group_wave); ng = 1: one span
 template <int LPR, bool SOFT, int AM>
 __global__ __launch_bounds__(256) void bpr_update_kernel(
     const int32_t* __restrict__ tu, const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
     const int64_t* __restrict__ goff, int32_t ng, int32_t waves_per_group, float* U, float* V,
-    float* bias, int32_t ld4, uint32_t v_bytes, uint32_t b_bytes, BprScalars s) {
+    float* bias, int32_t ld4, uint32_t v_bytes, uint32_t b_bytes, uint32_t u_bytes,
+    int32_t flush_every, BprScalars s) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const mml::GroupWave gw = mml::group_wave(goff, ng, waves_per_group,
@@ -377,7 +384,13 @@ __global__ __launch_bounds__(256) void bpr_update_kernel(
     float4* V4 = reinterpret_cast<float4*>(V);
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t vrs = mml::buffer_rsrc(V, v_bytes);
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t brs = mml::buffer_rsrc(bias, b_bytes);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t urs = mml::buffer_rsrc(U, u_bytes);
+    // the flushing waves: wave 0 of every flush_every-th block of each XCD's group
+    [[maybe_unused]] const bool flusher = (AM & kBprFlush) != 0 && (threadIdx.x >> 6) == 0 &&
+                                          (blockIdx.x >> 3) % (uint32_t)flush_every == 0;
     for (int64_t base = begin; base < end; base += 64) {
+        if constexpr ((AM & kBprFlush) != 0)
+            if (flusher) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const int64_t x = base + lane;
         const bool in = x < end;
         const int32_t my_u = in ? tu[x] : 0, my_i = in ? ti[x] : 0, my_j = in ? tj[x] : 0;
@@ -392,7 +405,9 @@ __global__ __launch_bounds__(256) void bpr_update_kernel(
             if (step + sub >= cnt) continue;
             const int64_t ou = (int64_t)u * ld4 + q, oi = (int64_t)i * ld4 + q,
                           oj = (int64_t)j * ld4 + q;
-            const float4 w = U4[ou];
+            float4 w;
+            if constexpr ((AM & kBprUThru) != 0) w = mml::load4_l2(urs, (uint32_t)ou * 16u);
+            else w = U4[ou];
             float4 hi, hj;
             float bi, bj;
             if constexpr (!(AM & kBprLdL2)) {
@@ -431,8 +446,14 @@ __global__ __launch_bounds__(256) void bpr_update_kernel(
                         bias[j] = nbj;
                 }
             }
-            U4[ou] = make_float4(t.u(s, w.x, hi.x, hj.x), t.u(s, w.y, hi.y, hj.y),
-                                 t.u(s, w.z, hi.z, hj.z), t.u(s, w.w, hi.w, hj.w));
+            const float4 nw = make_float4(t.u(s, w.x, hi.x, hj.x), t.u(s, w.y, hi.y, hj.y),
+                                          t.u(s, w.z, hi.z, hj.z), t.u(s, w.w, hi.w, hj.w));
+            if constexpr ((AM & kBprUThru) != 0)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, nw), urs,
+                    (uint32_t)ou * 16u, 0, 16);
+            else
+                U4[ou] = nw;
             const float4 ni = make_float4(t.i(s, w.x, hi.x), t.i(s, w.y, hi.y),
                                           t.i(s, w.z, hi.z), t.i(s, w.w, hi.w));
             if constexpr ((AM & kBprIThru) != 0)
@@ -460,11 +481,15 @@ __global__ __launch_bounds__(256) void bpr_update_kernel(
 // double through v_readlane exactly as RowScalarProductWithRowDifference
 // (DataType/MatrixExtensions.cs:276-298), so the result is bit-faithful to the managed loop.
 template <bool SOFT, int KM>
-__global__ __launch_bounds__(64) void bpr_apply_ordered_kernel(
+// With W = blockDim.x / 64 > 1 waves, wave w applies the contiguous part [w n / W, (w+1) n / W) in
+// order: W streams in flight at once (the small-epoch Hogwild form, one CU, see mml_bpr_iterate).
+__global__ __launch_bounds__(256) void bpr_apply_ordered_kernel(
     const int32_t* __restrict__ tu, const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
     int64_t n, float* U, float* V, float* bias, int32_t k, int32_t ld, BprScalars s) {
-    const int lane = threadIdx.x;
-    for (int64_t x = 0; x < n; ++x) {
+    const int lane = threadIdx.x & 63;
+    const int64_t W = blockDim.x >> 6, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t x0 = n * w / W, x1 = n * (w + 1) / W;
+    for (int64_t x = x0; x < x1; ++x) {
         const int32_t u = tu[x], i = ti[x], j = tj[x];
         float* Wu = U + (int64_t)u * ld;
         float* Hi = V + (int64_t)i * ld;
@@ -675,6 +700,10 @@ extern "C" mml_status mml_bpr_create(mml_ctx* ctx, const mml_bpr_params* params,
 extern "C" mml_status mml_bpr_destroy(mml_bpr* h) {
     return guard([&] {
         if (!h) return;
+        if (!h->ctx) {  // a create that failed before binding the context
+            delete h;
+            return;
+        }
         if (h->ctx && h->ctx->multi()) {
             for (mml_bpr* s : h->shards)
                 if (s) mml_bpr_destroy(s);
@@ -919,12 +948,13 @@ namespace {
 
 // one wavefront applies n triples in order (bpr_apply_ordered_kernel), k <= 256
 void launch_apply_ordered(mml_bpr* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
-                          int64_t n, const BprScalars& s, hipStream_t st) {
+                          int64_t n, const BprScalars& s, hipStream_t st, int waves = 1) {
     const int km = (h->k + 63) / 64;
     const bool soft = h->p.model == MML_BPR_MODEL_SOFT_MARGIN;
-#define MML_APPLY(SOFT, KM)                                                                    \
-    bpr_apply_ordered_kernel<SOFT, KM><<<1, 64, 0, st>>>(tu, ti, tj, n, h->U.get(), h->V.get(), \
-                                                         h->bias.get(), h->k, h->ld, s)
+#define MML_APPLY(SOFT, KM)                                                                      \
+    bpr_apply_ordered_kernel<SOFT, KM><<<1, 64 * waves, 0, st>>>(tu, ti, tj, n, h->U.get(),     \
+                                                                 h->V.get(), h->bias.get(), h->k, \
+                                                                 h->ld, s)
 #define MML_APPLY_K(SOFT)                   \
     switch (km) {                           \
         case 1: MML_APPLY(SOFT, 1); break;  \
@@ -959,6 +989,8 @@ BprScalars scalars_of(const mml_bpr* h) {
 //   2  the same, V_j / b_j stored write-through (sc1)
 //   3  the same, V_i / b_i stored write-through too
 //   4  one span, item loads sc1 and all item stores write-through (no owner: coherent item side)
+//   5  mode 2 + one wave per XCD flushing its L2 after every batch of 64 triples (kBprFlush)
+//   6  mode 5 + user rows written through (kBprUThru; mode 5 where U >= 4 GiB)
 // Measured on the C3 replica (100k x 10k, tests/test_bpr_c3_replica_gpu.py): mode 1
 // collapses (AUC 0.60 vs 0.78: a foreign XCD's plain j store leaves a dirty, stale copy of a hot
 // row whose write-back reverts the owner's updates); modes 0 / 2 land +0.010 / +0.008 above the
@@ -974,12 +1006,14 @@ BprXcdMode bpr_xcd_mode(int sampler) {
     }();
     // WeightedBPRMF draws j by popularity: most j rows are hot rows of another XCD's group, so
     // the groups do not apply (mid replica: mode 2 +0.114 AUC, mode 0 -0.004)
-    const int m = env >= 0 ? env : (sampler == MML_BPR_SAMPLER_WEIGHTED ? 0 : 2);
+    const int m = env >= 0 ? env : (sampler == MML_BPR_SAMPLER_WEIGHTED ? 0 : 6);
     switch (m) {
         case 1: return {true, kBprLdL2};
         case 2: return {true, kBprLdL2 | kBprJThru};
         case 3: return {true, kBprLdL2 | kBprJThru | kBprIThru};
         case 4: return {false, kBprLdL2 | kBprJThru | kBprIThru};
+        case 5: return {true, kBprLdL2 | kBprJThru | kBprFlush};
+        case 6: return {true, kBprLdL2 | kBprJThru | kBprFlush | kBprUThru};
         default: return {false, 0};
     }
 }
@@ -991,13 +1025,21 @@ void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff, cons
     const int32_t wpg = (int32_t)(blocks / ng * wpb);
     const uint32_t vb = (uint32_t)std::min<uint64_t>((uint64_t)h->n_items * h->ld * 4, 0xFFFFFFFFull);
     const uint32_t bb = (uint32_t)((uint64_t)h->n_items * 4);
+    const uint64_t u_all = (uint64_t)h->n_users * h->ld * 4;
+    const uint32_t ub = (uint32_t)std::min<uint64_t>(u_all, 0xFFFFFFFFull);
+    if (u_all >= (1ull << 32)) am &= ~kBprUThru;
 #define MML_UPD(AM)                                                                             \
     bpr_update_kernel<LPR, SOFT, AM><<<(int)blocks, 64 * wpb, 0, st>>>(                        \
-        tu, ti, tj, goff, ng, wpg, h->U.get(), h->V.get(), h->bias.get(), h->ld / 4, vb, bb, s)
+        tu, ti, tj, goff, ng, wpg, h->U.get(), h->V.get(), h->bias.get(), h->ld / 4, vb, bb, ub, \
+        mml::flush_every(), s)
     switch (am) {
         case kBprLdL2: MML_UPD(kBprLdL2); break;
         case kBprLdL2 | kBprJThru: MML_UPD(kBprLdL2 | kBprJThru); break;
         case kBprLdL2 | kBprJThru | kBprIThru: MML_UPD(kBprLdL2 | kBprJThru | kBprIThru); break;
+        case kBprLdL2 | kBprJThru | kBprFlush: MML_UPD(kBprLdL2 | kBprJThru | kBprFlush); break;
+        case kBprLdL2 | kBprJThru | kBprFlush | kBprUThru:
+            MML_UPD(kBprLdL2 | kBprJThru | kBprFlush | kBprUThru);
+            break;
         default: MML_UPD(0); break;
     }
 #undef MML_UPD
@@ -1192,9 +1234,15 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         MML_HIP(hipEventRecord(h->ctx->ev_mid, st));
         if (ordered && n > 0)
             launch_apply_ordered(h, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), n, s, st);
-        if (!ordered && !fused && n > 0) {
-            launch_update(h, soft, am, ng, goff, tu, ti, tj, blocks, blocks == 1 ? (int)waves : 4,
-                          s, st);
+        if (!ordered && !fused && n > 0 && blocks == 1) {
+            // a small epoch (< 16 waves' worth): Hogwild with one stream per wave of ONE CU, each
+            // applied in order (the lanes own factors, the exact arithmetic): 4 triples in flight
+            // instead of 4 x 64 / LPR.  Measured on a 4,000-user WeightedBPRMF replica, whose
+            // popularity-drawn j puts the hottest items into most concurrent triples: 1 wave of 16
+            // triples per step -0.032 AUC vs the sequential oracle, 4 waves -0.038
+            launch_apply_ordered(h, tu, ti, tj, n, s, st, (int)waves);
+        } else if (!ordered && !fused && n > 0) {
+            launch_update(h, soft, am, ng, goff, tu, ti, tj, blocks, 4, s, st);
         } else if (fused) {
 #define MML_BPR(LPR)                                                                            \
     if (pair)                                                                                   \

@@ -158,6 +158,9 @@ std::vector<int64_t> device_id_counts(hipStream_t st, const int32_t* ids, int64_
 
 struct mml_ctx;
 namespace mml {
+// Hogwild flushing waves: wave 0 of every flush_every()-th block of an XCD group writes the L2's
+// dirty lines back after each batch of 64 updates (MML_FLUSH_EVERY, default 8)
+int32_t flush_every();
 // 8 when blocks b and b + 8 run on one XCD for every b of a 2,048-block grid (probed once per
 // context on the device; MML_XCD_GROUPS=1 forces 1), else 1
 int32_t xcd_groups(mml_ctx* ctx);

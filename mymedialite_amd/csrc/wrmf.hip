@@ -716,6 +716,10 @@ extern "C" mml_status mml_wrmf_create(mml_ctx* ctx, const mml_wrmf_params* param
 extern "C" mml_status mml_wrmf_destroy(mml_wrmf* h) {
     return guard([&] {
         if (!h) return;
+        if (!h->ctx) {  // a create that failed before binding the context
+            delete h;
+            return;
+        }
         if (h->ctx && h->ctx->multi()) {
             for (mml_wrmf* s : h->shards)
                 if (s) mml_wrmf_destroy(s);

@@ -732,10 +732,12 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_wood_kernel(
                 const float* hr = sm.u.hs[cur][cc + h];
 #pragma unroll
                 for (int s = 0; s < C::SLOTS; ++s) {
-                    const bool ok = TI[s] >= 0;
-                    const float a = ok ? hr[32 * TJ[s] + q] : 0.0f;
-                    const float bb = ok ? hr[32 * TI[s] + q] : 0.0f;
-                    acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc[s], 0, 0, 0);
+                    // the b-row tiles (I = NT) are set below, not accumulated: no MFMAs for them
+                    // (TI is wave-uniform, so this is a scalar branch)
+                    if (TI[s] < 0 || TI[s] >= NT) continue;
+                    acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(hr[32 * TJ[s] + q],
+                                                                  hr[32 * TI[s] + q], acc[s], 0, 0,
+                                                                  0);
                 }
             }
             if (more) stash(cur ^ 1);

@@ -117,6 +117,14 @@ __global__ __launch_bounds__(256) void xcd_histogram_kernel(const int32_t* __res
 
 namespace mml {
 
+int32_t flush_every() {
+    static const int32_t v = [] {
+        const char* e = std::getenv("MML_FLUSH_EVERY");
+        return e ? std::max(1, std::atoi(e)) : 8;
+    }();
+    return v;
+}
+
 int32_t xcd_groups(mml_ctx* ctx) {
     if (ctx->xcd_groups > 0) return ctx->xcd_groups;
     const char* e = std::getenv("MML_XCD_GROUPS");

@@ -238,8 +238,13 @@ class BPRMF(_MFBase):
                                              N.ptr(j, N._i32p), n))
         return u, i, j
 
+    def _order_before_init(self):
+        """A visit order drawn before InitModel (MultiCoreBPRMF.Train); None for BPRMF."""
+        return None
+
     def init_model(self):
         """InitModel (BPRMF.cs:121-126): MF factors + zero item biases; data to the device."""
+        pre = self._order_before_init()
         U, V = self._init_factors()
         bias = np.zeros(self.MaxItemID + 1, np.float32)
         self._release()
@@ -250,8 +255,9 @@ class BPRMF(_MFBase):
                                        self.MaxItemID + 1, ctypes.byref(h)))
         self._h = h
         fb = self._feedback
-        order = None
-        if self._sampler() == N.BPR_SAMPLER_UNIFORM_PAIR:  # Feedback.RandomIndex (:250), once
+        order = pre
+        if order is None and self._sampler() == N.BPR_SAMPLER_UNIFORM_PAIR:
+            # Feedback.RandomIndex (:250), shuffled once
             order = Random.get_instance().shuffle(np.arange(fb.count, dtype=np.int32))
         N.check(N.lib().mml_bpr_set_data(h, N.ptr(fb.users, N._i32p), N.ptr(fb.items, N._i32p),
                                          fb.count, N.ptr(order, N._i32p)))
@@ -319,6 +325,45 @@ class BPRMF(_MFBase):
                 f"num_iter={self.NumIter} LearnRate={g(self.LearnRate)} "
                 f"uniform_user_sampling={self.UniformUserSampling} "
                 f"with_replacement={self.WithReplacement} update_j={self.UpdateJ}")
+
+
+class MultiCoreBPRMF(BPRMF):
+    """MultiCoreBPRMF (ItemRecommendation/MultiCoreBPRMF.cs:30-73): BPRMF with UniformUserSampling =
+    false, WithReplacement = false and MaxThreads = 100 (:42-47), whose Train() first splits
+    Feedback.RandomIndex round-robin into MaxThreads blocks (MultiCore.PartitionIndices,
+    MultiCore.cs:79-92) and whose IterateWithoutReplacementUniformPair walks the blocks in parallel,
+    each in order (:57-62): Hogwild over events.  On the GPU the blocks, concatenated, are the visit
+    order of the pair sampler (MML_BPR_SAMPLER_UNIFORM_PAIR: (u, i) = the event, j = SampleOtherItem)
+    and the Hogwild schedule applies it with thousands of wavefronts, each walking a contiguous run
+    of a block.  Schedule = "ordered" applies the same stream in order (MaxThreads = 1)."""
+    TYPE_NAME = "MyMediaLite.ItemRecommendation.MultiCoreBPRMF"
+    PROPERTIES = dict(BPRMF.PROPERTIES, MaxThreads="int")
+
+    def __init__(self, **kw):
+        super().__init__()
+        self.WithReplacement = False
+        self.UniformUserSampling = False
+        self.MaxThreads = 100
+        self.Schedule = "hogwild"
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+    def _order_before_init(self):
+        """Train(): index_blocks = Feedback.PartitionIndices(MaxThreads) before base.Train()."""
+        n = self._feedback.count
+        idx = Random.get_instance().shuffle(np.arange(n, dtype=np.int32))  # RandomIndex
+        g = max(1, min(int(self.MaxThreads), n))
+        return np.ascontiguousarray(np.concatenate([idx[b::g] for b in range(g)]))
+
+    def __str__(self):
+        """MultiCoreBPRMF.ToString() (:66-72)."""
+        g = lambda x: f"{float(np.float32(x)):.7g}"
+        return (f"MultiCoreBPRMF num_factors={self.NumFactors} bias_reg={g(self.BiasReg)} "
+                f"reg_u={g(self.RegU)} reg_i={g(self.RegI)} reg_j={g(self.RegJ)} "
+                f"num_iter={self.NumIter} learn_rate={g(self.LearnRate)} "
+                f"uniform_user_sampling={self.UniformUserSampling} "
+                f"with_replacement={self.WithReplacement} update_j={self.UpdateJ} "
+                f"max_threads={self.MaxThreads}")
 
 
 class WeightedBPRMF(BPRMF):

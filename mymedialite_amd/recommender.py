@@ -88,3 +88,49 @@ class Recommender:
         if not found:
             report_error(f"Recommender {type(self).__name__} does not have a parameter named "
                          f"'{nkey}'.\n{self}")
+
+
+# ------------------------------------------------------------------ discovery by type name
+def _registry(namespace: str) -> dict:
+    """TYPE_NAME (lower-cased) -> class for the GPU recommenders of one namespace."""
+    from . import item_recommendation, rating_prediction
+    mod = rating_prediction if namespace == "RatingPrediction" else item_recommendation
+    out = {}
+    for obj in vars(mod).values():
+        # the class's own TYPE_NAME (a subclass inherits its parent's until it declares one)
+        name = vars(obj).get("TYPE_NAME") if isinstance(obj, type) else None
+        if name and name.startswith(f"MyMediaLite.{namespace}."):
+            out[name.lower()] = obj
+    return out
+
+
+def create_rating_predictor(typename: str):
+    """Extensions.CreateRatingPredictor(string) (Extensions.cs:170-182): the namespace prefix is
+    optional and the name matches case-insensitively (Assembly.GetType(name, false, true)); None
+    when no such GPU recommender exists."""
+    if not typename.startswith("MyMediaLite.RatingPrediction."):
+        typename = "MyMediaLite.RatingPrediction." + typename
+    cls = _registry("RatingPrediction").get(typename.lower())
+    return cls() if cls is not None else None
+
+
+def create_item_recommender(typename: str):
+    """Extensions.CreateItemRecommender(string) (Extensions.cs:216-228)."""
+    if not typename.startswith("MyMediaLite.ItemRecommendation"):
+        typename = "MyMediaLite.ItemRecommendation." + typename
+    cls = _registry("ItemRecommendation").get(typename.lower())
+    return cls() if cls is not None else None
+
+
+def create_recommender(typename: str):
+    """Extensions.CreateRecommender(string) (Extensions.cs:187-195)."""
+    if typename.startswith("MyMediaLite.RatingPrediction."):
+        return create_rating_predictor(typename)
+    if typename.startswith("MyMediaLite.ItemRecommendation."):
+        return create_item_recommender(typename)
+    raise IOError(f"Unknown recommender namespace in type name '{typename}'")
+
+
+def list_recommenders(namespace: str) -> list:
+    """The type names create_* finds (cf. Extensions.ListRecommenders, Extensions.cs:292-312)."""
+    return sorted(c.TYPE_NAME.split(".")[-1] for c in _registry(namespace).values())

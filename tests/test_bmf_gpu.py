@@ -208,8 +208,10 @@ def test_hogwild_statistical_parity_c2_shape():
             got.append(m.evaluate(Ratings(tu, ti, tv))["RMSE"])
         res[sched] = got
     print(f"C2-shape RMSE {res} oracle {ref}")
-    # plain Hogwild: per-XCD cache replicas of hot items -> 1.5e-2 (measured ~1.0e-2)
-    assert all(abs(a - b) <= 1.5e-2 for a, b in zip(res["hogwild"], ref)), (res, ref)
+    # Hogwild on XCD-owned item groups (xcd.hip; every item row cached in ONE XCD's L2): 2e-3
+    # (measured 1.0e-3 / 1.5e-3 after epochs 1 / 2; the round-1 spread over all XCDs, whose L2s
+    # held replicas of the hot rows, measured 1.0e-2 / 8e-3: MML_HOGWILD_XCD=0)
+    assert all(abs(a - b) <= 2e-3 for a, b in zip(res["hogwild"], ref)), (res, ref)
     # coherent Hogwild: only in-flight staleness remains -> 2e-3 (measured ~3e-4)
     assert all(abs(a - b) <= 2e-3 for a, b in zip(res["hogwild_coherent"], ref)), (res, ref)
 

@@ -42,12 +42,13 @@ def c3_replica(seed=2, n_users=NU, n_items=NI, per_user=20):
     return u[~test], i[~test], u[test], i[test]
 
 
-@pytest.fixture(scope="module")
-def replica():
+@pytest.fixture(scope="module", params=[K, 128], ids=["k64", "k128"])
+def replica(request):
+    k = request.param
     tr_u, tr_i, te_u, te_i = c3_replica()
     t0 = time.perf_counter()
-    st = O.bpr_train(tr_u, tr_i, NU, NI, seed=7, k=K, num_iter=ITERS)
-    ref = BPRMF(NumFactors=K, Schedule="hogwild")
+    st = O.bpr_train(tr_u, tr_i, NU, NI, seed=7, k=k, num_iter=ITERS)
+    ref = BPRMF(NumFactors=k, Schedule="hogwild")
     ref.feedback = PosOnlyFeedback(tr_u, tr_i)
     ref.MaxUserID, ref.MaxItemID = NU - 1, NI - 1
     ref.init_model()  # the training data on the device (AUC ignores training items per user)
@@ -56,16 +57,16 @@ def replica():
     ref._host = None
     test = PosOnlyFeedback(te_u, te_i)
     auc = ref.evaluate_auc(test)
-    print(f"\noracle: AUC {auc['AUC']:.5f} ({time.perf_counter() - t0:.1f} s)")
-    return tr_u, tr_i, test, st, auc
+    print(f"\noracle k={k}: AUC {auc['AUC']:.5f} ({time.perf_counter() - t0:.1f} s)")
+    return tr_u, tr_i, test, st, auc, k
 
 
 @pytest.mark.parametrize("schedule,lo,hi", [("ordered", -0.005, 0.005),
                                             ("hogwild", -0.005, 0.015)])
 def test_c3_replica_auc_parity(replica, schedule, lo, hi):
-    tr_u, tr_i, test, st, auc_ref = replica
+    tr_u, tr_i, test, st, auc_ref, k = replica
     Random.set_seed(7)
-    m = BPRMF(NumFactors=K, NumIter=ITERS, Schedule=schedule)
+    m = BPRMF(NumFactors=k, NumIter=ITERS, Schedule=schedule)
     m.feedback = PosOnlyFeedback(tr_u, tr_i)
     m.MaxUserID, m.MaxItemID = NU - 1, NI - 1
     m.init_model()
@@ -76,7 +77,7 @@ def test_c3_replica_auc_parity(replica, schedule, lo, hi):
     dt = time.perf_counter() - t0
     auc = m.evaluate_auc(test)
     d = auc["AUC"] - auc_ref["AUC"]
-    print(f"C3 replica {schedule}: AUC gpu {auc['AUC']:.5f} oracle {auc_ref['AUC']:.5f} "
+    print(f"C3 replica k={k} {schedule}: AUC gpu {auc['AUC']:.5f} oracle {auc_ref['AUC']:.5f} "
           f"d {d:+.5f} users {auc['num_users']} ({dt:.2f} s for {ITERS} epochs)")
     assert auc["num_users"] == auc_ref["num_users"] > 90_000
     assert auc_ref["AUC"] > 0.6

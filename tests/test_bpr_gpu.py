@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from mymedialite_amd import BPRMF, PosOnlyFeedback, Random
+from mymedialite_amd import BPRMF, MultiCoreBPRMF, PosOnlyFeedback, Random
 
 pytestmark = pytest.mark.gpu
 
@@ -44,7 +44,7 @@ def auc_of(U, V, bias, tr_u, tr_i, te_u, te_i, seed=99):
 
 
 @pytest.mark.parametrize("schedule", ["ordered", "hogwild"])
-@pytest.mark.parametrize("sampling", ["uniform_user", "uniform_pair"])
+@pytest.mark.parametrize("sampling", ["uniform_user", "uniform_pair", "multicore"])
 def test_bpr_auc_parity(sampling, schedule):
     tr_u, tr_i, te_u, te_i = planted_feedback(1, 4000, 600, 25)
     nu, ni = int(tr_u.max()) + 1, int(tr_i.max()) + 1
@@ -52,11 +52,15 @@ def test_bpr_auc_parity(sampling, schedule):
     st = O.bpr_train(tr_u, tr_i, nu, ni, seed=5, k=k, num_iter=iters)
     auc_ref, n_ref = auc_of(st["U"], st["V"], st["bias"], tr_u, tr_i, te_u, te_i)
     Random.set_seed(5)
-    m = BPRMF(NumFactors=k, NumIter=iters, UniformUserSampling=(sampling == "uniform_user"),
-              Schedule=schedule)
+    if sampling == "multicore":  # MultiCoreBPRMF: pair sampler over PartitionIndices' blocks
+        m = MultiCoreBPRMF(NumFactors=k, NumIter=iters, Schedule=schedule)
+    else:
+        m = BPRMF(NumFactors=k, NumIter=iters, UniformUserSampling=(sampling == "uniform_user"),
+                  Schedule=schedule)
     m.feedback = PosOnlyFeedback(tr_u, tr_i)
     m.init_model()
-    np.testing.assert_array_equal(m.user_factors, st["init_U"])  # same host RNG init
+    if sampling != "multicore":  # (MultiCoreBPRMF.Train draws RandomIndex before InitModel)
+        np.testing.assert_array_equal(m.user_factors, st["init_U"])  # same host RNG init
     for _ in range(iters):
         m.iterate()
     auc_gpu, n_gpu = auc_of(m.user_factors, m.item_factors, m.item_bias, tr_u, tr_i, te_u, te_i)
