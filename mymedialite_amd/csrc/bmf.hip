@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
     const int64_t* __restrict__ goff, int32_t ng, int32_t waves_per_group, float* U, float* V,
     float* bu, float* bi, int32_t ld4, uint32_t v_bytes, uint32_t bi_bytes, uint32_t u_bytes,
-    uint32_t bu_bytes, int32_t flush_every, BmfScalars s, const int32_t* __restrict__ cnt_u,
+    uint32_t bu_bytes, int32_t flushers, BmfScalars s, const int32_t* __restrict__ cnt_u,
     const int32_t* __restrict__ cnt_i) {
     constexpr int RPW = 64 / LPR;  // ratings per wave step
     constexpr bool COH = AM == kAccCoherent;
@@ -300,9 +300,10 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t brs = mml::buffer_rsrc(bi, bi_bytes);
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t urs = mml::buffer_rsrc(U, u_bytes);
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t burs = mml::buffer_rsrc(bu, bu_bytes);
-    // the flushing waves: wave 0 of every flush_every-th block of each XCD's group
-    [[maybe_unused]] const bool flusher = (AM & kAccFlush) != 0 && (threadIdx.x >> 6) == 0 &&
-                                          (blockIdx.x >> 3) % (uint32_t)flush_every == 0;
+    // the flushing waves: wave 0 of `flushers` evenly spaced blocks of each XCD's group
+    [[maybe_unused]] const bool flusher =
+        (AM & kAccFlush) != 0 && (threadIdx.x >> 6) == 0 &&
+        (blockIdx.x >> 3) % max(1u, (gridDim.x >> 3) / (uint32_t)flushers) == 0;
     for (int64_t base = begin; base < end; base += 64) {
         if constexpr ((AM & kAccFlush) != 0)
             if (flusher) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1487,7 +1488,7 @@ void ensure_xstream(mml_bmf* h) {
 
 // MML_HOGWILD_XCD: 4 (default) = XCD-owned item groups with L2-served item loads, user rows written
 // through and flushing waves; 1 = the groups with L2-served item loads only, 2 = the groups
-// with plain loads, 3 = 1 + user rows written through, 4 = 3 + flushing waves (mml::flush_every),
+// with plain loads, 3 = 1 + user rows written through, 4 = 3 + flushing waves (mml::flushers_per_xcd),
 // 5 = 1 + the flushing waves, 0 = one span over all XCDs (the round-1 kernel)
 static int hogwild_xcd_mode() {
     static const int m = [] {
@@ -1551,7 +1552,7 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
 #define MML_HOG1(LPR, VPL, AM)                                                                  \
     bmf_sgd_hogwild_kernel<LOSS, LPR, VPL, AM><<<(int)blocks, 256, 0, st>>>(                  \
         su, si, sr, goff, ng, wpg, h->U.get(), h->V.get(), h->bu.get(), h->bi.get(), ld4, vb, bb, \
-        ub, bub, mml::flush_every(), s, cu, ci)
+        ub, bub, mml::flushers_per_xcd(1), s, cu, ci)
 #define MML_HOGV(LPR, VPL)                                                       \
     switch (am) {                                                                \
         case kAccCoherent: MML_HOG1(LPR, VPL, kAccCoherent); break;              \

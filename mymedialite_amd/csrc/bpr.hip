@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void bpr_update_kernel(
     const int32_t* __restrict__ tu, const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
     const int64_t* __restrict__ goff, int32_t ng, int32_t waves_per_group, float* U, float* V,
     float* bias, int32_t ld4, uint32_t v_bytes, uint32_t b_bytes, uint32_t u_bytes,
-    int32_t flush_every, BprScalars s) {
+    int32_t flushers, BprScalars s) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const mml::GroupWave gw = mml::group_wave(goff, ng, waves_per_group,
@@ -385,9 +385,10 @@ __global__ __launch_bounds__(256) void bpr_update_kernel(
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t vrs = mml::buffer_rsrc(V, v_bytes);
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t brs = mml::buffer_rsrc(bias, b_bytes);
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t urs = mml::buffer_rsrc(U, u_bytes);
-    // the flushing waves: wave 0 of every flush_every-th block of each XCD's group
-    [[maybe_unused]] const bool flusher = (AM & kBprFlush) != 0 && (threadIdx.x >> 6) == 0 &&
-                                          (blockIdx.x >> 3) % (uint32_t)flush_every == 0;
+    // the flushing waves: wave 0 of `flushers` evenly spaced blocks of each XCD's group
+    [[maybe_unused]] const bool flusher =
+        (AM & kBprFlush) != 0 && (threadIdx.x >> 6) == 0 &&
+        (blockIdx.x >> 3) % max(1u, (gridDim.x >> 3) / (uint32_t)flushers) == 0;
     for (int64_t base = begin; base < end; base += 64) {
         if constexpr ((AM & kBprFlush) != 0)
             if (flusher) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1031,7 +1032,7 @@ void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff, cons
 #define MML_UPD(AM)                                                                             \
     bpr_update_kernel<LPR, SOFT, AM><<<(int)blocks, 64 * wpb, 0, st>>>(                        \
         tu, ti, tj, goff, ng, wpg, h->U.get(), h->V.get(), h->bias.get(), h->ld / 4, vb, bb, ub, \
-        mml::flush_every(), s)
+        mml::flushers_per_xcd(4), s)
     switch (am) {
         case kBprLdL2: MML_UPD(kBprLdL2); break;
         case kBprLdL2 | kBprJThru: MML_UPD(kBprLdL2 | kBprJThru); break;

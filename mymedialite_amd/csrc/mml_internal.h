@@ -158,9 +158,10 @@ std::vector<int64_t> device_id_counts(hipStream_t st, const int32_t* ids, int64_
 
 struct mml_ctx;
 namespace mml {
-// Hogwild flushing waves: wave 0 of every flush_every()-th block of an XCD group writes the L2's
-// dirty lines back after each batch of 64 updates (MML_FLUSH_EVERY, default 8)
-int32_t flush_every();
+// Hogwild flushing waves per XCD: wave 0 of that many evenly spaced blocks of an XCD group writes
+// the L2's dirty lines back after each batch of 64 updates (MML_FLUSHERS overrides the kernel's
+// default: BiasedMF 1, BPR 4 -- measured in DESIGN.md)
+int32_t flushers_per_xcd(int32_t dflt);
 // 8 when blocks b and b + 8 run on one XCD for every b of a 2,048-block grid (probed once per
 // context on the device; MML_XCD_GROUPS=1 forces 1), else 1
 int32_t xcd_groups(mml_ctx* ctx);

@@ -641,8 +641,12 @@ struct WoodSmem {
     int32_t ids[C::ITEMS];
 };
 
+// __launch_bounds__' second argument is the minimum waves per SIMD: 4 caps the kernel at 128
+// registers, so two 8-wave workgroups (4 rows) share a CU.  With (kThreads, 2) the compiler took
+// 142 VGPRs at NT = 4 and only one workgroup fit (C5 PMC: MFMA busy 25 %, waves parked 58 % of
+// their cycles on memory / barrier waits).
 template <int NT>
-__global__ __launch_bounds__(kThreads, 2) void wrmf_wood_kernel(
+__global__ __launch_bounds__(kThreads, 4) void wrmf_wood_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, int32_t* __restrict__ counter,
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols,
     const float* __restrict__ Q, int32_t k, float alpha, float* __restrict__ Tout) {

@@ -117,12 +117,12 @@ __global__ __launch_bounds__(256) void xcd_histogram_kernel(const int32_t* __res
 
 namespace mml {
 
-int32_t flush_every() {
+int32_t flushers_per_xcd(int32_t dflt) {
     static const int32_t v = [] {
-        const char* e = std::getenv("MML_FLUSH_EVERY");
-        return e ? std::max(1, std::atoi(e)) : 8;
+        const char* e = std::getenv("MML_FLUSHERS");
+        return e ? std::max(1, std::atoi(e)) : 0;
     }();
-    return v;
+    return v > 0 ? v : dflt;
 }
 
 int32_t xcd_groups(mml_ctx* ctx) {

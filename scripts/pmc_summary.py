@@ -1,7 +1,7 @@
 """Per-kernel PMC summary of a rocprofv3 --pmc run (rocpd SQLite output): counter sums per kernel
 name, dispatch count, total duration, and derived MFMA / issue utilisation on gfx950.
 
-  python scripts/pmc_summary.py <results.db> [kernel-substring ...]
+  python scripts/pmc_summary.py <results.db | csv output dir> [kernel-substring ...]
 MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 256 CUs * 4 SIMDs)
 (SQ_VALU_MFMA_BUSY_CYCLES counts cycles summed over SIMDs; GRBM_GUI_ACTIVE is summed over XCDs,
 MI355X_MICROARCH.md).  SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* are quad-cycles."""
@@ -10,10 +10,27 @@ import sys
 from collections import defaultdict
 
 
-def main(db, subs):
-    c = sqlite3.connect(db)
-    rows = c.execute("select dispatch_id, kernel_name, counter_name, value, duration "
+def load_rows(path):
+    """(dispatch, kernel, counter, value, duration ns) from a rocpd SQLite file or from a
+    directory holding rocprofv3's *counter_collection.csv (--output-format csv)."""
+    import csv
+    import glob
+    import os
+    if os.path.isdir(path):
+        rows = []
+        for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                dur = float(r.get("End_Timestamp", 0) or 0) - float(r.get("Start_Timestamp", 0) or 0)
+                rows.append((r["Dispatch_Id"], r["Kernel_Name"], r["Counter_Name"],
+                             float(r["Counter_Value"]), dur))
+        return rows
+    c = sqlite3.connect(path)
+    return c.execute("select dispatch_id, kernel_name, counter_name, value, duration "
                      "from counters_collection").fetchall()
+
+
+def main(db, subs):
+    rows = load_rows(db)
     acc = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
     dur = defaultdict(dict)

@@ -1,14 +1,17 @@
 """C3's AUC parity case: BPRMF on a 100k-user x 10k-item replica of the C3
 generator (users uniform, items Zipf(0.8), distinct positives, one positive per user held out),
-the GPU vs the exact-stream CPU oracle from the same initial model, k = 64, 8 epochs.
+the GPU vs the exact-stream CPU oracle from the same initial model, 8 epochs, at k = 64 and at C3's
+own k = 128.
 
 Both models are scored by the GPU Eval.Items AUC (mml_bpr_auc), which equals the oracle's
 Items.Evaluate restatement per user (tests/test_auc_gpu.py).
 
 * ORDERED (the device sampler's triples applied in sample order): stated tolerance |dAUC| <= 0.005
   (measured 0.0003-0.0006; the oracle itself spreads 0.0003 across seeds).
-* HOGWILD (the schedule C3 runs): measured +0.0095 above the sequential AUC (0.7875 vs 0.7778),
-  i.e. a different -- here better -- trajectory, not a worse one; asserted within [-0.005, +0.015].
+* HOGWILD (the schedule C3 runs): |dAUC| <= 0.005.  Measured +0.0038 (k = 64) and
+  +0.0028 (k = 128) with XCD-owned item groups, write-through j and user rows and 4 flushing waves
+  per XCD (bpr.hip); the round-1 kernel spread over all XCDs measured +0.0099 / +0.0061,
+  because each XCD's L2 held its own stale replicas of the hot rows.
 """
 import time
 
@@ -62,7 +65,7 @@ def replica(request):
 
 
 @pytest.mark.parametrize("schedule,lo,hi", [("ordered", -0.005, 0.005),
-                                            ("hogwild", -0.005, 0.015)])
+                                            ("hogwild", -0.005, 0.005)])
 def test_c3_replica_auc_parity(replica, schedule, lo, hi):
     tr_u, tr_i, test, st, auc_ref, k = replica
     Random.set_seed(7)

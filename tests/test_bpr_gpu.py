@@ -67,9 +67,9 @@ def test_bpr_auc_parity(sampling, schedule):
     print(f"BPR {sampling} {schedule}: AUC gpu {auc_gpu:.5f} oracle {auc_ref:.5f} users {n_gpu}")
     assert n_gpu == n_ref
     assert auc_ref > 0.75
-    # ORDERED: |dAUC| <= 0.01; HOGWILD applies 16 triples per wave step concurrently and lands at
-    # or above the sequential AUC (measured up to +0.012 on these replicas): [-0.01, +0.025]
-    lo, hi = (-0.01, 0.01) if schedule == "ordered" else (-0.01, 0.025)
+    # ORDERED: |dAUC| <= 0.01.  HOGWILD on this 96k-event replica (under 16 waves' worth) runs 4
+    # in-order streams on one CU (bpr.hip, small epochs): |dAUC| <= 0.01 as well
+    lo, hi = -0.01, 0.01
     assert lo <= auc_gpu - auc_ref <= hi
 
 
