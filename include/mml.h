@@ -103,6 +103,13 @@ enum {
     MML_READ_ITEM_IDENTITY = 4,
     MML_READ_WITHOUT_RATINGS = 8,
     MML_READ_ITEM_DATA = 16,
+    /* ABI 4: the binary cache of FileSerializer (IO/FileSerializer.cs:34-77): only when both
+     * columns use IdentityMapping (FileSerializer.Should), the parse result is kept next to the file
+     * as <path>.bin.mml.StaticRatings (ItemData: .bin.mml.PosOnlyFeedback) -- the library's own
+     * format, not BinaryFormatter's -- and a later read with the same flags loads it instead of
+     * parsing (the reference loads its cache whatever the flags; here they must match, else the
+     * text is parsed and the cache rewritten).  A cache that cannot be written is skipped. */
+    MML_READ_BINARY_CACHE = 32,
 };
 typedef struct mml_rating_file mml_rating_file;
 mml_status mml_rating_file_read(const char* path, int32_t flags, int32_t n_threads,

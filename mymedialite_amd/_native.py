@@ -184,7 +184,7 @@ def lib():
 
 
 READ_IGNORE_FIRST_LINE, READ_USER_IDENTITY, READ_ITEM_IDENTITY = 1, 2, 4
-READ_WITHOUT_RATINGS, READ_ITEM_DATA = 8, 16
+READ_WITHOUT_RATINGS, READ_ITEM_DATA, READ_BINARY_CACHE = 8, 16, 32
 
 
 def check(status: int):

@@ -1096,9 +1096,12 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         s.bias_reg = h->p.bias_reg;
         s.update_j = h->p.update_j;
         const int64_t n = h->n_events;  // Feedback.Count samples per epoch (:218)
+        // >= 65,536 triples per wave: C3 (500 M) still runs 7,629 waves, and a 1.9 M-event epoch
+        // runs 32 instead of 128 -- on the C3 replica the Hogwild AUC offset grows with the
+        // triples in flight (+0.0037 at 32 waves, +0.0050 at 128, k = 128; profiles/r2_xcd/r2i_*)
         static const int64_t min_chunk = [] {
             const char* e = std::getenv("MML_HOGWILD_MIN_CHUNK");
-            return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)16384;
+            return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)65536;
         }();
         int64_t waves = std::min<int64_t>(256 * 32, std::max<int64_t>(1, n / min_chunk));
         // fewer than 16 waves' worth of samples run as ONE workgroup: one CU, one L2, where 2+

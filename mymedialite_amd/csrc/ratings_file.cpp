@@ -212,6 +212,65 @@ void map_column(const uint64_t* hash, const Key* key, int64_t N, const char* con
 
 using mml::guard;
 
+namespace {
+
+// FileSerializer's cache restated for the native reader: header "MMLRAT01", the flags that shape
+// the parse, n_lines, n_ratings, then users[], items[], values[] (host byte order).
+constexpr char kCacheMagic[8] = {'M', 'M', 'L', 'R', 'A', 'T', '0', '1'};
+constexpr int32_t kCacheFlagMask = MML_READ_IGNORE_FIRST_LINE | MML_READ_WITHOUT_RATINGS |
+                                   MML_READ_ITEM_DATA;
+
+bool load_cache(const std::string& bin, int32_t flags, mml_rating_file& f) {
+    std::ifstream in(bin, std::ios::binary);
+    if (!in) return false;
+    char magic[8];
+    int32_t fl = 0;
+    int64_t nl = 0, nr = 0;
+    in.read(magic, 8);
+    in.read(reinterpret_cast<char*>(&fl), sizeof fl);
+    in.read(reinterpret_cast<char*>(&nl), sizeof nl);
+    in.read(reinterpret_cast<char*>(&nr), sizeof nr);
+    if (!in || std::memcmp(magic, kCacheMagic, 8) != 0 || fl != (flags & kCacheFlagMask) ||
+        nr < 0 || nl < nr)
+        return false;
+    f.n_lines = nl;
+    f.n_ratings = nr;
+    f.users.reset(new int32_t[std::max<int64_t>(1, nr)]);
+    f.items.reset(new int32_t[std::max<int64_t>(1, nr)]);
+    f.values.reset(new float[std::max<int64_t>(1, nr)]);
+    in.read(reinterpret_cast<char*>(f.users.get()), (std::streamsize)(sizeof(int32_t) * nr));
+    in.read(reinterpret_cast<char*>(f.items.get()), (std::streamsize)(sizeof(int32_t) * nr));
+    in.read(reinterpret_cast<char*>(f.values.get()), (std::streamsize)(sizeof(float) * nr));
+    return (bool)in;
+}
+
+void save_cache(const std::string& bin, int32_t flags, const mml_rating_file& f) {
+    // FileSerializer.CanWrite: no writable location, no cache
+    const std::string tmp = bin + ".tmp";
+    {
+        std::ofstream out(tmp, std::ios::binary | std::ios::trunc);
+        if (!out) return;
+        const int32_t fl = flags & kCacheFlagMask;
+        out.write(kCacheMagic, 8);
+        out.write(reinterpret_cast<const char*>(&fl), sizeof fl);
+        out.write(reinterpret_cast<const char*>(&f.n_lines), sizeof f.n_lines);
+        out.write(reinterpret_cast<const char*>(&f.n_ratings), sizeof f.n_ratings);
+        out.write(reinterpret_cast<const char*>(f.users.get()),
+                  (std::streamsize)(sizeof(int32_t) * f.n_ratings));
+        out.write(reinterpret_cast<const char*>(f.items.get()),
+                  (std::streamsize)(sizeof(int32_t) * f.n_ratings));
+        out.write(reinterpret_cast<const char*>(f.values.get()),
+                  (std::streamsize)(sizeof(float) * f.n_ratings));
+        if (!out) {
+            std::remove(tmp.c_str());
+            return;
+        }
+    }
+    std::rename(tmp.c_str(), bin.c_str());  // readers never see a partial cache
+}
+
+}  // namespace
+
 extern "C" mml_status mml_rating_file_read(const char* path, int32_t flags, int32_t n_threads,
                                            const char* const* user_seed, int32_t n_user_seed,
                                            const char* const* item_seed, int32_t n_item_seed,
@@ -225,6 +284,14 @@ extern "C" mml_status mml_rating_file_read(const char* path, int32_t flags, int3
         const bool item_data = flags & MML_READ_ITEM_DATA;
         const int want = item_data || (flags & MML_READ_WITHOUT_RATINGS) ? 2 : 3;
         std::unique_ptr<mml_rating_file> f(new mml_rating_file());
+        // FileSerializer.Should: neither column uses a Mapping
+        const bool use_cache = (flags & MML_READ_BINARY_CACHE) && user_identity && item_identity;
+        const std::string bin =
+            std::string(path) + (item_data ? ".bin.mml.PosOnlyFeedback" : ".bin.mml.StaticRatings");
+        if (use_cache && load_cache(bin, flags, *f)) {
+            *out = f.release();
+            return;
+        }
         size_t n = 0;
         std::unique_ptr<char[]> text;
         {
@@ -350,6 +417,7 @@ extern "C" mml_status mml_rating_file_read(const char* path, int32_t flags, int3
         if (!item_identity)
             map_column(ih.get(), ik.get(), N, item_seed, n_item_seed, T, at, f->items.get(),
                        f->new_items);
+        if (use_cache) save_cache(bin, flags, *f);
         *out = f.release();
     });
 }

@@ -211,7 +211,7 @@ def _native_read(path, user_mapping, item_mapping, flags, n_threads):
 
 
 def read_ratings(path: str, user_mapping=None, item_mapping=None, ignore_first_line=False,
-                 native=True, n_threads=8, with_ratings=True):
+                 native=True, n_threads=8, with_ratings=True, binary_cache=False):
     """StaticRatingData.Read (IO/StaticRatingData.cs:36-117): arrays sized by the line count,
     empty lines skipped, >= 3 columns (>= 2 and rating 0 with ``with_ratings=False``, the
     TestRatingFileFormat.WITHOUT_RATINGS variant).
@@ -219,6 +219,9 @@ def read_ratings(path: str, user_mapping=None, item_mapping=None, ignore_first_l
     Quirk kept: the rating scale is built from the whole sized array,
     so a blank line adds a level 0.  ``native``: the library's multi-threaded reader
     (mml_rating_file_read); False: this Python restatement (the two are tested equal).
+    ``binary_cache``: FileSerializer's cache (StaticRatingData.cs:43-59), used when both mappings
+    are IdentityMapping -- <path>.bin.mml.StaticRatings is loaded instead of parsing the text,
+    or written after the parse (MML_READ_BINARY_CACHE).
     """
     user_mapping = user_mapping or IdentityMapping()
     item_mapping = item_mapping or IdentityMapping()
@@ -226,7 +229,8 @@ def read_ratings(path: str, user_mapping=None, item_mapping=None, ignore_first_l
     if native:
         from . import _native as N
         flags = (N.READ_IGNORE_FIRST_LINE if ignore_first_line else 0) | \
-            (0 if with_ratings else N.READ_WITHOUT_RATINGS)
+            (0 if with_ratings else N.READ_WITHOUT_RATINGS) | \
+            (N.READ_BINARY_CACHE if binary_cache else 0)
         users, items, values, n_lines = _native_read(path, user_mapping, item_mapping, flags,
                                                      n_threads)
         scale = np.zeros(n_lines, np.float32)  # the sized array: blank lines are 0 (quirk above)
@@ -252,14 +256,15 @@ def read_ratings(path: str, user_mapping=None, item_mapping=None, ignore_first_l
 
 
 def read_items(path: str, user_mapping=None, item_mapping=None, ignore_first_line=False,
-               native=True, n_threads=8):
+               native=True, n_threads=8, binary_cache=False):
     """ItemData.Read (IO/ItemData.cs:59-94): user item per line, lines that Trim() to nothing
     skipped, >= 2 columns.  ``native``: mml_rating_file_read with MML_READ_ITEM_DATA."""
     user_mapping = user_mapping or IdentityMapping()
     item_mapping = item_mapping or IdentityMapping()
     if native:
         from . import _native as N
-        flags = N.READ_ITEM_DATA | (N.READ_IGNORE_FIRST_LINE if ignore_first_line else 0)
+        flags = N.READ_ITEM_DATA | (N.READ_IGNORE_FIRST_LINE if ignore_first_line else 0) | \
+            (N.READ_BINARY_CACHE if binary_cache else 0)
         users, items, _, _ = _native_read(path, user_mapping, item_mapping, flags, n_threads)
         return PosOnlyFeedback(users, items)
     users, items = [], []

@@ -8,10 +8,11 @@ Items.Evaluate restatement per user (tests/test_auc_gpu.py).
 
 * ORDERED (the device sampler's triples applied in sample order): stated tolerance |dAUC| <= 0.005
   (measured 0.0003-0.0006; the oracle itself spreads 0.0003 across seeds).
-* HOGWILD (the schedule C3 runs): |dAUC| <= 0.005.  Measured +0.0038 (k = 64) and
-  +0.0028 (k = 128) with XCD-owned item groups, write-through j and user rows and 4 flushing waves
-  per XCD (bpr.hip); the round-1 kernel spread over all XCDs measured +0.0099 / +0.0061,
-  because each XCD's L2 held its own stale replicas of the hot rows.
+* HOGWILD (the schedule C3 runs): |dAUC| <= 0.005.  Measured +0.0029 (k = 64) and
+  +0.0037 (k = 128) with XCD-owned item groups, write-through j and user rows, 4 flushing waves per
+  XCD and >= 65,536 triples per wave (32 waves here; bpr.hip).  The round-1 kernel
+  spread over all XCDs measured +0.0099 / +0.0083, because each XCD's L2 held its own stale
+  replicas of the hot rows; at 128 waves the new kernel measured +0.0039 / +0.0050 (in flight).
 """
 import time
 

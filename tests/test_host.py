@@ -316,3 +316,36 @@ def test_native_item_data_reader_equals_restatement(tmp_path):
     q.write_text("1 2\n34\n")
     with pytest.raises(Exception, match="at least 2 columns"):
         read_items(str(q))
+
+
+def test_binary_cache_like_file_serializer(tmp_path):
+    """FileSerializer's cache (IO/FileSerializer.cs:34-77, StaticRatingData.cs:43-59, ItemData.cs:
+    38-48) on the native reader: written after the first parse when both columns use
+    IdentityMapping, then loaded instead of the text (even after the text changes, as the
+    reference does); never with a Mapping; a flag change re-parses."""
+    import os
+    from mymedialite_amd import Mapping, read_items, read_ratings
+    p = tmp_path / "r.txt"
+    p.write_text("1 2 3\n4 5 1.5\n\n7 8 5\n")
+    a = read_ratings(str(p), binary_cache=True)
+    cache = str(p) + ".bin.mml.StaticRatings"
+    assert os.path.exists(cache)
+    p.write_text("9 9 9\n")  # the cache wins over the changed text
+    b = read_ratings(str(p), binary_cache=True)
+    np.testing.assert_array_equal(a.users, b.users)
+    np.testing.assert_array_equal(a.values, b.values)
+    assert list(b.users) == [1, 4, 7] and b.count == 3
+    c = read_ratings(str(p), binary_cache=False)  # no cache requested: the text
+    assert list(c.users) == [9]
+    d = read_ratings(str(p), ignore_first_line=True, binary_cache=True)  # other flags: re-parse
+    assert d.count == 0
+    m = Mapping()
+    e = read_ratings(str(p), user_mapping=m, binary_cache=True)  # a Mapping: never cached
+    assert list(e.users) == [0] and m.internal_to_original == ["9"]
+    q = tmp_path / "f.txt"
+    q.write_text("1 2\n3 4\n")
+    f1 = read_items(str(q), binary_cache=True)
+    assert os.path.exists(str(q) + ".bin.mml.PosOnlyFeedback")
+    q.write_text("5 6\n")
+    f2 = read_items(str(q), binary_cache=True)
+    np.testing.assert_array_equal(f1.users, f2.users)
