@@ -26,4 +26,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
   step pmc_c3_$c 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc_c3_${c}_$TAG -o c3 -- python bench.py --workload c3 --steps 2 --warmup 1 --no-cpu-baseline
 done
 step pmc_c5_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_c5_sq_$TAG -o c5 -- python bench.py --workload c5 --steps 1 --warmup 0 --no-cpu-baseline
+[ "${2:-}" = ingest ] || exit 0
 step ingest_1b 900 python -u scripts/bench_ingest_1b.py 1000000000 16 /dev/shm

@@ -292,3 +292,46 @@ def test_two_rank_bpr_user_shards_equal_emulation(tmp_path):
     s = U @ V.T + states[0][2]
     pos = s[u, i].mean()
     assert pos > s.mean() + 0.01
+
+
+def test_model_averaging_rmse_cost_vs_single_trajectory():
+    """The RMSE cost of SURVEY 8(e)'s per-epoch item averaging, measured with the oracle on the C1
+    stand-in (943 x 1,682, 80k training ratings, k = 10, the reference's defaults, 15 epochs):
+    N user shards each run their epoch from the same item side, then V || b_i is averaged (what
+    bench.py --gpus N and mml_ctx_create_multi do on the GPU).  Each shard's item updates are
+    divided by N, so the item side learns more slowly; the test states the measured cost."""
+    import oracle as O
+    from mymedialite_amd.synthetic import ml100k_standin
+    u, i, v, tu, ti, tv = ml100k_standin()
+    nu, ni, k = 943, 1682, 10
+    gb = O.global_bias(v, 1.0, 5.0)
+    kw = dict(gb=gb, min_rating=np.float32(1), range_=np.float32(4), lr=np.float32(0.01))
+    order = O.Rng(3).shuffle(np.arange(len(u), dtype=np.int32))
+    u, i, v = u[order], i[order], v[order]
+    rmse = {}
+    for world in (1, 2, 4):
+        r = O.Rng(1)
+        U = r.fill_normal(nu * k, 0, 0.1).reshape(nu, k)
+        V = r.fill_normal(ni * k, 0, 0.1).reshape(ni, k)
+        bu, bi = np.zeros(nu, np.float32), np.zeros(ni, np.float32)
+        bnd = balanced_user_shards(np.bincount(u, minlength=nu), world)
+        shards = [shard_ratings(u, i, v, bnd, x) for x in range(world)]
+        for _ in range(15):
+            Vs, bis = [], []
+            for su, si, sv in shards:
+                Vx, bix = V.copy(), bi.copy()
+                O.bmf_iterate(su, si, sv, np.arange(len(su), dtype=np.int32), U, Vx, bu, bix,
+                              **kw)
+                Vs.append(Vx)
+                bis.append(bix)
+            V = (sum(Vs) / np.float32(world)).astype(np.float32)
+            bi = (sum(bis) / np.float32(world)).astype(np.float32)
+        p = O.bmf_predict(tu, ti, U, V, bu, bi, gb, np.float32(1), np.float32(4))
+        rmse[world] = float(O.rating_eval(p, tv)[0])
+    print("test RMSE after 15 epochs by number of user shards:", rmse)
+    # measured: 1 shard 0.8926, 2 shards 0.9273, 4 shards 0.9487: the averaged item side learns
+    # N times more slowly at this size (each item gets ~50 ratings per epoch).  Summing the shards'
+    # deltas instead tracks the single trajectory at 2 shards (0.8966) but oscillates at 4 and 8
+    # (hot items overshoot), so the north star's averaging stays; DESIGN.md section 5.
+    assert rmse[1] < rmse[2] < rmse[4]
+    assert rmse[2] - rmse[1] <= 0.04 and rmse[4] - rmse[1] <= 0.07
