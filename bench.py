@@ -64,6 +64,10 @@ def main():
     ap.add_argument("--max-threads", type=int, default=4096,
                     help="C2 with --schedule dsgd: the reference's MaxThreads = G (G x G blocks, "
                          "G sub-epochs, deterministic and equal to the reference's DSGD)")
+    ap.add_argument("--ring", default="",
+                    help="C2 with --schedule dsgd: one multi-device context over these device ids "
+                         "(comma-separated, repeats allowed: several shards on one GPU) running the "
+                         "DSGD item-group ring from one process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--sampler", default="uniform_user",
@@ -100,7 +104,10 @@ def bench_c2(args):
     n_users_total = users_local
     n_items = args.items
 
-    ctx = N.Context(local)
+    ring = [int(x) for x in args.ring.split(",") if x.strip()] if args.ring else None
+    if ring and args.schedule != "dsgd":
+        raise SystemExit("--ring runs the DSGD schedule (--schedule dsgd)")
+    ctx = N.Context(ring if ring else local)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     lo = rank * users_local
@@ -129,8 +136,14 @@ def bench_c2(args):
     h = N._vp()
     N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(params), n_users_total, n_items,
                                    ctypes.byref(h)))
-    N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
-                                            values.data_ptr(), n_local, None))
+    if ring:  # a multi-device context takes host arrays and deals them out in set_blocks
+        hu_, hi_, hv_ = users.cpu().numpy(), items.cpu().numpy(), values.cpu().numpy()
+        N.check(N.lib().mml_bmf_set_data(h, N.ptr(hu_, N._i32p), N.ptr(hi_, N._i32p),
+                                         N.ptr(hv_, N._f32p), n_local, None))
+        del hu_, hi_, hv_
+    else:
+        N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
+                                                values.data_ptr(), n_local, None))
     N.check(N.lib().mml_bmf_set_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
                                       N.ptr(bu, N._f32p), N.ptr(bi, N._f32p), gb, 1.0, 5.0))
     # the same workload on the host for the CPU baseline: the whole stream (one full epoch each
@@ -219,7 +232,8 @@ def bench_c2(args):
             "config": {"workload": workload, "num_factors": k, "ratings_per_gpu": n_local,
                        "users_per_gpu": users_local, "items": n_items,
                        "schedule": args.schedule + (f" (MaxThreads={G})" if G else ""),
-                       "parallelism": f"user-shard x{world}"},
+                       "parallelism": (f"dsgd ring over devices {args.ring} (one process)"
+                                       if ring else f"user-shard x{world}")},
             "final_rmse": rmse,
             "initial_rmse": rmse0,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -48,11 +48,16 @@ mml_status mml_ctx_destroy(mml_ctx* ctx);
 /* One context over n GPUs driven from ONE process (ABI 4) -- the shape of the reference's
  * single-process front end (RatingPrediction.cs:161-331): an ncclCommInitAll communicator, one
  * stream per device.  Handles created on it shard the work over the devices: mml_bmf / mml_bpr
- * split the ratings into user ranges of equal rating count and average V || item biases with one
- * RCCL all-reduce after every epoch; mml_wrmf solves row shards and all-gathers
- * them after each half-step.  Each call drives the devices from one host thread per device and
- * returns when all have finished.  On such handles the exact schedules (ORDERED / DSGD), the
- * _device data setters and the sibling-model extras return MML_ERR_STATE. */
+ * on the HOGWILD schedules split the ratings into user ranges of equal rating count and average
+ * V || item biases with one RCCL all-reduce after every epoch; mml_bmf on the DSGD
+ * schedule runs the reference's MaxThreads = G blocks (BiasedMatrixFactorization.cs:205-215) as a
+ * ring: device d owns block rows [d G/n, (d+1) G/n), item groups move by peer copy to the device
+ * whose rows visit them next, and the model equals the single-device DSGD model bit for bit
+ * (G must be a multiple of n); mml_wrmf solves row shards and all-gathers them after each
+ * half-step.  Each call returns when all devices have finished.  On such handles the ORDERED
+ * schedule, the _device data setters and the sibling-model extras return MML_ERR_STATE.  A device
+ * id may be listed more than once (several shards on one GPU, e.g. to test the ring on one
+ * device); such a context has no communicator, so only the DSGD ring runs on it. */
 mml_status mml_ctx_create_multi(const int32_t* device_ids, int32_t n_devices, mml_ctx** out);
 /* RCCL communicator across processes (one rank per GPU): rank 0 creates the 128-byte id, the host
  * broadcasts it (e.g. torch.distributed / MPI), then every rank calls mml_ctx_comm_init. */
@@ -200,7 +205,9 @@ mml_status mml_bmf_set_data_device(mml_bmf* h, const int32_t* users_device,
                                    const int32_t* items_device, const float* values_device,
                                    int64_t n, const int32_t* order_device);
 /* DSGD blocks (MML_SCHEDULE_DSGD): CSR over b = user_group*G + item_group of rating indices,
- * as produced by MultiCore.PartitionUsersAndItems / mml_partition_users_and_items. */
+ * as produced by MultiCore.PartitionUsersAndItems / mml_partition_users_and_items.  On a
+ * multi-device context the indices address the arrays given to mml_bmf_set_data, and the call
+ * deals the block rows out to the devices. */
 mml_status mml_bmf_set_blocks(mml_bmf* h, int32_t num_groups, const int64_t* offsets,
                               const int32_t* indices);
 /* Model upload (InitModel is host-side RNG work: MatrixFactorization.cs:99-116). */

@@ -30,6 +30,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <vector>
 
@@ -125,16 +126,17 @@ struct RatingStep<kPlainMF> {
 };
 
 // ORDERED / DSGD: workgroup = one wavefront; wavefront j walks block (j, (subepoch+j) mod G).
-// KM = factors per lane (k <= 64 * KM).
+// A DSGD ring shard holds the block rows row0 .. row0 + gridDim.x - 1 only (block_off local to
+// them).  KM = factors per lane (k <= 64 * KM).
 template <int LOSS, int KM>
 __global__ __launch_bounds__(64) void bmf_sgd_ordered_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
-    const int64_t* __restrict__ block_off, int32_t G, int32_t subepoch, float* U, float* V,
-    float* bu, float* bi, int32_t k, int32_t ld, BmfScalars s, const int32_t* __restrict__ cnt_u,
-    const int32_t* __restrict__ cnt_i) {
+    const int64_t* __restrict__ block_off, int32_t G, int32_t subepoch, int32_t row0, float* U,
+    float* V, float* bu, float* bi, int32_t k, int32_t ld, BmfScalars s,
+    const int32_t* __restrict__ cnt_u, const int32_t* __restrict__ cnt_i) {
     const int lane = threadIdx.x;
-    const int j = blockIdx.x;
-    const int64_t b = (int64_t)j * G + (subepoch + j) % G;
+    const int j = row0 + blockIdx.x;
+    const int64_t b = (int64_t)blockIdx.x * G + (subepoch + j) % G;
     const int64_t begin = block_off[b], end = block_off[b + 1];
     for (int64_t x = begin; x < end; ++x) {
         const int32_t u = su[x], i = si[x];
@@ -869,6 +871,38 @@ __global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ a, int64
         a[x] *= f;
 }
 
+// packed[x] = M[ids[x]] (rows of ld floats) and packed_b[x] = b[ids[x]] (b may be null)
+__global__ __launch_bounds__(256) void rows_gather_kernel(const float* __restrict__ M,
+                                                          const float* __restrict__ b,
+                                                          const int32_t* __restrict__ ids,
+                                                          int64_t n, int32_t ld,
+                                                          float* __restrict__ packed,
+                                                          float* __restrict__ packed_b) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * ld;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = e / ld;
+        const int32_t f = (int32_t)(e - x * ld), r = ids[x];
+        packed[e] = M[(int64_t)r * ld + f];
+        if (f == 0 && b) packed_b[x] = b[r];
+    }
+}
+
+// the inverse: M[ids[x]] = packed[x], b[ids[x]] = packed_b[x]
+__global__ __launch_bounds__(256) void rows_scatter_kernel(const float* __restrict__ packed,
+                                                           const float* __restrict__ packed_b,
+                                                           const int32_t* __restrict__ ids,
+                                                           int64_t n, int32_t ld,
+                                                           float* __restrict__ M,
+                                                           float* __restrict__ b) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * ld;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = e / ld;
+        const int32_t f = (int32_t)(e - x * ld), r = ids[x];
+        M[(int64_t)r * ld + f] = packed[e];
+        if (f == 0) b[r] = packed_b[x];
+    }
+}
+
 inline int grid_for(int64_t n, int block = 256, int cap = 8192) {
     const int64_t g = (n + block - 1) / block;
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
@@ -1286,6 +1320,23 @@ struct mml_bmf {
     // (U, b_u trained there; V, b_i replicated and averaged after every epoch)
     std::vector<mml_bmf*> shards;
     std::vector<int32_t> ub;
+    std::vector<int32_t> cnt_u_host, cnt_i_host;  // the whole data set's counts
+    // DSGD ring on a multi-device context: device d owns the block rows [d m, (d + 1) m) (m = G /
+    // devices) and with them its user groups; item groups travel to the device whose window
+    // needs them.  The multi handle keeps the raw ratings until set_blocks deals them out, the
+    // group of every user / item (-1: no rating), and per item group the device holding its
+    // newest rows (-1: every device, as after set_model).  A shard keeps its first block row,
+    // the items of every group in group order (gi_off on the host), the staging rows of the
+    // peer copies and the event its last pack recorded.
+    std::vector<int32_t> hu, hi;
+    std::vector<float> hr;
+    std::vector<int32_t> ugroup, igroup, hold;
+    std::vector<int64_t> gi_off;
+    bool synced0 = true;  // shard 0 holds the newest copy of every row
+    int32_t row0 = 0;
+    mml::DeviceArray<int32_t> gi_ids;
+    mml::DeviceArray<float> stage_v, stage_b;
+    hipEvent_t ev_pack = nullptr;
 };
 
 namespace {
@@ -1447,14 +1498,13 @@ void social_epoch(mml_bmf* h, const BmfScalars& s) {
 
 template <int LOSS>
 void launch_ordered(mml_bmf* h, const int64_t* off, int32_t G, int32_t sub, int grid,
-                    const BmfScalars& s, const int32_t* cu, const int32_t* ci) {
+                    const BmfScalars& s, const int32_t* cu, const int32_t* ci, int32_t row0 = 0) {
     const int km = (h->k + 63) / 64;
     hipStream_t st = h->ctx->stream;
 #define MML_ORD(KM)                                                                            \
-    bmf_sgd_ordered_kernel<LOSS, KM><<<grid, 64, 0, st>>>(h->su.get(), h->si.get(), h->sr.get(), \
-                                                          off, G, sub, h->U.get(), h->V.get(),  \
-                                                          h->bu.get(), h->bi.get(), h->k, h->ld, \
-                                                          s, cu, ci)
+    bmf_sgd_ordered_kernel<LOSS, KM><<<grid, 64, 0, st>>>(                                     \
+        h->su.get(), h->si.get(), h->sr.get(), off, G, sub, row0, h->U.get(), h->V.get(),       \
+        h->bu.get(), h->bi.get(), h->k, h->ld, s, cu, ci)
     switch (km) {
         case 1: MML_ORD(1); break;
         case 2: MML_ORD(2); break;
@@ -1758,8 +1808,11 @@ void multi_create(mml_ctx* ctx, const mml_bmf_params* params, int32_t n_users, i
     MML_REQUIRE(params->model == MML_MF_BIASED || params->model == MML_MF_PLAIN,
                 "a multi-device context trains MML_MF_BIASED / MML_MF_PLAIN");
     MML_REQUIRE(params->schedule == MML_SCHEDULE_HOGWILD ||
-                    params->schedule == MML_SCHEDULE_HOGWILD_COHERENT,
-                "a multi-device context trains with the HOGWILD schedules (user shards)");
+                    params->schedule == MML_SCHEDULE_HOGWILD_COHERENT ||
+                    params->schedule == MML_SCHEDULE_DSGD,
+                "a multi-device context trains with the HOGWILD schedules (user shards) or DSGD "
+                "(the item-group ring)");
+    if (params->schedule != MML_SCHEDULE_DSGD) mml::require_comm(ctx);
     h->ctx = ctx;
     h->p = *params;
     h->n_users = n_users;
@@ -1774,6 +1827,24 @@ void multi_create(mml_ctx* ctx, const mml_bmf_params* params, int32_t n_users, i
     h->ub[0] = 0;
 }
 
+bool multi_dsgd(const mml_bmf* h) { return h->p.schedule == MML_SCHEDULE_DSGD; }
+
+// a shard's frequency-regularisation / InitModel counts are the whole data set's
+mml_status upload_counts(mml_bmf* s, const std::vector<int32_t>& cu,
+                         const std::vector<int32_t>& ci) {
+    return mml::guard([&] {
+        s->ctx->activate();
+        hipStream_t st = s->ctx->stream;
+        if (!cu.empty())
+            MML_HIP(hipMemcpyAsync(s->cnt_u.get(), cu.data(), sizeof(int32_t) * cu.size(),
+                                   hipMemcpyHostToDevice, st));
+        if (!ci.empty())
+            MML_HIP(hipMemcpyAsync(s->cnt_i.get(), ci.data(), sizeof(int32_t) * ci.size(),
+                                   hipMemcpyHostToDevice, st));
+        MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
 void multi_set_data(mml_bmf* h, const int32_t* users, const int32_t* items, const float* values,
                     int64_t n, const int32_t* order) {
     const int32_t nd = (int32_t)h->shards.size();
@@ -1782,6 +1853,21 @@ void multi_set_data(mml_bmf* h, const int32_t* users, const int32_t* items, cons
                         items[x] < h->n_items,
                     "rating user/item id or order index out of range");
         if (order) MML_REQUIRE(order[x] >= 0 && order[x] < n, "order index out of range");
+    }
+    h->cnt_u_host.assign(h->n_users, 0);
+    h->cnt_i_host.assign(h->n_items, 0);
+    for (int64_t x = 0; x < n; ++x) {
+        ++h->cnt_u_host[users[x]];
+        ++h->cnt_i_host[items[x]];
+    }
+    if (multi_dsgd(h)) {  // dealt out by set_blocks (its indices address these raw arrays)
+        h->hu.assign(users, users + n);
+        h->hi.assign(items, items + n);
+        h->hr.assign(values, values + n);
+        h->G = 0;
+        h->n = n;
+        h->has_data = true;
+        return;
     }
     h->ub = mml::balanced_user_bounds(users, n, h->n_users, nd);
     std::vector<std::vector<int32_t>> su(nd), si(nd);
@@ -1794,8 +1880,10 @@ void multi_set_data(mml_bmf* h, const int32_t* users, const int32_t* items, cons
         sr[d].push_back(values[o]);
     }
     mml::on_devices(h->ctx, [&](int32_t d) {
-        return mml_bmf_set_data(h->shards[d], su[d].data(), si[d].data(), sr[d].data(),
-                                (int64_t)su[d].size(), nullptr);
+        mml_status st = mml_bmf_set_data(h->shards[d], su[d].data(), si[d].data(), sr[d].data(),
+                                         (int64_t)su[d].size(), nullptr);
+        if (st == MML_OK) st = upload_counts(h->shards[d], h->cnt_u_host, h->cnt_i_host);
+        return st;
     });
     h->n = n;
     h->has_data = true;
@@ -1882,6 +1970,260 @@ void multi_get_model(mml_bmf* h, float* U, float* V, float* bu, float* bi) {
     });
 }
 
+// ---- DSGD ring (the reference's MaxThreads = G schedule, BiasedMatrixFactorization.cs:205-215,
+// over several devices).  Blocks of one sub-epoch share no user or item, so each device runs the
+// block rows it owns exactly as the single-device DSGD launch would, and the only exchange is an
+// item group moving to the device whose window (the m item groups its rows visit) needs it next:
+// its rows are packed on the holder, peer-copied (one xGMI hop; a device-local copy when a device
+// is listed twice) and scattered on the new owner, ordered by events.  The result is the
+// single-device DSGD result, bit for bit.
+
+// the model with each row taken from the device holding its newest copy (host arrays, each
+// nullable): users from their group's device, items from their group's holder, rows without a
+// rating from device 0 (every device holds the same copy of those)
+void dsgd_gather(mml_bmf* h, float* U, float* V, float* bu, float* bi) {
+    const int32_t nd = (int32_t)h->shards.size();
+    const int32_t m = h->G > 0 ? h->G / nd : 1;
+    std::vector<std::vector<int32_t>> uid(nd), iid(nd);
+    for (int32_t u = 0; u < h->n_users; ++u) {
+        const int32_t g = h->G > 0 ? h->ugroup[u] : -1;
+        uid[g < 0 ? 0 : g / m].push_back(u);
+    }
+    for (int32_t i = 0; i < h->n_items; ++i) {
+        const int32_t g = h->G > 0 ? h->igroup[i] : -1;
+        iid[g < 0 || h->hold[g] < 0 ? 0 : h->hold[g]].push_back(i);
+    }
+    mml::on_devices(h->ctx, [&](int32_t d) {
+        return mml::guard([&] {
+            mml_bmf* s = h->shards[d];
+            s->ctx->activate();
+            hipStream_t st = s->ctx->stream;
+            auto pull = [&](const std::vector<int32_t>& ids, const float* M, const float* b,
+                            float* outM, float* outB) {
+                const int64_t n = (int64_t)ids.size();
+                if (n == 0 || (!outM && !outB)) return;
+                mml::DeviceArray<int32_t> di;
+                mml::DeviceArray<float> pm, pb;
+                di.alloc(n);
+                pm.alloc((size_t)n * s->ld);
+                pb.alloc(n);
+                MML_HIP(hipMemcpyAsync(di.get(), ids.data(), sizeof(int32_t) * n,
+                                       hipMemcpyHostToDevice, st));
+                rows_gather_kernel<<<grid_for(n * s->ld), 256, 0, st>>>(M, b, di.get(), n, s->ld,
+                                                                         pm.get(), pb.get());
+                MML_HIP(hipGetLastError());
+                std::vector<float> hm((size_t)n * s->ld), hb(n);
+                MML_HIP(hipMemcpyAsync(hm.data(), pm.get(), sizeof(float) * hm.size(),
+                                       hipMemcpyDeviceToHost, st));
+                MML_HIP(hipMemcpyAsync(hb.data(), pb.get(), sizeof(float) * n,
+                                       hipMemcpyDeviceToHost, st));
+                MML_HIP(hipStreamSynchronize(st));
+                for (int64_t x = 0; x < n; ++x) {
+                    if (outM)
+                        std::copy(hm.begin() + x * s->ld, hm.begin() + x * s->ld + s->k,
+                                  outM + (int64_t)ids[x] * s->k);
+                    if (outB) outB[ids[x]] = hb[x];
+                }
+            };
+            pull(uid[d], s->U.get(), s->bu.get(), U, bu);
+            pull(iid[d], s->V.get(), s->bi.get(), V, bi);
+        });
+    });
+}
+
+// every device gets the newest model (before the groups change)
+void dsgd_sync_all(mml_bmf* h) {
+    std::vector<float> U((size_t)h->n_users * h->k), V((size_t)h->n_items * h->k),
+        bu(h->n_users), bi(h->n_items);
+    dsgd_gather(h, U.data(), V.data(), bu.data(), bi.data());
+    mml_bmf* s0 = h->shards[0];
+    mml::on_devices(h->ctx, [&](int32_t d) {
+        return mml_bmf_set_model(h->shards[d], U.data(), V.data(), bu.data(), bi.data(), s0->gb,
+                                 s0->min_rating, s0->max_rating);
+    });
+    std::fill(h->hold.begin(), h->hold.end(), -1);
+    h->synced0 = true;
+}
+
+// device 0 gets the newest copy of every row (Predict / Evaluate run there); the other devices'
+// rows and the holders stay as they are
+void dsgd_sync0(mml_bmf* h) {
+    if (h->synced0) return;
+    std::vector<float> U((size_t)h->n_users * h->k), V((size_t)h->n_items * h->k),
+        bu(h->n_users), bi(h->n_items);
+    dsgd_gather(h, U.data(), V.data(), bu.data(), bi.data());
+    mml_bmf* s0 = h->shards[0];
+    const mml_status st = mml_bmf_set_model(s0, U.data(), V.data(), bu.data(), bi.data(), s0->gb,
+                                            s0->min_rating, s0->max_rating);
+    if (st != MML_OK) mml::fail(st, mml_last_error());
+    h->synced0 = true;
+}
+
+void multi_set_blocks(mml_bmf* h, int32_t G, const int64_t* offsets, const int32_t* indices) {
+    const int32_t nd = (int32_t)h->shards.size();
+    MML_REQUIRE(multi_dsgd(h), "set_blocks on a multi-device context needs the DSGD schedule");
+    MML_REQUIRE(h->has_data, "set_data must precede set_blocks");
+    MML_REQUIRE(G % nd == 0, "the DSGD ring needs num_groups (MaxThreads) to be a multiple of "
+                             "the device count");
+    const int64_t nb = (int64_t)G * G;
+    MML_REQUIRE(offsets[0] == 0, "offsets[0] must be 0");
+    for (int64_t b = 0; b < nb; ++b)
+        MML_REQUIRE(offsets[b + 1] >= offsets[b], "offsets must be non-decreasing");
+    MML_REQUIRE(offsets[nb] <= h->n && (offsets[nb] == 0 || indices),
+                "block indices exceed ratings");
+    for (int64_t x = 0; x < offsets[nb]; ++x)
+        MML_REQUIRE(indices[x] >= 0 && indices[x] < h->n, "block index out of range");
+    if (h->has_model && h->G > 0) dsgd_sync_all(h);  // the holders refer to the old groups
+    std::vector<int32_t> ug(h->n_users, -1), ig(h->n_items, -1);
+    for (int64_t b = 0; b < nb; ++b) {
+        const int32_t j = (int32_t)(b / G), c = (int32_t)(b % G);
+        for (int64_t x = offsets[b]; x < offsets[b + 1]; ++x) {
+            int32_t& gu = ug[h->hu[indices[x]]];
+            int32_t& gi = ig[h->hi[indices[x]]];
+            MML_REQUIRE((gu < 0 || gu == j) && (gi < 0 || gi == c),
+                        "blocks are not a user-group x item-group partition");
+            gu = j;
+            gi = c;
+        }
+    }
+    const int32_t m = G / nd;
+    std::vector<int64_t> gi_off(G + 1, 0);
+    for (int32_t i = 0; i < h->n_items; ++i)
+        if (ig[i] >= 0) ++gi_off[ig[i] + 1];
+    for (int32_t c = 0; c < G; ++c) gi_off[c + 1] += gi_off[c];
+    std::vector<int32_t> gi_ids(std::max<int64_t>(1, gi_off[G]));
+    {
+        std::vector<int64_t> at(gi_off.begin(), gi_off.end() - 1);
+        for (int32_t i = 0; i < h->n_items; ++i)
+            if (ig[i] >= 0) gi_ids[at[ig[i]]++] = i;
+    }
+    mml::on_devices(h->ctx, [&](int32_t d) {
+        mml_bmf* s = h->shards[d];
+        std::vector<int32_t> lu, li;
+        std::vector<float> lr;
+        std::vector<int64_t> loff((size_t)m * G + 1, 0);
+        for (int64_t lb = 0; lb < (int64_t)m * G; ++lb) {
+            const int64_t b = (int64_t)d * m * G + lb;  // block rows d m .. (d + 1) m - 1
+            for (int64_t x = offsets[b]; x < offsets[b + 1]; ++x) {
+                lu.push_back(h->hu[indices[x]]);
+                li.push_back(h->hi[indices[x]]);
+                lr.push_back(h->hr[indices[x]]);
+            }
+            loff[lb + 1] = (int64_t)lu.size();
+        }
+        mml_status st = mml_bmf_set_data(s, lu.data(), li.data(), lr.data(), (int64_t)lu.size(),
+                                         nullptr);
+        if (st == MML_OK) st = upload_counts(s, h->cnt_u_host, h->cnt_i_host);
+        if (st != MML_OK) return st;
+        return mml::guard([&] {
+            s->ctx->activate();
+            hipStream_t hs = s->ctx->stream;
+            s->block_off.alloc(loff.size());
+            MML_HIP(hipMemcpyAsync(s->block_off.get(), loff.data(), sizeof(int64_t) * loff.size(),
+                                   hipMemcpyHostToDevice, hs));
+            s->gi_ids.alloc(gi_ids.size());
+            MML_HIP(hipMemcpyAsync(s->gi_ids.get(), gi_ids.data(),
+                                   sizeof(int32_t) * gi_ids.size(), hipMemcpyHostToDevice, hs));
+            s->stage_v.alloc(gi_ids.size() * (size_t)s->ld);
+            s->stage_b.alloc(gi_ids.size());
+            if (!s->ev_pack) MML_HIP(hipEventCreateWithFlags(&s->ev_pack, hipEventDisableTiming));
+            MML_HIP(hipStreamSynchronize(hs));
+            s->G = G;
+            s->row0 = d * m;
+        });
+    });
+    h->ugroup.swap(ug);
+    h->igroup.swap(ig);
+    h->gi_off.swap(gi_off);
+    h->hold.assign(G, -1);
+    h->G = G;
+}
+
+template <int LOSS>
+void dsgd_ring_epoch(mml_bmf* h, float learn_rate, const int32_t* seq) {
+    const int32_t nd = (int32_t)h->shards.size(), G = h->G, m = G / nd;
+    const mml_bmf* s0 = h->shards[0];
+    BmfScalars sc;
+    sc.gb = s0->gb;
+    sc.min_rating = s0->min_rating;
+    sc.range = s0->max_rating - s0->min_rating;
+    sc.lr = learn_rate;
+    sc.blr = h->p.bias_learn_rate * learn_rate;
+    sc.bias_reg = h->p.bias_reg;
+    sc.reg_u = h->p.reg_u;
+    sc.reg_i = h->p.reg_i;
+    struct Move {
+        int32_t from, to;
+        int64_t r0, r1;  // rows of the group-ordered item list
+    };
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<Move> mv;
+    std::vector<char> packed(nd);
+    for (int32_t x = 0; x < G; ++x) {
+        const int32_t sq = seq[x];
+        mv.clear();
+        for (int32_t c = 0; c < G; ++c) {  // group c is visited by block row (c - sq) mod G
+            const int32_t to = ((c - sq) % G + G) % G / m, from = h->hold[c];
+            h->hold[c] = to;
+            if (from < 0 || from == to || h->gi_off[c + 1] == h->gi_off[c]) continue;
+            if (!mv.empty() && mv.back().from == from && mv.back().to == to &&
+                mv.back().r1 == h->gi_off[c])
+                mv.back().r1 = h->gi_off[c + 1];
+            else
+                mv.push_back({from, to, h->gi_off[c], h->gi_off[c + 1]});
+        }
+        std::fill(packed.begin(), packed.end(), 0);
+        for (const Move& v : mv) {
+            mml_bmf* a = h->shards[v.from];
+            a->ctx->activate();
+            const int64_t n = v.r1 - v.r0;
+            rows_gather_kernel<<<grid_for(n * a->ld), 256, 0, a->ctx->stream>>>(
+                a->V.get(), a->bi.get(), a->gi_ids.get() + v.r0, n, a->ld,
+                a->stage_v.get() + v.r0 * a->ld, a->stage_b.get() + v.r0);
+            MML_HIP(hipGetLastError());
+            packed[v.from] = 1;
+        }
+        for (int32_t d = 0; d < nd; ++d)
+            if (packed[d]) {
+                mml_bmf* a = h->shards[d];
+                a->ctx->activate();
+                MML_HIP(hipEventRecord(a->ev_pack, a->ctx->stream));
+            }
+        for (const Move& v : mv) {
+            mml_bmf *a = h->shards[v.from], *b = h->shards[v.to];
+            b->ctx->activate();
+            hipStream_t st = b->ctx->stream;
+            const int64_t n = v.r1 - v.r0;
+            MML_HIP(hipStreamWaitEvent(st, a->ev_pack, 0));
+            MML_HIP(hipMemcpyPeerAsync(b->stage_v.get() + v.r0 * b->ld, b->ctx->device,
+                                       a->stage_v.get() + v.r0 * a->ld, a->ctx->device,
+                                       sizeof(float) * n * b->ld, st));
+            MML_HIP(hipMemcpyPeerAsync(b->stage_b.get() + v.r0, b->ctx->device,
+                                       a->stage_b.get() + v.r0, a->ctx->device, sizeof(float) * n,
+                                       st));
+            rows_scatter_kernel<<<grid_for(n * b->ld), 256, 0, st>>>(
+                b->stage_v.get() + v.r0 * b->ld, b->stage_b.get() + v.r0, b->gi_ids.get() + v.r0,
+                n, b->ld, b->V.get(), b->bi.get());
+            MML_HIP(hipGetLastError());
+        }
+        for (int32_t d = 0; d < nd; ++d) {
+            mml_bmf* s = h->shards[d];
+            s->ctx->activate();
+            const bool fr = h->p.frequency_regularization != 0;
+            launch_ordered<LOSS>(s, s->block_off.get(), G, sq, m, sc, fr ? s->cnt_u.get() : nullptr,
+                                 fr ? s->cnt_i.get() : nullptr, s->row0);
+        }
+    }
+    for (int32_t d = 0; d < nd; ++d) {
+        h->shards[d]->ctx->activate();
+        MML_HIP(hipStreamSynchronize(h->shards[d]->ctx->stream));
+    }
+    h->last_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0)
+                     .count();
+    h->last_launches = G * nd;
+    h->synced0 = false;
+}
+
 }  // namespace
 
 extern "C" mml_status mml_bmf_create(mml_ctx* ctx, const mml_bmf_params* params, int32_t n_users,
@@ -1946,6 +2288,7 @@ extern "C" mml_status mml_bmf_destroy(mml_bmf* h) {
         }
         (void)hipSetDevice(h->ctx->device);
         (void)hipStreamSynchronize(h->ctx->stream);
+        if (h->ev_pack) (void)hipEventDestroy(h->ev_pack);
         delete h;
     });
 }
@@ -2013,7 +2356,10 @@ extern "C" mml_status mml_bmf_set_blocks(mml_bmf* h, int32_t num_groups, const i
                                          const int32_t* indices) {
     return guard([&] {
         check_handle(h);
-        single_device_only(h);
+        if (h->ctx->multi()) {
+            MML_REQUIRE(num_groups >= 1 && offsets, "bad block arguments");
+            return multi_set_blocks(h, num_groups, offsets, indices);
+        }
         MML_REQUIRE(h->has_data, "set_data must precede set_blocks");
         MML_REQUIRE(num_groups >= 1 && offsets, "bad block arguments");
         const int64_t nb = (int64_t)num_groups * num_groups;
@@ -2064,6 +2410,8 @@ extern "C" mml_status mml_bmf_set_model(mml_bmf* h, const float* U, const float*
                 return mml_bmf_set_model(h->shards[d], U, V, bu, bi, global_bias, min_rating,
                                          max_rating);
             });
+            std::fill(h->hold.begin(), h->hold.end(), -1);
+            h->synced0 = true;
             h->has_model = true;
             return;
         }
@@ -2112,10 +2460,13 @@ extern "C" mml_status mml_bmf_init_model(mml_bmf* h, uint64_t seed, double mean,
         check_handle(h);
         if (h->ctx->multi()) {  // same seed on every device: one item side, users by range
             MML_REQUIRE(h->has_data, "set_data must precede init_model");
+            MML_REQUIRE(!multi_dsgd(h) || h->G > 0, "set_blocks must precede init_model");
             mml::on_devices(h->ctx, [&](int32_t d) {
                 return mml_bmf_init_model(h->shards[d], seed, mean, stddev, global_bias,
                                           min_rating, max_rating);
             });
+            std::fill(h->hold.begin(), h->hold.end(), -1);
+            h->synced0 = true;
             h->has_model = true;
             return;
         }
@@ -2146,6 +2497,7 @@ extern "C" mml_status mml_bmf_get_model(mml_bmf* h, float* U, float* V, float* b
         check_handle(h);
         if (h->ctx->multi()) {
             MML_REQUIRE(h->has_model, "no model");
+            if (multi_dsgd(h)) return dsgd_gather(h, U, V, bu, bi);
             return multi_get_model(h, U, V, bu, bi);
         }
         MML_REQUIRE(h->has_model, "no model (set_model first)");
@@ -2167,6 +2519,26 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
                                       const int32_t* subepoch_sequence) {
     return guard([&] {
         check_handle(h);
+        if (h->ctx->multi() && multi_dsgd(h)) {  // one host thread drives the ring
+            MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
+            MML_REQUIRE(h->G > 0, "DSGD schedule needs set_blocks");
+            MML_REQUIRE(subepoch_sequence, "DSGD schedule needs a sub-epoch sequence");
+            for (int32_t x = 0; x < h->G; ++x)
+                MML_REQUIRE(subepoch_sequence[x] >= 0 && subepoch_sequence[x] < h->G,
+                            "sub-epoch index out of range");
+            if (h->n == 0) return;
+            switch (h->p.model == MML_MF_PLAIN ? kPlainMF : h->p.loss) {
+                case kPlainMF: dsgd_ring_epoch<kPlainMF>(h, learn_rate, subepoch_sequence); break;
+                case MML_LOSS_MAE:
+                    dsgd_ring_epoch<MML_LOSS_MAE>(h, learn_rate, subepoch_sequence);
+                    break;
+                case MML_LOSS_LOGISTIC:
+                    dsgd_ring_epoch<MML_LOSS_LOGISTIC>(h, learn_rate, subepoch_sequence);
+                    break;
+                default: dsgd_ring_epoch<MML_LOSS_RMSE>(h, learn_rate, subepoch_sequence); break;
+            }
+            return;
+        }
         if (h->ctx->multi()) {  // every device's epoch, then the item all-reduce (its thread)
             MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
             std::vector<float> ms(h->shards.size(), 0.0f);
@@ -2258,6 +2630,12 @@ extern "C" mml_status mml_bmf_predict(mml_bmf* h, const int32_t* users, const in
         if (h->ctx->multi()) {
             MML_REQUIRE(n >= 0 && (n == 0 || (users && items && out)), "null arrays");
             MML_REQUIRE(h->has_model, "no model");
+            if (multi_dsgd(h)) {
+                dsgd_sync0(h);
+                const mml_status st = mml_bmf_predict(h->shards[0], users, items, n, out);
+                if (st != MML_OK) mml::fail(st, mml_last_error());
+                return;
+            }
             return multi_predict(h, users, items, n, out);
         }
         MML_REQUIRE(h->has_model, "no model");
@@ -2285,6 +2663,12 @@ extern "C" mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const i
         if (h->ctx->multi()) {
             MML_REQUIRE(n >= 0 && (n == 0 || (users && items && values)) && out, "null arrays");
             MML_REQUIRE(h->has_model, "no model");
+            if (multi_dsgd(h)) {
+                dsgd_sync0(h);
+                const mml_status st = mml_bmf_evaluate(h->shards[0], users, items, values, n, out);
+                if (st != MML_OK) mml::fail(st, mml_last_error());
+                return;
+            }
             return multi_evaluate(h, users, items, values, n, out);
         }
         MML_REQUIRE(h->has_model, "no model");

@@ -654,6 +654,7 @@ extern "C" mml_status mml_bpr_create(mml_ctx* ctx, const mml_bpr_params* params,
                         params->schedule <= MML_BPR_SCHEDULE_ORDERED,
                     "unknown schedule");
         if (ctx->multi()) {
+            mml::require_comm(ctx);
             MML_REQUIRE(params->schedule != MML_BPR_SCHEDULE_ORDERED,
                         "a multi-device context trains with the HOGWILD / AUTO schedules");
             auto* h = new mml_bpr();

@@ -62,10 +62,11 @@ extern "C" mml_status mml_ctx_create_multi(const int32_t* device_ids, int32_t n_
                                            mml_ctx** out) {
     return guard([&] {
         MML_REQUIRE(out && device_ids && n_devices >= 1, "need >= 1 device id");
+        bool repeated = false;
         for (int32_t a = 0; a < n_devices; ++a)
-            for (int32_t b = a + 1; b < n_devices; ++b)
-                MML_REQUIRE(device_ids[a] != device_ids[b], "duplicate device id");
+            for (int32_t b = a + 1; b < n_devices; ++b) repeated |= device_ids[a] == device_ids[b];
         auto* ctx = new mml_ctx();
+        ctx->repeated = repeated;
         try {
             for (int32_t d = 0; d < n_devices; ++d) {
                 mml_ctx* s = nullptr;
@@ -74,12 +75,14 @@ extern "C" mml_status mml_ctx_create_multi(const int32_t* device_ids, int32_t n_
                 ctx->sub.push_back(s);
             }
             // one communicator over the devices, driven from this process (no unique-id exchange)
-            std::vector<ncclComm_t> comms(n_devices);
-            MML_RCCL(ncclCommInitAll(comms.data(), n_devices, device_ids));
-            for (int32_t d = 0; d < n_devices; ++d) {
-                ctx->sub[d]->comm = comms[d];
-                ctx->sub[d]->nranks = n_devices;
-                ctx->sub[d]->rank = d;
+            if (!repeated) {
+                std::vector<ncclComm_t> comms(n_devices);
+                MML_RCCL(ncclCommInitAll(comms.data(), n_devices, device_ids));
+                for (int32_t d = 0; d < n_devices; ++d) {
+                    ctx->sub[d]->comm = comms[d];
+                    ctx->sub[d]->nranks = n_devices;
+                    ctx->sub[d]->rank = d;
+                }
             }
             ctx->device = ctx->sub[0]->device;
             ctx->stream = ctx->sub[0]->stream;

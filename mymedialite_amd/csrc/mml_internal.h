@@ -172,6 +172,9 @@ struct mml_ctx {
     // holding rank d of one ncclCommInitAll communicator; the fields below are sub[0]'s copies
     std::vector<mml_ctx*> sub;
     bool multi() const { return !sub.empty(); }
+    // a device id listed more than once (several shards on one GPU): no communicator is built, so
+    // only the schedules that move data with peer copies (BiasedMF DSGD) run on it
+    bool repeated = false;
     int32_t device = 0;
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;
@@ -202,6 +205,13 @@ void on_devices(const mml_ctx* ctx, F&& f) {
     for (size_t d = 0; d < n; ++d)
         if (st[d] != MML_OK)
             fail(st[d], "device " + std::to_string(ctx->sub[d]->device) + ": " + msg[d]);
+}
+
+// the collectives of the user-sharded Hogwild handles need one communicator over distinct devices
+inline void require_comm(const mml_ctx* ctx) {
+    if (ctx->repeated)
+        fail(MML_ERR_STATE, "a multi-device context that lists a device more than once has no "
+                            "communicator: only the BiasedMF DSGD schedule runs on it");
 }
 
 // contiguous user ranges [b[d], b[d + 1]) with balanced rating counts (the multi-device shards;

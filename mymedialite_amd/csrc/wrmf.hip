@@ -671,6 +671,7 @@ extern "C" mml_status mml_wrmf_create(mml_ctx* ctx, const mml_wrmf_params* param
         MML_REQUIRE(params->num_factors >= 1 && params->num_factors <= 256,
                     "num_factors must be in [1, 256]");
         if (ctx->multi()) {
+            mml::require_comm(ctx);
             auto* h = new mml_wrmf();
             h->ctx = ctx;
             h->p = *params;

@@ -143,3 +143,62 @@ def test_wrmf_multi_device_context_equals_single():
     np.testing.assert_array_equal(out["multi"][1], out["single"][1])
     st = O.wrmf_train(u, i, 300, 140, seed=4, k=6, num_iter=2)
     assert np.max(np.abs(out["multi"][0] - st["U"])) <= 1e-5 * (1 + np.max(np.abs(st["U"])))
+
+
+@pytest.mark.parametrize("ndev,G,loss,freq", [(2, 4, "RMSE", False), (2, 8, "MAE", True),
+                                              (4, 8, "RMSE", False), (3, 6, "LogisticLoss", False)])
+def test_bmf_dsgd_ring_equals_single_device(ndev, G, loss, freq):
+    """The DSGD ring (BiasedMatrixFactorization.cs:205-215 over several devices): ``ndev`` shards
+    on one GPU (a device listed ``ndev`` times: every shard has its own stream, model copy and
+    staging rows, and the item groups really travel between them by peer copy) give the
+    single-device MaxThreads = G DSGD model bit for bit, after every epoch, and the same
+    Predict / Evaluate."""
+    from test_bmf_gpu import gpu_train
+    u, i, v = synth_ratings(31, 600, 250, 30000)
+    tu, ti, tv = synth_ratings(32, 600, 250, 3000)
+    out = {}
+    for name, props in (("single", dict(Device=0)), ("ring", dict(Gpus=",".join(["0"] * ndev)))):
+        m, snaps = gpu_train(u, i, v, seed=13, k=24, num_iter=3, snapshots=True, MaxThreads=G,
+                             Loss=loss, FrequencyRegularization=freq, **props)
+        assert m.schedule() == "dsgd"
+        out[name] = (snaps, m.predict(tu, ti), m.evaluate(Ratings(tu, ti, tv))["RMSE"])
+    (s1, p1, r1), (s2, p2, r2) = out["single"], out["ring"]
+    for e in range(4):
+        for key in ("U", "V", "bu", "bi"):
+            np.testing.assert_array_equal(s2[e][key], s1[e][key], err_msg=f"epoch {e} {key}")
+    np.testing.assert_array_equal(p2, p1)
+    assert r2 == r1
+
+
+def test_bmf_dsgd_ring_matches_oracle():
+    """Two shards, MaxThreads = 8, against the oracle's DSGD (the CPU restatement of the
+    reference's threaded epoch)."""
+    from test_bmf_gpu import gpu_train
+    u, i, v = synth_ratings(44, 1500, 800, 40000)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    r = Ratings(u, i, v)
+    st = O.bmf_train(u, i, v, nu, ni, r.scale_min, r.scale_max, seed=8, k=32, num_iter=2,
+                     max_threads=8)
+    m, _ = gpu_train(u, i, v, seed=8, k=32, num_iter=2, MaxThreads=8, Gpus="0,0")
+    md = m.get_model()
+    for key, ok in (("U", "U"), ("V", "V"), ("bi", "bi"), ("bu", "bu")):
+        assert np.max(np.abs(md[key] - st[ok])) <= 1e-5, key
+
+
+def test_repeated_device_context_limits():
+    """A context listing a device twice has no communicator: the Hogwild user shards (which
+    average through RCCL) refuse it, and the ring needs MaxThreads divisible by the devices."""
+    u, i, v = synth_ratings(5, 200, 90, 4000)
+    with pytest.raises(N.MMLError, match="communicator"):
+        m = BiasedMatrixFactorization(NumFactors=4, NumIter=1, Schedule="hogwild", Gpus="0,0")
+        m.ratings = Ratings(u, i, v)
+        m.train()
+    with pytest.raises(N.MMLError, match="communicator"):
+        tr_u, tr_i, _, _ = planted_feedback(2, 300, 60, 8)
+        b = BPRMF(NumFactors=4, NumIter=1, Gpus="0,0")
+        b.feedback = PosOnlyFeedback(tr_u, tr_i)
+        b.train()
+    with pytest.raises(N.MMLError, match="multiple of the device count"):
+        m = BiasedMatrixFactorization(NumFactors=4, NumIter=1, MaxThreads=5, Gpus="0,0")
+        m.ratings = Ratings(u, i, v)
+        m.train()
