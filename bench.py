@@ -68,6 +68,9 @@ def main():
                     help="C2 with --schedule dsgd: one multi-device context over these device ids "
                          "(comma-separated, repeats allowed: several shards on one GPU) running the "
                          "DSGD item-group ring from one process")
+    ap.add_argument("--wrmf-precision", default="fp64", choices=["fp64", "fp32"],
+                    help="C5: fp64 = the fp32 MFMA solve + one pass of fp64 iterative refinement "
+                         "(the reference's fp64 result); fp32 = the solve alone (throughput)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--sampler", default="uniform_user",
@@ -653,8 +656,9 @@ def bench_wrmf(args):
     deg_i = torch.bincount(keys % n_items, minlength=n_items).double()
     nnz = int(keys.numel())
     del keys
-    flops_exec = wrmf_executed_flops(deg_u, deg_i, k)
-    p = N.WrmfParams(k, 0, 1.0, 0.015)
+    passes = 1 if args.wrmf_precision == "fp64" else 0
+    flops_exec = wrmf_executed_flops(deg_u, deg_i, k, passes, nnz)
+    p = N.WrmfParams(k, passes, 1.0, 0.015)
     h = N._vp()
     N.check(N.lib().mml_wrmf_create(ctx.handle, ctypes.byref(p), n_users, n_items,
                                     ctypes.byref(h)))
@@ -691,8 +695,11 @@ def bench_wrmf(args):
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None,
-        "dtype": "f32 (k > 128: fp32 row solves, HH in fp64; the reference solves in fp64, so "
-                 "this line is a throughput figure, parity is stated at 2e-3 in the tests)",
+        "dtype": ("f64 (fp32 MFMA row solves + one pass of iterative refinement with the residual "
+                  "b - A x in fp64: the fp64 solution, 2e-7 of the oracle in the tests)"
+                  if passes else
+                  "f32 (k > 128: fp32 row solves, HH in fp64; the reference solves in fp64, so "
+                  "this line is a throughput figure, parity is stated at 2e-3 in the tests)"),
         "data": "synthetic (100 positives per user, items Zipf(0.8), generated in HBM)",
         "config": {"workload": "C5: WRMF 5M users x 500k items, 500M positives, k=256",
                    "num_factors": k, "events": n, "users": n_users, "items": n_items,
@@ -705,7 +712,11 @@ def bench_wrmf(args):
                      "flops_note": "executed algorithmic flops: Woodbury rows (deg <= 128) "
                                    "deg(deg+1)k + deg^3/3 + 2 deg k + 2k^2, direct rows "
                                    "k(k+1)deg + k^3/3 + 2k^2 + 2 deg k, per half HH k(k+1)n and "
-                                   "Q = H L^-T n k^2, on the distinct (user, item) sets",
+                                   "Q = H L^-T n k^2, on the distinct (user, item) sets; each "
+                                   "refinement pass repeats the row solves (+ 2k^2 per Woodbury "
+                                   "row for s = L^-1 r) and adds the fp64 residual 2 n k^2 + "
+                                   "4 nnz k",
+                     "refine_passes": passes,
                      "flops_direct_equivalent": flops_direct,
                      "frac_direct_equivalent": flops_direct / (np.mean(ms) * 1e-3) / 1e12 / 157.3},
         "cpu_baseline": None if (args.no_cpu_baseline or world > 1) else cpu_baseline_wrmf(
@@ -719,19 +730,23 @@ def bench_wrmf(args):
     ctx.close()
 
 
-def wrmf_executed_flops(deg_u, deg_i, k):
+def wrmf_executed_flops(deg_u, deg_i, k, passes=0, nnz=0):
     """Flops one WRMF.Iterate() of the library executes (algorithmic, no padding): the user half
     solves rows with deg <= 128 by Woodbury (k > 128, wrmf_tiles.hip), the rest directly; the
-    item half likewise.  deg_*: float64 torch tensors of distinct-set sizes."""
+    item half likewise.  Each fp64 refinement pass repeats the row solves (plus s = L^-1 r on the
+    Woodbury rows) and adds the residual (X HH: 2 n k^2; the entries: 4 nnz k).  deg_*: float64
+    torch tensors of distinct-set sizes."""
     def half(deg, n_other):
         wood = (deg <= 128) & (deg > 0) if k > 128 else torch.zeros_like(deg, dtype=torch.bool)
         direct = (deg > 0) & ~wood
         dw, dd = deg[wood], deg[direct]
-        f = float((dw * (dw + 1) * k + dw ** 3 / 3 + 2 * dw * k).sum()) + 2.0 * k * k * len(dw)
-        f += float((k * (k + 1) * dd + 2 * dd * k).sum()) + (k ** 3 / 3 + 2 * k * k) * len(dd)
-        f += k * (k + 1) * n_other  # HH = H^T H
+        solve = float((dw * (dw + 1) * k + dw ** 3 / 3 + 2 * dw * k).sum()) + 2.0 * k * k * len(dw)
+        solve += float((k * (k + 1) * dd + 2 * dd * k).sum()) + (k ** 3 / 3 + 2 * k * k) * len(dd)
+        f = solve + k * (k + 1) * n_other  # HH = H^T H
         if len(dw):
             f += n_other * k * k  # Q = H L^-T
+        if passes and k > 128:
+            f += passes * (solve + 2.0 * k * k * len(dw) + 2.0 * len(deg) * k * k + 4.0 * nnz * k)
         return f
     return half(deg_u, len(deg_i)) + half(deg_i, len(deg_u))
 

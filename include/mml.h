@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 4
+#define MML_ABI_VERSION 5
 
 typedef int32_t mml_status;
 enum {
@@ -391,8 +391,10 @@ mml_status mml_bpr_allreduce_items(mml_bpr* h);
 /* ------------------------------------------------------------------ WRMF */
 typedef struct {
     int32_t num_factors;   /* NumFactors (MF.cs:43-45), <= 256: k <= 128 solves in fp64, k > 128
-                              in fp32 (packed A must fit the 160 KiB LDS) */
-    int32_t reserved;
+                              in fp32 on the matrix cores (A in fp64 does not fit the LDS) */
+    int32_t refine_passes; /* k > 128 (ABI 5): passes of fp64 iterative refinement after the fp32
+                              solve, x += A^{-1} (b - A x) with the residual in fp64; 1 reaches the
+                              fp64 solution (WRMF.cs:137-154), 0 = the fp32 result */
     double alpha;          /* Alpha (WRMF.cs:56) */
     double regularization; /* Regularization (WRMF.cs:59) */
 } mml_wrmf_params;

@@ -64,7 +64,7 @@ BPR_SCHEDULE_AUTO, BPR_SCHEDULE_HOGWILD, BPR_SCHEDULE_ORDERED = 0, 1, 2
 
 class WrmfParams(ctypes.Structure):
     """mml_wrmf_params (include/mml.h)."""
-    _fields_ = [("num_factors", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    _fields_ = [("num_factors", ctypes.c_int32), ("refine_passes", ctypes.c_int32),
                 ("alpha", ctypes.c_double), ("regularization", ctypes.c_double)]
 
 # every exported symbol of include/mml.h: name -> (restype, argtypes)

@@ -128,12 +128,34 @@ struct WrmfTilePlan {
     DeviceArray<int32_t> wood[4];
     int32_t n_wood[4] = {0, 0, 0, 0};
     DeviceArray<float> linv, linvt, qbuf, tbuf;  // L^{-1}, L^{-T} of HH + reg I; Q = H L^{-T}; t rows
+    DeviceArray<float> sbuf;                      // refinement: s = L^{-1} r per Woodbury row
+    // fp64 iterative refinement (wrmf_tile_refine): the residual's entry segments (rows with
+    // several segments reduce their partials in order), x and r in fp64 for rows [r0, r1), the
+    // residual / correction rows in fp32 (W-shaped), a rocBLAS handle for X HH
+    int64_t r0 = 0, r1 = 0;
+    DeviceArray<uint8_t> rsegs, rmulti;
+    int64_t n_rsegs = 0, n_rmulti = 0, n_rslots = 0;
+    DeviceArray<double> rpartial, x64, r64;
+    DeviceArray<float> rf, df;
+    void* blas = nullptr;
+    WrmfTilePlan() = default;
+    WrmfTilePlan(const WrmfTilePlan&) = delete;
+    WrmfTilePlan& operator=(const WrmfTilePlan&) = delete;
+    ~WrmfTilePlan();
 };
 void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p, int64_t r0,
                     int64_t r1, bool woodbury);  // rows [r0, r1) of this rank
+// rhs == nullptr: W rows <- A^{-1} b (fp32).  rhs (W-shaped, fp32): W rows <- A^{-1} rhs rows,
+// reusing the tables the preceding plain call of the same half-step built.
 void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
                      const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
-                     double alpha, double reg, int& launches);
+                     double alpha, double reg, int& launches, const float* rhs = nullptr);
+// after wrmf_tile_solve: `passes` rounds of x += A^{-1}(b - A x) with the residual in fp64 (exact
+// float products, double sums) and the correction from the fp32 solver, so W rows [r0, r1) reach
+// the accuracy of the reference's fp64 solve (WRMF.cs:137-154)
+void wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
+                      const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
+                      double alpha, double reg, int32_t passes, int& launches);
 
 // XCD-owned item groups (xcd.hip): items dealt into 8 groups of equal weight, a stream partitioned
 // (stable) by the group of its item; group g's span goff[g] .. goff[g + 1] is served by blocks

@@ -25,6 +25,8 @@
 //   * backward substitution L^T w = y by 32-column blocks: w_J = T_J^T (y_J - sum_{I>J} L_IJ^T w_I).
 // Precision: fp32 with fused multiply-adds (the packed fp64 matrix of the parity path does not fit
 // the LDS at k > 128); the tolerance against the fp64 oracle is stated in tests/test_wrmf_gpu.py.
+#include <rocblas/rocblas.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -396,7 +398,8 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, int32_t* __restrict__ counter,
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols, float* __restrict__ W,
     const float* __restrict__ H, const float* __restrict__ HHt, const double* __restrict__ gram,
-    int32_t k, int32_t kdim, float alpha, float* __restrict__ Tout, int32_t dbg) {
+    int32_t k, int32_t kdim, float alpha, float* __restrict__ Tout, int32_t dbg,
+    const float* __restrict__ rhs) {
     __shared__ Smem sm;
     const int wave = threadIdx.x >> 6;
     const int nt = (kdim + 31) >> 5, nr = nt + 1;
@@ -450,6 +453,12 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
                     const float* hh = HHt + tile_id(tl.I[s], tl.J[s], nr) * 1024 + lane;
 #pragma unroll
                     for (int g = 0; g < 16; ++g) acc[s][g] = hh[g * 64] + alpha * acc[s][g];
+                } else if (rhs) {  // a refinement pass: the residual row replaces b
+#pragma unroll
+                    for (int g = 0; g < 16; ++g) {
+                        const int cc = 32 * tl.J[s] + rho(g, h);
+                        acc[s][g] = (q == 0 && cc < k) ? rhs[(int64_t)row * k + cc] : 0.0f;
+                    }
                 } else {
 #pragma unroll
                     for (int g = 0; g < 16; ++g) acc[s][g] *= 1.0f + alpha;
@@ -638,6 +647,7 @@ struct WoodSmem {
     float wv[C::HSW];
     float sv[32];
     float part[NT][32];
+    float yr[C::ITEMS];  // a refinement pass: the b row y = Q_S s
     int32_t ids[C::ITEMS];
 };
 
@@ -649,7 +659,8 @@ template <int NT>
 __global__ __launch_bounds__(kThreads, 4) void wrmf_wood_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, int32_t* __restrict__ counter,
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols,
-    const float* __restrict__ Q, int32_t k, float alpha, float* __restrict__ Tout) {
+    const float* __restrict__ Q, int32_t k, float alpha, float* __restrict__ Tout,
+    const float* __restrict__ S) {
     using C = WoodCfg<NT>;
     extern __shared__ __attribute__((aligned(16))) char wood_smem[];
     __shared__ int32_t base_row;
@@ -748,7 +759,19 @@ __global__ __launch_bounds__(kThreads, 4) void wrmf_wood_kernel(
             __syncthreads();
             cur ^= 1;
         }
-        // ---- C' = [I / alpha + C (identity on the padding); b row = 1 on the deg columns]
+        // a refinement pass solves A d = r: with s = L^{-1} r (S, one row per list entry) the
+        // b row is y = Q_S s and the output t = s - Q_S^T w (then d = L^{-T} t, scale 1)
+        if (S) {
+            for (int x = tg; x < C::ITEMS; x += C::TG) {
+                float a = 0.0f;
+                if (x < deg)
+                    for (int f = 0; f < k; ++f)
+                        a += Q[(int64_t)sm.ids[x] * k + f] * S[(int64_t)li * k + f];
+                sm.yr[x] = a;
+            }
+            __syncthreads();
+        }
+        // ---- C' = [I / alpha + C (identity on the padding); b row = 1 (or y) on the deg columns]
 #pragma unroll
         for (int s = 0; s < C::SLOTS; ++s) {
             if (TI[s] < 0) continue;
@@ -760,7 +783,7 @@ __global__ __launch_bounds__(kThreads, 4) void wrmf_wood_kernel(
                 if (TI[s] < NT) {
                     if (r == cc) v += cc < deg ? ainv : 1.0f;
                 } else {
-                    v = (q == 0 && cc < deg) ? 1.0f : 0.0f;
+                    v = (q == 0 && cc < deg) ? (S ? sm.yr[cc] : 1.0f) : 0.0f;
                 }
                 acc[s][g] = v;
             }
@@ -873,7 +896,7 @@ __global__ __launch_bounds__(kThreads, 4) void wrmf_wood_kernel(
                     a1 += sm.wv[x + 1] * Q[(int64_t)sm.ids[x + 1] * k + f];
                 }
                 if (x < deg) a0 += sm.wv[x] * Q[(int64_t)sm.ids[x] * k + f];
-                Tout[(int64_t)li * k + f] = a0 + a1;
+                Tout[(int64_t)li * k + f] = S ? S[(int64_t)li * k + f] - (a0 + a1) : a0 + a1;
             }
     }
 }
@@ -881,7 +904,7 @@ __global__ __launch_bounds__(kThreads, 4) void wrmf_wood_kernel(
 template <int NT>
 void launch_wood(hipStream_t st, const int32_t* rows, int32_t n, int32_t* counter,
                  const int64_t* off, const int32_t* cols, const float* Q, int32_t k, float alpha,
-                 float* Tout) {
+                 float* Tout, const float* S) {
     using C = WoodCfg<NT>;
     constexpr size_t lds = sizeof(WoodSmem<NT>) * C::R;
     static const bool attr = [] {
@@ -893,7 +916,7 @@ void launch_wood(hipStream_t st, const int32_t* rows, int32_t n, int32_t* counte
     MML_HIP(hipMemsetAsync(counter, 0, sizeof(int32_t), st));
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + C::R - 1) / C::R, 512));
     wrmf_wood_kernel<NT><<<grid, kThreads, lds, st>>>(rows, n, counter, off, cols, Q, k, alpha,
-                                                      Tout);
+                                                      Tout, S);
 }
 
 // Y[yrow(r)] = scale * X[xrow(r)] * M for n rows (X, Y row-major [.. x k], M [k x k] row-major,
@@ -955,6 +978,94 @@ int debug_mask() {
         return e ? std::atoi(e) : 0;
     }();
     return v;
+}
+
+// ---- fp64 iterative refinement: r = b - A x = sum_{i in S} ((1 + alpha) - alpha h_i.x) h_i
+//      - (HH + reg I) x, the first term per entry segment (one wave per entry, lane l holds
+//      features 4l .. 4l + 3: h_i.x by a wave reduction, then the scaled h_i accumulated), the
+//      second by one dgemm over all rows (R is initialised to it).  float * float products are
+//      exact in double, so A is the reference's matrix up to its own float rounding of products.
+struct RSeg {
+    int32_t row;   // local row (row - r0)
+    int32_t slot;  // -1: the row's only segment (adds into R); else its partial's slot
+    int64_t b, e;
+};
+struct RMulti {
+    int32_t row, slot0, nslot, pad;
+};
+constexpr int kRSeg = 2048;  // entries per residual segment
+
+__global__ __launch_bounds__(256) void wrmf_resid_seg_kernel(
+    const RSeg* __restrict__ segs, int64_t nseg, const int32_t* __restrict__ cols,
+    const float* __restrict__ H, int32_t k, const double* __restrict__ X, double alpha,
+    double* __restrict__ R, double* __restrict__ partial) {
+    __shared__ double red[4][256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, f0 = 4 * lane;
+    for (int64_t sgi = blockIdx.x; sgi < nseg; sgi += gridDim.x) {
+        const RSeg sg = segs[sgi];
+        const double* xr = X + (int64_t)sg.row * k;
+        double x[4], acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = f0 + j < k ? xr[f0 + j] : 0.0;
+        for (int64_t e = sg.b + wave; e < sg.e; e += 4) {
+            const float* hr = H + (int64_t)cols[e] * k;
+            double hv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) hv[j] = f0 + j < k ? (double)hr[f0 + j] : 0.0;
+            double t = hv[0] * x[0] + hv[1] * x[1] + hv[2] * x[2] + hv[3] * x[3];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+            const double c = (1.0 + alpha) - alpha * t;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] += c * hv[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[wave][f0 + j] = acc[j];
+        __syncthreads();
+        const int f = threadIdx.x;
+        if (f < k) {
+            const double v = red[0][f] + red[1][f] + red[2][f] + red[3][f];
+            if (sg.slot < 0)
+                R[(int64_t)sg.row * k + f] += v;
+            else
+                partial[(int64_t)sg.slot * k + f] = v;
+        }
+        __syncthreads();
+    }
+}
+
+// rows with several segments: R += their partials, in segment order (deterministic)
+__global__ __launch_bounds__(256) void wrmf_resid_multi_kernel(const RMulti* __restrict__ m,
+                                                               int64_t n, int32_t k,
+                                                               const double* __restrict__ partial,
+                                                               double* __restrict__ R) {
+    for (int64_t x = blockIdx.x; x < n; x += gridDim.x) {
+        const RMulti r = m[x];
+        for (int f = threadIdx.x; f < k; f += blockDim.x) {
+            double v = 0.0;
+            for (int s = 0; s < r.nslot; ++s) v += partial[(int64_t)(r.slot0 + s) * k + f];
+            R[(int64_t)r.row * k + f] += v;
+        }
+    }
+}
+
+// rows [r0, r0 + n): op 0 X = (double) W, 1 Rf = (float) R, 2 X += D, 3 W = (float) X
+__global__ __launch_bounds__(256) void wrmf_refine_rows_kernel(int op, int64_t r0, int64_t n,
+                                                               int32_t k, float* __restrict__ W,
+                                                               double* __restrict__ X,
+                                                               const double* __restrict__ R,
+                                                               float* __restrict__ Rf,
+                                                               const float* __restrict__ D) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * k;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t g = r0 * k + e;
+        switch (op) {
+            case 0: X[e] = (double)W[g]; break;
+            case 1: Rf[g] = (float)R[e]; break;
+            case 2: X[e] += (double)D[g]; break;
+            default: W[g] = (float)X[e]; break;
+        }
+    }
 }
 
 constexpr int kHeavy = 8192;   // rows with more entries take the split Gram
@@ -1021,7 +1132,97 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
         MML_HIP(hipMemcpyAsync(p.segs.get(), segs.data(), segs.size() * sizeof(Seg),
                                hipMemcpyHostToDevice, st));
     p.counter.alloc(1);
+    // the refinement residual's entry segments over rows [r0, r1)
+    std::vector<RSeg> rs;
+    std::vector<RMulti> rm;
+    int32_t slots = 0;
+    for (int64_t r = r0; r < r1; ++r) {
+        const int64_t b = begin[r], e = begin[r + 1];
+        if (e == b) continue;
+        const int32_t lr = (int32_t)(r - r0);
+        if (e - b <= kRSeg) {
+            rs.push_back(RSeg{lr, -1, b, e});
+            continue;
+        }
+        const int32_t s0 = slots;
+        for (int64_t x = b; x < e; x += kRSeg) rs.push_back(RSeg{lr, slots++, x, std::min(e, x + kRSeg)});
+        rm.push_back(RMulti{lr, s0, slots - s0, 0});
+    }
+    p.r0 = r0;
+    p.r1 = r1;
+    p.n_rsegs = (int64_t)rs.size();
+    p.n_rmulti = (int64_t)rm.size();
+    p.n_rslots = slots;
+    p.rsegs.alloc(std::max<size_t>(1, rs.size() * sizeof(RSeg)));
+    if (!rs.empty())
+        MML_HIP(hipMemcpyAsync(p.rsegs.get(), rs.data(), rs.size() * sizeof(RSeg),
+                               hipMemcpyHostToDevice, st));
+    p.rmulti.alloc(std::max<size_t>(1, rm.size() * sizeof(RMulti)));
+    if (!rm.empty())
+        MML_HIP(hipMemcpyAsync(p.rmulti.get(), rm.data(), rm.size() * sizeof(RMulti),
+                               hipMemcpyHostToDevice, st));
     MML_HIP(hipStreamSynchronize(st));
+}
+
+WrmfTilePlan::~WrmfTilePlan() {
+    if (blas) (void)rocblas_destroy_handle(reinterpret_cast<rocblas_handle>(blas));
+}
+
+void wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
+                      const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
+                      double alpha, double reg, int32_t passes, int& launches) {
+    const int64_t n = p.r1 - p.r0, n_w = (int64_t)(p.r1);  // W rows addressed up to r1
+    if (passes <= 0 || n <= 0) return;
+    if (!p.blas) {
+        rocblas_handle bh = nullptr;
+        if (rocblas_create_handle(&bh) != rocblas_status_success)
+            fail(MML_ERR_HIP, "rocblas_create_handle failed");
+        p.blas = bh;
+    }
+    auto bh = reinterpret_cast<rocblas_handle>(p.blas);
+    if (rocblas_set_stream(bh, st) != rocblas_status_success)
+        fail(MML_ERR_HIP, "rocblas_set_stream failed");
+    p.x64.alloc((size_t)n * k);
+    p.r64.alloc((size_t)n * k);
+    p.rf.alloc((size_t)n_w * k);
+    p.df.alloc((size_t)n_w * k);
+    p.rpartial.alloc(std::max<int64_t>(1, p.n_rslots) * (size_t)k);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n * k + 255) / 256, 16384));
+    auto rows = [&](int op) {
+        wrmf_refine_rows_kernel<<<grid, 256, 0, st>>>(op, p.r0, n, k, W, p.x64.get(), p.r64.get(),
+                                                      p.rf.get(), p.df.get());
+        ++launches;
+    };
+    rows(0);
+    const double m1 = -1.0, mreg = -reg;
+    for (int32_t pass = 0; pass < passes; ++pass) {
+        // R = -(HH + reg I) X, then + sum_i c_i h_i per row
+        MML_HIP(hipMemcpyAsync(p.r64.get(), p.x64.get(), sizeof(double) * n * k,
+                               hipMemcpyDeviceToDevice, st));
+        if (rocblas_dgemm(bh, rocblas_operation_none, rocblas_operation_none, k, (rocblas_int)n, k,
+                          &m1, HH, k, p.x64.get(), k, &mreg, p.r64.get(), k) !=
+            rocblas_status_success)
+            fail(MML_ERR_HIP, "rocblas_dgemm failed");
+        if (p.n_rsegs > 0) {
+            const int gs = (int)std::min<int64_t>(p.n_rsegs, 8192);
+            wrmf_resid_seg_kernel<<<gs, 256, 0, st>>>(
+                reinterpret_cast<const RSeg*>(p.rsegs.get()), p.n_rsegs, cols, H, k, p.x64.get(),
+                alpha, p.r64.get(), p.rpartial.get());
+        }
+        if (p.n_rmulti > 0)
+            wrmf_resid_multi_kernel<<<(int)std::min<int64_t>(p.n_rmulti, 8192), 256, 0, st>>>(
+                reinterpret_cast<const RMulti*>(p.rmulti.get()), p.n_rmulti, k, p.rpartial.get(),
+                p.r64.get());
+        MML_HIP(hipGetLastError());
+        rows(1);
+        // D = A^{-1} R on the fp32 solver (rows outside [r0, r1) are not read)
+        wrmf_tile_solve(st, p, p.df.get(), H, h_rows, off, cols, HH, k, alpha, reg, launches,
+                        p.rf.get());
+        rows(2);
+        launches += 3;
+    }
+    rows(3);
+    MML_HIP(hipGetLastError());
 }
 
 // L^{-1} (lower) of B = HH + reg I by Cholesky in fp64 on the host (k <= 256: ~10 M flops)
@@ -1051,13 +1252,15 @@ static void chol_inverse(const std::vector<double>& HH, int k, double reg, std::
 
 void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
                      const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
-                     double alpha, double reg, int& launches) {
+                     double alpha, double reg, int& launches, const float* rhs) {
     MML_REQUIRE(k > 128 && k <= 256, "tile solver covers 128 < k <= 256");
     const int nt = (k + 31) >> 5, nr = nt + 1;
     const int ntile = nt * nr - nt * (nt - 1) / 2;
-    p.hht.alloc((size_t)kTiles * 1024);
-    wrmf_tile_hh_kernel<<<(ntile * 1024 + 255) / 256, 256, 0, st>>>(HH, k, reg, p.hht.get());
-    ++launches;
+    if (!rhs) {  // a refinement pass reuses the half-step's HHt, L^{-1} and Q
+        p.hht.alloc((size_t)kTiles * 1024);
+        wrmf_tile_hh_kernel<<<(ntile * 1024 + 255) / 256, 256, 0, st>>>(HH, k, reg, p.hht.get());
+        ++launches;
+    }
     const int grid_cap = 256 * 2;  // 256 CUs; a second resident workgroup where registers allow
     // heavy rows: batches whose fp64 Grams fit the workspace
     const int64_t per_row = (int64_t)kTiles * 1024 * sizeof(double);
@@ -1076,7 +1279,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
         const int gs = (int)std::min<int64_t>(h1 - h0, grid_cap);
         wrmf_tile_solve_kernel<0><<<gs, kThreads, 0, st>>>(
             p.heavy_dev.get() + h0, (int32_t)(h1 - h0), p.counter.get(), off, cols, W, H,
-            p.hht.get(), p.gram.get(), k, k, (float)alpha, nullptr, debug_mask());
+            p.hht.get(), p.gram.get(), k, k, (float)alpha, nullptr, debug_mask(), rhs);
         MML_HIP(hipGetLastError());
         launches += 2;
     }
@@ -1085,7 +1288,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
         const int gs = (int)std::min<int64_t>(p.n_light, grid_cap);
         wrmf_tile_solve_kernel<0><<<gs, kThreads, 0, st>>>(
             p.light.get(), p.n_light, p.counter.get(), off, cols, W, H, p.hht.get(), nullptr, k, k,
-            (float)alpha, nullptr, debug_mask());
+            (float)alpha, nullptr, debug_mask(), rhs);
         MML_HIP(hipGetLastError());
         ++launches;
     }
@@ -1095,6 +1298,25 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
         nw_max = std::max<int64_t>(nw_max, p.n_wood[g]);
     }
     if (nw == 0) return;
+    if (rhs) {  // d = L^{-T} (s - Q_S^T w), s = L^{-1} r, C w = Q_S s
+        p.sbuf.alloc((size_t)nw_max * k);
+        for (int g = 0; g < 4; ++g) {
+            if (!p.n_wood[g]) continue;
+            const int gw = (int)std::min<int64_t>((p.n_wood[g] + 31) / 32, 8192);
+            wrmf_rows_matmul_kernel<<<gw, 256, 0, st>>>(rhs, p.wood[g].get(), p.n_wood[g],
+                                                        p.linvt.get(), k, 1.0f, p.sbuf.get(),
+                                                        nullptr);
+            auto* L = g == 0 ? &launch_wood<1> : g == 1 ? &launch_wood<2>
+                      : g == 2 ? &launch_wood<3> : &launch_wood<4>;
+            L(st, p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, p.qbuf.get(), k,
+              (float)alpha, p.tbuf.get(), p.sbuf.get());
+            wrmf_rows_matmul_kernel<<<gw, 256, 0, st>>>(p.tbuf.get(), nullptr, p.n_wood[g],
+                                                        p.linv.get(), k, 1.0f, W, p.wood[g].get());
+            MML_HIP(hipGetLastError());
+            launches += 3;
+        }
+        return;
+    }
     // Woodbury rows: B = HH + reg I = L L^T (host fp64), Q = H L^{-T}, per-row C v = 1 and
     // t = Q_S^T v on the tiles, then W rows = ((1 + alpha) / alpha) t L^{-1}
     std::vector<double> hh((size_t)k * k), li;
@@ -1127,12 +1349,13 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             const int gs = (int)std::min<int64_t>(p.n_wood[g], grid_cap);
             wrmf_tile_solve_kernel<1><<<gs, kThreads, 0, st>>>(
                 p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, W, p.qbuf.get(),
-                nullptr, nullptr, k, 32 * (g + 1), (float)alpha, p.tbuf.get(), debug_mask());
+                nullptr, nullptr, k, 32 * (g + 1), (float)alpha, p.tbuf.get(), debug_mask(),
+                nullptr);
         } else {
             auto* L = g == 0 ? &launch_wood<1> : g == 1 ? &launch_wood<2>
                       : g == 2 ? &launch_wood<3> : &launch_wood<4>;
             L(st, p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, p.qbuf.get(), k,
-              (float)alpha, p.tbuf.get());
+              (float)alpha, p.tbuf.get(), nullptr);
         }
         const int gw = (int)std::min<int64_t>((p.n_wood[g] + 31) / 32, 8192);
         wrmf_rows_matmul_kernel<<<gw, 256, 0, st>>>(p.tbuf.get(), nullptr, p.n_wood[g],

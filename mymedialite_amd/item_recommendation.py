@@ -411,16 +411,27 @@ class SoftMarginRankingMF(BPRMF):
 class WRMF(_MFBase):
     PROPERTIES = {
         "Alpha": "double", "Device": "int", "Gpus": "string", "InitMean": "double", "InitStdDev": "double",
-        "NumFactors": "uint", "NumIter": "uint", "Regularization": "double",
+        "NumFactors": "uint", "NumIter": "uint", "Precision": "string", "Regularization": "double",
     }
+    # Precision (GPU only, 128 < NumFactors): "fp64" = the fp32 MFMA solve + one pass of fp64
+    # iterative refinement (the fp64 solution, WRMF.cs:137-154; further passes change nothing
+    # measurable: scripts/diag_wrmf_refine.py); "fp32" = the solve alone
+    REFINE_PASSES = {"fp64": 1, "fp32": 0}
 
     def __init__(self, **kw):
         super().__init__()
         self.Alpha = 1.0             # WRMF.cs:56
         self.Regularization = 0.015  # WRMF.cs:59
         self.NumIter = 15            # WRMF() :62-65
+        self.Precision = "fp64"
         for k, v in kw.items():
             setattr(self, k, v)
+
+    def _wrmf_params(self):
+        if self.Precision not in self.REFINE_PASSES:
+            raise ValueError(f"unknown Precision '{self.Precision}' (fp64 | fp32)")
+        return N.WrmfParams(int(self.NumFactors), self.REFINE_PASSES[self.Precision],
+                            float(self.Alpha), float(self.Regularization))
 
     def _auc_symbol(self):
         return "mml_wrmf_auc"
@@ -430,7 +441,7 @@ class WRMF(_MFBase):
     def _load_device_model(self, U, V, bias):
         self._release()
         self._ctx = N.Context(N.device_arg(self))
-        p = N.WrmfParams(int(self.NumFactors), 0, float(self.Alpha), float(self.Regularization))
+        p = self._wrmf_params()
         h = N._vp()
         N.check(N.lib().mml_wrmf_create(self._ctx.handle, ctypes.byref(p), U.shape[0], V.shape[0],
                                         ctypes.byref(h)))
@@ -443,7 +454,7 @@ class WRMF(_MFBase):
         U, V = self._init_factors()
         self._release()
         self._ctx = N.Context(N.device_arg(self))
-        p = N.WrmfParams(int(self.NumFactors), 0, float(self.Alpha), float(self.Regularization))
+        p = self._wrmf_params()
         h = N._vp()
         N.check(N.lib().mml_wrmf_create(self._ctx.handle, ctypes.byref(p), self.MaxUserID + 1,
                                         self.MaxItemID + 1, ctypes.byref(h)))
