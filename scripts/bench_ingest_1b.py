@@ -16,7 +16,8 @@ from mymedialite_amd import read_ratings  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000_000
 threads = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 d = sys.argv[3] if len(sys.argv) > 3 else "/dev/shm"
-exe = os.path.join(d, "mml_gen_ratings")
+os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+exe = os.path.join(ROOT, "build", "mml_gen_ratings")  # /dev/shm may be noexec
 path = os.path.join(d, "mml_c4_ratings.txt")
 try:
     subprocess.run(["gcc", "-O2", "-o", exe, os.path.join(ROOT, "scripts", "gen_ratings.c")],
