@@ -5,9 +5,12 @@ as the reference (src/MyMediaLite/RatingPrediction/BiasedMatrixFactorization.cs:
 MatrixFactorization.cs:50-418); the per-rating SGD loop runs in libmml_hip.so on the MI355X.
 
 Schedule (GPU-only property):
-  * ``auto``    -> MaxThreads <= 1: ``ordered`` (the reference's sequential loop, exact);
-                   MaxThreads > 1: ``dsgd`` (the reference's DSGD blocks, exact) or, with
-                   NaiveParallelization, ``hogwild`` (the reference's racy mode);
+  * ``auto``    -> below AUTO_EXACT_MAX ratings the reference's own schedule, exactly:
+                   MaxThreads <= 1: ``ordered`` (the sequential loop, one wavefront);
+                   MaxThreads > 1: ``dsgd`` (the DSGD blocks) or, with NaiveParallelization,
+                   ``hogwild`` (the reference's racy mode).  From AUTO_EXACT_MAX ratings on:
+                   ``hogwild`` (statistical parity; the exact schedules are bounded by the
+                   hottest item's sequential updates, ~2e7 ratings/s, DESIGN.md section 3);
   * ``ordered`` / ``dsgd`` / ``hogwild`` / ``hogwild_coherent`` to force one (the last keeps every
     row access agent-coherent: closer to the sequential trajectory, slower on hot items).
 """
@@ -24,8 +27,14 @@ from .random import Random
 from .recommender import Recommender
 
 _LOSS = {"RMSE": N.LOSS_RMSE, "MAE": N.LOSS_MAE, "LogisticLoss": N.LOSS_LOGISTIC}
+# ``auto`` switches from the exact schedules to Hogwild at this many training ratings
+AUTO_EXACT_MAX = 4_000_000
 _SCHED = {"ordered": N.SCHEDULE_ORDERED, "dsgd": N.SCHEDULE_DSGD, "hogwild": N.SCHEDULE_HOGWILD,
           "hogwild_coherent": N.SCHEDULE_HOGWILD_COHERENT}
+
+
+def _large(ratings) -> bool:
+    return ratings is not None and ratings.count >= AUTO_EXACT_MAX
 
 
 class MatrixFactorization(Recommender):
@@ -82,7 +91,7 @@ class MatrixFactorization(Recommender):
 
     def schedule(self) -> str:
         if self.Schedule == "auto":
-            return "ordered"
+            return "hogwild" if _large(self._ratings) else "ordered"
         if self.Schedule not in ("ordered", "hogwild", "hogwild_coherent"):
             raise ValueError(f"unknown Schedule '{self.Schedule}' for {type(self).__name__}")
         return self.Schedule
@@ -367,7 +376,7 @@ class BiasedMatrixFactorization(MatrixFactorization):
             if self.Schedule not in _SCHED:
                 raise ValueError(f"unknown Schedule '{self.Schedule}'")
             return self.Schedule
-        if self.NaiveParallelization and self.MaxThreads > 1:
+        if (self.NaiveParallelization and self.MaxThreads > 1) or _large(self._ratings):
             return "hogwild"
         return "dsgd" if self.MaxThreads > 1 else "ordered"
 
@@ -669,8 +678,9 @@ class _AsymmetricFactorModel(BiasedMatrixFactorization):
     """The Sigmoid*AsymmetricFactorModels (ITransductiveRatingPredictor): a BiasedMatrixFactorization
     in which users and / or items are represented by implicit factors summed over their feedback
     lists (training and ``additional_feedback``) / sqrt(count).  Side 0 = y over the items each
-    user rated, side 1 = x over the users who rated each item.  ``ordered`` (default) is the
-    reference's sequential loop bit for bit; ``hogwild`` runs many wavefronts.  BoldDriver (their
+    user rated, side 1 = x over the users who rated each item.  ``ordered`` (``auto`` below
+    AUTO_EXACT_MAX ratings) is the reference's sequential loop bit for bit; ``hogwild`` (``auto``
+    from there on) runs many wavefronts.  BoldDriver (their
     own ComputeObjective), MaxThreads > 1 and FoldIn are not on the GPU path."""
     PROPERTIES = dict(BiasedMatrixFactorization.PROPERTIES)
     SIDES = ()          # the implicit sides the model uses
@@ -688,7 +698,10 @@ class _AsymmetricFactorModel(BiasedMatrixFactorization):
             setattr(self, k, v)
 
     def schedule(self) -> str:
-        s = "ordered" if self.Schedule == "auto" else self.Schedule
+        if self.Schedule == "auto":
+            s = "hogwild" if _large(self._ratings) else "ordered"
+        else:
+            s = self.Schedule
         if s not in ("ordered", "hogwild"):
             raise ValueError(f"unknown Schedule '{self.Schedule}' for {type(self).__name__}")
         return s

@@ -55,3 +55,30 @@ def test_gpus_option_selects_a_multi_device_context():
     assert N.device_arg(m) == [0, 1, 2, 3]
     b = M.BPRMF(Device=2)
     assert N.device_arg(b) == 2
+
+
+def test_auto_schedule_switches_to_hogwild_at_scale():
+    """Schedule="auto": the reference's exact schedule below AUTO_EXACT_MAX training ratings
+    (ordered, or DSGD for MaxThreads > 1), Hogwild from there on (the exact schedules run at
+    ~2e7 ratings/s whatever the GPU)."""
+    from mymedialite_amd import rating_prediction as RP
+    small = M.Ratings(np.zeros(10, np.int32), np.arange(10, dtype=np.int32),
+                      np.ones(10, np.float32))
+    n = RP.AUTO_EXACT_MAX
+    big = M.Ratings(np.arange(n, dtype=np.int32) % 1000, np.arange(n, dtype=np.int32) % 997,
+                    np.ones(n, np.float32))
+    for cls in (M.BiasedMatrixFactorization, M.MatrixFactorization,
+                M.SigmoidItemAsymmetricFactorModel):
+        m = cls()
+        assert m.schedule() == "ordered"
+        m.ratings = small
+        assert m.schedule() == "ordered"
+        m.ratings = big
+        assert m.schedule() == "hogwild", cls
+        m.Schedule = "ordered"
+        assert m.schedule() == "ordered"
+    m = M.BiasedMatrixFactorization(MaxThreads=8)
+    m.ratings = small
+    assert m.schedule() == "dsgd"
+    m.ratings = big
+    assert m.schedule() == "hogwild"
