@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "mml_internal.h"
@@ -919,6 +920,211 @@ void launch_wood(hipStream_t st, const int32_t* rows, int32_t n, int32_t* counte
                                                       Tout, S);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Woodbury rows by conjugate gradients.  C = I/alpha + Q_S Q_S^T has its spectrum in
+// [1/alpha, 1/alpha + 1]: Q_S Q_S^T = H_S B^{-1} H_S^T and H_S^T H_S <= HH <= B = HH + reg I, so
+// cond(C) <= 1 + alpha and CG gains a factor (sqrt(1+alpha) - 1) / (sqrt(1+alpha) + 1) per step
+// (0.17 at alpha = 1) whatever the row.  One 4-wave workgroup per row: thread f keeps column f of
+// Q_S (deg <= NJ values) in registers for the whole solve, so each step is two register
+// mat-vecs -- u = Q_S^T p (p broadcast from LDS) and z = Q_S u, whose sum over the 256 features
+// is a transposing butterfly (each xor stage halves the values a lane carries, ~NJ shuffles per
+// step instead of 6 NJ) plus a 4-wave LDS sum.  Output as wrmf_wood_kernel: t = Q_S^T v for
+// C v = 1, or t = s - Q_S^T w for C w = Q_S s when S (a refinement pass) is given.
+template <int N, int SIZE, int M>
+struct XorReduce {  // v[0 .. SIZE) per lane -> sums over the 64 lanes, SIZE / 64 values per lane
+    __device__ static __forceinline__ void run(float (&v)[N], int lane) {
+        if constexpr (M > 0) {
+            if constexpr (SIZE > 1) {
+                constexpr int H = SIZE / 2;
+                const bool lo = (lane & M) == 0;
+#pragma unroll
+                for (int x = 0; x < H; ++x) {
+                    const float keep = lo ? v[x] : v[x + H];
+                    const float send = lo ? v[x + H] : v[x];
+                    v[x] = keep + __shfl_xor(send, M, 64);
+                }
+                XorReduce<N, H, M / 2>::run(v, lane);
+            } else {
+                v[0] += __shfl_xor(v[0], M, 64);
+                XorReduce<N, 1, M / 2>::run(v, lane);
+            }
+        }
+    }
+};
+
+// (x, y) summed over the workgroup, in one pass (sdot: 2 x WAVES floats)
+template <int WAVES>
+__device__ __forceinline__ float2 block_sum2(float x, float y, float* sdot) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        x += __shfl_xor(x, o, 64);
+        y += __shfl_xor(y, o, 64);
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        sdot[threadIdx.x >> 6] = x;
+        sdot[WAVES + (threadIdx.x >> 6)] = y;
+    }
+    __syncthreads();
+    float2 r = make_float2(0.0f, 0.0f);
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) {
+        r.x += sdot[w];
+        r.y += sdot[WAVES + w];
+    }
+    return r;
+}
+
+// NJ = 32 / 64: 4 waves, thread f holds q[0 .. NJ) of feature f.  NJ = 128: 8 waves, the items
+// split in two halves of 64 (waves 0-3 / 4-7), so a thread holds 64 values (128 would spill);
+// bounds of 4 waves per SIMD keep two such workgroups per CU (128 VGPRs), since the solve is
+// barrier-latency bound.  The CG is Chronopoulos-Gear's single-reduction form: one mat-vec
+// w = C r and one fused reduction of (r.r, w.r) per step.
+template <int NJ>
+__global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_wood_cg_kernel(
+    const int32_t* __restrict__ rows, int32_t n_list, const int64_t* __restrict__ off,
+    const int32_t* __restrict__ cols, const float* __restrict__ Q, int32_t k, float alpha,
+    const float* __restrict__ S, float* __restrict__ Tout, int32_t max_it, float tol2) {
+    static_assert(NJ == 32 || NJ == 64 || NJ == 128, "NJ: 32, 64 or 128");
+    constexpr int HALVES = NJ > 64 ? 2 : 1;
+    constexpr int WAVES = 4 * HALVES;
+    constexpr int NL = NJ / HALVES;             // items per thread (<= 64)
+    constexpr int E = NL / 8;                   // partial sums after the fused first stages
+    constexpr int NV = NL >= 64 ? NL / 64 : 1;  // butterfly outputs per lane
+    constexpr int LPJ = NL >= 64 ? 1 : 64 / NL; // lanes holding one output (NL < 64)
+    __shared__ int32_t sid[NJ];
+    __shared__ float sp[NJ];
+    __shared__ float su[HALVES][256];
+    __shared__ float red[WAVES][NL];
+    __shared__ float sdot[2 * WAVES];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int f = t & 255, half = t >> 8, hw = wave & 3;  // feature, item half, wave in half
+    const float ainv = 1.0f / alpha;
+    const bool fon = f < k;
+    for (int li = blockIdx.x; li < n_list; li += gridDim.x) {
+        const int32_t row = rows[li];
+        const int64_t rb = off[row];
+        const int deg = (int)(off[row + 1] - rb);
+        __syncthreads();  // the previous row is done with the LDS
+        if (t < NJ) sid[t] = t < deg ? cols[rb + t] : 0;
+        __syncthreads();
+        float q[NL];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int jj = half * NL + j;
+            q[j] = (fon && jj < deg) ? Q[(int64_t)sid[jj] * k + f] : 0.0f;
+        }
+        // z_j (thread j < NJ) = sum_f Q_S[j][f] uf; the first three butterfly stages (xor 32,
+        // 16, 8) are fused per group of 8 products, so only NL / 8 partial sums sit next to q
+        auto qs_times = [&](float uf) -> float {
+            float v[E];
+            const bool l1 = (lane & 32) == 0, l2 = (lane & 16) == 0, l3 = (lane & 8) == 0;
+#pragma unroll
+            for (int x = 0; x < E; ++x) {
+                float s1[4], s2[2];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float a = q[x + c * E] * uf, b = q[x + (c + 4) * E] * uf;
+                    s1[c] = (l1 ? a : b) + __shfl_xor(l1 ? b : a, 32, 64);
+                }
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+                    s2[c] = (l2 ? s1[c] : s1[c + 2]) + __shfl_xor(l2 ? s1[c + 2] : s1[c], 16, 64);
+                v[x] = (l3 ? s2[0] : s2[1]) + __shfl_xor(l3 ? s2[1] : s2[0], 8, 64);
+            }
+            XorReduce<E, E, 4>::run(v, lane);
+            if constexpr (NL >= 64) {
+#pragma unroll
+                for (int x = 0; x < NV; ++x) red[wave][NV * lane + x] = v[x];
+            } else {
+                if (lane % LPJ == 0) red[wave][lane / LPJ] = v[0];
+            }
+            __syncthreads();
+            float z = 0.0f;
+            if (t < NJ) {
+                const int h = t / NL, jl = t % NL;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) z += red[4 * h + w][jl];
+            }
+            return z;
+        };
+        auto qt_times = [&]() -> float {  // u_f = sum_j Q_S[j][f] sp[j] (all threads: feature f)
+            float u = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NL; ++j) u += q[j] * sp[half * NL + j];
+            if constexpr (HALVES == 1) return u;
+            su[half][f] = u;
+            __syncthreads();
+            return su[0][f] + su[1][f];
+        };
+        float sf = 0.0f, y;
+        if (S) {
+            sf = fon ? S[(int64_t)li * k + f] : 0.0f;
+            y = qs_times(sf);
+        } else {
+            y = t < deg ? 1.0f : 0.0f;
+        }
+        float w = 0.0f, r = t < deg ? y : 0.0f, p = 0.0f, sv = 0.0f;
+        float g_prev = 1.0f, a_prev = 1.0f, stop = 0.0f;
+        for (int it = 0; it <= max_it; ++it) {
+            if (t < NJ) sp[t] = r;
+            __syncthreads();
+            const float uf = qt_times();
+            const float cr = (t < deg ? r * ainv : 0.0f) + qs_times(uf);  // C r
+            const float2 gd = block_sum2<WAVES>(t < NJ ? r * r : 0.0f, t < NJ ? cr * r : 0.0f,
+                                                sdot);
+            if (it == 0) stop = tol2 * gd.x;
+            if (gd.x <= stop || it == max_it) break;
+            const float b = it == 0 ? 0.0f : gd.x / g_prev;
+            const float a = it == 0 ? gd.x / gd.y : gd.x / (gd.y - b * gd.x / a_prev);
+            p = r + b * p;
+            sv = cr + b * sv;  // C p
+            w += a * p;
+            r -= a * sv;
+            g_prev = gd.x;
+            a_prev = a;
+        }
+        __syncthreads();
+        if (t < NJ) sp[t] = t < deg ? w : 0.0f;
+        __syncthreads();
+        const float tf = qt_times();
+        if (fon && half == 0) Tout[(int64_t)li * k + f] = S ? sf - tf : tf;
+        (void)hw;
+    }
+}
+
+// MML_WRMF_WOOD=chol keeps the Cholesky Woodbury kernel (A/B measurements); the default solves
+// the Woodbury rows by CG
+bool wood_cg() {
+    static const bool v = [] {
+        const char* e = std::getenv("MML_WRMF_WOOD");
+        return !(e && std::string(e) == "chol");
+    }();
+    return v;
+}
+
+void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const int64_t* off,
+                    const int32_t* cols, const float* Q, int32_t k, float alpha, float* Tout,
+                    const float* S) {
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, 256 * 4));
+    // main solve: relative residual 1e-6 (fp32 CG stagnates not far below: a tighter target
+    // just runs to max_it on trained factors); a refinement correction needs 1e-4.  max_it =
+    // the steps the cond(C) <= 1 + alpha bound needs, + 4
+    const double tol = S ? 1e-4 : 1e-6;
+    const double rho = (std::sqrt(1.0 + alpha) - 1.0) / (std::sqrt(1.0 + alpha) + 1.0);
+    const int max_it = std::min(200, (int)std::ceil(std::log(tol) / std::log(rho)) + 4);
+    const float tol2 = (float)(tol * tol);
+    if (g == 0)
+        wrmf_wood_cg_kernel<32><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
+                                                      max_it, tol2);
+    else if (g == 1)
+        wrmf_wood_cg_kernel<64><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
+                                                      max_it, tol2);
+    else
+        wrmf_wood_cg_kernel<128><<<grid, 512, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
+                                                       max_it, tol2);
+}
+
 // Y[yrow(r)] = scale * X[xrow(r)] * M for n rows (X, Y row-major [.. x k], M [k x k] row-major,
 // k <= 256; xrows / yrows null = identity).  32 rows per workgroup staged in LDS, 4 waves x 2
 // output tiles of 32 x 32 on v_mfma_f32_32x32x2_f32; M streams from L2.
@@ -1306,10 +1512,15 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             wrmf_rows_matmul_kernel<<<gw, 256, 0, st>>>(rhs, p.wood[g].get(), p.n_wood[g],
                                                         p.linvt.get(), k, 1.0f, p.sbuf.get(),
                                                         nullptr);
-            auto* L = g == 0 ? &launch_wood<1> : g == 1 ? &launch_wood<2>
-                      : g == 2 ? &launch_wood<3> : &launch_wood<4>;
-            L(st, p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, p.qbuf.get(), k,
-              (float)alpha, p.tbuf.get(), p.sbuf.get());
+            if (wood_cg()) {
+                launch_wood_cg(st, g, p.wood[g].get(), p.n_wood[g], off, cols, p.qbuf.get(), k,
+                               (float)alpha, p.tbuf.get(), p.sbuf.get());
+            } else {
+                auto* L = g == 0 ? &launch_wood<1> : g == 1 ? &launch_wood<2>
+                          : g == 2 ? &launch_wood<3> : &launch_wood<4>;
+                L(st, p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, p.qbuf.get(), k,
+                  (float)alpha, p.tbuf.get(), p.sbuf.get());
+            }
             wrmf_rows_matmul_kernel<<<gw, 256, 0, st>>>(p.tbuf.get(), nullptr, p.n_wood[g],
                                                         p.linv.get(), k, 1.0f, W, p.wood[g].get());
             MML_HIP(hipGetLastError());
@@ -1351,6 +1562,9 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                 p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, W, p.qbuf.get(),
                 nullptr, nullptr, k, 32 * (g + 1), (float)alpha, p.tbuf.get(), debug_mask(),
                 nullptr);
+        } else if (wood_cg()) {
+            launch_wood_cg(st, g, p.wood[g].get(), p.n_wood[g], off, cols, p.qbuf.get(), k,
+                           (float)alpha, p.tbuf.get(), nullptr);
         } else {
             auto* L = g == 0 ? &launch_wood<1> : g == 1 ? &launch_wood<2>
                       : g == 2 ? &launch_wood<3> : &launch_wood<4>;
