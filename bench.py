@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -709,13 +710,13 @@ def bench_wrmf(args):
                      "kernel": "wrmf_wood_kernel + wrmf_tile_solve_kernel + wrmf_tile_gram_kernel "
                                "+ wrmf_gram_* (whole iteration)",
                      "kernel_avg_ms": float(np.mean(ms)), "flops_per_iteration": flops_exec,
-                     "flops_note": "executed algorithmic flops: Woodbury rows (deg <= 128) "
-                                   "deg(deg+1)k + deg^3/3 + 2 deg k + 2k^2, direct rows "
-                                   "k(k+1)deg + k^3/3 + 2k^2 + 2 deg k, per half HH k(k+1)n and "
-                                   "Q = H L^-T n k^2, on the distinct (user, item) sets; each "
-                                   "refinement pass repeats the row solves (+ 2k^2 per Woodbury "
-                                   "row for s = L^-1 r) and adds the fp64 residual 2 n k^2 + "
-                                   "4 nnz k",
+                     "flops_note": "executed algorithmic flops (bench.wrmf_executed_flops): "
+                                   "Woodbury rows (deg <= 128) by CG, 4 deg k per C mat-vec at "
+                                   "the cond(C) <= 1 + alpha step bound (an upper bound), + 2k^2; "
+                                   "direct rows k(k+1)deg + k^3/3 + 2k^2 + 2 deg k; per half HH "
+                                   "k(k+1)n and Q = H L^-T 2nk^2; per refinement pass the fp64 "
+                                   "residual 2nk^2 + 4 nnz k, 2k^2 per direct row (kept factor), "
+                                   "a 1e-4 CG per Woodbury row; the CG rows run on the VALU",
                      "refine_passes": passes,
                      "flops_direct_equivalent": flops_direct,
                      "frac_direct_equivalent": flops_direct / (np.mean(ms) * 1e-3) / 1e12 / 157.3},
@@ -730,23 +731,31 @@ def bench_wrmf(args):
     ctx.close()
 
 
-def wrmf_executed_flops(deg_u, deg_i, k, passes=0, nnz=0):
-    """Flops one WRMF.Iterate() of the library executes (algorithmic, no padding): the user half
-    solves rows with deg <= 128 by Woodbury (k > 128, wrmf_tiles.hip), the rest directly; the
-    item half likewise.  Each fp64 refinement pass repeats the row solves (plus s = L^-1 r on the
-    Woodbury rows) and adds the residual (X HH: 2 n k^2; the entries: 4 nnz k).  deg_*: float64
-    torch tensors of distinct-set sizes."""
+def wrmf_executed_flops(deg_u, deg_i, k, passes=0, nnz=0, alpha=1.0):
+    """Flops one WRMF.Iterate() of the library executes (algorithmic, no padding), k > 128
+    (wrmf_tiles.hip): rows with deg <= 128 take the Woodbury solve by CG (each matrix-vector
+    product with C = I/alpha + Q_S Q_S^T is 4 deg k; the step count is its bound for
+    cond(C) <= 1 + alpha, an upper bound of what runs), longer rows the direct Gram + Cholesky;
+    per half HH = H^T H and Q = H L^-T.  Each fp64 refinement pass adds the residual (X HH:
+    2 n k^2; the entries: 4 nnz k), two triangular solves per direct row (its kept factor) and a
+    looser CG per Woodbury row.  deg_*: float64 torch tensors of distinct-set sizes."""
+    rho = (math.sqrt(1.0 + alpha) - 1.0) / (math.sqrt(1.0 + alpha) + 1.0)
+    steps = lambda tol: math.ceil(math.log(tol) / math.log(rho)) + 4 + 1  # mat-vecs
+
     def half(deg, n_other):
         wood = (deg <= 128) & (deg > 0) if k > 128 else torch.zeros_like(deg, dtype=torch.bool)
         direct = (deg > 0) & ~wood
         dw, dd = deg[wood], deg[direct]
-        solve = float((dw * (dw + 1) * k + dw ** 3 / 3 + 2 * dw * k).sum()) + 2.0 * k * k * len(dw)
-        solve += float((k * (k + 1) * dd + 2 * dd * k).sum()) + (k ** 3 / 3 + 2 * k * k) * len(dd)
-        f = solve + k * (k + 1) * n_other  # HH = H^T H
+        f = float((steps(1e-6) * 4 * dw * k + 2 * dw * k).sum()) + 2.0 * k * k * len(dw)
+        f += float((k * (k + 1) * dd + 2 * dd * k).sum()) + (k ** 3 / 3 + 2 * k * k) * len(dd)
+        f += k * (k + 1) * n_other  # HH = H^T H
         if len(dw):
-            f += n_other * k * k  # Q = H L^-T
+            f += 2.0 * n_other * k * k  # Q = H L^-T
         if passes and k > 128:
-            f += passes * (solve + 2.0 * k * k * len(dw) + 2.0 * len(deg) * k * k + 4.0 * nnz * k)
+            per = 2.0 * len(deg) * k * k + 4.0 * float(deg.sum()) * k  # residual
+            per += 2.0 * k * k * len(dd)  # L y = r, L^T d = y on the kept factors
+            per += float((steps(1e-4) * 4 * dw * k + 4 * dw * k).sum()) + 4.0 * k * k * len(dw)
+            f += passes * per
         return f
     return half(deg_u, len(deg_i)) + half(deg_i, len(deg_u))
 

@@ -138,6 +138,10 @@ struct WrmfTilePlan {
     DeviceArray<double> rpartial, x64, r64;
     DeviceArray<float> rf, df;
     void* blas = nullptr;
+    // fp64 mode: the direct rows keep their factor tiles (L_IJ, T_J = L_JJ^{-1}; light rows, then
+    // heavy ones) so a refinement pass is two triangular solves (wrmf_tile_resolve_kernel)
+    bool keep_factor = false;
+    DeviceArray<float> factor;
     WrmfTilePlan() = default;
     WrmfTilePlan(const WrmfTilePlan&) = delete;
     WrmfTilePlan& operator=(const WrmfTilePlan&) = delete;

@@ -616,6 +616,7 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
         run_blocked<float, 256>(h, W, r0, r1, H, off, cols, n_data_rows);
     } else {
         mml::WrmfTilePlan& plan = W == h->U.get() ? h->uplan : h->iplan;
+        plan.keep_factor = h->p.refine_passes > 0;
         mml::wrmf_tile_solve(st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha,
                              h->p.regularization, launches);
         mml::wrmf_tile_refine(st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha,

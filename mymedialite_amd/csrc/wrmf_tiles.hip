@@ -388,6 +388,52 @@ __device__ __forceinline__ void factor_tile(Smem& sm, f32x16 (&acc)[kSlots], int
         }
 }
 
+// L^T w = y by 32-column blocks, w_J = T_J^T (y_J - sum_{I>J} L_IJ^T w_I): the factor in the
+// owners' accumulators (L_IJ below the diagonal, T_J = L_JJ^{-1} on it), y in sm.yv, w to sm.wv.
+__device__ __forceinline__ void back_substitute(Smem& sm, f32x16 (&acc)[kSlots], Tiles& tl,
+                                                int nt) {
+    const int t = opaque_tid(), lane = t & 63, q = lane & 31, h = lane >> 5;
+    for (int J = nt - 1; J >= 0; --J) {
+        launder(tl);
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) {
+            if (tl.J[s] != J) continue;
+            if (tl.I[s] == J) {
+#pragma unroll
+                for (int g = 0; g < 16; ++g) sm.tT[0][2 * g + h][q] = acc[s][g];
+            } else if (tl.I[s] < nt) {
+                const float wr = sm.wv[32 * tl.I[s] + q];
+                const int pi = tl.I[s] - J - 1;
+#pragma unroll
+                for (int g = 0; g < 16; ++g) sm.u.red[pi][rho(g, h)][q] = acc[s][g] * wr;
+            }
+        }
+        __syncthreads();
+        const int nparts = nt - 1 - J;
+        if (t < 32 * nparts) {
+            const int pi = t >> 5, c = t & 31;
+            float sacc = 0.0f;
+#pragma unroll
+            for (int x = 0; x < 32; ++x) sacc += sm.u.red[pi][c][x];
+            sm.part[pi][c] = sacc;
+        }
+        __syncthreads();
+        if (t < 32) {
+            float sacc = sm.yv[32 * J + t];
+            for (int pi = 0; pi < nparts; ++pi) sacc -= sm.part[pi][t];
+            sm.sv[t] = sacc;
+        }
+        __syncthreads();
+        if (t < 32) {
+            float w = 0.0f;
+#pragma unroll
+            for (int c = 0; c < 32; ++c) w += (c >= t) ? sm.tT[0][t][c] * sm.sv[c] : 0.0f;
+            sm.wv[32 * J + t] = w;
+        }
+    }
+}
+
 // MODE 0: the direct row solve (W_u = A_u^{-1} b_u), kdim = k.
 // MODE 1: the Woodbury row solve for rows with deg <= kWood (WRMF.cs:110-156 restated):
 //   A_u = B + alpha H_S^T H_S with B = HH + reg I = L L^T shared by all rows, Q = H L^{-T}:
@@ -400,7 +446,7 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols, float* __restrict__ W,
     const float* __restrict__ H, const float* __restrict__ HHt, const double* __restrict__ gram,
     int32_t k, int32_t kdim, float alpha, float* __restrict__ Tout, int32_t dbg,
-    const float* __restrict__ rhs) {
+    const float* __restrict__ rhs, float* __restrict__ F) {
     __shared__ Smem sm;
     const int wave = threadIdx.x >> 6;
     const int nt = (kdim + 31) >> 5, nr = nt + 1;
@@ -551,47 +597,17 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
             }
             __syncthreads();
         }
-        // ---- 4. backward substitution L^T w = y (padding entries come out 0)
-        for (int J = nt - 1; J >= 0; --J) {
-            if (dbg & 4) break;
-            launder(tl);
-            __syncthreads();
+        // the factor, kept for the refinement passes (wrmf_tile_resolve_kernel)
+        if (MODE == 0 && F)
 #pragma unroll
             for (int s = 0; s < kSlots; ++s) {
-                if (tl.J[s] != J) continue;
-                if (tl.I[s] == J) {
+                if (tl.I[s] < 0 || tl.I[s] >= nt) continue;
+                float* dst = F + ((int64_t)li * kTiles + s * kWaves + wave) * 1024 + lane;
 #pragma unroll
-                    for (int g = 0; g < 16; ++g) sm.tT[0][2 * g + h][q] = acc[s][g];
-                } else if (tl.I[s] < nt) {
-                    const float wr = sm.wv[32 * tl.I[s] + q];
-                    const int pi = tl.I[s] - J - 1;
-#pragma unroll
-                    for (int g = 0; g < 16; ++g) sm.u.red[pi][rho(g, h)][q] = acc[s][g] * wr;
-                }
+                for (int g = 0; g < 16; ++g) dst[g * 64] = acc[s][g];
             }
-            __syncthreads();
-            const int nparts = nt - 1 - J;
-            if (t < 32 * nparts) {
-                const int pi = t >> 5, c = t & 31;
-                float sacc = 0.0f;
-#pragma unroll
-                for (int x = 0; x < 32; ++x) sacc += sm.u.red[pi][c][x];
-                sm.part[pi][c] = sacc;
-            }
-            __syncthreads();
-            if (t < 32) {
-                float sacc = sm.yv[32 * J + t];
-                for (int pi = 0; pi < nparts; ++pi) sacc -= sm.part[pi][t];
-                sm.sv[t] = sacc;
-            }
-            __syncthreads();
-            if (t < 32) {
-                float w = 0.0f;
-#pragma unroll
-                for (int c = 0; c < 32; ++c) w += (c >= t) ? sm.tT[0][t][c] * sm.sv[c] : 0.0f;
-                sm.wv[32 * J + t] = w;
-            }
-        }
+        // ---- 4. backward substitution L^T w = y (padding entries come out 0)
+        if (!(dbg & 4)) back_substitute(sm, acc, tl, nt);
         __syncthreads();
         if constexpr (MODE == 0) {
             for (int f = t; f < k; f += kThreads) W[(int64_t)row * k + f] = sm.wv[f];
@@ -612,6 +628,74 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
                 Tout[(int64_t)li * k + f] = a0 + a1;
             }
         }
+    }
+}
+
+// A refinement pass on a direct row whose factor wrmf_tile_solve_kernel<0> kept in F: forward
+// substitution L y = r by 32-row blocks, y_J = T_J (r_J - sum_{K<J} L_JK y_K), then the same
+// backward substitution; W row <- L^{-T} y.  No Gram, no factorisation.
+__global__ __launch_bounds__(kThreads, 2) void wrmf_tile_resolve_kernel(
+    const int32_t* __restrict__ rows, int32_t n_list, int32_t* __restrict__ counter,
+    const float* __restrict__ F, const float* __restrict__ rhs, int32_t k, float* __restrict__ W) {
+    __shared__ Smem sm;
+    const int wave = threadIdx.x >> 6;
+    const int nt = (k + 31) >> 5, nr = nt + 1;
+    const int ntile = nt * nr - nt * (nt - 1) / 2;
+    Tiles tl;
+    my_tiles(wave, nr, ntile, tl);
+    for (;;) {
+        const int t = opaque_tid(), lane = t & 63, q = lane & 31, h = lane >> 5;
+        __syncthreads();
+        if (t == 0) sm.row = atomicAdd(counter, 1);
+        __syncthreads();
+        const int li = sm.row;
+        if (li >= n_list) break;
+        launder(tl);
+        const int32_t row = rows[li];
+        f32x16 acc[kSlots];
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) {
+            const bool own = tl.I[s] >= 0 && tl.I[s] < nt;
+            const float* src = F + ((int64_t)li * kTiles + s * kWaves + wave) * 1024 + lane;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) acc[s][g] = own ? src[g * 64] : 0.0f;
+        }
+        for (int J = 0; J < nt; ++J) {
+            launder(tl);
+#pragma unroll
+            for (int s = 0; s < kSlots; ++s) {
+                if (tl.I[s] != J || tl.J[s] > J) continue;
+                if (tl.J[s] == J) {  // T_J, for the 32 threads below
+#pragma unroll
+                    for (int g = 0; g < 16; ++g) sm.tT[0][2 * g + h][q] = acc[s][g];
+                    continue;
+                }
+                // row q of L_JK y_K: this lane's 16 columns, then the other half's
+                float a = 0.0f;
+#pragma unroll
+                for (int g = 0; g < 16; ++g) a += acc[s][g] * sm.yv[32 * tl.J[s] + rho(g, h)];
+                a += __shfl_xor(a, 32, 64);
+                if (h == 0) sm.part[tl.J[s]][q] = a;
+            }
+            __syncthreads();
+            if (t < 32) {
+                const int f = 32 * J + t;
+                float sacc = f < k ? rhs[(int64_t)row * k + f] : 0.0f;
+                for (int K = 0; K < J; ++K) sacc -= sm.part[K][t];
+                sm.sv[t] = sacc;
+            }
+            __syncthreads();
+            if (t < 32) {  // y_J = T_J s, T_J lower: tT[c][m] = T_J[m][c]
+                float y = 0.0f;
+#pragma unroll
+                for (int c = 0; c < 32; ++c) y += (c <= t) ? sm.tT[0][c][t] * sm.sv[c] : 0.0f;
+                sm.yv[32 * J + t] = y;
+            }
+            __syncthreads();
+        }
+        back_substitute(sm, acc, tl, nt);
+        __syncthreads();
+        for (int f = t; f < k; f += kThreads) W[(int64_t)row * k + f] = sm.wv[f];
     }
 }
 
@@ -1468,35 +1552,61 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
         ++launches;
     }
     const int grid_cap = 256 * 2;  // 256 CUs; a second resident workgroup where registers allow
-    // heavy rows: batches whose fp64 Grams fit the workspace
-    const int64_t per_row = (int64_t)kTiles * 1024 * sizeof(double);
-    const int64_t batch_rows = std::max<int64_t>(1, kGramBatchBytes / per_row);
     const int64_t nh = (int64_t)p.heavy.size();
-    for (int64_t h0 = 0; h0 < nh; h0 += batch_rows) {
-        const int64_t h1 = std::min(nh, h0 + batch_rows);
-        const int64_t s0 = p.seg_first[h0], s1 = p.seg_first[h1];
-        p.gram.alloc((size_t)std::min(nh, batch_rows) * kTiles * 1024);
-        MML_HIP(hipMemsetAsync(p.gram.get(), 0, (size_t)(h1 - h0) * per_row, st));
-        const int gg = (int)std::min<int64_t>(s1 - s0, grid_cap);
-        wrmf_tile_gram_kernel<<<gg, kThreads, 0, st>>>(reinterpret_cast<const Seg*>(p.segs.get()) + s0,
-                                                  (int32_t)(s1 - s0), (int32_t)h0, cols, H, k,
-                                                  p.gram.get());
-        MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
-        const int gs = (int)std::min<int64_t>(h1 - h0, grid_cap);
-        wrmf_tile_solve_kernel<0><<<gs, kThreads, 0, st>>>(
-            p.heavy_dev.get() + h0, (int32_t)(h1 - h0), p.counter.get(), off, cols, W, H,
-            p.hht.get(), p.gram.get(), k, k, (float)alpha, nullptr, debug_mask(), rhs);
+    const size_t tile_floats = (size_t)kTiles * 1024;
+    if (rhs && p.keep_factor) {  // refinement: the kept factors, no Gram, no factorisation
+        if (nh > 0) {
+            MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
+            wrmf_tile_resolve_kernel<<<(int)std::min<int64_t>(nh, grid_cap), kThreads, 0, st>>>(
+                p.heavy_dev.get(), (int32_t)nh, p.counter.get(),
+                p.factor.get() + (size_t)p.n_light * tile_floats, rhs, k, W);
+            ++launches;
+        }
+        if (p.n_light > 0) {
+            MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
+            wrmf_tile_resolve_kernel<<<(int)std::min<int64_t>(p.n_light, grid_cap), kThreads, 0,
+                                       st>>>(p.light.get(), p.n_light, p.counter.get(),
+                                             p.factor.get(), rhs, k, W);
+            ++launches;
+        }
         MML_HIP(hipGetLastError());
-        launches += 2;
-    }
-    if (p.n_light > 0) {
-        MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
-        const int gs = (int)std::min<int64_t>(p.n_light, grid_cap);
-        wrmf_tile_solve_kernel<0><<<gs, kThreads, 0, st>>>(
-            p.light.get(), p.n_light, p.counter.get(), off, cols, W, H, p.hht.get(), nullptr, k, k,
-            (float)alpha, nullptr, debug_mask(), rhs);
-        MML_HIP(hipGetLastError());
-        ++launches;
+    } else {
+        // the factors of the direct rows, kept when refinement passes follow (fp64 mode)
+        float* F = nullptr;
+        if (p.keep_factor && !rhs) {
+            p.factor.alloc(std::max<size_t>(1, (size_t)(p.n_light + nh) * tile_floats));
+            F = p.factor.get();
+        }
+        // heavy rows: batches whose fp64 Grams fit the workspace
+        const int64_t per_row = (int64_t)kTiles * 1024 * sizeof(double);
+        const int64_t batch_rows = std::max<int64_t>(1, kGramBatchBytes / per_row);
+        for (int64_t h0 = 0; h0 < nh; h0 += batch_rows) {
+            const int64_t h1 = std::min(nh, h0 + batch_rows);
+            const int64_t s0 = p.seg_first[h0], s1 = p.seg_first[h1];
+            p.gram.alloc((size_t)std::min(nh, batch_rows) * kTiles * 1024);
+            MML_HIP(hipMemsetAsync(p.gram.get(), 0, (size_t)(h1 - h0) * per_row, st));
+            const int gg = (int)std::min<int64_t>(s1 - s0, grid_cap);
+            wrmf_tile_gram_kernel<<<gg, kThreads, 0, st>>>(
+                reinterpret_cast<const Seg*>(p.segs.get()) + s0, (int32_t)(s1 - s0), (int32_t)h0,
+                cols, H, k, p.gram.get());
+            MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
+            const int gs = (int)std::min<int64_t>(h1 - h0, grid_cap);
+            wrmf_tile_solve_kernel<0><<<gs, kThreads, 0, st>>>(
+                p.heavy_dev.get() + h0, (int32_t)(h1 - h0), p.counter.get(), off, cols, W, H,
+                p.hht.get(), p.gram.get(), k, k, (float)alpha, nullptr, debug_mask(), rhs,
+                F ? F + (size_t)(p.n_light + h0) * tile_floats : nullptr);
+            MML_HIP(hipGetLastError());
+            launches += 2;
+        }
+        if (p.n_light > 0) {
+            MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
+            const int gs = (int)std::min<int64_t>(p.n_light, grid_cap);
+            wrmf_tile_solve_kernel<0><<<gs, kThreads, 0, st>>>(
+                p.light.get(), p.n_light, p.counter.get(), off, cols, W, H, p.hht.get(), nullptr,
+                k, k, (float)alpha, nullptr, debug_mask(), rhs, F);
+            MML_HIP(hipGetLastError());
+            ++launches;
+        }
     }
     int64_t nw = 0, nw_max = 0;
     for (int g = 0; g < 4; ++g) {
@@ -1561,7 +1671,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             wrmf_tile_solve_kernel<1><<<gs, kThreads, 0, st>>>(
                 p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, W, p.qbuf.get(),
                 nullptr, nullptr, k, 32 * (g + 1), (float)alpha, p.tbuf.get(), debug_mask(),
-                nullptr);
+                nullptr, nullptr);
         } else if (wood_cg()) {
             launch_wood_cg(st, g, p.wood[g].get(), p.n_wood[g], off, cols, p.qbuf.get(), k,
                            (float)alpha, p.tbuf.get(), nullptr);
