@@ -481,14 +481,29 @@ __global__ __launch_bounds__(256) void bpr_update_kernel(
 // wavefront, lane f owns factors f, f + 64, ... (KM per lane); x_uij summed left to right in
 // double through v_readlane exactly as RowScalarProductWithRowDifference
 // (DataType/MatrixExtensions.cs:276-298), so the result is bit-faithful to the managed loop.
-template <bool SOFT, int KM>
+template <bool SOFT, int KM, bool XCD1 = false>
 // With W = blockDim.x / 64 > 1 waves, wave w applies the contiguous part [w n / W, (w+1) n / W) in
 // order: W streams in flight at once (the small-epoch Hogwild form, one CU, see mml_bpr_iterate).
+// XCD1: the streams of all blocks b with b % 8 == 0, i.e. of the CUs of ONE XCD (probed by
+// mml::xcd_groups), whose single L2 then holds every row: loads are L2-served (sc1, past the
+// CUs' non-coherent L1s), so no update is lost to a stale replica; the other blocks exit.
 __global__ __launch_bounds__(256) void bpr_apply_ordered_kernel(
     const int32_t* __restrict__ tu, const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
-    int64_t n, float* U, float* V, float* bias, int32_t k, int32_t ld, BprScalars s) {
+    int64_t n, float* U, float* V, float* bias, int32_t k, int32_t ld, BprScalars s,
+    uint32_t u_bytes = 0, uint32_t v_bytes = 0, uint32_t b_bytes = 0) {
     const int lane = threadIdx.x & 63;
-    const int64_t W = blockDim.x >> 6, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int64_t W = blockDim.x >> 6, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if constexpr (XCD1) {
+        if (blockIdx.x % 8 != 0) return;
+        w += (int64_t)(blockIdx.x / 8) * W;
+        W *= (int64_t)((gridDim.x + 7) / 8);
+    }
+    const auto ru = mml::buffer_rsrc(U, u_bytes), rv = mml::buffer_rsrc(V, v_bytes),
+               rb = mml::buffer_rsrc(bias, b_bytes);
+    auto ld1 = [&](__amdgpu_buffer_rsrc_t r, const float* base, const float* p) -> float {
+        if constexpr (XCD1) return mml::load1_l2(r, (uint32_t)((p - base) * 4));
+        return *p;
+    };
     const int64_t x0 = n * w / W, x1 = n * (w + 1) / W;
     for (int64_t x = x0; x < x1; ++x) {
         const int32_t u = tu[x], i = ti[x], j = tj[x];
@@ -499,9 +514,9 @@ __global__ __launch_bounds__(256) void bpr_apply_ordered_kernel(
 #pragma unroll
         for (int m = 0; m < KM; ++m) {
             const int f = lane + 64 * m;
-            w[m] = f < k ? Wu[f] : 0.0f;
-            hi[m] = f < k ? Hi[f] : 0.0f;
-            hj[m] = f < k ? Hj[f] : 0.0f;
+            w[m] = f < k ? ld1(ru, U, Wu + f) : 0.0f;
+            hi[m] = f < k ? ld1(rv, V, Hi + f) : 0.0f;
+            hj[m] = f < k ? ld1(rv, V, Hj + f) : 0.0f;
             prod[m] = w[m] * (hi[m] - hj[m]);
         }
         double dot = 0.0;
@@ -512,7 +527,7 @@ __global__ __launch_bounds__(256) void bpr_apply_ordered_kernel(
             for (int l = 0; l < lim; ++l)
                 dot += (double)__int_as_float(__builtin_amdgcn_readlane(bits, l));
         }
-        const float bi = bias[i], bj = bias[j];
+        const float bi = ld1(rb, bias, bias + i), bj = ld1(rb, bias, bias + j);
         const TripleStep<SOFT> t(s, (double)(bi - bj) + dot);
         if (t.skip) continue;
         if (lane == 0) {  // i == j: the reference re-reads item_bias[j] after writing [i]
@@ -950,13 +965,20 @@ namespace {
 
 // one wavefront applies n triples in order (bpr_apply_ordered_kernel), k <= 256
 void launch_apply_ordered(mml_bpr* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
-                          int64_t n, const BprScalars& s, hipStream_t st, int waves = 1) {
+                          int64_t n, const BprScalars& s, hipStream_t st, int waves = 1,
+                          int xcd1_blocks = 0) {
     const int km = (h->k + 63) / 64;
     const bool soft = h->p.model == MML_BPR_MODEL_SOFT_MARGIN;
-#define MML_APPLY(SOFT, KM)                                                                      \
-    bpr_apply_ordered_kernel<SOFT, KM><<<1, 64 * waves, 0, st>>>(tu, ti, tj, n, h->U.get(),     \
-                                                                 h->V.get(), h->bias.get(), h->k, \
-                                                                 h->ld, s)
+    const uint32_t ub = (uint32_t)((uint64_t)h->n_users * h->ld * 4);
+    const uint32_t vb = (uint32_t)((uint64_t)h->n_items * h->ld * 4);
+    const uint32_t bb = (uint32_t)((uint64_t)h->n_items * 4);
+#define MML_APPLY(SOFT, KM)                                                                     \
+    if (xcd1_blocks > 0)                                                                        \
+        bpr_apply_ordered_kernel<SOFT, KM, true><<<8 * xcd1_blocks, 64 * waves, 0, st>>>(      \
+            tu, ti, tj, n, h->U.get(), h->V.get(), h->bias.get(), h->k, h->ld, s, ub, vb, bb); \
+    else                                                                                        \
+        bpr_apply_ordered_kernel<SOFT, KM><<<1, 64 * waves, 0, st>>>(                           \
+            tu, ti, tj, n, h->U.get(), h->V.get(), h->bias.get(), h->k, h->ld, s)
 #define MML_APPLY_K(SOFT)                   \
     switch (km) {                           \
         case 1: MML_APPLY(SOFT, 1); break;  \
@@ -972,6 +994,20 @@ void launch_apply_ordered(mml_bpr* h, const int32_t* tu, const int32_t* ti, cons
 #undef MML_APPLY_K
 #undef MML_APPLY
     MML_HIP(hipGetLastError());
+}
+
+// WeightedBPRMF Hogwild: streams on one XCD (MML_BPR_WSTREAMS overrides; 0 = the Hogwild update
+// kernel over the whole chip); needs the probed block -> XCD mapping and rows < 4 GiB (the
+// buffer resources of the L2-served loads)
+int weighted_streams(mml_bpr* h) {
+    static const int env = [] {
+        const char* e = std::getenv("MML_BPR_WSTREAMS");
+        return e ? std::max(0, std::min(128, std::atoi(e))) / 4 * 4 : -1;
+    }();
+    const int v = env >= 0 ? env : 128;
+    const bool fits = (uint64_t)h->n_users * h->ld * 4 < (1ull << 32) &&
+                      (uint64_t)h->n_items * h->ld * 4 < (1ull << 32);
+    return v > 0 && fits && mml::xcd_groups(h->ctx) == 8 ? v : 0;
 }
 
 BprScalars scalars_of(const mml_bpr* h) {
@@ -1246,6 +1282,11 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             // popularity-drawn j puts the hottest items into most concurrent triples: 1 wave of 16
             // triples per step -0.032 AUC vs the sequential oracle, 4 waves -0.038
             launch_apply_ordered(h, tu, ti, tj, n, s, st, (int)waves);
+        } else if (!ordered && !fused && n > 0 && weighted && weighted_streams(h) > 0) {
+            // WeightedBPRMF: popularity-drawn j puts the hottest rows into most triples in flight,
+            // so it runs in-order streams on the CUs of one XCD (one L2, L2-served loads): fewer
+            // triples in flight and no stale per-XCD replicas
+            launch_apply_ordered(h, tu, ti, tj, n, s, st, 4, weighted_streams(h) / 4);
         } else if (!ordered && !fused && n > 0) {
             launch_update(h, soft, am, ng, goff, tu, ti, tj, blocks, 4, s, st);
         } else if (fused) {
