@@ -83,8 +83,14 @@ __host__ __device__ __forceinline__ int tile_id(int I, int J, int nr) {
 
 struct Smem {
     union {
-        float hs[2][kCH * kHSW];        // Gram: staged item vectors, double-buffered
-        float pn[kNT][32][kPS];         // Cholesky: L_IJ of the current panel, row-major
+        float hs[2][kCH * kHSW];        // Gram (MODE 1): staged vectors, double-buffered
+        // Gram (MODE 0): the staged vectors as three bf16 planes (x = x0 + x1 + x2), each row f
+        // holding the kCH vectors' element f (two 16-B halves, swapped on rows with f & 8)
+        alignas(16) uint16_t pl[2][3][kHSW][kCH];
+        struct {
+            float pn[kNT][32][kPS];     // Cholesky: L_IJ of the current panel, row-major
+            float park[kSlots][4][64][4];  // one wave's accumulators during a diagonal factor
+        } fz;
         float red[kNT][32][kDS];        // backward: per-tile partial products
     } u;
     float dg[32][kDG];                  // diagonal tile (rows 16-B aligned)
@@ -93,7 +99,6 @@ struct Smem {
     float wv[kHSW];
     float sv[32];
     float part[kNT][32];
-    float park[kSlots][4][64][4];       // one wave's accumulators during a diagonal factorisation
     int32_t row;
 };
 
@@ -258,6 +263,120 @@ __device__ __forceinline__ void gram_accumulate(Smem& sm, f32x16 (&acc)[kSlots],
     }
 }
 
+// MODE 0's Gram on the bf16 matrix cores at f32 accuracy.  Each staged value is split exactly
+// into three bf16 parts, x = x0 + x1 + x2 (8 significant bits each: 24 = f32), and a tile takes
+// the six products x_a y_b with a + b <= 2 -- the dropped ones are below 2^-24 relative, f32's own
+// rounding -- on v_mfma_f32_32x32x16_bf16 (16 vectors per instruction, accumulating in f32):
+// 6 x 32 cycles per 16 vectors against 8 x 64 for v_mfma_f32_32x32x2_f32.  Staging: wave w
+// converts features [32w, 32w + 32) of the chunk's 16 vectors, lane (r, c2) features 8g + r of
+// vectors 2 c2, 2 c2 + 1, and writes each plane as one conflict-free 32-bit word per lane (8 rows x
+// 8 words); the operand reads are ds_read_b128 of 8 vectors, conflict-free through the swap of
+// the two 16-B halves on rows with f & 8.
+using bf16x8 = __attribute__((ext_vector_type(8))) short;
+
+__device__ __forceinline__ uint32_t bf16_rn(float x) {  // round to nearest even, top 16 bits
+    const uint32_t b = __float_as_uint(x);
+    return (b + 0x7FFFu + ((b >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ void split3(float x, uint32_t& a, uint32_t& b, uint32_t& c) {
+    a = bf16_rn(x);
+    const float r1 = x - __uint_as_float(a << 16);
+    b = bf16_rn(r1);
+    c = bf16_rn(r1 - __uint_as_float(b << 16));  // exact: <= 8 significant bits remain
+}
+__device__ __forceinline__ int pl_pos(int f, int c) {  // element (f, c) within row f
+    return ((((c >> 3) ^ (f >> 3)) & 1) << 3) | (c & 7);
+}
+
+__device__ __forceinline__ void gram_accumulate_x3(Smem& sm, f32x16 (&acc)[kSlots], Tiles& tl,
+                                                   int nslot, const int32_t* __restrict__ cols,
+                                                   int64_t b, int64_t e,
+                                                   const float* __restrict__ H, int k, int hsw) {
+    static_assert(kCH == 16 && kThreads == 512, "bf16x3 staging: 16 vectors, 8 waves");
+    const int t = opaque_tid(), lane = t & 63, wave = t >> 6, q = lane & 31, h = lane >> 5;
+    const int r = lane >> 3, c2 = lane & 7;  // staging: row in an 8-row group, vector pair
+    const int kb = hsw - 32;
+    // two chunks' gathers in flight (the MFMAs of one bf16x3 chunk take ~1 us per SIMD, less
+    // than an HBM gather's latency): va = chunk c + 1, vb = chunk c + 2
+    float va0[4], va1[4], vb0[4], vb1[4];
+    auto fetch = [&](int64_t base, float (&v0)[4], float (&v1)[4]) {
+        const int64_t e0 = base + 2 * c2, e1 = e0 + 1;
+        const float* s0 = H + (int64_t)(e0 < e ? cols[e0] : 0) * k;
+        const float* s1 = H + (int64_t)(e1 < e ? cols[e1] : 0) * k;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {  // features >= k: 0, except row kb (1 on live vectors)
+            const int f = 32 * wave + 8 * g + r;
+            v0[g] = e0 < e ? (f < k ? s0[f] : (f == kb ? 1.0f : 0.0f)) : 0.0f;
+            v1[g] = e1 < e ? (f < k ? s1[f] : (f == kb ? 1.0f : 0.0f)) : 0.0f;
+        }
+    };
+    auto stash = [&](int buf, int64_t base, const float (&v0)[4], const float (&v1)[4]) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f = 32 * wave + 8 * g + r;
+            uint32_t a0, a1, a2, b0, b1, b2;
+            split3(v0[g], a0, a1, a2);
+            split3(v1[g], b0, b1, b2);
+            const int pos = pl_pos(f, 2 * c2);
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][0][f][pos]) = a0 | (b0 << 16);
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][1][f][pos]) = a1 | (b1 << 16);
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][2][f][pos]) = a2 | (b2 << 16);
+        }
+        // rows 256 .. hsw (k = 256): zero, except row kb: 1 for the live vectors (so that row kb
+        // of the Gram accumulates sum_i h_i)
+        for (int x = t; x < (hsw - 256 > 0 ? hsw - 256 : 0) * 8; x += kThreads) {
+            const int f = 256 + x / 8, w2 = x % 8;
+            const int64_t ea = base + 2 * w2, eb2 = ea + 1;
+            const uint32_t one_a = (f == kb && ea < e) ? 0x3F80u : 0u;
+            const uint32_t one_b = (f == kb && eb2 < e) ? 0x3F80u : 0u;
+            const int pos = pl_pos(f, 2 * w2);
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][0][f][pos]) = one_a | (one_b << 16);
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][1][f][pos]) = 0u;
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][2][f][pos]) = 0u;
+        }
+    };
+    if (e <= b) return;
+    __syncthreads();  // the LDS union may still be read by the previous row's last phase
+    fetch(b, va0, va1);
+    stash(0, b, va0, va1);
+    if (b + kCH < e) fetch(b + kCH, va0, va1);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t base = b; base < e; base += kCH) {
+        const int64_t nb = base + kCH;
+        const bool more = nb < e;
+        if (nb + kCH < e) fetch(nb + kCH, vb0, vb1);  // chunk c + 2 joins c + 1 in flight
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) {
+            if (s >= nslot || tl.I[s] < 0) continue;
+            const int fa = 32 * tl.J[s] + q, fb = 32 * tl.I[s] + q;
+            bf16x8 A[3], B[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {  // 16-B aligned: one ds_read_b128 each
+                A[p] = *static_cast<const bf16x8*>(__builtin_assume_aligned(
+                    &sm.u.pl[cur][p][fa][pl_pos(fa, 8 * h)], 16));
+                B[p] = *static_cast<const bf16x8*>(__builtin_assume_aligned(
+                    &sm.u.pl[cur][p][fb][pl_pos(fb, 8 * h)], 16));
+            }
+            // small products first
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], acc[s], 0, 0, 0);
+        }
+        if (more) stash(cur ^ 1, nb, va0, va1);
+        __syncthreads();
+        cur ^= 1;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            va0[g] = vb0[g];
+            va1[g] = vb1[g];
+        }
+    }
+}
+
 // Split Gram of the heavy rows: one workgroup per (row, segment of <= kSeg entries), fp64 atomics
 // into gram[(li * kTiles + tile) * 1024 + g * 64 + lane].
 struct Seg {
@@ -281,7 +400,7 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_gram_kernel(
         for (int s = 0; s < kSlots; ++s)
 #pragma unroll
             for (int g = 0; g < 16; ++g) acc[s][g] = 0.0f;
-        gram_accumulate<0>(sm, acc, tl, kSlots, cols, sg.b, sg.e, H, k, 32 * nr, k);
+        gram_accumulate_x3(sm, acc, tl, kSlots, cols, sg.b, sg.e, H, k, 32 * nr);
 #pragma unroll
         for (int s = 0; s < kSlots; ++s) {
             if (tl.I[s] < 0) continue;
@@ -372,7 +491,7 @@ __device__ __forceinline__ void factor_tile(Smem& sm, f32x16 (&acc)[kSlots], int
             for (int g = 0; g < 16; ++g) sm.dg[q][rho(g, h)] = acc[s][g];
 #pragma unroll
         for (int g = 0; g < 16; g += 4)
-            *reinterpret_cast<float4*>(&sm.park[s][g / 4][lane][0]) =
+            *reinterpret_cast<float4*>(&sm.u.fz.park[s][g / 4][lane][0]) =
                 make_float4(acc[s][g], acc[s][g + 1], acc[s][g + 2], acc[s][g + 3]);
     }
     diag_factor(sm.dg, tT);
@@ -383,7 +502,7 @@ __device__ __forceinline__ void factor_tile(Smem& sm, f32x16 (&acc)[kSlots], int
     for (int s = 0; s < kSlots; ++s)
 #pragma unroll
         for (int g = 0; g < 16; g += 4) {
-            const float4 v = *reinterpret_cast<const float4*>(&sm.park[s][g / 4][lane][0]);
+            const float4 v = *reinterpret_cast<const float4*>(&sm.u.fz.park[s][g / 4][lane][0]);
             acc[s][g] = v.x; acc[s][g + 1] = v.y; acc[s][g + 2] = v.z; acc[s][g + 3] = v.w;
         }
 }
@@ -448,6 +567,7 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
     int32_t k, int32_t kdim, float alpha, float* __restrict__ Tout, int32_t dbg,
     const float* __restrict__ rhs, float* __restrict__ F) {
     __shared__ Smem sm;
+    const bool gram_x3 = !(dbg & 32);  // MML_WRMF_DEBUG & 32: the f32 MFMA Gram (A/B)
     const int wave = threadIdx.x >> 6;
     const int nt = (kdim + 31) >> 5, nr = nt + 1;
     const int ntile = nt * nr - nt * (nt - 1) / 2;
@@ -488,7 +608,12 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
                 for (int g = 0; g < 16; ++g) acc[s][g] = (float)src[g * 64];
             }
         } else if (!(dbg & 8)) {
-            gram_accumulate<MODE>(sm, acc, tl, nslot, cols, rb, re, H, k, hsw, kdim);
+            if constexpr (MODE == 0) {
+                if (gram_x3) gram_accumulate_x3(sm, acc, tl, nslot, cols, rb, re, H, k, hsw);
+                else gram_accumulate<0>(sm, acc, tl, nslot, cols, rb, re, H, k, hsw, kdim);
+            } else {
+                gram_accumulate<MODE>(sm, acc, tl, nslot, cols, rb, re, H, k, hsw, kdim);
+            }
         }
         // ---- 2. A' = HHt + alpha * S above row kb (HHt = HH + reg I, identity on the padding;
         //         S is 0 on the padding), (1 + alpha) * S on the b-row tile
@@ -562,7 +687,7 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
                 acc[s] = nv;
                 const int pi = tl.I[s] - J - 1;
 #pragma unroll
-                for (int g = 0; g < 16; ++g) sm.u.pn[pi][q][rho(g, h)] = nv[g];
+                for (int g = 0; g < 16; ++g) sm.u.fz.pn[pi][q][rho(g, h)] = nv[g];
                 if (tl.I[s] == nt && q == 0)  // row kb: y_J
 #pragma unroll
                     for (int g = 0; g < 16; ++g) sm.yv[32 * J + rho(g, h)] = nv[g];
@@ -575,7 +700,7 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
 #pragma unroll
                 for (int s = 0; s < kSlots; ++s) {
                     if (s != own) continue;
-                    const float* lr = sm.u.pn[0][q];
+                    const float* lr = sm.u.fz.pn[0][q];
                     if (!(dbg & 2))
 #pragma unroll
                         for (int st = 0; st < 16; ++st)
@@ -588,8 +713,8 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
             for (int s = 0; s < kSlots; ++s) {
                 if (tl.I[s] < 0 || tl.J[s] <= J || (dbg & 2)) continue;
                 if (s * kWaves + wave == tdn) continue;
-                const float* lk = sm.u.pn[tl.J[s] - J - 1][q];
-                const float* lr = sm.u.pn[tl.I[s] - J - 1][q];
+                const float* lk = sm.u.fz.pn[tl.J[s] - J - 1][q];
+                const float* lr = sm.u.fz.pn[tl.I[s] - J - 1][q];
 #pragma unroll
                 for (int st = 0; st < 16; ++st)
                     acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(-lk[2 * st + h], lr[2 * st + h],
