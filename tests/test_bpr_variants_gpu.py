@@ -82,31 +82,40 @@ def test_random_triples_applied_exactly(model, k):
     ("BPRMF", "weighted"),
 ])
 def test_sibling_auc_parity(model, sampler, schedule):
+    """ORDERED applies the device sampler's triples in sequence: |dAUC| <= 0.01 on one seed.
+    HOGWILD on this small epoch (96k events, under 16 waves' worth) runs 4 in-order streams on
+    one CU (bpr.hip), whose interleaving varies run to run: SoftMarginRankingMF (learn rate 0.1)
+    measured -0.001 .. +0.013 over six runs of one seed, so its check is the mean over seeds
+    5 / 6 / 7 on both sides, |dAUC| <= 0.01 (WeightedBPRMF: -0.004 .. -0.006; with 16 triples per
+    wave step it was -0.032..-0.042: popularity-drawn negatives put the hottest items into most
+    concurrent triples).  test_weighted_hogwild_auc_parity_mid_scale covers the many-wave Hogwild
+    at 1.9M events."""
     tr_u, tr_i, te_u, te_i = planted_feedback(1, 4000, 600, 25)
     nu, ni = int(tr_u.max()) + 1, int(tr_i.max()) + 1
     k, iters = 16, 20
     lr = 0.1 if model == "SoftMarginRankingMF" else 0.05
-    st = O.bpr_train(tr_u, tr_i, nu, ni, seed=5, k=k, num_iter=iters, model=model,
-                     sampler=sampler, learn_rate=lr)
-    auc_ref, n_ref = auc_of(st["U"], st["V"], st["bias"], tr_u, tr_i, te_u, te_i)
     cls = WeightedBPRMF if sampler == "weighted" else CLS[model]
-    Random.set_seed(5)
-    m = cls(NumFactors=k, NumIter=iters, Schedule=schedule)
-    m.feedback = PosOnlyFeedback(tr_u, tr_i)
-    m.init_model()
-    np.testing.assert_array_equal(m.user_factors, st["init_U"])
-    for _ in range(iters):
-        m.iterate()
-    auc_gpu, n_gpu = auc_of(m.user_factors, m.item_factors, m.item_bias, tr_u, tr_i, te_u, te_i)
-    print(f"{cls.__name__} {schedule}: AUC gpu {auc_gpu:.5f} oracle {auc_ref:.5f} users {n_gpu}")
-    assert n_gpu == n_ref
-    # ORDERED applies the device sampler's triples in sequence: |dAUC| <= 0.01.  HOGWILD on this
-    # small epoch (96k events, under 16 waves' worth) runs 4 in-order streams on one CU
-    # (bpr.hip): |dAUC| <= 0.01 too (WeightedBPRMF measured -0.007; with 16 triples per wave step
-    # it was -0.032..-0.042: popularity-drawn negatives put the hottest items into most
-    # concurrent triples).  test_weighted_hogwild_auc_parity_mid_scale covers the many-wave
-    # Hogwild at 1.9M events.
-    assert -0.01 <= auc_gpu - auc_ref <= 0.01
+    gpu, ref = [], []
+    for seed in ((5,) if schedule == "ordered" else (5, 6, 7)):
+        st = O.bpr_train(tr_u, tr_i, nu, ni, seed=seed, k=k, num_iter=iters, model=model,
+                         sampler=sampler, learn_rate=lr)
+        auc_ref, n_ref = auc_of(st["U"], st["V"], st["bias"], tr_u, tr_i, te_u, te_i)
+        Random.set_seed(seed)
+        m = cls(NumFactors=k, NumIter=iters, Schedule=schedule)
+        m.feedback = PosOnlyFeedback(tr_u, tr_i)
+        m.init_model()
+        np.testing.assert_array_equal(m.user_factors, st["init_U"])
+        for _ in range(iters):
+            m.iterate()
+        auc_gpu, n_gpu = auc_of(m.user_factors, m.item_factors, m.item_bias, tr_u, tr_i, te_u,
+                                te_i)
+        print(f"{cls.__name__} {schedule} seed {seed}: AUC gpu {auc_gpu:.5f} oracle {auc_ref:.5f}")
+        assert n_gpu == n_ref
+        gpu.append(auc_gpu)
+        ref.append(auc_ref)
+    d = float(np.mean(gpu) - np.mean(ref))
+    print(f"{cls.__name__} {schedule}: mean dAUC {d:+.5f}")
+    assert -0.01 <= d <= 0.01
 
 
 def test_weighted_sampler_without_negatives_fails_instead_of_hanging():
