@@ -1422,17 +1422,40 @@ __global__ __launch_bounds__(256) void wrmf_resid_seg_kernel(
         double x[4], acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < 4; ++j) x[j] = f0 + j < k ? xr[f0 + j] : 0.0;
-        for (int64_t e = sg.b + wave; e < sg.e; e += 4) {
-            const float* hr = H + (int64_t)cols[e] * k;
-            double hv[4];
+        // four entries per wave step, their loads and reductions interleaved
+        for (int64_t e0 = sg.b + 4 * wave; e0 < sg.e; e0 += 16) {
+            double hv[4][4], t[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) hv[j] = f0 + j < k ? (double)hr[f0 + j] : 0.0;
-            double t = hv[0] * x[0] + hv[1] * x[1] + hv[2] * x[2] + hv[3] * x[3];
+            for (int u = 0; u < 4; ++u) {
+                const int64_t e = e0 + u;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (e < sg.e) {
+                    const float* hr = H + (int64_t)cols[e] * k;
+                    if ((k & 3) == 0) {
+                        if (f0 < k) v = *reinterpret_cast<const float4*>(hr + f0);
+                    } else {
+                        v.x = f0 < k ? hr[f0] : 0.f;
+                        v.y = f0 + 1 < k ? hr[f0 + 1] : 0.f;
+                        v.z = f0 + 2 < k ? hr[f0 + 2] : 0.f;
+                        v.w = f0 + 3 < k ? hr[f0 + 3] : 0.f;
+                    }
+                }
+                hv[u][0] = v.x;
+                hv[u][1] = v.y;
+                hv[u][2] = v.z;
+                hv[u][3] = v.w;
+                t[u] = hv[u][0] * x[0] + hv[u][1] * x[1] + hv[u][2] * x[2] + hv[u][3] * x[3];
+            }
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
-            const double c = (1.0 + alpha) - alpha * t;
+            for (int o = 32; o >= 1; o >>= 1)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[j] += c * hv[j];
+                for (int u = 0; u < 4; ++u) t[u] += __shfl_xor(t[u], o, 64);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {  // entries past the segment have h = 0
+                const double c = (1.0 + alpha) - alpha * t[u];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] += c * hv[u][j];
+            }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) red[wave][f0 + j] = acc[j];
