@@ -39,6 +39,9 @@
 
 namespace {
 
+#define MML_DPP(v, ctrl) \
+    __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
+
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 constexpr int kWaves = 8;
@@ -1139,23 +1142,66 @@ void launch_wood(hipStream_t st, const int32_t* rows, int32_t n, int32_t* counte
 // is a transposing butterfly (each xor stage halves the values a lane carries, ~NJ shuffles per
 // step instead of 6 NJ) plus a 4-wave LDS sum.  Output as wrmf_wood_kernel: t = Q_S^T v for
 // C v = 1, or t = s - Q_S^T w for C w = Q_S s when S (a refinement pass) is given.
-template <int N, int SIZE, int M>
-struct XorReduce {  // v[0 .. SIZE) per lane -> sums over the 64 lanes, SIZE / 64 values per lane
+// Cross-lane steps without the LDS (ds_bpermute): lane i pairs with i ^ 32 through
+// v_permlane32_swap, with i ^ 16 through v_permlane16_swap (gfx950), and within a 16-lane row with
+// 15 - i (row_mirror), 7 - i within 8 (row_half_mirror), i ^ 2 and i ^ 1 (quad_perm) through DPP.
+// Partners always differ in the stage's bit (5, 4, 3, 2, 1, 0) and agree above it, so the stages
+// form a butterfly: after all six every lane has combined all 64.
+__device__ __forceinline__ float fbits(uint32_t u) { return __uint_as_float(u); }
+template <int STAGE>  // 0..5 = bit 5 .. bit 0
+__device__ __forceinline__ float partner_of(float v) {
+    if constexpr (STAGE == 2) return MML_DPP(v, 0x140);   // row_mirror
+    if constexpr (STAGE == 3) return MML_DPP(v, 0x141);   // row_half_mirror
+    if constexpr (STAGE == 4) return MML_DPP(v, 0x4E);    // quad_perm [2,3,0,1]
+    if constexpr (STAGE == 5) return MML_DPP(v, 0xB1);    // quad_perm [1,0,3,2]
+    return v;
+}
+// keep + partner's send, lane bit b = 5 - STAGE: lo lanes (bit clear) keep index x and hi lanes
+// x + H; the permlane swaps do the exchange and the selection in one instruction per pair
+template <int STAGE>
+__device__ __forceinline__ float tstage(float a, float b, int lane) {  // a = v[x], b = v[x + H]
+    if constexpr (STAGE == 0) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b),
+                                                        false, false);
+        return fbits(r[0]) + fbits(r[1]);
+    } else if constexpr (STAGE == 1) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b),
+                                                        false, false);
+        return fbits(r[0]) + fbits(r[1]);
+    } else {
+        const bool lo = (lane & (32 >> STAGE)) == 0;
+        return (lo ? a : b) + partner_of<STAGE>(lo ? b : a);
+    }
+}
+template <int STAGE>
+__device__ __forceinline__ float pstage(float x) {  // x + the partner's x
+    if constexpr (STAGE == 0) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x),
+                                                        false, false);
+        return fbits(r[0]) + fbits(r[1]);
+    } else if constexpr (STAGE == 1) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x),
+                                                        false, false);
+        return fbits(r[0]) + fbits(r[1]);
+    } else {
+        return x + partner_of<STAGE>(x);
+    }
+}
+
+// v[0 .. SIZE) per lane -> sums over the 64 lanes, SIZE / 64 values per lane (lane l holds
+// indices (SIZE / 64) l + x), or one value for SIZE < 64 (index l / (64 / SIZE))
+template <int N, int SIZE, int STAGE>
+struct XorReduce {
     __device__ static __forceinline__ void run(float (&v)[N], int lane) {
-        if constexpr (M > 0) {
+        if constexpr (STAGE < 6) {
             if constexpr (SIZE > 1) {
                 constexpr int H = SIZE / 2;
-                const bool lo = (lane & M) == 0;
 #pragma unroll
-                for (int x = 0; x < H; ++x) {
-                    const float keep = lo ? v[x] : v[x + H];
-                    const float send = lo ? v[x + H] : v[x];
-                    v[x] = keep + __shfl_xor(send, M, 64);
-                }
-                XorReduce<N, H, M / 2>::run(v, lane);
+                for (int x = 0; x < H; ++x) v[x] = tstage<STAGE>(v[x], v[x + H], lane);
+                XorReduce<N, H, STAGE + 1>::run(v, lane);
             } else {
-                v[0] += __shfl_xor(v[0], M, 64);
-                XorReduce<N, 1, M / 2>::run(v, lane);
+                v[0] = pstage<STAGE>(v[0]);
+                XorReduce<N, 1, STAGE + 1>::run(v, lane);
             }
         }
     }
@@ -1164,11 +1210,12 @@ struct XorReduce {  // v[0 .. SIZE) per lane -> sums over the 64 lanes, SIZE / 6
 // (x, y) summed over the workgroup, in one pass (sdot: 2 x WAVES floats)
 template <int WAVES>
 __device__ __forceinline__ float2 block_sum2(float x, float y, float* sdot) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        x += __shfl_xor(x, o, 64);
-        y += __shfl_xor(y, o, 64);
-    }
+    x = pstage<0>(x); y = pstage<0>(y);
+    x = pstage<1>(x); y = pstage<1>(y);
+    x = pstage<2>(x); y = pstage<2>(y);
+    x = pstage<3>(x); y = pstage<3>(y);
+    x = pstage<4>(x); y = pstage<4>(y);
+    x = pstage<5>(x); y = pstage<5>(y);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) {
         sdot[threadIdx.x >> 6] = x;
@@ -1227,21 +1274,17 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
         // 16, 8) are fused per group of 8 products, so only NL / 8 partial sums sit next to q
         auto qs_times = [&](float uf) -> float {
             float v[E];
-            const bool l1 = (lane & 32) == 0, l2 = (lane & 16) == 0, l3 = (lane & 8) == 0;
 #pragma unroll
             for (int x = 0; x < E; ++x) {
                 float s1[4], s2[2];
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float a = q[x + c * E] * uf, b = q[x + (c + 4) * E] * uf;
-                    s1[c] = (l1 ? a : b) + __shfl_xor(l1 ? b : a, 32, 64);
-                }
+                for (int c = 0; c < 4; ++c)
+                    s1[c] = tstage<0>(q[x + c * E] * uf, q[x + (c + 4) * E] * uf, lane);
 #pragma unroll
-                for (int c = 0; c < 2; ++c)
-                    s2[c] = (l2 ? s1[c] : s1[c + 2]) + __shfl_xor(l2 ? s1[c + 2] : s1[c], 16, 64);
-                v[x] = (l3 ? s2[0] : s2[1]) + __shfl_xor(l3 ? s2[1] : s2[0], 8, 64);
+                for (int c = 0; c < 2; ++c) s2[c] = tstage<1>(s1[c], s1[c + 2], lane);
+                v[x] = tstage<2>(s2[0], s2[1], lane);
             }
-            XorReduce<E, E, 4>::run(v, lane);
+            XorReduce<E, E, 3>::run(v, lane);
             if constexpr (NL >= 64) {
 #pragma unroll
                 for (int x = 0; x < NV; ++x) red[wave][NV * lane + x] = v[x];
