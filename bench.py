@@ -707,8 +707,9 @@ def bench_wrmf(args):
                    "alpha": 1.0, "regularization": 0.015, "device_ingest_s": ingest_s},
         "roofline": {"bound": "mfma", "achieved": tflops, "peak": 157.3, "unit": "TFLOP/s",
                      "frac": tflops / 157.3, "traffic": None,
-                     "kernel": "wrmf_wood_kernel + wrmf_tile_solve_kernel + wrmf_tile_gram_kernel "
-                               "+ wrmf_gram_* (whole iteration)",
+                     "kernel": "wrmf_wood_cg_kernel + wrmf_tile_solve_kernel + "
+                               "wrmf_tile_gram_kernel + wrmf_gram_* (+ wrmf_resid_seg_kernel, "
+                               "wrmf_tile_resolve_kernel in the fp64 mode; whole iteration)",
                      "kernel_avg_ms": float(np.mean(ms)), "flops_per_iteration": flops_exec,
                      "flops_note": "executed algorithmic flops (bench.wrmf_executed_flops): "
                                    "Woodbury rows (deg <= 128) by CG, 4 deg k per C mat-vec at "
@@ -716,10 +717,16 @@ def bench_wrmf(args):
                                    "direct rows k(k+1)deg + k^3/3 + 2k^2 + 2 deg k; per half HH "
                                    "k(k+1)n and Q = H L^-T 2nk^2; per refinement pass the fp64 "
                                    "residual 2nk^2 + 4 nnz k, 2k^2 per direct row (kept factor), "
-                                   "a 1e-4 CG per Woodbury row; the CG rows run on the VALU",
+                                   "a 1e-4 CG per Woodbury row; the CG rows run on the VALU; "
+                                   "the direct rows' Grams run as six bf16 MFMA products per "
+                                   "f32 product (exact 3-way bf16 split), counted once",
                      "refine_passes": passes,
                      "flops_direct_equivalent": flops_direct,
-                     "frac_direct_equivalent": flops_direct / (np.mean(ms) * 1e-3) / 1e12 / 157.3},
+                     "direct_equivalent_tflops": flops_direct / (np.mean(ms) * 1e-3) / 1e12,
+                     "direct_equivalent_note": "SURVEY 8(d)'s count (every row a direct k x k "
+                                               "solve) over the iteration time: a rate, not a "
+                                               "fraction of any peak -- the library executes "
+                                               "fewer flops (flops_per_iteration)"},
         "cpu_baseline": None if (args.no_cpu_baseline or world > 1) else cpu_baseline_wrmf(
             k, args.cpu_seconds, n_users, n_items, per_user),
     }
