@@ -764,7 +764,8 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
 // backward substitution; W row <- L^{-T} y.  No Gram, no factorisation.
 __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_resolve_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, int32_t* __restrict__ counter,
-    const float* __restrict__ F, const float* __restrict__ rhs, int32_t k, float* __restrict__ W) {
+    const int64_t* __restrict__ off, const float* __restrict__ F, const float* __restrict__ rhs,
+    int32_t k, float* __restrict__ W) {
     __shared__ Smem sm;
     const int wave = threadIdx.x >> 6;
     const int nt = (k + 31) >> 5, nr = nt + 1;
@@ -780,6 +781,10 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_resolve_kernel(
         if (li >= n_list) break;
         launder(tl);
         const int32_t row = rows[li];
+        if (off[row + 1] == off[row]) {  // no entries: the main solve kept no factor; d = 0
+            for (int f = t; f < k; f += kThreads) W[(int64_t)row * k + f] = 0.0f;
+            continue;
+        }
         f32x16 acc[kSlots];
 #pragma unroll
         for (int s = 0; s < kSlots; ++s) {
@@ -1749,14 +1754,14 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
         if (nh > 0) {
             MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
             wrmf_tile_resolve_kernel<<<(int)std::min<int64_t>(nh, grid_cap), kThreads, 0, st>>>(
-                p.heavy_dev.get(), (int32_t)nh, p.counter.get(),
+                p.heavy_dev.get(), (int32_t)nh, p.counter.get(), off,
                 p.factor.get() + (size_t)p.n_light * tile_floats, rhs, k, W);
             ++launches;
         }
         if (p.n_light > 0) {
             MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
             wrmf_tile_resolve_kernel<<<(int)std::min<int64_t>(p.n_light, grid_cap), kThreads, 0,
-                                       st>>>(p.light.get(), p.n_light, p.counter.get(),
+                                       st>>>(p.light.get(), p.n_light, p.counter.get(), off,
                                              p.factor.get(), rhs, k, W);
             ++launches;
         }

@@ -163,3 +163,25 @@ def test_wrmf_fp64_refinement_reaches_float_parity(k):
     print(f"WRMF k={k}: fp32 {res['fp32']}, fp64 {res['fp64']}")
     assert max(res["fp64"]) <= 2e-7
     assert max(res["fp64"]) < max(res["fp32"])
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_wrmf_large_k_rows_without_events(prec):
+    """128 < k: users and items without events solve to 0 (WRMF.cs:126-155) on the tile path,
+    the fp64 refinement pass included (those rows keep no factor)."""
+    rs = np.random.default_rng(12)
+    u = rs.integers(0, 300, 12_000).astype(np.int32)
+    i = rs.integers(0, 200, 12_000).astype(np.int32)
+    u[u % 7 == 3] = 0  # users 3, 10, 17, ... and items >= 200 get no events
+    nu, ni = 300, 260
+    Random.set_seed(2)
+    m = WRMF(NumFactors=160, NumIter=2, Precision=prec)
+    m.feedback = PosOnlyFeedback(u, i)
+    m.MaxUserID, m.MaxItemID = nu - 1, ni - 1
+    m.train()
+    U, V = m.user_factors, m.item_factors
+    assert np.all(np.isfinite(U)) and np.all(np.isfinite(V))
+    empty_u = np.setdiff1d(np.arange(U.shape[0]), u)
+    empty_i = np.setdiff1d(np.arange(V.shape[0]), i)
+    assert len(empty_u) > 0
+    assert np.all(U[empty_u] == 0) and np.all(V[empty_i] == 0)
