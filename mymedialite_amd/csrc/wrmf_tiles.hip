@@ -1367,7 +1367,11 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
     // main solve: relative residual 1e-6 (fp32 CG stagnates not far below: a tighter target
     // just runs to max_it on trained factors); a refinement correction needs 1e-4.  max_it =
     // the steps the cond(C) <= 1 + alpha bound needs, + 4
-    const double tol = S ? 1e-4 : 1e-6;
+    static const double refine_tol = [] {
+        const char* e = std::getenv("MML_WRMF_REFINE_TOL");
+        return e ? std::atof(e) : 1e-4;
+    }();
+    const double tol = S ? refine_tol : 1e-6;
     const double rho = (std::sqrt(1.0 + alpha) - 1.0) / (std::sqrt(1.0 + alpha) + 1.0);
     const int max_it = std::min(200, (int)std::ceil(std::log(tol) / std::log(rho)) + 4);
     const float tol2 = (float)(tol * tol);
@@ -1458,65 +1462,133 @@ struct RMulti {
 };
 constexpr int kRSeg = 2048;  // entries per residual segment
 
+// doubles across lanes, both 32-bit halves moved by the same instruction
+__device__ __forceinline__ uint32_t lo32(double v) { return (uint32_t)(uint64_t)__double_as_longlong(v); }
+__device__ __forceinline__ uint32_t hi32(double v) {
+    return (uint32_t)((uint64_t)__double_as_longlong(v) >> 32);
+}
+__device__ __forceinline__ double f64_of(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    return f64_of((uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo32(v), CTRL, 0xF, 0xF, false),
+                  (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi32(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    return f64_of((uint32_t)__builtin_amdgcn_readlane((int)lo32(v), l),
+                  (uint32_t)__builtin_amdgcn_readlane((int)hi32(v), l));
+}
+// The butterfly of the CG kernel's tstage / pstage on doubles: stage s pairs lanes differing in bit
+// 5 - s (permlane32 / permlane16 swaps, then row_mirror, row_half_mirror, quad_perm xor 2 / xor 1)
+template <int STAGE>
+__device__ __forceinline__ double partner_f64(double v) {
+    if constexpr (STAGE == 2) return dpp_f64<0x140>(v);
+    if constexpr (STAGE == 3) return dpp_f64<0x141>(v);
+    if constexpr (STAGE == 4) return dpp_f64<0x4E>(v);
+    return dpp_f64<0xB1>(v);
+}
+template <int STAGE>  // a = v[x], b = v[x + H]: lanes with the stage's bit clear keep x, set x + H
+__device__ __forceinline__ double tstage_f64(double a, double b, int lane) {
+    if constexpr (STAGE <= 1) {
+        const auto rl = STAGE == 0 ? __builtin_amdgcn_permlane32_swap(lo32(a), lo32(b), false, false)
+                                   : __builtin_amdgcn_permlane16_swap(lo32(a), lo32(b), false, false);
+        const auto rh = STAGE == 0 ? __builtin_amdgcn_permlane32_swap(hi32(a), hi32(b), false, false)
+                                   : __builtin_amdgcn_permlane16_swap(hi32(a), hi32(b), false, false);
+        return f64_of(rl[0], rh[0]) + f64_of(rl[1], rh[1]);
+    } else {
+        const bool lo = (lane & (32 >> STAGE)) == 0;
+        return (lo ? a : b) + partner_f64<STAGE>(lo ? b : a);
+    }
+}
+template <int STAGE>
+__device__ __forceinline__ double pstage_f64(double x) {
+    return x + partner_f64<STAGE>(x);
+}
+
+// One wave per entry segment, lane l holding features 4 l .. 4 l + 3 (h_i's 1 KB row is one
+// coalesced float4 load per lane).  The segment's column ids are read 64 at a time (one load), and
+// kResE entries per step are in flight together: their rows are loaded, h_i.x is summed by a
+// transposing butterfly (kResE values per lane -> one, 3 swaps + 3 DPP stages, no LDS), and each
+// entry's sum is read back from lane 8 u.  No barrier and no LDS: a wave's only dependent latencies
+// are its segment's ids and its rows, so thousands of waves keep the gathers in flight.  The order
+// of every sum is fixed (deterministic).
+constexpr int kResE = 8;
 __global__ __launch_bounds__(256) void wrmf_resid_seg_kernel(
     const RSeg* __restrict__ segs, int64_t nseg, const int32_t* __restrict__ cols,
     const float* __restrict__ H, int32_t k, const double* __restrict__ X, double alpha,
     double* __restrict__ R, double* __restrict__ partial) {
-    __shared__ double red[4][256];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, f0 = 4 * lane;
-    for (int64_t sgi = blockIdx.x; sgi < nseg; sgi += gridDim.x) {
-        const RSeg sg = segs[sgi];
+    static_assert(kResE == 8, "the butterfly below reduces 8 entries");
+    const int lane = threadIdx.x & 63, f0 = 4 * lane;
+    const int64_t wave0 =
+        (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t nwave = (int64_t)gridDim.x * 4;
+    const bool vec = (k & 3) == 0;
+    for (int64_t s = wave0; s < nseg; s += nwave) {
+        const RSeg sg = segs[s];
         const double* xr = X + (int64_t)sg.row * k;
-        double x[4], acc[4] = {0.0, 0.0, 0.0, 0.0};
+        double x[4], acc[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[j] = f0 + j < k ? xr[f0 + j] : 0.0;
-        // four entries per wave step, their loads and reductions interleaved
-        for (int64_t e0 = sg.b + 4 * wave; e0 < sg.e; e0 += 16) {
-            double hv[4][4], t[4];
+        for (int j = 0; j < 4; ++j) {
+            x[j] = f0 + j < k ? xr[f0 + j] : 0.0;
+            acc[j] = 0.0;
+        }
+        for (int64_t e0 = sg.b; e0 < sg.e; e0 += 64) {
+            const int n = (int)min((int64_t)64, sg.e - e0);
+            const int32_t my = lane < n ? cols[e0 + lane] : 0;
+            for (int x0 = 0; x0 < n; x0 += kResE) {
+                float v[kResE][4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int64_t e = e0 + u;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (e < sg.e) {
-                    const float* hr = H + (int64_t)cols[e] * k;
-                    if ((k & 3) == 0) {
-                        if (f0 < k) v = *reinterpret_cast<const float4*>(hr + f0);
-                    } else {
-                        v.x = f0 < k ? hr[f0] : 0.f;
-                        v.y = f0 + 1 < k ? hr[f0 + 1] : 0.f;
-                        v.z = f0 + 2 < k ? hr[f0 + 2] : 0.f;
-                        v.w = f0 + 3 < k ? hr[f0 + 3] : 0.f;
+                for (int u = 0; u < kResE; ++u) {
+                    v[u][0] = v[u][1] = v[u][2] = v[u][3] = 0.0f;
+                    if (x0 + u < n) {  // wave-uniform; entries past the segment have h = 0
+                        const float* hr = H + (int64_t)__builtin_amdgcn_readlane(my, x0 + u) * k;
+                        if (vec) {
+                            if (f0 < k) {
+                                const float4 q = *reinterpret_cast<const float4*>(hr + f0);
+                                v[u][0] = q.x;
+                                v[u][1] = q.y;
+                                v[u][2] = q.z;
+                                v[u][3] = q.w;
+                            }
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) v[u][j] = f0 + j < k ? hr[f0 + j] : 0.0f;
+                        }
                     }
                 }
-                hv[u][0] = v.x;
-                hv[u][1] = v.y;
-                hv[u][2] = v.z;
-                hv[u][3] = v.w;
-                t[u] = hv[u][0] * x[0] + hv[u][1] * x[1] + hv[u][2] * x[2] + hv[u][3] * x[3];
-            }
+                double t[kResE];
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1)
+                for (int u = 0; u < kResE; ++u)
+                    t[u] = (double)v[u][0] * x[0] + (double)v[u][1] * x[1] +
+                           (double)v[u][2] * x[2] + (double)v[u][3] * x[3];
+                double a4[4], a2[2];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) t[u] += __shfl_xor(t[u], o, 64);
+                for (int u = 0; u < 4; ++u) a4[u] = tstage_f64<0>(t[u], t[u + 4], lane);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {  // entries past the segment have h = 0
-                const double c = (1.0 + alpha) - alpha * t[u];
+                for (int u = 0; u < 2; ++u) a2[u] = tstage_f64<1>(a4[u], a4[u + 2], lane);
+                double a1 = tstage_f64<2>(a2[0], a2[1], lane);  // entry lane / 8
+                a1 = pstage_f64<3>(a1);
+                a1 = pstage_f64<4>(a1);
+                a1 = pstage_f64<5>(a1);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] += c * hv[u][j];
+                for (int u = 0; u < kResE; ++u) {
+                    const double c = (1.0 + alpha) - alpha * readlane_f64(a1, 8 * u);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[j] += c * (double)v[u][j];
+                }
             }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) red[wave][f0 + j] = acc[j];
-        __syncthreads();
-        const int f = threadIdx.x;
-        if (f < k) {
-            const double v = red[0][f] + red[1][f] + red[2][f] + red[3][f];
-            if (sg.slot < 0)
-                R[(int64_t)sg.row * k + f] += v;
-            else
-                partial[(int64_t)sg.slot * k + f] = v;
+        for (int j = 0; j < 4; ++j) {
+            const int f = f0 + j;
+            if (f < k) {
+                if (sg.slot < 0)
+                    R[(int64_t)sg.row * k + f] += acc[j];
+                else
+                    partial[(int64_t)sg.slot * k + f] = acc[j];
+            }
         }
-        __syncthreads();
     }
 }
 
@@ -1690,7 +1762,7 @@ void wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H,
             rocblas_status_success)
             fail(MML_ERR_HIP, "rocblas_dgemm failed");
         if (p.n_rsegs > 0) {
-            const int gs = (int)std::min<int64_t>(p.n_rsegs, 8192);
+            const int gs = (int)std::min<int64_t>((p.n_rsegs + 3) / 4, 8192);  // 4 waves
             wrmf_resid_seg_kernel<<<gs, 256, 0, st>>>(
                 reinterpret_cast<const RSeg*>(p.rsegs.get()), p.n_rsegs, cols, H, k, p.x64.get(),
                 alpha, p.r64.get(), p.rpartial.get());
