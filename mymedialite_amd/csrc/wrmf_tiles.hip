@@ -275,6 +275,10 @@ __device__ __forceinline__ void gram_accumulate(Smem& sm, f32x16 (&acc)[kSlots],
 // vectors 2 c2, 2 c2 + 1, and writes each plane as one conflict-free 32-bit word per lane (8 rows x
 // 8 words); the operand reads are ds_read_b128 of 8 vectors, conflict-free through the swap of
 // the two 16-B halves on rows with f & 8.
+// The b-row tiles (I = nt) hold one useful row of 32 (row kb: sum_i h_i), so they take no MFMA:
+// each staging thread sums its features of its two vectors on the VALU, the 8 vector-pair lanes of
+// a feature are reduced once per row, and the tiles' row kb is filled from that sum at the end
+// (C5 direct rows: 9 instead of 11 tiles of MFMA work per SIMD and chunk).
 using bf16x8 = __attribute__((ext_vector_type(8))) short;
 
 __device__ __forceinline__ uint32_t bf16_rn(float x) {  // round to nearest even, top 16 bits
@@ -302,6 +306,8 @@ __device__ __forceinline__ void gram_accumulate_x3(Smem& sm, f32x16 (&acc)[kSlot
     // two chunks' gathers in flight (the MFMAs of one bf16x3 chunk take ~1 us per SIMD, less
     // than an HBM gather's latency): va = chunk c + 1, vb = chunk c + 2
     float va0[4], va1[4], vb0[4], vb1[4];
+    float bacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // sum over this thread's vectors, features f < k
+    const int ntb = hsw / 32 - 1;              // the b-row tile row
     auto fetch = [&](int64_t base, float (&v0)[4], float (&v1)[4]) {
         const int64_t e0 = base + 2 * c2, e1 = e0 + 1;
         const float* s0 = H + (int64_t)(e0 < e ? cols[e0] : 0) * k;
@@ -314,9 +320,11 @@ __device__ __forceinline__ void gram_accumulate_x3(Smem& sm, f32x16 (&acc)[kSlot
         }
     };
     auto stash = [&](int buf, int64_t base, const float (&v0)[4], const float (&v1)[4]) {
+        (void)base;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int f = 32 * wave + 8 * g + r;
+            if (f < k) bacc[g] += v0[g] + v1[g];
             uint32_t a0, a1, a2, b0, b1, b2;
             split3(v0[g], a0, a1, a2);
             split3(v1[g], b0, b1, b2);
@@ -325,18 +333,7 @@ __device__ __forceinline__ void gram_accumulate_x3(Smem& sm, f32x16 (&acc)[kSlot
             *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][1][f][pos]) = a1 | (b1 << 16);
             *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][2][f][pos]) = a2 | (b2 << 16);
         }
-        // rows 256 .. hsw (k = 256): zero, except row kb: 1 for the live vectors (so that row kb
-        // of the Gram accumulates sum_i h_i)
-        for (int x = t; x < (hsw - 256 > 0 ? hsw - 256 : 0) * 8; x += kThreads) {
-            const int f = 256 + x / 8, w2 = x % 8;
-            const int64_t ea = base + 2 * w2, eb2 = ea + 1;
-            const uint32_t one_a = (f == kb && ea < e) ? 0x3F80u : 0u;
-            const uint32_t one_b = (f == kb && eb2 < e) ? 0x3F80u : 0u;
-            const int pos = pl_pos(f, 2 * w2);
-            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][0][f][pos]) = one_a | (one_b << 16);
-            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][1][f][pos]) = 0u;
-            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][2][f][pos]) = 0u;
-        }
+        // (rows >= kb are read by the b-row tiles only, which take no MFMA: not staged)
     };
     if (e <= b) return;
     __syncthreads();  // the LDS union may still be read by the previous row's last phase
@@ -351,7 +348,7 @@ __device__ __forceinline__ void gram_accumulate_x3(Smem& sm, f32x16 (&acc)[kSlot
         if (nb + kCH < e) fetch(nb + kCH, vb0, vb1);  // chunk c + 2 joins c + 1 in flight
 #pragma unroll
         for (int s = 0; s < kSlots; ++s) {
-            if (s >= nslot || tl.I[s] < 0) continue;
+            if (s >= nslot || tl.I[s] < 0 || tl.I[s] == ntb) continue;
             const int fa = 32 * tl.J[s] + q, fb = 32 * tl.I[s] + q;
             bf16x8 A[3], B[3];
 #pragma unroll
@@ -377,6 +374,25 @@ __device__ __forceinline__ void gram_accumulate_x3(Smem& sm, f32x16 (&acc)[kSlot
             va0[g] = vb0[g];
             va1[g] = vb1[g];
         }
+    }
+    // row kb of the b-row tiles: sum_i h_i, the 8 vector-pair lanes (lane & 7) of a feature
+    // reduced, then read by the tiles' owners (lanes q = 0, columns 32 J + rho(g, h))
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        float v = bacc[g];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        const int f = 32 * wave + 8 * g + r;
+        if (c2 == 0 && f < kb) sm.wv[f] = f < k ? v : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+        if (s >= nslot || tl.I[s] != ntb) continue;
+#pragma unroll
+        for (int g = 0; g < 16; ++g)
+            acc[s][g] += q == 0 ? sm.wv[32 * tl.J[s] + rho(g, h)] : 0.0f;
     }
 }
 

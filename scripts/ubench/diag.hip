@@ -74,6 +74,54 @@ __global__ __launch_bounds__(64) void k_diag(float* out, long long* cyc, int rep
                 for (int m = 0; m < 32; ++m) tT[q][m] = tc[m];
             keep += tT[q][q & 7];
         }
+        if (MODE & 8) {  // right-looking inverse: column j of L from a transposed copy in LDS
+            __shared__ float lT[32][36];
+            if (h == 0)
+#pragma unroll
+                for (int c = 0; c < 32; ++c) lT[c][q] = x[c];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            float sv[32];
+#pragma unroll
+            for (int m = 0; m < 32; ++m) sv[m] = (m == q) ? 1.0f : 0.0f;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                sv[j] *= __builtin_amdgcn_rcpf(lT[j][j]);
+#pragma unroll
+                for (int m4 = (j + 1) & ~3; m4 < 32; m4 += 4) {
+                    const float4 l = *reinterpret_cast<const float4*>(&lT[j][m4]);
+                    if (m4 > j) sv[m4] -= l.x * sv[j];
+                    if (m4 + 1 > j) sv[m4 + 1] -= l.y * sv[j];
+                    if (m4 + 2 > j) sv[m4 + 2] -= l.z * sv[j];
+                    if (m4 + 3 > j) sv[m4 + 3] -= l.w * sv[j];
+                }
+            }
+            if (h == 0)
+#pragma unroll
+                for (int m = 0; m < 32; ++m) tT[q][m] = sv[m];
+            keep += tT[q][q & 7];
+        }
+        if (MODE & 16) {  // the kernel's single-accumulator inverse
+            float tc[32];
+#pragma unroll
+            for (int m = 0; m < 32; ++m) {
+                float sacc = (m == q) ? 1.0f : 0.0f;
+#pragma unroll
+                for (int j4 = 0; j4 < m; j4 += 4) {
+                    const float4 l = *reinterpret_cast<const float4*>(&dg[m][j4]);
+                    sacc -= l.x * tc[j4];
+                    if (j4 + 1 < m) sacc -= l.y * tc[j4 + 1];
+                    if (j4 + 2 < m) sacc -= l.z * tc[j4 + 2];
+                    if (j4 + 3 < m) sacc -= l.w * tc[j4 + 3];
+                }
+                tc[m] = sacc * __builtin_amdgcn_rcpf(dg[m][m]);
+            }
+            if (h == 0)
+#pragma unroll
+                for (int m = 0; m < 32; ++m) tT[q][m] = tc[m];
+            keep += tT[q][q & 7];
+        }
 #pragma unroll
         for (int c = 0; c < 32; ++c) keep += x[c];
         asm volatile("" : "+v"(keep));
@@ -99,5 +147,9 @@ int main() {
     run(k_diag<3>, "factor+inverse");
     run(k_diag<4>, "factor packed");
     run(k_diag<6>, "packed+inverse");
+    run(k_diag<16>, "inverse 1-acc");
+    run(k_diag<8>, "inverse right");
+    run(k_diag<17>, "factor+inv 1-acc");
+    run(k_diag<9>, "factor+inv right");
     return 0;
 }
