@@ -291,6 +291,21 @@ __device__ __forceinline__ void split3(float x, uint32_t& a, uint32_t& b, uint32
     b = bf16_rn(r1);
     c = bf16_rn(r1 - __uint_as_float(b << 16));  // exact: <= 8 significant bits remain
 }
+// The same exact split in fewer VALU ops: x0 = x truncated to its top half (2 ops), x1 = x - x0
+// rounded to nearest bf16 (4 ops), x2 = the rest, which has <= 8 significant bits (exact); the
+// parts are the top halves of a, b, c.  |x1| < 2^-7 |x| and |x2| <= 2^-16 |x|, so the dropped
+// products x1 y2, x2 y1, x2 y2 stay below 2^-22 relative (RN of all parts: 2^-24), well inside
+// the fp32 mode's tolerance and corrected by the fp64 mode's refinement.
+__device__ __forceinline__ void split3t(float x, uint32_t& a, uint32_t& b, uint32_t& c) {
+    a = __float_as_uint(x);
+    const float r1 = x - __uint_as_float(a & 0xFFFF0000u);
+    const uint32_t u1 = __float_as_uint(r1);
+    b = (u1 + 0x7FFFu + ((u1 >> 16) & 1u)) & 0xFFFF0000u;
+    c = __float_as_uint(r1 - __uint_as_float(b));
+}
+__device__ __forceinline__ uint32_t pack_hi(uint32_t lo, uint32_t hi) {  // {lo.hi16, hi.hi16}
+    return __builtin_amdgcn_perm(hi, lo, 0x07060302u);
+}
 __device__ __forceinline__ int pl_pos(int f, int c) {  // element (f, c) within row f
     return ((((c >> 3) ^ (f >> 3)) & 1) << 3) | (c & 7);
 }
@@ -306,12 +321,20 @@ __device__ __forceinline__ void gram_accumulate_x3(Smem& sm, f32x16 (&acc)[kSlot
     // two chunks' gathers in flight (the MFMAs of one bf16x3 chunk take ~1 us per SIMD, less
     // than an HBM gather's latency): va = chunk c + 1, vb = chunk c + 2
     float va0[4], va1[4], vb0[4], vb1[4];
+#if MML_GRAM_DEPTH3
+    float vc0[4], vc1[4];
+#endif
     float bacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // sum over this thread's vectors, features f < k
     const int ntb = hsw / 32 - 1;              // the b-row tile row
     auto fetch = [&](int64_t base, float (&v0)[4], float (&v1)[4]) {
         const int64_t e0 = base + 2 * c2, e1 = e0 + 1;
+#if MML_GRAM_NOLOAD  // timing experiment only: every vector is row 0 (cache-resident)
+        const float* s0 = H;
+        const float* s1 = H;
+#else
         const float* s0 = H + (int64_t)(e0 < e ? cols[e0] : 0) * k;
         const float* s1 = H + (int64_t)(e1 < e ? cols[e1] : 0) * k;
+#endif
 #pragma unroll
         for (int g = 0; g < 4; ++g) {  // features >= k: 0, except row kb (1 on live vectors)
             const int f = 32 * wave + 8 * g + r;
@@ -326,12 +349,20 @@ __device__ __forceinline__ void gram_accumulate_x3(Smem& sm, f32x16 (&acc)[kSlot
             const int f = 32 * wave + 8 * g + r;
             if (f < k) bacc[g] += v0[g] + v1[g];
             uint32_t a0, a1, a2, b0, b1, b2;
+            const int pos = pl_pos(f, 2 * c2);
+#if MML_GRAM_SPLIT_RN
             split3(v0[g], a0, a1, a2);
             split3(v1[g], b0, b1, b2);
-            const int pos = pl_pos(f, 2 * c2);
             *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][0][f][pos]) = a0 | (b0 << 16);
             *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][1][f][pos]) = a1 | (b1 << 16);
             *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][2][f][pos]) = a2 | (b2 << 16);
+#else
+            split3t(v0[g], a0, a1, a2);
+            split3t(v1[g], b0, b1, b2);
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][0][f][pos]) = pack_hi(a0, b0);
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][1][f][pos]) = pack_hi(a1, b1);
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[buf][2][f][pos]) = pack_hi(a2, b2);
+#endif
         }
         // (rows >= kb are read by the b-row tiles only, which take no MFMA: not staged)
     };
@@ -340,12 +371,19 @@ __device__ __forceinline__ void gram_accumulate_x3(Smem& sm, f32x16 (&acc)[kSlot
     fetch(b, va0, va1);
     stash(0, b, va0, va1);
     if (b + kCH < e) fetch(b + kCH, va0, va1);
+#if MML_GRAM_DEPTH3
+    if (b + 2 * kCH < e) fetch(b + 2 * kCH, vb0, vb1);
+#endif
     __syncthreads();
     int cur = 0;
     for (int64_t base = b; base < e; base += kCH) {
         const int64_t nb = base + kCH;
         const bool more = nb < e;
+#if MML_GRAM_DEPTH3
+        if (nb + 2 * kCH < e) fetch(nb + 2 * kCH, vc0, vc1);  // chunks c + 1 .. c + 3 in flight
+#else
         if (nb + kCH < e) fetch(nb + kCH, vb0, vb1);  // chunk c + 2 joins c + 1 in flight
+#endif
 #pragma unroll
         for (int s = 0; s < kSlots; ++s) {
             if (s >= nslot || tl.I[s] < 0 || tl.I[s] == ntb) continue;
@@ -373,6 +411,10 @@ __device__ __forceinline__ void gram_accumulate_x3(Smem& sm, f32x16 (&acc)[kSlot
         for (int g = 0; g < 4; ++g) {
             va0[g] = vb0[g];
             va1[g] = vb1[g];
+#if MML_GRAM_DEPTH3
+            vb0[g] = vc0[g];
+            vb1[g] = vc1[g];
+#endif
         }
     }
     // row kb of the b-row tiles: sum_i h_i, the 8 vector-pair lanes (lane & 7) of a feature

@@ -1,10 +1,10 @@
 #!/bin/bash
-# build/variants/NAME/libmml_hip.so: the library with extra compile flags (A/B experiments; load it
+# variants/NAME/libmml_hip.so: the library with extra compile flags (A/B experiments; load it
 # with MML_LIB_PATH=...).  Usage: scripts/build_variant.sh NAME "-DFLAG ..."
 set -e
 name=$1; flags=$2
 root=$(cd "$(dirname "$0")/.." && pwd)
-out=$root/build/variants/$name
+out=$root/variants/$name  # not under build/: that is gpurun-ignored
 mkdir -p "$out"
 cd "$root/mymedialite_amd/csrc"
 objs=()
@@ -17,6 +17,6 @@ for f in *.cpp; do
   objs+=("$out/${f%.cpp}.o")
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/libmml_hip.so" "${objs[@]}" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/libmml_hip.so" "${objs[@]}" -L/opt/rocm/lib -lrccl -lrocblas -Wl,-rpath,/opt/rocm/lib
 rm -f "${objs[@]}"
 echo "$out/libmml_hip.so"
