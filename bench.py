@@ -717,7 +717,7 @@ def bench_wrmf(args):
                                    "direct rows k(k+1)deg + k^3/3 + 2k^2 + 2 deg k; per half HH "
                                    "k(k+1)n and Q = H L^-T 2nk^2; per refinement pass the fp64 "
                                    "residual 2nk^2 + 4 nnz k, 2k^2 per direct row (kept factor), "
-                                   "a 1e-4 CG per Woodbury row; the CG rows run on the VALU; "
+                                   "a 3e-3 CG per Woodbury row; the CG rows run on the VALU; "
                                    "the direct rows' Grams run as six bf16 MFMA products per "
                                    "f32 product (exact 3-way bf16 split), counted once",
                      "refine_passes": passes,
@@ -761,7 +761,7 @@ def wrmf_executed_flops(deg_u, deg_i, k, passes=0, nnz=0, alpha=1.0):
         if passes and k > 128:
             per = 2.0 * len(deg) * k * k + 4.0 * float(deg.sum()) * k  # residual
             per += 2.0 * k * k * len(dd)  # L y = r, L^T d = y on the kept factors
-            per += float((steps(1e-4) * 4 * dw * k + 4 * dw * k).sum()) + 4.0 * k * k * len(dw)
+            per += float((steps(3e-3) * 4 * dw * k + 4 * dw * k).sum()) + 4.0 * k * k * len(dw)
             f += passes * per
         return f
     return half(deg_u, len(deg_i)) + half(deg_i, len(deg_u))

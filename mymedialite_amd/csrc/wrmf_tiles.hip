@@ -890,6 +890,117 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_resolve_kernel(
     }
 }
 
+// The same refinement pass with one wave per row and no workgroup barrier: the wave streams the
+// row's kept tiles from memory (each lower tile once per substitution) instead of holding them in
+// 8 waves' registers, so ~100 VGPRs and many rows per CU keep the tile loads in flight; the
+// workgroup version waits on 56 barriers per row, with one row per CU.
+//   forward  y_J = T_J (r_J - sum_{K<J} L_JK y_K):  lane (q, h) sums its 16 columns rho(g, h) of
+//            row q against y from LDS, the halves meet by a lane-32 swap;
+//   backward w_J = T_J^T (y_J - sum_{I>J} L_IJ^T w_I):  lane (q, h) scales its 16 columns by w_I[q]
+//            (its own row), and the column sums over q go through a transposed LDS tile.
+// Tile (I, J) of row li is F[(li * kTiles + tile_id(I, J, nr)) * 1024 + g * 64 + lane]: lane (q, h)
+// register g holds L[32 I + q][32 J + rho(g, h)] below the diagonal and T_J[q][2 g + h] on it.
+constexpr int kRvWaves = 4;
+constexpr int kRvS = 36;  // transposed-tile row stride (16-B aligned rows)
+struct alignas(16) RvSmem {
+    float ys[kHSW];          // y, then read by the backward pass
+    float ws[kHSW];          // w
+    float sv[32];
+    float red[32 * kRvS];    // red[c * kRvS + q]: column sums over q
+};
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__global__ __launch_bounds__(64 * kRvWaves) void wrmf_tile_resolve_wave_kernel(
+    const int32_t* __restrict__ rows, int32_t n_list, const int64_t* __restrict__ off,
+    const float* __restrict__ F, const float* __restrict__ rhs, int32_t k, float* __restrict__ W) {
+    __shared__ RvSmem smem[kRvWaves];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane & 31, h = lane >> 5;
+    RvSmem& sm = smem[wv];
+    const int nt = (k + 31) >> 5, nr = nt + 1;
+    const int64_t nwave = (int64_t)gridDim.x * kRvWaves;
+    for (int64_t li = (int64_t)blockIdx.x * kRvWaves + wv; li < n_list; li += nwave) {
+        const int32_t row = rows[li];
+        float* wr = W + (int64_t)row * k;
+        if (off[row + 1] == off[row]) {  // no entries: the main solve kept no factor; d = 0
+            for (int f = lane; f < k; f += 64) wr[f] = 0.0f;
+            continue;
+        }
+        const float* Fr = F + (int64_t)li * kTiles * 1024 + lane;
+        const float* rr = rhs + (int64_t)row * k;
+        float tv[16];
+        auto load_tile = [&](int I, int J) {
+            const float* src = Fr + (int64_t)tile_id(I, J, nr) * 1024;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) tv[g] = src[g * 64];
+        };
+        // ---- forward substitution
+        for (int J = 0; J < nt; ++J) {
+            float a = 0.0f;
+            for (int K = 0; K < J; ++K) {
+                load_tile(J, K);
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const float4 y4 = *reinterpret_cast<const float4*>(&sm.ys[32 * K + 8 * m + 4 * h]);
+                    a += tv[4 * m] * y4.x + tv[4 * m + 1] * y4.y + tv[4 * m + 2] * y4.z +
+                         tv[4 * m + 3] * y4.w;
+                }
+            }
+            a += __shfl_xor(a, 32, 64);
+            const int f = 32 * J + q;
+            const float s = (f < k ? rr[f] : 0.0f) - a;
+            if (h == 0) sm.sv[q] = s;
+            load_tile(J, J);
+            wave_sync();
+            float y = 0.0f;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) y += tv[g] * sm.sv[2 * g + h];
+            y += __shfl_xor(y, 32, 64);
+            if (h == 0) sm.ys[f] = y;
+            wave_sync();
+        }
+        // ---- backward substitution
+        for (int J = nt - 1; J >= 0; --J) {
+            float p[16];
+#pragma unroll
+            for (int g = 0; g < 16; ++g) p[g] = 0.0f;
+            for (int I = J + 1; I < nt; ++I) {
+                load_tile(I, J);
+                const float wq = sm.ws[32 * I + q];
+#pragma unroll
+                for (int g = 0; g < 16; ++g) p[g] += tv[g] * wq;
+            }
+#pragma unroll
+            for (int g = 0; g < 16; ++g) sm.red[rho(g, h) * kRvS + q] = p[g];
+            load_tile(J, J);
+            wave_sync();
+            float v = sm.ys[32 * J + q];
+#pragma unroll
+            for (int x = 0; x < 32; x += 4) {
+                const float4 r4 = *reinterpret_cast<const float4*>(&sm.red[q * kRvS + x]);
+                v -= (r4.x + r4.y) + (r4.z + r4.w);
+            }
+            wave_sync();
+            // w_J[c] = sum_m T_J[m][c] v[m]: lane (q, h) holds T_J[q][2 g + h], v[q] is its own
+#pragma unroll
+            for (int g = 0; g < 16; ++g) sm.red[(2 * g + h) * kRvS + q] = tv[g] * v;
+            wave_sync();
+            float w = 0.0f;
+#pragma unroll
+            for (int x = 0; x < 32; x += 4) {
+                const float4 r4 = *reinterpret_cast<const float4*>(&sm.red[q * kRvS + x]);
+                w += (r4.x + r4.y) + (r4.z + r4.w);
+            }
+            if (h == 0) sm.ws[32 * J + q] = w;
+            wave_sync();
+        }
+        for (int f = lane; f < k; f += 64) wr[f] = sm.ws[f];
+        wave_sync();  // the next row's forward pass rewrites ys / ws
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Woodbury rows, several per workgroup.  A row with deg <= 32 NT entries has only
 // NT (NT + 1) - NT (NT - 1) / 2 tiles (<= 14), so the 8 waves split into R groups of WPG waves and
@@ -1423,11 +1534,14 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
                     const float* S) {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, 256 * 4));
     // main solve: relative residual 1e-6 (fp32 CG stagnates not far below: a tighter target
-    // just runs to max_it on trained factors); a refinement correction needs 1e-4.  max_it =
-    // the steps the cond(C) <= 1 + alpha bound needs, + 4
+    // just runs to max_it on trained factors).  A refinement correction d needs only 3e-3: x is
+    // already within ~1e-6 of the solution, so d's own error leaves ~3e-9 after x += d, below the
+    // float W's rounding (the fp64 tests measure the same errors at 1e-4, 3e-3 and 1e-2; C5's
+    // refinement CG 1e-4 -> 3e-3: 278 -> 254 ms per iteration).  max_it = the steps the
+    // cond(C) <= 1 + alpha bound needs, + 4
     static const double refine_tol = [] {
         const char* e = std::getenv("MML_WRMF_REFINE_TOL");
-        return e ? std::atof(e) : 1e-4;
+        return e ? std::atof(e) : 3e-3;
     }();
     const double tol = S ? refine_tol : 1e-6;
     const double rho = (std::sqrt(1.0 + alpha) - 1.0) / (std::sqrt(1.0 + alpha) + 1.0);
@@ -1881,20 +1995,26 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
     const int64_t nh = (int64_t)p.heavy.size();
     const size_t tile_floats = (size_t)kTiles * 1024;
     if (rhs && p.keep_factor) {  // refinement: the kept factors, no Gram, no factorisation
-        if (nh > 0) {
-            MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
-            wrmf_tile_resolve_kernel<<<(int)std::min<int64_t>(nh, grid_cap), kThreads, 0, st>>>(
-                p.heavy_dev.get(), (int32_t)nh, p.counter.get(), off,
-                p.factor.get() + (size_t)p.n_light * tile_floats, rhs, k, W);
+        // one wave per row (default) or the 8-wave workgroup per row (MML_WRMF_RESOLVE=wg, A/B)
+        static const bool wg = [] {
+            const char* e = std::getenv("MML_WRMF_RESOLVE");
+            return e && std::string(e) == "wg";
+        }();
+        auto resolve = [&](const int32_t* list, int64_t n, const float* Fl) {
+            if (n <= 0) return;
+            if (wg) {
+                MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
+                wrmf_tile_resolve_kernel<<<(int)std::min<int64_t>(n, grid_cap), kThreads, 0, st>>>(
+                    list, (int32_t)n, p.counter.get(), off, Fl, rhs, k, W);
+            } else {
+                const int64_t blocks = std::min<int64_t>((n + kRvWaves - 1) / kRvWaves, 256 * 16);
+                wrmf_tile_resolve_wave_kernel<<<(int)blocks, 64 * kRvWaves, 0, st>>>(
+                    list, (int32_t)n, off, Fl, rhs, k, W);
+            }
             ++launches;
-        }
-        if (p.n_light > 0) {
-            MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
-            wrmf_tile_resolve_kernel<<<(int)std::min<int64_t>(p.n_light, grid_cap), kThreads, 0,
-                                       st>>>(p.light.get(), p.n_light, p.counter.get(), off,
-                                             p.factor.get(), rhs, k, W);
-            ++launches;
-        }
+        };
+        resolve(p.heavy_dev.get(), nh, p.factor.get() + (size_t)p.n_light * tile_floats);
+        resolve(p.light.get(), p.n_light, p.factor.get());
         MML_HIP(hipGetLastError());
     } else {
         // the factors of the direct rows, kept when refinement passes follow (fp64 mode)
