@@ -15,7 +15,7 @@ for v in ${VARIANTS:-base depth3 noload}; do
   cp "$f" gpurun_out/ab_${v}_kernel_stats.csv; rm -rf gpurun_out/ab_$v
   python - gpurun_out/ab_${v}_kernel_stats.csv $v <<'PY'
 import csv, sys
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if "tile_solve" in r["Name"] or "tile_gram" in r["Name"]]
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if any(x in r["Name"] for x in ("tile_solve", "tile_gram", "wood_cg"))]
 print(sys.argv[2], "; ".join(f"{r['Name'][24:50]} {float(r['TotalDurationNs'])/1e6:.1f} ms" for r in rows), flush=True)
 PY
 done
