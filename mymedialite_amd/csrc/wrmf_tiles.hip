@@ -1381,7 +1381,9 @@ struct XorReduce {
     }
 };
 
-// (x, y) summed over the workgroup, in one pass (sdot: 2 x WAVES floats)
+// (x, y) summed over the workgroup, in one pass (sdot: 2 x WAVES floats).  One barrier: the
+// caller alternates two sdot buffers, and every earlier read of this buffer (two calls back) is
+// ordered by the barriers between the calls.
 template <int WAVES>
 __device__ __forceinline__ float2 block_sum2(float x, float y, float* sdot) {
     x = pstage<0>(x); y = pstage<0>(y);
@@ -1390,7 +1392,6 @@ __device__ __forceinline__ float2 block_sum2(float x, float y, float* sdot) {
     x = pstage<3>(x); y = pstage<3>(y);
     x = pstage<4>(x); y = pstage<4>(y);
     x = pstage<5>(x); y = pstage<5>(y);
-    __syncthreads();
     if ((threadIdx.x & 63) == 0) {
         sdot[threadIdx.x >> 6] = x;
         sdot[WAVES + (threadIdx.x >> 6)] = y;
@@ -1426,7 +1427,7 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
     __shared__ float sp[NJ];
     __shared__ float su[HALVES][256];
     __shared__ float red[WAVES][NL];
-    __shared__ float sdot[2 * WAVES];
+    __shared__ float sdot[2][2 * WAVES];  // alternated per CG step (block_sum2)
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int f = t & 255, half = t >> 8, hw = wave & 3;  // feature, item half, wave in half
     const float ainv = 1.0f / alpha;
@@ -1498,7 +1499,7 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
             const float uf = qt_times();
             const float cr = (t < deg ? r * ainv : 0.0f) + qs_times(uf);  // C r
             const float2 gd = block_sum2<WAVES>(t < NJ ? r * r : 0.0f, t < NJ ? cr * r : 0.0f,
-                                                sdot);
+                                                sdot[it & 1]);
             if (it == 0) stop = tol2 * gd.x;
             if (gd.x <= stop || it == max_it) break;
             const float b = it == 0 ? 0.0f : gd.x / g_prev;
