@@ -1610,6 +1610,118 @@ __global__ __launch_bounds__(256) void wrmf_rows_matmul_kernel(
     }
 }
 
+// The same row GEMM on the bf16 matrix cores at f32 accuracy (the Gram's 3-way split, six
+// products per K step, split3t): 2.7x fewer MFMA cycles than v_mfma_f32_32x32x2_f32.  M comes as
+// its bf16 planes, transposed and K-padded (wrmf_split_mt_kernel, once per half-step), so a lane's
+// B operand (8 consecutive k of one column) is one 16-B load from L2; X's 32 rows are split into
+// three bf16 planes in LDS (row stride kXS: the A reads are conflict-free per 16 lanes).
+constexpr int kXS = 264;
+__global__ __launch_bounds__(256) void wrmf_split_mt_kernel(const float* __restrict__ M, int32_t k,
+                                                            int32_t kpad,
+                                                            uint16_t* __restrict__ MT) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)k * kpad;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e / kpad), kk = (int)(e - (int64_t)c * kpad);
+        const float v = kk < k ? M[(int64_t)kk * k + c] : 0.0f;
+        uint32_t a, b, d;
+        split3t(v, a, b, d);
+        MT[((int64_t)0 * k + c) * kpad + kk] = (uint16_t)(a >> 16);
+        MT[((int64_t)1 * k + c) * kpad + kk] = (uint16_t)(b >> 16);
+        MT[((int64_t)2 * k + c) * kpad + kk] = (uint16_t)(d >> 16);
+    }
+}
+__global__ __launch_bounds__(256) void wrmf_rows_matmul_x3_kernel(
+    const float* __restrict__ X, const int32_t* __restrict__ xrows, int64_t n,
+    const uint16_t* __restrict__ MT, int32_t k, int32_t kpad, float scale, float* __restrict__ Y,
+    const int32_t* __restrict__ yrows) {
+    __shared__ __attribute__((aligned(16))) uint16_t xs[3][32 * kXS];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, q = lane & 31, h = lane >> 5;
+    const int nct = (k + 31) >> 5;
+    const bool vec = (k & 3) == 0;
+    for (int64_t blk = blockIdx.x; blk * 32 < n; blk += gridDim.x) {
+        const int64_t r0 = blk * 32;
+        __syncthreads();
+        for (int x = 4 * t; x < 32 * kpad; x += 4 * 256) {  // 4 consecutive k of one row
+            const int i = x / kpad, f = x - i * kpad;
+            float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (r0 + i < n) {
+                const float* src = X + (xrows ? (int64_t)xrows[r0 + i] : r0 + i) * k;
+                if (vec && f + 3 < k) {
+                    const float4 v4 = *reinterpret_cast<const float4*>(src + f);
+                    v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] = f + j < k ? src[f + j] : 0.0f;
+                }
+            }
+            uint32_t a[4], b[4], c[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) split3t(v[j], a[j], b[j], c[j]);
+            uint2* d0 = reinterpret_cast<uint2*>(&xs[0][i * kXS + f]);
+            uint2* d1 = reinterpret_cast<uint2*>(&xs[1][i * kXS + f]);
+            uint2* d2 = reinterpret_cast<uint2*>(&xs[2][i * kXS + f]);
+            *d0 = make_uint2(pack_hi(a[0], a[1]), pack_hi(a[2], a[3]));
+            *d1 = make_uint2(pack_hi(b[0], b[1]), pack_hi(b[2], b[3]));
+            *d2 = make_uint2(pack_hi(c[0], c[1]), pack_hi(c[2], c[3]));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+            const int J = wave * 2 + jt;
+            if (J >= nct) continue;
+            const int col = 32 * J + q;
+            const bool cok = col < k;
+            const uint16_t* m0 = MT + ((int64_t)(cok ? col : 0)) * kpad + 8 * h;
+            const int64_t pstride = (int64_t)k * kpad;
+            f32x16 d;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) d[g] = 0.0f;
+            for (int kc = 0; kc < kpad; kc += 16) {
+                bf16x8 A[3], B[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    A[p] = *reinterpret_cast<const bf16x8*>(&xs[p][q * kXS + kc + 8 * h]);
+                    B[p] = *reinterpret_cast<const bf16x8*>(m0 + p * pstride + kc);
+                }
+                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], d, 0, 0, 0);
+            }
+            if (cok)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const int i = rho(g, h);
+                    if (r0 + i < n) {
+                        const int64_t dst = yrows ? yrows[r0 + i] : r0 + i;
+                        Y[dst * k + col] = scale * d[g];
+                    }
+                }
+        }
+    }
+}
+
+// Y = scale X M through the bf16x3 kernel (MX: M's planes from wrmf_split_mt_kernel), or the f32
+// MFMA kernel with MML_WRMF_GEMM=f32 (A/B)
+bool gemm_f32() {
+    static const bool v = [] {
+        const char* e = std::getenv("MML_WRMF_GEMM");
+        return e && std::string(e) == "f32";
+    }();
+    return v;
+}
+void rows_matmul(hipStream_t st, const float* X, const int32_t* xrows, int64_t n, const float* M,
+                 const uint16_t* MX, int32_t k, float scale, float* Y, const int32_t* yrows) {
+    const int grid = (int)std::min<int64_t>((n + 31) / 32, 8192);
+    if (gemm_f32())
+        wrmf_rows_matmul_kernel<<<grid, 256, 0, st>>>(X, xrows, n, M, k, scale, Y, yrows);
+    else
+        wrmf_rows_matmul_x3_kernel<<<grid, 256, 0, st>>>(X, xrows, n, MX, k, (k + 15) & ~15, scale,
+                                                         Y, yrows);
+}
+
 // MML_WRMF_DEBUG: phase-skip mask for timing experiments only (results are wrong when set):
 // 1 diagonal factorisation, 2 panel MFMAs, 4 backward substitution, 8 Gram
 int debug_mask() {
@@ -2065,10 +2177,8 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
         p.sbuf.alloc((size_t)nw_max * k);
         for (int g = 0; g < 4; ++g) {
             if (!p.n_wood[g]) continue;
-            const int gw = (int)std::min<int64_t>((p.n_wood[g] + 31) / 32, 8192);
-            wrmf_rows_matmul_kernel<<<gw, 256, 0, st>>>(rhs, p.wood[g].get(), p.n_wood[g],
-                                                        p.linvt.get(), k, 1.0f, p.sbuf.get(),
-                                                        nullptr);
+            rows_matmul(st, rhs, p.wood[g].get(), p.n_wood[g], p.linvt.get(), p.linvt_x3.get(), k,
+                        1.0f, p.sbuf.get(), nullptr);
             if (wood_cg()) {
                 launch_wood_cg(st, g, p.wood[g].get(), p.n_wood[g], off, cols, p.qbuf.get(), k,
                                (float)alpha, p.tbuf.get(), p.sbuf.get());
@@ -2078,8 +2188,8 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                 L(st, p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, p.qbuf.get(), k,
                   (float)alpha, p.tbuf.get(), p.sbuf.get());
             }
-            wrmf_rows_matmul_kernel<<<gw, 256, 0, st>>>(p.tbuf.get(), nullptr, p.n_wood[g],
-                                                        p.linv.get(), k, 1.0f, W, p.wood[g].get());
+            rows_matmul(st, p.tbuf.get(), nullptr, p.n_wood[g], p.linv.get(), p.linv_x3.get(), k,
+                        1.0f, W, p.wood[g].get());
             MML_HIP(hipGetLastError());
             launches += 3;
         }
@@ -2103,10 +2213,16 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                            hipMemcpyHostToDevice, st));
     MML_HIP(hipMemcpyAsync(p.linvt.get(), ltf.data(), sizeof(float) * ltf.size(),
                            hipMemcpyHostToDevice, st));
+    const int kpad = (k + 15) & ~15;
+    p.linv_x3.alloc((size_t)3 * k * kpad);
+    p.linvt_x3.alloc((size_t)3 * k * kpad);
+    const int gsp = (int)std::min<int64_t>(((int64_t)k * kpad + 255) / 256, 1024);
+    wrmf_split_mt_kernel<<<gsp, 256, 0, st>>>(p.linv.get(), k, kpad, p.linv_x3.get());
+    wrmf_split_mt_kernel<<<gsp, 256, 0, st>>>(p.linvt.get(), k, kpad, p.linvt_x3.get());
+    launches += 2;
     p.qbuf.alloc((size_t)h_rows * k);
-    const int gq = (int)std::min<int64_t>((h_rows + 31) / 32, 8192);
-    wrmf_rows_matmul_kernel<<<gq, 256, 0, st>>>(H, nullptr, h_rows, p.linvt.get(), k, 1.0f,
-                                                p.qbuf.get(), nullptr);
+    rows_matmul(st, H, nullptr, h_rows, p.linvt.get(), p.linvt_x3.get(), k, 1.0f, p.qbuf.get(),
+                nullptr);
     p.tbuf.alloc((size_t)nw_max * k);
     const float cw = (float)((1.0 + alpha) / alpha);
     launches += 1;
@@ -2128,9 +2244,8 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             L(st, p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, p.qbuf.get(), k,
               (float)alpha, p.tbuf.get(), nullptr);
         }
-        const int gw = (int)std::min<int64_t>((p.n_wood[g] + 31) / 32, 8192);
-        wrmf_rows_matmul_kernel<<<gw, 256, 0, st>>>(p.tbuf.get(), nullptr, p.n_wood[g],
-                                                    p.linv.get(), k, cw, W, p.wood[g].get());
+        rows_matmul(st, p.tbuf.get(), nullptr, p.n_wood[g], p.linv.get(), p.linv_x3.get(), k, cw,
+                    W, p.wood[g].get());
         MML_HIP(hipGetLastError());
         launches += 2;
     }
