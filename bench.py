@@ -719,7 +719,8 @@ def bench_wrmf(args):
                                    "residual 2nk^2 + 4 nnz k, 2k^2 per direct row (kept factor), "
                                    "a 3e-3 CG per Woodbury row; the CG rows run on the VALU; "
                                    "the direct rows' Grams run as six bf16 MFMA products per "
-                                   "f32 product (exact 3-way bf16 split), counted once",
+                                   "f32 product (exact 3-way bf16 split), counted once; so do the row GEMMs (Q = H L^-T, the "
+                                   "W rows, the refinement transforms)",
                      "refine_passes": passes,
                      "flops_direct_equivalent": flops_direct,
                      "direct_equivalent_tflops": flops_direct / (np.mean(ms) * 1e-3) / 1e12,
