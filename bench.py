@@ -8,9 +8,14 @@ BiasedMatrixFactorization.cs:264-310) over every rank's ratings, plus -- for N >
 RCCL all-reduce of item factors and item biases (model averaging).
 
 Workloads (BASELINE.json configs, synthetic data generated in HBM, inputs resident before timing):
-  N = 1 : C2 -- 1M users x 100k items, 100M ratings, k = 64 fp32.
+  N = 1 : C2 -- 1M users x 100k items, 100M ratings, k = 64 fp32 (the headline `value`), then the
+          other configurations as extra keys of the same line, each timed on HIP events with its
+          own roofline and CPU baseline: "c4_n1" (C4's 1B ratings, the data set of the N > 1 runs,
+          3 epochs), "c3" (BPRMF k=128, 2 epochs), "c5" (WRMF k=256 fp64 mode, 2 iterations);
+          --no-extras skips them.
   N > 1 : C4 strong scaling -- 1B ratings, 10M users x 100k items, user shards of equal rating
-          count (the same data set at every N; --workload c4 runs its N = 1 point).
+          count (the same data set at every N, so N / 1 compares with the line's c4_n1 at N = 1;
+          --workload c4 runs the N = 1 point alone).
 The line carries the roofline of the SGD kernel (algorithmic bytes 16k+28 per update)
 and the CPU oracle's Iterate() and MaxThreads = T DSGD, one full epoch each (rank 0, N = 1 only).
 """
@@ -79,23 +84,37 @@ def main():
                              "pair_replacement"],
                     help="C3 only: BPRMF's Iterate() variant (BPRMF.cs:160-268)")
     ap.add_argument("--workload", default=None, choices=["c2", "c3", "c4", "c5", "svdpp"],
-                    help="default: c2 at N = 1, c4 at N > 1 (BiasedMF k=64); c3: BPRMF k=128 "
-                         "(N > 1: user shards); c4: BiasedMF 1B ratings, strong scaling; "
-                         "c5: WRMF k=256")
+                    help="default: c2 at N = 1 (+ the c4_n1 / c3 / c5 keys), c4 at N > 1 "
+                         "(BiasedMF k=64); c3: BPRMF k=128 (N > 1: user shards); c4: BiasedMF 1B "
+                         "ratings, strong scaling; c5: WRMF k=256")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="N = 1 default run: the C2 line only (no c4_n1 / c3 / c5 keys)")
     args = ap.parse_args()
     world = env_rank()[0]
     workload = args.workload or ("c2" if world == 1 else "c4")
-    if workload == "c3":
-        return bench_bpr(args)
-    if workload == "c4":
-        return bench_c4(args)
-    if workload == "c5":
-        return bench_wrmf(args)
-    if workload == "svdpp":
-        return bench_svdpp(args)
-    if world > 1:
+    fn = {"c2": bench_c2, "c3": bench_bpr, "c4": bench_c4, "c5": bench_wrmf,
+          "svdpp": bench_svdpp}[workload]
+    if workload == "c2" and world > 1:
         raise SystemExit("C2 is the single-GPU configuration; N > 1 runs C4 (--workload c4)")
-    return bench_c2(args)
+    line = fn(args)
+    if workload == "c2" and args.workload is None and not args.no_extras:
+        # the other configurations on the same GPU, as keys of the one line (BASELINE.json
+        # configs 3-5; C4's N = 1 point is the denominator of the N > 1 strong-scaling runs)
+        for key, f, steps, warmup in (("c4_n1", bench_c4, 3, 1), ("c3", bench_bpr, 2, 1),
+                                      ("c5", bench_wrmf, 2, 1)):
+            sub = argparse.Namespace(**vars(args))
+            sub.steps, sub.warmup = steps, warmup
+            torch.cuda.empty_cache()
+            t0 = time.perf_counter()
+            x = f(sub)
+            x["wall_s"] = time.perf_counter() - t0
+            for drop in ("n_gpus", "higher_is_better", "vs_baseline", "data"):
+                x.pop(drop, None)
+            line[key] = x
+            print(f"{key}: {x['value']:.4g} {x['unit']} ({x['wall_s']:.0f} s)", file=sys.stderr,
+                  flush=True)
+    if line is not None:
+        print(json.dumps(line), flush=True)
 
 
 def bench_c2(args):
@@ -229,7 +248,7 @@ def bench_c2(args):
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "none",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (planted rank-8 model, Zipf(0.8) items, generated in HBM)",
@@ -247,11 +266,9 @@ def bench_c2(args):
                          "kernel_avg_ms": avg_kernel_ms, "bytes_per_update": bpu},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
     N.lib().mml_bmf_destroy(h)
     ctx.close()
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    return line
 
 
 def cpu_threads() -> int:
@@ -332,30 +349,40 @@ def cpu_baseline(h, k, n_users, n_items, gb, seconds, sample):
             **host, "single_thread": single}
 
 
+def cpu_baseline_dsgd(h, k, n_users, n_items, gb, sample, name):
+    """The oracle's MaxThreads = T DSGD epoch (BiasedMatrixFactorization.cs:205-215, blocks from
+    MultiCore.PartitionUsersAndItems) on T = this process's cores over a slice of the stream, from
+    the GPU model's current state (C4's CPU baseline on a 100M-rating slice)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    U = np.empty((n_users, k), np.float32)
+    V = np.empty((n_items, k), np.float32)
+    bu = np.empty(n_users, np.float32)
+    bi = np.empty(n_items, np.float32)
+    N.check(N.lib().mml_bmf_get_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
+                                      N.ptr(bu, N._f32p), N.ptr(bi, N._f32p)))
+    u, i, v = sample
+    n = len(u)
+    kw = dict(gb=np.float32(gb), min_rating=np.float32(1), range_=np.float32(4), lr=0.01)
+    T = cpu_threads()
+    rng = O.Rng(1)
+    blocks = O.partition_users_and_items(rng, u, i, n_users - 1, n_items - 1, T)
+    seq = rng.shuffle(np.arange(blocks[0], dtype=np.int32))
+    t0 = time.perf_counter()
+    O.bmf_dsgd_epoch_mt(u, i, v, blocks, seq, T, U, V, bu, bi, **kw)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "rating-updates/s", "cores": T, "kind": "port",
+            "sample": f"one DSGD epoch (MaxThreads={T}: {blocks[0]}x{blocks[0]} user x item blocks, "
+                      f"BiasedMatrixFactorization.cs:205-215) over a {n}-rating slice of the "
+                      f"{name} stream (its first ratings), k={k}, oracle C restatement on {T} "
+                      f"threads, {dt:.1f} s",
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(), "process_cpus": T}
+
+
 def c4_shard(rank, world, n_total, n_users, n_items, n_test, device, chunks=64):
-    """C4's data set as 64 user-range chunks (chunk c: users [c U/64, (c+1) U/64), n_total/64
-    ratings, seed 4000 + c; test ratings seed 5000 + c), so that the whole data set is the same
-    for every world size and rank r of N holds chunks [r 64/N, (r+1) 64/N): user shards of equal
-    rating count, disjoint users."""
-    from mymedialite_amd.synthetic import planted_ratings_torch
-    assert chunks % world == 0, "world size must divide 64"
-    per = n_total // chunks
-    mine = range(rank * chunks // world, (rank + 1) * chunks // world)
-    n_local = per * len(mine)
-    t_per = max(1, n_test // chunks)
-    out = [torch.empty(n_local, dtype=t, device=device)
-           for t in (torch.int32, torch.int32, torch.float32)]
-    test = [torch.empty(t_per * len(mine), dtype=t, device=device)
-            for t in (torch.int32, torch.int32, torch.float32)]
-    for x, c in enumerate(mine):
-        rng_ = (c * n_users // chunks, (c + 1) * n_users // chunks)
-        for dst, cnt, seed in ((out, per, 4000 + c), (test, t_per, 5000 + c)):
-            part = planted_ratings_torch(n_users, n_items, cnt, seed=seed, device=device,
-                                         user_range=rng_)
-            for d, p_ in zip(dst, part):
-                d[x * cnt:(x + 1) * cnt] = p_
-            del part
-    return out, test, (mine[0] * n_users // chunks, (mine[-1] + 1) * n_users // chunks)
+    """C4's data set as 64 seeded user-range chunks (synthetic.c4_chunks)."""
+    from mymedialite_amd.synthetic import c4_chunks
+    return c4_chunks(rank, world, n_total, n_users, n_items, n_test, device, chunks)
 
 
 def bench_c4(args):
@@ -397,6 +424,12 @@ def bench_c4(args):
     N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
                                             values.data_ptr(), n_local, None))
     ingest_s = time.perf_counter() - t0
+    # SURVEY 8(d)'s C4 CPU baseline: the oracle DSGD on this process's cores over a 100M-rating
+    # slice of the same stream (rank 0 at N = 1 only)
+    cpu_sample = None
+    if world == 1 and not args.no_cpu_baseline:
+        m = min(n_local, 100_000_000)
+        cpu_sample = (users[:m].cpu().numpy(), items[:m].cpu().numpy(), values[:m].cpu().numpy())
     del users, items, values
     torch.cuda.empty_cache()
     # InitModel on the device (640M normals at N = 1); rows of other ranks' users stay 0.  The
@@ -416,15 +449,12 @@ def bench_c4(args):
 
     rmse0 = evaluate()
     timing = np.zeros(2, np.float32)
-    ar_ms = []
 
     def step():
         N.check(N.lib().mml_bmf_iterate(h, lr, None))
         N.lib().mml_bmf_last_timing(h, N.ptr(timing, N._f32p))
-        if world > 1:
-            t1 = time.perf_counter()
+        if world > 1:  # stream-ordered ncclAvg: the next epoch's kernel queues behind it
             N.check(N.lib().mml_bmf_allreduce_items(h))
-            ar_ms.append((time.perf_counter() - t1) * 1e3)
 
     for _ in range(args.warmup):
         step()
@@ -432,7 +462,6 @@ def bench_c4(args):
         torch.distributed.barrier()
     torch.cuda.synchronize()
     kernel_ms = []
-    ar_ms.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -441,11 +470,17 @@ def bench_c4(args):
     if world > 1:
         torch.distributed.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
+    ar = np.zeros(1, np.float32)
+    N.check(N.lib().mml_bmf_last_allreduce_ms(h, N.ptr(ar, N._f32p)))
     rmse = evaluate()
     value = n_total * args.steps / elapsed
     avg_kernel_ms = float(np.mean(kernel_ms))
     bpu = bytes_per_update(k)
     achieved = n_local * bpu / (avg_kernel_ms * 1e-3) / 1e9
+    cpu = None
+    if cpu_sample is not None:
+        cpu = cpu_baseline_dsgd(h, k, n_users, n_items, gb, cpu_sample, "C4")
+    line = None
     if rank == 0:
         line = {
             "metric": "SGD rating-updates/sec + final RMSE, BiasedMF k=64 at 1/2/4/8 MI355X",
@@ -471,19 +506,21 @@ def bench_c4(args):
             "final_rmse": rmse,
             "initial_rmse": rmse0,
             "epochs_trained": args.warmup + args.steps,
-            "allreduce_ms": float(np.mean(ar_ms)) if ar_ms else None,
+            "allreduce_ms": float(ar[0]) if world > 1 else None,
+            "allreduce_note": "device time of the last step's ncclAvg all-reduce of V||b_i "
+                              "(HIP events around it on the library stream)" if world > 1 else None,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": f"bmf_sgd_hogwild_kernel<RMSE,{max(1, (k + 3) // 4)}>",
                          "kernel_avg_ms": avg_kernel_ms, "bytes_per_update": bpu,
                          "per": "GPU (rank 0's shard)"},
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
     N.lib().mml_bmf_destroy(h)
     ctx.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+    return line
 
 
 def c3_shard(rank, world, n_total, n_users, n_items, device, chunks=64):
@@ -549,15 +586,12 @@ def bench_bpr(args):
     torch.cuda.empty_cache()
     N.check(N.lib().mml_bpr_init_model(h, 2, 0.0, 0.1))  # same seed: V identical on every rank
     timing = np.zeros(2, np.float32)
-    ar_ms = []
 
     def step(seed):
         N.check(N.lib().mml_bpr_iterate(h, seed))
         N.lib().mml_bpr_last_timing(h, N.ptr(timing, N._f32p))
-        if world > 1:
-            t1 = time.perf_counter()
+        if world > 1:  # stream-ordered ncclAvg: the next epoch's kernels queue behind it
             N.check(N.lib().mml_bpr_allreduce_items(h))
-            ar_ms.append((time.perf_counter() - t1) * 1e3)
 
     for w in range(args.warmup):
         step(1000 + 97 * w + rank)
@@ -565,7 +599,6 @@ def bench_bpr(args):
     if world > 1:
         torch.distributed.barrier()
     ms, ums = [], []
-    ar_ms.clear()
     t0 = time.perf_counter()
     for st_ in range(args.steps):
         step(2000 + 97 * st_ + rank)
@@ -590,7 +623,7 @@ def bench_bpr(args):
         "value": n_total * args.steps / elapsed,
         "unit": "triple-updates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak",
+        "scaling": "strong" if world > 1 else "none",
         "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (users uniform, items Zipf(0.8), generated in HBM)",
         "config": {"workload": "C3: BPRMF 10M users x 1M items, 500M positives, k=128",
@@ -601,7 +634,6 @@ def bench_bpr(args):
                    "parallelism": f"user-shard x{world}" + (
                        ", per-epoch RCCL all-reduce of V||b" if world > 1 else ""),
                    "device_ingest_s": ingest_s},
-        "allreduce_ms": float(np.mean(ar_ms)) if ar_ms else None,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_note": traffic_note,
@@ -615,12 +647,11 @@ def bench_bpr(args):
                                   "update)"},
         "cpu_baseline": cpu,
     }
-    if rank == 0:
-        print(json.dumps(line), flush=True)
     N.lib().mml_bpr_destroy(h)
     ctx.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+    return line if rank == 0 else None
 
 
 def bench_wrmf(args):
@@ -694,7 +725,7 @@ def bench_wrmf(args):
         "metric": "WRMF iterations/sec, k=256 (C5)", "value": args.steps / elapsed,
         "unit": "iterations/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak",
+        "scaling": "strong" if world > 1 else "none",
         "vs_baseline": None,
         "dtype": ("f64 (fp32 MFMA row solves + one pass of iterative refinement with the residual "
                   "b - A x in fp64: the fp64 solution, 2e-7 of the oracle in the tests)"
@@ -733,10 +764,9 @@ def bench_wrmf(args):
     }
     if world > 1:
         line["config"]["parallelism"] = f"row shards x{world}, RCCL all-gather per half-step"
-    if rank == 0:
-        print(json.dumps(line), flush=True)
     N.lib().mml_wrmf_destroy(h)
     ctx.close()
+    return line if rank == 0 else None
 
 
 def wrmf_executed_flops(deg_u, deg_i, k, passes=0, nnz=0, alpha=1.0):
@@ -871,7 +901,7 @@ def bench_svdpp(args):
         "metric": "SVD++ rating-updates/sec, SVDPlusPlus k=64 Hogwild", "value": n * args.steps /
         elapsed, "unit": "rating-updates/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (planted rank-4 model, Zipf(0.8) items; host-generated)",
         "config": {"workload": f"SVDPlusPlus {n_users} users x {n_items} items, {n} ratings",
                    "num_factors": k, "mean_items_per_user": float(deg.mean()),
@@ -889,7 +919,7 @@ def bench_svdpp(args):
                      "bytes_per_epoch": total_bytes},
         "cpu_baseline": cpu,
     }
-    print(json.dumps(line), flush=True)
+    return line
 
 
 def cpu_baseline_bpr(k, seconds):

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 5
+#define MML_ABI_VERSION 6
 
 typedef int32_t mml_status;
 enum {
@@ -54,10 +54,14 @@ mml_status mml_ctx_destroy(mml_ctx* ctx);
  * ring: device d owns block rows [d G/n, (d+1) G/n), item groups move by peer copy to the device
  * whose rows visit them next, and the model equals the single-device DSGD model bit for bit
  * (G must be a multiple of n); mml_wrmf solves row shards and all-gathers them after each
- * half-step.  Each call returns when all devices have finished.  On such handles the ORDERED
- * schedule, the _device data setters and the sibling-model extras return MML_ERR_STATE.  A device
- * id may be listed more than once (several shards on one GPU, e.g. to test the ring on one
- * device); such a context has no communicator, so only the DSGD ring runs on it. */
+ * half-step.  Each call returns when all devices have finished.  mml_bmf's user shards also run
+ * the ORDERED schedule (ABI 6: each shard its own range in visit order, deterministic), and
+ * mml_bmf_set_data_device takes arrays on the first listed device and shards them there (ABI 6).
+ * The sibling-model extras return MML_ERR_STATE.  A device id may be listed more than once
+ * (several shards on one GPU, e.g. to emulate N devices on one): such a context has no
+ * communicator; mml_bmf then runs the shards one after another and averages V || item biases
+ * with peer copies and a device kernel (sum in shard order, then / N), the DSGD ring moves its
+ * groups by peer copy, and mml_bpr / mml_wrmf refuse it. */
 mml_status mml_ctx_create_multi(const int32_t* device_ids, int32_t n_devices, mml_ctx** out);
 /* RCCL communicator across processes (one rank per GPU): rank 0 creates the 128-byte id, the host
  * broadcasts it (e.g. torch.distributed / MPI), then every rank calls mml_ctx_comm_init. */
@@ -244,8 +248,13 @@ mml_status mml_bmf_last_timing(mml_bmf* h, float* out);
  * (:225-244) compares consecutive values on the host. */
 mml_status mml_bmf_objective(mml_bmf* h, double* out);
 /* Multi-GPU (user shards): in-place RCCL all-reduce of item factors and item
- * biases over the context's communicator, then scale by 1/nranks (model averaging). */
+ * biases over the context's communicator with ncclAvg (model averaging).  Stream-ordered (ABI 6):
+ * the call returns once the collective is enqueued; the next call on the handle runs after it. */
 mml_status mml_bmf_allreduce_items(mml_bmf* h);
+/* Device time of the last item average (ABI 6): mml_bmf_allreduce_items, or the average inside
+ * a multi-device mml_bmf_iterate (RCCL: the slowest shard; peer copies: the whole average).
+ * Waits for it to finish; 0 when none has run. */
+mml_status mml_bmf_last_allreduce_ms(mml_bmf* h, float* out);
 /* SocialMF.UserRelation (SocialMF.cs:50): rows [0, n_rows) of the user_connections
  * SparseBooleanMatrix as CSR (offsets[n_rows + 1], cols = the rows' HashSet enumeration order, no
  * duplicates within a row, ids < n_users); the library builds the Transpose() the batch step walks
@@ -385,7 +394,9 @@ mml_status mml_bpr_last_triples(mml_bpr* h, int32_t* users, int32_t* items, int3
 mml_status mml_bpr_auc(mml_bpr* h, const int32_t* candidates, int32_t n_candidates,
                        const int32_t* users, int32_t n_users, const int64_t* test_off,
                        const int32_t* test_items, double* out_auc);
-/* Multi-GPU (user shards): RCCL all-reduce of item factors + item biases, scaled by 1/nranks. */
+/* Multi-GPU (user shards): RCCL all-reduce of item factors + item biases with ncclAvg (model
+ * averaging), stream-ordered like mml_bmf_allreduce_items (ABI 6).  The WEIGHTED sampler is
+ * single-device only (its j draws follow the global item popularity). */
 mml_status mml_bpr_allreduce_items(mml_bpr* h);
 
 /* ------------------------------------------------------------------ WRMF */

@@ -119,6 +119,7 @@ SIGNATURES = {
     "mml_bmf_last_timing": (_st, [_vp, _f32p]),
     "mml_bmf_objective": (_st, [_vp, _f64p]),
     "mml_bmf_allreduce_items": (_st, [_vp]),
+    "mml_bmf_last_allreduce_ms": (_st, [_vp, _f32p]),
     "mml_bpr_create": (_st, [_vp, ctypes.POINTER(BprParams), ctypes.c_int32, ctypes.c_int32,
                              ctypes.POINTER(_vp)]),
     "mml_bpr_destroy": (_st, [_vp]),

@@ -879,10 +879,19 @@ __global__ __launch_bounds__(256) void check_order_kernel(const int32_t* __restr
         if (order[x] < 0 || order[x] >= n) atomicOr(bad, 1);
 }
 
-__global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ a, int64_t n, float f) {
+// the user shards' item average without a communicator: dst (shard 0's rows) <- (dst + the other
+// shards' copies staged at stage[p * stride], summed in shard order) / parts -- the left-to-right
+// float sum, then one correctly rounded division, as the in-process emulation computes it
+__global__ __launch_bounds__(256) void average_rows_kernel(float* __restrict__ dst,
+                                                           const float* __restrict__ stage,
+                                                           int64_t n, int64_t stride,
+                                                           int32_t parts) {
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
-         x += (int64_t)gridDim.x * blockDim.x)
-        a[x] *= f;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        float s = dst[x];
+        for (int32_t p = 0; p + 1 < parts; ++p) s += stage[(int64_t)p * stride + x];
+        dst[x] = s / (float)parts;
+    }
 }
 
 // packed[x] = M[ids[x]] (rows of ld floats) and packed_b[x] = b[ids[x]] (b may be null)
@@ -1351,6 +1360,12 @@ struct mml_bmf {
     mml::DeviceArray<int32_t> gi_ids;
     mml::DeviceArray<float> stage_v, stage_b;
     hipEvent_t ev_pack = nullptr;
+    // the item average after an epoch: RCCL (ncclAvg) on a communicator, else (a device listed
+    // more than once) the other shards' V || b_i staged on shard 0's device, averaged there and
+    // copied back; events around it time it (mml_bmf_last_allreduce_ms)
+    mml::DeviceArray<float> avg_stage;
+    hipEvent_t ev_ar0 = nullptr, ev_ar1 = nullptr;
+    bool has_ar = false;
 };
 
 namespace {
@@ -1556,7 +1571,7 @@ void ensure_xstream(mml_bmf* h) {
 // 5 = 1 + the flushing waves, 0 = one span over all XCDs (the round-1 kernel)
 static int hogwild_xcd_mode() {
     static const int m = [] {
-        const char* e = std::getenv("MML_HOGWILD_XCD");
+        const char* e = MML_EXPERIMENT_ENV("MML_HOGWILD_XCD");
         return e ? std::atoi(e) : 4;
     }();
     return m;
@@ -1573,7 +1588,7 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     // group g's ratings on the blocks b % 8 == g of one XCD, so a hot item's row lives in one L2
     // instead of 8 replicas whose write-backs overwrite each other's updates.
     static const int64_t min_chunk = [] {
-        const char* e = std::getenv("MML_HOGWILD_MIN_CHUNK");
+        const char* e = MML_EXPERIMENT_ENV("MML_HOGWILD_MIN_CHUNK");
         return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)12000;
     }();
     int64_t waves = std::min<int64_t>(256 * 32, std::max<int64_t>(1, n / min_chunk));
@@ -1703,7 +1718,7 @@ void asym_precompute(mml_bmf* h) {
 // MML_ASYM_CACHE: rows of a list kept in registers from the sum to the step at k <= 64 (0 / 32 /
 // 64, default 64); read per epoch so a test can switch it
 static int asym_cache_rows() {
-    const char* e = std::getenv("MML_ASYM_CACHE");
+    const char* e = MML_EXPERIMENT_ENV("MML_ASYM_CACHE");
     return e ? std::atoi(e) : 64;
 }
 
@@ -1717,7 +1732,7 @@ void asym_epoch(mml_bmf* h, const BmfScalars& s) {
         // ORDERED: one wavefront, the whole stream in order.  HOGWILD: a wavefront per >= 1,024
         // ratings (a rating reads and writes whole lists of implicit rows), at most 256 CUs x 32
         static const int64_t cap = [] {
-            const char* e = std::getenv("MML_ASYM_WAVES");
+            const char* e = MML_EXPERIMENT_ENV("MML_ASYM_WAVES");
             return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)256 * 32;
         }();
         int64_t waves = 1;
@@ -1821,12 +1836,9 @@ void multi_create(mml_ctx* ctx, const mml_bmf_params* params, int32_t n_users, i
                   mml_bmf* h) {
     MML_REQUIRE(params->model == MML_MF_BIASED || params->model == MML_MF_PLAIN,
                 "a multi-device context trains MML_MF_BIASED / MML_MF_PLAIN");
-    MML_REQUIRE(params->schedule == MML_SCHEDULE_HOGWILD ||
-                    params->schedule == MML_SCHEDULE_HOGWILD_COHERENT ||
-                    params->schedule == MML_SCHEDULE_DSGD,
-                "a multi-device context trains with the HOGWILD schedules (user shards) or DSGD "
-                "(the item-group ring)");
-    if (params->schedule != MML_SCHEDULE_DSGD) mml::require_comm(ctx);
+    MML_REQUIRE(params->schedule >= MML_SCHEDULE_ORDERED &&
+                    params->schedule <= MML_SCHEDULE_HOGWILD_COHERENT,
+                "unknown schedule");
     h->ctx = ctx;
     h->p = *params;
     h->n_users = n_users;
@@ -1842,6 +1854,7 @@ void multi_create(mml_ctx* ctx, const mml_bmf_params* params, int32_t n_users, i
 }
 
 bool multi_dsgd(const mml_bmf* h) { return h->p.schedule == MML_SCHEDULE_DSGD; }
+void dsgd_sync_all(mml_bmf* h);
 
 // a shard's frequency-regularisation / InitModel counts are the whole data set's
 mml_status upload_counts(mml_bmf* s, const std::vector<int32_t>& cu,
@@ -1875,6 +1888,9 @@ void multi_set_data(mml_bmf* h, const int32_t* users, const int32_t* items, cons
         ++h->cnt_i_host[items[x]];
     }
     if (multi_dsgd(h)) {  // dealt out by set_blocks (its indices address these raw arrays)
+        // the ring's shards hold diverged item groups: bring every device to the newest model
+        // before the groups are forgotten
+        if (h->has_model && h->G > 0) dsgd_sync_all(h);
         h->hu.assign(users, users + n);
         h->hi.assign(items, items + n);
         h->hr.assign(values, values + n);
@@ -1982,6 +1998,200 @@ void multi_get_model(mml_bmf* h, float* U, float* V, float* bu, float* bi) {
             MML_HIP(hipStreamSynchronize(s->ctx->stream));
         });
     });
+}
+
+// mml_bmf_set_data_device on a multi-device context: the arrays live on the context's first
+// device.  The counts, the user ranges of equal rating count and a stable partition of the
+// (visit-ordered) stream by owner run there; each shard then takes its contiguous part (a peer
+// copy when its device differs).  Equal to mml_bmf_set_data with the same arrays on the host.
+void multi_set_data_device(mml_bmf* h, const int32_t* users, const int32_t* items,
+                           const float* values, int64_t n, const int32_t* order) {
+    MML_REQUIRE(!multi_dsgd(h), "the DSGD ring takes host arrays (mml_bmf_set_data, then "
+                                "mml_bmf_set_blocks)");
+    const int32_t nd = (int32_t)h->shards.size();
+    mml_bmf* s0 = h->shards[0];
+    s0->ctx->activate();
+    hipStream_t st = s0->ctx->stream;
+    mml::DeviceArray<int32_t> cu, ci, bad;
+    cu.alloc(std::max<int32_t>(1, h->n_users));
+    ci.alloc(std::max<int32_t>(1, h->n_items));
+    bad.alloc(1);
+    MML_HIP(hipMemsetAsync(cu.get(), 0, sizeof(int32_t) * cu.count, st));
+    MML_HIP(hipMemsetAsync(ci.get(), 0, sizeof(int32_t) * ci.count, st));
+    MML_HIP(hipMemsetAsync(bad.get(), 0, sizeof(int32_t), st));
+    if (n > 0) {
+        count_kernel<<<grid_for(n), 256, 0, st>>>(users, items, n, h->n_users, h->n_items,
+                                                   cu.get(), ci.get(), bad.get());
+        if (order) check_order_kernel<<<grid_for(n), 256, 0, st>>>(order, n, n, bad.get());
+        MML_HIP(hipGetLastError());
+    }
+    int32_t flag = 0;
+    h->cnt_u_host.assign(h->n_users, 0);
+    h->cnt_i_host.assign(h->n_items, 0);
+    MML_HIP(hipMemcpyAsync(&flag, bad.get(), sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    if (h->n_users)
+        MML_HIP(hipMemcpyAsync(h->cnt_u_host.data(), cu.get(), sizeof(int32_t) * h->n_users,
+                               hipMemcpyDeviceToHost, st));
+    if (h->n_items)
+        MML_HIP(hipMemcpyAsync(h->cnt_i_host.data(), ci.get(), sizeof(int32_t) * h->n_items,
+                               hipMemcpyDeviceToHost, st));
+    MML_HIP(hipStreamSynchronize(st));
+    MML_REQUIRE(!flag, "rating user/item id or order index out of range");
+    h->has_data = false;
+    h->ub = mml::balanced_user_bounds_counts(
+        std::vector<int64_t>(h->cnt_u_host.begin(), h->cnt_u_host.end()), n, nd);
+    // the stream in visit order, partitioned stably by the owner of its user
+    mml::DeviceArray<int32_t> ou, oi, orr, pu, pi, pr;
+    const int32_t *su = users, *si = items;
+    const int32_t* sr = reinterpret_cast<const int32_t*>(values);
+    std::vector<int64_t> goff(nd + 1, 0);
+    goff[nd] = n;
+    if (n > 0 && order) {
+        ou.alloc(n);
+        oi.alloc(n);
+        orr.alloc(n);
+        gather_stream_kernel<<<grid_for(n), 256, 0, st>>>(users, items, values, order, n,
+                                                          ou.get(), oi.get(),
+                                                          reinterpret_cast<float*>(orr.get()));
+        MML_HIP(hipGetLastError());
+        su = ou.get();
+        si = oi.get();
+        sr = orr.get();
+    }
+    if (n > 0 && nd > 1) {
+        MML_REQUIRE(nd <= 8, "mml_bmf_set_data_device on a multi-device context shards over at "
+                             "most 8 devices (use mml_bmf_set_data)");
+        std::vector<uint8_t> table(h->n_users);
+        for (int32_t d = 0; d < nd; ++d)
+            for (int32_t u = h->ub[d]; u < h->ub[d + 1]; ++u) table[u] = (uint8_t)d;
+        mml::XcdSplit xs;
+        xs.set_table(st, table);
+        pu.alloc(n);
+        pi.alloc(n);
+        pr.alloc(n);
+        const int32_t* in[3] = {su, si, sr};
+        int32_t* out[3] = {pu.get(), pi.get(), pr.get()};
+        xs.partition(st, su, n, 3, in, out);
+        int64_t g[9];
+        MML_HIP(hipMemcpyAsync(g, xs.goff.get(), sizeof(g), hipMemcpyDeviceToHost, st));
+        MML_HIP(hipStreamSynchronize(st));
+        for (int32_t d = 0; d < nd; ++d) goff[d] = g[d];
+        ou.reset();
+        oi.reset();
+        orr.reset();
+        su = pu.get();
+        si = pi.get();
+        sr = pr.get();
+    }
+    MML_HIP(hipStreamSynchronize(st));
+    for (int32_t d = 0; d < nd; ++d) {
+        mml_bmf* s = h->shards[d];
+        const int64_t o = goff[d], m = goff[d + 1] - goff[d];
+        const int32_t* du = m ? su + o : nullptr;
+        const int32_t* di = m ? si + o : nullptr;
+        const float* dr = m ? reinterpret_cast<const float*>(sr) + o : nullptr;
+        mml::DeviceArray<int32_t> tu, ti, tr;  // the shard's part on its own device
+        if (m > 0 && s->ctx->device != s0->ctx->device) {
+            s->ctx->activate();
+            tu.alloc(m);
+            ti.alloc(m);
+            tr.alloc(m);
+            hipStream_t ss = s->ctx->stream;
+            MML_HIP(hipMemcpyPeerAsync(tu.get(), s->ctx->device, du, s0->ctx->device,
+                                       sizeof(int32_t) * m, ss));
+            MML_HIP(hipMemcpyPeerAsync(ti.get(), s->ctx->device, di, s0->ctx->device,
+                                       sizeof(int32_t) * m, ss));
+            MML_HIP(hipMemcpyPeerAsync(tr.get(), s->ctx->device, dr, s0->ctx->device,
+                                       sizeof(float) * m, ss));
+            MML_HIP(hipStreamSynchronize(ss));
+            du = tu.get();
+            di = ti.get();
+            dr = reinterpret_cast<const float*>(tr.get());
+        }
+        mml_status r = mml_bmf_set_data_device(s, du, di, dr, m, nullptr);
+        if (r == MML_OK) r = upload_counts(s, h->cnt_u_host, h->cnt_i_host);
+        if (r != MML_OK)
+            mml::fail(r, "device " + std::to_string(s->ctx->device) + ": " + mml_last_error());
+    }
+    h->n = n;
+    h->has_data = true;
+}
+
+// The item average of the user shards without a communicator (a device listed more than once):
+// the other shards' V || b_i are staged on shard 0's device (peer copies; device-local when the
+// device repeats), averaged there in shard order (average_rows_kernel) and copied back.  Every
+// shard's stream waits for the copies before its next call.  Equal bit for bit to the in-process
+// emulation (tests/test_dist.py): sum over the shards left to right, then / N.
+void multi_average_peer(mml_bmf* h) {
+    const int32_t nd = (int32_t)h->shards.size();
+    mml_bmf* s0 = h->shards[0];
+    s0->ctx->activate();
+    hipStream_t st = s0->ctx->stream;
+    const int64_t nv = (int64_t)h->n_items * s0->ld, ni = h->n_items, slot = nv + ni;
+    if (!h->ev_ar0) {
+        MML_HIP(hipEventCreate(&h->ev_ar0));
+        MML_HIP(hipEventCreate(&h->ev_ar1));
+    }
+    MML_HIP(hipEventRecord(h->ev_ar0, st));
+    if (nd > 1 && ni > 0) {
+        h->avg_stage.alloc((size_t)(nd - 1) * slot);
+        float* stage = h->avg_stage.get();
+        for (int32_t d = 1; d < nd; ++d) {
+            mml_bmf* s = h->shards[d];
+            float* dst = stage + (int64_t)(d - 1) * slot;
+            MML_HIP(hipMemcpyPeerAsync(dst, s0->ctx->device, s->V.get(), s->ctx->device,
+                                       sizeof(float) * nv, st));
+            MML_HIP(hipMemcpyPeerAsync(dst + nv, s0->ctx->device, s->bi.get(), s->ctx->device,
+                                       sizeof(float) * ni, st));
+        }
+        average_rows_kernel<<<grid_for(nv), 256, 0, st>>>(s0->V.get(), stage, nv, slot, nd);
+        average_rows_kernel<<<grid_for(ni), 256, 0, st>>>(s0->bi.get(), stage + nv, ni, slot, nd);
+        MML_HIP(hipGetLastError());
+        for (int32_t d = 1; d < nd; ++d) {
+            mml_bmf* s = h->shards[d];
+            MML_HIP(hipMemcpyPeerAsync(s->V.get(), s->ctx->device, s0->V.get(), s0->ctx->device,
+                                       sizeof(float) * nv, st));
+            MML_HIP(hipMemcpyPeerAsync(s->bi.get(), s->ctx->device, s0->bi.get(),
+                                       s0->ctx->device, sizeof(float) * ni, st));
+        }
+    }
+    MML_HIP(hipEventRecord(h->ev_ar1, st));
+    for (int32_t d = 1; d < nd; ++d) {
+        mml_bmf* s = h->shards[d];
+        s->ctx->activate();
+        MML_HIP(hipStreamWaitEvent(s->ctx->stream, h->ev_ar1, 0));
+    }
+    h->has_ar = true;
+}
+
+// One epoch of the user shards, then the item average.  Phase 1 runs every shard's epoch (one
+// after another when the devices repeat -- each shard then has the whole GPU, as it would have a
+// GPU of its own -- else one host thread per device); phase 2 averages V || b_i and runs only
+// after every shard succeeded, so no rank ever waits in a collective another one skipped.
+void multi_epoch(mml_bmf* h, float learn_rate) {
+    const int32_t nd = (int32_t)h->shards.size();
+    std::vector<float> ms(nd, 0.0f);
+    auto epoch = [&](int32_t d) {
+        const mml_status st = mml_bmf_iterate(h->shards[d], learn_rate, nullptr);
+        if (st == MML_OK) ms[d] = h->shards[d]->last_ms;
+        return st;
+    };
+    if (h->ctx->repeated) {
+        for (int32_t d = 0; d < nd; ++d) {
+            const mml_status st = epoch(d);
+            if (st != MML_OK) mml::fail(st, "shard " + std::to_string(d) + ": " + mml_last_error());
+        }
+    } else {
+        mml::on_devices(h->ctx, epoch);
+    }
+    if (h->ctx->repeated || !h->shards[0]->ctx->comm) {
+        multi_average_peer(h);
+    } else {
+        mml::on_devices(h->ctx, [&](int32_t d) { return mml_bmf_allreduce_items(h->shards[d]); });
+        h->has_ar = false;
+    }
+    h->last_ms = *std::max_element(ms.begin(), ms.end());
+    h->last_launches = h->shards[0]->last_launches;
 }
 
 // ---- DSGD ring (the reference's MaxThreads = G schedule, BiasedMatrixFactorization.cs:205-215,
@@ -2295,6 +2505,12 @@ extern "C" mml_status mml_bmf_destroy(mml_bmf* h) {
             return;
         }
         if (!h->shards.empty() || (h->ctx && h->ctx->multi())) {
+            if (h->ev_ar0 && !h->shards.empty() && h->shards[0]) {
+                (void)hipSetDevice(h->shards[0]->ctx->device);
+                (void)hipStreamSynchronize(h->shards[0]->ctx->stream);
+                (void)hipEventDestroy(h->ev_ar0);
+                (void)hipEventDestroy(h->ev_ar1);
+            }
             for (mml_bmf* s : h->shards)
                 if (s) mml_bmf_destroy(s);
             delete h;
@@ -2303,6 +2519,8 @@ extern "C" mml_status mml_bmf_destroy(mml_bmf* h) {
         (void)hipSetDevice(h->ctx->device);
         (void)hipStreamSynchronize(h->ctx->stream);
         if (h->ev_pack) (void)hipEventDestroy(h->ev_pack);
+        if (h->ev_ar0) (void)hipEventDestroy(h->ev_ar0);
+        if (h->ev_ar1) (void)hipEventDestroy(h->ev_ar1);
         delete h;
     });
 }
@@ -2344,9 +2562,9 @@ extern "C" mml_status mml_bmf_set_data_device(mml_bmf* h, const int32_t* users,
                                               int64_t n, const int32_t* order) {
     return guard([&] {
         check_handle(h);
-        single_device_only(h);
         MML_REQUIRE(n >= 0 && n <= INT32_MAX, "rating count out of range");
         MML_REQUIRE(n == 0 || (users && items && values), "null rating arrays");
+        if (h->ctx->multi()) return multi_set_data_device(h, users, items, values, n, order);
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         h->has_data = false;
@@ -2553,17 +2771,9 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
             }
             return;
         }
-        if (h->ctx->multi()) {  // every device's epoch, then the item all-reduce (its thread)
+        if (h->ctx->multi()) {  // every shard's epoch, then the item average
             MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
-            std::vector<float> ms(h->shards.size(), 0.0f);
-            mml::on_devices(h->ctx, [&](int32_t d) {
-                mml_status st = mml_bmf_iterate(h->shards[d], learn_rate, nullptr);
-                if (st == MML_OK) ms[d] = h->shards[d]->last_ms;
-                if (st == MML_OK) st = mml_bmf_allreduce_items(h->shards[d]);
-                return st;
-            });
-            h->last_ms = *std::max_element(ms.begin(), ms.end());
-            h->last_launches = h->shards[0]->last_launches;
+            multi_epoch(h, learn_rate);
             return;
         }
         MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
@@ -2761,19 +2971,49 @@ extern "C" mml_status mml_bmf_allreduce_items(mml_bmf* h) {
         MML_REQUIRE(!is_asym(h), "the asymmetric models' implicit factors are not averaged across ranks");
         c->activate();
         hipStream_t st = c->stream;
+        if (!h->ev_ar0) {
+            MML_HIP(hipEventCreate(&h->ev_ar0));
+            MML_HIP(hipEventCreate(&h->ev_ar1));
+        }
+        // model averaging inside the collective (ncclAvg); stream-ordered, no host wait: the next
+        // epoch's kernel and every download run on this stream after it
         const size_t nv = (size_t)h->n_items * h->ld;
+        MML_HIP(hipEventRecord(h->ev_ar0, st));
         MML_RCCL(ncclGroupStart());
-        MML_RCCL(ncclAllReduce(h->V.get(), h->V.get(), nv, ncclFloat, ncclSum, c->comm, st));
-        MML_RCCL(ncclAllReduce(h->bi.get(), h->bi.get(), (size_t)h->n_items, ncclFloat, ncclSum,
+        MML_RCCL(ncclAllReduce(h->V.get(), h->V.get(), nv, ncclFloat, ncclAvg, c->comm, st));
+        MML_RCCL(ncclAllReduce(h->bi.get(), h->bi.get(), (size_t)h->n_items, ncclFloat, ncclAvg,
                                c->comm, st));
         MML_RCCL(ncclGroupEnd());
-        if (c->nranks > 1) {
-            const float f = 1.0f / (float)c->nranks;
-            scale_kernel<<<grid_for((int64_t)nv), 256, 0, st>>>(h->V.get(), (int64_t)nv, f);
-            scale_kernel<<<grid_for(h->n_items), 256, 0, st>>>(h->bi.get(), h->n_items, f);
-            MML_HIP(hipGetLastError());
+        MML_HIP(hipEventRecord(h->ev_ar1, st));
+        h->has_ar = true;
+    });
+}
+
+extern "C" mml_status mml_bmf_last_allreduce_ms(mml_bmf* h, float* out) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(out, "out is null");
+        *out = 0.0f;
+        auto one = [](mml_bmf* x) {
+            if (!x->has_ar) return 0.0f;
+            x->ctx->activate();
+            float ms = 0.0f;
+            MML_HIP(hipEventSynchronize(x->ev_ar1));
+            MML_HIP(hipEventElapsedTime(&ms, x->ev_ar0, x->ev_ar1));
+            return ms;
+        };
+        if (h->ctx->multi()) {
+            if (h->has_ar) {  // the peer average, on shard 0's device
+                mml_bmf* s0 = h->shards[0];
+                s0->ctx->activate();
+                MML_HIP(hipEventSynchronize(h->ev_ar1));
+                MML_HIP(hipEventElapsedTime(out, h->ev_ar0, h->ev_ar1));
+                return;
+            }
+            for (mml_bmf* s : h->shards) *out = std::max(*out, one(s));
+            return;
         }
-        MML_HIP(hipStreamSynchronize(st));
+        *out = one(h);
     });
 }
 

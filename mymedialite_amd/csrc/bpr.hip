@@ -672,6 +672,10 @@ extern "C" mml_status mml_bpr_create(mml_ctx* ctx, const mml_bpr_params* params,
             mml::require_comm(ctx);
             MML_REQUIRE(params->schedule != MML_BPR_SCHEDULE_ORDERED,
                         "a multi-device context trains with the HOGWILD / AUTO schedules");
+            // WeightedBPRMF draws j by item popularity (WeightedBPRMF.cs:55-67); a shard holds
+            // only its users' events, so its popularity would be shard-local, not the reference's
+            MML_REQUIRE(params->sampler != MML_BPR_SAMPLER_WEIGHTED,
+                        "the WEIGHTED sampler (global item popularity) is single-device only");
             auto* h = new mml_bpr();
             h->ctx = ctx;
             h->p = *params;
@@ -1001,7 +1005,7 @@ void launch_apply_ordered(mml_bpr* h, const int32_t* tu, const int32_t* ti, cons
 // buffer resources of the L2-served loads)
 int weighted_streams(mml_bpr* h) {
     static const int env = [] {
-        const char* e = std::getenv("MML_BPR_WSTREAMS");
+        const char* e = MML_EXPERIMENT_ENV("MML_BPR_WSTREAMS");
         return e ? std::max(0, std::min(128, std::atoi(e))) / 4 * 4 : -1;
     }();
     const int v = env >= 0 ? env : 128;
@@ -1039,7 +1043,7 @@ struct BprXcdMode {
 };
 BprXcdMode bpr_xcd_mode(int sampler) {
     static const int env = [] {
-        const char* e = std::getenv("MML_BPR_XCD");
+        const char* e = MML_EXPERIMENT_ENV("MML_BPR_XCD");
         return e ? std::atoi(e) : -1;
     }();
     // WeightedBPRMF draws j by popularity: most j rows are hot rows of another XCD's group, so
@@ -1111,13 +1115,17 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
             const size_t nd = h->shards.size();
             std::vector<float> ms(nd, 0.0f), ums(nd, 0.0f);
+            // phase 1: every shard's epoch; phase 2 (only when all succeeded, so no rank waits in
+            // a collective another one skipped): the item average
             mml::on_devices(h->ctx, [&](int32_t d) {
-                mml_status st = mml_bpr_iterate(h->shards[d], seed + 0x9E3779B97F4A7C15ull * d);
+                const mml_status st =
+                    mml_bpr_iterate(h->shards[d], seed + 0x9E3779B97F4A7C15ull * d);
                 ms[d] = h->shards[d]->last_ms;
                 ums[d] = h->shards[d]->last_update_ms;
-                if (st == MML_OK) st = mml_bpr_allreduce_items(h->shards[d]);
                 return st;
             });
+            mml::on_devices(h->ctx,
+                            [&](int32_t d) { return mml_bpr_allreduce_items(h->shards[d]); });
             h->last_ms = *std::max_element(ms.begin(), ms.end());
             h->last_update_ms = *std::max_element(ums.begin(), ums.end());
             return;
@@ -1137,7 +1145,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         // runs 32 instead of 128 -- on the C3 replica the Hogwild AUC offset grows with the
         // triples in flight (+0.0037 at 32 waves, +0.0050 at 128, k = 128; profiles/r2_xcd/r2i_*)
         static const int64_t min_chunk = [] {
-            const char* e = std::getenv("MML_HOGWILD_MIN_CHUNK");
+            const char* e = MML_EXPERIMENT_ENV("MML_HOGWILD_MIN_CHUNK");
             return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)65536;
         }();
         int64_t waves = std::min<int64_t>(256 * 32, std::max<int64_t>(1, n / min_chunk));
@@ -1145,7 +1153,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         // workgroups on different XCDs would each cache the hot item rows and overwrite each
         // other's updates on write-back (bmf.hip launch_hogwild)
         static const int64_t small_waves = [] {
-            const char* e = std::getenv("MML_BPR_SMALL_WAVES");
+            const char* e = MML_EXPERIMENT_ENV("MML_BPR_SMALL_WAVES");
             return e ? std::max<int64_t>(1, std::min<int64_t>(4, std::atoll(e))) : (int64_t)4;
         }();
         if (waves < 16) waves = small_waves;
@@ -1158,7 +1166,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         const bool weighted = h->p.sampler == MML_BPR_SAMPLER_WEIGHTED;
         const bool user_repl = h->p.sampler == MML_BPR_SAMPLER_USER_REPLACEMENT;
         static const bool fused_env = [] {
-            const char* e = std::getenv("MML_BPR_FUSED");
+            const char* e = MML_EXPERIMENT_ENV("MML_BPR_FUSED");
             return e && std::atoi(e) > 0;
         }();
         // ORDERED (or AUTO on a small epoch): the sampled triples are applied in sample order by
@@ -1327,7 +1335,7 @@ extern "C" mml_status mml_bpr_last_triples(mml_bpr* h, int32_t* users, int32_t* 
         MML_REQUIRE(h && h->ctx, "null handle");
         bpr_single_device_only(h);
         MML_REQUIRE(h->has_triples, "no sampled epoch to report (run mml_bpr_iterate first; the "
-                                    "MML_BPR_FUSED epoch keeps no triples)");
+                                    "fused experiment epoch keeps no triples)");
         MML_REQUIRE(n == h->n_events && users && items && other_items,
                     "n must equal the epoch's sample count (Feedback.Count)");
         h->ctx->activate();
@@ -1426,13 +1434,6 @@ extern "C" mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const in
     });
 }
 
-__global__ __launch_bounds__(256) void bpr_scale_kernel(float* __restrict__ a, int64_t n,
-                                                        float f) {
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
-         x += (int64_t)gridDim.x * blockDim.x)
-        a[x] *= f;
-}
-
 extern "C" mml_status mml_bpr_allreduce_items(mml_bpr* h) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
@@ -1442,20 +1443,14 @@ extern "C" mml_status mml_bpr_allreduce_items(mml_bpr* h) {
         MML_REQUIRE(c->comm, "context has no communicator (mml_ctx_comm_init)");
         c->activate();
         hipStream_t st = c->stream;
+        // model averaging inside the collective (ncclAvg), stream-ordered: the next epoch's
+        // kernels and every download run on this stream after it
         const size_t nv = (size_t)h->n_items * h->ld;
         MML_RCCL(ncclGroupStart());
-        MML_RCCL(ncclAllReduce(h->V.get(), h->V.get(), nv, ncclFloat, ncclSum, c->comm, st));
+        MML_RCCL(ncclAllReduce(h->V.get(), h->V.get(), nv, ncclFloat, ncclAvg, c->comm, st));
         MML_RCCL(ncclAllReduce(h->bias.get(), h->bias.get(), (size_t)h->n_items, ncclFloat,
-                               ncclSum, c->comm, st));
+                               ncclAvg, c->comm, st));
         MML_RCCL(ncclGroupEnd());
-        if (c->nranks > 1) {
-            const float f = 1.0f / (float)c->nranks;
-            bpr_scale_kernel<<<grid_for((int64_t)nv), 256, 0, st>>>(h->V.get(), (int64_t)nv, f);
-            bpr_scale_kernel<<<grid_for(h->n_items), 256, 0, st>>>(h->bias.get(), h->n_items,
-                                                                    f);
-            MML_HIP(hipGetLastError());
-        }
-        MML_HIP(hipStreamSynchronize(st));
     });
 }
 

@@ -115,11 +115,11 @@ extern "C" mml_status mml_ctx_destroy(mml_ctx* ctx) {
 }
 
 namespace mml {
-std::vector<int32_t> balanced_user_bounds(const int32_t* users, int64_t n, int32_t n_users,
-                                          int32_t parts) {
+std::vector<int32_t> balanced_user_bounds_counts(const std::vector<int64_t>& count, int64_t n,
+                                                 int32_t parts) {
+    const int32_t n_users = (int32_t)count.size();
     std::vector<int64_t> c((size_t)n_users + 1, 0);
-    for (int64_t x = 0; x < n; ++x) c[(size_t)users[x] + 1]++;
-    for (int32_t u = 0; u < n_users; ++u) c[u + 1] += c[u];  // c[u] = ratings of users < u
+    for (int32_t u = 0; u < n_users; ++u) c[u + 1] = c[u] + count[u];  // c[u] = ratings of users < u
     std::vector<int32_t> b(parts + 1, n_users);
     b[0] = 0;
     for (int32_t r = 1; r < parts; ++r) {
@@ -130,6 +130,13 @@ std::vector<int32_t> balanced_user_bounds(const int32_t* users, int64_t n, int32
         b[r] = std::min(std::max(b[r], b[r - 1]), n_users);
     }
     return b;
+}
+
+std::vector<int32_t> balanced_user_bounds(const int32_t* users, int64_t n, int32_t n_users,
+                                          int32_t parts) {
+    std::vector<int64_t> c((size_t)n_users, 0);
+    for (int64_t x = 0; x < n; ++x) c[(size_t)users[x]]++;
+    return balanced_user_bounds_counts(c, n, parts);
 }
 }  // namespace mml
 

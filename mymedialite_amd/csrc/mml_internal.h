@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <exception>
 #include <new>
 #include <string>
@@ -15,6 +16,17 @@
 #include <vector>
 
 #include "mml.h"
+
+// Experiment switches (environment variables that select A/B variants of a kernel: MML_HOGWILD_XCD,
+// MML_WRMF_DEBUG, ...) exist only in a library built with -DMML_EXPERIMENTS
+// (scripts/build_variant.sh).  The release library never reads the environment: the macro drops
+// the variable's name, so a stray setting on a user's machine cannot select a slower or a
+// deliberately wrong path.
+#ifdef MML_EXPERIMENTS
+#define MML_EXPERIMENT_ENV(name) std::getenv(name)
+#else
+#define MML_EXPERIMENT_ENV(name) ((const char*)nullptr)
+#endif
 
 namespace mml {
 
@@ -172,6 +184,8 @@ struct XcdSplit {
     DeviceArray<int64_t> cnt, base;
     DeviceArray<uint8_t> tmp;
     void set_groups(hipStream_t st, const std::vector<int64_t>& weight, int32_t groups);
+    // an explicit group per key (< 8), e.g. the device that owns a user (multi-device set_data)
+    void set_table(hipStream_t st, const std::vector<uint8_t>& table);
     // out[c][...] = in[c][...] reordered by group(key[x]), stable; goff written on the device
     void partition(hipStream_t st, const int32_t* key, int64_t n, int32_t npay,
                    const int32_t* const* in, int32_t* const* out);
@@ -199,8 +213,9 @@ struct mml_ctx {
     // holding rank d of one ncclCommInitAll communicator; the fields below are sub[0]'s copies
     std::vector<mml_ctx*> sub;
     bool multi() const { return !sub.empty(); }
-    // a device id listed more than once (several shards on one GPU): no communicator is built, so
-    // only the schedules that move data with peer copies (BiasedMF DSGD) run on it
+    // a device id listed more than once (several shards on one GPU): no communicator is built;
+    // BiasedMF moves data with peer copies instead (the DSGD ring; the user shards' item
+    // averaging), the other handles refuse such a context
     bool repeated = false;
     int32_t device = 0;
     hipStream_t stream = nullptr;
@@ -245,6 +260,9 @@ inline void require_comm(const mml_ctx* ctx) {
 // distributed.balanced_user_shards's rule)
 std::vector<int32_t> balanced_user_bounds(const int32_t* users, int64_t n, int32_t n_users,
                                           int32_t parts);
+// the same from per-user rating counts (n = their sum)
+std::vector<int32_t> balanced_user_bounds_counts(const std::vector<int64_t>& count, int64_t n,
+                                                 int32_t parts);
 inline int32_t owner_of(const std::vector<int32_t>& b, int32_t u) {
     int32_t d = (int32_t)(std::upper_bound(b.begin(), b.end(), u) - b.begin()) - 1;
     return d < 0 ? 0 : (d >= (int32_t)b.size() - 1 ? (int32_t)b.size() - 2 : d);

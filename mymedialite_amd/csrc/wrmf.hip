@@ -555,7 +555,7 @@ namespace {
 // MML_WRMF_SOLVER=blocked keeps the LDS-packed fp32 solver for k > 128 (A/B measurements)
 bool use_blocked_solver() {
     static const bool v = [] {
-        const char* e = std::getenv("MML_WRMF_SOLVER");
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_SOLVER");
         return e && std::string(e) == "blocked";
     }();
     return v;
@@ -564,7 +564,7 @@ bool use_blocked_solver() {
 // MML_WRMF_WOODBURY=0 solves every row directly (A/B measurements of the Woodbury rows)
 bool no_woodbury() {
     static const bool v = [] {
-        const char* e = std::getenv("MML_WRMF_WOODBURY");
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOODBURY");
         return e && std::string(e) == "0";
     }();
     return v;

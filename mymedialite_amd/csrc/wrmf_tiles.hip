@@ -1524,7 +1524,7 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
 // the Woodbury rows by CG
 bool wood_cg() {
     static const bool v = [] {
-        const char* e = std::getenv("MML_WRMF_WOOD");
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOOD");
         return !(e && std::string(e) == "chol");
     }();
     return v;
@@ -1541,7 +1541,7 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
     // refinement CG 1e-4 -> 3e-3: 278 -> 254 ms per iteration).  max_it = the steps the
     // cond(C) <= 1 + alpha bound needs, + 4
     static const double refine_tol = [] {
-        const char* e = std::getenv("MML_WRMF_REFINE_TOL");
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_REFINE_TOL");
         return e ? std::atof(e) : 3e-3;
     }();
     const double tol = S ? refine_tol : 1e-6;
@@ -1707,7 +1707,7 @@ __global__ __launch_bounds__(256) void wrmf_rows_matmul_x3_kernel(
 // MFMA kernel with MML_WRMF_GEMM=f32 (A/B)
 bool gemm_f32() {
     static const bool v = [] {
-        const char* e = std::getenv("MML_WRMF_GEMM");
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_GEMM");
         return e && std::string(e) == "f32";
     }();
     return v;
@@ -1726,7 +1726,7 @@ void rows_matmul(hipStream_t st, const float* X, const int32_t* xrows, int64_t n
 // 1 diagonal factorisation, 2 panel MFMAs, 4 backward substitution, 8 Gram
 int debug_mask() {
     static const int v = [] {
-        const char* e = std::getenv("MML_WRMF_DEBUG");
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_DEBUG");
         return e ? std::atoi(e) : 0;
     }();
     return v;
@@ -2110,7 +2110,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
     if (rhs && p.keep_factor) {  // refinement: the kept factors, no Gram, no factorisation
         // one wave per row (default) or the 8-wave workgroup per row (MML_WRMF_RESOLVE=wg, A/B)
         static const bool wg = [] {
-            const char* e = std::getenv("MML_WRMF_RESOLVE");
+            const char* e = MML_EXPERIMENT_ENV("MML_WRMF_RESOLVE");
             return e && std::string(e) == "wg";
         }();
         auto resolve = [&](const int32_t* list, int64_t n, const float* Fl) {

@@ -119,7 +119,7 @@ namespace mml {
 
 int32_t flushers_per_xcd(int32_t dflt) {
     static const int32_t v = [] {
-        const char* e = std::getenv("MML_FLUSHERS");
+        const char* e = MML_EXPERIMENT_ENV("MML_FLUSHERS");
         return e ? std::max(1, std::atoi(e)) : 0;
     }();
     return v > 0 ? v : dflt;
@@ -127,7 +127,7 @@ int32_t flushers_per_xcd(int32_t dflt) {
 
 int32_t xcd_groups(mml_ctx* ctx) {
     if (ctx->xcd_groups > 0) return ctx->xcd_groups;
-    const char* e = std::getenv("MML_XCD_GROUPS");
+    const char* e = MML_EXPERIMENT_ENV("MML_XCD_GROUPS");
     if (e && std::atoi(e) <= 1) return ctx->xcd_groups = 1;
     constexpr int kBlocks = 2048;  // the Hogwild launches' grid size
     DeviceArray<int32_t> ids;
@@ -175,6 +175,16 @@ void XcdSplit::set_groups(hipStream_t st, const std::vector<int64_t>& weight, in
     group.alloc(std::max<size_t>(1, g.size()));
     if (!g.empty())
         MML_HIP(hipMemcpyAsync(group.get(), g.data(), g.size(), hipMemcpyHostToDevice, st));
+    goff.alloc(9);
+    MML_HIP(hipStreamSynchronize(st));
+}
+
+void XcdSplit::set_table(hipStream_t st, const std::vector<uint8_t>& table) {
+    ng = 8;
+    n_items = (int32_t)table.size();
+    group.alloc(std::max<size_t>(1, table.size()));
+    if (!table.empty())
+        MML_HIP(hipMemcpyAsync(group.get(), table.data(), table.size(), hipMemcpyHostToDevice, st));
     goff.alloc(9);
     MML_HIP(hipStreamSynchronize(st));
 }

@@ -93,3 +93,32 @@ def planted_ratings_torch(n_users: int, n_items: int, n: int, seed: int, device,
         items[s:e] = i.to(torch.int32)
         values[s:e] = sc.round().clamp_(1, 5)
     return users, items, values
+
+
+def c4_chunks(rank: int, world: int, n_total: int, n_users: int, n_items: int, n_test: int,
+              device, chunks: int = 64):
+    """C4's data set (BiasedMF k=64, 1B ratings, 10M users x 100k items, Zipf(0.8))
+    as 64 user-range chunks: chunk c holds users [c U/64, (c+1) U/64), n_total/64 training ratings
+    (seed 4000 + c) and n_test/64 test ratings (seed 5000 + c).  The whole set is the same for
+    every world size; rank r of N holds chunks [r 64/N, (r+1) 64/N), i.e. a user shard with 1/N of
+    the ratings.  Returns ((users, items, values), (test users, items, values), (u_lo, u_hi)) as
+    torch tensors on `device`."""
+    import torch
+    assert chunks % world == 0, "world size must divide 64"
+    per = n_total // chunks
+    mine = range(rank * chunks // world, (rank + 1) * chunks // world)
+    n_local = per * len(mine)
+    t_per = max(1, n_test // chunks)
+    out = [torch.empty(n_local, dtype=t, device=device)
+           for t in (torch.int32, torch.int32, torch.float32)]
+    test = [torch.empty(t_per * len(mine), dtype=t, device=device)
+            for t in (torch.int32, torch.int32, torch.float32)]
+    for x, c in enumerate(mine):
+        rng_ = (c * n_users // chunks, (c + 1) * n_users // chunks)
+        for dst, cnt, seed in ((out, per, 4000 + c), (test, t_per, 5000 + c)):
+            part = planted_ratings_torch(n_users, n_items, cnt, seed=seed, device=device,
+                                         user_range=rng_)
+            for d, p_ in zip(dst, part):
+                d[x * cnt:(x + 1) * cnt] = p_
+            del part
+    return out, test, (mine[0] * n_users // chunks, (mine[-1] + 1) * n_users // chunks)

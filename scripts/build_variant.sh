@@ -1,8 +1,10 @@
 #!/bin/bash
 # variants/NAME/libmml_hip.so: the library with extra compile flags (A/B experiments; load it
 # with MML_LIB_PATH=...).  Usage: scripts/build_variant.sh NAME "-DFLAG ..."
+# Every variant is an experiments build (-DMML_EXPERIMENTS): its MML_* environment switches
+# (MML_HOGWILD_XCD, MML_WRMF_DEBUG, ...) are live; the release library ignores them.
 set -e
-name=$1; flags=$2
+name=$1; flags="-DMML_EXPERIMENTS ${2:-}"
 root=$(cd "$(dirname "$0")/.." && pwd)
 out=$root/variants/$name  # not under build/: that is gpurun-ignored
 mkdir -p "$out"

@@ -200,20 +200,25 @@ def test_hogwild_statistical_parity_c2_shape():
     O.bmf_train(u, i, v, r.max_user_id + 1, r.max_item_id + 1, r.scale_min, r.scale_max, seed=1,
                 k=64, num_iter=2, callback=cb)
     res = {}
-    for sched in ("hogwild", "hogwild_coherent"):
-        m, _ = gpu_train(u, i, v, seed=1, k=64, num_iter=0, Schedule=sched)
+    for name, props in (("hogwild", dict(Schedule="hogwild")),
+                        ("hogwild_coherent", dict(Schedule="hogwild_coherent")),
+                        ("hogwild_multi1", dict(Schedule="hogwild", Gpus="0"))):
+        m, _ = gpu_train(u, i, v, seed=1, k=64, num_iter=0, **props)
         got = []
         for _ in range(2):
             m.iterate()
             got.append(m.evaluate(Ratings(tu, ti, tv))["RMSE"])
-        res[sched] = got
-    print(f"C2-shape RMSE {res} oracle {ref}")
-    # Hogwild on XCD-owned item groups (xcd.hip; every item row cached in ONE XCD's L2): 2e-3
-    # (measured 1.0e-3 / 1.5e-3 after epochs 1 / 2; the round-1 spread over all XCDs, whose L2s
-    # held replicas of the hot rows, measured 1.0e-2 / 8e-3: MML_HOGWILD_XCD=0)
-    assert all(abs(a - b) <= 2e-3 for a, b in zip(res["hogwild"], ref)), (res, ref)
-    # coherent Hogwild: only in-flight staleness remains -> 2e-3 (measured ~3e-4)
-    assert all(abs(a - b) <= 2e-3 for a, b in zip(res["hogwild_coherent"], ref)), (res, ref)
+        res[name] = got
+    for name, got in res.items():
+        print(f"C2-shape test RMSE {name}: {got[0]:.6f} / {got[1]:.6f} vs oracle "
+              f"{ref[0]:.6f} / {ref[1]:.6f}: delta {got[0] - ref[0]:+.2e} / {got[1] - ref[1]:+.2e}")
+    # Hogwild on XCD-owned item groups (xcd.hip; every item row cached in ONE XCD's L2, users
+    # written through, one flushing wave per XCD; DESIGN.md section 3 measured 3.0e-4 / 2.5e-4;
+    # the round-1 spread over all XCDs, whose L2s held replicas of the hot rows, 1.0e-2 / 8e-3);
+    # the same kernel behind a one-shard multi-device context (Gpus=0, the user-shard path with
+    # its 1-rank ncclAvg) and the coherent schedule (only in-flight staleness, ~3e-4) -> 1e-3
+    for name, got in res.items():
+        assert all(abs(a - b) <= 1e-3 for a, b in zip(got, ref)), (name, res, ref)
 
 
 def test_dsgd_many_groups_exact():

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert set(declared) == set(N.SIGNATURES), set(declared) ^ set(N.SIGNATURES)
-    assert L.mml_abi_version() == 5
+    assert L.mml_abi_version() == 6
 
 
 def test_no_device_is_an_error_not_a_crash():
@@ -349,3 +349,22 @@ def test_binary_cache_like_file_serializer(tmp_path):
     q.write_text("5 6\n")
     f2 = read_items(str(q), binary_cache=True)
     np.testing.assert_array_equal(f1.users, f2.users)
+
+
+def test_release_library_ignores_experiment_switches():
+    """the A/B switches (MML_WRMF_DEBUG -- which skips solve phases and gives wrong
+    results --, MML_HOGWILD_XCD, MML_BPR_XCD, ...) exist only in a -DMML_EXPERIMENTS build
+    (scripts/build_variant.sh).  The release library drops their names at compile time, so no
+    environment setting can reach them: none of the names is in the shared object."""
+    from mymedialite_amd import _native as N
+    data = open(N.LIB_PATH, "rb").read()
+    for name in ("MML_WRMF_DEBUG", "MML_HOGWILD_XCD", "MML_BPR_XCD", "MML_BPR_FUSED",
+                 "MML_WRMF_GEMM", "MML_WRMF_WOOD", "MML_WRMF_RESOLVE", "MML_HOGWILD_MIN_CHUNK",
+                 "MML_ASYM_CACHE", "MML_FLUSHERS", "MML_XCD_GROUPS", "MML_WRMF_SOLVER",
+                 "MML_WRMF_REFINE_TOL", "MML_BPR_WSTREAMS"):
+        assert name.encode() not in data, name
+    src = os.path.join(os.path.dirname(N.LIB_PATH), "..", "csrc")
+    for f in os.listdir(src):
+        if f.endswith((".hip", ".cpp", ".h")):
+            text = open(os.path.join(src, f)).read()
+            assert "std::getenv(" not in text.replace("std::getenv(name)", ""), f

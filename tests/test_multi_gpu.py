@@ -3,8 +3,10 @@
 The box has one GPU, so the collectives run on 1-rank communicators: the RCCL calls inside
 mml_bmf_allreduce_items / mml_bpr_allreduce_items / the WRMF row all-gather execute (an all-reduce
 over one rank is the identity), and the one-process multi-device handles (mml_ctx_create_multi,
-``Gpus=0``) run their shard / route / gather logic over one shard.  The N > 1 decompositions are
-covered by the gloo tests in tests/test_dist.py and run on 8 GPUs in the driver's scaling bench.
+``Gpus=0``) run their shard / route / gather logic over one shard.  N > 1 BiasedMF user shards run
+here too, on a context that lists the GPU N times (``Gpus=0,0,...``): the shards train one after
+another and the library averages V || b_i by peer copy and a device kernel -- the same
+decomposition as bench.py's N-GPU run, with the averaging arithmetic inside libmml_hip.so.
 """
 import ctypes
 
@@ -120,11 +122,17 @@ def test_bmf_multi_device_context_one_shard():
     qu = np.concatenate([tu[:500], [2500]]).astype(np.int32)  # + an unknown user
     qi = np.concatenate([ti[:500], [3]]).astype(np.int32)
     np.testing.assert_array_equal(m.predict(qu, qi), q.predict(qu, qi))
-    # the exact schedules are single-device only
-    with pytest.raises(N.MMLError, match="HOGWILD"):
-        m2 = BiasedMatrixFactorization(NumFactors=4, NumIter=1, Schedule="ordered", Gpus="0")
-        m2.ratings = Ratings(u, i, v)
+    # ORDERED over one shard is the single-device ORDERED epoch (and the 1-rank ncclAvg is the
+    # identity): the models are equal bit for bit
+    got = {}
+    for name, props in (("single", dict(Device=0)), ("multi", dict(Gpus="0"))):
+        Random.set_seed(4)
+        m2 = BiasedMatrixFactorization(NumFactors=8, NumIter=2, Schedule="ordered", **props)
+        m2.ratings = Ratings(u[:20000], i[:20000], v[:20000])
         m2.train()
+        got[name] = m2.get_model()
+    for key in ("U", "V", "bu", "bi"):
+        np.testing.assert_array_equal(got["multi"][key], got["single"][key])
 
 
 def test_bpr_multi_device_context_one_shard():
@@ -199,13 +207,9 @@ def test_bmf_dsgd_ring_matches_oracle():
 
 
 def test_repeated_device_context_limits():
-    """A context listing a device twice has no communicator: the Hogwild user shards (which
-    average through RCCL) refuse it, and the ring needs MaxThreads divisible by the devices."""
+    """A context listing a device twice has no communicator: BPR's user shards (which average
+    through RCCL) refuse it, and the ring needs MaxThreads divisible by the devices."""
     u, i, v = synth_ratings(5, 200, 90, 4000)
-    with pytest.raises(N.MMLError, match="communicator"):
-        m = BiasedMatrixFactorization(NumFactors=4, NumIter=1, Schedule="hogwild", Gpus="0,0")
-        m.ratings = Ratings(u, i, v)
-        m.train()
     with pytest.raises(N.MMLError, match="communicator"):
         tr_u, tr_i, _, _ = planted_feedback(2, 300, 60, 8)
         b = BPRMF(NumFactors=4, NumIter=1, Gpus="0,0")
@@ -215,3 +219,162 @@ def test_repeated_device_context_limits():
         m = BiasedMatrixFactorization(NumFactors=4, NumIter=1, MaxThreads=5, Gpus="0,0")
         m.ratings = Ratings(u, i, v)
         m.train()
+
+
+def _emulate_user_shards(u, i, v, bnd, U, V, bu, bi, epochs, kw, snaps):
+    """The N-shard decomposition in one process with the oracle (tests/test_dist.py): every shard
+    runs its users' ratings in visit order from the same item side, then V || b_i = (sum of the
+    shards' copies, left to right) / N."""
+    nd = len(bnd) - 1
+    shards = [(u[(u >= bnd[x]) & (u < bnd[x + 1])], i[(u >= bnd[x]) & (u < bnd[x + 1])],
+               v[(u >= bnd[x]) & (u < bnd[x + 1])]) for x in range(nd)]
+    for _ in range(epochs):
+        Vs, bis = [], []
+        for su, si, sv in shards:
+            Vx, bix = V.copy(), bi.copy()
+            O.bmf_iterate(su, si, sv, np.arange(len(su), dtype=np.int32), U, Vx, bu, bix, **kw)
+            Vs.append(Vx)
+            bis.append(bix)
+        V = Vs[0].copy()
+        bi = bis[0].copy()
+        for x in range(1, nd):
+            V += Vs[x]
+            bi += bis[x]
+        V = (V / np.float32(nd)).astype(np.float32)
+        bi = (bi / np.float32(nd)).astype(np.float32)
+        snaps.append(dict(U=U.copy(), V=V.copy(), bu=bu.copy(), bi=bi.copy()))
+    return U, V, bu, bi
+
+
+@pytest.mark.parametrize("ndev,loss,freq", [(2, "RMSE", False), (4, "RMSE", True),
+                                            (3, "MAE", False)])
+def test_bmf_user_shards_ordered_equal_emulation(ndev, loss, freq):
+    """SURVEY 8(e)'s user shards + item averaging inside libmml_hip.so, on N shards of one GPU
+    (``Gpus=0,0,...``: a context listing the device N times) with the ORDERED schedule per shard:
+    after every epoch U, V and both biases equal the in-process emulation with the oracle
+    (tests/test_dist.py's decomposition) bit for bit -- shard bounds, the visit order within a
+    shard, the per-shard epoch and the averaging arithmetic (sum in shard order, then / N) all
+    match.  Reference: BiasedMatrixFactorization.cs:205-215 and :264-310, MultiCore.cs:43-73."""
+    from mymedialite_amd.distributed import balanced_user_shards
+    from test_bmf_gpu import gpu_train
+    u, i, v = synth_ratings(61, 700, 260, 30000)
+    tu, ti, tv = synth_ratings(62, 700, 260, 3000)
+    k, epochs = 12, 3
+    m, snaps = gpu_train(u, i, v, seed=21, k=k, num_iter=epochs, snapshots=True,
+                         Schedule="ordered", Gpus=",".join(["0"] * ndev), Loss=loss,
+                         FrequencyRegularization=freq)
+    r = Ratings(u, i, v)
+    nu, ni = r.max_user_id + 1, r.max_item_id + 1
+    rng = O.Rng(21)  # InitModel draws, then the RandomIndex shuffle (first Iterate)
+    U = rng.fill_normal(nu * k, 0, 0.1).reshape(nu, k)
+    V = rng.fill_normal(ni * k, 0, 0.1).reshape(ni, k)
+    cu, ci = np.bincount(u, minlength=nu), np.bincount(i, minlength=ni)
+    U[cu == 0] = 0
+    V[ci == 0] = 0
+    order = rng.shuffle(np.arange(len(u), dtype=np.int32))
+    bu, bi = np.zeros(nu, np.float32), np.zeros(ni, np.float32)
+    np.testing.assert_array_equal(snaps[0]["U"], U)
+    np.testing.assert_array_equal(snaps[0]["V"], V)
+    gb = np.float32(m.global_bias)
+    assert gb == O.global_bias(v, r.scale_min, r.scale_max)
+    kw = dict(gb=gb, min_rating=np.float32(r.scale_min),
+              range_=np.float32(r.scale_max - r.scale_min), lr=np.float32(0.01),
+              loss={"RMSE": 0, "MAE": 1}[loss], freq_reg=freq,
+              count_by_user=cu.astype(np.int32), count_by_item=ci.astype(np.int32))
+    bnd = balanced_user_shards(cu, ndev)
+    assert np.all(np.diff(bnd) > 0)
+    emu = []
+    _emulate_user_shards(u[order], i[order], v[order], bnd, U, V, bu, bi, epochs, kw, emu)
+    for e in range(epochs):
+        for key in ("U", "V", "bu", "bi"):
+            np.testing.assert_array_equal(snaps[e + 1][key], emu[e][key],
+                                          err_msg=f"epoch {e + 1} {key}")
+    # Predict / Evaluate route each user to its shard, whose item side is the averaged one
+    last = emu[-1]
+    p = O.bmf_predict(tu, ti, last["U"], last["V"], last["bu"], last["bi"], gb,
+                      np.float32(r.scale_min), np.float32(r.scale_max - r.scale_min))
+    np.testing.assert_allclose(m.predict(tu, ti), p, rtol=0, atol=1e-6)
+    assert abs(m.evaluate(Ratings(tu, ti, tv))["RMSE"] - O.rating_eval(p, tv)[0]) <= 1e-6
+
+
+def test_bmf_user_shards_device_data_equals_host_data():
+    """mml_bmf_set_data_device on a 4-shard context (arrays in HBM, partitioned by owner on the
+    device) trains exactly like mml_bmf_set_data with the same arrays on the host (ORDERED)."""
+    import torch
+    u, i, v = synth_ratings(63, 900, 300, 40000)
+    out = []
+    for dev_data in (False, True):
+        ctx = N.Context([0, 0, 0, 0])
+        p = N.BmfParams(8, N.LOSS_RMSE, 0, N.SCHEDULE_ORDERED, 1.0, 0.01, 0.015, 0.015)
+        h = N._vp()
+        N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(p), 900, 300, ctypes.byref(h)))
+        if dev_data:
+            tu_, ti_, tv_ = (torch.from_numpy(a).cuda() for a in (u, i, v))
+            N.check(N.lib().mml_bmf_set_data_device(h, tu_.data_ptr(), ti_.data_ptr(),
+                                                    tv_.data_ptr(), len(u), None))
+        else:
+            N.check(N.lib().mml_bmf_set_data(h, N.ptr(u, N._i32p), N.ptr(i, N._i32p),
+                                             N.ptr(v, N._f32p), len(u), None))
+        N.check(N.lib().mml_bmf_init_model(h, 9, 0.0, 0.1, 0.3, 1.0, 5.0))
+        for _ in range(2):
+            N.check(N.lib().mml_bmf_iterate(h, 0.01, None))
+        ms = np.zeros(1, np.float32)
+        N.check(N.lib().mml_bmf_last_allreduce_ms(h, N.ptr(ms, N._f32p)))
+        assert ms[0] > 0
+        got = [np.zeros(s_, np.float32) for s_ in (900 * 8, 300 * 8, 900, 300)]
+        N.check(N.lib().mml_bmf_get_model(h, *[N.ptr(a, N._f32p) for a in got]))
+        out.append(got)
+        N.lib().mml_bmf_destroy(h)
+        ctx.close()
+    for a, b in zip(*out):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_c4_model_averaging_cost_on_hip():
+    """the full C4 set (1B ratings, 10M users x 100k items, the 64 seeded chunks of
+    bench.py) trained 3 epochs by one handle (N = 1) and by 8 user shards on one GPU (the N = 8
+    decomposition emulated: each shard trains its eighth with the whole GPU, then the library
+    averages V || b_i), both from the same device InitModel.  Prints and bounds the test-RMSE cost
+    of 8-way averaging at C4 scale."""
+    import time
+    import torch
+    from mymedialite_amd.synthetic import c4_chunks
+    dev = torch.device("cuda:0")
+    n_total, nu, ni, k = 1_000_000_000, 10_000_000, 100_000, 64
+    (users, items, values), (tu, ti, tv), _ = c4_chunks(0, 1, n_total, nu, ni, 1_000_000, dev)
+    mean = float(values.double().mean().item())
+    avg = np.float32((np.float32(mean) - np.float32(1.0)) / np.float32(4.0))
+    gb = float(np.float32(np.log(avg / (1 - avg))))
+    tus, tis, tvs = tu.cpu().numpy(), ti.cpu().numpy(), tv.cpu().numpy()
+    res = {}
+    for nd in (1, 8):
+        ctx = N.Context(0 if nd == 1 else [0] * nd)
+        p = N.BmfParams(k, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
+        h = N._vp()
+        N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(p), nu, ni, ctypes.byref(h)))
+        N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
+                                                values.data_ptr(), n_total, None))
+        N.check(N.lib().mml_bmf_init_model(h, 4, 0.0, 0.1, gb, 1.0, 5.0))
+        rm, ep_ms, ar_ms = [], [], []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            N.check(N.lib().mml_bmf_iterate(h, 0.01, None))
+            ep_ms.append((time.perf_counter() - t0) * 1e3)
+            if nd > 1:
+                x = np.zeros(1, np.float32)
+                N.check(N.lib().mml_bmf_last_allreduce_ms(h, N.ptr(x, N._f32p)))
+                ar_ms.append(float(x[0]))
+            out = np.zeros(2, np.float32)
+            N.check(N.lib().mml_bmf_evaluate(h, N.ptr(tus, N._i32p), N.ptr(tis, N._i32p),
+                                             N.ptr(tvs, N._f32p), len(tus), N.ptr(out, N._f32p)))
+            rm.append(float(out[0]))
+        res[nd] = rm
+        print(f"C4 N={nd}: test RMSE per epoch {rm}, host ms per epoch {ep_ms}, average ms {ar_ms}")
+        N.lib().mml_bmf_destroy(h)
+        ctx.close()
+        torch.cuda.empty_cache()
+    d = [b - a for a, b in zip(res[1], res[8])]
+    print(f"C4 RMSE cost of 8-way averaging per epoch: {d}")
+    assert all(r < 0.76 for r in res[8])  # both learn (initial test RMSE 0.757)
+    assert res[8][-1] < res[8][0] and res[1][-1] < res[1][0]
+    assert all(x < 0.05 for x in d), d
