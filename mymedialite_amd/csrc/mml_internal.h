@@ -148,13 +148,20 @@ struct WrmfTilePlan {
     int64_t r0 = 0, r1 = 0;
     DeviceArray<uint8_t> rsegs, rmulti;
     int64_t n_rsegs = 0, n_rmulti = 0, n_rslots = 0;
-    DeviceArray<double> rpartial, x64, r64;
-    DeviceArray<float> rf, df;
     void* blas = nullptr;
     // fp64 mode: the direct rows keep their factor tiles (L_IJ, T_J = L_JJ^{-1}; light rows, then
-    // heavy ones) so a refinement pass is two triangular solves (wrmf_tile_resolve_kernel)
+    // heavy ones) so a refinement pass is two triangular solves (wrmf_tile_resolve_kernel).  Set
+    // per half-step: false when the tiles do not fit the free HBM (the refinement then
+    // refactors each row instead).
     bool keep_factor = false;
-    DeviceArray<float> factor;
+    // the refinement's buffers (factor tiles, x and r in fp64, residual / correction rows): only
+    // needed inside one half-step, so both plans of a handle point at ONE workspace (ws)
+    struct Refine {
+        DeviceArray<double> rpartial, x64, r64;
+        DeviceArray<float> rf, df, factor;
+    };
+    Refine own;
+    Refine* ws = &own;
     WrmfTilePlan() = default;
     WrmfTilePlan(const WrmfTilePlan&) = delete;
     WrmfTilePlan& operator=(const WrmfTilePlan&) = delete;

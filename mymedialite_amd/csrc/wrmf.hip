@@ -647,6 +647,8 @@ void ensure_shards(mml_wrmf* h) {
     h->ub = mml::balanced_rows(h->udeg, h->k, nr);
     h->ib = mml::balanced_rows(h->ideg, h->k, nr);
     if (h->k > 128) {
+        // the half-steps run one after another on one stream: one refinement workspace for both
+        h->iplan.ws = &h->uplan.own;
         const bool wood = h->p.alpha > 0.0 && !no_woodbury();
         mml::wrmf_tile_plan(h->udeg, h->ctx->stream, h->uplan, h->ub[rk], h->ub[rk + 1], wood);
         mml::wrmf_tile_plan(h->ideg, h->ctx->stream, h->iplan, h->ib[rk], h->ib[rk + 1], wood);

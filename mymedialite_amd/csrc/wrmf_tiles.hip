@@ -2025,42 +2025,42 @@ void wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H,
     auto bh = reinterpret_cast<rocblas_handle>(p.blas);
     if (rocblas_set_stream(bh, st) != rocblas_status_success)
         fail(MML_ERR_HIP, "rocblas_set_stream failed");
-    p.x64.alloc((size_t)n * k);
-    p.r64.alloc((size_t)n * k);
-    p.rf.alloc((size_t)n_w * k);
-    p.df.alloc((size_t)n_w * k);
-    p.rpartial.alloc(std::max<int64_t>(1, p.n_rslots) * (size_t)k);
+    p.ws->x64.alloc((size_t)n * k);
+    p.ws->r64.alloc((size_t)n * k);
+    p.ws->rf.alloc((size_t)n_w * k);
+    p.ws->df.alloc((size_t)n_w * k);
+    p.ws->rpartial.alloc(std::max<int64_t>(1, p.n_rslots) * (size_t)k);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n * k + 255) / 256, 16384));
     auto rows = [&](int op) {
-        wrmf_refine_rows_kernel<<<grid, 256, 0, st>>>(op, p.r0, n, k, W, p.x64.get(), p.r64.get(),
-                                                      p.rf.get(), p.df.get());
+        wrmf_refine_rows_kernel<<<grid, 256, 0, st>>>(op, p.r0, n, k, W, p.ws->x64.get(), p.ws->r64.get(),
+                                                      p.ws->rf.get(), p.ws->df.get());
         ++launches;
     };
     rows(0);
     const double m1 = -1.0, mreg = -reg;
     for (int32_t pass = 0; pass < passes; ++pass) {
         // R = -(HH + reg I) X, then + sum_i c_i h_i per row
-        MML_HIP(hipMemcpyAsync(p.r64.get(), p.x64.get(), sizeof(double) * n * k,
+        MML_HIP(hipMemcpyAsync(p.ws->r64.get(), p.ws->x64.get(), sizeof(double) * n * k,
                                hipMemcpyDeviceToDevice, st));
         if (rocblas_dgemm(bh, rocblas_operation_none, rocblas_operation_none, k, (rocblas_int)n, k,
-                          &m1, HH, k, p.x64.get(), k, &mreg, p.r64.get(), k) !=
+                          &m1, HH, k, p.ws->x64.get(), k, &mreg, p.ws->r64.get(), k) !=
             rocblas_status_success)
             fail(MML_ERR_HIP, "rocblas_dgemm failed");
         if (p.n_rsegs > 0) {
             const int gs = (int)std::min<int64_t>((p.n_rsegs + 3) / 4, 8192);  // 4 waves
             wrmf_resid_seg_kernel<<<gs, 256, 0, st>>>(
-                reinterpret_cast<const RSeg*>(p.rsegs.get()), p.n_rsegs, cols, H, k, p.x64.get(),
-                alpha, p.r64.get(), p.rpartial.get());
+                reinterpret_cast<const RSeg*>(p.rsegs.get()), p.n_rsegs, cols, H, k, p.ws->x64.get(),
+                alpha, p.ws->r64.get(), p.ws->rpartial.get());
         }
         if (p.n_rmulti > 0)
             wrmf_resid_multi_kernel<<<(int)std::min<int64_t>(p.n_rmulti, 8192), 256, 0, st>>>(
-                reinterpret_cast<const RMulti*>(p.rmulti.get()), p.n_rmulti, k, p.rpartial.get(),
-                p.r64.get());
+                reinterpret_cast<const RMulti*>(p.rmulti.get()), p.n_rmulti, k, p.ws->rpartial.get(),
+                p.ws->r64.get());
         MML_HIP(hipGetLastError());
         rows(1);
         // D = A^{-1} R on the fp32 solver (rows outside [r0, r1) are not read)
-        wrmf_tile_solve(st, p, p.df.get(), H, h_rows, off, cols, HH, k, alpha, reg, launches,
-                        p.rf.get());
+        wrmf_tile_solve(st, p, p.ws->df.get(), H, h_rows, off, cols, HH, k, alpha, reg, launches,
+                        p.ws->rf.get());
         rows(2);
         launches += 3;
     }
@@ -2126,15 +2126,26 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             }
             ++launches;
         };
-        resolve(p.heavy_dev.get(), nh, p.factor.get() + (size_t)p.n_light * tile_floats);
-        resolve(p.light.get(), p.n_light, p.factor.get());
+        resolve(p.heavy_dev.get(), nh, p.ws->factor.get() + (size_t)p.n_light * tile_floats);
+        resolve(p.light.get(), p.n_light, p.ws->factor.get());
         MML_HIP(hipGetLastError());
     } else {
         // the factors of the direct rows, kept when refinement passes follow (fp64 mode)
         float* F = nullptr;
         if (p.keep_factor && !rhs) {
-            p.factor.alloc(std::max<size_t>(1, (size_t)(p.n_light + nh) * tile_floats));
-            F = p.factor.get();
+            // 176 KB per direct row at k = 256: keep them only if they fit the free HBM with a
+            // margin (the workspace's current block counts as free: it is reallocated here)
+            const size_t need = std::max<size_t>(1, (size_t)(p.n_light + nh) * tile_floats);
+            size_t free_b = 0, total_b = 0;
+            MML_HIP(hipMemGetInfo(&free_b, &total_b));
+            const size_t have = free_b + p.ws->factor.count * sizeof(float);
+            if (need * sizeof(float) + total_b / 16 > have) {
+                p.keep_factor = false;
+                p.ws->factor.reset();
+            } else {
+                p.ws->factor.alloc(need);
+                F = p.ws->factor.get();
+            }
         }
         // heavy rows: batches whose fp64 Grams fit the workspace
         const int64_t per_row = (int64_t)kTiles * 1024 * sizeof(double);

@@ -1098,10 +1098,36 @@ void ora_wrmf_square(const float* H, int64_t rows, int k, double* HH) {
         }
 }
 
-/* WRMF.Optimize(u, data, W, H, HH) :110-156 over rows [row_begin, row_end) */
+/* WRMF.Optimize(u, data, W, H, HH) :110-156 over rows [row_begin, row_end).  exact = 0: the
+ * reference's arithmetic -- each product h[f1] * h[f2] of the row Gram rounded to float before its
+ * double sum (:116-121).  exact = 1 (test infrastructure, not a reference function): the same
+ * system with those products exact in double, (double) h[f1] * (double) h[f2]; HH (the caller's,
+ * ComputeSquareMatrix's float products) and everything else unchanged.  That is the system an
+ * fp64 solver with an exact residual lands on (the library's Precision = fp64 mode), so it pins
+ * the refinement independently of the float-product floor. */
+static void wrmf_optimize_rows_impl(const int64_t* off, const int32_t* cols, int64_t row_begin,
+                                    int64_t row_end, int64_t n_data_rows, float* W,
+                                    const float* H, const double* HH, int k, double alpha,
+                                    double reg, int exact);
+
 void ora_wrmf_optimize_rows(const int64_t* off, const int32_t* cols, int64_t row_begin,
                             int64_t row_end, int64_t n_data_rows, float* W, const float* H,
                             const double* HH, int k, double alpha, double reg) {
+    wrmf_optimize_rows_impl(off, cols, row_begin, row_end, n_data_rows, W, H, HH, k, alpha, reg,
+                            0);
+}
+
+void ora_wrmf_optimize_rows_exact(const int64_t* off, const int32_t* cols, int64_t row_begin,
+                                  int64_t row_end, int64_t n_data_rows, float* W, const float* H,
+                                  const double* HH, int k, double alpha, double reg) {
+    wrmf_optimize_rows_impl(off, cols, row_begin, row_end, n_data_rows, W, H, HH, k, alpha, reg,
+                            1);
+}
+
+static void wrmf_optimize_rows_impl(const int64_t* off, const int32_t* cols, int64_t row_begin,
+                                    int64_t row_end, int64_t n_data_rows, float* W,
+                                    const float* H, const double* HH, int k, double alpha,
+                                    double reg, int exact) {
     double* HC = (double*)malloc(sizeof(double) * (size_t)k * k);
     double* m = (double*)malloc(sizeof(double) * (size_t)k * k);
     double* inv = (double*)malloc(sizeof(double) * (size_t)k * k);
@@ -1115,7 +1141,7 @@ void ora_wrmf_optimize_rows(const int64_t* off, const int32_t* cols, int64_t row
                 double d = 0.0;
                 for (int64_t x = b; x < e; x++) {
                     const float* h = H + (int64_t)cols[x] * k;
-                    d += (double)(h[f1] * h[f2]);
+                    d += exact ? (double)h[f1] * (double)h[f2] : (double)(h[f1] * h[f2]);
                 }
                 HC[f1 * k + f2] = d * alpha;
                 HC[f2 * k + f1] = d * alpha;

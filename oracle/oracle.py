@@ -121,6 +121,9 @@ def lib():
         L.ora_wrmf_optimize_rows.argtypes = [_i64p, _i32p, ctypes.c_int64, ctypes.c_int64,
                                              ctypes.c_int64, _f32p, _f32p, _f64p, ctypes.c_int,
                                              ctypes.c_double, ctypes.c_double]
+        L.ora_wrmf_optimize_rows_exact.argtypes = [_i64p, _i32p, ctypes.c_int64, ctypes.c_int64,
+                                             ctypes.c_int64, _f32p, _f32p, _f64p, ctypes.c_int,
+                                             ctypes.c_double, ctypes.c_double]
         L.ora_auc_compute.argtypes = [_i32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]
         L.ora_auc_compute.restype = ctypes.c_double
         L.ora_item_eval_auc.argtypes = [
@@ -810,16 +813,19 @@ def wrmf_square(H):
     return HH
 
 
-def wrmf_optimize(off, cols, W, H, alpha, reg):
-    """WRMF.Optimize(data, W, H) (:79-92) in place on W."""
+def wrmf_optimize(off, cols, W, H, alpha, reg, exact_products=False):
+    """WRMF.Optimize(data, W, H) (:79-92) in place on W.  exact_products: the row Gram's products
+    exact in double instead of rounded to float (ora_wrmf_optimize_rows_exact; a test variant,
+    the system the library's fp64 refinement solves)."""
     HH = wrmf_square(H)
-    lib().ora_wrmf_optimize_rows(_p(off, _i64p), _p(cols, _i32p), 0, W.shape[0], len(off) - 1,
-                                 _p(W, _f32p), _p(f32(H), _f32p), _p(HH, _f64p), W.shape[1],
-                                 float(alpha), float(reg))
+    fn = lib().ora_wrmf_optimize_rows_exact if exact_products else lib().ora_wrmf_optimize_rows
+    fn(_p(off, _i64p), _p(cols, _i32p), 0, W.shape[0], len(off) - 1, _p(W, _f32p),
+       _p(f32(H), _f32p), _p(HH, _f64p), W.shape[1], float(alpha), float(reg))
 
 
 def wrmf_train(users, items, n_users, n_items, *, seed=1, k=10, num_iter=15, alpha=1.0,
-               regularization=0.015, init_mean=0.0, init_stddev=0.1, rng=None, callback=None):
+               regularization=0.015, init_mean=0.0, init_stddev=0.1, rng=None, callback=None,
+               exact_products=False):
     users, items = i32(users), i32(items)
     rng = rng if rng is not None else Rng(seed)
     U = rng.fill_normal(n_users * k, init_mean, init_stddev).reshape(n_users, k)
@@ -828,8 +834,8 @@ def wrmf_train(users, items, n_users, n_items, *, seed=1, k=10, num_iter=15, alp
     uoff, ucols = insertion_order_rows(users, items, n_users)
     ioff, icols = insertion_order_rows(items, users, n_items)
     for epoch in range(num_iter):
-        wrmf_optimize(uoff, ucols, U, V, alpha, regularization)
-        wrmf_optimize(ioff, icols, V, U, alpha, regularization)
+        wrmf_optimize(uoff, ucols, U, V, alpha, regularization, exact_products)
+        wrmf_optimize(ioff, icols, V, U, alpha, regularization, exact_products)
         if callback is not None:
             callback(epoch, dict(U=U, V=V))
     return dict(U=U, V=V, init_U=init_U, init_V=init_V, rng=rng)

@@ -17,4 +17,5 @@ step() {  # step <name> <seconds> <command...>
 }
 step multi 600 python -u -m pytest tests/test_multi_gpu.py -x -v -s --timeout 300 --timeout-method thread
 step c2shape 300 python -u -m pytest tests/test_bmf_gpu.py -x -v -s --timeout 200 --timeout-method thread -k c2_shape
+step wrmf_exact 300 python -u -m pytest tests/test_wrmf_gpu.py -x -v -s --timeout 200 --timeout-method thread -k exact_product
 step bench 600 python -u bench.py --steps 5 --warmup 1

@@ -185,3 +185,54 @@ def test_wrmf_large_k_rows_without_events(prec):
     empty_i = np.setdiff1d(np.arange(V.shape[0]), i)
     assert len(empty_u) > 0
     assert np.all(U[empty_u] == 0) and np.all(V[empty_i] == 0)
+
+
+def _woodbury_set(k):
+    rs = np.random.default_rng(k)
+    degs = [1, 5, 31, 32, 33, 64, 65, 96, 97, 127, 128, 129, 200, 300]
+    us, its = [], []
+    for u, d in enumerate(degs * 20):
+        us += [u] * d
+        its += rs.choice(420, size=d, replace=False).tolist()
+    return np.array(us, np.int32), np.array(its, np.int32), 420
+
+
+@pytest.mark.parametrize("case,k,alpha,iters", [
+    ("small", 129, 1.0, 1), ("small", 256, 1.0, 1),          # 120 items < k: cond ~1e4
+    ("woodbury", 160, 1.0, 2), ("woodbury", 256, 4.0, 2),    # 280 users, Woodbury + direct rows
+    ("woodbury", 200, 0.0, 2),                                # every row direct
+    ("wellcond", 256, 1.0, 1)])
+def test_wrmf_fp64_lands_on_exact_product_solution(case, k, alpha, iters):
+    """what the fp64 refinement is worth, asserted on every set.  The residual
+    b - A x is computed with exact float x float products, so the fp64 mode solves the system
+    whose row Gram has exact products (oracle ora_wrmf_optimize_rows_exact; HH keeps
+    ComputeSquareMatrix's float products, WRMF.cs:94-108).  Against THAT solution the device lands
+    within 2e-7 (float parity) even where cond(A) ~ 1e4 puts both 1e-5 away from the
+    float-product reference (the documented floor, test_wrmf_large_k_matches_oracle /
+    test_wrmf_woodbury_and_direct_rows_match_oracle: 1e-4).  Reference: WRMF.cs:110-156."""
+    if case == "small":
+        u, i = synth_feedback(70 + k, 160, 120, 40)
+        nu, ni = int(u.max()) + 1, int(i.max()) + 1
+        seed = 3
+    elif case == "woodbury":
+        u, i, ni = _woodbury_set(k)
+        nu = int(u.max()) + 1
+        seed = 9
+    else:
+        u, i = synth_feedback(5, 1500, 1000, 150)
+        nu, ni = int(u.max()) + 1, int(i.max()) + 1
+        seed = 5
+    exact = O.wrmf_train(u, i, nu, ni, seed=seed, k=k, num_iter=iters, alpha=alpha,
+                         exact_products=True)
+    ref = O.wrmf_train(u, i, nu, ni, seed=seed, k=k, num_iter=iters, alpha=alpha)
+    Random.set_seed(seed)
+    m = WRMF(NumFactors=k, NumIter=iters, Alpha=alpha, Precision="fp64")
+    m.feedback = PosOnlyFeedback(u, i)
+    m.train()
+    de = max(_close(m.user_factors, exact["U"]), _close(m.item_factors, exact["V"]))
+    dr = max(_close(m.user_factors, ref["U"]), _close(m.item_factors, ref["V"]))
+    floor = max(_close(exact["U"], ref["U"]), _close(exact["V"], ref["V"]))
+    print(f"WRMF {case} k={k} alpha={alpha}: fp64 vs exact-product oracle {de:.2e}, vs the "
+          f"reference's float products {dr:.2e} (the two oracles differ by {floor:.2e})")
+    assert de <= 2e-7
+    assert dr <= 1e-4
