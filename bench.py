@@ -688,8 +688,7 @@ def bench_wrmf(args):
     deg_i = torch.bincount(keys % n_items, minlength=n_items).double()
     nnz = int(keys.numel())
     del keys
-    passes = 1 if args.wrmf_precision == "fp64" else 0
-    flops_exec = wrmf_executed_flops(deg_u, deg_i, k, passes, nnz)
+    passes = 3 if args.wrmf_precision == "fp64" else 0  # at most (adaptive)
     p = N.WrmfParams(k, passes, 1.0, 0.015)
     h = N._vp()
     N.check(N.lib().mml_wrmf_create(ctx.handle, ctypes.byref(p), n_users, n_items,
@@ -716,6 +715,10 @@ def bench_wrmf(args):
     if world > 1:
         torch.distributed.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
+    ran = ctypes.c_int32(0)
+    N.check(N.lib().mml_wrmf_last_refine_passes(h, ctypes.byref(ran)))
+    passes_run = ran.value
+    flops_exec = wrmf_executed_flops(deg_u, deg_i, k, passes_run, nnz)
     # SURVEY 8(d)'s count: every row a direct k x k solve (2 nnz k^2 Grams, 2 n k^2 HH, ...)
     half = lambda rows, other: 2 * n * k * k + 2 * other * k * k + rows * (k ** 3 / 3 + 2 * k * k) \
         + 2 * n * k
@@ -752,7 +755,8 @@ def bench_wrmf(args):
                                    "the direct rows' Grams run as six bf16 MFMA products per "
                                    "f32 product (exact 3-way bf16 split), counted once; so do the row GEMMs (Q = H L^-T, the "
                                    "W rows, the refinement transforms)",
-                     "refine_passes": passes,
+                     "refine_passes": passes_run,
+                     "refine_passes_max": passes,
                      "flops_direct_equivalent": flops_direct,
                      "direct_equivalent_tflops": flops_direct / (np.mean(ms) * 1e-3) / 1e12,
                      "direct_equivalent_note": "SURVEY 8(d)'s count (every row a direct k x k "

@@ -403,9 +403,12 @@ mml_status mml_bpr_allreduce_items(mml_bpr* h);
 typedef struct {
     int32_t num_factors;   /* NumFactors (MF.cs:43-45), <= 256: k <= 128 solves in fp64, k > 128
                               in fp32 on the matrix cores (A in fp64 does not fit the LDS) */
-    int32_t refine_passes; /* k > 128 (ABI 5): passes of fp64 iterative refinement after the fp32
-                              solve, x += A^{-1} (b - A x) with the residual in fp64; 1 reaches the
-                              fp64 solution (WRMF.cs:137-154), 0 = the fp32 result */
+    int32_t refine_passes; /* k > 128 (ABI 5): at most this many passes of fp64 iterative
+                              refinement after the fp32 solve, x += A^{-1} (b - A x) with the
+                              residual in fp64 (exact float products); a further pass runs only
+                              while the last correction exceeded 1e-4 relative (ABI 6): one pass
+                              reaches the fp64 solution on well-conditioned systems, cond ~1e4
+                              takes two (WRMF.cs:137-154); 0 = the fp32 result */
     double alpha;          /* Alpha (WRMF.cs:56) */
     double regularization; /* Regularization (WRMF.cs:59) */
 } mml_wrmf_params;
@@ -431,6 +434,8 @@ mml_status mml_wrmf_iterate(mml_wrmf* h);
 mml_status mml_wrmf_predict(mml_wrmf* h, const int32_t* users, const int32_t* items, int64_t n,
                             float* out);
 mml_status mml_wrmf_last_timing(mml_wrmf* h, float* out);
+/* The most refinement passes a half-step of the last mml_wrmf_iterate ran (ABI 6). */
+mml_status mml_wrmf_last_refine_passes(mml_wrmf* h, int32_t* out);
 /* As mml_bpr_auc for the WRMF (MF.Predict) scorer. */
 mml_status mml_wrmf_auc(mml_wrmf* h, const int32_t* candidates, int32_t n_candidates,
                         const int32_t* users, int32_t n_users, const int64_t* test_off,

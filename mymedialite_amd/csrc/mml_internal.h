@@ -159,6 +159,7 @@ struct WrmfTilePlan {
     struct Refine {
         DeviceArray<double> rpartial, x64, r64;
         DeviceArray<float> rf, df, factor;
+        DeviceArray<unsigned> dmax;  // the last pass's largest relative correction (float bits)
     };
     Refine own;
     Refine* ws = &own;
@@ -174,10 +175,11 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
 void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
                      const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
                      double alpha, double reg, int& launches, const float* rhs = nullptr);
-// after wrmf_tile_solve: `passes` rounds of x += A^{-1}(b - A x) with the residual in fp64 (exact
-// float products, double sums) and the correction from the fp32 solver, so W rows [r0, r1) reach
-// the accuracy of the reference's fp64 solve (WRMF.cs:137-154)
-void wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
+// after wrmf_tile_solve: up to `passes` rounds of x += A^{-1}(b - A x) with the residual in fp64
+// (exact float products, double sums) and the correction from the fp32 solver, so W rows [r0, r1)
+// reach the accuracy of the reference's fp64 solve (WRMF.cs:137-154); a further round runs only
+// while the last correction exceeded 1e-4 relative.  Returns the rounds run.
+int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
                       const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
                       double alpha, double reg, int32_t passes, int& launches);
 

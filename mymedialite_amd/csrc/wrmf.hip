@@ -536,6 +536,7 @@ struct mml_wrmf {
     bool has_data = false, has_model = false;
     float last_ms = 0.0f;
     int32_t last_launches = 0;
+    int32_t last_refine = 0;  // the most refinement passes a half-step of the last iterate ran
     int32_t nparts = 1;
     int64_t nnz = 0;
     mml::DeviceArray<uint8_t> hhp;  // HH + reg I, block-packed (k > 64 path)
@@ -619,8 +620,11 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
         plan.keep_factor = h->p.refine_passes > 0;
         mml::wrmf_tile_solve(st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha,
                              h->p.regularization, launches);
-        mml::wrmf_tile_refine(st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha,
-                              h->p.regularization, h->p.refine_passes, launches);
+        const int32_t done = mml::wrmf_tile_refine(st, plan, W, H, h_rows, off, cols,
+                                                   h->HH.get(), k, h->p.alpha,
+                                                   h->p.regularization, h->p.refine_passes,
+                                                   launches);
+        h->last_refine = std::max(h->last_refine, done);
     }
     MML_HIP(hipGetLastError());
     launches += 1;
@@ -896,12 +900,15 @@ extern "C" mml_status mml_wrmf_iterate(mml_wrmf* h) {
             });
             h->last_ms = *std::max_element(ms.begin(), ms.end());
             h->last_launches = h->shards[0]->last_launches;
+            h->last_refine = 0;
+            for (mml_wrmf* s : h->shards) h->last_refine = std::max(h->last_refine, s->last_refine);
             return;
         }
         MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         int launches = 0;
+        h->last_refine = 0;
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
         ensure_shards(h);
         const int rk = h->shard_rank;
@@ -925,6 +932,13 @@ extern "C" mml_status mml_wrmf_last_timing(mml_wrmf* h, float* out) {
         MML_REQUIRE(h && out, "null argument");
         out[0] = h->last_ms;
         out[1] = (float)h->last_launches;
+    });
+}
+
+extern "C" mml_status mml_wrmf_last_refine_passes(mml_wrmf* h, int32_t* out) {
+    return guard([&] {
+        MML_REQUIRE(h && out, "null argument");
+        *out = h->last_refine;
     });
 }
 

@@ -31,6 +31,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <string>
+#include <cstring>
 #include <vector>
 
 #include "mml_internal.h"
@@ -1893,21 +1894,34 @@ __global__ __launch_bounds__(256) void wrmf_resid_multi_kernel(const RMulti* __r
 }
 
 // rows [r0, r0 + n): op 0 X = (double) W, 1 Rf = (float) R, 2 X += D, 3 W = (float) X
+// op 0: X = W; 1: Rf = R; 2: X += D, and dmax = max |D| / (1 + |X|) over the rows (the size of
+// the correction relative to the solution: the error the pass removed); 3: W = X
 __global__ __launch_bounds__(256) void wrmf_refine_rows_kernel(int op, int64_t r0, int64_t n,
                                                                int32_t k, float* __restrict__ W,
                                                                double* __restrict__ X,
                                                                const double* __restrict__ R,
                                                                float* __restrict__ Rf,
-                                                               const float* __restrict__ D) {
+                                                               const float* __restrict__ D,
+                                                               unsigned* __restrict__ dmax) {
+    float m = 0.0f;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * k;
          e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t g = r0 * k + e;
         switch (op) {
             case 0: X[e] = (double)W[g]; break;
             case 1: Rf[g] = (float)R[e]; break;
-            case 2: X[e] += (double)D[g]; break;
+            case 2: {
+                const double x = X[e] + (double)D[g];
+                X[e] = x;
+                m = fmaxf(m, (float)(fabs((double)D[g]) / (1.0 + fabs(x))));
+                break;
+            }
             default: W[g] = (float)X[e]; break;
         }
+    }
+    if (op == 2) {  // non-negative floats order like their bit patterns
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        if ((threadIdx.x & 63) == 0 && m > 0.0f) atomicMax(dmax, __float_as_uint(m));
     }
 }
 
@@ -2011,11 +2025,17 @@ WrmfTilePlan::~WrmfTilePlan() {
     if (blas) (void)rocblas_destroy_handle(reinterpret_cast<rocblas_handle>(blas));
 }
 
-void wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
-                      const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
-                      double alpha, double reg, int32_t passes, int& launches) {
+// a further pass runs while the last correction was larger than this (relative to 1 + |x|): the
+// error left after a pass is about the square of the first correction (x0's error times the
+// solver's contraction, both ~ cond(A) eps_fp32), so 1e-4 leaves ~1e-8.  Well-conditioned rows
+// (C5) stop after one pass; cond(A) ~ 1e4 takes two.
+constexpr float kRefineStop = 1e-4f;
+
+int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H,
+                         int64_t h_rows, const int64_t* off, const int32_t* cols, const double* HH,
+                         int32_t k, double alpha, double reg, int32_t passes, int& launches) {
     const int64_t n = p.r1 - p.r0, n_w = (int64_t)(p.r1);  // W rows addressed up to r1
-    if (passes <= 0 || n <= 0) return;
+    if (passes <= 0 || n <= 0) return 0;
     if (!p.blas) {
         rocblas_handle bh = nullptr;
         if (rocblas_create_handle(&bh) != rocblas_status_success)
@@ -2030,14 +2050,17 @@ void wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H,
     p.ws->rf.alloc((size_t)n_w * k);
     p.ws->df.alloc((size_t)n_w * k);
     p.ws->rpartial.alloc(std::max<int64_t>(1, p.n_rslots) * (size_t)k);
+    if (!p.ws->dmax.get()) p.ws->dmax.alloc(1);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n * k + 255) / 256, 16384));
     auto rows = [&](int op) {
-        wrmf_refine_rows_kernel<<<grid, 256, 0, st>>>(op, p.r0, n, k, W, p.ws->x64.get(), p.ws->r64.get(),
-                                                      p.ws->rf.get(), p.ws->df.get());
+        wrmf_refine_rows_kernel<<<grid, 256, 0, st>>>(op, p.r0, n, k, W, p.ws->x64.get(),
+                                                      p.ws->r64.get(), p.ws->rf.get(),
+                                                      p.ws->df.get(), p.ws->dmax.get());
         ++launches;
     };
     rows(0);
     const double m1 = -1.0, mreg = -reg;
+    int32_t done = 0;
     for (int32_t pass = 0; pass < passes; ++pass) {
         // R = -(HH + reg I) X, then + sum_i c_i h_i per row
         MML_HIP(hipMemcpyAsync(p.ws->r64.get(), p.ws->x64.get(), sizeof(double) * n * k,
@@ -2061,11 +2084,23 @@ void wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H,
         // D = A^{-1} R on the fp32 solver (rows outside [r0, r1) are not read)
         wrmf_tile_solve(st, p, p.ws->df.get(), H, h_rows, off, cols, HH, k, alpha, reg, launches,
                         p.ws->rf.get());
+        MML_HIP(hipMemsetAsync(p.ws->dmax.get(), 0, sizeof(unsigned), st));
         rows(2);
         launches += 3;
+        ++done;
+        if (pass + 1 < passes) {  // another pass only while the correction was large
+            unsigned bits = 0;
+            MML_HIP(hipMemcpyAsync(&bits, p.ws->dmax.get(), sizeof(unsigned),
+                                   hipMemcpyDeviceToHost, st));
+            MML_HIP(hipStreamSynchronize(st));
+            float d;
+            std::memcpy(&d, &bits, sizeof(d));
+            if (!(d > kRefineStop)) break;
+        }
     }
     rows(3);
     MML_HIP(hipGetLastError());
+    return done;
 }
 
 // L^{-1} (lower) of B = HH + reg I by Cholesky in fp64 on the host (k <= 256: ~10 M flops)

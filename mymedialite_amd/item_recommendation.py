@@ -413,10 +413,11 @@ class WRMF(_MFBase):
         "Alpha": "double", "Device": "int", "Gpus": "string", "InitMean": "double", "InitStdDev": "double",
         "NumFactors": "uint", "NumIter": "uint", "Precision": "string", "Regularization": "double",
     }
-    # Precision (GPU only, 128 < NumFactors): "fp64" = the fp32 MFMA solve + one pass of fp64
-    # iterative refinement (the fp64 solution, WRMF.cs:137-154; further passes change nothing
-    # measurable: scripts/diag_wrmf_refine.py); "fp32" = the solve alone
-    REFINE_PASSES = {"fp64": 1, "fp32": 0}
+    # Precision (GPU only, 128 < NumFactors): "fp64" = the fp32 MFMA solve + fp64 iterative
+    # refinement, up to 3 passes, a further one only while the last correction exceeded 1e-4
+    # relative (well-conditioned systems stop after one, cond ~1e4 after two: the fp64 solution,
+    # WRMF.cs:137-154); "fp32" = the solve alone
+    REFINE_PASSES = {"fp64": 3, "fp32": 0}  # at most; a pass runs while the correction is large
 
     def __init__(self, **kw):
         super().__init__()
