@@ -8,9 +8,10 @@ Schedule (GPU-only property):
   * ``auto``    -> below AUTO_EXACT_MAX ratings the reference's own schedule, exactly:
                    MaxThreads <= 1: ``ordered`` (the sequential loop, one wavefront);
                    MaxThreads > 1: ``dsgd`` (the DSGD blocks) or, with NaiveParallelization,
-                   ``hogwild`` (the reference's racy mode).  From AUTO_EXACT_MAX ratings on:
-                   ``hogwild`` (statistical parity; the exact schedules are bounded by the
-                   hottest item's sequential updates, ~2e7 ratings/s, DESIGN.md section 3);
+                   ``hogwild`` (the reference's racy mode), at any size.  MaxThreads = 1 from
+                   AUTO_EXACT_MAX ratings on: ``hogwild`` (statistical parity, noted once on
+                   stderr; the exact schedules are bounded by the hottest item's sequential
+                   updates, ~2e7 ratings/s, DESIGN.md section 3);
   * ``ordered`` / ``dsgd`` / ``hogwild`` / ``hogwild_coherent`` to force one (the last keeps every
     row access agent-coherent: closer to the sequential trajectory, slower on hot items).
 """
@@ -35,6 +36,17 @@ _SCHED = {"ordered": N.SCHEDULE_ORDERED, "dsgd": N.SCHEDULE_DSGD, "hogwild": N.S
 
 def _large(ratings) -> bool:
     return ratings is not None and ratings.count >= AUTO_EXACT_MAX
+
+
+def _note_auto_hogwild(rec):
+    """Schedule=auto leaves the reference's sequential loop for Hogwild on large sets: say so once
+    per recommender (the result is then statistically, not bitwise, the reference's)."""
+    if getattr(rec, "_auto_noted", False):
+        return
+    rec._auto_noted = True
+    print(f"{type(rec).__name__}: Schedule=auto with {rec._ratings.count} >= {AUTO_EXACT_MAX} "
+          "ratings runs the lock-free Hogwild epoch (statistical parity); Schedule=ordered forces "
+          "the reference's sequential loop, MaxThreads > 1 its DSGD", file=sys.stderr)
 
 
 class MatrixFactorization(Recommender):
@@ -376,9 +388,14 @@ class BiasedMatrixFactorization(MatrixFactorization):
             if self.Schedule not in _SCHED:
                 raise ValueError(f"unknown Schedule '{self.Schedule}'")
             return self.Schedule
-        if (self.NaiveParallelization and self.MaxThreads > 1) or _large(self._ratings):
+        if self.NaiveParallelization and self.MaxThreads > 1:
+            return "hogwild"  # the reference's racy mode, as asked
+        if self.MaxThreads > 1:
+            return "dsgd"  # the reference's deterministic multi-core schedule, as asked
+        if _large(self._ratings):
+            _note_auto_hogwild(self)
             return "hogwild"
-        return "dsgd" if self.MaxThreads > 1 else "ordered"
+        return "ordered"
 
     # ------------------------------------------------------------------ model
     def _params(self) -> N.BmfParams:

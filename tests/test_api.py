@@ -58,9 +58,9 @@ def test_gpus_option_selects_a_multi_device_context():
 
 
 def test_auto_schedule_switches_to_hogwild_at_scale():
-    """Schedule="auto": the reference's exact schedule below AUTO_EXACT_MAX training ratings
-    (ordered, or DSGD for MaxThreads > 1), Hogwild from there on (the exact schedules run at
-    ~2e7 ratings/s whatever the GPU)."""
+    """Schedule="auto": the reference's sequential loop below AUTO_EXACT_MAX training ratings,
+    Hogwild from there on (the exact schedules run at ~2e7 ratings/s whatever the GPU, DESIGN.md
+    section 3; noted once on stderr); MaxThreads > 1 keeps the reference's DSGD at any size."""
     from mymedialite_amd import rating_prediction as RP
     small = M.Ratings(np.zeros(10, np.int32), np.arange(10, dtype=np.int32),
                       np.ones(10, np.float32))
@@ -77,8 +77,12 @@ def test_auto_schedule_switches_to_hogwild_at_scale():
         assert m.schedule() == "hogwild", cls
         m.Schedule = "ordered"
         assert m.schedule() == "ordered"
+    # an explicit MaxThreads > 1 asks for the reference's deterministic DSGD: kept at any size
+    # (a silent switch to the racy schedule would surprise such a caller)
     m = M.BiasedMatrixFactorization(MaxThreads=8)
     m.ratings = small
     assert m.schedule() == "dsgd"
     m.ratings = big
+    assert m.schedule() == "dsgd"
+    m.NaiveParallelization = True
     assert m.schedule() == "hogwild"
