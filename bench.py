@@ -716,7 +716,8 @@ def bench_wrmf(args):
         torch.distributed.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
     ran = ctypes.c_int32(0)
-    N.check(N.lib().mml_wrmf_last_refine_passes(h, ctypes.byref(ran)))
+    corr = np.zeros(8, np.float32)
+    N.check(N.lib().mml_wrmf_last_refine_passes(h, ctypes.byref(ran), N.ptr(corr, N._f32p)))
     passes_run = ran.value
     flops_exec = wrmf_executed_flops(deg_u, deg_i, k, passes_run, nnz)
     # SURVEY 8(d)'s count: every row a direct k x k solve (2 nnz k^2 Grams, 2 n k^2 HH, ...)
@@ -757,6 +758,7 @@ def bench_wrmf(args):
                                    "W rows, the refinement transforms)",
                      "refine_passes": passes_run,
                      "refine_passes_max": passes,
+                     "refine_corrections": [float(x) for x in corr],
                      "flops_direct_equivalent": flops_direct,
                      "direct_equivalent_tflops": flops_direct / (np.mean(ms) * 1e-3) / 1e12,
                      "direct_equivalent_note": "SURVEY 8(d)'s count (every row a direct k x k "

@@ -434,8 +434,10 @@ mml_status mml_wrmf_iterate(mml_wrmf* h);
 mml_status mml_wrmf_predict(mml_wrmf* h, const int32_t* users, const int32_t* items, int64_t n,
                             float* out);
 mml_status mml_wrmf_last_timing(mml_wrmf* h, float* out);
-/* The most refinement passes a half-step of the last mml_wrmf_iterate ran (ABI 6). */
-mml_status mml_wrmf_last_refine_passes(mml_wrmf* h, int32_t* out);
+/* The most refinement passes a half-step of the last mml_wrmf_iterate ran (ABI 6);
+ * corrections (nullable, [8]): per half-step (users 0..3, items 4..7) and pass, the largest
+ * correction relative to 1 + |x| that decided whether another pass ran (0: not read back). */
+mml_status mml_wrmf_last_refine_passes(mml_wrmf* h, int32_t* out, float* corrections);
 /* As mml_bpr_auc for the WRMF (MF.Predict) scorer. */
 mml_status mml_wrmf_auc(mml_wrmf* h, const int32_t* candidates, int32_t n_candidates,
                         const int32_t* users, int32_t n_users, const int64_t* test_off,

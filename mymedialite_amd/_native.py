@@ -152,7 +152,7 @@ SIGNATURES = {
     "mml_wrmf_iterate": (_st, [_vp]),
     "mml_wrmf_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
     "mml_wrmf_last_timing": (_st, [_vp, _f32p]),
-    "mml_wrmf_last_refine_passes": (_st, [_vp, _i32p]),
+    "mml_wrmf_last_refine_passes": (_st, [_vp, _i32p, _f32p]),
     "mml_wrmf_auc": (_st, [_vp, _i32p, ctypes.c_int32, _i32p, ctypes.c_int32, _i64p, _i32p,
                            _f64p]),
 }

@@ -179,9 +179,10 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
 // (exact float products, double sums) and the correction from the fp32 solver, so W rows [r0, r1)
 // reach the accuracy of the reference's fp64 solve (WRMF.cs:137-154); a further round runs only
 // while the last correction exceeded 1e-4 relative.  Returns the rounds run.
-int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
-                      const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
-                      double alpha, double reg, int32_t passes, int& launches);
+int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H,
+                         int64_t h_rows, const int64_t* off, const int32_t* cols, const double* HH,
+                         int32_t k, double alpha, double reg, int32_t passes, int& launches,
+                         float* corrections = nullptr);  // [4]: each pass's max correction
 
 // XCD-owned item groups (xcd.hip): items dealt into 8 groups of equal weight, a stream partitioned
 // (stable) by the group of its item; group g's span goff[g] .. goff[g + 1] is served by blocks

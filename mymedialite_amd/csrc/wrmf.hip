@@ -537,6 +537,7 @@ struct mml_wrmf {
     float last_ms = 0.0f;
     int32_t last_launches = 0;
     int32_t last_refine = 0;  // the most refinement passes a half-step of the last iterate ran
+    float last_corr[8] = {};  // per half-step (users, items) and pass: the max relative correction
     int32_t nparts = 1;
     int64_t nnz = 0;
     mml::DeviceArray<uint8_t> hhp;  // HH + reg I, block-packed (k > 64 path)
@@ -620,10 +621,9 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
         plan.keep_factor = h->p.refine_passes > 0;
         mml::wrmf_tile_solve(st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha,
                              h->p.regularization, launches);
-        const int32_t done = mml::wrmf_tile_refine(st, plan, W, H, h_rows, off, cols,
-                                                   h->HH.get(), k, h->p.alpha,
-                                                   h->p.regularization, h->p.refine_passes,
-                                                   launches);
+        const int32_t done = mml::wrmf_tile_refine(
+            st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha, h->p.regularization,
+            h->p.refine_passes, launches, h->last_corr + (W == h->U.get() ? 0 : 4));
         h->last_refine = std::max(h->last_refine, done);
     }
     MML_HIP(hipGetLastError());
@@ -909,6 +909,7 @@ extern "C" mml_status mml_wrmf_iterate(mml_wrmf* h) {
         hipStream_t st = h->ctx->stream;
         int launches = 0;
         h->last_refine = 0;
+        std::fill(h->last_corr, h->last_corr + 8, 0.0f);
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
         ensure_shards(h);
         const int rk = h->shard_rank;
@@ -935,10 +936,12 @@ extern "C" mml_status mml_wrmf_last_timing(mml_wrmf* h, float* out) {
     });
 }
 
-extern "C" mml_status mml_wrmf_last_refine_passes(mml_wrmf* h, int32_t* out) {
+extern "C" mml_status mml_wrmf_last_refine_passes(mml_wrmf* h, int32_t* out,
+                                                  float* corrections) {
     return guard([&] {
         MML_REQUIRE(h && out, "null argument");
         *out = h->last_refine;
+        if (corrections) std::copy(h->last_corr, h->last_corr + 8, corrections);
     });
 }
 

@@ -55,8 +55,7 @@ constexpr int kCH = 16;                                  // gathered vectors per
 constexpr int kHSW = 32 * kNR;                           // staged vector width
 constexpr int kPS = 34;                                  // panel row stride (conflict-free reads)
 constexpr int kDS = 33;                                  // diagonal-tile / reduction row stride
-constexpr int kTS = 40;                                  // T_J^T row stride
-constexpr int kDG = 36;                                  // diagonal-tile row stride
+constexpr int kTS = 33;                                  // T_J^T row stride (conflict-free rows)
 
 __device__ __forceinline__ int rho(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
 
@@ -93,11 +92,9 @@ struct Smem {
         alignas(16) uint16_t pl[2][3][kHSW][kCH];
         struct {
             float pn[kNT][32][kPS];     // Cholesky: L_IJ of the current panel, row-major
-            float park[kSlots][4][64][4];  // one wave's accumulators during a diagonal factor
         } fz;
         float red[kNT][32][kDS];        // backward: per-tile partial products
     } u;
-    float dg[32][kDG];                  // diagonal tile (rows 16-B aligned)
     float tT[2][32][kTS];               // tT[c][m] = T_J[m][c], double-buffered (lookahead)
     float yv[kHSW];
     float wv[kHSW];
@@ -492,81 +489,72 @@ __global__ __launch_bounds__(256) void wrmf_tile_hh_kernel(const double* __restr
     }
 }
 
-// One wave: T = L^{-1} for the diagonal tile the caller wrote to sm.dg (row-major):
-// L = chol(tile) with row q of the tile in lane q (v_readlane broadcasts of the pivot column), then
-// column q of T in lane q from the rows of L broadcast out of LDS.  Writes tT[c][m] = T[m][c].
-__device__ __forceinline__ void diag_factor(float (*dg)[kDG], float (*tT)[kTS]) {
-    const int lane = opaque_tid() & 63, q = lane & 31, h = lane >> 5;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float x[32];
-#pragma unroll
-    for (int c = 0; c < 32; c += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(&dg[q][c]);
-        x[c] = v.x; x[c + 1] = v.y; x[c + 2] = v.z; x[c + 3] = v.w;
-    }
-#pragma unroll
-    for (int c = 0; c < 32; ++c) {
-        const float piv = lane_bcast(x[c], c);
-        const float inv = __builtin_amdgcn_rsqf(piv);
-        x[c] = (q == c) ? piv * inv : x[c] * inv;
-#pragma unroll
-        for (int c2 = c + 1; c2 < 32; ++c2) x[c2] -= x[c] * lane_bcast(x[c], c2);
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (h == 0)
-#pragma unroll
-        for (int c = 0; c < 32; c += 4)
-            *reinterpret_cast<float4*>(&dg[q][c]) = make_float4(x[c], x[c + 1], x[c + 2], x[c + 3]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float tc[32];
-#pragma unroll
-    for (int m = 0; m < 32; ++m) {
-        float sacc = (m == q) ? 1.0f : 0.0f;
-#pragma unroll
-        for (int j4 = 0; j4 < m; j4 += 4) {
-            const float4 l = *reinterpret_cast<const float4*>(&dg[m][j4]);
-            sacc -= l.x * tc[j4];
-            if (j4 + 1 < m) sacc -= l.y * tc[j4 + 1];
-            if (j4 + 2 < m) sacc -= l.z * tc[j4 + 2];
-            if (j4 + 3 < m) sacc -= l.w * tc[j4 + 3];
-        }
-        tc[m] = sacc * __builtin_amdgcn_rcpf(dg[m][m]);
-    }
-    if (h == 0)
-#pragma unroll
-        for (int m = 0; m < 32; ++m) tT[q][m] = tc[m];
+// lanes 0-31 <-> 32-63: each lane gets its partner half's x (v_permlane32_swap)
+__device__ __forceinline__ float half_swap(float x, int h) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                    false);
+    return __uint_as_float(h ? r[0] : r[1]);
 }
 
-// The calling wave parks its accumulators in LDS around diag_factor, so the factorisation's
-// registers do not have to coexist with the tiles (which would spill).
+// One wave: T = L^{-1} of the SPD diagonal tile a (held in the C/D layout: lane (q, h), register g
+// = element (rho(g, h), q), symmetric), written as tT[c][m] = T[m][c].  Right-looking Cholesky by
+// column PAIRS on the matrix core: per pair (c, c + 1) the two pivots and L's two columns come
+// from v_readlane broadcasts, then ONE v_mfma_f32_32x32x2_f32 applies the rank-2 update
+// A -= l_c l_c^T + l_{c+1} l_{c+1}^T to the whole tile (the operand of lane (q, h) is
+// l_{c+h}[q] for both A and B).  T is built alongside from R = I by the same elimination: rows c,
+// c + 1 of R are scaled and combined on the VALU (they live in registers gc, gc + 1 of one half),
+// then one MFMA applies R[m] -= L[m][c] R[c] + L[m][c+1] R[c+1] to the rows below.  16 dependent
+// steps of ~1 MFMA latency each, instead of 32 x 31 serial readlane updates and a row-by-row
+// substitution for T (~12 k cycles per tile).
+__device__ __forceinline__ void diag_factor_mfma(f32x16 a, float (*tT)[kTS]) {
+    const int lane = opaque_tid() & 63, q = lane & 31, h = lane >> 5;
+    f32x16 r;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) r[g] = rho(g, h) == q ? 1.0f : 0.0f;
+#pragma unroll
+    for (int c = 0; c < 32; c += 2) {
+        const int hc = (c >> 2) & 1, gc = (c & 3) + 4 * (c >> 3);  // rho(gc, hc) = c
+        // columns c, c + 1 of the updated tile in every lane (row q)
+        const float s0 = half_swap(a[gc], h), s1 = half_swap(a[gc + 1], h);
+        const float a0 = h == hc ? a[gc] : s0;
+        const float piv0 = lane_bcast(a0, c);
+        const float rs0 = __builtin_amdgcn_rsqf(piv0);
+        const float l0 = q < c ? 0.0f : (q == c ? piv0 * rs0 : a0 * rs0);
+        const float l10 = lane_bcast(l0, c + 1);
+        const float a1 = (h == hc ? a[gc + 1] : s1) - l0 * l10;
+        const float piv1 = lane_bcast(a1, c + 1);
+        const float rs1 = __builtin_amdgcn_rsqf(piv1);
+        const float l1 = q <= c ? 0.0f : (q == c + 1 ? piv1 * rs1 : a1 * rs1);
+        // rows c, c + 1 of R: R[c] /= L[c][c]; R[c+1] = (R[c+1] - L[c+1][c] R[c]) / L[c+1][c+1]
+        const float r0 = r[gc] * rs0;
+        const float r1 = (r[gc + 1] - l10 * r0) * rs1;
+        r[gc] = h == hc ? r0 : r[gc];
+        r[gc + 1] = h == hc ? r1 : r[gc + 1];
+        if (c + 2 < 32) {
+            const float op = h ? l1 : l0;
+            a = __builtin_amdgcn_mfma_f32_32x32x2f32(-op, op, a, 0, 0, 0);
+            const float t0 = half_swap(r[gc], h), t1 = half_swap(r[gc + 1], h);
+            const float opb = hc == 0 ? (h == 0 ? r[gc] : t1) : (h == 0 ? t0 : r[gc + 1]);
+            const float opa = q > c + 1 ? op : 0.0f;
+            r = __builtin_amdgcn_mfma_f32_32x32x2f32(-opa, opb, r, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) tT[q][rho(g, h)] = r[g];
+}
+
+// The owner of diagonal tile `slot` factors it (T_J = L_JJ^{-1} to tT); no LDS parking: the
+// factorisation needs ~40 registers beside the accumulators.
 __device__ __forceinline__ void factor_tile(Smem& sm, f32x16 (&acc)[kSlots], int slot,
                                             float (*tT)[kTS]) {
-    const int lane = opaque_tid() & 63, q = lane & 31, h = lane >> 5;
+    (void)sm;
+    f32x16 a;
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s) {
-        if (s == slot)
-#pragma unroll
-            for (int g = 0; g < 16; ++g) sm.dg[q][rho(g, h)] = acc[s][g];
-#pragma unroll
-        for (int g = 0; g < 16; g += 4)
-            *reinterpret_cast<float4*>(&sm.u.fz.park[s][g / 4][lane][0]) =
-                make_float4(acc[s][g], acc[s][g + 1], acc[s][g + 2], acc[s][g + 3]);
-    }
-    diag_factor(sm.dg, tT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int g = 0; g < 16; ++g) a[g] = 0.0f;
 #pragma unroll
     for (int s = 0; s < kSlots; ++s)
-#pragma unroll
-        for (int g = 0; g < 16; g += 4) {
-            const float4 v = *reinterpret_cast<const float4*>(&sm.u.fz.park[s][g / 4][lane][0]);
-            acc[s][g] = v.x; acc[s][g + 1] = v.y; acc[s][g + 2] = v.z; acc[s][g + 3] = v.w;
-        }
+        if (s == slot) a = acc[s];
+    diag_factor_mfma(a, tT);
 }
 
 // L^T w = y by 32-column blocks, w_J = T_J^T (y_J - sum_{I>J} L_IJ^T w_I): the factor in the
@@ -1029,7 +1017,6 @@ struct WoodSmem {
         float pn[NT][32][kPS];
         float red[NT][32][kDS];
     } u;
-    float dg[32][kDG];
     float tT[2][32][kTS];
     float yv[C::HSW];
     float wv[C::HSW];
@@ -1178,12 +1165,13 @@ __global__ __launch_bounds__(kThreads, 4) void wrmf_wood_kernel(
         }
         // ---- blocked Cholesky with a one-panel lookahead (as wrmf_tile_solve_kernel)
         auto factor_owned = [&](int tile, float (*tT)[kTS]) {
+            f32x16 a;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) a[g] = 0.0f;
 #pragma unroll
             for (int s = 0; s < C::SLOTS; ++s)
-                if (s * C::WPG + wig == tile)
-#pragma unroll
-                    for (int g = 0; g < 16; ++g) sm.dg[q][rho(g, h)] = acc[s][g];
-            diag_factor(sm.dg, tT);
+                if (s * C::WPG + wig == tile) a = acc[s];
+            diag_factor_mfma(a, tT);
         };
         if (wig == 0) factor_owned(0, sm.tT[0]);
         __syncthreads();
@@ -2025,15 +2013,17 @@ WrmfTilePlan::~WrmfTilePlan() {
     if (blas) (void)rocblas_destroy_handle(reinterpret_cast<rocblas_handle>(blas));
 }
 
-// a further pass runs while the last correction was larger than this (relative to 1 + |x|): the
-// error left after a pass is about the square of the first correction (x0's error times the
-// solver's contraction, both ~ cond(A) eps_fp32), so 1e-4 leaves ~1e-8.  Well-conditioned rows
-// (C5) stop after one pass; cond(A) ~ 1e4 takes two.
-constexpr float kRefineStop = 1e-4f;
+// a further pass runs while the last correction was larger than this (relative to 1 + |x|).  The
+// error left after a pass is the correction times the pass's contraction, which the fp32 solver
+// (fp32 L^-1 and a 3e-3 CG for the Woodbury rows, the fp32 factor for the direct rows) keeps
+// below ~0.05 on the test sets: 2e-6 leaves <= 1e-7.  The fp32 solve of a well-conditioned system
+// (C5) is ~1e-6 off, so one pass; cond ~1e4 (fp32 6e-5 off) takes two or three.
+constexpr float kRefineStop = 2e-6f;
 
 int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H,
                          int64_t h_rows, const int64_t* off, const int32_t* cols, const double* HH,
-                         int32_t k, double alpha, double reg, int32_t passes, int& launches) {
+                         int32_t k, double alpha, double reg, int32_t passes, int& launches,
+                         float* corrections) {
     const int64_t n = p.r1 - p.r0, n_w = (int64_t)(p.r1);  // W rows addressed up to r1
     if (passes <= 0 || n <= 0) return 0;
     if (!p.blas) {
@@ -2095,6 +2085,7 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
             MML_HIP(hipStreamSynchronize(st));
             float d;
             std::memcpy(&d, &bits, sizeof(d));
+            if (corrections && pass < 4) corrections[pass] = d;
             if (!(d > kRefineStop)) break;
         }
     }

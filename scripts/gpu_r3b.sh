@@ -15,5 +15,5 @@ step() {  # step <name> <seconds> <command...>
     tail -3 "gpurun_out/${name}_$TAG.log" | cut -c1-400
     [ $rc -eq 0 ] || exit $rc
 }
-step wrmf 600 python -u -m pytest tests/test_wrmf_gpu.py -x -v -s --timeout 200 --timeout-method thread
+step wrmf 600 python -u -m pytest tests/test_wrmf_gpu.py -v -s --timeout 200 --timeout-method thread -k "exact_product or refinement or woodbury or large_k"
 step bench 600 python -u bench.py --steps 5 --warmup 1
