@@ -54,6 +54,13 @@ constexpr int kSlots = (kTiles + kWaves - 1) / kWaves;   // 6 tiles per wave
 constexpr int kCH = 16;                                  // gathered vectors per LDS chunk
 constexpr int kHSW = 32 * kNR;                           // staged vector width
 constexpr int kPS = 34;                                  // panel row stride (conflict-free reads)
+constexpr int kRB = 4;    // Gram: raw fp32 chunks in the LDS ring (kRB - 1 chunks of gathers in flight)
+constexpr int kRS = 260;  // raw row stride in floats (1 KiB of row + pad: conflict-free reads)
+#ifdef MML_NO_GRAM_RING  // A/B variant (scripts/build_variant.sh): the register-staged Gram only
+constexpr bool kGramRing = false;
+#else
+constexpr bool kGramRing = true;
+#endif
 constexpr int kDS = 33;                                  // diagonal-tile / reduction row stride
 constexpr int kTS = 33;                                  // T_J^T row stride (conflict-free rows)
 
@@ -90,6 +97,10 @@ struct Smem {
         // Gram (MODE 0): the staged vectors as three bf16 planes (x = x0 + x1 + x2), each row f
         // holding the kCH vectors' element f (two 16-B halves, swapped on rows with f & 8)
         alignas(16) uint16_t pl[2][3][kHSW][kCH];
+        struct {  // the same planes, then the ring the vectors are gathered into (global -> LDS)
+            alignas(16) uint16_t pl[2][3][kHSW][kCH];
+            alignas(16) float raw[kRB][kCH][kRS];
+        } gx;
         struct {
             float pn[kNT][32][kPS];     // Cholesky: L_IJ of the current panel, row-major
         } fz;
@@ -436,6 +447,154 @@ __device__ __forceinline__ void gram_accumulate_x3(Smem& sm, f32x16 (&acc)[kSlot
     }
 }
 
+// gram_accumulate_x3 with the gathers going global -> LDS directly (global_load_lds_dwordx4: one
+// wave-instruction moves one 1 KiB vector row, no VGPR destination) into a ring of kRB raw fp32
+// chunks, so kRB - 1 chunks of gathers are in flight without holding registers (the register
+// version keeps two chunks in 16 VGPRs of a kernel at the register cap; its waves wait on memory
+// more than half the time).  Per chunk: wave w gathers vectors 2w, 2w + 1;
+// the waves convert the previous chunk from the ring into the bf16 planes (same thread map and
+// plane layout as the register version), and run the MFMAs of the chunk before that.  One barrier
+// per chunk, raw s_barrier with counted vmcnt waits: __syncthreads() would drain the ring
+// (vmcnt(0)).  k % 4 == 0 (16-B rows).
+__device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_addr) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_addr)
+        : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// LDS writes done, then the workgroup barrier, without waiting for the ring's loads
+__device__ __forceinline__ void ring_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void gram_accumulate_x3g(Smem& sm, f32x16 (&acc)[kSlots], Tiles& tl,
+                                                    int nslot, const int32_t* __restrict__ cols,
+                                                    int64_t b, int64_t e,
+                                                    const float* __restrict__ H, int k, int hsw) {
+    static_assert(kCH == 16 && kThreads == 512, "two vectors per wave and chunk");
+    static_assert(kRB >= 3, "at least one chunk of gathers in flight beyond the converted one");
+    const int t = opaque_tid(), lane = t & 63, q = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int r = lane >> 3, c2 = lane & 7;
+    const int kb = hsw - 32;
+    const int ntb = hsw / 32 - 1;
+    float bacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (e <= b) return;
+    const int64_t nch = (e - b + kCH - 1) / kCH;
+    // gather chunk c's vectors 2w, 2w + 1 into ring slot c % kRB; chunks past the end load row 0
+    // (never converted) so every wave issues exactly two loads per chunk: the vmcnt counts hold
+    const int lo = 4 * lane < k ? 4 * lane : 0;
+    // the two item ids of chunk c (scalar loads, fetched one chunk before their gathers issue)
+    auto ids = [&](int64_t c, int32_t& i0, int32_t& i1) {
+        const int64_t e0 = b + c * kCH + 2 * wave;
+        i0 = e0 < e ? cols[e0] : 0;
+        i1 = e0 + 1 < e ? cols[e0 + 1] : 0;
+    };
+    auto gather = [&](int64_t c, int32_t i0, int32_t i1) {
+        float* dst = &sm.u.gx.raw[c % kRB][2 * wave][0];
+        glds16(H + (int64_t)i0 * k + lo, lds_addr_of(dst));
+        glds16(H + (int64_t)i1 * k + lo, lds_addr_of(dst + kRS));
+    };
+    // ring slot of chunk c -> bf16 planes of buffer pb (vectors past the end are 0, row kb = 1 on
+    // live vectors, features >= k are 0)
+    auto convert = [&](int64_t c, int pb) {
+        const float* src = &sm.u.gx.raw[c % kRB][0][0];
+        const int64_t e0 = b + c * kCH + 2 * c2;
+        const bool l0 = e0 < e, l1 = e0 + 1 < e;
+        float x0[4], x1[4];  // all eight LDS reads first (unconditional: one wait, no branches)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f = 32 * wave + 8 * g + r;
+            x0[g] = src[(2 * c2) * kRS + f];
+            x1[g] = src[(2 * c2 + 1) * kRS + f];
+        }
+        asm volatile("" : "+v"(x0[0]), "+v"(x0[1]), "+v"(x0[2]), "+v"(x0[3]), "+v"(x1[0]),
+                     "+v"(x1[1]), "+v"(x1[2]), "+v"(x1[3]));
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f = 32 * wave + 8 * g + r;
+            float v0 = x0[g], v1 = x1[g];
+            v0 = l0 ? (f < k ? v0 : (f == kb ? 1.0f : 0.0f)) : 0.0f;
+            v1 = l1 ? (f < k ? v1 : (f == kb ? 1.0f : 0.0f)) : 0.0f;
+            if (f < k) bacc[g] += v0 + v1;
+            uint32_t a0, a1, a2, b0, b1, b2;
+            const int pos = pl_pos(f, 2 * c2);
+            split3t(v0, a0, a1, a2);
+            split3t(v1, b0, b1, b2);
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[pb][0][f][pos]) = pack_hi(a0, b0);
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[pb][1][f][pos]) = pack_hi(a1, b1);
+            *reinterpret_cast<uint32_t*>(&sm.u.pl[pb][2][f][pos]) = pack_hi(a2, b2);
+        }
+    };
+    __syncthreads();  // the LDS union may still be read by the previous row's last phase
+#pragma unroll
+    for (int c = 0; c < kRB - 1; ++c) {
+        int32_t i0, i1;
+        ids(c, i0, i1);
+        gather(c, i0, i1);
+    }
+    int32_t n0, n1;  // the ids of the next chunk to gather
+    ids(kRB - 1, n0, n1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * (kRB - 2)) : "memory");  // chunk 0 landed
+    ring_barrier();
+    convert(0, 0);
+    for (int64_t c = 0; c < nch; ++c) {
+        gather(c + kRB - 1, n0, n1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * (kRB - 2)) : "memory");  // chunk c + 1
+        ring_barrier();  // planes of chunk c and every wave's ring slot of chunk c + 1 are ready
+        ids(c + kRB, n0, n1);  // in flight until the next chunk's gathers
+        const int cur = (int)(c & 1);
+        // (past the last chunk the slot holds row-0 loads: masked to 0, the planes never read)
+        convert(c + 1, cur ^ 1);
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) {
+            if (s >= nslot || tl.I[s] < 0 || tl.I[s] == ntb) continue;
+            const int fa = 32 * tl.J[s] + q, fb = 32 * tl.I[s] + q;
+            bf16x8 A[3], B[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                A[p] = *static_cast<const bf16x8*>(__builtin_assume_aligned(
+                    &sm.u.pl[cur][p][fa][pl_pos(fa, 8 * h)], 16));
+                B[p] = *static_cast<const bf16x8*>(__builtin_assume_aligned(
+                    &sm.u.pl[cur][p][fb][pl_pos(fb, 8 * h)], 16));
+            }
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], acc[s], 0, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing loads (past the end)
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        float v = bacc[g];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        const int f = 32 * wave + 8 * g + r;
+        if (c2 == 0 && f < kb) sm.wv[f] = f < k ? v : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+        if (s >= nslot || tl.I[s] != ntb) continue;
+#pragma unroll
+        for (int g = 0; g < 16; ++g)
+            acc[s][g] += q == 0 ? sm.wv[32 * tl.J[s] + rho(g, h)] : 0.0f;
+    }
+}
+
 // Split Gram of the heavy rows: one workgroup per (row, segment of <= kSeg entries), fp64 atomics
 // into gram[(li * kTiles + tile) * 1024 + g * 64 + lane].
 struct Seg {
@@ -459,7 +618,10 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_gram_kernel(
         for (int s = 0; s < kSlots; ++s)
 #pragma unroll
             for (int g = 0; g < 16; ++g) acc[s][g] = 0.0f;
-        gram_accumulate_x3(sm, acc, tl, kSlots, cols, sg.b, sg.e, H, k, 32 * nr);
+        if (kGramRing && (k & 3) == 0)
+            gram_accumulate_x3g(sm, acc, tl, kSlots, cols, sg.b, sg.e, H, k, 32 * nr);
+        else
+            gram_accumulate_x3(sm, acc, tl, kSlots, cols, sg.b, sg.e, H, k, 32 * nr);
 #pragma unroll
         for (int s = 0; s < kSlots; ++s) {
             if (tl.I[s] < 0) continue;
@@ -659,7 +821,10 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
             }
         } else if (!(dbg & 8)) {
             if constexpr (MODE == 0) {
-                if (gram_x3) gram_accumulate_x3(sm, acc, tl, nslot, cols, rb, re, H, k, hsw);
+                if (gram_x3 && kGramRing && (k & 3) == 0)
+                    gram_accumulate_x3g(sm, acc, tl, nslot, cols, rb, re, H, k, hsw);
+                else if (gram_x3)
+                    gram_accumulate_x3(sm, acc, tl, nslot, cols, rb, re, H, k, hsw);
                 else gram_accumulate<0>(sm, acc, tl, nslot, cols, rb, re, H, k, hsw, kdim);
             } else {
                 gram_accumulate<MODE>(sm, acc, tl, nslot, cols, rb, re, H, k, hsw, kdim);
