@@ -144,11 +144,10 @@ struct WrmfTilePlan {
     DeviceArray<float> sbuf;                      // refinement: s = L^{-1} r per Woodbury row
     // fp64 iterative refinement (wrmf_tile_refine): the residual's entry segments (rows with
     // several segments reduce their partials in order), x and r in fp64 for rows [r0, r1), the
-    // residual / correction rows in fp32 (W-shaped), a rocBLAS handle for X HH
+    // residual / correction rows in fp32 (W-shaped)
     int64_t r0 = 0, r1 = 0;
     DeviceArray<uint8_t> rsegs, rmulti;
     int64_t n_rsegs = 0, n_rmulti = 0, n_rslots = 0;
-    void* blas = nullptr;
     // fp64 mode: the direct rows keep their factor tiles (L_IJ, T_J = L_JJ^{-1}; light rows, then
     // heavy ones) so a refinement pass is two triangular solves (wrmf_tile_resolve_kernel).  Set
     // per half-step: false when the tiles do not fit the free HBM (the refinement then

@@ -25,8 +25,6 @@
 //   * backward substitution L^T w = y by 32-column blocks: w_J = T_J^T (y_J - sum_{I>J} L_IJ^T w_I).
 // Precision: fp32 with fused multiply-adds (the packed fp64 matrix of the parity path does not fit
 // the LDS at k > 128); the tolerance against the fp64 oracle is stated in tests/test_wrmf_gpu.py.
-#include <rocblas/rocblas.h>
-
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -2047,6 +2045,81 @@ __global__ __launch_bounds__(256) void wrmf_resid_multi_kernel(const RMulti* __r
 }
 
 // rows [r0, r0 + n): op 0 X = (double) W, 1 Rf = (float) R, 2 X += D, 3 W = (float) X
+// The refinement residual's dense part on the fp64 matrix cores: R = -X (HH + reg I) for the rows
+// of X ([n x k] fp64, row-major; HH symmetric, so X HH = (HH x_r^T)^T per row).  A workgroup takes
+// 64 rows and all k <= 256 columns: 4 waves x 16 rows, 16 column tiles of v_mfma_f64_16x16x4_f64
+// each (64 f64 accumulators per lane); K runs in chunks of 16 staged through LDS, HH's chunk
+// (16 x 256) shared by the 4 waves, double-buffered so the next chunk's loads fly during the
+// current chunk's 64 MFMAs per wave.  (Replaces the rocBLAS dgemm: the training path links no
+// vendor BLAS.)
+using f64x4 = __attribute__((ext_vector_type(4))) double;
+constexpr int kXB = 64, kXK = 16, kXN = 256, kXNP = kXN + 2, kXKP = kXK + 1;
+__global__ __launch_bounds__(256) void wrmf_xhh_kernel(const double* __restrict__ X,
+                                                       const double* __restrict__ HH, int64_t n,
+                                                       int32_t k, double reg,
+                                                       double* __restrict__ R) {
+    __shared__ double sb[2][kXK][kXNP];
+    __shared__ double sa[2][kXB][kXKP];
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, i = lane & 15, kk = lane >> 4;
+    const int nk = (k + kXK - 1) / kXK;
+    for (int64_t r0 = (int64_t)blockIdx.x * kXB; r0 < n; r0 += (int64_t)gridDim.x * kXB) {
+        f64x4 acc[16];
+#pragma unroll
+        for (int jt = 0; jt < 16; ++jt) acc[jt] = f64x4{0.0, 0.0, 0.0, 0.0};
+        // staging of chunk c into buffer bb: HH rows c*16 .. +16 (all columns), X rows r0 .. r0+64
+        // columns c*16 .. +16; zero past k and past n
+        double hv[16], xv[4];
+        auto load = [&](int c) {
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {  // 16 x 256 HH values: thread t -> row x, column t
+                const int f = c * kXK + x;
+                hv[x] = (f < k && t < k) ? HH[(int64_t)f * k + t] : 0.0;
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {  // 64 x 16 X values: thread t -> row t / 4, col 4(t%4)+x
+                const int64_t row = r0 + (t >> 2);
+                const int f = c * kXK + 4 * (t & 3) + x;
+                xv[x] = (row < n && f < k) ? X[row * k + f] : 0.0;
+            }
+        };
+        auto store = [&](int bb) {
+#pragma unroll
+            for (int x = 0; x < 16; ++x) sb[bb][x][t] = hv[x];
+#pragma unroll
+            for (int x = 0; x < 4; ++x) sa[bb][t >> 2][4 * (t & 3) + x] = xv[x];
+        };
+        load(0);
+        __syncthreads();  // the previous row block's last chunk has been read
+        store(0);
+        __syncthreads();
+        for (int c = 0; c < nk; ++c) {
+            const int bb = c & 1;
+            if (c + 1 < nk) load(c + 1);  // in flight during this chunk's MFMAs
+#pragma unroll
+            for (int s = 0; s < kXK / 4; ++s) {
+                const double a = sa[bb][16 * wave + i][4 * s + kk];
+#pragma unroll
+                for (int jt = 0; jt < 16; ++jt)
+                    acc[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, sb[bb][4 * s + kk][16 * jt + i],
+                                                                   acc[jt], 0, 0, 0);
+            }
+            if (c + 1 < nk) store(bb ^ 1);
+            __syncthreads();
+        }
+        // D layout: column 16 jt + (lane & 15), row 4 v + (lane >> 4) of the wave's 16 rows
+#pragma unroll
+        for (int jt = 0; jt < 16; ++jt) {
+            const int col = 16 * jt + i;
+            if (col >= k) continue;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int64_t row = r0 + 16 * wave + 4 * v + kk;
+                if (row < n) R[row * k + col] = -acc[jt][v] - reg * X[row * k + col];
+            }
+        }
+    }
+}
+
 // op 0: X = W; 1: Rf = R; 2: X += D, and dmax = max |D| / (1 + |X|) over the rows (the size of
 // the correction relative to the solution: the error the pass removed); 3: W = X
 __global__ __launch_bounds__(256) void wrmf_refine_rows_kernel(int op, int64_t r0, int64_t n,
@@ -2174,9 +2247,7 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
     MML_HIP(hipStreamSynchronize(st));
 }
 
-WrmfTilePlan::~WrmfTilePlan() {
-    if (blas) (void)rocblas_destroy_handle(reinterpret_cast<rocblas_handle>(blas));
-}
+WrmfTilePlan::~WrmfTilePlan() = default;
 
 // a further pass runs while the last correction was larger than this (relative to 1 + |x|).  The
 // error left after a pass is the correction times the pass's contraction, which the fp32 solver
@@ -2191,15 +2262,6 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
                          float* corrections) {
     const int64_t n = p.r1 - p.r0, n_w = (int64_t)(p.r1);  // W rows addressed up to r1
     if (passes <= 0 || n <= 0) return 0;
-    if (!p.blas) {
-        rocblas_handle bh = nullptr;
-        if (rocblas_create_handle(&bh) != rocblas_status_success)
-            fail(MML_ERR_HIP, "rocblas_create_handle failed");
-        p.blas = bh;
-    }
-    auto bh = reinterpret_cast<rocblas_handle>(p.blas);
-    if (rocblas_set_stream(bh, st) != rocblas_status_success)
-        fail(MML_ERR_HIP, "rocblas_set_stream failed");
     p.ws->x64.alloc((size_t)n * k);
     p.ws->r64.alloc((size_t)n * k);
     p.ws->rf.alloc((size_t)n_w * k);
@@ -2214,16 +2276,12 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
         ++launches;
     };
     rows(0);
-    const double m1 = -1.0, mreg = -reg;
     int32_t done = 0;
     for (int32_t pass = 0; pass < passes; ++pass) {
-        // R = -(HH + reg I) X, then + sum_i c_i h_i per row
-        MML_HIP(hipMemcpyAsync(p.ws->r64.get(), p.ws->x64.get(), sizeof(double) * n * k,
-                               hipMemcpyDeviceToDevice, st));
-        if (rocblas_dgemm(bh, rocblas_operation_none, rocblas_operation_none, k, (rocblas_int)n, k,
-                          &m1, HH, k, p.ws->x64.get(), k, &mreg, p.ws->r64.get(), k) !=
-            rocblas_status_success)
-            fail(MML_ERR_HIP, "rocblas_dgemm failed");
+        // R = -X (HH + reg I) on the fp64 matrix cores, then + sum_i c_i h_i per row
+        const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((n + kXB - 1) / kXB, 2048));
+        wrmf_xhh_kernel<<<gx, 256, 0, st>>>(p.ws->x64.get(), HH, n, k, reg, p.ws->r64.get());
+        ++launches;
         if (p.n_rsegs > 0) {
             const int gs = (int)std::min<int64_t>((p.n_rsegs + 3) / 4, 8192);  // 4 waves
             wrmf_resid_seg_kernel<<<gs, 256, 0, st>>>(

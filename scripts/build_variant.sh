@@ -19,6 +19,6 @@ for f in *.cpp; do
   objs+=("$out/${f%.cpp}.o")
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/libmml_hip.so" "${objs[@]}" -L/opt/rocm/lib -lrccl -lrocblas -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/libmml_hip.so" "${objs[@]}" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f "${objs[@]}"
 echo "$out/libmml_hip.so"
