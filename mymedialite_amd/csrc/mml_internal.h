@@ -99,6 +99,12 @@ struct DeviceArray {
         MML_HIP(hipMalloc(reinterpret_cast<void**>(&ptr), n * sizeof(T)));
         count = n;
     }
+    // at least n elements, keeping a larger block (buffers shared by passes of different sizes:
+    // no free / malloc round trip per use)
+    void reserve(size_t n) {
+        if (n <= count && ptr) return;
+        alloc(n);
+    }
     T* get() const { return ptr; }
     void swap(DeviceArray& o) noexcept {
         std::swap(ptr, o.ptr);

@@ -1687,14 +1687,14 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
                     const float* S) {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, 256 * 4));
     // main solve: relative residual 1e-6 (fp32 CG stagnates not far below: a tighter target
-    // just runs to max_it on trained factors).  A refinement correction d needs only 3e-3: x is
-    // already within ~1e-6 of the solution, so d's own error leaves ~3e-9 after x += d, below the
-    // float W's rounding (the fp64 tests measure the same errors at 1e-4, 3e-3 and 1e-2; C5's
-    // refinement CG 1e-4 -> 3e-3: 278 -> 254 ms per iteration).  max_it = the steps the
-    // cond(C) <= 1 + alpha bound needs, + 4
+    // just runs to max_it on trained factors).  A refinement correction d: 1e-4, so that one
+    // pass takes x from the fp32 solve's error (up to ~1e-4 on ill-conditioned rows) to <= ~1e-8
+    // (round 2 ran 3e-3, 24 ms per C5 iteration cheaper, which left rows whose first correction
+    // was 6e-5 at 2e-7 of the fp64 solution; tests/test_wrmf_gpu.py exact_product).  max_it = the
+    // steps the cond(C) <= 1 + alpha bound needs, + 4
     static const double refine_tol = [] {
         const char* e = MML_EXPERIMENT_ENV("MML_WRMF_REFINE_TOL");
-        return e ? std::atof(e) : 3e-3;
+        return e ? std::atof(e) : 1e-4;
     }();
     const double tol = S ? refine_tol : 1e-6;
     const double rho = (std::sqrt(1.0 + alpha) - 1.0) / (std::sqrt(1.0 + alpha) + 1.0);
@@ -2250,11 +2250,12 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
 WrmfTilePlan::~WrmfTilePlan() = default;
 
 // a further pass runs while the last correction was larger than this (relative to 1 + |x|).  The
-// error left after a pass is the correction times the pass's contraction, which the fp32 solver
-// (fp32 L^-1 and a 3e-3 CG for the Woodbury rows, the fp32 factor for the direct rows) keeps
-// below ~0.05 on the test sets: 2e-6 leaves <= 1e-7.  The fp32 solve of a well-conditioned system
-// (C5) is ~1e-6 off, so one pass; cond ~1e4 (fp32 6e-5 off) takes two or three.
-constexpr float kRefineStop = 2e-6f;
+// error left after a pass is the correction times the pass's contraction: the kept fp32 factor's
+// accuracy for direct rows (measured 2e-5 .. 3e-6: C5's largest item correction 1.1e-4 was
+// followed by 3e-10) and, for Woodbury rows, the refinement CG's tolerance (1e-4 times
+// cond(C) <= 1 + alpha).  1e-3 therefore leaves <= ~5e-7 in the worst case and ~1e-8 typically;
+// every set measured so far (tests, C5) stops after one pass.
+constexpr float kRefineStop = 1e-3f;
 
 int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H,
                          int64_t h_rows, const int64_t* off, const int32_t* cols, const double* HH,
@@ -2262,11 +2263,11 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
                          float* corrections) {
     const int64_t n = p.r1 - p.r0, n_w = (int64_t)(p.r1);  // W rows addressed up to r1
     if (passes <= 0 || n <= 0) return 0;
-    p.ws->x64.alloc((size_t)n * k);
-    p.ws->r64.alloc((size_t)n * k);
-    p.ws->rf.alloc((size_t)n_w * k);
-    p.ws->df.alloc((size_t)n_w * k);
-    p.ws->rpartial.alloc(std::max<int64_t>(1, p.n_rslots) * (size_t)k);
+    p.ws->x64.reserve((size_t)n * k);
+    p.ws->r64.reserve((size_t)n * k);
+    p.ws->rf.reserve((size_t)n_w * k);
+    p.ws->df.reserve((size_t)n_w * k);
+    p.ws->rpartial.reserve(std::max<int64_t>(1, p.n_rslots) * (size_t)k);
     if (!p.ws->dmax.get()) p.ws->dmax.alloc(1);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n * k + 255) / 256, 16384));
     auto rows = [&](int op) {
@@ -2388,7 +2389,9 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             size_t free_b = 0, total_b = 0;
             MML_HIP(hipMemGetInfo(&free_b, &total_b));
             const size_t have = free_b + p.ws->factor.count * sizeof(float);
-            if (need * sizeof(float) + total_b / 16 > have) {
+            if (need <= p.ws->factor.count) {
+                F = p.ws->factor.get();  // the shared workspace already holds enough
+            } else if (need * sizeof(float) + total_b / 16 > have) {
                 p.keep_factor = false;
                 p.ws->factor.reset();
             } else {
