@@ -1687,14 +1687,14 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
                     const float* S) {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, 256 * 4));
     // main solve: relative residual 1e-6 (fp32 CG stagnates not far below: a tighter target
-    // just runs to max_it on trained factors).  A refinement correction d: 1e-4, so that one
-    // pass takes x from the fp32 solve's error (up to ~1e-4 on ill-conditioned rows) to <= ~1e-8
-    // (round 2 ran 3e-3, 24 ms per C5 iteration cheaper, which left rows whose first correction
-    // was 6e-5 at 2e-7 of the fp64 solution; tests/test_wrmf_gpu.py exact_product).  max_it = the
-    // steps the cond(C) <= 1 + alpha bound needs, + 4
+    // just runs to max_it on trained factors).  A refinement correction d: 3e-3.  The pass's
+    // contraction on Woodbury rows is set by fp32 rounding in the CG as much as by this target
+    // (1e-4 measured 0.027 .. 0.06 on the tests' sets, no better than 3e-3), so the error left is
+    // bounded by further passes instead (kRefineStopWood), and C5, whose Woodbury corrections are
+    // ~1e-8, keeps the cheaper target.  max_it = the steps the cond(C) <= 1 + alpha bound needs, + 4
     static const double refine_tol = [] {
         const char* e = MML_EXPERIMENT_ENV("MML_WRMF_REFINE_TOL");
-        return e ? std::atof(e) : 1e-4;
+        return e ? std::atof(e) : 3e-3;
     }();
     const double tol = S ? refine_tol : 1e-6;
     const double rho = (std::sqrt(1.0 + alpha) - 1.0) / (std::sqrt(1.0 + alpha) + 1.0);
@@ -2120,16 +2120,19 @@ __global__ __launch_bounds__(256) void wrmf_xhh_kernel(const double* __restrict_
     }
 }
 
-// op 0: X = W; 1: Rf = R; 2: X += D, and dmax = max |D| / (1 + |X|) over the rows (the size of
-// the correction relative to the solution: the error the pass removed); 3: W = X
+// op 0: X = W; 1: Rf = R; 2: X += D, and dmax[t] = max |D| / (1 + |X|) over the rows of type t
+// (0 direct, 1 Woodbury: 1 <= deg <= kWood when wood): the size of the correction relative to the
+// solution, i.e. the error the pass removed; 3: W = X
 __global__ __launch_bounds__(256) void wrmf_refine_rows_kernel(int op, int64_t r0, int64_t n,
                                                                int32_t k, float* __restrict__ W,
                                                                double* __restrict__ X,
                                                                const double* __restrict__ R,
                                                                float* __restrict__ Rf,
                                                                const float* __restrict__ D,
+                                                               const int64_t* __restrict__ off,
+                                                               int wood,
                                                                unsigned* __restrict__ dmax) {
-    float m = 0.0f;
+    float m[2] = {0.0f, 0.0f};
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * k;
          e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t g = r0 * k + e;
@@ -2139,16 +2142,21 @@ __global__ __launch_bounds__(256) void wrmf_refine_rows_kernel(int op, int64_t r
             case 2: {
                 const double x = X[e] + (double)D[g];
                 X[e] = x;
-                m = fmaxf(m, (float)(fabs((double)D[g]) / (1.0 + fabs(x))));
+                const int64_t r = r0 + e / k, deg = off[r + 1] - off[r];
+                const float c = (float)(fabs((double)D[g]) / (1.0 + fabs(x)));
+                if (wood && deg >= 1 && deg <= 128) m[1] = fmaxf(m[1], c);
+                else m[0] = fmaxf(m[0], c);
                 break;
             }
             default: W[g] = (float)X[e]; break;
         }
     }
-    if (op == 2) {  // non-negative floats order like their bit patterns
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-        if ((threadIdx.x & 63) == 0 && m > 0.0f) atomicMax(dmax, __float_as_uint(m));
-    }
+    if (op == 2)  // non-negative floats order like their bit patterns
+        for (int t = 0; t < 2; ++t) {
+            float v = m[t];
+            for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+            if ((threadIdx.x & 63) == 0 && v > 0.0f) atomicMax(dmax + t, __float_as_uint(v));
+        }
 }
 
 constexpr int kHeavy = 8192;   // rows with more entries take the split Gram
@@ -2163,6 +2171,7 @@ namespace mml {
 void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p, int64_t r0,
                     int64_t r1, bool woodbury) {
     const int32_t n = (int32_t)deg.size();
+    p.woodbury = woodbury;
     // light rows by degree, descending (longest first: the work queue then ends on short rows)
     std::vector<int32_t> light, heavy;
     std::vector<int64_t> begin(n + 1, 0);
@@ -2249,13 +2258,15 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
 
 WrmfTilePlan::~WrmfTilePlan() = default;
 
-// a further pass runs while the last correction was larger than this (relative to 1 + |x|).  The
-// error left after a pass is the correction times the pass's contraction: the kept fp32 factor's
-// accuracy for direct rows (measured 2e-5 .. 3e-6: C5's largest item correction 1.1e-4 was
-// followed by 3e-10) and, for Woodbury rows, the refinement CG's tolerance (1e-4 times
-// cond(C) <= 1 + alpha).  1e-3 therefore leaves <= ~5e-7 in the worst case and ~1e-8 typically;
-// every set measured so far (tests, C5) stops after one pass.
-constexpr float kRefineStop = 1e-3f;
+// a further pass runs while the last correction was larger than these (relative to 1 + |x|), per
+// row type.  The error left after a pass is the correction times the pass's contraction.  Direct
+// rows solve the correction on the kept fp32 factor: contraction 3e-6 .. 2e-5 measured (C5's
+// largest item correction 1.1e-4 was followed by 3e-10), so 3e-4 leaves <= ~6e-9.  Woodbury rows
+// solve it by the fp32 CG at launch_wood_cg's refinement tolerance: contraction up to 0.06 measured on the tests'
+// ill-conditioned small sets (a 3.4e-5 correction left 9.4e-7), so 2e-6 leaves <= ~1.2e-7.  C5
+// (users Woodbury, corrections ~1e-8; items direct, ~1e-4) stops after one pass.
+constexpr float kRefineStopDirect = 3e-4f;
+constexpr float kRefineStopWood = 2e-6f;
 
 int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H,
                          int64_t h_rows, const int64_t* off, const int32_t* cols, const double* HH,
@@ -2268,12 +2279,13 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
     p.ws->rf.reserve((size_t)n_w * k);
     p.ws->df.reserve((size_t)n_w * k);
     p.ws->rpartial.reserve(std::max<int64_t>(1, p.n_rslots) * (size_t)k);
-    if (!p.ws->dmax.get()) p.ws->dmax.alloc(1);
+    if (!p.ws->dmax.get()) p.ws->dmax.alloc(2);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n * k + 255) / 256, 16384));
     auto rows = [&](int op) {
         wrmf_refine_rows_kernel<<<grid, 256, 0, st>>>(op, p.r0, n, k, W, p.ws->x64.get(),
                                                       p.ws->r64.get(), p.ws->rf.get(),
-                                                      p.ws->df.get(), p.ws->dmax.get());
+                                                      p.ws->df.get(), off, p.woodbury ? 1 : 0,
+                                                      p.ws->dmax.get());
         ++launches;
     };
     rows(0);
@@ -2298,19 +2310,19 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
         // D = A^{-1} R on the fp32 solver (rows outside [r0, r1) are not read)
         wrmf_tile_solve(st, p, p.ws->df.get(), H, h_rows, off, cols, HH, k, alpha, reg, launches,
                         p.ws->rf.get());
-        MML_HIP(hipMemsetAsync(p.ws->dmax.get(), 0, sizeof(unsigned), st));
+        MML_HIP(hipMemsetAsync(p.ws->dmax.get(), 0, 2 * sizeof(unsigned), st));
         rows(2);
         launches += 3;
         ++done;
         if (pass + 1 < passes) {  // another pass only while the correction was large
-            unsigned bits = 0;
-            MML_HIP(hipMemcpyAsync(&bits, p.ws->dmax.get(), sizeof(unsigned),
-                                   hipMemcpyDeviceToHost, st));
+            unsigned bits[2] = {0, 0};
+            MML_HIP(hipMemcpyAsync(bits, p.ws->dmax.get(), sizeof(bits), hipMemcpyDeviceToHost,
+                                   st));
             MML_HIP(hipStreamSynchronize(st));
-            float d;
-            std::memcpy(&d, &bits, sizeof(d));
-            if (corrections && pass < 4) corrections[pass] = d;
-            if (!(d > kRefineStop)) break;
+            float d[2];
+            std::memcpy(d, bits, sizeof(d));
+            if (corrections && pass < 4) corrections[pass] = std::max(d[0], d[1]);
+            if (!(d[0] > kRefineStopDirect) && !(d[1] > kRefineStopWood)) break;
         }
     }
     rows(3);

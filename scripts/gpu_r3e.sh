@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 3: WRMF after the grow-only refinement workspace and the 1e-4 refinement CG: the WRMF
+# Round 3: WRMF after the grow-only refinement workspace and the per-row-type refinement stop: the WRMF
 # tests, C5 with and without the ring Gram, kernel profiles of both.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -13,7 +13,8 @@ step() {  # step <name> <seconds> <command...>
     local rc=$?
     echo "$name rc=$rc"
     tail -2 "gpurun_out/${name}_$TAG.log" | cut -c1-300
-    [ $rc -eq 0 ] || exit $rc
+    # a pytest failure (rc 1) of a test step is read afterwards; anything else ends the call
+    [ $rc -eq 0 ] || { [ $rc -eq 1 ] && [ "$name" = wrmf ]; } || exit $rc
 }
 keep_stats() {  # keep_stats <dir>: the kernel stats CSV only
     local f
@@ -21,7 +22,7 @@ keep_stats() {  # keep_stats <dir>: the kernel stats CSV only
     cp "$f" "$1_kernel_stats.csv"
     rm -rf "$1"
 }
-step wrmf 900 python -u -m pytest tests/test_wrmf_gpu.py -v -s --timeout 200 --timeout-method thread -k "large_k or woodbury or refinement or exact"
+step wrmf 900 python -u -m pytest tests/test_wrmf_gpu.py -v -s --timeout 200 --timeout-method thread -k "exact or refinement"
 step c5 300 python -u bench.py --workload c5 --steps 2 --warmup 1 --no-cpu-baseline
 step prof_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c5_$TAG -o c5 -- python bench.py --workload c5 --steps 1 --warmup 1 --no-cpu-baseline
 keep_stats gpurun_out/prof_c5_$TAG

@@ -197,10 +197,11 @@ def _woodbury_set(k):
     return np.array(us, np.int32), np.array(its, np.int32), 420
 
 
-# One iteration: the first half-step of a second iteration starts from factors that the device
-# and the oracle each rounded to float from fp64 solutions ~1e-9 apart, so a few entries differ by
-# one ulp (6e-8), and cond(A) ~1e4 amplifies that past 2e-7 whatever the solver (measured at two
-# iterations: 2.1e-7, 7.6e-6, 1.05e-6 with the refinement converged to 1e-8..1e-11 in every pass).
+# Each half-step is checked against the exact-product solve of the system it was given: the users
+# from the shared initial item factors, the items from the DEVICE's user floats.  (Chained through
+# the oracle's own user floats instead, entries whose fp64 solutions sit ~1e-9 apart round to
+# different floats, one ulp = 6e-8, and the item Gram's cond(A) ~1e4 amplifies that past 2e-7
+# whatever the solver: measured 2.3e-6 at k=256 alpha=4 with both half-steps refined to <= 3e-8.)
 @pytest.mark.parametrize("case,k,alpha,iters", [
     ("small", 129, 1.0, 1), ("small", 256, 1.0, 1),          # 120 items < k: cond ~1e4
     ("woodbury", 160, 1.0, 1), ("woodbury", 256, 4.0, 1),    # 280 users, Woodbury + direct rows
@@ -210,8 +211,8 @@ def test_wrmf_fp64_lands_on_exact_product_solution(case, k, alpha, iters):
     """what the fp64 refinement is worth, asserted on every set.  The residual
     b - A x is computed with exact float x float products, so the fp64 mode solves the system
     whose row Gram has exact products (oracle ora_wrmf_optimize_rows_exact; HH keeps
-    ComputeSquareMatrix's float products, WRMF.cs:94-108).  Against THAT solution the device lands
-    within 2e-7 (float parity) even where cond(A) ~ 1e4 puts both 1e-5 away from the
+    ComputeSquareMatrix's float products, WRMF.cs:94-108).  Against THAT solution each half-step
+    lands within 2e-7 (float parity) even where cond(A) ~ 1e4 puts both 1e-5 away from the
     float-product reference (the documented floor, test_wrmf_large_k_matches_oracle /
     test_wrmf_woodbury_and_direct_rows_match_oracle: 1e-4).  Reference: WRMF.cs:110-156."""
     if case == "small":
@@ -238,13 +239,21 @@ def test_wrmf_fp64_lands_on_exact_product_solution(case, k, alpha, iters):
     ran, corr = ctypes.c_int32(0), np.zeros(8, np.float32)
     N.check(N.lib().mml_wrmf_last_refine_passes(m._h, ctypes.byref(ran), N.ptr(corr, N._f32p)))
     print(f"refinement passes {ran.value}, max corrections users {corr[:4]} items {corr[4:]}")
-    de = max(_close(m.user_factors, exact["U"]), _close(m.item_factors, exact["V"]))
+    # the items half-step's exact-product solve from the device's user factors
+    ioff, icols = O.insertion_order_rows(i, u, ni)
+    v_given = np.zeros((ni, k), np.float32)
+    O.wrmf_optimize(ioff, icols, v_given, np.array(m.user_factors, np.float32), alpha, 0.015,
+                    exact_products=True)
+    de_u = _close(m.user_factors, exact["U"])
+    de_v = _close(m.item_factors, v_given)
+    chained = _close(m.item_factors, exact["V"])
     dr = max(_close(m.user_factors, ref["U"]), _close(m.item_factors, ref["V"]))
     floor = max(_close(exact["U"], ref["U"]), _close(exact["V"], ref["V"]))
-    print(f"WRMF {case} k={k} alpha={alpha}: fp64 vs exact-product oracle {de:.2e}, vs the "
+    print(f"WRMF {case} k={k} alpha={alpha}: fp64 vs exact-product solve users {de_u:.2e}, items "
+          f"{de_v:.2e} (chained through the oracle's user floats {chained:.2e}); vs the "
           f"reference's float products {dr:.2e} (the two oracles differ by {floor:.2e})")
-    assert de <= 2e-7
+    assert de_u <= 2e-7 and de_v <= 2e-7
     assert dr <= 1e-4
-    # the refinement ran until its correction was below 2e-6 (relative): one pass on the
-    # well-conditioned set, two where cond(A) ~1e4
+    # the refinement ran until its correction was below the per-row-type stop (wrmf_tiles.hip
+    # kRefineStopDirect / kRefineStopWood)
     assert 1 <= ran.value <= 3
