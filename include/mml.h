@@ -406,9 +406,10 @@ typedef struct {
     int32_t refine_passes; /* k > 128 (ABI 5): at most this many passes of fp64 iterative
                               refinement after the fp32 solve, x += A^{-1} (b - A x) with the
                               residual in fp64 (exact float products); a further pass runs only
-                              while the last correction exceeded 1e-4 relative (ABI 6): one pass
-                              reaches the fp64 solution on well-conditioned systems, cond ~1e4
-                              takes two (WRMF.cs:137-154); 0 = the fp32 result */
+                              while the last correction exceeded 3e-4 relative on a direct row
+                              or 2e-6 on a Woodbury row (the two solvers' contractions): one
+                              pass reaches the fp64 solution on well-conditioned systems,
+                              cond ~1e4 takes two (WRMF.cs:137-154); 0 = the fp32 result */
     double alpha;          /* Alpha (WRMF.cs:56) */
     double regularization; /* Regularization (WRMF.cs:59) */
 } mml_wrmf_params;
