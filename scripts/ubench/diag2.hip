@@ -1,7 +1,8 @@
 // Microbenchmark + check of wrmf_tiles.hip's diag_factor_mfma: T = L^{-1} of an SPD 32 x 32 tile
 // held in the v_mfma_f32_32x32x2_f32 C/D layout, by column pairs on the matrix core.  Prints the
 // cycles per factorisation (one wave, repeated) and max |T A T^T - I| against the input tile.
-// hipcc --offload-arch=gfx950 -O3 diag2.hip -o diag2
+// hipcc --offload-arch=gfx950 -O3 diag2.hip -o diag2 -mllvm -amdgpu-mfma-vgpr-form=1 (as in the
+// solve kernel, whose accumulators are VGPRs: AGPR accumulators add 2 x 16 moves per MFMA here)
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
