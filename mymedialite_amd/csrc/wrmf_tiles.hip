@@ -1567,7 +1567,8 @@ template <int NJ>
 __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_wood_cg_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, const int64_t* __restrict__ off,
     const int32_t* __restrict__ cols, const float* __restrict__ Q, int32_t k, float alpha,
-    const float* __restrict__ S, float* __restrict__ Tout, int32_t max_it, float tol2) {
+    const float* __restrict__ S, float* __restrict__ Tout, int32_t max_it, float tol2,
+    float skip2, float abs2) {
     static_assert(NJ == 32 || NJ == 64 || NJ == 128, "NJ: 32, 64 or 128");
     constexpr int HALVES = NJ > 64 ? 2 : 1;
     constexpr int WAVES = 4 * HALVES;
@@ -1589,6 +1590,19 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
         const int64_t rb = off[row];
         const int deg = (int)(off[row + 1] - rb);
         __syncthreads();  // the previous row is done with the LDS
+        float sf = 0.0f;
+        if (S) {
+            // refinement, d = L^-T (s - Q_S^T w) with C w = Q_S s: |d|_2 <= |L^-1|_2 |s|_2 (the
+            // middle factor I - Q_S^T C^-1 Q_S has norm <= 1), so a row whose bound is below the
+            // absolute target keeps d = 0 without gathering Q_S
+            sf = fon && half == 0 ? S[(int64_t)li * k + f] : 0.0f;
+            const float2 ss = block_sum2<WAVES>(sf * sf, 0.0f, sdot[1]);
+            if (ss.x <= skip2) {
+                if (fon && half == 0) Tout[(int64_t)li * k + f] = 0.0f;
+                continue;
+            }
+            if (half != 0) sf = fon ? S[(int64_t)li * k + f] : 0.0f;
+        }
         if (t < NJ) sid[t] = t < deg ? cols[rb + t] : 0;
         __syncthreads();
         float q[NL];
@@ -1636,9 +1650,8 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
             __syncthreads();
             return su[0][f] + su[1][f];
         };
-        float sf = 0.0f, y;
+        float y;
         if (S) {
-            sf = fon ? S[(int64_t)li * k + f] : 0.0f;
             y = qs_times(sf);
         } else {
             y = t < deg ? 1.0f : 0.0f;
@@ -1652,7 +1665,9 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
             const float cr = (t < deg ? r * ainv : 0.0f) + qs_times(uf);  // C r
             const float2 gd = block_sum2<WAVES>(t < NJ ? r * r : 0.0f, t < NJ ? cr * r : 0.0f,
                                                 sdot[it & 1]);
-            if (it == 0) stop = tol2 * gd.x;
+            // relative target, or (refinement) the absolute one: d's error from w's is at most
+            // |L^-1|_2 |C^-1|_2 |res| <= |L^-1|_2 alpha |res|
+            if (it == 0) stop = fmaxf(tol2 * gd.x, abs2);
             if (gd.x <= stop || it == max_it) break;
             const float b = it == 0 ? 0.0f : gd.x / g_prev;
             const float a = it == 0 ? gd.x / gd.y : gd.x / (gd.y - b * gd.x / a_prev);
@@ -1682,9 +1697,14 @@ bool wood_cg() {
     return v;
 }
 
+// the refinement's absolute target for a Woodbury row's correction d (2-norm, so also per entry
+// relative to 1 + |x|): far below the float rounding of W (6e-8 relative) and the fp64 mode's 2e-7
+constexpr double kWoodAbs = 1e-8;
+
+// lnorm: |L^{-1}|_2 (refinement only)
 void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const int64_t* off,
                     const int32_t* cols, const float* Q, int32_t k, float alpha, float* Tout,
-                    const float* S) {
+                    const float* S, double lnorm = 0.0) {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, 256 * 4));
     // main solve: relative residual 1e-6 (fp32 CG stagnates not far below: a tighter target
     // just runs to max_it on trained factors).  A refinement correction d: 3e-3.  The pass's
@@ -1700,15 +1720,17 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
     const double rho = (std::sqrt(1.0 + alpha) - 1.0) / (std::sqrt(1.0 + alpha) + 1.0);
     const int max_it = std::min(200, (int)std::ceil(std::log(tol) / std::log(rho)) + 4);
     const float tol2 = (float)(tol * tol);
+    const double sk = S && lnorm > 0.0 ? kWoodAbs / lnorm : 0.0, ab = sk / alpha;
+    const float skip2 = S ? (float)(sk * sk) : -1.0f, abs2 = (float)(ab * ab);
     if (g == 0)
         wrmf_wood_cg_kernel<32><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
-                                                      max_it, tol2);
+                                                      max_it, tol2, skip2, abs2);
     else if (g == 1)
         wrmf_wood_cg_kernel<64><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
-                                                      max_it, tol2);
+                                                      max_it, tol2, skip2, abs2);
     else
         wrmf_wood_cg_kernel<128><<<grid, 512, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
-                                                       max_it, tol2);
+                                                       max_it, tol2, skip2, abs2);
 }
 
 // Y[yrow(r)] = scale * X[xrow(r)] * M for n rows (X, Y row-major [.. x k], M [k x k] row-major,
@@ -2355,6 +2377,33 @@ static void chol_inverse(const std::vector<double>& HH, int k, double reg, std::
         }
 }
 
+// |Li|_2 of a lower-triangular k x k matrix: sqrt of the largest eigenvalue of Li^T Li by power
+// iteration (60 steps from a fixed start), times 1.25.  Power iteration approaches the eigenvalue
+// from below; the margin covers what 60 steps leave when the top eigenvalues are close.
+static double spectral_norm_lower(const std::vector<double>& Li, int k) {
+    std::vector<double> v(k), u(k);
+    for (int i = 0; i < k; ++i) v[i] = 1.0 + 0.001 * (i % 7);
+    double lam = 0.0;
+    for (int it = 0; it < 60; ++it) {
+        double nv = 0.0;
+        for (double x : v) nv += x * x;
+        nv = std::sqrt(nv);
+        for (double& x : v) x /= nv;
+        for (int i = 0; i < k; ++i) {  // u = Li v
+            double a = 0.0;
+            for (int j = 0; j <= i; ++j) a += Li[(size_t)i * k + j] * v[j];
+            u[i] = a;
+        }
+        double uu = 0.0;
+        for (double x : u) uu += x * x;
+        lam = uu;  // v^T Li^T Li v, |v| = 1
+        std::fill(v.begin(), v.end(), 0.0);  // v = Li^T u
+        for (int i = 0; i < k; ++i)
+            for (int j = 0; j <= i; ++j) v[j] += Li[(size_t)i * k + j] * u[i];
+    }
+    return 1.25 * std::sqrt(lam);
+}
+
 void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
                      const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
                      double alpha, double reg, int& launches, const float* rhs) {
@@ -2456,7 +2505,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                         1.0f, p.sbuf.get(), nullptr);
             if (wood_cg()) {
                 launch_wood_cg(st, g, p.wood[g].get(), p.n_wood[g], off, cols, p.qbuf.get(), k,
-                               (float)alpha, p.tbuf.get(), p.sbuf.get());
+                               (float)alpha, p.tbuf.get(), p.sbuf.get(), p.linv_norm);
             } else {
                 auto* L = g == 0 ? &launch_wood<1> : g == 1 ? &launch_wood<2>
                           : g == 2 ? &launch_wood<3> : &launch_wood<4>;
@@ -2476,6 +2525,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
     MML_HIP(hipMemcpyAsync(hh.data(), HH, sizeof(double) * hh.size(), hipMemcpyDeviceToHost, st));
     MML_HIP(hipStreamSynchronize(st));
     chol_inverse(hh, k, reg, li);
+    p.linv_norm = spectral_norm_lower(li, k);
     std::vector<float> lf((size_t)k * k), ltf((size_t)k * k);
     for (int i = 0; i < k; ++i)
         for (int j = 0; j < k; ++j) {
