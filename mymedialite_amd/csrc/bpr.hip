@@ -248,6 +248,44 @@ __device__ __forceinline__ bool row_has(const int32_t* __restrict__ cols, int64_
     return lo < re && cols[lo] == j;
 }
 
+// Per-user Bloom filter of S_u (512 bits = one 64-B line per user, three bits per item): the
+// rejection test of j reads the user's line and scans the row only when all three bits are set.
+// No false negatives, so the accepted j are exactly those of the plain test; for uniform j the
+// scan then runs with probability ~(1 - e^{-3 deg / 512})^3 (1.6 % at deg 50) instead of always:
+// one line per draw instead of the 2-3 lines of an unaligned row.
+constexpr int kBloomWords = 16;
+__device__ __forceinline__ void bloom_bits(int32_t j, uint32_t& b0, uint32_t& b1, uint32_t& b2) {
+    const uint64_t x = (uint64_t)(uint32_t)j * 0x9E3779B97F4A7C15ull;
+    b0 = (uint32_t)(x >> 55);
+    b1 = (uint32_t)(x >> 46) & 511u;
+    b2 = (uint32_t)(x >> 37) & 511u;
+}
+__device__ __forceinline__ bool bloom_maybe(const uint32_t* __restrict__ bl, int32_t j) {
+    uint32_t b0, b1, b2;
+    bloom_bits(j, b0, b1, b2);
+    return ((bl[b0 >> 5] >> (b0 & 31)) & (bl[b1 >> 5] >> (b1 & 31)) & (bl[b2 >> 5] >> (b2 & 31)) &
+            1u) != 0;
+}
+// 16 lanes per user, lane w owns word w of the user's filter
+__global__ __launch_bounds__(256) void bpr_bloom_build_kernel(const int64_t* __restrict__ off,
+                                                              const int32_t* __restrict__ cols,
+                                                              int32_t n_users,
+                                                              uint32_t* __restrict__ bloom) {
+    const int w = threadIdx.x & (kBloomWords - 1);
+    for (int64_t u = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kBloomWords; u < n_users;
+         u += (int64_t)gridDim.x * blockDim.x / kBloomWords) {
+        uint32_t word = 0;
+        for (int64_t e = off[u]; e < off[u + 1]; ++e) {
+            uint32_t b0, b1, b2;
+            bloom_bits(cols[e], b0, b1, b2);
+            if ((int)(b0 >> 5) == w) word |= 1u << (b0 & 31);
+            if ((int)(b1 >> 5) == w) word |= 1u << (b1 & 31);
+            if ((int)(b2 >> 5) == w) word |= 1u << (b2 & 31);
+        }
+        bloom[u * kBloomWords + w] = word;
+    }
+}
+
 // SAMPLER: MML_BPR_SAMPLER_*.  eligible == nullptr: every user is eligible (u = the draw itself,
 // no gather).  WEIGHTED (WeightedBPRMF.SampleTriple): (u, i) = event draw 0, j = the item of event
 // draw d until j is not in S_u -- capped at kMaxWeightedDraws, after which the sample is flagged
@@ -261,7 +299,8 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
     const int32_t* __restrict__ eligible, int32_t n_eligible, const int32_t* __restrict__ ev_u,
     const int32_t* __restrict__ ev_i, int64_t n_samples, int32_t n_items, uint64_t seed,
     int32_t* __restrict__ tu, int32_t* __restrict__ ti, int32_t* __restrict__ tj,
-    int32_t* __restrict__ fail, uint64_t* __restrict__ user_keys) {
+    int32_t* __restrict__ fail, uint64_t* __restrict__ user_keys,
+    const uint32_t* __restrict__ bloom) {
     for (int64_t smp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; smp < n_samples;
          smp += (int64_t)gridDim.x * blockDim.x) {
         int32_t u, i = 0, j = 0;
@@ -278,6 +317,8 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
             u = eligible ? eligible[du] : (int32_t)du;
         }
         const int64_t rb = off[u], re = off[u + 1];
+        const uint32_t* bl = bloom + (int64_t)u * kBloomWords;
+        auto in_row = [&](int32_t c) { return bloom_maybe(bl, c) && row_has(cols, rb, re, c); };
         if constexpr (SAMPLER == MML_BPR_SAMPLER_UNIFORM_USER)
             i = cols[rb + draw(seed, smp, 1, (uint32_t)(re - rb))];
         // USER_REPLACEMENT: i is resolved after the epoch's samples are ranked per user
@@ -287,7 +328,7 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
             uint32_t d = 1;
             for (; d <= kMaxWeightedDraws; ++d) {
                 j = ev_i[draw(seed, smp, d, (uint32_t)n_samples)];
-                if (!row_has(cols, rb, re, j)) break;
+                if (!in_row(j)) break;
             }
             if (d > kMaxWeightedDraws) {
                 atomicOr(fail, 1);
@@ -296,7 +337,7 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
         } else {
             for (uint32_t d = 2;; ++d) {
                 j = (int32_t)draw(seed, smp, d, (uint32_t)n_items);
-                if (!row_has(cols, rb, re, j)) break;
+                if (!in_row(j)) break;
             }
         }
         tu[smp] = u;
@@ -591,6 +632,7 @@ struct mml_bpr {
     mml::DeviceArray<int32_t> cols, eligible, ev_u, ev_i, q_u, q_i;
     mml::DeviceArray<int32_t> tri_u, tri_i, tri_j;  // the epoch's triples (two-phase epoch)
     mml::DeviceArray<int32_t> fail;                 // WEIGHTED sampler: a sample ran out of draws
+    mml::DeviceArray<uint32_t> bloom;               // per-user Bloom filter of S_u (sampler)
     mml::DeviceArray<uint64_t> rank_keys, rank_sorted;  // USER_REPLACEMENT: (u << 32 | s)
     mml::DeviceArray<int64_t> rank_head;                // USER_REPLACEMENT: first position per user
     mml::DeviceArray<uint8_t> rank_tmp;                 // its radix-sort scratch
@@ -766,6 +808,10 @@ void bpr_ingest(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t 
     h->off.swap(csr.off);
     h->cols.swap(csr.cols);
     h->nnz = csr.nnz;
+    h->bloom.alloc((size_t)h->n_users * kBloomWords);
+    bpr_bloom_build_kernel<<<grid_for((int64_t)h->n_users * kBloomWords), 256, 0, st>>>(
+        h->off.get(), h->cols.get(), h->n_users, h->bloom.get());
+    MML_HIP(hipGetLastError());
     h->n_events = n;
     h->n_eligible = (int32_t)elig.size();
     h->eligible.alloc(elig.size());
@@ -1209,7 +1255,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
     bpr_sample_kernel<KIND><<<sgrid, 256, 0, st>>>(                                            \
         h->off.get(), h->cols.get(), ELIG, h->n_eligible, h->ev_u.get(), h->ev_i.get(), n,    \
         h->n_items, seed, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), h->fail.get(),       \
-        h->rank_keys.get())
+        h->rank_keys.get(), h->bloom.get())
             int32_t* elig = h->n_eligible == h->n_users ? nullptr : h->eligible.get();
             switch (h->p.sampler) {
                 case MML_BPR_SAMPLER_UNIFORM_PAIR:
