@@ -1499,6 +1499,29 @@ __device__ __forceinline__ float tstage(float a, float b, int lane) {  // a = v[
         return (lo ? a : b) + partner_of<STAGE>(lo ? b : a);
     }
 }
+// two independent tstage's on packed pairs (a.x with b.x, a.y with b.y): the swaps stay per
+// register, the products and the sums after them become v_pk_mul_f32 / v_pk_add_f32
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+template <int STAGE>
+__device__ __forceinline__ f32x2 tstage2(f32x2 a, f32x2 b, int lane) {
+    if constexpr (STAGE == 0 || STAGE == 1) {
+        const auto r0 = STAGE == 0 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x),
+                                                                       __float_as_uint(b.x), false,
+                                                                       false)
+                                   : __builtin_amdgcn_permlane16_swap(__float_as_uint(a.x),
+                                                                       __float_as_uint(b.x), false,
+                                                                       false);
+        const auto r1 = STAGE == 0 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y),
+                                                                       __float_as_uint(b.y), false,
+                                                                       false)
+                                   : __builtin_amdgcn_permlane16_swap(__float_as_uint(a.y),
+                                                                       __float_as_uint(b.y), false,
+                                                                       false);
+        return f32x2{fbits(r0[0]), fbits(r1[0])} + f32x2{fbits(r0[1]), fbits(r1[1])};
+    } else {
+        return f32x2{tstage<STAGE>(a.x, b.x, lane), tstage<STAGE>(a.y, b.y, lane)};
+    }
+}
 template <int STAGE>
 __device__ __forceinline__ float pstage(float x) {  // x + the partner's x
     if constexpr (STAGE == 0) {
@@ -1613,17 +1636,23 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
         }
         // z_j (thread j < NJ) = sum_f Q_S[j][f] uf; the first three butterfly stages (xor 32,
         // 16, 8) are fused per group of 8 products, so only NL / 8 partial sums sit next to q
+        static_assert(E % 2 == 0, "packed pairs of partial sums");
         auto qs_times = [&](float uf) -> float {
             float v[E];
+            const f32x2 u2 = {uf, uf};
 #pragma unroll
-            for (int x = 0; x < E; ++x) {
-                float s1[4], s2[2];
+            for (int x = 0; x < E; x += 2) {  // partial sums x and x + 1 as packed pairs
+                f32x2 s1[4], s2[2];
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    s1[c] = tstage<0>(q[x + c * E] * uf, q[x + (c + 4) * E] * uf, lane);
+                    s1[c] = tstage2<0>(f32x2{q[x + c * E], q[x + 1 + c * E]} * u2,
+                                       f32x2{q[x + (c + 4) * E], q[x + 1 + (c + 4) * E]} * u2,
+                                       lane);
 #pragma unroll
-                for (int c = 0; c < 2; ++c) s2[c] = tstage<1>(s1[c], s1[c + 2], lane);
-                v[x] = tstage<2>(s2[0], s2[1], lane);
+                for (int c = 0; c < 2; ++c) s2[c] = tstage2<1>(s1[c], s1[c + 2], lane);
+                const f32x2 r = tstage2<2>(s2[0], s2[1], lane);
+                v[x] = r.x;
+                v[x + 1] = r.y;
             }
             XorReduce<E, E, 3>::run(v, lane);
             if constexpr (NL >= 64) {
@@ -1642,9 +1671,16 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
             return z;
         };
         auto qt_times = [&]() -> float {  // u_f = sum_j Q_S[j][f] sp[j] (all threads: feature f)
-            float u = 0.0f;
+            // two packed accumulators (v_pk_fma_f32): partial sums over j = 0, 1 mod 4 and 2, 3
+            static_assert(NL % 4 == 0, "packed accumulators");
+            f32x2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f};
 #pragma unroll
-            for (int j = 0; j < NL; ++j) u += q[j] * sp[half * NL + j];
+            for (int j = 0; j < NL; j += 4) {
+                const float* pj = sp + half * NL + j;
+                a0 = __builtin_elementwise_fma(f32x2{q[j], q[j + 1]}, f32x2{pj[0], pj[1]}, a0);
+                a1 = __builtin_elementwise_fma(f32x2{q[j + 2], q[j + 3]}, f32x2{pj[2], pj[3]}, a1);
+            }
+            float u = (a0.x + a0.y) + (a1.x + a1.y);
             if constexpr (HALVES == 1) return u;
             su[half][f] = u;
             __syncthreads();
@@ -1720,7 +1756,11 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
     const double rho = (std::sqrt(1.0 + alpha) - 1.0) / (std::sqrt(1.0 + alpha) + 1.0);
     const int max_it = std::min(200, (int)std::ceil(std::log(tol) / std::log(rho)) + 4);
     const float tol2 = (float)(tol * tol);
-    const double sk = S && lnorm > 0.0 ? kWoodAbs / lnorm : 0.0, ab = sk / alpha;
+    static const double wood_abs = [] {  // A/B of the absolute target (experiments builds)
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOOD_ABS");
+        return e ? std::atof(e) : kWoodAbs;
+    }();
+    const double sk = S && lnorm > 0.0 ? wood_abs / lnorm : 0.0, ab = sk / alpha;
     const float skip2 = S ? (float)(sk * sk) : -1.0f, abs2 = (float)(ab * ab);
     if (g == 0)
         wrmf_wood_cg_kernel<32><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
