@@ -944,11 +944,16 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
 #pragma unroll
                 for (int g = 0; g < 16; ++g) dst[g * 64] = acc[s][g];
             }
-        // ---- 4. backward substitution L^T w = y (padding entries come out 0)
-        if (!(dbg & 4)) back_substitute(sm, acc, tl, nt);
+        // ---- 4. backward substitution L^T w = y (padding entries come out 0).  With the factor
+        //         kept (fp64 mode) it is deferred to wrmf_tile_resolve_wave_kernel (backward_only):
+        //         y goes to the W row, and one wave per row streams the kept tiles, without the
+        //         8-wave workgroup's barrier per block row (31 -> ~11 ms per C5 iteration)
+        const bool defer = MODE == 0 && F != nullptr;
+        if (!defer && !(dbg & 4)) back_substitute(sm, acc, tl, nt);
         __syncthreads();
         if constexpr (MODE == 0) {
-            for (int f = t; f < k; f += kThreads) W[(int64_t)row * k + f] = sm.wv[f];
+            const float* src = defer ? sm.yv : sm.wv;
+            for (int f = t; f < k; f += kThreads) W[(int64_t)row * k + f] = src[f];
         } else {
             // t = Q_S^T v (the item ids staged in LDS first)
             const int deg = (int)(re - rb);
@@ -1065,9 +1070,11 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// backward_only: rhs holds y = L^{-1} b already (the main solve's forward result, deferred here
+// from wrmf_tile_solve_kernel), and may alias W: the wave reads its row into LDS before writing.
 __global__ __launch_bounds__(64 * kRvWaves) void wrmf_tile_resolve_wave_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, const int64_t* __restrict__ off,
-    const float* __restrict__ F, const float* __restrict__ rhs, int32_t k, float* __restrict__ W) {
+    const float* __restrict__ F, const float* rhs, int32_t k, float* W, int32_t backward_only) {
     __shared__ RvSmem smem[kRvWaves];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane & 31, h = lane >> 5;
     RvSmem& sm = smem[wv];
@@ -1088,8 +1095,12 @@ __global__ __launch_bounds__(64 * kRvWaves) void wrmf_tile_resolve_wave_kernel(
 #pragma unroll
             for (int g = 0; g < 16; ++g) tv[g] = src[g * 64];
         };
+        if (backward_only) {
+            for (int f = lane; f < 32 * nt; f += 64) sm.ys[f] = f < k ? rr[f] : 0.0f;
+            wave_sync();
+        }
         // ---- forward substitution
-        for (int J = 0; J < nt; ++J) {
+        for (int J = 0; J < (backward_only ? 0 : nt); ++J) {
             float a = 0.0f;
             for (int K = 0; K < J; ++K) {
                 load_tile(J, K);
@@ -1734,8 +1745,10 @@ bool wood_cg() {
 }
 
 // the refinement's absolute target for a Woodbury row's correction d (2-norm, so also per entry
-// relative to 1 + |x|): far below the float rounding of W (6e-8 relative) and the fp64 mode's 2e-7
-constexpr double kWoodAbs = 1e-8;
+// relative to 1 + |x|): under one float ulp at |x| = 1 and a quarter of the fp64 mode's 2e-7.
+// C5 (A/B, experiments build): refinement CG 118 ms per iteration at 1e-8, 90 at 3e-8, 12 at 1e-7
+// (most rows' bound |L^-1| |s| then falls under the target before Q_S is gathered)
+constexpr double kWoodAbs = 5e-8;
 
 // lnorm: |L^{-1}|_2 (refinement only)
 void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const int64_t* off,
@@ -2473,7 +2486,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             } else {
                 const int64_t blocks = std::min<int64_t>((n + kRvWaves - 1) / kRvWaves, 256 * 16);
                 wrmf_tile_resolve_wave_kernel<<<(int)blocks, 64 * kRvWaves, 0, st>>>(
-                    list, (int32_t)n, off, Fl, rhs, k, W);
+                    list, (int32_t)n, off, Fl, rhs, k, W, 0);
             }
             ++launches;
         };
@@ -2529,6 +2542,18 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                 k, k, (float)alpha, nullptr, debug_mask(), rhs, F);
             MML_HIP(hipGetLastError());
             ++launches;
+        }
+        if (F) {  // the deferred backward substitutions: W rows hold y, the kept tiles L
+            auto back = [&](const int32_t* list, int64_t n, const float* Fl) {
+                if (n <= 0) return;
+                const int64_t blocks = std::min<int64_t>((n + kRvWaves - 1) / kRvWaves, 256 * 16);
+                wrmf_tile_resolve_wave_kernel<<<(int)blocks, 64 * kRvWaves, 0, st>>>(
+                    list, (int32_t)n, off, Fl, W, k, W, 1);
+                ++launches;
+            };
+            back(p.heavy_dev.get(), nh, F + (size_t)p.n_light * tile_floats);
+            back(p.light.get(), p.n_light, F);
+            MML_HIP(hipGetLastError());
         }
     }
     int64_t nw = 0, nw_max = 0;
