@@ -1862,17 +1862,25 @@ __global__ __launch_bounds__(256) void wrmf_rows_matmul_x3_kernel(
     const uint16_t* __restrict__ MT, int32_t k, int32_t kpad, float scale, float* __restrict__ Y,
     const int32_t* __restrict__ yrows) {
     __shared__ __attribute__((aligned(16))) uint16_t xs[3][32 * kXS];
+    __shared__ int64_t srow[2][32];  // the block's source / destination rows (-1: past n)
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, q = lane & 31, h = lane >> 5;
     const int nct = (k + 31) >> 5;
     const bool vec = (k & 3) == 0;
     for (int64_t blk = blockIdx.x; blk * 32 < n; blk += gridDim.x) {
         const int64_t r0 = blk * 32;
         __syncthreads();
+        if (t < 64) {  // the row ids once per block: staging and stores then read them from LDS
+            const int i = t & 31;
+            const int32_t* ids = t < 32 ? xrows : yrows;
+            srow[t >> 5][i] = r0 + i < n ? (ids ? (int64_t)ids[r0 + i] : r0 + i) : -1;
+        }
+        __syncthreads();
         for (int x = 4 * t; x < 32 * kpad; x += 4 * 256) {  // 4 consecutive k of one row
             const int i = x / kpad, f = x - i * kpad;
             float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (r0 + i < n) {
-                const float* src = X + (xrows ? (int64_t)xrows[r0 + i] : r0 + i) * k;
+            const int64_t sr = srow[0][i];
+            if (sr >= 0) {
+                const float* src = X + sr * k;
                 if (vec && f + 3 < k) {
                     const float4 v4 = *reinterpret_cast<const float4*>(src + f);
                     v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
@@ -1903,28 +1911,33 @@ __global__ __launch_bounds__(256) void wrmf_rows_matmul_x3_kernel(
             f32x16 d;
 #pragma unroll
             for (int g = 0; g < 16; ++g) d[g] = 0.0f;
-            for (int kc = 0; kc < kpad; kc += 16) {
-                bf16x8 A[3], B[3];
+            // B (from L2) one K step ahead of the MFMAs that use it
+            bf16x8 B[3], Bn[3];
 #pragma unroll
-                for (int p = 0; p < 3; ++p) {
+            for (int p = 0; p < 3; ++p) B[p] = *reinterpret_cast<const bf16x8*>(m0 + p * pstride);
+            for (int kc = 0; kc < kpad; kc += 16) {
+                const int kn = kc + 16 < kpad ? kc + 16 : kc;
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    Bn[p] = *reinterpret_cast<const bf16x8*>(m0 + p * pstride + kn);
+                bf16x8 A[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
                     A[p] = *reinterpret_cast<const bf16x8*>(&xs[p][q * kXS + kc + 8 * h]);
-                    B[p] = *reinterpret_cast<const bf16x8*>(m0 + p * pstride + kc);
-                }
                 d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], d, 0, 0, 0);
                 d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], d, 0, 0, 0);
                 d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], d, 0, 0, 0);
                 d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], d, 0, 0, 0);
                 d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], d, 0, 0, 0);
                 d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], d, 0, 0, 0);
+#pragma unroll
+                for (int p = 0; p < 3; ++p) B[p] = Bn[p];
             }
             if (cok)
 #pragma unroll
                 for (int g = 0; g < 16; ++g) {
-                    const int i = rho(g, h);
-                    if (r0 + i < n) {
-                        const int64_t dst = yrows ? yrows[r0 + i] : r0 + i;
-                        Y[dst * k + col] = scale * d[g];
-                    }
+                    const int64_t dst = srow[1][rho(g, h)];
+                    if (dst >= 0) Y[dst * k + col] = scale * d[g];
                 }
         }
     }
