@@ -805,27 +805,47 @@ def wrmf_executed_flops(deg_u, deg_i, k, passes=0, nnz=0, alpha=1.0):
 
 
 def cpu_baseline_wrmf(k, seconds, n_users, n_items, per_user):
-    """Oracle WRMF row solve (fp64, single thread, WRMF.cs:110-156) timed on a sample of rows,
-    extrapolated to one iteration's rows (stated as extrapolated)."""
+    """Oracle WRMF (fp64, single thread, WRMF.cs:68-156) timed on a bounded sample and composed into
+    one iteration: ComputeSquareMatrix on a 20k-row slice (scaled to both halves' rows), and row
+    solves at degrees 100, 1000 and 8000 (the user rows and the range of C5's Zipf item rows),
+    fitted as t(deg) = c0 + c1 deg and summed over every row (sum of degrees = 2 x events).  Stated
+    as extrapolated."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     rs = np.random.default_rng(5)
-    H = (rs.standard_normal((n_items, k)) * 0.1).astype(np.float32)
-    rows = 8
-    off = np.arange(0, (rows + 1) * per_user, per_user, dtype=np.int64)
-    cols = rs.integers(0, n_items, rows * per_user).astype(np.int32)
-    W = np.zeros((rows, k), np.float32)
+    H = (rs.standard_normal((max(n_items, 20000), k)) * 0.1).astype(np.float32)
     HH = np.zeros((k, k), np.float64)
     t0 = time.perf_counter()
-    O.lib().ora_wrmf_optimize_rows(O._p(off, O._i64p), O._p(cols, O._i32p), 0, rows, rows,
-                                   O._p(W, O._f32p), O._p(H, O._f32p), O._p(HH, O._f64p), k, 1.0,
-                                   0.015)
-    dt = (time.perf_counter() - t0) / rows
-    it = dt * (n_users + n_items)
+    O.lib().ora_wrmf_square(O._p(H[:20000], O._f32p), 20000, k, O._p(HH, O._f64p))
+    t_hh_row = (time.perf_counter() - t0) / 20000
+    degs, times = [100, 1000, 8000], []
+    for deg in degs:
+        rows = 4 if deg == 100 else 1
+        off = np.arange(0, (rows + 1) * deg, deg, dtype=np.int64)
+        cols = np.concatenate([rs.choice(n_items, deg, replace=False) for _ in range(rows)])
+        W = np.zeros((rows, k), np.float32)
+        t0 = time.perf_counter()
+        O.lib().ora_wrmf_optimize_rows(O._p(off, O._i64p), O._p(cols.astype(np.int32), O._i32p), 0,
+                                       rows, rows, O._p(W, O._f32p), O._p(H, O._f32p),
+                                       O._p(HH, O._f64p), k, 1.0, 0.015)
+        times.append((time.perf_counter() - t0) / rows)
+    # item degrees of the C5 generator (Zipf(0.8) ranks, expected counts); a row's time is
+    # interpolated in log(deg) between the measured points, linear in deg past the last one
+    from mymedialite_amd.synthetic import zipf_cdf
+    events = n_users * per_user
+    item_deg = np.diff(np.concatenate([[0.0], zipf_cdf(n_items, 0.8)])) * events
+    def row_time(d):
+        d = np.maximum(np.asarray(d, float), 1.0)
+        t = np.interp(np.log(d), np.log(degs), times)
+        return np.where(d > degs[-1], times[-1] * d / degs[-1], t)
+    it = (t_hh_row * (n_users + n_items) + n_users * float(row_time(per_user)) +
+          float(row_time(item_deg).sum()))
     return {"value": 1.0 / it, "unit": "iterations/s", "cores": 1, "kind": "port",
-            "sample": f"{rows} row solves (deg {per_user}, k={k}) of the oracle's fp64 "
-                      f"WRMF.Optimize(u) = {dt * 1e3:.1f} ms/row, extrapolated to "
-                      f"{n_users + n_items} rows per iteration (HH not included)"}
+            "sample": f"oracle fp64 WRMF on one thread: ComputeSquareMatrix {t_hh_row * 1e6:.1f} "
+                      f"us/row (20k-row slice), row solves {', '.join(f'{t * 1e3:.1f}' for t in times)} "
+                      f"ms at deg {degs}; composed into one iteration over {n_users} user rows "
+                      f"(deg {per_user}) and {n_items} item rows (the generator's Zipf(0.8) "
+                      f"degrees) = {it:.0f} s (extrapolated)"}
 
 
 def svdpp_data(n_users, n_items, n, seed=7):
