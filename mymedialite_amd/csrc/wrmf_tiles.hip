@@ -1750,6 +1750,7 @@ bool wood_cg() {
 // (most rows' bound |L^-1| |s| then falls under the target before Q_S is gathered)
 constexpr double kWoodAbs = 5e-8;
 
+int debug_mask();
 // lnorm: |L^{-1}|_2 (refinement only)
 void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const int64_t* off,
                     const int32_t* cols, const float* Q, int32_t k, float alpha, float* Tout,
@@ -1767,7 +1768,9 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
     }();
     const double tol = S ? refine_tol : 1e-6;
     const double rho = (std::sqrt(1.0 + alpha) - 1.0) / (std::sqrt(1.0 + alpha) + 1.0);
-    const int max_it = std::min(200, (int)std::ceil(std::log(tol) / std::log(rho)) + 4);
+    // MML_WRMF_DEBUG & 64 (timing only): no CG step, the gathers and the t = Q_S^T w pass alone
+    const int max_it = (debug_mask() & 64) ? 0
+                       : std::min(200, (int)std::ceil(std::log(tol) / std::log(rho)) + 4);
     const float tol2 = (float)(tol * tol);
     static const double wood_abs = [] {  // A/B of the absolute target (experiments builds)
         const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOOD_ABS");
@@ -1857,87 +1860,106 @@ __global__ __launch_bounds__(256) void wrmf_split_mt_kernel(const float* __restr
         MT[((int64_t)2 * k + c) * kpad + kk] = (uint16_t)(d >> 16);
     }
 }
+// 64 rows per workgroup, so each 16-B B load from L2 feeds two row tiles (B is re-read once per 64
+// rows instead of per 32: the kernel waits on those loads, 80 % of its wave cycles at 32 rows);
+// wave w takes column tiles 2w and 2w + 1 for both row tiles (4 accumulators).  X is staged in K
+// halves of kRH columns (3 planes x 64 rows x (kRH + 8) bf16 = 52 KB of LDS: 3 workgroups per CU).
+constexpr int kRH = 128, kRHS = kRH + 8;
 __global__ __launch_bounds__(256) void wrmf_rows_matmul_x3_kernel(
     const float* __restrict__ X, const int32_t* __restrict__ xrows, int64_t n,
     const uint16_t* __restrict__ MT, int32_t k, int32_t kpad, float scale, float* __restrict__ Y,
     const int32_t* __restrict__ yrows) {
-    __shared__ __attribute__((aligned(16))) uint16_t xs[3][32 * kXS];
-    __shared__ int64_t srow[2][32];  // the block's source / destination rows (-1: past n)
+    __shared__ __attribute__((aligned(16))) uint16_t xs[3][64 * kRHS];
+    __shared__ int64_t srow[2][64];  // the block's source / destination rows (-1: past n)
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, q = lane & 31, h = lane >> 5;
     const int nct = (k + 31) >> 5;
     const bool vec = (k & 3) == 0;
-    for (int64_t blk = blockIdx.x; blk * 32 < n; blk += gridDim.x) {
-        const int64_t r0 = blk * 32;
+    const int64_t pstride = (int64_t)k * kpad;
+    for (int64_t blk = blockIdx.x; blk * 64 < n; blk += gridDim.x) {
+        const int64_t r0 = blk * 64;
         __syncthreads();
-        if (t < 64) {  // the row ids once per block: staging and stores then read them from LDS
-            const int i = t & 31;
-            const int32_t* ids = t < 32 ? xrows : yrows;
-            srow[t >> 5][i] = r0 + i < n ? (ids ? (int64_t)ids[r0 + i] : r0 + i) : -1;
+        if (t < 128) {  // the row ids once per block: staging and stores read them from LDS
+            const int i = t & 63;
+            const int32_t* ids = t < 64 ? xrows : yrows;
+            srow[t >> 6][i] = r0 + i < n ? (ids ? (int64_t)ids[r0 + i] : r0 + i) : -1;
         }
-        __syncthreads();
-        for (int x = 4 * t; x < 32 * kpad; x += 4 * 256) {  // 4 consecutive k of one row
-            const int i = x / kpad, f = x - i * kpad;
-            float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            const int64_t sr = srow[0][i];
-            if (sr >= 0) {
-                const float* src = X + sr * k;
-                if (vec && f + 3 < k) {
-                    const float4 v4 = *reinterpret_cast<const float4*>(src + f);
-                    v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
-                } else {
+        f32x16 d[2][2];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) v[j] = f + j < k ? src[f + j] : 0.0f;
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) d[rt][jt][g] = 0.0f;
+        for (int k0 = 0; k0 < kpad; k0 += kRH) {
+            const int kw = min(kRH, kpad - k0);  // a multiple of 16
+            __syncthreads();  // the previous half's reads (and the row ids' writes) are done
+            for (int x = 4 * t; x < 64 * kw; x += 4 * 256) {  // 4 consecutive k of one row
+                const int i = x / kw, fl = x - i * kw, f = k0 + fl;
+                float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                const int64_t sr = srow[0][i];
+                if (sr >= 0) {
+                    const float* src = X + sr * k;
+                    if (vec && f + 3 < k) {
+                        const float4 v4 = *reinterpret_cast<const float4*>(src + f);
+                        v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] = f + j < k ? src[f + j] : 0.0f;
+                    }
                 }
-            }
-            uint32_t a[4], b[4], c[4];
+                uint32_t a[4], b[4], c[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) split3t(v[j], a[j], b[j], c[j]);
-            uint2* d0 = reinterpret_cast<uint2*>(&xs[0][i * kXS + f]);
-            uint2* d1 = reinterpret_cast<uint2*>(&xs[1][i * kXS + f]);
-            uint2* d2 = reinterpret_cast<uint2*>(&xs[2][i * kXS + f]);
-            *d0 = make_uint2(pack_hi(a[0], a[1]), pack_hi(a[2], a[3]));
-            *d1 = make_uint2(pack_hi(b[0], b[1]), pack_hi(b[2], b[3]));
-            *d2 = make_uint2(pack_hi(c[0], c[1]), pack_hi(c[2], c[3]));
+                for (int j = 0; j < 4; ++j) split3t(v[j], a[j], b[j], c[j]);
+                *reinterpret_cast<uint2*>(&xs[0][i * kRHS + fl]) =
+                    make_uint2(pack_hi(a[0], a[1]), pack_hi(a[2], a[3]));
+                *reinterpret_cast<uint2*>(&xs[1][i * kRHS + fl]) =
+                    make_uint2(pack_hi(b[0], b[1]), pack_hi(b[2], b[3]));
+                *reinterpret_cast<uint2*>(&xs[2][i * kRHS + fl]) =
+                    make_uint2(pack_hi(c[0], c[1]), pack_hi(c[2], c[3]));
+            }
+            __syncthreads();
+            for (int kc = 0; kc < kw; kc += 16) {
+                bf16x8 B[2][3], A[2][3];
+#pragma unroll
+                for (int jt = 0; jt < 2; ++jt) {
+                    const int col = 32 * (wave * 2 + jt) + q;
+                    const uint16_t* m0 = MT + (int64_t)(col < k ? col : 0) * kpad + k0 + kc + 8 * h;
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        B[jt][p] = *reinterpret_cast<const bf16x8*>(m0 + p * pstride);
+                }
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        A[rt][p] = *reinterpret_cast<const bf16x8*>(
+                            &xs[p][(32 * rt + q) * kRHS + kc + 8 * h]);
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                    for (int jt = 0; jt < 2; ++jt) {
+                        if (wave * 2 + jt >= nct) continue;
+                        f32x16 e = d[rt][jt];
+                        e = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][2], B[jt][0], e, 0, 0, 0);
+                        e = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][1], B[jt][1], e, 0, 0, 0);
+                        e = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][0], B[jt][2], e, 0, 0, 0);
+                        e = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][1], B[jt][0], e, 0, 0, 0);
+                        e = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][0], B[jt][1], e, 0, 0, 0);
+                        e = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][0], B[jt][0], e, 0, 0, 0);
+                        d[rt][jt] = e;
+                    }
+            }
         }
-        __syncthreads();
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt) {
-            const int J = wave * 2 + jt;
-            if (J >= nct) continue;
-            const int col = 32 * J + q;
-            const bool cok = col < k;
-            const uint16_t* m0 = MT + ((int64_t)(cok ? col : 0)) * kpad + 8 * h;
-            const int64_t pstride = (int64_t)k * kpad;
-            f32x16 d;
+            const int col = 32 * (wave * 2 + jt) + q;
+            if (col >= k) continue;
 #pragma unroll
-            for (int g = 0; g < 16; ++g) d[g] = 0.0f;
-            // B (from L2) one K step ahead of the MFMAs that use it
-            bf16x8 B[3], Bn[3];
-#pragma unroll
-            for (int p = 0; p < 3; ++p) B[p] = *reinterpret_cast<const bf16x8*>(m0 + p * pstride);
-            for (int kc = 0; kc < kpad; kc += 16) {
-                const int kn = kc + 16 < kpad ? kc + 16 : kc;
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    Bn[p] = *reinterpret_cast<const bf16x8*>(m0 + p * pstride + kn);
-                bf16x8 A[3];
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    A[p] = *reinterpret_cast<const bf16x8*>(&xs[p][q * kXS + kc + 8 * h]);
-                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], d, 0, 0, 0);
-#pragma unroll
-                for (int p = 0; p < 3; ++p) B[p] = Bn[p];
-            }
-            if (cok)
+            for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
                 for (int g = 0; g < 16; ++g) {
-                    const int64_t dst = srow[1][rho(g, h)];
-                    if (dst >= 0) Y[dst * k + col] = scale * d[g];
+                    const int64_t dst = srow[1][32 * rt + rho(g, h)];
+                    if (dst >= 0) Y[dst * k + col] = scale * d[rt][jt][g];
                 }
         }
     }
@@ -1955,15 +1977,16 @@ bool gemm_f32() {
 void rows_matmul(hipStream_t st, const float* X, const int32_t* xrows, int64_t n, const float* M,
                  const uint16_t* MX, int32_t k, float scale, float* Y, const int32_t* yrows) {
     const int grid = (int)std::min<int64_t>((n + 31) / 32, 8192);
+    const int grid64 = (int)std::min<int64_t>((n + 63) / 64, 8192);
     if (gemm_f32())
         wrmf_rows_matmul_kernel<<<grid, 256, 0, st>>>(X, xrows, n, M, k, scale, Y, yrows);
     else
-        wrmf_rows_matmul_x3_kernel<<<grid, 256, 0, st>>>(X, xrows, n, MX, k, (k + 15) & ~15, scale,
-                                                         Y, yrows);
+        wrmf_rows_matmul_x3_kernel<<<grid64, 256, 0, st>>>(X, xrows, n, MX, k, (k + 15) & ~15,
+                                                           scale, Y, yrows);
 }
 
 // MML_WRMF_DEBUG: phase-skip mask for timing experiments only (results are wrong when set):
-// 1 diagonal factorisation, 2 panel MFMAs, 4 backward substitution, 8 Gram
+// 1 diagonal factorisation, 2 panel MFMAs, 4 backward substitution, 8 Gram, 64 no CG steps
 int debug_mask() {
     static const int v = [] {
         const char* e = MML_EXPERIMENT_ENV("MML_WRMF_DEBUG");
