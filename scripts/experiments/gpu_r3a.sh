@@ -2,7 +2,7 @@
 # Round 3: the multi-device user shards on one GPU (repeated-device contexts, peer-copy item
 # averaging, ORDERED per shard), the C4 averaging cost, and the tightened C2-shape Hogwild band.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r3a}

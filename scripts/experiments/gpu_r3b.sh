@@ -2,7 +2,7 @@
 # Round 3: WRMF adaptive refinement vs the exact-product oracle, the WRMF suite, then the default
 # bench line (C2 + c4_n1 / c3 / c5 keys).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r3b}

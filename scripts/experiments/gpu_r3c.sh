@@ -2,7 +2,7 @@
 # Round 3: the MFMA column-pair diagonal factor (ubench + the WRMF suite), the default bench line
 # (C2 + c4_n1 / c3 / c5 keys) and a C5 kernel profile.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r3c}

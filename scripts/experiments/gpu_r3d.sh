@@ -2,7 +2,7 @@
 # Round 3: WRMF direct rows -- the MFMA column-pair diagonal factor + the global->LDS ring Gram:
 # ubench, the WRMF tests, C5 with and without the ring (variants/noring), a C5 kernel profile.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r3d}

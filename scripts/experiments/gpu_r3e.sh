@@ -2,7 +2,7 @@
 # Round 3: WRMF after the grow-only refinement workspace and the per-row-type refinement stop: the WRMF
 # tests, C5 with and without the ring Gram, kernel profiles of both.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r3e}

@@ -2,7 +2,7 @@
 # Round 3: BPRMF USER_RUNS schedule -- its tests (exact single run, AUC parity, C3 replica), C3 with
 # both schedules, a kernel profile of each.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r3i}

@@ -2,7 +2,7 @@
 # Round 3: C3 Hogwild A/B on one box -- the current library vs the round-2 tree (variants/r2wt,
 # commit 67d7612), alternated; then C5 with the Woodbury refinement skip bound.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 ROOT=$PWD
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -3,7 +3,7 @@
 # MML_WRMF_DEBUG phase-skip masks (timing only; results wrong when set): 0 all, 1 no diagonal
 # factorisation, 2 no panel / trailing MFMAs, 4 no back substitution, 8 no Gram.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r3o}

@@ -2,7 +2,7 @@
 # Round 3: the Woodbury refinement's absolute target, A/B on one box (experiments build,
 # MML_WRMF_WOOD_ABS): C5 fp64, refinement CG time and the bench line per target.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r3p}

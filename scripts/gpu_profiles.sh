@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round 3 profiles for every bench key: rocprofv3 kernel stats of C2 (the headline line), C4 at
+# Profiles for every bench key: rocprofv3 kernel stats of C2 (the headline line), C4 at
 # N = 1, C3 and C5; a C5 kernel trace (idle gaps); one PMC pass over a C5 iteration (MFMA busy,
 # waits, LDS bank conflicts per kernel).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${1:-r3k}
+TAG=${1:-prof}
 step() {  # step <name> <seconds> <command...>
     local name=$1 secs=$2
     shift 2

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round 3 rehearsal of the driver's round-end tiers: the whole -m gpu suite, smoke(), the default
+# Rehearsal of the driver's round-end tiers: the whole -m gpu suite, smoke(), the default
 # bench line (C2 + the c4_n1 / c3 / c5 keys) with its CPU baselines.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${1:-r3h}
+TAG=${1:-rehearsal}
 step() {  # step <name> <seconds> <command...>
     local name=$1 secs=$2
     shift 2
