@@ -1602,7 +1602,7 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
     const int32_t* __restrict__ rows, int32_t n_list, const int64_t* __restrict__ off,
     const int32_t* __restrict__ cols, const float* __restrict__ Q, int32_t k, float alpha,
     const float* __restrict__ S, float* __restrict__ Tout, int32_t max_it, float tol2,
-    float skip2, float abs2) {
+    float skip2, float abs2, int32_t cheb_m, float cheb_theta, float cheb_delta) {
     static_assert(NJ == 32 || NJ == 64 || NJ == 128, "NJ: 32, 64 or 128");
     constexpr int HALVES = NJ > 64 ? 2 : 1;
     constexpr int WAVES = 4 * HALVES;
@@ -1705,7 +1705,25 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
         }
         float w = 0.0f, r = t < deg ? y : 0.0f, p = 0.0f, sv = 0.0f;
         float g_prev = 1.0f, a_prev = 1.0f, stop = 0.0f;
-        for (int it = 0; it <= max_it; ++it) {
+        if (cheb_m > 0) {
+            // Chebyshev iteration on the known spectrum [1/alpha, 1/alpha + 1] (centre theta,
+            // half-width delta): no inner products, so no block reduction and no barrier beyond
+            // the mat-vec's own; cheb_m updates take cheb_m - 1 mat-vecs
+            const float s1 = cheb_theta / cheb_delta;
+            float dv = r / cheb_theta, rho_p = 1.0f / s1;
+            for (int it = 0; it < cheb_m; ++it) {
+                w += dv;
+                if (it + 1 == cheb_m) break;
+                if (t < NJ) sp[t] = dv;
+                __syncthreads();
+                const float uf = qt_times();
+                r -= (t < deg ? dv * ainv : 0.0f) + qs_times(uf);  // r -= C d
+                const float rho = 1.0f / (2.0f * s1 - rho_p);
+                dv = rho * rho_p * dv + (2.0f * rho / cheb_delta) * r;
+                rho_p = rho;
+            }
+        }
+        for (int it = 0; it <= (cheb_m > 0 ? -1 : max_it); ++it) {
             if (t < NJ) sp[t] = r;
             __syncthreads();
             const float uf = qt_times();
@@ -1778,15 +1796,30 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
     }();
     const double sk = S && lnorm > 0.0 ? wood_abs / lnorm : 0.0, ab = sk / alpha;
     const float skip2 = S ? (float)(sk * sk) : -1.0f, abs2 = (float)(ab * ab);
+    // the main solve by Chebyshev iteration: error <= 2 / T_m(theta / delta) relative, so
+    // m = acosh(2 / tol) / acosh(theta / delta) updates, + 1 for fp32 (alpha = 1: 10 updates and 9
+    // mat-vecs, against 13 mat-vecs and 13 block reductions for the CG at its step cap);
+    // MML_WRMF_WOOD_MAIN=cg (experiments builds) keeps the CG
+    static const bool main_cg = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOOD_MAIN");
+        return e && std::string(e) == "cg";
+    }();
+    const double theta = 1.0 / alpha + 0.5, delta = 0.5;
+    const int cheb_m = (S || main_cg || (debug_mask() & 64))
+                           ? 0
+                           : (int)std::ceil(std::acosh(2.0 / tol) / std::acosh(theta / delta)) + 1;
     if (g == 0)
         wrmf_wood_cg_kernel<32><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
-                                                      max_it, tol2, skip2, abs2);
+                                                      max_it, tol2, skip2, abs2, cheb_m,
+                                                      (float)theta, (float)delta);
     else if (g == 1)
         wrmf_wood_cg_kernel<64><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
-                                                      max_it, tol2, skip2, abs2);
+                                                      max_it, tol2, skip2, abs2, cheb_m,
+                                                      (float)theta, (float)delta);
     else
         wrmf_wood_cg_kernel<128><<<grid, 512, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
-                                                       max_it, tol2, skip2, abs2);
+                                                       max_it, tol2, skip2, abs2, cheb_m,
+                                                       (float)theta, (float)delta);
 }
 
 // Y[yrow(r)] = scale * X[xrow(r)] * M for n rows (X, Y row-major [.. x k], M [k x k] row-major,
