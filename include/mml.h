@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 6
+#define MML_ABI_VERSION 7
 
 typedef int32_t mml_status;
 enum {
@@ -135,6 +135,23 @@ mml_status mml_rating_file_get(mml_rating_file* f, int32_t* users, int32_t* item
 mml_status mml_rating_file_new_ids(mml_rating_file* f, int32_t which, char* buf, int64_t cap,
                                    int64_t* bytes);
 mml_status mml_rating_file_destroy(mml_rating_file* f);
+/* ABI 7: the same read with the arrays landing in `ctx`'s HBM.  The file's bytes are copied to the
+ * device once and tokenised there (StaticRatingData.Read's rules as above; Mapping columns resolved
+ * on the device in first-appearance order when every id and seed is a canonical decimal, "0" or
+ * [1-9][0-9]{0,17}; ratings on the correctly rounded fast path: <= 2^24 significant value, decimal
+ * exponent within +-10).  Anything else -- ITEM_DATA, BINARY_CACHE, other id or rating spellings,
+ * a malformed line -- runs mml_rating_file_read and uploads its arrays: same result and error text
+ * either way.  counts / get (a device-to-host copy) / new_ids work as for a host read. */
+mml_status mml_rating_file_read_device(mml_ctx* ctx, const char* path, int32_t flags,
+                                       int32_t n_threads, const char* const* user_seed,
+                                       int32_t n_user_seed, const char* const* item_seed,
+                                       int32_t n_item_seed, mml_rating_file** out);
+/* Device pointers of a read_device result (owned by f, valid until destroy; pass them to
+ * mml_bmf_set_data_device etc.); *device_parsed = 1 when the device tokenised the file, 0 when the
+ * host reader ran. */
+mml_status mml_rating_file_device_arrays(mml_rating_file* f, const int32_t** users,
+                                         const int32_t** items, const float** values,
+                                         int32_t* device_parsed);
 
 /* ------------------------------------------------------------------ BiasedMatrixFactorization */
 enum { MML_LOSS_RMSE = 0, MML_LOSS_MAE = 1, MML_LOSS_LOGISTIC = 2 }; /* OptimizationTarget */

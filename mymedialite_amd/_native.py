@@ -96,6 +96,12 @@ SIGNATURES = {
     "mml_rating_file_new_ids": (_st, [_vp, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int64,
                                       _i64p]),
     "mml_rating_file_destroy": (_st, [_vp]),
+    "mml_rating_file_read_device": (_st, [_vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.POINTER(ctypes.c_char_p), ctypes.c_int32,
+                                          ctypes.POINTER(ctypes.c_char_p), ctypes.c_int32,
+                                          ctypes.POINTER(_vp)]),
+    "mml_rating_file_device_arrays": (_st, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                            ctypes.POINTER(_vp), _i32p]),
     "mml_balanced_rows": (_st, [_i64p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _i64p]),
     "mml_bmf_create": (_st, [_vp, ctypes.POINTER(BmfParams), ctypes.c_int32, ctypes.c_int32,
                              ctypes.POINTER(_vp)]),

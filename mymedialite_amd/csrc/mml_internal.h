@@ -9,6 +9,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <exception>
+#include <memory>
 #include <new>
 #include <string>
 #include <thread>
@@ -243,6 +244,21 @@ struct mml_ctx {
     int32_t xcd_groups = 0;  // mml::xcd_groups, 0 = not probed yet
     hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_mid = nullptr;
     void activate() const { MML_HIP(hipSetDevice(device)); }
+};
+
+// A parsed rating file (ratings_file.cpp; ratings_device.hip parses on the device): host arrays,
+// or (device_parsed / uploaded) arrays in `ctx`'s HBM with the host copies made on demand
+struct mml_rating_file {
+    int64_t n_lines = 0;    // StaticRatings size (lines after the skipped first one)
+    int64_t n_ratings = 0;  // non-empty lines
+    std::unique_ptr<int32_t[]> users, items;
+    std::unique_ptr<float[]> values;
+    std::vector<std::string> new_users, new_items;  // ids the mapping did not hold, in order
+    int32_t threads = 8;                            // the reader's thread count (copies, cache)
+    mml_ctx* ctx = nullptr;                         // set: the arrays live in this context's HBM
+    mml::DeviceArray<int32_t> d_users, d_items;
+    mml::DeviceArray<float> d_values;
+    int32_t device_parsed = 0;  // 1: parsed on the device; 0: host parse (then uploaded if ctx)
 };
 
 namespace mml {

@@ -32,14 +32,6 @@
 
 #include "mml_internal.h"
 
-struct mml_rating_file {
-    int64_t n_lines = 0;    // StaticRatings size (lines after the skipped first one)
-    int64_t n_ratings = 0;  // non-empty lines
-    std::unique_ptr<int32_t[]> users, items;
-    std::unique_ptr<float[]> values;
-    std::vector<std::string> new_users, new_items;  // ids the mapping did not hold, in order
-    int32_t threads = 8;                            // the reader's thread count (copies, cache)
-};
 
 namespace {
 
@@ -482,6 +474,19 @@ extern "C" mml_status mml_rating_file_get(mml_rating_file* f, int32_t* users, in
                                           float* values) {
     return guard([&] {
         MML_REQUIRE(f && users && items && values, "null argument");
+        if (!f->users && f->ctx) {  // parsed on the device: the arrays live in HBM
+            f->ctx->activate();
+            const size_t n = (size_t)f->n_ratings;
+            if (n > 0) {
+                MML_HIP(hipMemcpy(users, f->d_users.get(), sizeof(int32_t) * n,
+                                  hipMemcpyDeviceToHost));
+                MML_HIP(hipMemcpy(items, f->d_items.get(), sizeof(int32_t) * n,
+                                  hipMemcpyDeviceToHost));
+                MML_HIP(hipMemcpy(values, f->d_values.get(), sizeof(float) * n,
+                                  hipMemcpyDeviceToHost));
+            }
+            return;
+        }
         parallel_copy(users, f->users.get(), sizeof(int32_t) * f->n_ratings, f->threads);
         parallel_copy(items, f->items.get(), sizeof(int32_t) * f->n_ratings, f->threads);
         parallel_copy(values, f->values.get(), sizeof(float) * f->n_ratings, f->threads);
@@ -512,5 +517,8 @@ extern "C" mml_status mml_rating_file_new_ids(mml_rating_file* f, int32_t which,
 }
 
 extern "C" mml_status mml_rating_file_destroy(mml_rating_file* f) {
-    return guard([&] { delete f; });
+    return guard([&] {
+        if (f && f->ctx) (void)hipSetDevice(f->ctx->device);  // its HBM arrays are freed here
+        delete f;
+    });
 }

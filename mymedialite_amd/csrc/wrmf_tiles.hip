@@ -1876,9 +1876,8 @@ __global__ __launch_bounds__(256) void wrmf_rows_matmul_kernel(
 // The same row GEMM on the bf16 matrix cores at f32 accuracy (the Gram's 3-way split, six
 // products per K step, split3t): 2.7x fewer MFMA cycles than v_mfma_f32_32x32x2_f32.  M comes as
 // its bf16 planes, transposed and K-padded (wrmf_split_mt_kernel, once per half-step), so a lane's
-// B operand (8 consecutive k of one column) is one 16-B load from L2; X's 32 rows are split into
-// three bf16 planes in LDS (row stride kXS: the A reads are conflict-free per 16 lanes).
-constexpr int kXS = 264;
+// B operand (8 consecutive k of one column) is one 16-B load from L2; X's rows are split into
+// three bf16 planes in LDS (padded rows: the A reads are conflict-free per 16 lanes).
 __global__ __launch_bounds__(256) void wrmf_split_mt_kernel(const float* __restrict__ M, int32_t k,
                                                             int32_t kpad,
                                                             uint16_t* __restrict__ MT) {

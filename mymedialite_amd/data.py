@@ -165,10 +165,11 @@ def _read_lines(path: str, ignore_first_line: bool):
     return lines[1:] if ignore_first_line else lines
 
 
-def _native_read(path, user_mapping, item_mapping, flags, n_threads):
-    """mml_rating_file_read (ratings_file.cpp): the multi-threaded parse; the Mapping objects are
-    seeded into it and receive the new ids in first-appearance order.  Returns (users, items,
-    values, n_lines)."""
+def _native_open(path, user_mapping, item_mapping, flags, n_threads, device=None):
+    """mml_rating_file_read (ratings_file.cpp), or with ``device`` (a Context)
+    mml_rating_file_read_device (ratings_device.hip: the parse in its HBM).  The Mapping objects
+    are seeded into the read and receive the new ids in first-appearance order.  Returns the
+    handle and (n_ratings, n_lines)."""
     import ctypes
     from . import _native as N
     seeds = []
@@ -181,18 +182,19 @@ def _native_read(path, user_mapping, item_mapping, flags, n_threads):
                 *[x.encode() for x in m.internal_to_original])
             seeds.append((arr, len(m.internal_to_original)))
     h = N._vp()
-    N.check(N.lib().mml_rating_file_read(path.encode(), flags, n_threads, seeds[0][0],
-                                         seeds[0][1], seeds[1][0], seeds[1][1], ctypes.byref(h)))
+    if device is not None:
+        N.check(N.lib().mml_rating_file_read_device(device.handle, path.encode(), flags, n_threads,
+                                                    seeds[0][0], seeds[0][1], seeds[1][0],
+                                                    seeds[1][1], ctypes.byref(h)))
+    else:
+        N.check(N.lib().mml_rating_file_read(path.encode(), flags, n_threads, seeds[0][0],
+                                             seeds[0][1], seeds[1][0], seeds[1][1],
+                                             ctypes.byref(h)))
     try:
         nr, nl = ctypes.c_int64(), ctypes.c_int64()
         nu, ni = ctypes.c_int32(), ctypes.c_int32()
         N.check(N.lib().mml_rating_file_counts(h, ctypes.byref(nr), ctypes.byref(nl),
                                                ctypes.byref(nu), ctypes.byref(ni)))
-        users = np.empty(nr.value, np.int32)
-        items = np.empty(nr.value, np.int32)
-        values = np.empty(nr.value, np.float32)
-        N.check(N.lib().mml_rating_file_get(h, N.ptr(users, N._i32p), N.ptr(items, N._i32p),
-                                            N.ptr(values, N._f32p)))
         for which, m, cnt in ((0, user_mapping, nu.value), (1, item_mapping, ni.value)):
             if cnt == 0:
                 continue
@@ -205,13 +207,76 @@ def _native_read(path, user_mapping, item_mapping, flags, n_threads):
             base = len(m.internal_to_original)
             m.internal_to_original.extend(ids)
             m.original_to_internal.update(zip(ids, range(base, base + cnt)))
+    except BaseException:
+        N.lib().mml_rating_file_destroy(h)
+        raise
+    return h, nr.value, nl.value
+
+
+def _native_read(path, user_mapping, item_mapping, flags, n_threads, device=None):
+    """_native_open, the arrays copied to the host.  Returns (users, items, values, n_lines)."""
+    from . import _native as N
+    h, nr, nl = _native_open(path, user_mapping, item_mapping, flags, n_threads, device)
+    try:
+        users = np.empty(nr, np.int32)
+        items = np.empty(nr, np.int32)
+        values = np.empty(nr, np.float32)
+        N.check(N.lib().mml_rating_file_get(h, N.ptr(users, N._i32p), N.ptr(items, N._i32p),
+                                            N.ptr(values, N._f32p)))
     finally:
         N.lib().mml_rating_file_destroy(h)
-    return users, items, values, nl.value
+    return users, items, values, nl
+
+
+class DeviceRatingFile:
+    """StaticRatingData.Read with the result kept in a Context's HBM (mml_rating_file_read_device):
+    ``users_ptr`` / ``items_ptr`` / ``values_ptr`` are device pointers for the *_set_data_device
+    calls, valid until ``close()``; ``device_parsed`` is 1 when the device tokenised the file (0:
+    the host reader ran and its arrays were uploaded -- the same result)."""
+
+    def __init__(self, path: str, device, user_mapping=None, item_mapping=None,
+                 ignore_first_line=False, n_threads=8, with_ratings=True):
+        import ctypes
+        from . import _native as N
+        self.user_mapping = user_mapping or IdentityMapping()
+        self.item_mapping = item_mapping or IdentityMapping()
+        flags = (N.READ_IGNORE_FIRST_LINE if ignore_first_line else 0) | \
+            (0 if with_ratings else N.READ_WITHOUT_RATINGS)
+        self._h, self.count, self.n_lines = _native_open(path, self.user_mapping,
+                                                         self.item_mapping, flags, n_threads,
+                                                         device)
+        u, i, v = N._vp(), N._vp(), N._vp()
+        dp = ctypes.c_int32()
+        N.check(N.lib().mml_rating_file_device_arrays(self._h, ctypes.byref(u), ctypes.byref(i),
+                                                      ctypes.byref(v), ctypes.byref(dp)))
+        self.users_ptr, self.items_ptr, self.values_ptr = u.value, i.value, v.value
+        self.device_parsed = dp.value
+
+    def to_host(self):
+        """(users, items, values) copied from HBM."""
+        from . import _native as N
+        users = np.empty(self.count, np.int32)
+        items = np.empty(self.count, np.int32)
+        values = np.empty(self.count, np.float32)
+        N.check(N.lib().mml_rating_file_get(self._h, N.ptr(users, N._i32p),
+                                            N.ptr(items, N._i32p), N.ptr(values, N._f32p)))
+        return users, items, values
+
+    def close(self):
+        if self._h:
+            from . import _native as N
+            N.lib().mml_rating_file_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def read_ratings(path: str, user_mapping=None, item_mapping=None, ignore_first_line=False,
-                 native=True, n_threads=8, with_ratings=True, binary_cache=False):
+                 native=True, n_threads=8, with_ratings=True, binary_cache=False, device=None):
     """StaticRatingData.Read (IO/StaticRatingData.cs:36-117): arrays sized by the line count,
     empty lines skipped, >= 3 columns (>= 2 and rating 0 with ``with_ratings=False``, the
     TestRatingFileFormat.WITHOUT_RATINGS variant).
@@ -221,7 +286,8 @@ def read_ratings(path: str, user_mapping=None, item_mapping=None, ignore_first_l
     (mml_rating_file_read); False: this Python restatement (the two are tested equal).
     ``binary_cache``: FileSerializer's cache (StaticRatingData.cs:43-59), used when both mappings
     are IdentityMapping -- <path>.bin.mml.StaticRatings is loaded instead of parsing the text,
-    or written after the parse (MML_READ_BINARY_CACHE).
+    or written after the parse (MML_READ_BINARY_CACHE).  ``device``: a Context whose HBM the
+    parse runs in (mml_rating_file_read_device; the same result, copied back).
     """
     user_mapping = user_mapping or IdentityMapping()
     item_mapping = item_mapping or IdentityMapping()
@@ -232,7 +298,7 @@ def read_ratings(path: str, user_mapping=None, item_mapping=None, ignore_first_l
             (0 if with_ratings else N.READ_WITHOUT_RATINGS) | \
             (N.READ_BINARY_CACHE if binary_cache else 0)
         users, items, values, n_lines = _native_read(path, user_mapping, item_mapping, flags,
-                                                     n_threads)
+                                                     n_threads, device)
         scale = np.zeros(n_lines, np.float32)  # the sized array: blank lines are 0 (quirk above)
         scale[: len(values)] = values
         return Ratings(users, items, values, scale_values=scale)
