@@ -398,37 +398,61 @@ void map_keys_device(hipStream_t st, const int64_t* keys, int64_t N, const std::
     for (int32_t x = 0; x < n_new; ++x) fresh.push_back(std::to_string(allkeys[dord[x]]));
 }
 
-// the whole file into memory (parallel pread), with kPad zero bytes after it
-std::unique_ptr<uint8_t[]> read_file(const char* path, int64_t& n, int T) {
+// The file straight into a device buffer (kPad zero bytes after it): kRingSlots host threads each
+// own one pinned kChunk slot and one stream, and loop pread(chunk) -> async copy -> next chunk, so
+// the reads of one slot overlap the copies of the others and no file-sized host buffer is ever
+// allocated (first-touching 16 GB of fresh pages costs seconds on its own).  Returns false if the
+// file cannot be read (the host reader then reports it).
+constexpr size_t kChunk = (size_t)64 << 20;
+constexpr int kRingSlots = 8;
+bool upload_file(const char* path, int64_t& n, mml::DeviceArray<uint8_t>& B, uint8_t* head,
+                 hipStream_t st) {
     const int fd = ::open(path, O_RDONLY);
-    if (fd < 0) mml::fail(MML_ERR_ARG, std::string("cannot open ") + path);
+    if (fd < 0) return false;
     struct stat st_ {};
     if (::fstat(fd, &st_) != 0) {
         ::close(fd);
-        mml::fail(MML_ERR_ARG, std::string("cannot stat ") + path);
+        return false;
     }
     n = (int64_t)st_.st_size;
-    std::unique_ptr<uint8_t[]> buf(new uint8_t[n + kPad]);
-    std::memset(buf.get() + n, 0, kPad);
+    B.alloc((size_t)n + kPad);
+    MML_HIP(hipMemsetAsync(B.get() + n, 0, kPad, st));
+    const int64_t chunks = (n + (int64_t)kChunk - 1) / (int64_t)kChunk;
+    uint8_t* ring = nullptr;
+    MML_HIP(hipHostMalloc(reinterpret_cast<void**>(&ring), kChunk * kRingSlots, hipHostMallocDefault));
+    std::vector<int> ok(kRingSlots, 1);
     std::vector<std::thread> th;
-    std::vector<int> ok(T, 1);
-    for (int c = 0; c < T; ++c)
-        th.emplace_back([&, c] {
-            int64_t a = n * c / T;
-            const int64_t b = n * (c + 1) / T;
-            while (a < b) {
-                const ssize_t r = ::pread(fd, buf.get() + a, (size_t)(b - a), (off_t)a);
-                if (r <= 0) {
-                    ok[c] = 0;
-                    return;
-                }
-                a += r;
+    for (int t = 0; t < kRingSlots; ++t)
+        th.emplace_back([&, t] {
+            hipStream_t cs = nullptr;
+            if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) {
+                ok[t] = 0;
+                return;
             }
+            uint8_t* slot = ring + (size_t)t * kChunk;
+            for (int64_t c = t; c < chunks && ok[t]; c += kRingSlots) {
+                if (hipStreamSynchronize(cs) != hipSuccess) ok[t] = 0;  // the slot's last copy
+                const int64_t a0 = c * (int64_t)kChunk;
+                const int64_t len = std::min<int64_t>((int64_t)kChunk, n - a0);
+                for (int64_t got = 0; got < len && ok[t];) {
+                    const ssize_t r = ::pread(fd, slot + got, (size_t)(len - got), (off_t)(a0 + got));
+                    if (r <= 0) ok[t] = 0;
+                    else got += r;
+                }
+                if (c == 0 && ok[t]) std::memcpy(head, slot, (size_t)std::min<int64_t>(len, 3));
+                if (ok[t] && hipMemcpyAsync(B.get() + a0, slot, (size_t)len, hipMemcpyHostToDevice,
+                                            cs) != hipSuccess)
+                    ok[t] = 0;
+            }
+            if (hipStreamSynchronize(cs) != hipSuccess) ok[t] = 0;
+            (void)hipStreamDestroy(cs);
         });
-    for (auto& t : th) t.join();
+    for (auto& x : th) x.join();
     ::close(fd);
-    for (int c = 0; c < T; ++c) MML_REQUIRE(ok[c], std::string("cannot read ") + path);
-    return buf;
+    (void)hipHostFree(ring);
+    for (int t = 0; t < kRingSlots; ++t)
+        if (!ok[t]) return false;
+    return true;
 }
 
 // the host reader's result uploaded to the context (the fallback path)
@@ -490,14 +514,13 @@ extern "C" mml_status mml_rating_file_read_device(mml_ctx* ctx, const char* path
         }
         if ((flags & (MML_READ_ITEM_DATA | MML_READ_BINARY_CACHE)) || !seeds_ok) return host_path();
         int64_t n = 0;
-        std::unique_ptr<uint8_t[]> text = read_file(path, n, T);
+        uint8_t head[3] = {0, 0, 0};
+        mml::DeviceArray<uint8_t> B;
+        if (!upload_file(path, n, B, head, st)) return host_path();
         if (n >= INT32_MAX * (int64_t)kSeg) return host_path();
-        const int64_t bom = n >= 3 && std::memcmp(text.get(), "\xEF\xBB\xBF", 3) == 0 ? 3 : 0;
+        const int64_t bom = n >= 3 && std::memcmp(head, "\xEF\xBB\xBF", 3) == 0 ? 3 : 0;
         const int skip_first = (flags & MML_READ_IGNORE_FIRST_LINE) ? 1 : 0;
         const int want = (flags & MML_READ_WITHOUT_RATINGS) ? 2 : 3;
-        mml::DeviceArray<uint8_t> B;
-        B.alloc(n + kPad);
-        MML_HIP(hipMemcpyAsync(B.get(), text.get(), n + kPad, hipMemcpyHostToDevice, st));
         const int64_t nseg = std::max<int64_t>(1, (n + kSeg - 1) / kSeg);
         mml::DeviceArray<int64_t> lines, rows, at;
         lines.alloc(nseg);
@@ -547,7 +570,6 @@ extern "C" mml_status mml_rating_file_read_device(mml_ctx* ctx, const char* path
         MML_HIP(hipMemcpyAsync(&e, err.get(), sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         MML_HIP(hipStreamSynchronize(st));
         B.reset();
-        text.reset();
         if (e != 0) return host_path();  // the host reader gives the reference's error or result
         if (!user_identity) map_keys_device(st, ukeys.get(), N, useed, f->d_users.get(), f->new_users);
         if (!item_identity) map_keys_device(st, ikeys.get(), N, iseed, f->d_items.get(), f->new_items);
