@@ -59,6 +59,12 @@ constexpr bool kGramRing = false;
 #else
 constexpr bool kGramRing = true;
 #endif
+constexpr int kPP = 40;  // bf16 panel-plane row stride (80 B: conflict-free 16-B reads/writes)
+#ifdef MML_FACTOR_F32  // A/B variant (scripts/build_variant.sh): panel and trailing MFMAs in f32
+constexpr bool kFactorX3 = false;
+#else
+constexpr bool kFactorX3 = true;
+#endif
 constexpr int kDS = 33;                                  // diagonal-tile / reduction row stride
 constexpr int kTS = 33;                                  // T_J^T row stride (conflict-free rows)
 
@@ -100,7 +106,10 @@ struct Smem {
             alignas(16) float raw[kRB][kCH][kRS];
         } gx;
         struct {
-            float pn[kNT][32][kPS];     // Cholesky: L_IJ of the current panel, row-major
+            float pn[kNT][32][kPS];     // Cholesky: L_IJ of the current panel, row-major (f32 A/B)
+            // the same panel as bf16x3 planes in the MFMA K-slot order: pp[pi][p][q][pos] with
+            // pos = 16 (g >> 3) + 8 h + (g & 7) for register g of lane (q, h)
+            alignas(16) uint16_t pp[kNT][3][32][kPP];
         } fz;
         float red[kNT][32][kDS];        // backward: per-tile partial products
     } u;
@@ -313,6 +322,32 @@ __device__ __forceinline__ void split3t(float x, uint32_t& a, uint32_t& b, uint3
 __device__ __forceinline__ uint32_t pack_hi(uint32_t lo, uint32_t hi) {  // {lo.hi16, hi.hi16}
     return __builtin_amdgcn_perm(hi, lo, 0x07060302u);
 }
+using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+// v[0 .. 7] -> three bf16x8 operands (split3t parts 0, 1, 2 of each element, in order)
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&P)[3]) {
+    uint32_t a[8], b[8], c[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split3t(v[j], a[j], b[j], c[j]);
+    P[0] = __builtin_bit_cast(bf16x8, u32x4{pack_hi(a[0], a[1]), pack_hi(a[2], a[3]),
+                                            pack_hi(a[4], a[5]), pack_hi(a[6], a[7])});
+    P[1] = __builtin_bit_cast(bf16x8, u32x4{pack_hi(b[0], b[1]), pack_hi(b[2], b[3]),
+                                            pack_hi(b[4], b[5]), pack_hi(b[6], b[7])});
+    P[2] = __builtin_bit_cast(bf16x8, u32x4{pack_hi(c[0], c[1]), pack_hi(c[2], c[3]),
+                                            pack_hi(c[4], c[5]), pack_hi(c[6], c[7])});
+}
+__device__ __forceinline__ bf16x8 bf16_neg(bf16x8 x) {
+    return __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, x) ^ 0x80008000u);
+}
+// c + A B over one K step of 16 with both operands split three ways (smallest products first)
+__device__ __forceinline__ f32x16 mfma_x3(const bf16x8 (&A)[3], const bf16x8 (&B)[3], f32x16 c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], c, 0, 0, 0);
+    return c;
+}
 __device__ __forceinline__ int pl_pos(int f, int c) {  // element (f, c) within row f
     return ((((c >> 3) ^ (f >> 3)) & 1) << 3) | (c & 7);
 }
@@ -496,23 +531,31 @@ __device__ __forceinline__ void gram_accumulate_x3g(Smem& sm, f32x16 (&acc)[kSlo
         i0 = e0 < e ? cols[e0] : 0;
         i1 = e0 + 1 < e ? cols[e0 + 1] : 0;
     };
+    // ring row v starts 4 floats later when (v >> 3) & 1: the conversion's reads of vectors 2 c2
+    // (c2 = 0..7 across a 32-lane group) then hit 8 distinct bank quads instead of 4 (row stride
+    // 260: 2 * 260 = 8 mod 32 repeats every 4 vectors); the 260-float stride has the 4 spare floats
+    float* const ring_base = &sm.u.gx.raw[0][0][0];
+    auto ring_row = [&](int slot, int v) {
+        return ring_base + ((int64_t)slot * kCH + v) * kRS + 4 * ((v >> 3) & 1);
+    };
     auto gather = [&](int64_t c, int32_t i0, int32_t i1) {
-        float* dst = &sm.u.gx.raw[c % kRB][2 * wave][0];
+        float* dst = ring_row((int)(c % kRB), 2 * wave);
         glds16(H + (int64_t)i0 * k + lo, lds_addr_of(dst));
         glds16(H + (int64_t)i1 * k + lo, lds_addr_of(dst + kRS));
     };
     // ring slot of chunk c -> bf16 planes of buffer pb (vectors past the end are 0, row kb = 1 on
     // live vectors, features >= k are 0)
     auto convert = [&](int64_t c, int pb) {
-        const float* src = &sm.u.gx.raw[c % kRB][0][0];
+        const float* src0 = ring_row((int)(c % kRB), 2 * c2);
+        const float* src1 = src0 + kRS;  // vector 2 c2 + 1: the same (v >> 3) offset
         const int64_t e0 = b + c * kCH + 2 * c2;
         const bool l0 = e0 < e, l1 = e0 + 1 < e;
         float x0[4], x1[4];  // all eight LDS reads first (unconditional: one wait, no branches)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int f = 32 * wave + 8 * g + r;
-            x0[g] = src[(2 * c2) * kRS + f];
-            x1[g] = src[(2 * c2 + 1) * kRS + f];
+            x0[g] = src0[f];
+            x1[g] = src1[f];
         }
         asm volatile("" : "+v"(x0[0]), "+v"(x0[1]), "+v"(x0[2]), "+v"(x0[3]), "+v"(x1[0]),
                      "+v"(x1[1]), "+v"(x1[2]), "+v"(x1[3]));
@@ -717,6 +760,24 @@ __device__ __forceinline__ void factor_tile(Smem& sm, f32x16 (&acc)[kSlots], int
     diag_factor_mfma(a, tT);
 }
 
+// trailing update of tile (I, K) by panel tiles pk = K - J - 1, pi = I - J - 1:
+// a -= L_IJ L_KJ^T, from the bf16x3 planes (A = -L_KJ rows, B = L_IJ rows; 12 MFMAs of 32 cycles
+// against 16 of 64 for v_mfma_f32_32x32x2_f32)
+__device__ __forceinline__ f32x16 panel_update_x3(Smem& sm, f32x16 a, int pk, int pi, int q,
+                                                  int h) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 A[3], B[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            A[p] = bf16_neg(*reinterpret_cast<const bf16x8*>(&sm.u.fz.pp[pk][p][q][16 * s2 + 8 * h]));
+            B[p] = *reinterpret_cast<const bf16x8*>(&sm.u.fz.pp[pi][p][q][16 * s2 + 8 * h]);
+        }
+        a = mfma_x3(A, B, a);
+    }
+    return a;
+}
+
 // L^T w = y by 32-column blocks, w_J = T_J^T (y_J - sum_{I>J} L_IJ^T w_I): the factor in the
 // owners' accumulators (L_IJ below the diagonal, T_J = L_JJ^{-1} on it), y in sm.yv, w to sm.wv.
 __device__ __forceinline__ void back_substitute(Smem& sm, f32x16 (&acc)[kSlots], Tiles& tl,
@@ -892,15 +953,47 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
                 f32x16 nv;
 #pragma unroll
                 for (int g = 0; g < 16; ++g) nv[g] = 0.0f;
-                if (!(dbg & 2))
-#pragma unroll
-                    for (int st = 0; st < 16; ++st)
-                        nv = __builtin_amdgcn_mfma_f32_32x32x2f32(tT[rho(st, h)][q], acc[s][st], nv,
-                                                                  0, 0, 0);
-                acc[s] = nv;
                 const int pi = tl.I[s] - J - 1;
+                if constexpr (kFactorX3) {
+                    // bf16x3 on v_mfma_f32_32x32x16_bf16: K slot (h, j) of step s2 is column
+                    // rho(8 s2 + j, h), so B is registers 8 s2 .. 8 s2 + 7 of the tile as they sit
+                    // (12 instead of 16 x 64 MFMA cycles per tile)
+                    if (!(dbg & 2))
 #pragma unroll
-                for (int g = 0; g < 16; ++g) sm.u.fz.pn[pi][q][rho(g, h)] = nv[g];
+                        for (int s2 = 0; s2 < 2; ++s2) {
+                            float av[8], bv[8];
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) {
+                                av[j] = tT[rho(8 * s2 + j, h)][q];
+                                bv[j] = acc[s][8 * s2 + j];
+                            }
+                            bf16x8 A[3], B[3];
+                            split8(av, A);
+                            split8(bv, B);
+                            nv = mfma_x3(A, B, nv);
+                        }
+                    // the panel's planes for the trailing updates, in the same K-slot order
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        float v[8];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) v[j] = nv[8 * s2 + j];
+                        bf16x8 P[3];
+                        split8(v, P);
+#pragma unroll
+                        for (int p = 0; p < 3; ++p)
+                            *reinterpret_cast<bf16x8*>(&sm.u.fz.pp[pi][p][q][16 * s2 + 8 * h]) = P[p];
+                    }
+                } else {
+                    if (!(dbg & 2))
+#pragma unroll
+                        for (int st = 0; st < 16; ++st)
+                            nv = __builtin_amdgcn_mfma_f32_32x32x2f32(tT[rho(st, h)][q], acc[s][st],
+                                                                      nv, 0, 0, 0);
+#pragma unroll
+                    for (int g = 0; g < 16; ++g) sm.u.fz.pn[pi][q][rho(g, h)] = nv[g];
+                }
+                acc[s] = nv;
                 if (tl.I[s] == nt && q == 0)  // row kb: y_J
 #pragma unroll
                     for (int g = 0; g < 16; ++g) sm.yv[32 * J + rho(g, h)] = nv[g];
@@ -912,13 +1005,16 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
                 const int own = tdn / kWaves;
 #pragma unroll
                 for (int s = 0; s < kSlots; ++s) {
-                    if (s != own) continue;
-                    const float* lr = sm.u.fz.pn[0][q];
-                    if (!(dbg & 2))
+                    if (s != own || (dbg & 2)) continue;
+                    if constexpr (kFactorX3) {
+                        acc[s] = panel_update_x3(sm, acc[s], 0, 0, q, h);
+                    } else {
+                        const float* lr = sm.u.fz.pn[0][q];
 #pragma unroll
                         for (int st = 0; st < 16; ++st)
                             acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(
                                 -lr[2 * st + h], lr[2 * st + h], acc[s], 0, 0, 0);
+                    }
                 }
                 if (!(dbg & 1)) factor_tile(sm, acc, own, sm.tT[(J + 1) & 1]);
             }
@@ -926,12 +1022,16 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
             for (int s = 0; s < kSlots; ++s) {
                 if (tl.I[s] < 0 || tl.J[s] <= J || (dbg & 2)) continue;
                 if (s * kWaves + wave == tdn) continue;
-                const float* lk = sm.u.fz.pn[tl.J[s] - J - 1][q];
-                const float* lr = sm.u.fz.pn[tl.I[s] - J - 1][q];
+                if constexpr (kFactorX3) {
+                    acc[s] = panel_update_x3(sm, acc[s], tl.J[s] - J - 1, tl.I[s] - J - 1, q, h);
+                } else {
+                    const float* lk = sm.u.fz.pn[tl.J[s] - J - 1][q];
+                    const float* lr = sm.u.fz.pn[tl.I[s] - J - 1][q];
 #pragma unroll
-                for (int st = 0; st < 16; ++st)
-                    acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(-lk[2 * st + h], lr[2 * st + h],
-                                                                  acc[s], 0, 0, 0);
+                    for (int st = 0; st < 16; ++st)
+                        acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(-lk[2 * st + h],
+                                                                      lr[2 * st + h], acc[s], 0, 0, 0);
+                }
             }
             __syncthreads();
         }
