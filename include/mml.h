@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 7
+#define MML_ABI_VERSION 8
 
 typedef int32_t mml_status;
 enum {
@@ -291,6 +291,22 @@ mml_status mml_bmf_fold_in(mml_bmf* h, int32_t n_fold, const int64_t* rated_off,
                            const int32_t* rated_items, const float* rated_values,
                            const float* init_factors, int32_t num_iter, float learn_rate,
                            float decay, float* out_vectors);
+/* RetrainUser / RetrainItem (ABI 8; MatrixFactorization.cs:142-160, BiasedMatrixFactorization.cs:
+ * 419-431), the incremental-update hook behind AddRatings / UpdateRatings / RemoveRatings
+ * (MatrixFactorization.cs:262-290, IncrementalRatingPredictor.cs:40-78).  For every listed
+ * row r of side 0 (users) or 1 (items): its bias <- 0 (MML_MF_BIASED), its factors <-
+ * init_factors[x * k ..] (the row's RowInitNormal draws, DataType/MatrixExtensions.cs:35-42, drawn
+ * by the caller in list order), then num_iter x Iterate(ByUser[r] / ByItem[r], side == 0,
+ * side == 1) (:264-310; MatrixFactorization.cs:166-196): rated_ids[rated_off[x] .. rated_off[x+1])
+ * are the other side's ids of the row's ratings in rating-index order, rated_values their values,
+ * learn_rates[x * num_iter + it] the current_learnrate of that Iterate call (MatrixFactorization's
+ * decays per call, BiasedMatrixFactorization's does not; the caller carries it).  The other side
+ * stays fixed, so the rows are independent and run at once with the ORDERED kernel's exact
+ * arithmetic; a row may be listed once.  MML_MF_BIASED and MML_MF_PLAIN, single-device handles. */
+mml_status mml_bmf_retrain(mml_bmf* h, int32_t side, int32_t n_rows, const int32_t* rows,
+                           const int64_t* rated_off, const int32_t* rated_ids,
+                           const float* rated_values, const float* init_factors,
+                           int32_t num_iter, const float* learn_rates);
 /* Predict(float[] user_vector, int item_id) (BiasedMatrixFactorization.cs:327-335; MML_MF_PLAIN:
  * MatrixFactorization.cs:222-241, bound) for n (vector, item) pairs: vectors as mml_bmf_fold_in
  * writes them, vector_index[x] selects the vector of pair x.  MML_MF_PLAIN rejects items beyond the

@@ -632,6 +632,87 @@ __global__ __launch_bounds__(64) void bmf_fold_in_kernel(
     }
 }
 
+// RetrainUser / RetrainItem (MatrixFactorization.cs:142-160, BiasedMatrixFactorization.cs:419-431)
+// for row rows[blockIdx.x] of side SIDE (0: a user row of U, 1: an item row of V): bias <- 0, the
+// factors <- init (RowInitNormal's draws), then num_iter x Iterate(ByUser[u] / ByItem[i],
+// update_user = SIDE == 0, update_item = SIDE == 1) (:264-310 / MatrixFactorization.cs:166-196)
+// over the row's ratings in index order, with the other side fixed.  Rows of one side are therefore
+// independent: one wavefront per row, lane f owning factors f, f + 64, ...; the arithmetic is the
+// ORDERED kernel's (RowScalarProduct left to right via v_readlane, RatingStep's float/double mix).
+// Frequency regularisation reads count_by_user[u] (count_by_item[i]) = the row's own list length.
+// lrs[blockIdx.x * num_iter + it] = current_learnrate of that Iterate call.
+template <int LOSS, int KM, int SIDE>
+__global__ __launch_bounds__(64) void bmf_retrain_kernel(
+    const int32_t* __restrict__ rows, const int64_t* __restrict__ off,
+    const int32_t* __restrict__ other, const float* __restrict__ values,
+    const float* __restrict__ init, const float* __restrict__ lrs, int32_t num_iter, float* U,
+    float* V, float* bu, float* bi, int32_t k, int32_t ld, BmfScalars s, float bias_learn_rate,
+    int32_t freq) {
+    constexpr bool plain = LOSS == kPlainMF;
+    const int lane = threadIdx.x;
+    const int64_t b = blockIdx.x;
+    const int32_t row = rows[b];
+    const int64_t begin = off[b], end = off[b + 1];
+    float* own = (SIDE == 0 ? U : V) + (int64_t)row * ld;
+    const float* oth = SIDE == 0 ? V : U;
+    const float* obias = SIDE == 0 ? bi : bu;
+    float fac[KM];
+#pragma unroll
+    for (int m = 0; m < KM; ++m) {
+        const int f = lane + 64 * m;
+        fac[m] = f < k ? init[b * k + f] : 0.0f;
+    }
+    const float reg0 = SIDE == 0 ? s.reg_u : s.reg_i;
+    // FrequencyRegularization (:281-282) with the whole data set's count of this row
+    const float reg = (!plain && freq) ? (float)((double)reg0 / sqrt((double)(end - begin))) : reg0;
+    float ob = 0.0f;  // the row's own bias, reset by RetrainUser / RetrainItem
+    for (int32_t it = 0; it < num_iter; ++it) {
+        const float lr = lrs[b * num_iter + it];
+        const float blr = bias_learn_rate * lr;
+        for (int64_t x = begin; x < end; ++x) {
+            const int32_t o = other[x];
+            const float* Ro = oth + (int64_t)o * ld;
+            float ro[KM];
+            float dot = 0.0f;
+#pragma unroll
+            for (int m = 0; m < KM; ++m) {
+                const int f = lane + 64 * m;
+                ro[m] = f < k ? Ro[f] : 0.0f;
+                // RowScalarProduct(user_factors, u, item_factors, i): U_u[f] * V_i[f]
+                const int bits = __float_as_int(SIDE == 0 ? fac[m] * ro[m] : ro[m] * fac[m]);
+                const int lim = min(64, k - 64 * m);
+                for (int l = 0; l < lim; ++l)
+                    dot += __int_as_float(__builtin_amdgcn_readlane(bits, l));
+            }
+            if constexpr (plain) {
+                const float err = values[x] - (s.gb + dot);
+#pragma unroll
+                for (int m = 0; m < KM; ++m)
+                    fac[m] += (float)((double)lr * (double)(err * ro[m] - reg * fac[m]));
+            } else {
+                const float bu_u = SIDE == 0 ? ob : obias[o], bi_i = SIDE == 0 ? obias[o] : ob;
+                const double score = (double)(((s.gb + bu_u) + bi_i) + dot);
+                const double sig = 1.0 / (1.0 + exp(-score));
+                const double err =
+                    (double)values[x] - ((double)s.min_rating + sig * (double)s.range);
+                const float g = gradient_common<LOSS>(sig, err, s.range);
+                ob = ob + blr * (g - (s.bias_reg * reg) * ob);
+#pragma unroll
+                for (int m = 0; m < KM; ++m) {
+                    const double delta = (double)g * (double)ro[m] - (double)reg * (double)fac[m];
+                    fac[m] += (float)((double)lr * delta);
+                }
+            }
+        }
+    }
+    if (!plain && lane == 0) (SIDE == 0 ? bu : bi)[row] = ob;
+#pragma unroll
+    for (int m = 0; m < KM; ++m) {
+        const int f = lane + 64 * m;
+        if (f < k) own[f] = fac[m];
+    }
+}
+
 // Predict(float[] user_vector, int item_id) for (vector, item) pairs: BiasedMatrixFactorization
 // (:327-335) or, plain, MatrixFactorization's bound form (MatrixFactorization.cs:222-241).
 __global__ __launch_bounds__(256) void bmf_predict_vectors_kernel(
@@ -3101,6 +3182,119 @@ extern "C" mml_status mml_bmf_fold_in(mml_bmf* h, int32_t n_fold, const int64_t*
 #undef MML_FOLD_ARGS
         MML_HIP(hipMemcpyAsync(out_vectors, dout.get(), sizeof(float) * n_fold * w,
                                hipMemcpyDeviceToHost, st));
+        MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+namespace {
+template <int LOSS, int SIDE>
+void launch_retrain(mml_bmf* h, int32_t n, const int32_t* rows, const int64_t* off,
+                    const int32_t* other, const float* values, const float* init, const float* lrs,
+                    int32_t num_iter, const BmfScalars& s) {
+    hipStream_t st = h->ctx->stream;
+#define MML_RT(KM)                                                                              \
+    bmf_retrain_kernel<LOSS, KM, SIDE><<<n, 64, 0, st>>>(                                       \
+        rows, off, other, values, init, lrs, num_iter, h->U.get(), h->V.get(), h->bu.get(),     \
+        h->bi.get(), h->k, h->ld, s, h->p.bias_learn_rate, h->p.frequency_regularization)
+    switch ((h->k + 63) / 64) {
+        case 1: MML_RT(1); break;
+        case 2: MML_RT(2); break;
+        case 3: MML_RT(3); break;
+        default: MML_RT(4); break;
+    }
+#undef MML_RT
+    MML_HIP(hipGetLastError());
+}
+
+template <int LOSS>
+void launch_retrain_side(mml_bmf* h, int32_t side, int32_t n, const int32_t* rows,
+                         const int64_t* off, const int32_t* other, const float* values,
+                         const float* init, const float* lrs, int32_t num_iter,
+                         const BmfScalars& s) {
+    if (side == 0) launch_retrain<LOSS, 0>(h, n, rows, off, other, values, init, lrs, num_iter, s);
+    else launch_retrain<LOSS, 1>(h, n, rows, off, other, values, init, lrs, num_iter, s);
+}
+}  // namespace
+
+extern "C" mml_status mml_bmf_retrain(mml_bmf* h, int32_t side, int32_t n_rows,
+                                      const int32_t* rows, const int64_t* rated_off,
+                                      const int32_t* rated_ids, const float* rated_values,
+                                      const float* init_factors, int32_t num_iter,
+                                      const float* learn_rates) {
+    return guard([&] {
+        check_handle(h);
+        single_device_only(h);
+        MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(h->p.model == MML_MF_BIASED || h->p.model == MML_MF_PLAIN,
+                    "RetrainUser / RetrainItem on the GPU: BiasedMatrixFactorization and "
+                    "MatrixFactorization");
+        MML_REQUIRE(side == 0 || side == 1, "side: 0 (users) or 1 (items)");
+        MML_REQUIRE(n_rows >= 0 && num_iter >= 0, "negative sizes");
+        if (n_rows == 0) return;
+        MML_REQUIRE(rows && rated_off && init_factors && (num_iter == 0 || learn_rates),
+                    "null arguments");
+        const int32_t n_own = side == 0 ? h->n_users : h->n_items;
+        const int32_t n_oth = side == 0 ? h->n_items : h->n_users;
+        // rows of one side train independently (the other side is fixed), so they run at once;
+        // a row listed twice would race with itself: its last retraining alone decides the result
+        std::vector<int32_t> sorted(rows, rows + n_rows);
+        std::sort(sorted.begin(), sorted.end());
+        for (int32_t x = 0; x < n_rows; ++x) {
+            MML_REQUIRE(sorted[x] >= 0 && sorted[x] < n_own, "retrained row id beyond the model");
+            MML_REQUIRE(x == 0 || sorted[x] != sorted[x - 1], "a row is listed twice");
+        }
+        MML_REQUIRE(rated_off[0] == 0, "rated_off[0] must be 0");
+        for (int32_t x = 0; x < n_rows; ++x)
+            MML_REQUIRE(rated_off[x + 1] >= rated_off[x], "rated_off must be non-decreasing");
+        const int64_t nr = rated_off[n_rows];
+        MML_REQUIRE(nr == 0 || (rated_ids && rated_values), "null rated arrays");
+        for (int64_t x = 0; x < nr; ++x)
+            MML_REQUIRE(rated_ids[x] >= 0 && rated_ids[x] < n_oth, "rated id beyond the model");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        mml::DeviceArray<int64_t> doff;
+        mml::DeviceArray<int32_t> drows, dids;
+        mml::DeviceArray<float> dvals, dinit, dlrs;
+        doff.alloc(n_rows + 1);
+        drows.alloc(n_rows);
+        dids.alloc(std::max<int64_t>(1, nr));
+        dvals.alloc(std::max<int64_t>(1, nr));
+        dinit.alloc((size_t)n_rows * h->k);
+        dlrs.alloc(std::max<int64_t>(1, (int64_t)n_rows * num_iter));
+        MML_HIP(hipMemcpyAsync(doff.get(), rated_off, sizeof(int64_t) * (n_rows + 1),
+                               hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(drows.get(), rows, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice,
+                               st));
+        if (nr > 0) {
+            MML_HIP(hipMemcpyAsync(dids.get(), rated_ids, sizeof(int32_t) * nr,
+                                   hipMemcpyHostToDevice, st));
+            MML_HIP(hipMemcpyAsync(dvals.get(), rated_values, sizeof(float) * nr,
+                                   hipMemcpyHostToDevice, st));
+        }
+        MML_HIP(hipMemcpyAsync(dinit.get(), init_factors, sizeof(float) * n_rows * h->k,
+                               hipMemcpyHostToDevice, st));
+        if (num_iter > 0)
+            MML_HIP(hipMemcpyAsync(dlrs.get(), learn_rates,
+                                   sizeof(float) * (int64_t)n_rows * num_iter,
+                                   hipMemcpyHostToDevice, st));
+        BmfScalars s;
+        s.gb = h->gb;
+        s.min_rating = h->min_rating;
+        s.range = h->max_rating - h->min_rating;
+        s.lr = 0.0f;   // per Iterate call: learn_rates
+        s.blr = 0.0f;
+        s.bias_reg = h->p.bias_reg;
+        s.reg_u = h->p.reg_u;
+        s.reg_i = h->p.reg_i;
+#define MML_RT_ARGS h, side, n_rows, drows.get(), doff.get(), dids.get(), dvals.get(), dinit.get(), \
+                    dlrs.get(), num_iter, s
+        switch (h->p.model == MML_MF_PLAIN ? kPlainMF : h->p.loss) {
+            case kPlainMF: launch_retrain_side<kPlainMF>(MML_RT_ARGS); break;
+            case MML_LOSS_MAE: launch_retrain_side<MML_LOSS_MAE>(MML_RT_ARGS); break;
+            case MML_LOSS_LOGISTIC: launch_retrain_side<MML_LOSS_LOGISTIC>(MML_RT_ARGS); break;
+            default: launch_retrain_side<MML_LOSS_RMSE>(MML_RT_ARGS); break;
+        }
+#undef MML_RT_ARGS
         MML_HIP(hipStreamSynchronize(st));
     });
 }

@@ -248,41 +248,57 @@ __device__ __forceinline__ bool row_has(const int32_t* __restrict__ cols, int64_
     return lo < re && cols[lo] == j;
 }
 
-// Per-user Bloom filter of S_u (512 bits = one 64-B line per user, three bits per item): the
-// rejection test of j reads the user's line and scans the row only when all three bits are set.
-// No false negatives, so the accepted j are exactly those of the plain test; for uniform j the
-// scan then runs with probability ~(1 - e^{-3 deg / 512})^3 (1.6 % at deg 50) instead of always:
-// one line per draw instead of the 2-3 lines of an unaligned row.
-constexpr int kBloomWords = 16;
+// Per-user record of the sampler: one aligned 64-B line per user holding the row start (words
+// 0-1), |S_u| (word 2) and a 416-bit Bloom filter of S_u (words 3-15, three bits per item).  A
+// sample reads this line instead of off[u], off[u + 1] and a separate filter line; the rejection
+// test of j reads the filter and scans the row only when all three bits are set.  No false
+// negatives, so the accepted j are exactly those of the plain test; for uniform j the scan then
+// runs with probability ~(1 - e^{-3 deg / 416})^3 (2.8 % at deg 50).  The sampler is bound by the
+// lines it moves (~10^9 samples/s), so the record takes one line per sample off the off[] gather.
+constexpr int kRecWords = 16;
+constexpr int kBloomBits = 416;
+struct UserRec {
+    int64_t rb, re;
+};
 __device__ __forceinline__ void bloom_bits(int32_t j, uint32_t& b0, uint32_t& b1, uint32_t& b2) {
     const uint64_t x = (uint64_t)(uint32_t)j * 0x9E3779B97F4A7C15ull;
-    b0 = (uint32_t)(x >> 55);
-    b1 = (uint32_t)(x >> 46) & 511u;
-    b2 = (uint32_t)(x >> 37) & 511u;
+    b0 = 96u + (uint32_t)((((x >> 48) & 0xFFFFu) * kBloomBits) >> 16);  // bit 96 = word 3
+    b1 = 96u + (uint32_t)((((x >> 32) & 0xFFFFu) * kBloomBits) >> 16);
+    b2 = 96u + (uint32_t)((((x >> 16) & 0xFFFFu) * kBloomBits) >> 16);
 }
-__device__ __forceinline__ bool bloom_maybe(const uint32_t* __restrict__ bl, int32_t j) {
+__device__ __forceinline__ bool bloom_maybe(const uint32_t* __restrict__ rec, int32_t j) {
     uint32_t b0, b1, b2;
     bloom_bits(j, b0, b1, b2);
-    return ((bl[b0 >> 5] >> (b0 & 31)) & (bl[b1 >> 5] >> (b1 & 31)) & (bl[b2 >> 5] >> (b2 & 31)) &
+    return ((rec[b0 >> 5] >> (b0 & 31)) & (rec[b1 >> 5] >> (b1 & 31)) & (rec[b2 >> 5] >> (b2 & 31)) &
             1u) != 0;
 }
-// 16 lanes per user, lane w owns word w of the user's filter
-__global__ __launch_bounds__(256) void bpr_bloom_build_kernel(const int64_t* __restrict__ off,
-                                                              const int32_t* __restrict__ cols,
-                                                              int32_t n_users,
-                                                              uint32_t* __restrict__ bloom) {
-    const int w = threadIdx.x & (kBloomWords - 1);
-    for (int64_t u = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kBloomWords; u < n_users;
-         u += (int64_t)gridDim.x * blockDim.x / kBloomWords) {
+__device__ __forceinline__ UserRec user_rec(const uint32_t* __restrict__ rec) {
+    const uint4 h = *reinterpret_cast<const uint4*>(rec);  // words 0-3: one load from the line
+    const int64_t rb = (int64_t)(((uint64_t)h.y << 32) | h.x);
+    return {rb, rb + (int64_t)h.z};
+}
+// 16 lanes per user, lane w owns word w of the user's record
+__global__ __launch_bounds__(256) void bpr_user_rec_kernel(const int64_t* __restrict__ off,
+                                                           const int32_t* __restrict__ cols,
+                                                           int32_t n_users,
+                                                           uint32_t* __restrict__ recs) {
+    const int w = threadIdx.x & (kRecWords - 1);
+    for (int64_t u = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kRecWords; u < n_users;
+         u += (int64_t)gridDim.x * blockDim.x / kRecWords) {
+        const int64_t rb = off[u], re = off[u + 1];
         uint32_t word = 0;
-        for (int64_t e = off[u]; e < off[u + 1]; ++e) {
-            uint32_t b0, b1, b2;
-            bloom_bits(cols[e], b0, b1, b2);
-            if ((int)(b0 >> 5) == w) word |= 1u << (b0 & 31);
-            if ((int)(b1 >> 5) == w) word |= 1u << (b1 & 31);
-            if ((int)(b2 >> 5) == w) word |= 1u << (b2 & 31);
-        }
-        bloom[u * kBloomWords + w] = word;
+        if (w == 0) word = (uint32_t)(uint64_t)rb;
+        else if (w == 1) word = (uint32_t)((uint64_t)rb >> 32);
+        else if (w == 2) word = (uint32_t)(re - rb);
+        else
+            for (int64_t e = rb; e < re; ++e) {
+                uint32_t b0, b1, b2;
+                bloom_bits(cols[e], b0, b1, b2);
+                if ((int)(b0 >> 5) == w) word |= 1u << (b0 & 31);
+                if ((int)(b1 >> 5) == w) word |= 1u << (b1 & 31);
+                if ((int)(b2 >> 5) == w) word |= 1u << (b2 & 31);
+            }
+        recs[u * kRecWords + w] = word;
     }
 }
 
@@ -300,7 +316,7 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
     const int32_t* __restrict__ ev_i, int64_t n_samples, int32_t n_items, uint64_t seed,
     int32_t* __restrict__ tu, int32_t* __restrict__ ti, int32_t* __restrict__ tj,
     int32_t* __restrict__ fail, uint64_t* __restrict__ user_keys,
-    const uint32_t* __restrict__ bloom) {
+    const uint32_t* __restrict__ recs) {
     for (int64_t smp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; smp < n_samples;
          smp += (int64_t)gridDim.x * blockDim.x) {
         int32_t u, i = 0, j = 0;
@@ -316,9 +332,10 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
             const uint32_t du = draw(seed, smp, 0, (uint32_t)n_eligible);
             u = eligible ? eligible[du] : (int32_t)du;
         }
-        const int64_t rb = off[u], re = off[u + 1];
-        const uint32_t* bl = bloom + (int64_t)u * kBloomWords;
-        auto in_row = [&](int32_t c) { return bloom_maybe(bl, c) && row_has(cols, rb, re, c); };
+        const uint32_t* rec = recs + (int64_t)u * kRecWords;
+        const UserRec ur = user_rec(rec);
+        const int64_t rb = ur.rb, re = ur.re;
+        auto in_row = [&](int32_t c) { return bloom_maybe(rec, c) && row_has(cols, rb, re, c); };
         if constexpr (SAMPLER == MML_BPR_SAMPLER_UNIFORM_USER)
             i = cols[rb + draw(seed, smp, 1, (uint32_t)(re - rb))];
         // USER_REPLACEMENT: i is resolved after the epoch's samples are ranked per user
@@ -632,7 +649,7 @@ struct mml_bpr {
     mml::DeviceArray<int32_t> cols, eligible, ev_u, ev_i, q_u, q_i;
     mml::DeviceArray<int32_t> tri_u, tri_i, tri_j;  // the epoch's triples (two-phase epoch)
     mml::DeviceArray<int32_t> fail;                 // WEIGHTED sampler: a sample ran out of draws
-    mml::DeviceArray<uint32_t> bloom;               // per-user Bloom filter of S_u (sampler)
+    mml::DeviceArray<uint32_t> recs;                // per-user sampler records (row, |S_u|, Bloom)
     mml::DeviceArray<uint64_t> rank_keys, rank_sorted;  // USER_REPLACEMENT: (u << 32 | s)
     mml::DeviceArray<int64_t> rank_head;                // USER_REPLACEMENT: first position per user
     mml::DeviceArray<uint8_t> rank_tmp;                 // its radix-sort scratch
@@ -808,9 +825,9 @@ void bpr_ingest(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t 
     h->off.swap(csr.off);
     h->cols.swap(csr.cols);
     h->nnz = csr.nnz;
-    h->bloom.alloc((size_t)h->n_users * kBloomWords);
-    bpr_bloom_build_kernel<<<grid_for((int64_t)h->n_users * kBloomWords), 256, 0, st>>>(
-        h->off.get(), h->cols.get(), h->n_users, h->bloom.get());
+    h->recs.alloc((size_t)h->n_users * kRecWords);
+    bpr_user_rec_kernel<<<grid_for((int64_t)h->n_users * kRecWords), 256, 0, st>>>(
+        h->off.get(), h->cols.get(), h->n_users, h->recs.get());
     MML_HIP(hipGetLastError());
     h->n_events = n;
     h->n_eligible = (int32_t)elig.size();
@@ -1255,7 +1272,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
     bpr_sample_kernel<KIND><<<sgrid, 256, 0, st>>>(                                            \
         h->off.get(), h->cols.get(), ELIG, h->n_eligible, h->ev_u.get(), h->ev_i.get(), n,    \
         h->n_items, seed, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), h->fail.get(),       \
-        h->rank_keys.get(), h->bloom.get())
+        h->rank_keys.get(), h->recs.get())
             int32_t* elig = h->n_eligible == h->n_users ? nullptr : h->eligible.get();
             switch (h->p.sampler) {
                 case MML_BPR_SAMPLER_UNIFORM_PAIR:

@@ -95,6 +95,49 @@ class Ratings:
                 np.arange(self.count, dtype=np.int32))
         return self._random_index
 
+    def _invalidate(self):
+        self._count_by_user = None
+        self._count_by_item = None
+
+    def add(self, users, items, values):
+        """Ratings.Add for each rating in order (Data/Ratings.cs:150-175): appended, so every
+        existing index keeps its place; MaxUserID / MaxItemID grow; the scale stays."""
+        self.users = np.ascontiguousarray(np.concatenate([self.users, np.asarray(users, np.int32)]))
+        self.items = np.ascontiguousarray(np.concatenate([self.items, np.asarray(items, np.int32)]))
+        self.values = np.ascontiguousarray(
+            np.concatenate([self.values, np.asarray(values, np.float32)]))
+        if len(self.users):
+            self.max_user_id = max(self.max_user_id, int(self.users.max()))
+            self.max_item_id = max(self.max_item_id, int(self.items.max()))
+        self._invalidate()
+
+    def _first_index(self, u: int, i: int) -> int:
+        """DataSet.TryGetIndex (Data/DataSet.cs:229-241): the first index of (u, i), or -1."""
+        hit = np.flatnonzero((self.users == u) & (self.items == i))
+        return int(hit[0]) if len(hit) else -1
+
+    def update(self, users, items, values):
+        """IncrementalRatingPredictor.UpdateRatings' loop (:54-68): the value at TryGetIndex of
+        each (user, item) is replaced; a missing pair raises like the reference."""
+        for u, i, v in zip(np.asarray(users).tolist(), np.asarray(items).tolist(),
+                           np.asarray(values, np.float32).tolist()):
+            x = self._first_index(u, i)
+            if x < 0:
+                raise KeyError(f"Cannot update rating for user {u} and item {i}: No such rating "
+                               "exists.")
+            self.values[x] = np.float32(v)
+
+    def remove(self, users, items):
+        """IncrementalRatingPredictor.RemoveRatings' loop (:71-78): Ratings.RemoveAt (:193-201)
+        of TryGetIndex of each existing (user, item), one at a time (later indices shift)."""
+        for u, i in zip(np.asarray(users).tolist(), np.asarray(items).tolist()):
+            x = self._first_index(u, i)
+            if x >= 0:
+                self.users = np.delete(self.users, x)
+                self.items = np.delete(self.items, x)
+                self.values = np.delete(self.values, x)
+        self._invalidate()
+
     @property
     def average(self) -> float:
         """Ratings.Average (Data/Ratings.cs:76-84): double sum, (float) sum / Count."""

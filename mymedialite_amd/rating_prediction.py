@@ -38,6 +38,14 @@ def _large(ratings) -> bool:
     return ratings is not None and ratings.count >= AUTO_EXACT_MAX
 
 
+def _first_appearance(ids):
+    """DataSet.AllUsers / AllItems (Data/DataSet.cs:112-131): distinct ids in the insertion order
+    of a fresh HashSet, i.e. of first appearance."""
+    a = np.asarray(ids, np.int64)
+    _, first = np.unique(a, return_index=True)
+    return a[np.sort(first)].tolist()
+
+
 def _note_auto_hogwild(rec):
     """Schedule=auto leaves the reference's sequential loop for Hogwild on large sets: say so once
     per recommender (the result is then statistically, not bitwise, the reference's)."""
@@ -261,6 +269,143 @@ class MatrixFactorization(Recommender):
 
     def fold_in(self, rated_items) -> np.ndarray:
         return self.fold_in_batch([rated_items])[0]
+
+    # ------------------------------------------------------------------ incremental updates
+    UpdateUsers = True  # IncrementalRatingPredictor.UpdateUsers / UpdateItems (:27-36)
+    UpdateItems = True
+
+    def _decays_per_call(self) -> bool:
+        """MatrixFactorization.Iterate(IList, bool, bool) ends with UpdateLearnRate (:190-197);
+        BiasedMatrixFactorization's override (:264-310) does not."""
+        return self.MODEL == N.MF_PLAIN
+
+    def _retrain(self, side: int, ids):
+        """RetrainUser / RetrainItem over ``ids`` in order (MatrixFactorization.cs:142-160,
+        BiasedMatrixFactorization.cs:419-431) in one mml_bmf_retrain call: per id the RNG draws
+        of RowInitNormal (DataType/MatrixExtensions.cs:35-42) and the current_learnrate of each of
+        its NumIter Iterate(ByUser[u] / ByItem[i]) calls, computed here in the reference's order;
+        the device trains all rows at once (the other side is fixed, so they are independent).
+        An id listed twice is retrained twice by the reference: the last retraining decides."""
+        if self._h is None:
+            raise RuntimeError("Train() or load_model() first")
+        ids = [int(x) for x in ids]
+        if not ids:
+            return
+        update = self.UpdateUsers if side == 0 else self.UpdateItems
+        k, num_iter = int(self.NumFactors), int(self.NumIter)
+        last = {}
+        if update:
+            rng = Random.get_instance()
+            lr = np.float32(self.current_learnrate)
+            for pos, row in enumerate(ids):
+                init = rng.fill_normal(k, self.InitMean, self.InitStdDev)
+                lrs = np.empty(num_iter, np.float32)
+                for it in range(num_iter):
+                    lrs[it] = lr
+                    if self._decays_per_call():
+                        lr = np.float32(lr * np.float32(self.Decay))
+                last[row] = (pos, init, lrs)
+            self.current_learnrate = float(lr)
+        elif self.MODEL == N.MF_PLAIN:
+            return  # nothing to do: no bias, factors untouched
+        else:
+            # BiasedMatrixFactorization resets the bias even when the factors stay (:419-431):
+            # retrain with the current factors as "init" and no Iterate call
+            m = self.get_model()
+            src = m["U"] if side == 0 else m["V"]
+            for pos, row in enumerate(ids):
+                last[row] = (pos, np.array(src[row], np.float32), np.empty(0, np.float32))
+            num_iter = 0
+        rows = sorted(last, key=lambda r: last[r][0])
+        r = self._ratings
+        key = r.users if side == 0 else r.items
+        oth = r.items if side == 0 else r.users
+        order = np.argsort(key, kind="stable")  # ByUser / ByItem: rating indices ascending
+        starts = np.searchsorted(key[order], rows, side="left")
+        ends = np.searchsorted(key[order], rows, side="right")
+        sel = np.concatenate([order[a:b] for a, b in zip(starts, ends)]) if rows else \
+            np.zeros(0, np.int64)
+        off = np.zeros(len(rows) + 1, np.int64)
+        off[1:] = np.cumsum(ends - starts)
+        rows_a = N.i32(rows)
+        ids_a, vals_a = N.i32(oth[sel]), N.f32(r.values[sel])
+        init = N.f32(np.concatenate([last[x][1] for x in rows]))
+        lrs = N.f32(np.concatenate([last[x][2] for x in rows])) if num_iter else None
+        N.check(N.lib().mml_bmf_retrain(
+            self._h, side, len(rows), N.ptr(rows_a, N._i32p), N.ptr(off, N._i64p),
+            N.ptr(ids_a, N._i32p), N.ptr(vals_a, N._f32p), N.ptr(init, N._f32p), num_iter,
+            N.ptr(lrs, N._f32p)))
+        self._host = None
+
+    def retrain_user(self, user_id: int):
+        """RetrainUser (MatrixFactorization.cs:142-149; BiasedMatrixFactorization.cs:419-423)."""
+        self._retrain(0, [user_id])
+
+    def retrain_item(self, item_id: int):
+        """RetrainItem (MatrixFactorization.cs:153-160; BiasedMatrixFactorization.cs:426-431)."""
+        self._retrain(1, [item_id])
+
+    def retrain_users(self, user_ids):
+        """RetrainUser for each id in order, one device call."""
+        self._retrain(0, user_ids)
+
+    def retrain_items(self, item_ids):
+        """RetrainItem for each id in order, one device call."""
+        self._retrain(1, item_ids)
+
+    def _grow(self, max_user_id: int, max_item_id: int):
+        """AddUser / AddItem (MatrixFactorization.cs:292-303, Matrix.AddRows: new rows 0;
+        BiasedMatrixFactorization.cs:404-416: the bias arrays grow with zeros)."""
+        nu, ni = self.MaxUserID + 1, self.MaxItemID + 1
+        nu2, ni2 = max(nu, max_user_id + 1), max(ni, max_item_id + 1)
+        if (nu2, ni2) == (nu, ni):
+            return
+        m = self.get_model()
+        grown = {}
+        for name, n2 in (("U", nu2), ("V", ni2), ("bu", nu2), ("bi", ni2)):
+            if name not in m:
+                continue
+            a = m[name]
+            pad = np.zeros((n2 - a.shape[0],) + a.shape[1:], np.float32)
+            grown[name] = np.ascontiguousarray(np.concatenate([a, pad]), np.float32)
+        self.MaxUserID, self.MaxItemID = nu2 - 1, ni2 - 1
+        lr = self.current_learnrate
+        self._create_handle(nu2, ni2)
+        self._host = grown
+        self._upload_model(self.global_bias)
+        self._host = None
+        self.current_learnrate = lr
+
+    def add_ratings(self, new: Ratings):
+        """AddRatings (MatrixFactorization.cs:262-270 over IncrementalRatingPredictor.cs:40-51):
+        new users / items grow the model, the ratings are appended (Ratings.Add), then RetrainUser
+        for every user and RetrainItem for every item of ``new`` in first-appearance order
+        (DataSet.AllUsers / AllItems: a HashSet's insertion order)."""
+        if self._h is None:
+            raise RuntimeError("Train() or load_model() first")
+        self._grow(new.max_user_id, new.max_item_id)
+        self._ratings.add(new.users, new.items, new.values)
+        self._order_uploaded = False  # the next Iterate() uploads the grown set (RandomIndex anew)
+        self.retrain_users(_first_appearance(new.users))
+        self.retrain_items(_first_appearance(new.items))
+
+    def update_ratings(self, new: Ratings):
+        """UpdateRatings (MatrixFactorization.cs:272-280 over IncrementalRatingPredictor.cs:
+        54-68): each (user, item) must exist (Ratings.TryGetIndex: its first index); its value is
+        replaced, then the users and the items are retrained."""
+        self._ratings.update(new.users, new.items, new.values)
+        self._order_uploaded = False
+        self.retrain_users(_first_appearance(new.users))
+        self.retrain_items(_first_appearance(new.items))
+
+    def remove_ratings(self, gone):
+        """RemoveRatings (MatrixFactorization.cs:282-290 over IncrementalRatingPredictor.cs:
+        71-78): the first index of each existing (user, item) is removed (Ratings.RemoveAt), then
+        every user and item of ``gone`` is retrained."""
+        self._ratings.remove(gone.users, gone.items)
+        self._order_uploaded = False
+        self.retrain_users(_first_appearance(gone.users))
+        self.retrain_items(_first_appearance(gone.items))
 
     def predict_vectors(self, vectors, vector_index, items) -> np.ndarray:
         """Predict(float[] user_vector, int item_id) for (vector, item) pairs on the GPU."""

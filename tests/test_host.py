@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert set(declared) == set(N.SIGNATURES), set(declared) ^ set(N.SIGNATURES)
-    assert L.mml_abi_version() == 7
+    assert L.mml_abi_version() == 8
 
 
 def test_no_device_is_an_error_not_a_crash():
@@ -368,3 +368,23 @@ def test_release_library_ignores_experiment_switches():
         if f.endswith((".hip", ".cpp", ".h")):
             text = open(os.path.join(src, f)).read()
             assert "std::getenv(" not in text.replace("std::getenv(name)", ""), f
+
+
+def test_ratings_add_update_remove_semantics():
+    # Ratings.Add appends (Data/Ratings.cs:150-175); UpdateRatings / RemoveRatings act on
+    # DataSet.TryGetIndex's FIRST index (Data/DataSet.cs:229-241); AllUsers is first-appearance order
+    from mymedialite_amd import Ratings
+    from mymedialite_amd.rating_prediction import _first_appearance
+    r = Ratings(np.array([0, 1, 0], np.int32), np.array([2, 2, 2], np.int32),
+                np.array([1, 2, 3], np.float32))
+    r.add([5, 1], [0, 3], [4.0, 5.0])
+    assert r.count == 5 and r.max_user_id == 5 and r.max_item_id == 3
+    assert r.count_by_user.tolist() == [2, 2, 0, 0, 0, 1]
+    r.update([0], [2], [4.5])
+    assert r.values.tolist() == [4.5, 2.0, 3.0, 4.0, 5.0]
+    with pytest.raises(KeyError):
+        r.update([4], [4], [1.0])
+    r.remove([0, 9], [2, 9])  # a missing pair is skipped
+    assert r.users.tolist() == [1, 0, 5, 1] and r.values.tolist() == [2.0, 3.0, 4.0, 5.0]
+    assert r.count_by_user.tolist() == [1, 2, 0, 0, 0, 1]
+    assert _first_appearance([7, 3, 7, 1, 3]) == [7, 3, 1]
