@@ -464,6 +464,15 @@ mml_status mml_wrmf_get_model(mml_wrmf* h, float* user_factors, float* item_fact
 /* One WRMF.Iterate() (WRMF.cs:68-73): Optimize(users | items) then Optimize(items | users),
  * each = ComputeSquareMatrix (:94-108) + one k x k solve per row (:110-156), fp64. */
 mml_status mml_wrmf_iterate(mml_wrmf* h);
+/* WRMF.RetrainUser / RetrainItem (ABI 8; ItemRecommendation/WRMF.cs:159-170), the hook behind
+ * MF.AddFeedback / RemoveFeedback (ItemRecommendation/MF.cs:73-99): for every listed row r of
+ * side 0 (users) or 1 (items), Optimize(r) against the fixed other side with HH recomputed from it
+ * (ComputeSquareMatrix).  rated_ids[rated_off[x] .. rated_off[x+1]) are the other side's ids of
+ * row x's feedback (Feedback.UserMatrix / ItemMatrix row).  The rows are independent, so they run
+ * as one half-step over their own CSR with the iterate's solvers and precision; a row may be
+ * listed once.  Single-device handles. */
+mml_status mml_wrmf_retrain(mml_wrmf* h, int32_t side, int32_t n_rows, const int32_t* rows,
+                            const int64_t* rated_off, const int32_t* rated_ids);
 /* MF.Predict (MF.cs:151-157): float.MinValue for ids beyond the model. */
 mml_status mml_wrmf_predict(mml_wrmf* h, const int32_t* users, const int32_t* items, int64_t n,
                             float* out);

@@ -594,8 +594,10 @@ void run_blocked(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, 
 }
 
 // W rows [r0, r1) <- H (all h_rows rows); off/cols: the CSR of W's rows
+// (plan: the k > 128 row plan of W's rows; null = the handle's plan of U or V)
 void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, int64_t h_rows,
-               const int64_t* off, const int32_t* cols, int64_t n_data_rows, int& launches) {
+               const int64_t* off, const int32_t* cols, int64_t n_data_rows, int& launches,
+               mml::WrmfTilePlan* plan_in = nullptr) {
     hipStream_t st = h->ctx->stream;
     const int k = h->k;
     const int nt = (k + 63) / 64;
@@ -617,7 +619,7 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
     } else if (use_blocked_solver()) {
         run_blocked<float, 256>(h, W, r0, r1, H, off, cols, n_data_rows);
     } else {
-        mml::WrmfTilePlan& plan = W == h->U.get() ? h->uplan : h->iplan;
+        mml::WrmfTilePlan& plan = plan_in ? *plan_in : W == h->U.get() ? h->uplan : h->iplan;
         plan.keep_factor = h->p.refine_passes > 0;
         mml::wrmf_tile_solve(st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha,
                              h->p.regularization, launches);
@@ -925,6 +927,83 @@ extern "C" mml_status mml_wrmf_iterate(mml_wrmf* h) {
         MML_HIP(hipEventSynchronize(h->ctx->ev_end));
         MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));
         h->last_launches = launches;
+    });
+}
+
+namespace {
+__global__ __launch_bounds__(256) void wrmf_rows_scatter_kernel(const float* __restrict__ src,
+                                                                const int32_t* __restrict__ rows,
+                                                                int32_t n, int32_t k,
+                                                                float* __restrict__ W) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)n * k;
+         e += (int64_t)gridDim.x * blockDim.x)
+        W[(int64_t)rows[e / k] * k + e % k] = src[e];
+}
+}  // namespace
+
+extern "C" mml_status mml_wrmf_retrain(mml_wrmf* h, int32_t side, int32_t n_rows,
+                                       const int32_t* rows, const int64_t* rated_off,
+                                       const int32_t* rated_ids) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(!h->ctx->multi(), "RetrainUser / RetrainItem run on a single-device handle");
+        MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(side == 0 || side == 1, "side: 0 (users) or 1 (items)");
+        MML_REQUIRE(n_rows >= 0, "negative sizes");
+        if (n_rows == 0) return;
+        MML_REQUIRE(rows && rated_off, "null arguments");
+        const int32_t n_own = side == 0 ? h->n_users : h->n_items;
+        const int32_t n_oth = side == 0 ? h->n_items : h->n_users;
+        std::vector<int32_t> sorted(rows, rows + n_rows);
+        std::sort(sorted.begin(), sorted.end());
+        for (int32_t x = 0; x < n_rows; ++x) {
+            MML_REQUIRE(sorted[x] >= 0 && sorted[x] < n_own, "retrained row id beyond the model");
+            MML_REQUIRE(x == 0 || sorted[x] != sorted[x - 1], "a row is listed twice");
+        }
+        MML_REQUIRE(rated_off[0] == 0, "rated_off[0] must be 0");
+        std::vector<int64_t> deg(n_rows);
+        for (int32_t x = 0; x < n_rows; ++x) {
+            MML_REQUIRE(rated_off[x + 1] >= rated_off[x], "rated_off must be non-decreasing");
+            deg[x] = rated_off[x + 1] - rated_off[x];
+        }
+        const int64_t nr = rated_off[n_rows];
+        MML_REQUIRE(nr == 0 || rated_ids, "null rated ids");
+        for (int64_t x = 0; x < nr; ++x)
+            MML_REQUIRE(rated_ids[x] >= 0 && rated_ids[x] < n_oth, "rated id beyond the model");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        // the listed rows as a CSR of their own: one half-step over it solves them with the
+        // iterate's kernels (HH recomputed from the fixed side, as RetrainUser's
+        // ComputeSquareMatrix), then the solved rows go to their places
+        mml::DeviceArray<int64_t> doff;
+        mml::DeviceArray<int32_t> dids, drows;
+        mml::DeviceArray<float> wsub;
+        doff.alloc(n_rows + 1);
+        dids.alloc(std::max<int64_t>(1, nr));
+        drows.alloc(n_rows);
+        wsub.alloc((size_t)n_rows * h->k);
+        MML_HIP(hipMemcpyAsync(doff.get(), rated_off, sizeof(int64_t) * (n_rows + 1),
+                               hipMemcpyHostToDevice, st));
+        if (nr > 0)
+            MML_HIP(hipMemcpyAsync(dids.get(), rated_ids, sizeof(int32_t) * nr,
+                                   hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(drows.get(), rows, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice,
+                               st));
+        float* W = side == 0 ? h->U.get() : h->V.get();
+        const float* H = side == 0 ? h->V.get() : h->U.get();
+        const int64_t h_rows = side == 0 ? h->n_items : h->n_users;
+        mml::WrmfTilePlan plan;
+        if (h->k > 128)
+            mml::wrmf_tile_plan(deg, st, plan, 0, n_rows, h->p.alpha > 0.0 && !no_woodbury());
+        int launches = 0;
+        h->last_refine = 0;
+        std::fill(h->last_corr, h->last_corr + 8, 0.0f);
+        half_step(h, wsub.get(), 0, n_rows, H, h_rows, doff.get(), dids.get(), n_rows, launches,
+                  &plan);
+        wrmf_rows_scatter_kernel<<<(int)std::min<int64_t>(4096, ((int64_t)n_rows * h->k + 255) / 256),
+                                   256, 0, st>>>(wsub.get(), drows.get(), n_rows, h->k, W);
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipStreamSynchronize(st));
     });
 }
 

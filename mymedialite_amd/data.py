@@ -158,6 +158,25 @@ class PosOnlyFeedback:
     def count(self) -> int:
         return len(self.users)
 
+    def add(self, users, items):
+        """PosOnlyFeedback.Add for each pair in order (Data/PosOnlyFeedback.cs:88-104)."""
+        self.users = np.ascontiguousarray(np.concatenate([self.users, np.asarray(users, np.int32)]))
+        self.items = np.ascontiguousarray(np.concatenate([self.items, np.asarray(items, np.int32)]))
+        if len(self.users):
+            self.max_user_id = max(self.max_user_id, int(self.users.max()))
+            self.max_item_id = max(self.max_item_id, int(self.items.max()))
+        self._user_rows = self._item_rows = None
+
+    def remove(self, users, items):
+        """PosOnlyFeedback.Remove for each pair (Data/PosOnlyFeedback.cs:106-120): every event
+        of the pair goes, and the pair leaves both matrices."""
+        keep = np.ones(len(self.users), bool)
+        for u, i in zip(np.asarray(users).tolist(), np.asarray(items).tolist()):
+            keep &= ~((self.users == u) & (self.items == i))
+        self.users = np.ascontiguousarray(self.users[keep])
+        self.items = np.ascontiguousarray(self.items[keep])
+        self._user_rows = self._item_rows = None
+
     @staticmethod
     def _rows(r, c, n_rows):
         """Distinct (r, c) pairs grouped by r, each row in first-insertion order -> CSR."""

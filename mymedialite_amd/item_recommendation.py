@@ -493,6 +493,92 @@ class WRMF(_MFBase):
     def item_factors(self):
         return self.get_model()["V"]
 
+    # ------------------------------------------------------------------ incremental updates
+    UpdateUsers = True  # IncrementalItemRecommender.UpdateUsers / UpdateItems
+    UpdateItems = True
+
+    def _retrain(self, side: int, ids):
+        """RetrainUser / RetrainItem (WRMF.cs:159-170) for ``ids`` in one mml_wrmf_retrain call:
+        each row is Optimize(r) against the fixed other side, so the rows are independent and a
+        repeated id changes nothing (its second solve equals its first)."""
+        if self._h is None:
+            raise RuntimeError("Train() or load_model() first")
+        rows = list(dict.fromkeys(int(x) for x in ids))
+        if not rows:
+            return
+        fb = self._feedback
+        off, cols = fb.user_matrix if side == 0 else fb.item_matrix
+        nrow = len(off) - 1
+        parts = [cols[off[r]:off[r + 1]] if r < nrow else np.zeros(0, np.int32) for r in rows]
+        roff = np.zeros(len(rows) + 1, np.int64)
+        roff[1:] = np.cumsum([len(x) for x in parts])
+        rid = N.i32(np.concatenate(parts)) if parts else np.zeros(0, np.int32)
+        rows_a = N.i32(rows)
+        N.check(N.lib().mml_wrmf_retrain(self._h, side, len(rows), N.ptr(rows_a, N._i32p),
+                                         N.ptr(roff, N._i64p), N.ptr(rid, N._i32p)))
+        self._host = None
+
+    def retrain_users(self, user_ids):
+        self._retrain(0, user_ids)
+
+    def retrain_items(self, item_ids):
+        self._retrain(1, item_ids)
+
+    def _grow_and_reload(self, U, V):
+        """Re-create the handle at the grown sizes with the edited feedback and the factors."""
+        self._load_device_model(np.ascontiguousarray(U, np.float32),
+                                np.ascontiguousarray(V, np.float32), None)
+        fb = self._feedback
+        N.check(N.lib().mml_wrmf_set_data(self._h, N.ptr(fb.users, N._i32p),
+                                          N.ptr(fb.items, N._i32p), fb.count))
+
+    def add_feedback(self, users, items):
+        """MF.AddFeedback (ItemRecommendation/MF.cs:73-91) over IncrementalItemRecommender.
+        AddFeedback (:38-53): per (user, item) in order, a new user / item id grows the model
+        (MF.AddUser / AddItem, :108-122: AddRows, then RowInitNormal of that row from the shared
+        RNG), the pair is added to Feedback; then RetrainUser for the users and RetrainItem for
+        the items of the batch (HashSet insertion order)."""
+        users = [int(x) for x in np.atleast_1d(users)]
+        items = [int(x) for x in np.atleast_1d(items)]
+        m = self.get_model()
+        U, V = m["U"], m["V"]
+        k = int(self.NumFactors)
+        rng = Random.get_instance()
+        for u, i in zip(users, items):
+            if u > self.MaxUserID:
+                U = np.concatenate([U, np.zeros((u + 1 - U.shape[0], k), np.float32)])
+                U[u] = rng.fill_normal(k, self.InitMean, self.InitStdDev)
+                self.MaxUserID = u
+            if i > self.MaxItemID:
+                V = np.concatenate([V, np.zeros((i + 1 - V.shape[0], k), np.float32)])
+                V[i] = rng.fill_normal(k, self.InitMean, self.InitStdDev)
+                self.MaxItemID = i
+        self._feedback.add(users, items)
+        self._grow_and_reload(U, V)
+        if self.UpdateUsers:
+            self.retrain_users(users)
+        if self.UpdateItems:
+            self.retrain_items(items)
+
+    def remove_feedback(self, users, items):
+        """MF.RemoveFeedback (MF.cs:93-99) over IncrementalItemRecommender.RemoveFeedback
+        (:56-71): ids beyond the model raise; every occurrence of each pair leaves Feedback
+        (PosOnlyFeedback.Remove); then the users and items are retrained."""
+        users = [int(x) for x in np.atleast_1d(users)]
+        items = [int(x) for x in np.atleast_1d(items)]
+        for u, i in zip(users, items):
+            if u > self.MaxUserID:
+                raise ValueError(f"Unknown user {u}")
+            if i > self.MaxItemID:
+                raise ValueError(f"Unknown item {i}")
+        m = self.get_model()
+        self._feedback.remove(users, items)
+        self._grow_and_reload(m["U"], m["V"])
+        if self.UpdateUsers:
+            self.retrain_users(users)
+        if self.UpdateItems:
+            self.retrain_items(items)
+
     def predict(self, users, items) -> np.ndarray:
         u, i = N.i32(np.atleast_1d(users)), N.i32(np.atleast_1d(items))
         out = np.empty(len(u), np.float32)
