@@ -408,6 +408,18 @@ mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed);
  * path for a host that draws its own triples (e.g. the C# SampleTriple on System.Random). */
 mml_status mml_bpr_apply_triples(mml_bpr* h, const int32_t* users, const int32_t* items,
                                  const int32_t* other_items, int64_t n);
+/* The same with UpdateFactors' update_u / update_i / update_j per triple (ABI 8; flags[x] bits 0,
+ * 1, 2; BPRMF.cs:330-374): RetrainUser (:391-402) applies its SampleItemPair triples with u only,
+ * RetrainItem (:405-422) its SampleUser / SampleOtherItem triples with the retrained item only,
+ * strictly in order on one wavefront. */
+mml_status mml_bpr_apply_triples_flags(mml_bpr* h, const int32_t* users, const int32_t* items,
+                                       const int32_t* other_items, const uint8_t* flags,
+                                       int64_t n);
+/* Overwrite factor rows (ABI 8): side 0 user rows, 1 item rows, values [n_rows x num_factors]
+ * row-major, in list order (RowInitNormal of RetrainUser / RetrainItem, DataType/
+ * MatrixExtensions.cs:35-42, drawn on the host); biases untouched. */
+mml_status mml_bpr_set_rows(mml_bpr* h, int32_t side, int32_t n_rows, const int32_t* rows,
+                            const float* values);
 /* BPRMF.Predict (:425-431), batched: float.MinValue for ids beyond the model. */
 mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t n,
                            float* out);

@@ -118,6 +118,9 @@ SIGNATURES = {
     "mml_bmf_set_user_relation": (_st, [_vp, ctypes.c_int32, _i64p, _i32p]),
     "mml_bmf_fold_in": (_st, [_vp, ctypes.c_int32, _i64p, _i32p, _f32p, _f32p, ctypes.c_int32,
                               ctypes.c_float, ctypes.c_float, _f32p]),
+    "mml_bpr_apply_triples_flags": (_st, [_vp, _i32p, _i32p, _i32p, ctypes.c_void_p,
+                                          ctypes.c_int64]),
+    "mml_bpr_set_rows": (_st, [_vp, ctypes.c_int32, ctypes.c_int32, _i32p, _f32p]),
     "mml_wrmf_retrain": (_st, [_vp, ctypes.c_int32, ctypes.c_int32, _i32p, _i64p, _i32p]),
     "mml_bmf_retrain": (_st, [_vp, ctypes.c_int32, ctypes.c_int32, _i32p, _i64p, _i32p, _f32p,
                               _f32p, ctypes.c_int32, _f32p]),

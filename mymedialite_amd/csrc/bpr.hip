@@ -548,7 +548,8 @@ template <bool SOFT, int KM, bool XCD1 = false>
 __global__ __launch_bounds__(256) void bpr_apply_ordered_kernel(
     const int32_t* __restrict__ tu, const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
     int64_t n, float* U, float* V, float* bias, int32_t k, int32_t ld, BprScalars s,
-    uint32_t u_bytes = 0, uint32_t v_bytes = 0, uint32_t b_bytes = 0) {
+    uint32_t u_bytes = 0, uint32_t v_bytes = 0, uint32_t b_bytes = 0,
+    const uint8_t* __restrict__ flags = nullptr) {
     const int lane = threadIdx.x & 63;
     int64_t W = blockDim.x >> 6, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if constexpr (XCD1) {
@@ -588,18 +589,23 @@ __global__ __launch_bounds__(256) void bpr_apply_ordered_kernel(
         const float bi = ld1(rb, bias, bias + i), bj = ld1(rb, bias, bias + j);
         const TripleStep<SOFT> t(s, (double)(bi - bj) + dot);
         if (t.skip) continue;
+        // UpdateFactors' update_u / update_i / update_j (BPRMF.cs:330-374): per triple when
+        // flags are given (bits 0, 1, 2: RetrainUser / RetrainItem, :391-422), else u, i and
+        // UpdateJ as in Iterate
+        const int fl = flags ? (int)flags[x] : (3 | (s.update_j ? 4 : 0));
+        const bool up_u = (fl & 1) != 0, up_i = (fl & 2) != 0, up_j = (fl & 4) != 0;
         if (lane == 0) {  // i == j: the reference re-reads item_bias[j] after writing [i]
-            const float nbi = t.bias_i(s, bi);
-            bias[i] = nbi;
-            if (s.update_j) bias[j] = t.bias_j(s, i == j ? nbi : bj);
+            const float nbi = up_i ? t.bias_i(s, bi) : bi;
+            if (up_i) bias[i] = nbi;
+            if (up_j) bias[j] = t.bias_j(s, i == j ? nbi : bj);
         }
 #pragma unroll
         for (int m = 0; m < KM; ++m) {
             const int f = lane + 64 * m;
             if (f < k) {
-                Wu[f] = t.u(s, w[m], hi[m], hj[m]);
-                Hi[f] = t.i(s, w[m], hi[m]);
-                if (s.update_j) Hj[f] = t.j(s, w[m], hj[m]);
+                if (up_u) Wu[f] = t.u(s, w[m], hi[m], hj[m]);
+                if (up_i) Hi[f] = t.i(s, w[m], hi[m]);
+                if (up_j) Hj[f] = t.j(s, w[m], hj[m]);
             }
         }
     }
@@ -1033,7 +1039,7 @@ namespace {
 // one wavefront applies n triples in order (bpr_apply_ordered_kernel), k <= 256
 void launch_apply_ordered(mml_bpr* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
                           int64_t n, const BprScalars& s, hipStream_t st, int waves = 1,
-                          int xcd1_blocks = 0) {
+                          int xcd1_blocks = 0, const uint8_t* flags = nullptr) {
     const int km = (h->k + 63) / 64;
     const bool soft = h->p.model == MML_BPR_MODEL_SOFT_MARGIN;
     const uint32_t ub = (uint32_t)((uint64_t)h->n_users * h->ld * 4);
@@ -1045,7 +1051,7 @@ void launch_apply_ordered(mml_bpr* h, const int32_t* tu, const int32_t* ti, cons
             tu, ti, tj, n, h->U.get(), h->V.get(), h->bias.get(), h->k, h->ld, s, ub, vb, bb); \
     else                                                                                        \
         bpr_apply_ordered_kernel<SOFT, KM><<<1, 64 * waves, 0, st>>>(                           \
-            tu, ti, tj, n, h->U.get(), h->V.get(), h->bias.get(), h->k, h->ld, s)
+            tu, ti, tj, n, h->U.get(), h->V.get(), h->bias.get(), h->k, h->ld, s, 0, 0, 0, flags)
 #define MML_APPLY_K(SOFT)                   \
     switch (km) {                           \
         case 1: MML_APPLY(SOFT, 1); break;  \
@@ -1438,6 +1444,62 @@ extern "C" mml_status mml_bpr_apply_triples(mml_bpr* h, const int32_t* users,
         MML_HIP(hipMemcpyAsync(dj.get(), other_items, sizeof(int32_t) * n, hipMemcpyHostToDevice,
                                st));
         launch_apply_ordered(h, du.get(), di.get(), dj.get(), n, scalars_of(h), st);
+        MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+extern "C" mml_status mml_bpr_apply_triples_flags(mml_bpr* h, const int32_t* users,
+                                                   const int32_t* items,
+                                                   const int32_t* other_items,
+                                                   const uint8_t* flags, int64_t n) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        bpr_single_device_only(h);
+        MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(n >= 0 && (n == 0 || (users && items && other_items && flags)),
+                    "bad arguments");
+        for (int64_t x = 0; x < n; ++x)
+            MML_REQUIRE(users[x] >= 0 && users[x] < h->n_users && items[x] >= 0 &&
+                            items[x] < h->n_items && other_items[x] >= 0 &&
+                            other_items[x] < h->n_items && flags[x] < 8,
+                        "triple id or flag out of range");
+        if (n == 0) return;
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        mml::DeviceArray<int32_t> du, di, dj;
+        mml::DeviceArray<uint8_t> df;
+        du.alloc(n);
+        di.alloc(n);
+        dj.alloc(n);
+        df.alloc(n);
+        MML_HIP(hipMemcpyAsync(du.get(), users, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(di.get(), items, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+        MML_HIP(hipMemcpyAsync(dj.get(), other_items, sizeof(int32_t) * n, hipMemcpyHostToDevice,
+                               st));
+        MML_HIP(hipMemcpyAsync(df.get(), flags, n, hipMemcpyHostToDevice, st));
+        launch_apply_ordered(h, du.get(), di.get(), dj.get(), n, scalars_of(h), st, 1, 0,
+                             df.get());
+        MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+extern "C" mml_status mml_bpr_set_rows(mml_bpr* h, int32_t side, int32_t n_rows,
+                                       const int32_t* rows, const float* values) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        bpr_single_device_only(h);
+        MML_REQUIRE(h->has_model, "no model");
+        MML_REQUIRE(side == 0 || side == 1, "side: 0 (users) or 1 (items)");
+        MML_REQUIRE(n_rows >= 0 && (n_rows == 0 || (rows && values)), "bad arguments");
+        const int32_t n_own = side == 0 ? h->n_users : h->n_items;
+        for (int32_t x = 0; x < n_rows; ++x)
+            MML_REQUIRE(rows[x] >= 0 && rows[x] < n_own, "row id beyond the model");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        float* M = side == 0 ? h->U.get() : h->V.get();
+        for (int32_t x = 0; x < n_rows; ++x)  // in list order: a row listed twice takes the last
+            MML_HIP(hipMemcpyAsync(M + (int64_t)rows[x] * h->ld, values + (int64_t)x * h->k,
+                                   sizeof(float) * h->k, hipMemcpyHostToDevice, st));
         MML_HIP(hipStreamSynchronize(st));
     });
 }

@@ -1695,16 +1695,25 @@ __device__ __forceinline__ float2 block_sum2(float x, float y, float* sdot) {
 // NJ = 32 / 64: 4 waves, thread f holds q[0 .. NJ) of feature f.  NJ = 128: 8 waves, the items
 // split in two halves of 64 (waves 0-3 / 4-7), so a thread holds 64 values (128 would spill);
 // bounds of 4 waves per SIMD keep two such workgroups per CU (128 VGPRs), since the solve is
-// barrier-latency bound.  The CG is Chronopoulos-Gear's single-reduction form: one mat-vec
+// barrier-latency bound.  NJ = 96 (rows of 65 .. 96 items): 12 waves, three parts of 32 items
+// (32 values per thread, six waves per SIMD keep two workgroups per CU), instead of 128 slots
+// of which up to half sit idle.  The CG is Chronopoulos-Gear's single-reduction form: one mat-vec
 // w = C r and one fused reduction of (r.r, w.r) per step.
+// (PARTS = 4 at NJ = 128: 16 waves of 32 items each, the experiments build's A/B)
 template <int NJ>
-__global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_wood_cg_kernel(
+constexpr int wood_parts() {
+    return NJ == 96 ? 3 : NJ > 64 ? 2 : 1;
+}
+template <int NJ, int PARTS = wood_parts<NJ>()>
+__global__ __launch_bounds__(256 * PARTS, PARTS == 3 ? 6 : PARTS >= 2 ? 4 : 2) void
+wrmf_wood_cg_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, const int64_t* __restrict__ off,
     const int32_t* __restrict__ cols, const float* __restrict__ Q, int32_t k, float alpha,
     const float* __restrict__ S, float* __restrict__ Tout, int32_t max_it, float tol2,
     float skip2, float abs2, int32_t cheb_m, float cheb_theta, float cheb_delta) {
-    static_assert(NJ == 32 || NJ == 64 || NJ == 128, "NJ: 32, 64 or 128");
-    constexpr int HALVES = NJ > 64 ? 2 : 1;
+    static_assert(NJ == 32 || NJ == 64 || NJ == 96 || NJ == 128, "NJ: 32, 64, 96 or 128");
+    static_assert(NJ % PARTS == 0 && NJ / PARTS <= 64, "parts of <= 64 items");
+    constexpr int HALVES = PARTS;
     constexpr int WAVES = 4 * HALVES;
     constexpr int NL = NJ / HALVES;             // items per thread (<= 64)
     constexpr int E = NL / 8;                   // partial sums after the fused first stages
@@ -1795,7 +1804,10 @@ __global__ __launch_bounds__(NJ > 64 ? 512 : 256, NJ > 64 ? 4 : 2) void wrmf_woo
             if constexpr (HALVES == 1) return u;
             su[half][f] = u;
             __syncthreads();
-            return su[0][f] + su[1][f];
+            float sum = su[0][f];
+#pragma unroll
+            for (int x = 1; x < HALVES; ++x) sum += su[x][f];
+            return sum;
         };
         float y;
         if (S) {
@@ -1869,6 +1881,22 @@ bool wood_cg() {
 constexpr double kWoodAbs = 5e-8;
 
 int debug_mask();
+// rows of 65 .. 96 items on the 96-slot kernel (MML_WRMF_WOOD96=0 in experiments builds: 128)
+bool wood96() {
+    static const bool v = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOOD96");
+        return !(e && std::string(e) == "0");
+    }();
+    return v;
+}
+// MML_WRMF_WOOD128=4 (experiments builds): rows of 65 .. 128 items on 4 parts of 32 (16 waves)
+int wood128_parts() {
+    static const int v = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOOD128");
+        return e ? std::atoi(e) : 2;
+    }();
+    return v;
+}
 // lnorm: |L^{-1}|_2 (refinement only)
 void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const int64_t* off,
                     const int32_t* cols, const float* Q, int32_t k, float alpha, float* Tout,
@@ -1914,6 +1942,14 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
                                                       (float)theta, (float)delta);
     else if (g == 1)
         wrmf_wood_cg_kernel<64><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
+                                                      max_it, tol2, skip2, abs2, cheb_m,
+                                                      (float)theta, (float)delta);
+    else if (wood128_parts() == 4)
+        wrmf_wood_cg_kernel<128, 4><<<grid, 1024, 0, st>>>(
+            rows, n, off, cols, Q, k, alpha, S, Tout, max_it, tol2, skip2, abs2, cheb_m,
+            (float)theta, (float)delta);
+    else if (g == 2 && wood96())
+        wrmf_wood_cg_kernel<96><<<grid, 768, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
                                                       max_it, tol2, skip2, abs2, cheb_m,
                                                       (float)theta, (float)delta);
     else

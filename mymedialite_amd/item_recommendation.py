@@ -222,6 +222,168 @@ class BPRMF(_MFBase):
                                               N.ptr(j, N._i32p), len(u)))
         self._host = None
 
+    # ------------------------------------------------------------------ incremental updates
+    UpdateUsers = True  # IncrementalItemRecommender.UpdateUsers / UpdateItems
+    UpdateItems = True
+
+    def _apply_flagged(self, tri, flags):
+        if not flags:
+            return
+        u, i, j = (N.i32([t[c] for t in tri]) for c in range(3))
+        fl = np.ascontiguousarray(flags, np.uint8)
+        N.check(N.lib().mml_bpr_apply_triples_flags(
+            self._h, N.ptr(u, N._i32p), N.ptr(i, N._i32p), N.ptr(j, N._i32p),
+            fl.ctypes.data_as(ctypes.c_void_p), len(fl)))
+
+    def _set_rows(self, side, rows, values):
+        r = N.i32(rows)
+        v = N.f32(np.asarray(values, np.float32).reshape(len(rows), -1))
+        N.check(N.lib().mml_bpr_set_rows(self._h, side, len(r), N.ptr(r, N._i32p),
+                                         N.ptr(v, N._f32p)))
+
+    def retrain_users(self, user_ids):
+        """RetrainUser (BPRMF.cs:391-402) for each id in order: RowInitNormal, then |S_u| x
+        SampleItemPair (:290-296) + UpdateFactors(u, i, j, true, false, false).  The draws do not
+        depend on the factors, so the host draws them in the reference's order; only U_u changes
+        and V is fixed, so every user's triples go to the device in one in-order call (a user
+        listed twice keeps its last retraining, which re-initialises the row)."""
+        if self._h is None:
+            raise RuntimeError("Train() or load_model() first")
+        rng = Random.get_instance()
+        k, n_items = int(self.NumFactors), self.MaxItemID + 1
+        off, cols = self._feedback.user_matrix
+        last = {}
+        for u in (int(x) for x in user_ids):
+            init = rng.fill_normal(k, self.InitMean, self.InitStdDev)
+            row = cols[off[u]:off[u + 1]] if u + 1 < len(off) else np.zeros(0, np.int32)
+            items = row.tolist()
+            members = set(items)
+            tri = []
+            for _ in range(len(items)):
+                i = items[rng.next(len(items))]
+                j = rng.next(n_items)
+                while j in members:
+                    j = rng.next(n_items)
+                tri.append((u, i, j))
+            last[u] = (init, tri)
+        if not last:
+            return
+        rows = list(last)
+        self._set_rows(0, rows, np.concatenate([last[u][0] for u in rows]))
+        tri = [t for u in rows for t in last[u][1]]
+        self._apply_flagged(tri, [1] * len(tri))
+        self._host = None
+
+    def retrain_items(self, item_ids):
+        """RetrainItem (BPRMF.cs:405-422) for each id in order: RowInitNormal, then
+        NumberOfEntries / (MaxItemID + 1) x (SampleUser :300-310, SampleOtherItem :275-284) with
+        UpdateFactors updating only the retrained item (as i when it is the user's positive, else
+        as j).  Another retrained item can be a later triple's other item, so the items run one
+        after another, each its row reset and its triples applied in order."""
+        if self._h is None:
+            raise RuntimeError("Train() or load_model() first")
+        rng = Random.get_instance()
+        k, n_users, n_items = int(self.NumFactors), self.MaxUserID + 1, self.MaxItemID + 1
+        off, cols = self._feedback.user_matrix
+        sets = {}
+
+        def s_u(u):
+            if u not in sets:
+                sets[u] = set(cols[off[u]:off[u + 1]].tolist()) if u + 1 < len(off) else set()
+            return sets[u]
+
+        n_iter = int(off[-1]) // n_items  # Feedback.UserMatrix.NumberOfEntries / (MaxItemID + 1)
+        for item in (int(x) for x in item_ids):
+            init = rng.fill_normal(k, self.InitMean, self.InitStdDev)
+            tri, flags = [], []
+            for _ in range(n_iter):
+                while True:
+                    u = rng.next(n_users)
+                    if 0 < len(s_u(u)) < n_items:
+                        break
+                positive = item in s_u(u)
+                j = rng.next(n_items)
+                while (j in s_u(u)) == positive:
+                    j = rng.next(n_items)
+                if positive:
+                    tri.append((u, item, j))
+                    flags.append(2)
+                else:
+                    tri.append((u, j, item))
+                    flags.append(4)
+            self._set_rows(1, [item], init)
+            self._apply_flagged(tri, flags)
+        self._host = None
+
+    def add_feedback(self, users, items):
+        """MF.AddFeedback (ItemRecommendation/MF.cs:73-91): new ids grow the model (AddUser /
+        AddItem: AddRows + RowInitNormal; BPRMF.AddItem also grows item_bias with 0), the pairs
+        join Feedback, then RetrainUser / RetrainItem over the batch's users and items (HashSet
+        insertion order)."""
+        users = [int(x) for x in np.atleast_1d(users)]
+        items = [int(x) for x in np.atleast_1d(items)]
+        m = self.get_model()
+        U, V, b = m["U"], m["V"], m["bias"]
+        k = int(self.NumFactors)
+        rng = Random.get_instance()
+        for u, i in zip(users, items):
+            if u > self.MaxUserID:
+                U = np.concatenate([U, np.zeros((u + 1 - U.shape[0], k), np.float32)])
+                U[u] = rng.fill_normal(k, self.InitMean, self.InitStdDev)
+                self.MaxUserID = u
+            if i > self.MaxItemID:
+                V = np.concatenate([V, np.zeros((i + 1 - V.shape[0], k), np.float32)])
+                b = np.concatenate([b, np.zeros(i + 1 - b.shape[0], np.float32)])
+                V[i] = rng.fill_normal(k, self.InitMean, self.InitStdDev)
+                self.MaxItemID = i
+        self._feedback.add(users, items)
+        self._reload(U, V, b)
+        if self.UpdateUsers:
+            self.retrain_users(list(dict.fromkeys(users)))
+        if self.UpdateItems:
+            self.retrain_items(list(dict.fromkeys(items)))
+
+    def remove_feedback(self, users, items):
+        """MF.RemoveFeedback (MF.cs:93-99): the pairs leave Feedback, then the retraining."""
+        users = [int(x) for x in np.atleast_1d(users)]
+        items = [int(x) for x in np.atleast_1d(items)]
+        for u, i in zip(users, items):
+            if u > self.MaxUserID:
+                raise ValueError(f"Unknown user {u}")
+            if i > self.MaxItemID:
+                raise ValueError(f"Unknown item {i}")
+        m = self.get_model()
+        self._feedback.remove(users, items)
+        self._reload(m["U"], m["V"], m["bias"])
+        if self.UpdateUsers:
+            self.retrain_users(list(dict.fromkeys(users)))
+        if self.UpdateItems:
+            self.retrain_items(list(dict.fromkeys(items)))
+
+    def _reload(self, U, V, bias):
+        """The handle at the (grown) sizes, with the edited feedback and the current model.  The
+        pair sampler's visit order (Feedback.RandomIndex) is redrawn by the reference at its next
+        Iterate(), between this edit's draws and the epoch's: not restated, so the edits take the
+        default (uniform user) sampler."""
+        if self._sampler() == N.BPR_SAMPLER_UNIFORM_PAIR:
+            raise NotImplementedError("AddFeedback / RemoveFeedback with UniformUserSampling = "
+                                      "false: the RandomIndex redraw is not restated")
+        U, V = np.ascontiguousarray(U, np.float32), np.ascontiguousarray(V, np.float32)
+        bias = np.ascontiguousarray(bias, np.float32)
+        self._release()
+        self._ctx = N.Context(N.device_arg(self))
+        p = self._params()
+        h = N._vp()
+        N.check(N.lib().mml_bpr_create(self._ctx.handle, ctypes.byref(p), U.shape[0], V.shape[0],
+                                       ctypes.byref(h)))
+        self._h = h
+        fb = self._feedback
+        N.check(N.lib().mml_bpr_set_data(h, N.ptr(fb.users, N._i32p), N.ptr(fb.items, N._i32p),
+                                         fb.count, None))
+        N.check(N.lib().mml_bpr_set_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
+                                          N.ptr(bias, N._f32p)))
+        self._host = None
+
     def _sampler(self) -> int:
         """Iterate()'s dispatch (BPRMF.cs:160-178) on UniformUserSampling x WithReplacement."""
         if self.UniformUserSampling:
