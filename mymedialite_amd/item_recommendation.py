@@ -320,6 +320,7 @@ class BPRMF(_MFBase):
         AddItem: AddRows + RowInitNormal; BPRMF.AddItem also grows item_bias with 0), the pairs
         join Feedback, then RetrainUser / RetrainItem over the batch's users and items (HashSet
         insertion order)."""
+        self._check_editable()
         users = [int(x) for x in np.atleast_1d(users)]
         items = [int(x) for x in np.atleast_1d(items)]
         m = self.get_model()
@@ -345,6 +346,7 @@ class BPRMF(_MFBase):
 
     def remove_feedback(self, users, items):
         """MF.RemoveFeedback (MF.cs:93-99): the pairs leave Feedback, then the retraining."""
+        self._check_editable()
         users = [int(x) for x in np.atleast_1d(users)]
         items = [int(x) for x in np.atleast_1d(items)]
         for u, i in zip(users, items):
@@ -360,14 +362,18 @@ class BPRMF(_MFBase):
         if self.UpdateItems:
             self.retrain_items(list(dict.fromkeys(items)))
 
-    def _reload(self, U, V, bias):
-        """The handle at the (grown) sizes, with the edited feedback and the current model.  The
-        pair sampler's visit order (Feedback.RandomIndex) is redrawn by the reference at its next
-        Iterate(), between this edit's draws and the epoch's: not restated, so the edits take the
-        default (uniform user) sampler."""
+    def _check_editable(self):
+        """The pair sampler's visit order (Feedback.RandomIndex) is redrawn by the reference at
+        its next Iterate(), between an edit's draws and the epoch's: not restated, so the edits
+        take the default (uniform user) samplers; checked before anything changes."""
+        if self._h is None:
+            raise RuntimeError("Train() or load_model() first")
         if self._sampler() == N.BPR_SAMPLER_UNIFORM_PAIR:
             raise NotImplementedError("AddFeedback / RemoveFeedback with UniformUserSampling = "
                                       "false: the RandomIndex redraw is not restated")
+
+    def _reload(self, U, V, bias):
+        """The handle at the (grown) sizes, with the edited feedback and the current model."""
         U, V = np.ascontiguousarray(U, np.float32), np.ascontiguousarray(V, np.float32)
         bias = np.ascontiguousarray(bias, np.float32)
         self._release()
