@@ -2610,28 +2610,48 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
 }
 
 // L^{-1} (lower) of B = HH + reg I by Cholesky in fp64 on the host (k <= 256: ~10 M flops)
+// a . b over n doubles with four independent partial sums (the host step sits between two
+// half-step kernels with the GPU idle: the serial-add chain was most of its ~4 ms at k = 256)
+static inline double dot4(const double* a, const double* b, int n) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int m = 0;
+    for (; m + 4 <= n; m += 4) {
+        s0 += a[m] * b[m];
+        s1 += a[m + 1] * b[m + 1];
+        s2 += a[m + 2] * b[m + 2];
+        s3 += a[m + 3] * b[m + 3];
+    }
+    for (; m < n; ++m) s0 += a[m] * b[m];
+    return (s0 + s1) + (s2 + s3);
+}
+
 static void chol_inverse(const std::vector<double>& HH, int k, double reg, std::vector<double>& Li) {
     std::vector<double> L(HH);
     for (int i = 0; i < k; ++i) L[(size_t)i * k + i] += reg;
     for (int j = 0; j < k; ++j) {
-        double d = L[(size_t)j * k + j];
-        for (int m = 0; m < j; ++m) d -= L[(size_t)j * k + m] * L[(size_t)j * k + m];
+        const double* Lj = &L[(size_t)j * k];
+        double d = L[(size_t)j * k + j] - dot4(Lj, Lj, j);
         MML_REQUIRE(d > 0.0, "HH + reg I is not positive definite");
         d = std::sqrt(d);
         L[(size_t)j * k + j] = d;
         for (int i = j + 1; i < k; ++i) {
-            double v = L[(size_t)i * k + j];
-            for (int m = 0; m < j; ++m) v -= L[(size_t)i * k + m] * L[(size_t)j * k + m];
-            L[(size_t)i * k + j] = v / d;
+            const double* Lr = &L[(size_t)i * k];
+            L[(size_t)i * k + j] = (L[(size_t)i * k + j] - dot4(Lr, Lj, j)) / d;
         }
     }
+    // L^{-1} row by row: row i = (e_i - sum_{m < i} L[i][m] row m) / L[i][i], contiguous axpys
     Li.assign((size_t)k * k, 0.0);
-    for (int c = 0; c < k; ++c)  // column c of L^{-1}: forward substitution on e_c
-        for (int i = c; i < k; ++i) {
-            double v = (i == c) ? 1.0 : 0.0;
-            for (int m = c; m < i; ++m) v -= L[(size_t)i * k + m] * Li[(size_t)m * k + c];
-            Li[(size_t)i * k + c] = v / L[(size_t)i * k + i];
+    for (int i = 0; i < k; ++i) {
+        double* ri = &Li[(size_t)i * k];
+        ri[i] = 1.0;
+        for (int m = 0; m < i; ++m) {
+            const double c = L[(size_t)i * k + m];
+            const double* rm = &Li[(size_t)m * k];
+            for (int x = 0; x <= m; ++x) ri[x] -= c * rm[x];
         }
+        const double inv = 1.0 / L[(size_t)i * k + i];
+        for (int x = 0; x <= i; ++x) ri[x] *= inv;
+    }
 }
 
 // |Li|_2 of a lower-triangular k x k matrix: sqrt of the largest eigenvalue of Li^T Li by power
@@ -2646,11 +2666,7 @@ static double spectral_norm_lower(const std::vector<double>& Li, int k) {
         for (double x : v) nv += x * x;
         nv = std::sqrt(nv);
         for (double& x : v) x /= nv;
-        for (int i = 0; i < k; ++i) {  // u = Li v
-            double a = 0.0;
-            for (int j = 0; j <= i; ++j) a += Li[(size_t)i * k + j] * v[j];
-            u[i] = a;
-        }
+        for (int i = 0; i < k; ++i) u[i] = dot4(&Li[(size_t)i * k], v.data(), i + 1);  // u = Li v
         double uu = 0.0;
         for (double x : u) uu += x * x;
         lam = uu;  // v^T Li^T Li v, |v| = 1
