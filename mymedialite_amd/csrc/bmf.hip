@@ -276,6 +276,8 @@ constexpr int kAccUserThru = 4;  // user rows / biases loaded sc1 and stored sc1
                                  // reads the row from memory instead of a stale L2 copy
 constexpr int kAccFlush = 8;     // one wave per XCD writes its L2's dirty lines back after every
                                  // 64 ratings it applies (agent release fence = buffer_wbl2)
+constexpr int kAccUBiasPlain = 16;  // (experiments) with kAccUserThru: the user bias loaded and
+                                    // stored plain, only the user rows written through
 
 // The stream is split into ng group spans goff[g] .. goff[g + 1] (mml_device.h group_wave): ng = 8
 // for XCD-owned item groups (block b serves group b % 8, one XCD per group), ng = 1 for one span.
@@ -290,6 +292,7 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
     constexpr int RPW = 64 / LPR;  // ratings per wave step
     constexpr bool COH = AM == kAccCoherent;
     constexpr bool IL2 = (AM & kAccItemL2) != 0, UTH = (AM & kAccUserThru) != 0;
+    constexpr bool BTH = UTH && (AM & kAccUBiasPlain) == 0;  // user bias written through
     const int lane = threadIdx.x & 63;
     // wave-uniform (SGPR) bounds: the loops' branches stay scalar
     const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -325,7 +328,7 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
         bu_u = 0.0f;
         bi_i = 0.0f;
         if constexpr (biased) {
-            if constexpr (UTH) bu_u = mml::load1_l2(burs, (uint32_t)u * 4u);
+            if constexpr (BTH) bu_u = mml::load1_l2(burs, (uint32_t)u * 4u);
             else bu_u = load1<COH>(bu + u);
             if constexpr (IL2) bi_i = mml::load1_l2(brs, (uint32_t)i * 4u);
             else bi_i = load1<COH>(bi + i);
@@ -346,7 +349,7 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
         part = group_sum<LPR>(part);
         const RatingStep<LOSS> st(s, part, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
         if (biased && q == 0) {
-            if constexpr (UTH)
+            if constexpr (BTH)
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, st.new_bu), burs,
                                                       (uint32_t)u * 4u, 0, 16);
             else
@@ -1697,6 +1700,12 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
             case 4: am = u_fits ? kAccItemL2 | kAccUserThru | kAccFlush : kAccItemL2 | kAccFlush;
                 break;
             case 5: am = kAccItemL2 | kAccFlush; break;
+#ifdef MML_EXPERIMENTS
+            case 6:  // 4 with the user bias plain (A/B of its write-through cost)
+                am = u_fits ? kAccItemL2 | kAccUserThru | kAccFlush | kAccUBiasPlain
+                            : kAccItemL2 | kAccFlush;
+                break;
+#endif
             default: am = kAccItemL2; break;
         }
     }
@@ -1713,6 +1722,14 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     bmf_sgd_hogwild_kernel<LOSS, LPR, VPL, AM><<<(int)blocks, 256, 0, st>>>(                  \
         su, si, sr, goff, ng, wpg, h->U.get(), h->V.get(), h->bu.get(), h->bi.get(), ld4, vb, bb, \
         ub, bub, mml::flushers_per_xcd(1), s, cu, ci)
+#ifdef MML_EXPERIMENTS
+#define MML_HOG_EXP(LPR, VPL)                                                      \
+    case kAccItemL2 | kAccUserThru | kAccFlush | kAccUBiasPlain:                   \
+        MML_HOG1(LPR, VPL, kAccItemL2 | kAccUserThru | kAccFlush | kAccUBiasPlain); \
+        break;
+#else
+#define MML_HOG_EXP(LPR, VPL)
+#endif
 #define MML_HOGV(LPR, VPL)                                                       \
     switch (am) {                                                                \
         case kAccCoherent: MML_HOG1(LPR, VPL, kAccCoherent); break;              \
@@ -1722,6 +1739,7 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
         case kAccItemL2 | kAccUserThru | kAccFlush:                              \
             MML_HOG1(LPR, VPL, kAccItemL2 | kAccUserThru | kAccFlush); break;    \
         case kAccItemL2 | kAccFlush: MML_HOG1(LPR, VPL, kAccItemL2 | kAccFlush); break; \
+        MML_HOG_EXP(LPR, VPL)                                                    \
         default: MML_HOG1(LPR, VPL, kAccPlain); break;                           \
     }
     // one float4 of U_u and of V_i per lane (VPL 2 measured equal, VPL 4 10 % slower on C2)
@@ -1735,6 +1753,7 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
         default: MML_HOGV(64, 1); break;
     }
 #undef MML_HOGV
+#undef MML_HOG_EXP
 #undef MML_HOG1
     MML_HIP(hipGetLastError());
 }
