@@ -4,7 +4,7 @@
 # (variants/rec) against the separate off[] + Bloom arrays (variants/exp); then the C3 replica AUC
 # tests for each candidate.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-ab}

@@ -3,7 +3,7 @@
 # (release: user rows and biases written through) vs 6 (user bias plain), C2 bench and the C2-shape
 # statistical parity test for each.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp MML_LIB_PATH=$PWD/variants/exp/libmml_hip.so
 TAG=${1:-bias}

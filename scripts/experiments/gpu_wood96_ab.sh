@@ -3,7 +3,7 @@
 # parts of 64, 1 = rows of 65 .. 96 items on three parts of 32 (the release default), 4 = rows of
 # 65 .. 128 items on four parts of 32; then the WRMF tests on the release library.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-w96}
