@@ -7,17 +7,16 @@ One step = one epoch (BiasedMatrixFactorization.Iterate, src/MyMediaLite/RatingP
 BiasedMatrixFactorization.cs:264-310) over every rank's ratings, plus -- for N > 1 -- the per-epoch
 RCCL all-reduce of item factors and item biases (model averaging).
 
-Workloads (BASELINE.json configs, synthetic data generated in HBM, inputs resident before timing):
-  N = 1 : C2 -- 1M users x 100k items, 100M ratings, k = 64 fp32 (the headline `value`), then the
-          other configurations as extra keys of the same line, each timed on HIP events with its
-          own roofline and CPU baseline: "c4_n1" (C4's 1B ratings, the data set of the N > 1 runs,
-          3 epochs), "c3" (BPRMF k=128, 2 epochs), "c5" (WRMF k=256 fp64 mode, 2 iterations);
-          --no-extras skips them.
-  N > 1 : C4 strong scaling -- 1B ratings, 10M users x 100k items, user shards of equal rating
-          count (the same data set at every N, so N / 1 compares with the line's c4_n1 at N = 1;
-          --workload c4 runs the N = 1 point alone).
+The headline `value` is C4 at every N (BASELINE.json "BiasedMF k=64 at 1/2/4/8 MI355X"): 1B
+ratings, 10M users x 100k items, user shards of equal rating count -- the same data set at every N,
+so the driver's N-GPU / 1-GPU ratio divides like by like (strong scaling).  At N = 1 the other
+configurations follow as extra keys of the same line, each timed on HIP events with its own
+roofline and CPU baseline: "c2" (1M users x 100k items, 100M ratings, 10 epochs), "c3" (BPRMF
+k=128, 2 epochs, held-out AUC on 100k test users), "c5" (WRMF k=256 fp64 mode, 2 iterations, a row
+check against the oracle's fp64 solve); --no-extras skips them.  Synthetic data is generated in HBM
+and resident before the timed region.
 The line carries the roofline of the SGD kernel (algorithmic bytes 16k+28 per update)
-and the CPU oracle's Iterate() and MaxThreads = T DSGD, one full epoch each (rank 0, N = 1 only).
+and the CPU oracle's MaxThreads = T DSGD on a 100M-rating slice (rank 0, N = 1 only).
 """
 from __future__ import annotations
 
@@ -47,7 +46,7 @@ import torch  # noqa: E402
 from mymedialite_amd.distributed import (env_rank, init_host_group, max_over_ranks,  # noqa: E402
                                          share_unique_id)
 from mymedialite_amd.random import SystemRandom  # noqa: E402
-from mymedialite_amd.synthetic import planted_ratings_torch  # noqa: E402
+from mymedialite_amd.synthetic import c3_chunks, c3_holdout, planted_ratings_torch  # noqa: E402,E501
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -84,23 +83,23 @@ def main():
                              "pair_replacement"],
                     help="C3 only: BPRMF's Iterate() variant (BPRMF.cs:160-268)")
     ap.add_argument("--workload", default=None, choices=["c2", "c3", "c4", "c5", "svdpp"],
-                    help="default: c2 at N = 1 (+ the c4_n1 / c3 / c5 keys), c4 at N > 1 "
-                         "(BiasedMF k=64); c3: BPRMF k=128 (N > 1: user shards); c4: BiasedMF 1B "
-                         "ratings, strong scaling; c5: WRMF k=256")
+                    help="default: c4 at every N (BiasedMF k=64, 1B ratings, strong scaling; at "
+                         "N = 1 + the c2 / c3 / c5 keys); c2: 1M x 100k, 100M ratings, one GPU; "
+                         "c3: BPRMF k=128 (N > 1: user shards); c5: WRMF k=256")
     ap.add_argument("--no-extras", action="store_true",
-                    help="N = 1 default run: the C2 line only (no c4_n1 / c3 / c5 keys)")
+                    help="N = 1 default run: the C4 line only (no c2 / c3 / c5 keys)")
     args = ap.parse_args()
     world = env_rank()[0]
-    workload = args.workload or ("c2" if world == 1 else "c4")
+    workload = args.workload or "c4"
     fn = {"c2": bench_c2, "c3": bench_bpr, "c4": bench_c4, "c5": bench_wrmf,
           "svdpp": bench_svdpp}[workload]
     if workload == "c2" and world > 1:
         raise SystemExit("C2 is the single-GPU configuration; N > 1 runs C4 (--workload c4)")
     line = fn(args)
-    if workload == "c2" and args.workload is None and not args.no_extras:
+    if world == 1 and args.workload is None and not args.no_extras:
         # the other configurations on the same GPU, as keys of the one line (BASELINE.json
-        # configs 3-5; C4's N = 1 point is the denominator of the N > 1 strong-scaling runs)
-        for key, f, steps, warmup in (("c4_n1", bench_c4, 3, 1), ("c3", bench_bpr, 2, 1),
+        # configs 2, 3 and 5)
+        for key, f, steps, warmup in (("c2", bench_c2, 10, 2), ("c3", bench_bpr, 2, 1),
                                       ("c5", bench_wrmf, 2, 1)):
             sub = argparse.Namespace(**vars(args))
             sub.steps, sub.warmup = steps, warmup
@@ -523,35 +522,6 @@ def bench_c4(args):
     return line
 
 
-def c3_shard(rank, world, n_total, n_users, n_items, device, chunks=64):
-    """C3's events as 64 user-range chunks (chunk c: users [c U/64, (c+1) U/64) uniform, items
-    Zipf(0.8) over one shared permutation, n_total/64 events, seed 2000 + c); rank r of N holds
-    chunks [r 64/N, (r+1) 64/N), so the data set is the same at every N."""
-    from mymedialite_amd.synthetic import zipf_cdf
-    assert chunks % world == 0, "world size must divide 64"
-    per = n_total // chunks
-    mine = range(rank * chunks // world, (rank + 1) * chunks // world)
-    gp = torch.Generator(device=device)
-    gp.manual_seed(2)
-    perm = torch.randperm(n_items, generator=gp, device=device)
-    cdf = torch.from_numpy(zipf_cdf(n_items, 0.8)).to(device)
-    users = torch.empty(per * len(mine), dtype=torch.int32, device=device)
-    items = torch.empty(per * len(mine), dtype=torch.int32, device=device)
-    for x, c in enumerate(mine):
-        g = torch.Generator(device=device)
-        g.manual_seed(2000 + c)
-        lo, hi = c * n_users // chunks, (c + 1) * n_users // chunks
-        for s0 in range(0, per, 1 << 26):
-            e = min(per, s0 + (1 << 26))
-            o = x * per
-            users[o + s0:o + e] = torch.randint(lo, hi, (e - s0,), generator=g, device=device,
-                                                dtype=torch.int32)
-            r = torch.rand(e - s0, generator=g, device=device, dtype=torch.float64)
-            items[o + s0:o + e] = perm[torch.searchsorted(cdf, r).clamp_(max=n_items - 1)].to(
-                torch.int32)
-    return users, items
-
-
 def bench_bpr(args):
     """C3: BPRMF, 10M users x 1M items, 500M positive events, k = 128.  One step = one
     BPRMF.Iterate() = Feedback.Count sampled triples (BPRMF.cs:160-226).  N > 1: user shards of
@@ -568,8 +538,16 @@ def bench_bpr(args):
         ctx.comm_init(share_unique_id(rank, N.Context.unique_id), world, rank)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
-    users, items = c3_shard(rank, world, n_total, n_users, n_items, dev)
+    users, items, urange = c3_chunks(rank, world, n_total, n_users, n_items, dev)
+    # SURVEY 8(d)'s evaluation split: one held-out positive for each of 100k sampled test users
+    # (seed 2); this rank keeps the test users of its user range
+    users, items, te_u, te_i = c3_holdout(users, items, n_users, urange)
     n = len(users)
+    n_events = n
+    if world > 1:
+        t = torch.tensor([float(n)], dtype=torch.float64)
+        torch.distributed.all_reduce(t)
+        n_events = int(t.item())
     torch.cuda.synchronize()
     sampler = {"uniform_user": N.BPR_SAMPLER_UNIFORM_USER,
                "uniform_pair": N.BPR_SAMPLER_UNIFORM_PAIR,
@@ -608,9 +586,21 @@ def bench_bpr(args):
     if world > 1:
         torch.distributed.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
-    # the dominant kernel is bpr_update_kernel: U_u, V_i, V_j read + write (24k), b_i, b_j read +
-    # write (16), the triple (12); the sampler kernel (the rest of the epoch) is reported beside it
-    bpu = 24 * k + 28
+    # held-out AUC after the timed epochs (Eval.Items.Evaluate's AUC, Items.cs:126-209 /
+    # AUC.cs:42-68, on the device): all 1M items as candidates in a seeded shuffled order
+    t1 = time.perf_counter()
+    cand = torch.randperm(n_items, generator=torch.Generator().manual_seed(3)).numpy()
+    _, n_eval, per_user = N.auc_held_out("mml_bpr_auc", h, cand, te_u, te_i)
+    ok = per_user[~np.isnan(per_user)]
+    acc = torch.tensor([float(ok.sum()), float(len(ok))], dtype=torch.float64)
+    if world > 1:
+        torch.distributed.all_reduce(acc)
+    auc = float(acc[0].item() / max(1.0, acc[1].item()))
+    auc_s = time.perf_counter() - t1
+    # SURVEY 8(d)'s bytes per update, 24k + 32: U_u, V_i, V_j read + write (24k), b_i, b_j read +
+    # write (16), the sampler's CSR offsets, positive id and membership probe (16).  The dominant
+    # kernel is bpr_update_kernel; the sampler (the rest of the epoch) is reported beside it
+    bpu = 24 * k + 32
     avg_ms = float(np.mean(ms))
     upd_ms = float(np.mean(ums))
     achieved = n * bpu / (upd_ms * 1e-3) / 1e9
@@ -620,14 +610,15 @@ def bench_bpr(args):
         traffic, traffic_note = pmc_traffic("r2_c3_traffic.json", upd_ms)
     line = {
         "metric": "BPR triple-updates/sec, BPRMF k=128 (C3)",
-        "value": n_total * args.steps / elapsed,
+        "value": n_events * args.steps / elapsed,
         "unit": "triple-updates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "strong" if world > 1 else "none",
         "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (users uniform, items Zipf(0.8), generated in HBM)",
         "config": {"workload": "C3: BPRMF 10M users x 1M items, 500M positives, k=128",
-                   "num_factors": k, "events": n_total, "events_per_gpu": n,
+                   "num_factors": k, "events": n_events, "events_generated": n_total,
+                   "events_per_gpu": n,
                    "users": n_users, "items": n_items,
                    "sampler": args.sampler + (" (BPRMF default)" if args.sampler ==
                                               "uniform_user" else ""),
@@ -645,6 +636,13 @@ def bench_bpr(args):
                      "frac_note": "frac = the update kernel alone; frac_epoch = the same bytes "
                                   "over the whole device epoch (sampler + XCD partition + "
                                   "update)"},
+        "auc": auc,
+        "auc_users": int(acc[1].item()),
+        "auc_note": (f"held-out AUC after {args.warmup + args.steps} epochs: 100k test users "
+                     f"sampled with seed 2, each with the item of its first event held out (every "
+                     f"event of that pair removed from training), all {n_items} items as "
+                     f"candidates (training items ignored per user), mml_bpr_auc on the device "
+                     f"({auc_s:.1f} s)"),
         "cpu_baseline": cpu,
     }
     N.lib().mml_bpr_destroy(h)
@@ -664,28 +662,21 @@ def bench_wrmf(args):
     k = 256 if args.k == 64 else args.k
     n_users, n_items = args.users or 5_000_000, 500_000
     per_user = 100
-    n = n_users * per_user if not args.ratings else args.ratings
     ctx = N.Context(local)
     if world > 1:  # row shards per rank, all-gathered after each half-step
         ctx.comm_init(share_unique_id(rank, N.Context.unique_id), world, rank)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
-    g = torch.Generator(device=dev)
-    g.manual_seed(5)  # every rank generates the same full data set
-    from mymedialite_amd.synthetic import zipf_cdf
-    cdf = torch.from_numpy(zipf_cdf(n_items, 0.8)).to(dev)
-    perm = torch.randperm(n_items, generator=g, device=dev)
-    users = (torch.arange(n, device=dev, dtype=torch.int64) // per_user).to(torch.int32)
-    items = torch.empty(n, dtype=torch.int32, device=dev)
-    for s0 in range(0, n, 1 << 26):
-        e = min(n, s0 + (1 << 26))
-        x = torch.rand(e - s0, generator=g, device=dev, dtype=torch.float64)
-        items[s0:e] = perm[torch.searchsorted(cdf, x).clamp_(max=n_items - 1)].to(torch.int32)
+    # every rank generates the same full data set (seed 5)
+    from mymedialite_amd.synthetic import c5_events
+    users, items = c5_events(n_users, n_items, per_user, dev)
+    n = len(users)
     torch.cuda.synchronize()
     # distinct (user, item) sets: the executed flop count follows the degrees the solves see
     keys = torch.unique(users.to(torch.int64) * n_items + items.to(torch.int64))
-    deg_u = torch.bincount(keys // n_items, minlength=n_users).double()
-    deg_i = torch.bincount(keys % n_items, minlength=n_items).double()
+    ku, ki = (keys // n_items).to(torch.int32), (keys % n_items).to(torch.int32)
+    deg_u = torch.bincount(ku, minlength=n_users).double()
+    deg_i = torch.bincount(ki, minlength=n_items).double()
     nnz = int(keys.numel())
     del keys
     passes = 3 if args.wrmf_precision == "fp64" else 0  # at most (adaptive)
@@ -719,6 +710,10 @@ def bench_wrmf(args):
     corr = np.zeros(8, np.float32)
     N.check(N.lib().mml_wrmf_last_refine_passes(h, ctypes.byref(ran), N.ptr(corr, N._f32p)))
     passes_run = ran.value
+    check = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        check = wrmf_row_check(h, ku, ki, deg_u, deg_i, n_users, n_items, k)
+    del ku, ki
     flops_exec = wrmf_executed_flops(deg_u, deg_i, k, passes_run, nnz)
     # SURVEY 8(d)'s count: every row a direct k x k solve (2 nnz k^2 Grams, 2 n k^2 HH, ...)
     half = lambda rows, other: 2 * n * k * k + 2 * other * k * k + rows * (k ** 3 / 3 + 2 * k * k) \
@@ -768,11 +763,49 @@ def bench_wrmf(args):
         "cpu_baseline": None if (args.no_cpu_baseline or world > 1) else cpu_baseline_wrmf(
             k, args.cpu_seconds, n_users, n_items, per_user),
     }
+    if check is not None:
+        line.update(check)
     if world > 1:
         line["config"]["parallelism"] = f"row shards x{world}, RCCL all-gather per half-step"
     N.lib().mml_wrmf_destroy(h)
     ctx.close()
     return line if rank == 0 else None
+
+
+def wrmf_row_check(h, ku, ki, deg_u, deg_i, n_users, n_items, k):
+    """Checker (after the timed iterations, outside them): one more iteration, then sampled user
+    rows (solved from the V it started from) and item rows (solved from the new U) against the
+    oracle's fp64 row solve with exact float products (WRMF.cs:110-156) -- 64 user rows and 24 item
+    rows over the solver buckets (Woodbury deg <= 128, direct, split-Gram deg > 8192)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    t0 = time.perf_counter()
+    V0 = np.empty((n_items, k), np.float32)
+    N.check(N.lib().mml_wrmf_get_model(h, None, N.ptr(V0, N._f32p)))
+    N.check(N.lib().mml_wrmf_iterate(h))
+    U1 = np.empty((n_users, k), np.float32)
+    V1 = np.empty((n_items, k), np.float32)
+    N.check(N.lib().mml_wrmf_get_model(h, N.ptr(U1, N._f32p), N.ptr(V1, N._f32p)))
+    rs = np.random.default_rng(5)
+    out, n_rows = {}, 0
+    for side, W, H, deg, picks in (
+            ("user", U1, V0, deg_u.cpu().numpy(), [(1, 128, 64)]),
+            ("item", V1, U1, deg_i.cpu().numpy(), [(1, 128, 8), (129, 8192, 8), (8193, 20000, 8)])):
+        rows = []
+        for lo, hi, cnt in picks:
+            c = np.nonzero((deg >= lo) & (deg <= hi))[0]
+            if len(c):
+                rows.append(rs.choice(c, size=min(cnt, len(c)), replace=False))
+        rows = np.sort(np.concatenate(rows))
+        rel = O.wrmf_rows_check(rows, *((ku, ki) if side == "user" else (ki, ku)), W, H, k)
+        out[side] = float(rel.max())
+        n_rows += len(rows)
+    return {"row_check_max_rel": max(out.values()), "row_check_by_side": out,
+            "row_check_note": f"one further fp64-mode iteration after the timed ones; {n_rows} "
+                              f"sampled rows (64 user rows, 24 item rows over the Woodbury / "
+                              f"direct / split-Gram buckets) vs the oracle's fp64 row solve with "
+                              f"exact float products (WRMF.cs:110-156), max |dW| / (1 + |W|); "
+                              f"bar 2e-7 ({time.perf_counter() - t0:.0f} s)"}
 
 
 def wrmf_executed_flops(deg_u, deg_i, k, passes=0, nnz=0, alpha=1.0):

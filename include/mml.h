@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 8
+#define MML_ABI_VERSION 9
 
 typedef int32_t mml_status;
 enum {
@@ -59,9 +59,13 @@ mml_status mml_ctx_destroy(mml_ctx* ctx);
  * mml_bmf_set_data_device takes arrays on the first listed device and shards them there (ABI 6).
  * The sibling-model extras return MML_ERR_STATE.  A device id may be listed more than once
  * (several shards on one GPU, e.g. to emulate N devices on one): such a context has no
- * communicator; mml_bmf then runs the shards one after another and averages V || item biases
- * with peer copies and a device kernel (sum in shard order, then / N), the DSGD ring moves its
- * groups by peer copy, and mml_bpr / mml_wrmf refuse it. */
+ * communicator; mml_bmf and mml_bpr then run the shards one after another and average V || item
+ * biases with peer copies and a device kernel (sum in shard order, then / N), the DSGD ring moves
+ * its groups by peer copy, and mml_wrmf runs its row shards on one host thread each, all-gathering
+ * by peer copies between host barriers (ABI 9).  mml_bpr's user shards also run the ORDERED
+ * schedule (ABI 9), and mml_wrmf's shards take every refinement decision on the max over the
+ * shards' corrections (ABI 9), so a row-sharded WRMF model equals the one-device model bit for
+ * bit at any shard count, over RCCL or peer copies. */
 mml_status mml_ctx_create_multi(const int32_t* device_ids, int32_t n_devices, mml_ctx** out);
 /* RCCL communicator across processes (one rank per GPU): rank 0 creates the 128-byte id, the host
  * broadcasts it (e.g. torch.distributed / MPI), then every rank calls mml_ctx_comm_init. */
@@ -386,7 +390,9 @@ mml_status mml_bpr_destroy(mml_bpr* h);
  * counted in Feedback.Count = samples per epoch); order = Feedback.RandomIndex for UNIFORM_PAIR. */
 mml_status mml_bpr_set_data(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t n,
                             const int32_t* order);
-/* Same from arrays already in this context's HBM; the sets are built on the device (csr.hip). */
+/* Same from arrays already in this context's HBM; the sets are built on the device (csr.hip).
+ * On a multi-device context (ABI 9) the arrays live on the first listed device, which splits them
+ * into the user shards (as mml_bpr_set_data) and hands each device its part. */
 mml_status mml_bpr_set_data_device(mml_bpr* h, const int32_t* users_device,
                                    const int32_t* items_device, int64_t n,
                                    const int32_t* order_device);
@@ -427,7 +433,9 @@ mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const int32_t* item
  * triple sampler) */
 mml_status mml_bpr_last_timing(mml_bpr* h, float* out);
 /* The last epoch's sampled triples in sample order (n = Feedback.Count), e.g. for BPRMF's
- * loss_sample_* arrays (BPRMF.cs:136-150) or to check a sampler's distribution (ABI 3). */
+ * loss_sample_* arrays (BPRMF.cs:136-150) or to check a sampler's distribution (ABI 3).  On a
+ * multi-device context: each user shard's triples in its sample order, shard after shard (ABI 9;
+ * shard d holds the events of its user range, mml_bpr_set_data's equal-count bounds). */
 mml_status mml_bpr_last_triples(mml_bpr* h, int32_t* users, int32_t* items, int32_t* other_items,
                                 int64_t n);
 /* Eval.Items.Evaluate's AUC (Eval/Items.cs:126-209 + Recommender.Recommend n = -1 +

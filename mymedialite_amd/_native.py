@@ -258,6 +258,9 @@ class Context:
         self.handle = h
         self.device = device
         self.rank = 0
+        # objects holding native state bound to this context (DeviceRatingFile): closed first
+        import weakref
+        self._dependents = weakref.WeakSet()
 
     @staticmethod
     def unique_id() -> bytes:
@@ -278,6 +281,8 @@ class Context:
 
     def close(self):
         if getattr(self, "handle", None):
+            for d in list(getattr(self, "_dependents", ())):
+                d.close()  # their native state points at this context (mml_rating_file.ctx)
             lib().mml_ctx_destroy(self.handle)
             self.handle = None
 
@@ -286,3 +291,20 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+def auc_held_out(symbol: str, h, candidates, users, items):
+    """Eval.Items.Evaluate's AUC (Eval/Items.cs:126-209, AUC.cs:42-68) through mml_bpr_auc /
+    mml_wrmf_auc when every evaluated user holds exactly one test item (a held-out positive):
+    users[x]'s test item is items[x].  Returns (mean over the evaluated users accumulated in float as
+    Items.cs:177-188 does, number of users evaluated, per-user AUC with NaN = skipped)."""
+    users, items, cand = i32(users), i32(items), i32(candidates)
+    off = np.arange(len(users) + 1, dtype=np.int64)
+    out = np.empty(len(users), np.float64)
+    check(getattr(lib(), symbol)(h, ptr(cand, _i32p), len(cand), ptr(users, _i32p), len(users),
+                                 ptr(off, _i64p), ptr(items, _i32p), ptr(out, _f64p)))
+    ok = out[~np.isnan(out)].astype(np.float32)
+    acc = np.float32(0.0)
+    for a in ok:  # float accumulation, in user order
+        acc = np.float32(acc + a)
+    return (float(np.float32(acc / np.float32(len(ok)))) if len(ok) else 0.0), int(len(ok)), out

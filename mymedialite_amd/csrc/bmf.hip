@@ -963,21 +963,6 @@ __global__ __launch_bounds__(256) void check_order_kernel(const int32_t* __restr
         if (order[x] < 0 || order[x] >= n) atomicOr(bad, 1);
 }
 
-// the user shards' item average without a communicator: dst (shard 0's rows) <- (dst + the other
-// shards' copies staged at stage[p * stride], summed in shard order) / parts -- the left-to-right
-// float sum, then one correctly rounded division, as the in-process emulation computes it
-__global__ __launch_bounds__(256) void average_rows_kernel(float* __restrict__ dst,
-                                                           const float* __restrict__ stage,
-                                                           int64_t n, int64_t stride,
-                                                           int32_t parts) {
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
-         x += (int64_t)gridDim.x * blockDim.x) {
-        float s = dst[x];
-        for (int32_t p = 0; p + 1 < parts; ++p) s += stage[(int64_t)p * stride + x];
-        dst[x] = s / (float)parts;
-    }
-}
-
 // packed[x] = M[ids[x]] (rows of ld floats) and packed_b[x] = b[ids[x]] (b may be null)
 __global__ __launch_bounds__(256) void rows_gather_kernel(const float* __restrict__ M,
                                                           const float* __restrict__ b,
@@ -2223,44 +2208,20 @@ void multi_set_data_device(mml_bmf* h, const int32_t* users, const int32_t* item
 // shard's stream waits for the copies before its next call.  Equal bit for bit to the in-process
 // emulation (tests/test_dist.py): sum over the shards left to right, then / N.
 void multi_average_peer(mml_bmf* h) {
-    const int32_t nd = (int32_t)h->shards.size();
     mml_bmf* s0 = h->shards[0];
     s0->ctx->activate();
-    hipStream_t st = s0->ctx->stream;
-    const int64_t nv = (int64_t)h->n_items * s0->ld, ni = h->n_items, slot = nv + ni;
     if (!h->ev_ar0) {
         MML_HIP(hipEventCreate(&h->ev_ar0));
         MML_HIP(hipEventCreate(&h->ev_ar1));
     }
-    MML_HIP(hipEventRecord(h->ev_ar0, st));
-    if (nd > 1 && ni > 0) {
-        h->avg_stage.alloc((size_t)(nd - 1) * slot);
-        float* stage = h->avg_stage.get();
-        for (int32_t d = 1; d < nd; ++d) {
-            mml_bmf* s = h->shards[d];
-            float* dst = stage + (int64_t)(d - 1) * slot;
-            MML_HIP(hipMemcpyPeerAsync(dst, s0->ctx->device, s->V.get(), s->ctx->device,
-                                       sizeof(float) * nv, st));
-            MML_HIP(hipMemcpyPeerAsync(dst + nv, s0->ctx->device, s->bi.get(), s->ctx->device,
-                                       sizeof(float) * ni, st));
-        }
-        average_rows_kernel<<<grid_for(nv), 256, 0, st>>>(s0->V.get(), stage, nv, slot, nd);
-        average_rows_kernel<<<grid_for(ni), 256, 0, st>>>(s0->bi.get(), stage + nv, ni, slot, nd);
-        MML_HIP(hipGetLastError());
-        for (int32_t d = 1; d < nd; ++d) {
-            mml_bmf* s = h->shards[d];
-            MML_HIP(hipMemcpyPeerAsync(s->V.get(), s->ctx->device, s0->V.get(), s0->ctx->device,
-                                       sizeof(float) * nv, st));
-            MML_HIP(hipMemcpyPeerAsync(s->bi.get(), s->ctx->device, s0->bi.get(),
-                                       s0->ctx->device, sizeof(float) * ni, st));
-        }
+    std::vector<mml_ctx*> ctxs;
+    std::vector<std::vector<float*>> arr;
+    for (mml_bmf* s : h->shards) {
+        ctxs.push_back(s->ctx);
+        arr.push_back({s->V.get(), s->bi.get()});
     }
-    MML_HIP(hipEventRecord(h->ev_ar1, st));
-    for (int32_t d = 1; d < nd; ++d) {
-        mml_bmf* s = h->shards[d];
-        s->ctx->activate();
-        MML_HIP(hipStreamWaitEvent(s->ctx->stream, h->ev_ar1, 0));
-    }
+    mml::peer_average(ctxs, arr, {(int64_t)h->n_items * s0->ld, (int64_t)h->n_items},
+                      h->avg_stage, h->ev_ar0, h->ev_ar1);
     h->has_ar = true;
 }
 

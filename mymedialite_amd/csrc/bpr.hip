@@ -309,6 +309,26 @@ __global__ __launch_bounds__(256) void bpr_user_rec_kernel(const int64_t* __rest
 constexpr uint32_t kMaxWeightedDraws = 1u << 16;
 // MML_BPR_SCHEDULE_AUTO applies epochs below this many samples in order (one wavefront)
 constexpr int64_t kAutoOrderedBelow = 16 * 16384;
+// The default sampler's triple of sample smp (IterateWithoutReplacementUniformUser: SampleUser,
+// SampleItemPair, BPRMF.cs:290-310): u uniform over the eligible users, i uniform over S_u, j
+// uniform over the items outside S_u (Bloom filter, then the row)
+__device__ __forceinline__ void draw_uniform_user(const int32_t* __restrict__ cols,
+                                                  const int32_t* __restrict__ eligible,
+                                                  int32_t n_eligible, int32_t n_items,
+                                                  uint64_t seed, const uint32_t* __restrict__ recs,
+                                                  int64_t smp, int32_t& u, int32_t& i,
+                                                  int32_t& j) {
+    const uint32_t du = draw(seed, smp, 0, (uint32_t)n_eligible);
+    u = eligible ? eligible[du] : (int32_t)du;
+    const uint32_t* rec = recs + (int64_t)u * kRecWords;
+    const UserRec ur = user_rec(rec);
+    i = cols[ur.rb + draw(seed, smp, 1, (uint32_t)(ur.re - ur.rb))];
+    for (uint32_t d = 2;; ++d) {
+        j = (int32_t)draw(seed, smp, d, (uint32_t)n_items);
+        if (!(bloom_maybe(rec, j) && row_has(cols, ur.rb, ur.re, j))) break;
+    }
+}
+
 template <int SAMPLER>
 __global__ __launch_bounds__(256) void bpr_sample_kernel(
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols,
@@ -320,6 +340,13 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
     for (int64_t smp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; smp < n_samples;
          smp += (int64_t)gridDim.x * blockDim.x) {
         int32_t u, i = 0, j = 0;
+        if constexpr (SAMPLER == MML_BPR_SAMPLER_UNIFORM_USER) {
+            draw_uniform_user(cols, eligible, n_eligible, n_items, seed, recs, smp, u, i, j);
+            tu[smp] = u;
+            ti[smp] = i;
+            tj[smp] = j;
+            continue;
+        }
         if constexpr (SAMPLER == MML_BPR_SAMPLER_UNIFORM_PAIR) {
             u = ev_u[smp];
             i = ev_i[smp];
@@ -336,8 +363,6 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
         const UserRec ur = user_rec(rec);
         const int64_t rb = ur.rb, re = ur.re;
         auto in_row = [&](int32_t c) { return bloom_maybe(rec, c) && row_has(cols, rb, re, c); };
-        if constexpr (SAMPLER == MML_BPR_SAMPLER_UNIFORM_USER)
-            i = cols[rb + draw(seed, smp, 1, (uint32_t)(re - rb))];
         // USER_REPLACEMENT: i is resolved after the epoch's samples are ranked per user
         if constexpr (SAMPLER == MML_BPR_SAMPLER_USER_REPLACEMENT)
             user_keys[smp] = ((uint64_t)(uint32_t)u << 32) | (uint32_t)smp;
@@ -361,6 +386,111 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
         if constexpr (SAMPLER != MML_BPR_SAMPLER_USER_REPLACEMENT) ti[smp] = i;
         tj[smp] = j;
     }
+}
+
+// The default sampler writing each triple straight into the region of its XCD group (the group of
+// i, xcd.hip): the epoch's triples come out partitioned for the Hogwild update without the
+// count / scatter passes of XcdSplit::partition.  A block draws kGrpPer x 256 consecutive samples
+// (the same counter-based draws as bpr_sample_kernel: the same triples), ranks them per group in
+// LDS, reserves its run of each group's region with one global atomic per group, and writes.
+// Region g holds gcap[g] triples from gbeg[g]; gcnt[g] counts the triples it received.  A block
+// whose run would pass a region's end writes nothing of that group and raises *overflow (the
+// epoch is then redrawn through the two-pass path).  The order within a region follows the blocks'
+// atomics, not the sample index (the Hogwild update interleaves the triples anyway).
+constexpr int kGrpPer = 8;
+__global__ __launch_bounds__(256) void bpr_sample_grouped_kernel(
+    const int32_t* __restrict__ cols, const int32_t* __restrict__ eligible, int32_t n_eligible,
+    int64_t n_samples, int32_t n_items, uint64_t seed, const uint32_t* __restrict__ recs,
+    const uint8_t* __restrict__ group, const int64_t* __restrict__ gbeg,
+    const int64_t* __restrict__ gcap, unsigned long long* __restrict__ gcnt,
+    int32_t* __restrict__ xu, int32_t* __restrict__ xi, int32_t* __restrict__ xj,
+    int32_t* __restrict__ overflow) {
+    __shared__ int32_t cnt[8];
+    __shared__ int64_t base[8];
+    if (threadIdx.x < 8) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x * (256 * kGrpPer);
+    int32_t su[kGrpPer], si[kGrpPer], sj[kGrpPer], rk[kGrpPer];
+    int64_t rb[kGrpPer];
+    uint32_t dg[kGrpPer];
+    // the draws of draw_uniform_user, phase by phase over the thread's kGrpPer samples: each
+    // phase's loads are independent of each other, so they are in flight together
+#pragma unroll
+    for (int t = 0; t < kGrpPer; ++t) {
+        const int64_t smp = b0 + t * 256 + threadIdx.x;
+        const uint32_t du = draw(seed, smp, 0, (uint32_t)n_eligible);
+        su[t] = smp < n_samples ? (eligible ? eligible[du] : (int32_t)du) : 0;
+    }
+#pragma unroll
+    for (int t = 0; t < kGrpPer; ++t) {
+        const UserRec ur = user_rec(recs + (int64_t)su[t] * kRecWords);
+        rb[t] = ur.rb;
+        dg[t] = (uint32_t)(ur.re - ur.rb);
+    }
+#pragma unroll
+    for (int t = 0; t < kGrpPer; ++t) {
+        const int64_t smp = b0 + t * 256 + threadIdx.x;
+        si[t] = cols[rb[t] + draw(seed, smp, 1, dg[t] ? dg[t] : 1)];
+        sj[t] = (int32_t)draw(seed, smp, 2, (uint32_t)n_items);
+    }
+#pragma unroll
+    for (int t = 0; t < kGrpPer; ++t) {
+        const int64_t smp = b0 + t * 256 + threadIdx.x;
+        rk[t] = -1;
+        if (smp >= n_samples) continue;
+        const uint32_t* rec = recs + (int64_t)su[t] * kRecWords;
+        for (uint32_t d = 3; bloom_maybe(rec, sj[t]) && row_has(cols, rb[t], rb[t] + dg[t], sj[t]);
+             ++d)
+            sj[t] = (int32_t)draw(seed, smp, d, (uint32_t)n_items);
+        rk[t] = atomicAdd(&cnt[group[si[t]]], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 8) {
+        const int g = threadIdx.x;
+        base[g] = cnt[g] ? (int64_t)atomicAdd(&gcnt[g], (unsigned long long)cnt[g]) : 0;
+        if (cnt[g] && base[g] + cnt[g] > gcap[g]) {
+            atomicOr(overflow, 1);
+            base[g] = -1;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kGrpPer; ++t) {
+        if (rk[t] < 0) continue;
+        const int g = group[si[t]];
+        if (base[g] < 0) continue;
+        const int64_t pos = gbeg[g] + base[g] + rk[t];
+        xu[pos] = su[t];
+        xi[pos] = si[t];
+        xj[pos] = sj[t];
+    }
+}
+
+// Each group's share of the default sampler's i: (1 / n_eligible) sum over the eligible users of
+// |S_u in g| / |S_u| (u uniform, then i uniform in S_u) -- the expected region sizes
+__global__ __launch_bounds__(256) void bpr_group_share_kernel(
+    const int64_t* __restrict__ off, const int32_t* __restrict__ cols,
+    const int32_t* __restrict__ eligible, int32_t n_eligible, const uint8_t* __restrict__ group,
+    double* __restrict__ share) {
+    __shared__ double acc[8];
+    if (threadIdx.x < 8) acc[threadIdx.x] = 0.0;
+    __syncthreads();
+    double mine[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n_eligible;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t u = eligible ? eligible[x] : (int32_t)x;
+        const int64_t b = off[u], e = off[u + 1];
+        const double w = 1.0 / (double)(e - b);
+        for (int64_t c = b; c < e; ++c) {
+            const int g = group[cols[c]];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) mine[q] += q == g ? w : 0.0;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) atomicAdd(&acc[q], mine[q]);
+    __syncthreads();
+    if (threadIdx.x < 8) atomicAdd(&share[threadIdx.x], acc[threadIdx.x]);
 }
 
 // USER_REPLACEMENT, after a stable sort of the keys (u << 32 | s) by u: head[u] = the position
@@ -428,14 +558,14 @@ constexpr int kBprFlush = 8;  // one wave per XCD writes its L2's dirty lines ba
 template <int LPR, bool SOFT, int AM>
 __global__ __launch_bounds__(256) void bpr_update_kernel(
     const int32_t* __restrict__ tu, const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
-    const int64_t* __restrict__ goff, int32_t ng, int32_t waves_per_group, float* U, float* V,
-    float* bias, int32_t ld4, uint32_t v_bytes, uint32_t b_bytes, uint32_t u_bytes,
-    int32_t flushers, BprScalars s) {
+    const int64_t* __restrict__ goff, const unsigned long long* __restrict__ gcnt, int32_t ng,
+    int32_t waves_per_group, float* U, float* V, float* bias, int32_t ld4, uint32_t v_bytes,
+    uint32_t b_bytes, uint32_t u_bytes, int32_t flushers, BprScalars s) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const mml::GroupWave gw = mml::group_wave(goff, ng, waves_per_group,
                                               __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
-                                              blockDim.x >> 6);
+                                              blockDim.x >> 6, gcnt);
     const int64_t begin = gw.begin, end = gw.end;
     const int sub = lane / LPR, q = lane % LPR;
     float4* U4 = reinterpret_cast<float4*>(U);
@@ -665,9 +795,21 @@ struct mml_bpr {
     mml::DeviceArray<int32_t> xt_u, xt_i, xt_j;
     mml::DeviceArray<int64_t> span1;
     bool has_groups = false;
+    // the default sampler writing straight into per-group regions of xt_* (bpr_sample_grouped_
+    // kernel): region g = [rg_beg[g], rg_beg[g] + rg_cap[g]), rg_cnt[g] triples in it; sized for
+    // rg_n samples; grouped_last: the last epoch's triples sit in the regions
+    mml::DeviceArray<int64_t> rg_beg, rg_cap;
+    mml::DeviceArray<unsigned long long> rg_cnt;
+    mml::DeviceArray<int32_t> rg_over;
+    std::vector<int64_t> rg_beg_h;
+    int64_t rg_n = -1;
+    bool grouped_last = false;
     // multi-device context: one single-device handle per GPU over a user range ub[d] .. ub[d + 1]
     std::vector<mml_bpr*> shards;
     std::vector<int32_t> ub;
+    // a repeated-device context: the item average by peer copies (mml::peer_average)
+    mml::DeviceArray<float> avg_stage;
+    hipEvent_t ev_ar0 = nullptr, ev_ar1 = nullptr;
     int64_t n_events = 0, nnz = 0;
     int32_t n_eligible = 0;
     bool has_data = false, has_model = false, has_order = false, has_triples = false;
@@ -734,9 +876,6 @@ extern "C" mml_status mml_bpr_create(mml_ctx* ctx, const mml_bpr_params* params,
                         params->schedule <= MML_BPR_SCHEDULE_ORDERED,
                     "unknown schedule");
         if (ctx->multi()) {
-            mml::require_comm(ctx);
-            MML_REQUIRE(params->schedule != MML_BPR_SCHEDULE_ORDERED,
-                        "a multi-device context trains with the HOGWILD / AUTO schedules");
             // WeightedBPRMF draws j by item popularity (WeightedBPRMF.cs:55-67); a shard holds
             // only its users' events, so its popularity would be shard-local, not the reference's
             MML_REQUIRE(params->sampler != MML_BPR_SAMPLER_WEIGHTED,
@@ -793,6 +932,11 @@ extern "C" mml_status mml_bpr_destroy(mml_bpr* h) {
         if (h->ctx && h->ctx->multi()) {
             for (mml_bpr* s : h->shards)
                 if (s) mml_bpr_destroy(s);
+            if (h->ev_ar0) {
+                (void)hipSetDevice(h->ctx->device);
+                (void)hipEventDestroy(h->ev_ar0);
+                (void)hipEventDestroy(h->ev_ar1);
+            }
             delete h;
             return;
         }
@@ -860,6 +1004,111 @@ void bpr_ingest(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t 
     h->has_data = true;
 }
 
+__global__ __launch_bounds__(256) void bpr_check_ids_kernel(const int32_t* __restrict__ users,
+                                                            const int32_t* __restrict__ items,
+                                                            const int32_t* __restrict__ order,
+                                                            int64_t n, int32_t n_users,
+                                                            int32_t n_items,
+                                                            int32_t* __restrict__ bad) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        if (users[x] < 0 || users[x] >= n_users || items[x] < 0 || items[x] >= n_items)
+            atomicOr(bad, 1);
+        if (order && (order[x] < 0 || order[x] >= n)) atomicOr(bad, 2);
+    }
+}
+
+// mml_bpr_set_data_device on a multi-device context: the arrays live on the first device.  The
+// per-user counts, the user ranges of equal event count and a stable partition of the
+// (visit-ordered) events by owner run there; each shard then ingests its contiguous part (a peer
+// copy when its device differs) -- equal to mml_bpr_set_data with the same arrays on the host.
+void bpr_multi_set_data_device(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t n,
+                               const int32_t* order) {
+    const int32_t nd = (int32_t)h->shards.size();
+    MML_REQUIRE(nd <= 8, "mml_bpr_set_data_device on a multi-device context shards over at most "
+                         "8 devices (use mml_bpr_set_data)");
+    mml_bpr* s0 = h->shards[0];
+    s0->ctx->activate();
+    hipStream_t st = s0->ctx->stream;
+    {
+        mml::DeviceArray<int32_t> bad;
+        bad.alloc(1);
+        MML_HIP(hipMemsetAsync(bad.get(), 0, sizeof(int32_t), st));
+        bpr_check_ids_kernel<<<grid_for(n), 256, 0, st>>>(users, items, order, n, h->n_users,
+                                                          h->n_items, bad.get());
+        MML_HIP(hipGetLastError());
+        int32_t flag = 0;
+        MML_HIP(hipMemcpyAsync(&flag, bad.get(), sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        MML_HIP(hipStreamSynchronize(st));
+        MML_REQUIRE(!(flag & 1), "event user/item id out of range");
+        MML_REQUIRE(!(flag & 2), "order index out of range");
+    }
+    h->has_data = false;
+    h->ub = mml::balanced_user_bounds_counts(mml::device_id_counts(st, users, n, h->n_users), n,
+                                             nd);
+    mml::DeviceArray<int32_t> ou, oi, pu, pi;
+    const int32_t *su = users, *si = items;
+    if (order) {  // the visit order first (UNIFORM_PAIR's Feedback.RandomIndex)
+        ou.alloc(n);
+        oi.alloc(n);
+        bpr_gather_events_kernel<<<grid_for(n), 256, 0, st>>>(users, items, order, n, ou.get(),
+                                                              oi.get());
+        MML_HIP(hipGetLastError());
+        su = ou.get();
+        si = oi.get();
+    }
+    std::vector<int64_t> goff(nd + 1, 0);
+    goff[nd] = n;
+    if (nd > 1) {
+        std::vector<uint8_t> table(h->n_users);
+        for (int32_t d = 0; d < nd; ++d)
+            for (int32_t u = h->ub[d]; u < h->ub[d + 1]; ++u) table[u] = (uint8_t)d;
+        mml::XcdSplit xs;
+        xs.set_table(st, table);
+        pu.alloc(n);
+        pi.alloc(n);
+        const int32_t* in[2] = {su, si};
+        int32_t* out[2] = {pu.get(), pi.get()};
+        xs.partition(st, su, n, 2, in, out);
+        int64_t g[9];
+        MML_HIP(hipMemcpyAsync(g, xs.goff.get(), sizeof(g), hipMemcpyDeviceToHost, st));
+        MML_HIP(hipStreamSynchronize(st));
+        for (int32_t d = 0; d < nd; ++d) goff[d] = g[d];
+        ou.reset();
+        oi.reset();
+        su = pu.get();
+        si = pi.get();
+    }
+    MML_HIP(hipStreamSynchronize(st));
+    for (int32_t d = 0; d < nd; ++d)
+        MML_REQUIRE(goff[d + 1] > goff[d], "a device's user range holds no event");
+    for (int32_t d = 0; d < nd; ++d) {
+        mml_bpr* s = h->shards[d];
+        const int64_t o = goff[d], m = goff[d + 1] - goff[d];
+        const int32_t *du = su + o, *di = si + o;
+        mml::DeviceArray<int32_t> tu, ti;  // the shard's part on its own device
+        if (s->ctx->device != s0->ctx->device) {
+            s->ctx->activate();
+            tu.alloc(m);
+            ti.alloc(m);
+            hipStream_t ss = s->ctx->stream;
+            MML_HIP(hipMemcpyPeerAsync(tu.get(), s->ctx->device, du, s0->ctx->device,
+                                       sizeof(int32_t) * m, ss));
+            MML_HIP(hipMemcpyPeerAsync(ti.get(), s->ctx->device, di, s0->ctx->device,
+                                       sizeof(int32_t) * m, ss));
+            MML_HIP(hipStreamSynchronize(ss));
+            du = tu.get();
+            di = ti.get();
+        }
+        s->ctx->activate();
+        s->has_data = false;
+        bpr_ingest(s, du, di, m, nullptr);
+    }
+    s0->ctx->activate();
+    h->n_events = n;
+    h->has_data = true;
+}
+
 }  // namespace
 
 extern "C" mml_status mml_bpr_set_data(mml_bpr* h, const int32_t* users, const int32_t* items,
@@ -917,11 +1166,11 @@ extern "C" mml_status mml_bpr_set_data_device(mml_bpr* h, const int32_t* users,
                                               const int32_t* order) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
-        bpr_single_device_only(h);
         MML_REQUIRE(n >= 1 && users && items, "need >= 1 event");
         MML_REQUIRE(!order || (h->p.sampler != MML_BPR_SAMPLER_UNIFORM_USER &&
                                h->p.sampler != MML_BPR_SAMPLER_USER_REPLACEMENT),
                     "a device order is not used by the user-sampling samplers");
+        if (h->ctx->multi()) return bpr_multi_set_data_device(h, users, items, n, order);
         h->ctx->activate();
         h->has_data = false;
         bpr_ingest(h, users, items, n, order);
@@ -1130,9 +1379,10 @@ BprXcdMode bpr_xcd_mode(int sampler) {
 }
 
 template <int LPR, bool SOFT>
-void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff, const int32_t* tu,
-                       const int32_t* ti, const int32_t* tj, int64_t blocks, int wpb,
-                       const BprScalars& s, hipStream_t st) {
+void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff,
+                       const unsigned long long* gcnt, const int32_t* tu, const int32_t* ti,
+                       const int32_t* tj, int64_t blocks, int wpb, const BprScalars& s,
+                       hipStream_t st) {
     const int32_t wpg = (int32_t)(blocks / ng * wpb);
     const uint32_t vb = (uint32_t)std::min<uint64_t>((uint64_t)h->n_items * h->ld * 4, 0xFFFFFFFFull);
     const uint32_t bb = (uint32_t)((uint64_t)h->n_items * 4);
@@ -1141,7 +1391,8 @@ void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff, cons
     if (u_all >= (1ull << 32)) am &= ~kBprUThru;
 #define MML_UPD(AM)                                                                             \
     bpr_update_kernel<LPR, SOFT, AM><<<(int)blocks, 64 * wpb, 0, st>>>(                        \
-        tu, ti, tj, goff, ng, wpg, h->U.get(), h->V.get(), h->bias.get(), h->ld / 4, vb, bb, ub, \
+        tu, ti, tj, goff, gcnt, ng, wpg, h->U.get(), h->V.get(), h->bias.get(), h->ld / 4, vb, bb, \
+        ub, \
         mml::flushers_per_xcd(4), s)
     switch (am) {
         case kBprLdL2: MML_UPD(kBprLdL2); break;
@@ -1157,11 +1408,14 @@ void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff, cons
 }
 
 void launch_update(mml_bpr* h, bool soft, int am, int32_t ng, const int64_t* goff,
-                   const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t blocks,
-                   int wpb, const BprScalars& s, hipStream_t st) {
-#define MML_UPL(LPR)                                                                        \
-    if (soft) launch_update_lpr<LPR, true>(h, am, ng, goff, tu, ti, tj, blocks, wpb, s, st); \
-    else launch_update_lpr<LPR, false>(h, am, ng, goff, tu, ti, tj, blocks, wpb, s, st)
+                   const unsigned long long* gcnt, const int32_t* tu, const int32_t* ti,
+                   const int32_t* tj, int64_t blocks, int wpb, const BprScalars& s,
+                   hipStream_t st) {
+#define MML_UPL(LPR)                                                                           \
+    if (soft)                                                                                  \
+        launch_update_lpr<LPR, true>(h, am, ng, goff, gcnt, tu, ti, tj, blocks, wpb, s, st);   \
+    else                                                                                       \
+        launch_update_lpr<LPR, false>(h, am, ng, goff, gcnt, tu, ti, tj, blocks, wpb, s, st)
     switch (h->lpr) {
         case 1: MML_UPL(1); break;
         case 2: MML_UPL(2); break;
@@ -1177,6 +1431,59 @@ void launch_update(mml_bpr* h, bool soft, int am, int32_t ng, const int64_t* gof
 
 }  // namespace
 
+namespace {
+
+// MML_BPR_GROUPED=0 keeps the two-pass sampler + XcdSplit::partition (A/B of the grouped sampler)
+bool grouped_sampler_enabled() {
+    static const bool v = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_BPR_GROUPED");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+
+// The grouped sampler's regions for an epoch of n samples: region g gets its expected share of
+// the default sampler's i (bpr_group_share_kernel) + 8 standard deviations + one block's run, so an
+// overflow (then the two-pass path runs) is practically never seen.
+void plan_group_regions(mml_bpr* h, int64_t n, hipStream_t st) {
+    mml::DeviceArray<double> share;
+    share.alloc(8);
+    MML_HIP(hipMemsetAsync(share.get(), 0, 8 * sizeof(double), st));
+    const int32_t* elig = h->n_eligible == h->n_users ? nullptr : h->eligible.get();
+    bpr_group_share_kernel<<<grid_for(h->n_eligible, 256, 2048), 256, 0, st>>>(
+        h->off.get(), h->cols.get(), elig, h->n_eligible, h->xs.group.get(), share.get());
+    MML_HIP(hipGetLastError());
+    double sh[8];
+    MML_HIP(hipMemcpyAsync(sh, share.get(), sizeof(sh), hipMemcpyDeviceToHost, st));
+    MML_HIP(hipStreamSynchronize(st));
+    std::vector<int64_t> beg(8), cap(8);
+    int64_t total = 0;
+    for (int g = 0; g < 8; ++g) {
+        const double p = std::max(0.0, sh[g] / (double)h->n_eligible);
+        cap[g] = (int64_t)std::ceil(p * (double)n + 8.0 * std::sqrt(p * (double)n) +
+                                    256.0 * kGrpPer);
+        cap[g] = std::min(cap[g], n);
+        beg[g] = total;
+        total += cap[g];
+    }
+    h->xt_u.reserve(total);
+    h->xt_i.reserve(total);
+    h->xt_j.reserve(total);
+    h->rg_beg.alloc(8);
+    h->rg_cap.alloc(8);
+    h->rg_cnt.alloc(8);
+    h->rg_over.alloc(1);
+    MML_HIP(hipMemcpyAsync(h->rg_beg.get(), beg.data(), sizeof(int64_t) * 8,
+                           hipMemcpyHostToDevice, st));
+    MML_HIP(hipMemcpyAsync(h->rg_cap.get(), cap.data(), sizeof(int64_t) * 8,
+                           hipMemcpyHostToDevice, st));
+    MML_HIP(hipStreamSynchronize(st));
+    h->rg_beg_h = beg;
+    h->rg_n = n;
+}
+
+}  // namespace
+
 extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
@@ -1186,15 +1493,41 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             std::vector<float> ms(nd, 0.0f), ums(nd, 0.0f);
             // phase 1: every shard's epoch; phase 2 (only when all succeeded, so no rank waits in
             // a collective another one skipped): the item average
-            mml::on_devices(h->ctx, [&](int32_t d) {
+            auto epoch = [&](int32_t d) {
                 const mml_status st =
                     mml_bpr_iterate(h->shards[d], seed + 0x9E3779B97F4A7C15ull * d);
                 ms[d] = h->shards[d]->last_ms;
                 ums[d] = h->shards[d]->last_update_ms;
                 return st;
-            });
-            mml::on_devices(h->ctx,
-                            [&](int32_t d) { return mml_bpr_allreduce_items(h->shards[d]); });
+            };
+            if (h->ctx->repeated) {
+                // shards of one GPU: one after another, each with the whole device (as it would
+                // have a GPU of its own), then the average by peer copies, summed in shard order
+                for (int32_t d = 0; d < (int32_t)nd; ++d) {
+                    const mml_status st = epoch(d);
+                    if (st != MML_OK)
+                        mml::fail(st, "shard " + std::to_string(d) + ": " + mml_last_error());
+                }
+                mml_bpr* s0 = h->shards[0];
+                s0->ctx->activate();
+                if (!h->ev_ar0) {
+                    MML_HIP(hipEventCreate(&h->ev_ar0));
+                    MML_HIP(hipEventCreate(&h->ev_ar1));
+                }
+                std::vector<mml_ctx*> ctxs;
+                std::vector<std::vector<float*>> arr;
+                for (mml_bpr* s : h->shards) {
+                    ctxs.push_back(s->ctx);
+                    arr.push_back({s->V.get(), s->bias.get()});
+                }
+                mml::peer_average(ctxs, arr, {(int64_t)h->n_items * s0->ld, (int64_t)h->n_items},
+                                  h->avg_stage, h->ev_ar0, h->ev_ar1);
+                MML_HIP(hipEventSynchronize(h->ev_ar1));
+            } else {
+                mml::on_devices(h->ctx, epoch);
+                mml::on_devices(h->ctx,
+                                [&](int32_t d) { return mml_bpr_allreduce_items(h->shards[d]); });
+            }
             h->last_ms = *std::max_element(ms.begin(), ms.end());
             h->last_update_ms = *std::max_element(ums.begin(), ums.end());
             return;
@@ -1245,11 +1578,30 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         // the fused single-kernel epoch exists for the BPRMF update with the uniform samplers
         const bool fused = fused_env && !soft && !ordered &&
                            (pair || h->p.sampler == MML_BPR_SAMPLER_UNIFORM_USER);
-        if (!fused && n > 0 && (int64_t)h->tri_u.count < n) {
-            h->tri_u.alloc(n);
-            h->tri_i.alloc(n);
-            h->tri_j.alloc(n);
+        // XCD-owned item groups: the triples partitioned by the group of i (part of the sampling
+        // phase), so that every access to V_i comes from the XCD that owns i
+        const BprXcdMode xm = bpr_xcd_mode(h->p.sampler);
+        const bool v_fits = (uint64_t)h->n_items * h->ld * sizeof(float) < (1ull << 32);
+        const bool part = !ordered && !fused && n > 0 && waves >= 16 && xm.partition && v_fits &&
+                          mml::xcd_groups(h->ctx) == 8;
+        if (part && !h->has_groups) {
+            h->xs.set_groups(st, mml::device_id_counts(st, h->cols.get(), h->nnz, h->n_items), 8);
+            h->has_groups = true;
+            h->rg_n = -1;
         }
+        // the default sampler draws straight into the groups' regions (no tri_* copy, no
+        // count / scatter pass)
+        bool grouped = part && h->p.sampler == MML_BPR_SAMPLER_UNIFORM_USER &&
+                       grouped_sampler_enabled() && n <= (int64_t)INT32_MAX * 64;
+        if (grouped && h->rg_n != n) plan_group_regions(h, n, st);
+        auto alloc_tri = [&] {
+            if ((int64_t)h->tri_u.count < n) {
+                h->tri_u.alloc(n);
+                h->tri_i.alloc(n);
+                h->tri_j.alloc(n);
+            }
+        };
+        if (!fused && n > 0 && !grouped) alloc_tri();
         // USER_REPLACEMENT: rank keys, their sorted copy, per-user heads and the sort's scratch
         int rank_end_bit = 0;
         size_t rank_tmp_bytes = 0;
@@ -1268,7 +1620,26 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             if (h->rank_tmp.count < rank_tmp_bytes) h->rank_tmp.alloc(rank_tmp_bytes);
         }
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
-        if (!fused && n > 0) {
+        if (grouped) {
+            MML_HIP(hipMemsetAsync(h->rg_cnt.get(), 0, 8 * sizeof(unsigned long long), st));
+            MML_HIP(hipMemsetAsync(h->rg_over.get(), 0, sizeof(int32_t), st));
+            const int32_t* elig = h->n_eligible == h->n_users ? nullptr : h->eligible.get();
+            const int64_t gb = (n + 256 * kGrpPer - 1) / (256 * kGrpPer);
+            bpr_sample_grouped_kernel<<<(int)gb, 256, 0, st>>>(
+                h->cols.get(), elig, h->n_eligible, n, h->n_items, seed, h->recs.get(),
+                h->xs.group.get(), h->rg_beg.get(), h->rg_cap.get(), h->rg_cnt.get(),
+                h->xt_u.get(), h->xt_i.get(), h->xt_j.get(), h->rg_over.get());
+            MML_HIP(hipGetLastError());
+            int32_t over = 0;
+            MML_HIP(hipMemcpyAsync(&over, h->rg_over.get(), sizeof(int32_t),
+                                   hipMemcpyDeviceToHost, st));
+            MML_HIP(hipStreamSynchronize(st));
+            if (over) {  // a region filled up: the same triples through the two-pass path
+                grouped = false;
+                alloc_tri();
+            }
+        }
+        if (!fused && n > 0 && !grouped) {
             const int sgrid = (int)std::min<int64_t>(256 * 64, (n + 255) / 256);
             if (weighted) {
                 h->fail.alloc(1);
@@ -1317,24 +1688,21 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
                               "negative item found in 65536 draws (the reference loops for ever)");
             }
         }
-        // XCD-owned item groups: the triples partitioned by the group of i (stable; part of the
-        // sampling phase), so that every access to V_i comes from the XCD that owns i
         int32_t ng = 1;
         const int64_t* goff = h->span1.get();
+        const unsigned long long* gcnt = nullptr;
         const int32_t *tu = h->tri_u.get(), *ti = h->tri_i.get(), *tj = h->tri_j.get();
-        const BprXcdMode xm = bpr_xcd_mode(h->p.sampler);
-        const bool v_fits = (uint64_t)h->n_items * h->ld * sizeof(float) < (1ull << 32);
-        const bool part = !ordered && !fused && n > 0 && waves >= 16 && xm.partition && v_fits &&
-                          mml::xcd_groups(h->ctx) == 8;
         // the access flags need the buffer resource (V < 4 GiB) and, for the owner modes, the
         // groups; a one-workgroup epoch keeps plain accesses (one CU, one L2)
         const int am = v_fits && waves >= 16 && (part || !xm.partition) ? xm.am : 0;
-        if (part) {
-            if (!h->has_groups) {
-                h->xs.set_groups(st, mml::device_id_counts(st, h->cols.get(), h->nnz, h->n_items),
-                                 8);
-                h->has_groups = true;
-            }
+        if (grouped) {
+            ng = 8;
+            goff = h->rg_beg.get();
+            gcnt = h->rg_cnt.get();
+            tu = h->xt_u.get();
+            ti = h->xt_i.get();
+            tj = h->xt_j.get();
+        } else if (part) {  // stable partition of the sampled triples (XcdSplit)
             if ((int64_t)h->xt_u.count < n) {
                 h->xt_u.alloc(n);
                 h->xt_i.alloc(n);
@@ -1365,7 +1733,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             // triples in flight and no stale per-XCD replicas
             launch_apply_ordered(h, tu, ti, tj, n, s, st, 4, weighted_streams(h) / 4);
         } else if (!ordered && !fused && n > 0) {
-            launch_update(h, soft, am, ng, goff, tu, ti, tj, blocks, 4, s, st);
+            launch_update(h, soft, am, ng, goff, gcnt, tu, ti, tj, blocks, 4, s, st);
         } else if (fused) {
 #define MML_BPR(LPR)                                                                            \
     if (pair)                                                                                   \
@@ -1395,6 +1763,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));
         MML_HIP(hipEventElapsedTime(&h->last_update_ms, h->ctx->ev_mid, h->ctx->ev_end));
         h->has_triples = !fused && n > 0;
+        h->grouped_last = grouped;
     });
 }
 
@@ -1402,13 +1771,45 @@ extern "C" mml_status mml_bpr_last_triples(mml_bpr* h, int32_t* users, int32_t* 
                                            int32_t* other_items, int64_t n) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
-        bpr_single_device_only(h);
+        if (h->ctx->multi()) {  // the shards' triples one after another, in shard order
+            MML_REQUIRE(n == h->n_events && users && items && other_items,
+                        "n must equal the epoch's sample count (Feedback.Count)");
+            int64_t o = 0;
+            for (mml_bpr* s : h->shards) {
+                const mml_status st = mml_bpr_last_triples(s, users + o, items + o,
+                                                           other_items + o, s->n_events);
+                if (st != MML_OK) mml::fail(st, mml_last_error());
+                o += s->n_events;
+            }
+            return;
+        }
         MML_REQUIRE(h->has_triples, "no sampled epoch to report (run mml_bpr_iterate first; the "
                                     "fused experiment epoch keeps no triples)");
         MML_REQUIRE(n == h->n_events && users && items && other_items,
                     "n must equal the epoch's sample count (Feedback.Count)");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
+        if (h->grouped_last) {  // the regions one after another (group order)
+            unsigned long long cnt[8];
+            MML_HIP(hipMemcpyAsync(cnt, h->rg_cnt.get(), sizeof(cnt), hipMemcpyDeviceToHost, st));
+            MML_HIP(hipStreamSynchronize(st));
+            int64_t o = 0;
+            for (int g = 0; g < 8; ++g) {
+                const int64_t b = h->rg_beg_h[g], c = (int64_t)cnt[g];
+                MML_REQUIRE(o + c <= n, "grouped triples exceed the epoch's sample count");
+                if (!c) continue;
+                MML_HIP(hipMemcpyAsync(users + o, h->xt_u.get() + b, sizeof(int32_t) * c,
+                                       hipMemcpyDeviceToHost, st));
+                MML_HIP(hipMemcpyAsync(items + o, h->xt_i.get() + b, sizeof(int32_t) * c,
+                                       hipMemcpyDeviceToHost, st));
+                MML_HIP(hipMemcpyAsync(other_items + o, h->xt_j.get() + b, sizeof(int32_t) * c,
+                                       hipMemcpyDeviceToHost, st));
+                o += c;
+            }
+            MML_HIP(hipStreamSynchronize(st));
+            MML_REQUIRE(o == n, "grouped triples do not add up to the epoch's sample count");
+            return;
+        }
         MML_HIP(hipMemcpyAsync(users, h->tri_u.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost,
                                st));
         MML_HIP(hipMemcpyAsync(items, h->tri_i.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost,

@@ -74,8 +74,16 @@ extern "C" mml_status mml_ctx_create_multi(const int32_t* device_ids, int32_t n_
                 if (st != MML_OK) mml::fail(st, mml_last_error());
                 ctx->sub.push_back(s);
             }
-            // one communicator over the devices, driven from this process (no unique-id exchange)
-            if (!repeated) {
+            // one communicator over the devices, driven from this process (no unique-id exchange);
+            // a repeated device: host barriers between the shards' threads instead (peer.hip)
+            if (repeated) {
+                auto g = std::make_shared<mml::PeerGroup>(n_devices);
+                g->devices.assign(device_ids, device_ids + n_devices);
+                for (int32_t d = 0; d < n_devices; ++d) {
+                    ctx->sub[d]->peers = g;
+                    ctx->sub[d]->peer_rank = d;
+                }
+            } else {
                 std::vector<ncclComm_t> comms(n_devices);
                 MML_RCCL(ncclCommInitAll(comms.data(), n_devices, device_ids));
                 for (int32_t d = 0; d < n_devices; ++d) {

@@ -18,6 +18,8 @@
 
 #include "mml.h"
 
+struct mml_ctx;
+
 // Experiment switches (environment variables that select A/B variants of a kernel: MML_HOGWILD_XCD,
 // MML_WRMF_DEBUG, ...) exist only in a library built with -DMML_EXPERIMENTS
 // (scripts/build_variant.sh).  The release library never reads the environment: the macro drops
@@ -188,10 +190,14 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
 // (exact float products, double sums) and the correction from the fp32 solver, so W rows [r0, r1)
 // reach the accuracy of the reference's fp64 solve (WRMF.cs:137-154); a further round runs only
 // while the last correction exceeded 1e-4 relative.  Returns the rounds run.
+// sync (nullable): the context whose ranks (communicator or peer group) each solve a row shard;
+// the decision to run another pass is then taken on the max over the ranks, so every rank runs the
+// same passes (a rank without rows still calls, to join the decisions).
 int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H,
                          int64_t h_rows, const int64_t* off, const int32_t* cols, const double* HH,
                          int32_t k, double alpha, double reg, int32_t passes, int& launches,
-                         float* corrections = nullptr);  // [4]: each pass's max correction
+                         float* corrections = nullptr,  // [4]: each pass's max correction
+                         const mml_ctx* sync = nullptr);
 
 // XCD-owned item groups (xcd.hip): items dealt into 8 groups of equal weight, a stream partitioned
 // (stable) by the group of its item; group g's span goff[g] .. goff[g + 1] is served by blocks
@@ -218,6 +224,40 @@ std::vector<int64_t> device_id_counts(hipStream_t st, const int32_t* ids, int64_
 
 struct mml_ctx;
 namespace mml {
+// Collectives of a context that lists a device more than once (peer.hip).  peer_average: arrays
+// arr[d][a] of shard d (on ctxs[d]), count[a] floats each, replaced on every shard by their
+// average over the shards (sum in shard order, then / N), staged on shard 0's device; ev0 / ev1
+// bracket it on shard 0's stream and every other shard's stream waits on ev1.
+void peer_average(const std::vector<mml_ctx*>& ctxs, const std::vector<std::vector<float*>>& arr,
+                  const std::vector<int64_t>& count, DeviceArray<float>& stage, hipEvent_t ev0,
+                  hipEvent_t ev1);
+// The ranks of such a context when each runs on a host thread of its own (mml::on_devices): host
+// barriers in place of a communicator.
+struct PeerGroup {
+    int32_t n;
+    std::vector<int32_t> devices;  // device of each rank
+    explicit PeerGroup(int32_t n);
+    ~PeerGroup();
+    PeerGroup(const PeerGroup&) = delete;
+    PeerGroup& operator=(const PeerGroup&) = delete;
+    // throws when a rank aborted (its call failed): the others then leave instead of waiting
+    void barrier();
+    void abort();  // by a failing rank
+    void reset();  // before the ranks start a call (no rank inside the group)
+    // every rank's rows [bounds[r], bounds[r + 1]) of W [rows x k] copied into every other rank's
+    // W (W = the same matrix of each rank's handle); called by all ranks
+    void allgather_rows(const mml_ctx* ctx, float* W, const std::vector<int64_t>& bounds,
+                        int32_t k);
+    // v[0 .. m) <- max over the ranks (m <= 4); called by all ranks
+    void max_u32(const mml_ctx* ctx, uint32_t* v, int32_t m);
+
+  private:
+    struct Impl;
+    Impl* impl;
+    std::vector<void*> ptr;
+    std::vector<uint32_t> u32;
+};
+
 // Hogwild flushing waves per XCD: wave 0 of that many evenly spaced blocks of an XCD group writes
 // the L2's dirty lines back after each batch of 64 updates (MML_FLUSHERS overrides the kernel's
 // default: BiasedMF 1, BPR 4 -- measured in DESIGN.md)
@@ -233,9 +273,13 @@ struct mml_ctx {
     std::vector<mml_ctx*> sub;
     bool multi() const { return !sub.empty(); }
     // a device id listed more than once (several shards on one GPU): no communicator is built;
-    // BiasedMF moves data with peer copies instead (the DSGD ring; the user shards' item
-    // averaging), the other handles refuse such a context
+    // the handles move data with peer copies instead (BiasedMF's DSGD ring; the BiasedMF / BPRMF
+    // user shards' item averaging, mml::peer_average; WRMF's row all-gather through `peers`)
     bool repeated = false;
+    // a repeated context's ranks (owned by the parent, shared by its sub-contexts): sub-context d
+    // is rank peer_rank = d of `peers`
+    std::shared_ptr<mml::PeerGroup> peers;
+    int32_t peer_rank = 0;
     int32_t device = 0;
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;
@@ -281,13 +325,6 @@ void on_devices(const mml_ctx* ctx, F&& f) {
     for (size_t d = 0; d < n; ++d)
         if (st[d] != MML_OK)
             fail(st[d], "device " + std::to_string(ctx->sub[d]->device) + ": " + msg[d]);
-}
-
-// the collectives of the user-sharded Hogwild handles need one communicator over distinct devices
-inline void require_comm(const mml_ctx* ctx) {
-    if (ctx->repeated)
-        fail(MML_ERR_STATE, "a multi-device context that lists a device more than once has no "
-                            "communicator: only the BiasedMF DSGD schedule runs on it");
 }
 
 // contiguous user ranges [b[d], b[d + 1]) with balanced rating counts (the multi-device shards;

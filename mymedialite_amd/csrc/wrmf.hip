@@ -609,7 +609,17 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
     wrmf_gram_reduce_kernel<<<(k * k + 255) / 256, 256, 0, st>>>(h->partial.get(), nparts, k,
                                                                   h->HH.get());
     launches += 2;
-    if (r1 <= r0) return;
+    const bool tiles_path = k > 128 && !use_blocked_solver();
+    if (r1 <= r0) {
+        // a rank without rows in this half still joins the ranks' refinement decisions
+        if (tiles_path && !plan_in) {
+            mml::WrmfTilePlan& plan = W == h->U.get() ? h->uplan : h->iplan;
+            mml::wrmf_tile_refine(st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha,
+                                  h->p.regularization, h->p.refine_passes, launches, nullptr,
+                                  h->ctx);
+        }
+        return;
+    }
     if (k <= kMaxK) {
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(r1 - r0, 256 * 16));
         wrmf_solve_kernel<<<grid, 256, 0, st>>>(off, cols, n_data_rows, r0, r1, W, H, h->HH.get(),
@@ -625,16 +635,23 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
                              h->p.regularization, launches);
         const int32_t done = mml::wrmf_tile_refine(
             st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha, h->p.regularization,
-            h->p.refine_passes, launches, h->last_corr + (W == h->U.get() ? 0 : 4));
+            h->p.refine_passes, launches, h->last_corr + (W == h->U.get() ? 0 : 4),
+            plan_in ? nullptr : h->ctx);
         h->last_refine = std::max(h->last_refine, done);
     }
     MML_HIP(hipGetLastError());
     launches += 1;
 }
 
-// all-gather of the row shards of W [rows x k] in place: one broadcast per rank, grouped
+// all-gather of the row shards of W [rows x k] in place: one broadcast per rank, grouped (a
+// repeated-device context: peer copies between the ranks' threads, peer.hip)
 void allgather_rows(mml_wrmf* h, float* W, const std::vector<int64_t>& b) {
     mml_ctx* c = h->ctx;
+    if (!c->comm) {
+        MML_REQUIRE(c->peers, "row shards without a communicator or peer group");
+        c->peers->allgather_rows(c, W, b, h->k);
+        return;
+    }
     MML_RCCL(ncclGroupStart());
     for (int r = 0; r < c->nranks; ++r) {
         const size_t cnt = (size_t)(b[r + 1] - b[r]) * h->k;
@@ -647,8 +664,9 @@ void allgather_rows(mml_wrmf* h, float* W, const std::vector<int64_t>& b) {
 
 // (re)derive the shards for the context's communicator and the row plans of this rank
 void ensure_shards(mml_wrmf* h) {
-    const int32_t nr = h->ctx->comm ? h->ctx->nranks : 1;
-    const int32_t rk = h->ctx->comm ? h->ctx->rank : 0;
+    const mml_ctx* c = h->ctx;
+    const int32_t nr = c->comm ? c->nranks : c->peers ? c->peers->n : 1;
+    const int32_t rk = c->comm ? c->rank : c->peers ? c->peer_rank : 0;
     if (nr == h->shard_nranks && rk == h->shard_rank) return;
     h->ub = mml::balanced_rows(h->udeg, h->k, nr);
     h->ib = mml::balanced_rows(h->ideg, h->k, nr);
@@ -683,7 +701,6 @@ extern "C" mml_status mml_wrmf_create(mml_ctx* ctx, const mml_wrmf_params* param
         MML_REQUIRE(params->num_factors >= 1 && params->num_factors <= 256,
                     "num_factors must be in [1, 256]");
         if (ctx->multi()) {
-            mml::require_comm(ctx);
             auto* h = new mml_wrmf();
             h->ctx = ctx;
             h->p = *params;
@@ -895,8 +912,12 @@ extern "C" mml_status mml_wrmf_iterate(mml_wrmf* h) {
         MML_REQUIRE(h && h->ctx, "null handle");
         if (h->ctx->multi()) {  // every device solves its row shards; all-gathers inside
             std::vector<float> ms(h->shards.size(), 0.0f);
+            // a repeated device: the shards are the ranks of a peer group (one thread each)
+            mml::PeerGroup* g = h->shards[0]->ctx->peers.get();
+            if (g) g->reset();
             mml::on_devices(h->ctx, [&](int32_t d) {
                 const mml_status st = mml_wrmf_iterate(h->shards[d]);
+                if (st != MML_OK && g) g->abort();  // the other ranks leave their barriers
                 ms[d] = h->shards[d]->last_ms;
                 return st;
             });

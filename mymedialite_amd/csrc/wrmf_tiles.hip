@@ -2550,15 +2550,41 @@ constexpr float kRefineStopWood = 2e-6f;
 int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float* H,
                          int64_t h_rows, const int64_t* off, const int32_t* cols, const double* HH,
                          int32_t k, double alpha, double reg, int32_t passes, int& launches,
-                         float* corrections) {
+                         float* corrections, const mml_ctx* sync) {
     const int64_t n = p.r1 - p.r0, n_w = (int64_t)(p.r1);  // W rows addressed up to r1
-    if (passes <= 0 || n <= 0) return 0;
+    // row shards over several ranks take each "another pass?" decision together (the max over
+    // the ranks of the last correction), so the sharded model is the one-rank model bit for bit
+    const bool rccl = sync && sync->comm && sync->nranks > 1;
+    const bool peers = sync && sync->peers && sync->peers->n > 1;
+    if (passes <= 0 || (n <= 0 && !rccl && !peers)) return 0;
+    if (!p.ws->dmax.get()) p.ws->dmax.alloc(2);
+    auto largest = [&](float d[2]) {  // this pass's corrections, combined over the ranks
+        unsigned bits[2] = {0, 0};
+        if (rccl)
+            MML_RCCL(ncclAllReduce(p.ws->dmax.get(), p.ws->dmax.get(), 2, ncclUint32, ncclMax,
+                                   sync->comm, st));
+        MML_HIP(hipMemcpyAsync(bits, p.ws->dmax.get(), sizeof(bits), hipMemcpyDeviceToHost, st));
+        MML_HIP(hipStreamSynchronize(st));
+        if (peers) sync->peers->max_u32(sync, bits, 2);
+        std::memcpy(d, bits, sizeof(bits));
+    };
+    auto stop = [](const float d[2]) {
+        return !(d[0] > kRefineStopDirect) && !(d[1] > kRefineStopWood);
+    };
+    if (n <= 0) {  // a rank without rows still joins every decision
+        for (int32_t pass = 0; pass + 1 < passes; ++pass) {
+            MML_HIP(hipMemsetAsync(p.ws->dmax.get(), 0, 2 * sizeof(unsigned), st));
+            float d[2];
+            largest(d);
+            if (stop(d)) break;
+        }
+        return 0;
+    }
     p.ws->x64.reserve((size_t)n * k);
     p.ws->r64.reserve((size_t)n * k);
     p.ws->rf.reserve((size_t)n_w * k);
     p.ws->df.reserve((size_t)n_w * k);
     p.ws->rpartial.reserve(std::max<int64_t>(1, p.n_rslots) * (size_t)k);
-    if (!p.ws->dmax.get()) p.ws->dmax.alloc(2);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n * k + 255) / 256, 16384));
     auto rows = [&](int op) {
         wrmf_refine_rows_kernel<<<grid, 256, 0, st>>>(op, p.r0, n, k, W, p.ws->x64.get(),
@@ -2594,14 +2620,10 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
         launches += 3;
         ++done;
         if (pass + 1 < passes) {  // another pass only while the correction was large
-            unsigned bits[2] = {0, 0};
-            MML_HIP(hipMemcpyAsync(bits, p.ws->dmax.get(), sizeof(bits), hipMemcpyDeviceToHost,
-                                   st));
-            MML_HIP(hipStreamSynchronize(st));
             float d[2];
-            std::memcpy(d, bits, sizeof(d));
+            largest(d);
             if (corrections && pass < 4) corrections[pass] = std::max(d[0], d[1]);
-            if (!(d[0] > kRefineStopDirect) && !(d[1] > kRefineStopWood)) break;
+            if (stop(d)) break;
         }
     }
     rows(3);

@@ -300,6 +300,12 @@ class DeviceRatingFile:
                  ignore_first_line=False, n_threads=8, with_ratings=True):
         import ctypes
         from . import _native as N
+        # the native file points at the context (its HBM, its device): keep the Context alive
+        # while the file is open, and let Context.close() close the file first
+        self._h = None
+        self._ctx = device
+        if device is not None and not getattr(device, "handle", None):
+            raise ValueError("DeviceRatingFile needs an open Context")
         self.user_mapping = user_mapping or IdentityMapping()
         self.item_mapping = item_mapping or IdentityMapping()
         flags = (N.READ_IGNORE_FIRST_LINE if ignore_first_line else 0) | \
@@ -313,10 +319,14 @@ class DeviceRatingFile:
                                                       ctypes.byref(v), ctypes.byref(dp)))
         self.users_ptr, self.items_ptr, self.values_ptr = u.value, i.value, v.value
         self.device_parsed = dp.value
+        if device is not None and hasattr(device, "_dependents"):
+            device._dependents.add(self)
 
     def to_host(self):
         """(users, items, values) copied from HBM."""
         from . import _native as N
+        if not self._h:
+            raise RuntimeError("the DeviceRatingFile is closed")
         users = np.empty(self.count, np.int32)
         items = np.empty(self.count, np.int32)
         values = np.empty(self.count, np.float32)
@@ -325,10 +335,14 @@ class DeviceRatingFile:
         return users, items, values
 
     def close(self):
-        if self._h:
+        """Releases the file's device arrays (before its Context: mml_rating_file keeps a pointer
+        to it); the device pointers are invalid afterwards."""
+        if getattr(self, "_h", None):
             from . import _native as N
             N.lib().mml_rating_file_destroy(self._h)
             self._h = None
+            self.users_ptr = self.items_ptr = self.values_ptr = None
+        self._ctx = None
 
     def __del__(self):
         try:

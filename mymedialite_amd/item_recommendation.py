@@ -157,6 +157,16 @@ class _MFBase(Recommender):
             pass
 
 
+def _single_device_only(rec):
+    """The incremental updates (mml_bpr_apply_triples_flags / mml_bpr_set_rows /
+    mml_wrmf_retrain) run on a single-device handle: refused up front on a multi-device context,
+    before the feedback or the model changes."""
+    ctx = rec._ctx
+    if ctx is not None and isinstance(ctx.device, (list, tuple)):
+        raise NotImplementedError("incremental updates run on a single-device handle (Device), "
+                                  "not on a multi-device context (Gpus)")
+
+
 class BPRMF(_MFBase):
     PROPERTIES = {
         "BiasReg": "float", "Device": "int", "Gpus": "string", "InitMean": "double", "InitStdDev": "double",
@@ -368,6 +378,7 @@ class BPRMF(_MFBase):
         take the default (uniform user) samplers; checked before anything changes."""
         if self._h is None:
             raise RuntimeError("Train() or load_model() first")
+        _single_device_only(self)
         if self._sampler() == N.BPR_SAMPLER_UNIFORM_PAIR:
             raise NotImplementedError("AddFeedback / RemoveFeedback with UniformUserSampling = "
                                       "false: the RandomIndex redraw is not restated")
@@ -671,6 +682,7 @@ class WRMF(_MFBase):
         repeated id changes nothing (its second solve equals its first)."""
         if self._h is None:
             raise RuntimeError("Train() or load_model() first")
+        _single_device_only(self)
         rows = list(dict.fromkeys(int(x) for x in ids))
         if not rows:
             return
@@ -706,6 +718,9 @@ class WRMF(_MFBase):
         (MF.AddUser / AddItem, :108-122: AddRows, then RowInitNormal of that row from the shared
         RNG), the pair is added to Feedback; then RetrainUser for the users and RetrainItem for
         the items of the batch (HashSet insertion order)."""
+        if self._h is None:
+            raise RuntimeError("Train() or load_model() first")
+        _single_device_only(self)
         users = [int(x) for x in np.atleast_1d(users)]
         items = [int(x) for x in np.atleast_1d(items)]
         m = self.get_model()
@@ -732,6 +747,9 @@ class WRMF(_MFBase):
         """MF.RemoveFeedback (MF.cs:93-99) over IncrementalItemRecommender.RemoveFeedback
         (:56-71): ids beyond the model raise; every occurrence of each pair leaves Feedback
         (PosOnlyFeedback.Remove); then the users and items are retrained."""
+        if self._h is None:
+            raise RuntimeError("Train() or load_model() first")
+        _single_device_only(self)
         users = [int(x) for x in np.atleast_1d(users)]
         items = [int(x) for x in np.atleast_1d(items)]
         for u, i in zip(users, items):

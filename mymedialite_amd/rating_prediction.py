@@ -286,8 +286,7 @@ class MatrixFactorization(Recommender):
         its NumIter Iterate(ByUser[u] / ByItem[i]) calls, computed here in the reference's order;
         the device trains all rows at once (the other side is fixed, so they are independent).
         An id listed twice is retrained twice by the reference: the last retraining decides."""
-        if self._h is None:
-            raise RuntimeError("Train() or load_model() first")
+        self._check_incremental()
         ids = [int(x) for x in ids]
         if not ids:
             return
@@ -376,13 +375,28 @@ class MatrixFactorization(Recommender):
         self._host = None
         self.current_learnrate = lr
 
+    def _check_incremental(self):
+        """The incremental updates retrain rows through mml_bmf_retrain, which serves
+        MatrixFactorization and BiasedMatrixFactorization on a single-device handle.  Checked
+        before anything changes, so a refused call leaves the ratings and the model as they were
+        (the subclasses' own RetrainUser paths, e.g. SocialMF's, are not restated)."""
+        if self._h is None:
+            raise RuntimeError("Train() or load_model() first")
+        if self.MODEL not in (N.MF_PLAIN, N.MF_BIASED):
+            raise NotImplementedError(f"{type(self).__name__}: incremental updates (AddRatings / "
+                                      f"UpdateRatings / RemoveRatings, RetrainUser / RetrainItem) "
+                                      f"are implemented for MatrixFactorization and "
+                                      f"BiasedMatrixFactorization only")
+        if self._ctx is not None and isinstance(self._ctx.device, (list, tuple)):
+            raise NotImplementedError("incremental updates run on a single-device handle "
+                                      "(Device), not on a multi-device context (Gpus)")
+
     def add_ratings(self, new: Ratings):
         """AddRatings (MatrixFactorization.cs:262-270 over IncrementalRatingPredictor.cs:40-51):
         new users / items grow the model, the ratings are appended (Ratings.Add), then RetrainUser
         for every user and RetrainItem for every item of ``new`` in first-appearance order
         (DataSet.AllUsers / AllItems: a HashSet's insertion order)."""
-        if self._h is None:
-            raise RuntimeError("Train() or load_model() first")
+        self._check_incremental()
         self._grow(new.max_user_id, new.max_item_id)
         self._ratings.add(new.users, new.items, new.values)
         self._order_uploaded = False  # the next Iterate() uploads the grown set (RandomIndex anew)
@@ -393,6 +407,7 @@ class MatrixFactorization(Recommender):
         """UpdateRatings (MatrixFactorization.cs:272-280 over IncrementalRatingPredictor.cs:
         54-68): each (user, item) must exist (Ratings.TryGetIndex: its first index); its value is
         replaced, then the users and the items are retrained."""
+        self._check_incremental()
         self._ratings.update(new.users, new.items, new.values)
         self._order_uploaded = False
         self.retrain_users(_first_appearance(new.users))
@@ -402,6 +417,7 @@ class MatrixFactorization(Recommender):
         """RemoveRatings (MatrixFactorization.cs:282-290 over IncrementalRatingPredictor.cs:
         71-78): the first index of each existing (user, item) is removed (Ratings.RemoveAt), then
         every user and item of ``gone`` is retrained."""
+        self._check_incremental()
         self._ratings.remove(gone.users, gone.items)
         self._order_uploaded = False
         self.retrain_users(_first_appearance(gone.users))

@@ -122,3 +122,86 @@ def c4_chunks(rank: int, world: int, n_total: int, n_users: int, n_items: int, n
                 d[x * cnt:(x + 1) * cnt] = p_
             del part
     return out, test, (mine[0] * n_users // chunks, (mine[-1] + 1) * n_users // chunks)
+
+
+def c3_chunks(rank: int, world: int, n_total: int, n_users: int, n_items: int, device,
+              chunks: int = 64):
+    """C3's events (BPRMF 10M users x 1M items, 500M positives, Zipf(0.8) items) as
+    64 user-range chunks: chunk c holds users [c U/64, (c+1) U/64) uniform, items Zipf(0.8) over one
+    shared permutation, n_total/64 events, seed 2000 + c.  Rank r of N holds chunks
+    [r 64/N, (r+1) 64/N), so the data set is the same at every N.  Returns (users, items, (u_lo,
+    u_hi)) as int32 torch tensors on `device`."""
+    import torch
+    assert chunks % world == 0, "world size must divide 64"
+    per = n_total // chunks
+    mine = range(rank * chunks // world, (rank + 1) * chunks // world)
+    gp = torch.Generator(device=device)
+    gp.manual_seed(2)
+    perm = torch.randperm(n_items, generator=gp, device=device)
+    cdf = torch.from_numpy(zipf_cdf(n_items, 0.8)).to(device)
+    users = torch.empty(per * len(mine), dtype=torch.int32, device=device)
+    items = torch.empty(per * len(mine), dtype=torch.int32, device=device)
+    for x, c in enumerate(mine):
+        g = torch.Generator(device=device)
+        g.manual_seed(2000 + c)
+        lo, hi = c * n_users // chunks, (c + 1) * n_users // chunks
+        for s0 in range(0, per, 1 << 26):
+            e = min(per, s0 + (1 << 26))
+            o = x * per
+            users[o + s0:o + e] = torch.randint(lo, hi, (e - s0,), generator=g, device=device,
+                                                dtype=torch.int32)
+            r = torch.rand(e - s0, generator=g, device=device, dtype=torch.float64)
+            items[o + s0:o + e] = perm[torch.searchsorted(cdf, r).clamp_(max=n_items - 1)].to(
+                torch.int32)
+    return users, items, (mine[0] * n_users // chunks, (mine[-1] + 1) * n_users // chunks)
+
+
+def c3_holdout(users, items, n_users: int, user_range, n_test_users: int = 100_000,
+               seed: int = 2):
+    """SURVEY 8(d)'s C3 evaluation split: 100k test users sampled over all users (seed 2); each
+    keeps the item of its first event in the stream as its one held-out positive, and every event
+    of that (user, item) pair leaves the training data (else it would be a training item, which
+    Eval.Items ignores, Items.cs:126-209).  Only the test users inside `user_range` (this rank's
+    chunks) are taken, so N ranks split the same 100k users.  Returns (train users, train items,
+    test users (sorted, int32 numpy), their held-out items (int32 numpy))."""
+    import torch
+    dev = users.device
+    rs = np.random.default_rng(seed)
+    test_all = np.sort(rs.choice(n_users, n_test_users, replace=False)).astype(np.int64)
+    lo, hi = user_range
+    test = test_all[(test_all >= lo) & (test_all < hi)]
+    is_test = torch.zeros(n_users, dtype=torch.bool, device=dev)
+    tt = torch.from_numpy(test).to(dev)
+    is_test[tt] = True
+    sel = is_test[users.long()]
+    pos = torch.nonzero(sel).squeeze(1)
+    first = torch.full((n_users,), users.numel(), dtype=torch.int64, device=dev)
+    first.scatter_reduce_(0, users[pos].long(), pos, reduce="amin")
+    held = torch.full((n_users,), -1, dtype=torch.int32, device=dev)
+    has = first[tt] < users.numel()  # a test user without events keeps no test item
+    held[tt[has]] = items[first[tt[has]]]
+    keep = ~(sel & (items == held[users.long()]))
+    del sel, pos, first
+    tu = test[has.cpu().numpy()].astype(np.int32)
+    ti = held[tt[has]].cpu().numpy().astype(np.int32)
+    return users[keep], items[keep], tu, ti
+
+
+def c5_events(n_users: int, n_items: int, per_user: int, device, seed: int = 5):
+    """C5's events (WRMF k=256, 5M users x 500k items, 500M positives): per_user
+    events per user (user u owns events [u per_user, (u+1) per_user)), items Zipf(0.8) over a random
+    permutation, seed 5; generated in HBM, duplicates kept (the sets are built from them).
+    Returns (users, items) int32 torch tensors on `device`."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    n = n_users * per_user
+    cdf = torch.from_numpy(zipf_cdf(n_items, 0.8)).to(device)
+    perm = torch.randperm(n_items, generator=g, device=device)
+    users = (torch.arange(n, device=device, dtype=torch.int64) // per_user).to(torch.int32)
+    items = torch.empty(n, dtype=torch.int32, device=device)
+    for s0 in range(0, n, 1 << 26):
+        e = min(n, s0 + (1 << 26))
+        x = torch.rand(e - s0, generator=g, device=device, dtype=torch.float64)
+        items[s0:e] = perm[torch.searchsorted(cdf, x).clamp_(max=n_items - 1)].to(torch.int32)
+    return users, items

@@ -280,11 +280,13 @@ def bmf_train(users, items, values, n_users, n_items, min_rating, max_rating, *,
               learn_rate=0.01, decay=1.0, reg_u=0.015, reg_i=0.015, bias_reg=0.01,
               bias_learn_rate=1.0, num_iter=30, init_mean=0.0, init_stddev=0.1, loss=0,
               frequency_regularization=False, max_threads=1, naive_parallelization=False,
-              bold_driver=False, rng=None, callback=None):
+              bold_driver=False, rng=None, callback=None, order=None):
     """BiasedMatrixFactorization.Train() (:173-194) and NumIter x Iterate() (:197-222).
 
     Returns a dict with the model and the RNG-derived schedule (so a GPU run can be fed the
     identical RandomIndex / DSGD blocks). ``callback(epoch, state)`` after every epoch.
+    ``order``: a visit order to use instead of the RNG's shuffle (the same InitModel with
+    another permutation: the order noise of the sequential loop, for the Hogwild bands).
     """
     users, items, values = i32(users), i32(items), f32(values)
     rng = rng if rng is not None else Rng(seed)
@@ -326,7 +328,7 @@ def bmf_train(users, items, values, n_users, n_items, min_rating, max_rating, *,
 
     blocks = None
     lists = None
-    random_index = None
+    random_index = None if order is None else i32(order)
     if max_threads > 1:
         if naive_parallelization:
             random_index = rng.shuffle(np.arange(len(users), dtype=np.int32))
@@ -870,3 +872,36 @@ def item_eval_auc(U, V, bias, train_users, train_items, test_users, test_items, 
         n_items_total, U.shape[0] - 1, V.shape[0] - 1, U.shape[1], _p(f32(U), _f32p),
         _p(f32(V), _f32p), _p(b, _f32p), ctypes.byref(nu))
     return float(auc), int(nu.value)
+
+
+def wrmf_rows_check(rows, row_ids, col_ids, W, H, k, alpha=1.0, reg=0.015):
+    """Checker for a library WRMF half-step at full size (the oracle solves only the sampled rows):
+    rows = sorted row ids; row_ids / col_ids = the distinct (row, col) entries of the half's CSR
+    (torch tensors on the GPU, or numpy); W = the library's solved rows' matrix, H = the matrix it
+    solved from.  Each sampled row is solved by WRMF.Optimize(u) (WRMF.cs:110-156) in fp64 with
+    exact float products (ora_wrmf_optimize_rows_exact), HH = H^T H in fp64 (on the GPU when H is
+    large).  Returns per-row max |W_lib - W_oracle| / (1 + max |W_oracle|)."""
+    import torch
+    rows = np.asarray(rows, np.int64)
+    dev = row_ids.device if isinstance(row_ids, torch.Tensor) else torch.device("cpu")
+    Ht = torch.from_numpy(np.ascontiguousarray(H)).to(dev, torch.float64)
+    HH = (Ht.T @ Ht).cpu().numpy()
+    del Ht
+    r_t = row_ids if isinstance(row_ids, torch.Tensor) else torch.from_numpy(row_ids)
+    c_t = col_ids if isinstance(col_ids, torch.Tensor) else torch.from_numpy(col_ids)
+    n_rows = int(max(int(r_t.max().item()) + 1, rows.max() + 1))
+    mask = torch.zeros(n_rows, dtype=torch.bool, device=dev)
+    mask[torch.from_numpy(rows).to(dev)] = True
+    m = mask[r_t.long()]
+    r_, c_ = r_t[m].cpu().numpy(), c_t[m].cpu().numpy()
+    o = np.argsort(r_, kind="stable")
+    r_, c_ = r_[o], i32(c_[o])
+    off = np.zeros(len(rows) + 1, np.int64)
+    off[1:] = np.cumsum(np.searchsorted(r_, rows, side="right") -
+                        np.searchsorted(r_, rows, side="left"))
+    Wr = np.zeros((len(rows), k), np.float32)
+    lib().ora_wrmf_optimize_rows_exact(_p(off, _i64p), _p(c_, _i32p), 0, len(rows), len(rows),
+                                       _p(Wr, _f32p), _p(f32(H), _f32p), _p(HH, _f64p), k,
+                                       float(alpha), float(reg))
+    got = np.asarray(W)[rows]
+    return np.abs(got - Wr).max(1) / (1.0 + np.abs(Wr).max(1))

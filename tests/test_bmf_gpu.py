@@ -188,37 +188,29 @@ def test_hogwild_statistical_parity_c2_shape():
     u, i, v = (t.numpy() for t in planted_ratings_torch(nu, ni, n + 100_000, seed=5, device="cpu"))
     tu, ti, tv = u[n:], i[n:], v[n:]
     u, i, v = u[:n].copy(), i[:n].copy(), v[:n].copy()
-    r = Ratings(u, i, v)
-    ref = []
-    gb = O.global_bias(v, r.scale_min, r.scale_max)
-
-    def cb(e, st):
-        p = O.bmf_predict(tu, ti, st["U"], st["V"], st["bu"], st["bi"], gb,
-                          np.float32(r.scale_min), np.float32(r.scale_max - r.scale_min))
-        ref.append(O.rating_eval(p, tv)[0])
-
-    O.bmf_train(u, i, v, r.max_user_id + 1, r.max_item_id + 1, r.scale_min, r.scale_max, seed=1,
-                k=64, num_iter=2, callback=cb)
+    from test_edge_cases_gpu import hogwild_band, order_noise
+    # the sequential oracle's order noise after 1 and 2 epochs (same InitModel, three other
+    # shuffles), on the held-out ratings
+    noise = [order_noise(u, i, v, seed=1, k=64, num_iter=e, eval_set=(tu, ti, tv))
+             for e in (1, 2)]
     res = {}
     for name, props in (("hogwild", dict(Schedule="hogwild")),
                         ("hogwild_coherent", dict(Schedule="hogwild_coherent")),
                         ("hogwild_multi1", dict(Schedule="hogwild", Gpus="0"))):
         m, _ = gpu_train(u, i, v, seed=1, k=64, num_iter=0, **props)
-        got = []
-        for _ in range(2):
+        ok = []
+        for e in range(2):
             m.iterate()
-            got.append(m.evaluate(Ratings(tu, ti, tv))["RMSE"])
-        res[name] = got
-    for name, got in res.items():
-        print(f"C2-shape test RMSE {name}: {got[0]:.6f} / {got[1]:.6f} vs oracle "
-              f"{ref[0]:.6f} / {ref[1]:.6f}: delta {got[0] - ref[0]:+.2e} / {got[1] - ref[1]:+.2e}")
+            p = m.predict(tu, ti).astype(np.float64)
+            rmse = float(np.sqrt(np.mean((p - tv) ** 2)))
+            ok.append(hogwild_band(f"C2-shape {name} epoch {e + 1} (test set)", rmse, p,
+                                   *noise[e]))
+        res[name] = ok
     # Hogwild on XCD-owned item groups (xcd.hip; every item row cached in ONE XCD's L2, users
-    # written through, one flushing wave per XCD; DESIGN.md section 3 measured 3.0e-4 / 2.5e-4;
-    # the round-1 spread over all XCDs, whose L2s held replicas of the hot rows, 1.0e-2 / 8e-3);
-    # the same kernel behind a one-shard multi-device context (Gpus=0, the user-shard path with
-    # its 1-rank ncclAvg) and the coherent schedule (only in-flight staleness, ~3e-4) -> 1e-3
-    for name, got in res.items():
-        assert all(abs(a - b) <= 1e-3 for a, b in zip(got, ref)), (name, res, ref)
+    # written through, one flushing wave per XCD), the same kernel behind a one-shard
+    # multi-device context (Gpus=0) and the coherent schedule: within 3x the sequential loop's
+    # own order noise after each epoch
+    assert all(all(v_) for v_ in res.values()), res
 
 
 def test_dsgd_many_groups_exact():

@@ -4,8 +4,8 @@
   factors and biases within 1e-5 of the oracle after each epoch (the reference's own loop,
   BiasedMatrixFactorization.cs:264-310).
 * HOGWILD at every lanes-per-rating variant the kernel selects (k = 1 .. 256) on a set large enough
-  for the multi-workgroup, XCD-grouped path: train RMSE after 2 epochs within 1e-2 of the oracle's
-  sequential loop (statistical parity; the measured offsets are printed: +1.9e-3 .. +4.3e-3).
+  for the multi-workgroup, XCD-grouped path: train RMSE and mean |dpred| after 2 epochs within 3x
+  the sequential oracle's own order noise (the same InitModel over three other shuffles; printed).
 * Degenerate data: no ratings at all (Iterate is a no-op), every rating on one user (one hot user
   row under Hogwild), ratings whose chunk ends are ragged (n not a multiple of 64).
 * Argument errors come back as MML_ERR_ARG, never as a device fault: k outside 1 .. 256, negative
@@ -64,26 +64,53 @@ def _planted(seed, n_users, n_items, n, rank=4):
     return u, i, v
 
 
+def order_noise(u, i, v, *, seed, k, num_iter, eval_set, perm_seeds=(101, 102, 103), **kw):
+    """The sequential oracle's own order noise: the same InitModel (seed) trained over three other
+    RandomIndex permutations (BiasedMatrixFactorization.cs:264-310 run on a different shuffle,
+    Data/DataSet.cs:100-110).  Returns (the oracle on the reference's own shuffle: (RMSE, preds)
+    on eval_set, the largest pairwise |dRMSE| over the three, the largest pairwise mean |dpred|)."""
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    r = Ratings(u, i, v)
+    eu, ei, ev = eval_set
+
+    def run(order):
+        st = O.bmf_train(u, i, v, nu, ni, r.scale_min, r.scale_max, seed=seed, k=k,
+                         num_iter=num_iter, order=order, **kw)
+        p = O.bmf_predict(eu, ei, st["U"], st["V"], st["bu"], st["bi"], st["global_bias"],
+                          st["min_rating"], st["range_"]).astype(np.float64)
+        return float(np.sqrt(np.mean((p - ev) ** 2))), p
+    ref = run(None)
+    runs = [run(np.random.default_rng(s_).permutation(len(u)).astype(np.int32))
+            for s_ in perm_seeds]
+    d_rmse = max(abs(a[0] - b[0]) for x, a in enumerate(runs) for b in runs[x + 1:])
+    d_pred = max(float(np.mean(np.abs(a[1] - b[1]))) for x, a in enumerate(runs)
+                 for b in runs[x + 1:])
+    return ref, d_rmse, d_pred
+
+
+def hogwild_band(name, rmse, pred, ref, d_rmse, d_pred):
+    """GPU Hogwild against the sequential oracle, held to 3x the oracle's own
+    order noise (|dRMSE| and mean |dpred|); the sign of dRMSE is printed (+ = Hogwild worse)."""
+    dr = rmse - ref[0]
+    mad = float(np.mean(np.abs(pred - ref[1])))
+    print(f"{name}: RMSE gpu {rmse:.6f} oracle {ref[0]:.6f} delta {dr:+.2e} (order noise "
+          f"{d_rmse:.2e}, ratio {abs(dr) / max(d_rmse, 1e-12):.2f}); mean |dpred| {mad:.3e} "
+          f"(order noise {d_pred:.3e}, ratio {mad / max(d_pred, 1e-12):.2f})")
+    return abs(dr) <= 3 * d_rmse and mad <= 3 * d_pred
+
+
 @pytest.mark.parametrize("k", [1, 8, 64, 100, 256])
 def test_hogwild_lane_variants_statistical(k):
     # 300 k ratings: >= 16 waves' worth, so the XCD-grouped multi-workgroup kernel runs
     u, i, v = _planted(90 + k, 3000, 800, 300_000)
-    nu, ni = int(u.max()) + 1, int(i.max()) + 1
-    r = Ratings(u, i, v)
-    st = O.bmf_train(u, i, v, nu, ni, r.scale_min, r.scale_max, seed=2, k=k, num_iter=2)
-    ref = O.bmf_predict(u, i, st["U"], st["V"], st["bu"], st["bi"], st["global_bias"],
-                        st["min_rating"], st["range_"]).astype(np.float64)
-    rmse_ref = float(np.sqrt(np.mean((ref - v) ** 2)))
+    ref, d_rmse, d_pred = order_noise(u, i, v, seed=2, k=k, num_iter=2, eval_set=(u, i, v))
     m = _train(u, i, v, seed=2, k=k, num_iter=2, Schedule="hogwild")
     pred = m.predict(u, i).astype(np.float64)
     rmse = float(np.sqrt(np.mean((pred - v) ** 2)))
-    mad = float(np.mean(np.abs(pred - ref)))
-    print(f"hogwild k={k}: train RMSE gpu {rmse:.5f} oracle {rmse_ref:.5f} "
-          f"delta {rmse - rmse_ref:+.2e}, mean |pred - oracle pred| {mad:.2e}")
     assert np.isfinite(m.user_factors).all() and np.isfinite(m.item_factors).all()
-    # measured +1.9e-3 .. +4.3e-3 (profiles/r3zf_pytest_edge_retrain.log); the per-rating trajectories
-    # differ (the XCD-grouped visit order), so only the statistic is compared
-    assert abs(rmse - rmse_ref) <= 1e-2
+    # the per-rating trajectories differ (Hogwild's interleaving and the XCD-grouped visit
+    # order): held to the spread three other shuffles give the sequential loop itself
+    assert hogwild_band(f"hogwild k={k} (train set)", rmse, pred, ref, d_rmse, d_pred)
 
 
 def test_no_ratings_iterate_is_a_noop():

@@ -207,18 +207,151 @@ def test_bmf_dsgd_ring_matches_oracle():
 
 
 def test_repeated_device_context_limits():
-    """A context listing a device twice has no communicator: BPR's user shards (which average
-    through RCCL) refuse it, and the ring needs MaxThreads divisible by the devices."""
+    """The DSGD ring on a context listing a device twice needs MaxThreads divisible by the
+    devices."""
     u, i, v = synth_ratings(5, 200, 90, 4000)
-    with pytest.raises(N.MMLError, match="communicator"):
-        tr_u, tr_i, _, _ = planted_feedback(2, 300, 60, 8)
-        b = BPRMF(NumFactors=4, NumIter=1, Gpus="0,0")
-        b.feedback = PosOnlyFeedback(tr_u, tr_i)
-        b.train()
     with pytest.raises(N.MMLError, match="multiple of the device count"):
         m = BiasedMatrixFactorization(NumFactors=4, NumIter=1, MaxThreads=5, Gpus="0,0")
         m.ratings = Ratings(u, i, v)
         m.train()
+
+
+def _wrmf_shard_data():
+    """9,000 users with 1..200 items each (Woodbury rows <= 128 entries and direct rows past it at
+    k = 256) + item 0 held by every user (a split-Gram heavy row, > 8,192 entries)."""
+    u, i = synth_feedback(77, 9000, 600, 200)
+    u = np.concatenate([u, np.arange(9000, dtype=np.int32)])
+    i = np.concatenate([np.where(i == 0, 1, i), np.zeros(9000, np.int32)]).astype(np.int32)
+    return u, i
+
+
+_WRMF_SINGLE = {}
+
+
+@pytest.mark.parametrize("ndev,k,precision", [(2, 64, "fp64"), (4, 64, "fp64"),
+                                              (2, 256, "fp64"), (4, 256, "fp64"),
+                                              (3, 256, "fp32")])
+def test_wrmf_row_shards_equal_single_handle(ndev, k, precision):
+    """WRMF's row shards (WRMF.cs:79-92) inside libmml_hip.so at N > 1,
+    on ``ndev`` shards of one GPU (``Gpus=0,0,...``: each shard a rank on its own host thread and
+    stream, all-gathering U after the user half and V after the item half by peer copies between
+    host barriers).  Rows are independent within a half-step and every shard takes the
+    refinement's "another pass?" decision on the max over the shards, so U and V equal the
+    single-device handle's bit for bit after every iteration."""
+    u, i = _wrmf_shard_data()
+    key = (k, precision)
+    if key not in _WRMF_SINGLE:
+        snaps = []
+        Random.set_seed(6)
+        m = WRMF(NumFactors=k, NumIter=0, Precision=precision, Device=0)
+        m.feedback = PosOnlyFeedback(u, i)
+        m.train()
+        for _ in range(2):
+            m.iterate()
+            snaps.append((m.user_factors.copy(), m.item_factors.copy()))
+        _WRMF_SINGLE[key] = snaps
+    single = _WRMF_SINGLE[key]
+    Random.set_seed(6)
+    m = WRMF(NumFactors=k, NumIter=0, Precision=precision, Gpus=",".join(["0"] * ndev))
+    m.feedback = PosOnlyFeedback(u, i)
+    m.train()
+    assert m._ctx.nranks == ndev
+    for it in range(2):
+        m.iterate()
+        np.testing.assert_array_equal(m.user_factors, single[it][0], err_msg=f"iteration {it} U")
+        np.testing.assert_array_equal(m.item_factors, single[it][1], err_msg=f"iteration {it} V")
+    ran = ctypes.c_int32(0)
+    N.check(N.lib().mml_wrmf_last_refine_passes(m._h, ctypes.byref(ran), None))
+    print(f"WRMF k={k} {precision} x{ndev} shards: equal to one device, refinement passes "
+          f"{ran.value}")
+
+
+@pytest.mark.parametrize("ndev,sampler", [(2, "uniform_user"), (3, "uniform_user"),
+                                          (2, "uniform_pair")])
+def test_bpr_user_shards_ordered_equal_emulation(ndev, sampler):
+    """BPRMF's user shards + item averaging inside libmml_hip.so at N > 1 (SURVEY
+    8(e); the reference's parallel form MultiCoreBPRMF.cs:49-63, BPRMF.cs:216-226), on ``ndev``
+    shards of one GPU with the ORDERED schedule per shard.  After every epoch each shard's triples
+    (mml_bpr_last_triples, shard after shard) are replayed with the oracle's UpdateFactors
+    (BPRMF.cs:330-374) from the epoch's starting model, each shard on its own copy of V || b;
+    then V || b = (sum of the shards' copies in shard order) / N.  The library's model equals that
+    emulation bit for bit, and so do Predict and the per-user AUC routing."""
+    from mymedialite_amd.distributed import balanced_user_shards
+    tr_u, tr_i, te_u, te_i = planted_feedback(3, 1200, 300, 15)
+    nu, ni, k = 1200, 300, 16
+    kw = dict(learn_rate=0.05, reg_u=0.0025, reg_i=0.0025, reg_j=0.00025, bias_reg=0.0)
+    Random.set_seed(8)
+    m = BPRMF(NumFactors=k, NumIter=0, Schedule="ordered", Gpus=",".join(["0"] * ndev),
+              UniformUserSampling=(sampler == "uniform_user"))
+    m.feedback = PosOnlyFeedback(tr_u, tr_i)
+    m.train()
+    bnd = balanced_user_shards(np.bincount(tr_u, minlength=nu), ndev)
+    counts = [int(((tr_u >= bnd[d]) & (tr_u < bnd[d + 1])).sum()) for d in range(ndev)]
+    st = {key: val.copy() for key, val in m.get_model().items()}
+    for epoch in range(3):
+        m.iterate()
+        tu, ti, tj = m.last_triples()
+        o = 0
+        Vs, bs = [], []
+        for d in range(ndev):
+            su, si, sj = tu[o:o + counts[d]], ti[o:o + counts[d]], tj[o:o + counts[d]]
+            o += counts[d]
+            assert np.all((su >= bnd[d]) & (su < bnd[d + 1])), "a triple outside its shard"
+            V, b = st["V"].copy(), st["bias"].copy()
+            for x in range(len(su)):
+                O.bpr_update(int(su[x]), int(si[x]), int(sj[x]), st["U"], V, b, **kw)
+            Vs.append(V)
+            bs.append(b)
+        V, b = Vs[0].copy(), bs[0].copy()
+        for d in range(1, ndev):
+            V += Vs[d]
+            b += bs[d]
+        st["V"] = (V / np.float32(ndev)).astype(np.float32)
+        st["bias"] = (b / np.float32(ndev)).astype(np.float32)
+        got = m.get_model()
+        for key in ("U", "V", "bias"):
+            np.testing.assert_array_equal(got[key], st[key], err_msg=f"epoch {epoch} {key}")
+    # Predict routes each user to its shard (BPRMF.Predict :425-431: item bias + RowScalarProduct,
+    # float, left to right)
+    ref = np.empty(len(te_u), np.float32)
+    for x in range(len(te_u)):
+        acc = np.float32(0)
+        for f in range(k):
+            acc = np.float32(acc + st["U"][te_u[x], f] * st["V"][te_i[x], f])
+        ref[x] = np.float32(st["bias"][te_i[x]] + acc)
+    np.testing.assert_array_equal(m.predict(te_u, te_i), ref)
+
+
+def test_incremental_updates_refused_before_any_change():
+    """the incremental-update hooks run on single-device handles of the model families
+    mml_bmf_retrain / mml_wrmf_retrain / mml_bpr_apply_triples_flags serve; other models and
+    multi-device contexts are refused before the ratings, the feedback or the model change."""
+    from mymedialite_amd import SVDPlusPlus
+    u, i, v = synth_ratings(5, 200, 90, 4000)
+    m = SVDPlusPlus(NumFactors=4, NumIter=1)
+    m.ratings = Ratings(u, i, v)
+    m.train()
+    n0, before = m.ratings.count, m.predict(u[:50], i[:50])
+    with pytest.raises(NotImplementedError):
+        m.add_ratings(Ratings(np.array([3], np.int32), np.array([4], np.int32),
+                              np.array([5], np.float32)))
+    assert m.ratings.count == n0
+    np.testing.assert_array_equal(m.predict(u[:50], i[:50]), before)
+    b = BiasedMatrixFactorization(NumFactors=4, NumIter=1, Gpus="0")
+    b.ratings = Ratings(u, i, v)
+    b.train()
+    with pytest.raises(NotImplementedError):
+        b.remove_ratings(Ratings(u[:1], i[:1], v[:1]))
+    assert b.ratings.count == len(u)
+    tr_u, tr_i, _, _ = planted_feedback(2, 300, 60, 8)
+    for cls in (BPRMF, WRMF):
+        r = cls(NumFactors=4, NumIter=1, Gpus="0")
+        r.feedback = PosOnlyFeedback(tr_u, tr_i)
+        r.train()
+        n0 = r.feedback.count
+        with pytest.raises(NotImplementedError):
+            r.add_feedback([0], [1])
+        assert r.feedback.count == n0
 
 
 def _emulate_user_shards(u, i, v, bnd, U, V, bu, bi, epochs, kw, snaps):
