@@ -1413,22 +1413,18 @@ struct mml_bmf {
     std::vector<mml_bmf*> shards;
     std::vector<int32_t> ub;
     std::vector<int32_t> cnt_u_host, cnt_i_host;  // the whole data set's counts
-    // DSGD ring on a multi-device context: device d owns the block rows [d m, (d + 1) m) (m = G /
-    // devices) and with them its user groups; item groups travel to the device whose window
-    // needs them.  The multi handle keeps the raw ratings until set_blocks deals them out, the
-    // group of every user / item (-1: no rating), and per item group the device holding its
-    // newest rows (-1: every device, as after set_model).  A shard keeps its first block row,
-    // the items of every group in group order (gi_off on the host), the staging rows of the
-    // peer copies and the event its last pack recorded.
-    std::vector<int32_t> hu, hi;
-    std::vector<float> hr;
+    // a rank of the DSGD ring (DSGD schedule on a context with a communicator or a peer group):
+    // it owns the block rows [row0, row0 + m) (m = G / ranks) and with them its user groups; item
+    // groups travel to the rank whose window needs them.  Every rank keeps the group of every
+    // user / item (-1: no rating), per item group the rank holding its newest rows (-1: every
+    // rank, as after set_model), the items of every group in group order (gi_off on the host)
+    // and the staging rows of the moves.
     std::vector<int32_t> ugroup, igroup, hold;
     std::vector<int64_t> gi_off;
-    bool synced0 = true;  // shard 0 holds the newest copy of every row
+    bool ring_synced = true;  // every rank holds the newest copy of every row
     int32_t row0 = 0;
     mml::DeviceArray<int32_t> gi_ids;
     mml::DeviceArray<float> stage_v, stage_b;
-    hipEvent_t ev_pack = nullptr;
     // the item average after an epoch: RCCL (ncclAvg) on a communicator, else (a device listed
     // more than once) the other shards' V || b_i staged on shard 0's device, averaged there and
     // copied back; events around it time it (mml_bmf_last_allreduce_ms)
@@ -1939,7 +1935,8 @@ void multi_create(mml_ctx* ctx, const mml_bmf_params* params, int32_t n_users, i
 }
 
 bool multi_dsgd(const mml_bmf* h) { return h->p.schedule == MML_SCHEDULE_DSGD; }
-void dsgd_sync_all(mml_bmf* h);
+template <class F>
+void ring_all(mml_bmf* h, F&& f);
 
 // a shard's frequency-regularisation / InitModel counts are the whole data set's
 mml_status upload_counts(mml_bmf* s, const std::vector<int32_t>& cu,
@@ -1972,13 +1969,10 @@ void multi_set_data(mml_bmf* h, const int32_t* users, const int32_t* items, cons
         ++h->cnt_u_host[users[x]];
         ++h->cnt_i_host[items[x]];
     }
-    if (multi_dsgd(h)) {  // dealt out by set_blocks (its indices address these raw arrays)
-        // the ring's shards hold diverged item groups: bring every device to the newest model
-        // before the groups are forgotten
-        if (h->has_model && h->G > 0) dsgd_sync_all(h);
-        h->hu.assign(users, users + n);
-        h->hi.assign(items, items + n);
-        h->hr.assign(values, values + n);
+    if (multi_dsgd(h)) {  // the ring's ranks each keep the whole set (set_blocks picks rows)
+        ring_all(h, [&](int32_t d) {
+            return mml_bmf_set_data(h->shards[d], users, items, values, n, order);
+        });
         h->G = 0;
         h->n = n;
         h->has_data = true;
@@ -2256,257 +2250,369 @@ void multi_epoch(mml_bmf* h, float learn_rate) {
 }
 
 // ---- DSGD ring (the reference's MaxThreads = G schedule, BiasedMatrixFactorization.cs:205-215,
-// over several devices).  Blocks of one sub-epoch share no user or item, so each device runs the
-// block rows it owns exactly as the single-device DSGD launch would, and the only exchange is an
-// item group moving to the device whose window (the m item groups its rows visit) needs it next:
-// its rows are packed on the holder, peer-copied (one xGMI hop; a device-local copy when a device
-// is listed twice) and scattered on the new owner, ordered by events.  The result is the
-// single-device DSGD result, bit for bit.
+// over several devices), one RANK per device.  Blocks of one sub-epoch share no user or item, so
+// rank r runs the block rows it owns, [r m, (r + 1) m) with m = G / ranks, exactly as the
+// single-device DSGD launch would, and the only exchange is an item group moving to the rank whose
+// window (the m item groups its rows visit) needs it next: packed on the holder, sent, scattered
+// on the new holder.  The result is the single-device DSGD result, bit for bit.
+//
+// Every rank keeps the whole rating set (set_data), derives the groups from the blocks
+// (set_blocks) and tracks which rank holds the newest rows of each item group (hold[], the same on
+// every rank).  Transport: RCCL ncclSend / ncclRecv and ncclBroadcast on a communicator (one
+// process per GPU, mml_ctx_comm_init; or mml_ctx_create_multi over distinct devices, one host
+// thread per rank), or peer copies between host barriers on a context that lists a device more
+// than once (mml::PeerGroup).  get_model / predict / evaluate on a rank first bring every rank to
+// the newest model (ring_sync, a collective: every rank calls them).
 
-// the model with each row taken from the device holding its newest copy (host arrays, each
-// nullable): users from their group's device, items from their group's holder, rows without a
-// rating from device 0 (every device holds the same copy of those)
-void dsgd_gather(mml_bmf* h, float* U, float* V, float* bu, float* bi) {
-    const int32_t nd = (int32_t)h->shards.size();
-    const int32_t m = h->G > 0 ? h->G / nd : 1;
-    std::vector<std::vector<int32_t>> uid(nd), iid(nd);
-    for (int32_t u = 0; u < h->n_users; ++u) {
-        const int32_t g = h->G > 0 ? h->ugroup[u] : -1;
-        uid[g < 0 ? 0 : g / m].push_back(u);
+struct RingRank {
+    int32_t r, n;
+};
+RingRank ring_rank(const mml_ctx* c) {
+    if (c->comm && c->nranks > 1) return {c->rank, c->nranks};
+    if (c->peers && c->peers->n > 1) return {c->peer_rank, c->peers->n};
+    return {0, 1};
+}
+// a single-device handle that is one rank of the ring
+bool ring_mode(const mml_bmf* h) {
+    return !h->ctx->multi() && h->p.schedule == MML_SCHEDULE_DSGD && h->p.model <= MML_MF_PLAIN &&
+           ring_rank(h->ctx).n > 1;
+}
+
+struct RingMove {
+    int32_t from, to;
+    int64_t r0, r1;  // rows of the group-ordered item list
+};
+
+// the group moves before sub-epoch sq (group c is visited by block row (c - sq) mod G), merged
+// into runs of consecutive groups with the same endpoints; updates hold[] -- the same on every rank
+std::vector<RingMove> ring_moves(mml_bmf* h, int32_t sq, int32_t m) {
+    const int32_t G = h->G;
+    std::vector<RingMove> mv;
+    for (int32_t c = 0; c < G; ++c) {
+        const int32_t to = ((c - sq) % G + G) % G / m, from = h->hold[c];
+        h->hold[c] = to;
+        if (from < 0 || from == to || h->gi_off[c + 1] == h->gi_off[c]) continue;
+        if (!mv.empty() && mv.back().from == from && mv.back().to == to &&
+            mv.back().r1 == h->gi_off[c])
+            mv.back().r1 = h->gi_off[c + 1];
+        else
+            mv.push_back({from, to, h->gi_off[c], h->gi_off[c + 1]});
     }
+    return mv;
+}
+
+// this rank's part of the moves: its packed runs to their new holders, the runs it receives into
+// its staging rows (same offsets as on the sender)
+void ring_exchange(mml_bmf* h, const std::vector<RingMove>& mv, int32_t r) {
+    mml_ctx* c = h->ctx;
+    hipStream_t st = c->stream;
+    const int64_t ld = h->ld;
+    if (c->comm) {
+        MML_RCCL(ncclGroupStart());
+        for (const RingMove& v : mv) {
+            const int64_t n = v.r1 - v.r0;
+            if (v.from == r) {
+                MML_RCCL(ncclSend(h->stage_v.get() + v.r0 * ld, (size_t)(n * ld), ncclFloat, v.to,
+                                  c->comm, st));
+                MML_RCCL(ncclSend(h->stage_b.get() + v.r0, (size_t)n, ncclFloat, v.to, c->comm,
+                                  st));
+            } else if (v.to == r) {
+                MML_RCCL(ncclRecv(h->stage_v.get() + v.r0 * ld, (size_t)(n * ld), ncclFloat,
+                                  v.from, c->comm, st));
+                MML_RCCL(ncclRecv(h->stage_b.get() + v.r0, (size_t)n, ncclFloat, v.from, c->comm,
+                                  st));
+            }
+        }
+        MML_RCCL(ncclGroupEnd());
+        return;
+    }
+    mml::PeerGroup* g = c->peers.get();
+    MML_HIP(hipStreamSynchronize(st));  // this rank's packs are complete
+    g->publish(c, 0, h->stage_v.get());
+    g->publish(c, 1, h->stage_b.get());
+    g->barrier();
+    for (const RingMove& v : mv) {
+        if (v.to != r) continue;
+        const int64_t n = v.r1 - v.r0;
+        MML_HIP(hipMemcpyPeerAsync(h->stage_v.get() + v.r0 * ld, c->device,
+                                   static_cast<float*>(g->peer(v.from, 0)) + v.r0 * ld,
+                                   g->devices[v.from], sizeof(float) * n * ld, st));
+        MML_HIP(hipMemcpyPeerAsync(h->stage_b.get() + v.r0, c->device,
+                                   static_cast<float*>(g->peer(v.from, 1)) + v.r0,
+                                   g->devices[v.from], sizeof(float) * n, st));
+    }
+    MML_HIP(hipStreamSynchronize(st));
+    g->barrier();  // the senders' staging rows are read before anyone packs again
+}
+
+// count floats of rank q's buffer broadcast to every rank (RCCL broadcast or peer copies)
+void ring_bcast(mml_bmf* h, float* buf, int64_t count, int32_t q) {
+    mml_ctx* c = h->ctx;
+    hipStream_t st = c->stream;
+    if (c->comm) {
+        if (count > 0)
+            MML_RCCL(ncclBroadcast(buf, buf, (size_t)count, ncclFloat, q, c->comm, st));
+        return;
+    }
+    mml::PeerGroup* g = c->peers.get();
+    MML_HIP(hipStreamSynchronize(st));
+    g->publish(c, 0, buf);
+    g->barrier();
+    if (c->peer_rank != q && count > 0)
+        MML_HIP(hipMemcpyPeerAsync(buf, c->device, g->peer(q, 0), g->devices[q],
+                                   sizeof(float) * count, st));
+    MML_HIP(hipStreamSynchronize(st));
+    g->barrier();
+}
+
+// every rank gets the newest copy of every row: rank q broadcasts the user rows of its block rows
+// and the item groups it holds, the others scatter them; then no group has a holder (hold = -1)
+void ring_sync(mml_bmf* h) {
+    if (h->ring_synced || h->G == 0) {
+        h->ring_synced = true;
+        return;
+    }
+    const RingRank rr = ring_rank(h->ctx);
+    const int32_t m = h->G / rr.n;
+    h->ctx->activate();
+    hipStream_t st = h->ctx->stream;
+    std::vector<std::vector<int32_t>> uid(rr.n), iid(rr.n);
+    for (int32_t u = 0; u < h->n_users; ++u)
+        if (h->ugroup[u] >= 0) uid[h->ugroup[u] / m].push_back(u);
     for (int32_t i = 0; i < h->n_items; ++i) {
-        const int32_t g = h->G > 0 ? h->igroup[i] : -1;
-        iid[g < 0 || h->hold[g] < 0 ? 0 : h->hold[g]].push_back(i);
+        const int32_t g = h->igroup[i];
+        if (g >= 0 && h->hold[g] >= 0) iid[h->hold[g]].push_back(i);
     }
-    mml::on_devices(h->ctx, [&](int32_t d) {
-        return mml::guard([&] {
-            mml_bmf* s = h->shards[d];
-            s->ctx->activate();
-            hipStream_t st = s->ctx->stream;
-            auto pull = [&](const std::vector<int32_t>& ids, const float* M, const float* b,
-                            float* outM, float* outB) {
-                const int64_t n = (int64_t)ids.size();
-                if (n == 0 || (!outM && !outB)) return;
-                mml::DeviceArray<int32_t> di;
-                mml::DeviceArray<float> pm, pb;
-                di.alloc(n);
-                pm.alloc((size_t)n * s->ld);
-                pb.alloc(n);
-                MML_HIP(hipMemcpyAsync(di.get(), ids.data(), sizeof(int32_t) * n,
-                                       hipMemcpyHostToDevice, st));
-                rows_gather_kernel<<<grid_for(n * s->ld), 256, 0, st>>>(M, b, di.get(), n, s->ld,
-                                                                         pm.get(), pb.get());
-                MML_HIP(hipGetLastError());
-                std::vector<float> hm((size_t)n * s->ld), hb(n);
-                MML_HIP(hipMemcpyAsync(hm.data(), pm.get(), sizeof(float) * hm.size(),
-                                       hipMemcpyDeviceToHost, st));
-                MML_HIP(hipMemcpyAsync(hb.data(), pb.get(), sizeof(float) * n,
-                                       hipMemcpyDeviceToHost, st));
-                MML_HIP(hipStreamSynchronize(st));
-                for (int64_t x = 0; x < n; ++x) {
-                    if (outM)
-                        std::copy(hm.begin() + x * s->ld, hm.begin() + x * s->ld + s->k,
-                                  outM + (int64_t)ids[x] * s->k);
-                    if (outB) outB[ids[x]] = hb[x];
-                }
-            };
-            pull(uid[d], s->U.get(), s->bu.get(), U, bu);
-            pull(iid[d], s->V.get(), s->bi.get(), V, bi);
-        });
-    });
-}
-
-// every device gets the newest model (before the groups change)
-void dsgd_sync_all(mml_bmf* h) {
-    std::vector<float> U((size_t)h->n_users * h->k), V((size_t)h->n_items * h->k),
-        bu(h->n_users), bi(h->n_items);
-    dsgd_gather(h, U.data(), V.data(), bu.data(), bi.data());
-    mml_bmf* s0 = h->shards[0];
-    mml::on_devices(h->ctx, [&](int32_t d) {
-        return mml_bmf_set_model(h->shards[d], U.data(), V.data(), bu.data(), bi.data(), s0->gb,
-                                 s0->min_rating, s0->max_rating);
-    });
+    mml::DeviceArray<int32_t> ids;
+    mml::DeviceArray<float> buf;
+    for (int32_t q = 0; q < rr.n; ++q) {
+        const int64_t nu = (int64_t)uid[q].size(), ni = (int64_t)iid[q].size();
+        const int64_t count = (nu + ni) * (h->ld + 1);
+        ids.reserve(std::max<int64_t>(1, nu + ni));
+        buf.reserve(std::max<int64_t>(1, count));
+        if (nu)
+            MML_HIP(hipMemcpyAsync(ids.get(), uid[q].data(), sizeof(int32_t) * nu,
+                                   hipMemcpyHostToDevice, st));
+        if (ni)
+            MML_HIP(hipMemcpyAsync(ids.get() + nu, iid[q].data(), sizeof(int32_t) * ni,
+                                   hipMemcpyHostToDevice, st));
+        float* bu_ = buf.get() + nu * h->ld;          // [U rows][b_u][V rows][b_i]
+        float* v_ = bu_ + nu;
+        float* bi_ = v_ + ni * h->ld;
+        if (q == rr.r) {
+            if (nu)
+                rows_gather_kernel<<<grid_for(nu * h->ld), 256, 0, st>>>(
+                    h->U.get(), h->bu.get(), ids.get(), nu, h->ld, buf.get(), bu_);
+            if (ni)
+                rows_gather_kernel<<<grid_for(ni * h->ld), 256, 0, st>>>(
+                    h->V.get(), h->bi.get(), ids.get() + nu, ni, h->ld, v_, bi_);
+            MML_HIP(hipGetLastError());
+        }
+        ring_bcast(h, buf.get(), count, q);
+        if (q != rr.r) {
+            if (nu)
+                rows_scatter_kernel<<<grid_for(nu * h->ld), 256, 0, st>>>(
+                    buf.get(), bu_, ids.get(), nu, h->ld, h->U.get(), h->bu.get());
+            if (ni)
+                rows_scatter_kernel<<<grid_for(ni * h->ld), 256, 0, st>>>(
+                    v_, bi_, ids.get() + nu, ni, h->ld, h->V.get(), h->bi.get());
+            MML_HIP(hipGetLastError());
+        }
+        MML_HIP(hipStreamSynchronize(st));  // ids / buf are reused by the next rank's round
+    }
     std::fill(h->hold.begin(), h->hold.end(), -1);
-    h->synced0 = true;
+    h->ring_synced = true;
 }
 
-// device 0 gets the newest copy of every row (Predict / Evaluate run there); the other devices'
-// rows and the holders stay as they are
-void dsgd_sync0(mml_bmf* h) {
-    if (h->synced0) return;
-    std::vector<float> U((size_t)h->n_users * h->k), V((size_t)h->n_items * h->k),
-        bu(h->n_users), bi(h->n_items);
-    dsgd_gather(h, U.data(), V.data(), bu.data(), bi.data());
-    mml_bmf* s0 = h->shards[0];
-    const mml_status st = mml_bmf_set_model(s0, U.data(), V.data(), bu.data(), bi.data(), s0->gb,
-                                            s0->min_rating, s0->max_rating);
-    if (st != MML_OK) mml::fail(st, mml_last_error());
-    h->synced0 = true;
+// the user group and item group of every rating of the blocks: block b = j G + c
+__global__ __launch_bounds__(256) void ring_groups_kernel(const int64_t* __restrict__ off,
+                                                          int64_t nb, int32_t G,
+                                                          const int32_t* __restrict__ idx,
+                                                          int64_t total,
+                                                          const int32_t* __restrict__ users,
+                                                          const int32_t* __restrict__ items,
+                                                          int32_t* __restrict__ ug,
+                                                          int32_t* __restrict__ ig, int32_t check,
+                                                          int32_t* __restrict__ bad) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = nb;  // the block of position x: off[b] <= x < off[b + 1]
+        while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (off[mid] <= x) lo = mid;
+            else hi = mid;
+        }
+        const int32_t j = (int32_t)(lo / G), c = (int32_t)(lo % G);
+        const int32_t u = users[idx[x]], i = items[idx[x]];
+        if (!check) {
+            ug[u] = j;
+            ig[i] = c;
+        } else if (ug[u] != j || ig[i] != c) {
+            atomicOr(bad, 1);
+        }
+    }
 }
 
-void multi_set_blocks(mml_bmf* h, int32_t G, const int64_t* offsets, const int32_t* indices) {
-    const int32_t nd = (int32_t)h->shards.size();
-    MML_REQUIRE(multi_dsgd(h), "set_blocks on a multi-device context needs the DSGD schedule");
-    MML_REQUIRE(h->has_data, "set_data must precede set_blocks");
-    MML_REQUIRE(G % nd == 0, "the DSGD ring needs num_groups (MaxThreads) to be a multiple of "
-                             "the device count");
+// set_blocks on a rank: the groups (checked to be a user-group x item-group partition), the item
+// list in group order, and this rank's block rows as its stream (block_off local to them)
+void ring_set_blocks(mml_bmf* h, int32_t G, const int64_t* offsets, const int32_t* indices) {
+    const RingRank rr = ring_rank(h->ctx);
+    MML_REQUIRE(G % rr.n == 0, "the DSGD ring needs num_groups (MaxThreads) to be a multiple of "
+                               "the device count");
     const int64_t nb = (int64_t)G * G;
     MML_REQUIRE(offsets[0] == 0, "offsets[0] must be 0");
     for (int64_t b = 0; b < nb; ++b)
         MML_REQUIRE(offsets[b + 1] >= offsets[b], "offsets must be non-decreasing");
-    MML_REQUIRE(offsets[nb] <= h->n && (offsets[nb] == 0 || indices),
-                "block indices exceed ratings");
-    for (int64_t x = 0; x < offsets[nb]; ++x)
-        MML_REQUIRE(indices[x] >= 0 && indices[x] < h->n, "block index out of range");
-    if (h->has_model && h->G > 0) dsgd_sync_all(h);  // the holders refer to the old groups
-    std::vector<int32_t> ug(h->n_users, -1), ig(h->n_items, -1);
-    for (int64_t b = 0; b < nb; ++b) {
-        const int32_t j = (int32_t)(b / G), c = (int32_t)(b % G);
-        for (int64_t x = offsets[b]; x < offsets[b + 1]; ++x) {
-            int32_t& gu = ug[h->hu[indices[x]]];
-            int32_t& gi = ig[h->hi[indices[x]]];
-            MML_REQUIRE((gu < 0 || gu == j) && (gi < 0 || gi == c),
-                        "blocks are not a user-group x item-group partition");
-            gu = j;
-            gi = c;
-        }
+    const int64_t total = offsets[nb];
+    MML_REQUIRE(total <= h->n && (total == 0 || indices), "block indices exceed ratings");
+    if (h->has_model && h->G > 0) ring_sync(h);  // the holders refer to the old groups
+    h->ctx->activate();
+    hipStream_t st = h->ctx->stream;
+    mml::DeviceArray<int64_t> doff;
+    mml::DeviceArray<int32_t> ord, ug, ig;
+    doff.alloc(nb + 1);
+    ord.alloc(std::max<int64_t>(1, total));
+    ug.alloc(std::max<int32_t>(1, h->n_users));
+    ig.alloc(std::max<int32_t>(1, h->n_items));
+    MML_HIP(hipMemcpyAsync(doff.get(), offsets, sizeof(int64_t) * (nb + 1), hipMemcpyHostToDevice,
+                           st));
+    if (total > 0)
+        MML_HIP(hipMemcpyAsync(ord.get(), indices, sizeof(int32_t) * total, hipMemcpyHostToDevice,
+                               st));
+    MML_HIP(hipMemsetAsync(ug.get(), 0xff, sizeof(int32_t) * ug.count, st));
+    MML_HIP(hipMemsetAsync(ig.get(), 0xff, sizeof(int32_t) * ig.count, st));
+    MML_HIP(hipMemsetAsync(h->scratch_i32.get(), 0, sizeof(int32_t), st));
+    int32_t bad = 0;
+    if (total > 0) {
+        check_order_kernel<<<grid_for(total), 256, 0, st>>>(ord.get(), total, h->n,
+                                                            h->scratch_i32.get());
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipMemcpyAsync(&bad, h->scratch_i32.get(), sizeof(int32_t), hipMemcpyDeviceToHost,
+                               st));
+        MML_HIP(hipStreamSynchronize(st));
+        MML_REQUIRE(!bad, "block index out of range");
+        for (int32_t check = 0; check < 2; ++check)
+            ring_groups_kernel<<<grid_for(total), 256, 0, st>>>(
+                doff.get(), nb, G, ord.get(), total, h->raw_u.get(), h->raw_i.get(), ug.get(),
+                ig.get(), check, h->scratch_i32.get());
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipMemcpyAsync(&bad, h->scratch_i32.get(), sizeof(int32_t), hipMemcpyDeviceToHost,
+                               st));
     }
-    const int32_t m = G / nd;
+    std::vector<int32_t> ugh(h->n_users), igh(h->n_items);
+    if (h->n_users)
+        MML_HIP(hipMemcpyAsync(ugh.data(), ug.get(), sizeof(int32_t) * h->n_users,
+                               hipMemcpyDeviceToHost, st));
+    if (h->n_items)
+        MML_HIP(hipMemcpyAsync(igh.data(), ig.get(), sizeof(int32_t) * h->n_items,
+                               hipMemcpyDeviceToHost, st));
+    MML_HIP(hipStreamSynchronize(st));
+    MML_REQUIRE(!bad, "blocks are not a user-group x item-group partition");
     std::vector<int64_t> gi_off(G + 1, 0);
     for (int32_t i = 0; i < h->n_items; ++i)
-        if (ig[i] >= 0) ++gi_off[ig[i] + 1];
+        if (igh[i] >= 0) ++gi_off[igh[i] + 1];
     for (int32_t c = 0; c < G; ++c) gi_off[c + 1] += gi_off[c];
     std::vector<int32_t> gi_ids(std::max<int64_t>(1, gi_off[G]));
     {
         std::vector<int64_t> at(gi_off.begin(), gi_off.end() - 1);
         for (int32_t i = 0; i < h->n_items; ++i)
-            if (ig[i] >= 0) gi_ids[at[ig[i]]++] = i;
+            if (igh[i] >= 0) gi_ids[at[igh[i]]++] = i;
     }
-    mml::on_devices(h->ctx, [&](int32_t d) {
-        mml_bmf* s = h->shards[d];
-        std::vector<int32_t> lu, li;
-        std::vector<float> lr;
-        std::vector<int64_t> loff((size_t)m * G + 1, 0);
-        for (int64_t lb = 0; lb < (int64_t)m * G; ++lb) {
-            const int64_t b = (int64_t)d * m * G + lb;  // block rows d m .. (d + 1) m - 1
-            for (int64_t x = offsets[b]; x < offsets[b + 1]; ++x) {
-                lu.push_back(h->hu[indices[x]]);
-                li.push_back(h->hi[indices[x]]);
-                lr.push_back(h->hr[indices[x]]);
-            }
-            loff[lb + 1] = (int64_t)lu.size();
-        }
-        mml_status st = mml_bmf_set_data(s, lu.data(), li.data(), lr.data(), (int64_t)lu.size(),
-                                         nullptr);
-        if (st == MML_OK) st = upload_counts(s, h->cnt_u_host, h->cnt_i_host);
-        if (st != MML_OK) return st;
-        return mml::guard([&] {
-            s->ctx->activate();
-            hipStream_t hs = s->ctx->stream;
-            s->block_off.alloc(loff.size());
-            MML_HIP(hipMemcpyAsync(s->block_off.get(), loff.data(), sizeof(int64_t) * loff.size(),
-                                   hipMemcpyHostToDevice, hs));
-            s->gi_ids.alloc(gi_ids.size());
-            MML_HIP(hipMemcpyAsync(s->gi_ids.get(), gi_ids.data(),
-                                   sizeof(int32_t) * gi_ids.size(), hipMemcpyHostToDevice, hs));
-            s->stage_v.alloc(gi_ids.size() * (size_t)s->ld);
-            s->stage_b.alloc(gi_ids.size());
-            if (!s->ev_pack) MML_HIP(hipEventCreateWithFlags(&s->ev_pack, hipEventDisableTiming));
-            MML_HIP(hipStreamSynchronize(hs));
-            s->G = G;
-            s->row0 = d * m;
-        });
-    });
-    h->ugroup.swap(ug);
-    h->igroup.swap(ig);
+    // this rank's block rows [r m, (r + 1) m): one contiguous run of the blocks' indices
+    const int32_t m = G / rr.n;
+    const int64_t b0 = (int64_t)rr.r * m * G, b1 = b0 + (int64_t)m * G;
+    const int64_t x0 = offsets[b0], x1 = offsets[b1];
+    if (x1 > x0) {
+        gather_stream_kernel<<<grid_for(x1 - x0), 256, 0, st>>>(
+            h->raw_u.get(), h->raw_i.get(), h->raw_r.get(), ord.get() + x0, x1 - x0, h->su.get(),
+            h->si.get(), h->sr.get());
+        MML_HIP(hipGetLastError());
+    }
+    std::vector<int64_t> loff((size_t)m * G + 1);
+    for (int64_t lb = 0; lb <= (int64_t)m * G; ++lb) loff[lb] = offsets[b0 + lb] - x0;
+    h->block_off.alloc(loff.size());
+    MML_HIP(hipMemcpyAsync(h->block_off.get(), loff.data(), sizeof(int64_t) * loff.size(),
+                           hipMemcpyHostToDevice, st));
+    h->gi_ids.alloc(gi_ids.size());
+    MML_HIP(hipMemcpyAsync(h->gi_ids.get(), gi_ids.data(), sizeof(int32_t) * gi_ids.size(),
+                           hipMemcpyHostToDevice, st));
+    h->stage_v.alloc(gi_ids.size() * (size_t)h->ld);
+    h->stage_b.alloc(gi_ids.size());
+    MML_HIP(hipStreamSynchronize(st));
+    h->ugroup.swap(ugh);
+    h->igroup.swap(igh);
     h->gi_off.swap(gi_off);
     h->hold.assign(G, -1);
+    h->ring_synced = true;
+    h->row0 = rr.r * m;
     h->G = G;
 }
 
 template <int LOSS>
-void dsgd_ring_epoch(mml_bmf* h, float learn_rate, const int32_t* seq) {
-    const int32_t nd = (int32_t)h->shards.size(), G = h->G, m = G / nd;
-    const mml_bmf* s0 = h->shards[0];
+void ring_epoch(mml_bmf* h, float learn_rate, const int32_t* seq) {
+    const RingRank rr = ring_rank(h->ctx);
+    const int32_t G = h->G, m = G / rr.n;
     BmfScalars sc;
-    sc.gb = s0->gb;
-    sc.min_rating = s0->min_rating;
-    sc.range = s0->max_rating - s0->min_rating;
+    sc.gb = h->gb;
+    sc.min_rating = h->min_rating;
+    sc.range = h->max_rating - h->min_rating;
     sc.lr = learn_rate;
     sc.blr = h->p.bias_learn_rate * learn_rate;
     sc.bias_reg = h->p.bias_reg;
     sc.reg_u = h->p.reg_u;
     sc.reg_i = h->p.reg_i;
-    struct Move {
-        int32_t from, to;
-        int64_t r0, r1;  // rows of the group-ordered item list
-    };
-    const auto t0 = std::chrono::steady_clock::now();
-    std::vector<Move> mv;
-    std::vector<char> packed(nd);
+    h->ctx->activate();
+    hipStream_t st = h->ctx->stream;
+    const bool fr = h->p.frequency_regularization != 0;
+    MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
     for (int32_t x = 0; x < G; ++x) {
-        const int32_t sq = seq[x];
-        mv.clear();
-        for (int32_t c = 0; c < G; ++c) {  // group c is visited by block row (c - sq) mod G
-            const int32_t to = ((c - sq) % G + G) % G / m, from = h->hold[c];
-            h->hold[c] = to;
-            if (from < 0 || from == to || h->gi_off[c + 1] == h->gi_off[c]) continue;
-            if (!mv.empty() && mv.back().from == from && mv.back().to == to &&
-                mv.back().r1 == h->gi_off[c])
-                mv.back().r1 = h->gi_off[c + 1];
-            else
-                mv.push_back({from, to, h->gi_off[c], h->gi_off[c + 1]});
-        }
-        std::fill(packed.begin(), packed.end(), 0);
-        for (const Move& v : mv) {
-            mml_bmf* a = h->shards[v.from];
-            a->ctx->activate();
+        const std::vector<RingMove> mv = ring_moves(h, seq[x], m);
+        for (const RingMove& v : mv) {  // pack what leaves this rank (after its last SGD launch)
+            if (v.from != rr.r) continue;
             const int64_t n = v.r1 - v.r0;
-            rows_gather_kernel<<<grid_for(n * a->ld), 256, 0, a->ctx->stream>>>(
-                a->V.get(), a->bi.get(), a->gi_ids.get() + v.r0, n, a->ld,
-                a->stage_v.get() + v.r0 * a->ld, a->stage_b.get() + v.r0);
-            MML_HIP(hipGetLastError());
-            packed[v.from] = 1;
+            rows_gather_kernel<<<grid_for(n * h->ld), 256, 0, st>>>(
+                h->V.get(), h->bi.get(), h->gi_ids.get() + v.r0, n, h->ld,
+                h->stage_v.get() + v.r0 * h->ld, h->stage_b.get() + v.r0);
         }
-        for (int32_t d = 0; d < nd; ++d)
-            if (packed[d]) {
-                mml_bmf* a = h->shards[d];
-                a->ctx->activate();
-                MML_HIP(hipEventRecord(a->ev_pack, a->ctx->stream));
-            }
-        for (const Move& v : mv) {
-            mml_bmf *a = h->shards[v.from], *b = h->shards[v.to];
-            b->ctx->activate();
-            hipStream_t st = b->ctx->stream;
+        MML_HIP(hipGetLastError());
+        if (!mv.empty()) ring_exchange(h, mv, rr.r);
+        for (const RingMove& v : mv) {  // scatter what arrived
+            if (v.to != rr.r) continue;
             const int64_t n = v.r1 - v.r0;
-            MML_HIP(hipStreamWaitEvent(st, a->ev_pack, 0));
-            MML_HIP(hipMemcpyPeerAsync(b->stage_v.get() + v.r0 * b->ld, b->ctx->device,
-                                       a->stage_v.get() + v.r0 * a->ld, a->ctx->device,
-                                       sizeof(float) * n * b->ld, st));
-            MML_HIP(hipMemcpyPeerAsync(b->stage_b.get() + v.r0, b->ctx->device,
-                                       a->stage_b.get() + v.r0, a->ctx->device, sizeof(float) * n,
-                                       st));
-            rows_scatter_kernel<<<grid_for(n * b->ld), 256, 0, st>>>(
-                b->stage_v.get() + v.r0 * b->ld, b->stage_b.get() + v.r0, b->gi_ids.get() + v.r0,
-                n, b->ld, b->V.get(), b->bi.get());
-            MML_HIP(hipGetLastError());
+            rows_scatter_kernel<<<grid_for(n * h->ld), 256, 0, st>>>(
+                h->stage_v.get() + v.r0 * h->ld, h->stage_b.get() + v.r0,
+                h->gi_ids.get() + v.r0, n, h->ld, h->V.get(), h->bi.get());
         }
-        for (int32_t d = 0; d < nd; ++d) {
-            mml_bmf* s = h->shards[d];
-            s->ctx->activate();
-            const bool fr = h->p.frequency_regularization != 0;
-            launch_ordered<LOSS>(s, s->block_off.get(), G, sq, m, sc, fr ? s->cnt_u.get() : nullptr,
-                                 fr ? s->cnt_i.get() : nullptr, s->row0);
-        }
+        MML_HIP(hipGetLastError());
+        launch_ordered<LOSS>(h, h->block_off.get(), G, seq[x], m, sc,
+                             fr ? h->cnt_u.get() : nullptr, fr ? h->cnt_i.get() : nullptr,
+                             h->row0);
     }
-    for (int32_t d = 0; d < nd; ++d) {
-        h->shards[d]->ctx->activate();
-        MML_HIP(hipStreamSynchronize(h->shards[d]->ctx->stream));
-    }
-    h->last_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0)
-                     .count();
-    h->last_launches = G * nd;
-    h->synced0 = false;
+    MML_HIP(hipEventRecord(h->ctx->ev_end, st));
+    MML_HIP(hipEventSynchronize(h->ctx->ev_end));
+    MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));
+    h->last_launches = G;
+    h->ring_synced = false;
+}
+
+// the ranks of a multi-device context, one host thread each (a repeated device: its peer group is
+// reset first and released by a failing rank, so no rank waits at a barrier for ever)
+template <class F>
+void ring_all(mml_bmf* h, F&& f) {
+    mml::PeerGroup* g = h->shards[0]->ctx->peers.get();
+    if (g) g->reset();
+    mml::on_devices(h->ctx, [&](int32_t d) {
+        const mml_status st = f(d);
+        if (st != MML_OK && g) g->abort();
+        return st;
+    });
+}
+
+// every shard (rank) of a multi-device DSGD handle brought to the newest model
+void multi_ring_sync(mml_bmf* h) {
+    ring_all(h, [&](int32_t d) {
+        return mml::guard([&] { ring_sync(h->shards[d]); });
+    });
 }
 
 }  // namespace
@@ -2579,7 +2685,6 @@ extern "C" mml_status mml_bmf_destroy(mml_bmf* h) {
         }
         (void)hipSetDevice(h->ctx->device);
         (void)hipStreamSynchronize(h->ctx->stream);
-        if (h->ev_pack) (void)hipEventDestroy(h->ev_pack);
         if (h->ev_ar0) (void)hipEventDestroy(h->ev_ar0);
         if (h->ev_ar1) (void)hipEventDestroy(h->ev_ar1);
         delete h;
@@ -2593,6 +2698,8 @@ extern "C" mml_status mml_bmf_set_data(mml_bmf* h, const int32_t* users, const i
         MML_REQUIRE(n >= 0 && n <= INT32_MAX, "rating count out of range");
         MML_REQUIRE(n == 0 || (users && items && values), "null rating arrays");
         if (h->ctx->multi()) return multi_set_data(h, users, items, values, n, order);
+        // a ring rank: every rank gets the newest model before the groups are forgotten
+        if (ring_mode(h) && h->has_model) ring_sync(h);
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         h->has_data = false;
@@ -2651,10 +2758,18 @@ extern "C" mml_status mml_bmf_set_blocks(mml_bmf* h, int32_t num_groups, const i
         check_handle(h);
         if (h->ctx->multi()) {
             MML_REQUIRE(num_groups >= 1 && offsets, "bad block arguments");
-            return multi_set_blocks(h, num_groups, offsets, indices);
+            MML_REQUIRE(multi_dsgd(h), "set_blocks on a multi-device context needs the DSGD "
+                                       "schedule");
+            MML_REQUIRE(h->has_data, "set_data must precede set_blocks");
+            ring_all(h, [&](int32_t d) {
+                return mml_bmf_set_blocks(h->shards[d], num_groups, offsets, indices);
+            });
+            h->G = num_groups;
+            return;
         }
         MML_REQUIRE(h->has_data, "set_data must precede set_blocks");
         MML_REQUIRE(num_groups >= 1 && offsets, "bad block arguments");
+        if (ring_mode(h)) return ring_set_blocks(h, num_groups, offsets, indices);
         const int64_t nb = (int64_t)num_groups * num_groups;
         MML_REQUIRE(offsets[0] == 0, "offsets[0] must be 0");
         for (int64_t b = 0; b < nb; ++b)
@@ -2703,8 +2818,6 @@ extern "C" mml_status mml_bmf_set_model(mml_bmf* h, const float* U, const float*
                 return mml_bmf_set_model(h->shards[d], U, V, bu, bi, global_bias, min_rating,
                                          max_rating);
             });
-            std::fill(h->hold.begin(), h->hold.end(), -1);
-            h->synced0 = true;
             h->has_model = true;
             return;
         }
@@ -2725,6 +2838,8 @@ extern "C" mml_status mml_bmf_set_model(mml_bmf* h, const float* U, const float*
         h->min_rating = min_rating;
         h->max_rating = max_rating;
         h->has_model = true;
+        std::fill(h->hold.begin(), h->hold.end(), -1);  // a ring rank: every rank has every row
+        h->ring_synced = true;
     });
 }
 
@@ -2758,8 +2873,6 @@ extern "C" mml_status mml_bmf_init_model(mml_bmf* h, uint64_t seed, double mean,
                 return mml_bmf_init_model(h->shards[d], seed, mean, stddev, global_bias,
                                           min_rating, max_rating);
             });
-            std::fill(h->hold.begin(), h->hold.end(), -1);
-            h->synced0 = true;
             h->has_model = true;
             return;
         }
@@ -2782,6 +2895,8 @@ extern "C" mml_status mml_bmf_init_model(mml_bmf* h, uint64_t seed, double mean,
         h->min_rating = min_rating;
         h->max_rating = max_rating;
         h->has_model = true;
+        std::fill(h->hold.begin(), h->hold.end(), -1);
+        h->ring_synced = true;
     });
 }
 
@@ -2790,10 +2905,18 @@ extern "C" mml_status mml_bmf_get_model(mml_bmf* h, float* U, float* V, float* b
         check_handle(h);
         if (h->ctx->multi()) {
             MML_REQUIRE(h->has_model, "no model");
-            if (multi_dsgd(h)) return dsgd_gather(h, U, V, bu, bi);
+            if (multi_dsgd(h)) {  // every rank synced (a collective), rank 0 downloads
+                ring_all(h, [&](int32_t d) {
+                    return d == 0 ? mml_bmf_get_model(h->shards[0], U, V, bu, bi)
+                                  : mml_bmf_get_model(h->shards[d], nullptr, nullptr, nullptr,
+                                                      nullptr);
+                });
+                return;
+            }
             return multi_get_model(h, U, V, bu, bi);
         }
         MML_REQUIRE(h->has_model, "no model (set_model first)");
+        if (ring_mode(h)) ring_sync(h);
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         if (U) download_padded(h, U, h->U.get(), h->n_users);
@@ -2812,24 +2935,17 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
                                       const int32_t* subepoch_sequence) {
     return guard([&] {
         check_handle(h);
-        if (h->ctx->multi() && multi_dsgd(h)) {  // one host thread drives the ring
+        if (h->ctx->multi() && multi_dsgd(h)) {  // the ranks' epochs, one host thread each
             MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
             MML_REQUIRE(h->G > 0, "DSGD schedule needs set_blocks");
-            MML_REQUIRE(subepoch_sequence, "DSGD schedule needs a sub-epoch sequence");
-            for (int32_t x = 0; x < h->G; ++x)
-                MML_REQUIRE(subepoch_sequence[x] >= 0 && subepoch_sequence[x] < h->G,
-                            "sub-epoch index out of range");
-            if (h->n == 0) return;
-            switch (h->p.model == MML_MF_PLAIN ? kPlainMF : h->p.loss) {
-                case kPlainMF: dsgd_ring_epoch<kPlainMF>(h, learn_rate, subepoch_sequence); break;
-                case MML_LOSS_MAE:
-                    dsgd_ring_epoch<MML_LOSS_MAE>(h, learn_rate, subepoch_sequence);
-                    break;
-                case MML_LOSS_LOGISTIC:
-                    dsgd_ring_epoch<MML_LOSS_LOGISTIC>(h, learn_rate, subepoch_sequence);
-                    break;
-                default: dsgd_ring_epoch<MML_LOSS_RMSE>(h, learn_rate, subepoch_sequence); break;
-            }
+            std::vector<float> ms(h->shards.size(), 0.0f);
+            ring_all(h, [&](int32_t d) {
+                const mml_status st = mml_bmf_iterate(h->shards[d], learn_rate, subepoch_sequence);
+                ms[d] = h->shards[d]->last_ms;
+                return st;
+            });
+            h->last_ms = *std::max_element(ms.begin(), ms.end());
+            h->last_launches = h->shards[0]->last_launches * (int32_t)h->shards.size();
             return;
         }
         if (h->ctx->multi()) {  // every shard's epoch, then the item average
@@ -2852,6 +2968,18 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
             for (int32_t x = 0; x < h->G; ++x)
                 MML_REQUIRE(subepoch_sequence[x] >= 0 && subepoch_sequence[x] < h->G,
                             "sub-epoch index out of range");
+        }
+        if (ring_mode(h)) {  // one rank of the DSGD ring
+            if (h->n == 0) return;
+            switch (h->p.model == MML_MF_PLAIN ? kPlainMF : h->p.loss) {
+                case kPlainMF: ring_epoch<kPlainMF>(h, learn_rate, subepoch_sequence); break;
+                case MML_LOSS_MAE: ring_epoch<MML_LOSS_MAE>(h, learn_rate, subepoch_sequence); break;
+                case MML_LOSS_LOGISTIC:
+                    ring_epoch<MML_LOSS_LOGISTIC>(h, learn_rate, subepoch_sequence);
+                    break;
+                default: ring_epoch<MML_LOSS_RMSE>(h, learn_rate, subepoch_sequence); break;
+            }
+            return;
         }
         h->ctx->activate();
         BmfScalars s;
@@ -2916,7 +3044,7 @@ extern "C" mml_status mml_bmf_predict(mml_bmf* h, const int32_t* users, const in
             MML_REQUIRE(n >= 0 && (n == 0 || (users && items && out)), "null arrays");
             MML_REQUIRE(h->has_model, "no model");
             if (multi_dsgd(h)) {
-                dsgd_sync0(h);
+                multi_ring_sync(h);
                 const mml_status st = mml_bmf_predict(h->shards[0], users, items, n, out);
                 if (st != MML_OK) mml::fail(st, mml_last_error());
                 return;
@@ -2925,6 +3053,7 @@ extern "C" mml_status mml_bmf_predict(mml_bmf* h, const int32_t* users, const in
         }
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(n >= 0 && (n == 0 || (users && items && out)), "bad arguments");
+        if (ring_mode(h)) ring_sync(h);  // a collective: every rank predicts
         if (n == 0) return;
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
@@ -2949,7 +3078,7 @@ extern "C" mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const i
             MML_REQUIRE(n >= 0 && (n == 0 || (users && items && values)) && out, "null arrays");
             MML_REQUIRE(h->has_model, "no model");
             if (multi_dsgd(h)) {
-                dsgd_sync0(h);
+                multi_ring_sync(h);
                 const mml_status st = mml_bmf_evaluate(h->shards[0], users, items, values, n, out);
                 if (st != MML_OK) mml::fail(st, mml_last_error());
                 return;
@@ -2958,6 +3087,7 @@ extern "C" mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const i
         }
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(n > 0 && users && items && values && out, "bad arguments");
+        if (ring_mode(h)) ring_sync(h);  // a collective: every rank evaluates
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         upload_pairs(h, users, items, n);

@@ -250,6 +250,9 @@ struct PeerGroup {
                         int32_t k);
     // v[0 .. m) <- max over the ranks (m <= 4); called by all ranks
     void max_u32(const mml_ctx* ctx, uint32_t* v, int32_t m);
+    // pointer slot (0 .. 3) of this rank, read by the others after the next barrier
+    void publish(const mml_ctx* ctx, int32_t slot, void* p);
+    void* peer(int32_t rank, int32_t slot) const { return ptr[(size_t)rank * 4 + slot]; }
 
   private:
     struct Impl;

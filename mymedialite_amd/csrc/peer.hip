@@ -9,7 +9,9 @@
 //  * PeerGroup: one host thread per shard (mml::on_devices), each driving its own stream, meeting
 //    at host barriers -- the shape of RCCL ranks.  WRMF's row shards all-gather through it
 //    (each rank copies the other ranks' rows into its own matrix) and agree on the refinement's
-//    stopping decision (the max over ranks of the last correction, as ncclMax would give).
+//    stopping decision (the max over ranks of the last correction, as ncclMax would give); the
+//    BiasedMF DSGD ring's ranks send item groups through it (bmf.hip ring_exchange / ring_bcast,
+//    the peer-copy twins of ncclSend / ncclRecv and ncclBroadcast).
 #include <condition_variable>
 #include <mutex>
 
@@ -93,7 +95,7 @@ struct PeerGroup::Impl {
     bool aborted = false;
 };
 
-PeerGroup::PeerGroup(int32_t n_) : n(n_), impl(new Impl), ptr(n_, nullptr), u32(n_ * 4, 0) {}
+PeerGroup::PeerGroup(int32_t n_) : n(n_), impl(new Impl), ptr((size_t)n_ * 4, nullptr), u32((size_t)n_ * 4, 0) {}
 PeerGroup::~PeerGroup() { delete impl; }
 
 void PeerGroup::barrier() {
@@ -122,17 +124,21 @@ void PeerGroup::reset() {
     impl->arrived = 0;
 }
 
+void PeerGroup::publish(const mml_ctx* ctx, int32_t slot, void* p) {
+    ptr[(size_t)ctx->peer_rank * 4 + slot] = p;
+}
+
 void PeerGroup::allgather_rows(const mml_ctx* ctx, float* W, const std::vector<int64_t>& bounds,
                                int32_t k) {
     const int32_t r = ctx->peer_rank;
     MML_HIP(hipStreamSynchronize(ctx->stream));  // this rank's rows are final
-    ptr[r] = W;
+    publish(ctx, 0, W);
     barrier();
     for (int32_t q = 0; q < n; ++q) {
         const int64_t rows = bounds[q + 1] - bounds[q];
         if (q == r || rows <= 0) continue;
         const size_t o = (size_t)bounds[q] * k;
-        MML_HIP(hipMemcpyPeerAsync(W + o, ctx->device, static_cast<float*>(ptr[q]) + o,
+        MML_HIP(hipMemcpyPeerAsync(W + o, ctx->device, static_cast<float*>(peer(q, 0)) + o,
                                    devices[q], sizeof(float) * rows * k, ctx->stream));
     }
     MML_HIP(hipStreamSynchronize(ctx->stream));
