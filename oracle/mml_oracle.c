@@ -207,6 +207,62 @@ void ora_bmf_iterate(const ora_bmf_params* p, const int32_t* users, const int32_
     }
 }
 
+/* Hogwild's staleness, restated for the Hogwild bands of the tests (not a reference behaviour):
+ * the stream idx[0 .. n_idx) is cut into W contiguous chunks, one per stream (a wavefront of the
+ * GPU kernel); at step t every stream takes its next R ratings.  All ratings of a step read the
+ * model as it was before the step (ora_bmf_iterate's arithmetic on those values), then their
+ * results are written in stream order, so a later stream's write of a row replaces an earlier
+ * one's (the lost update of two wavefronts writing one row).  W = 1, R = 1 is ora_bmf_iterate. */
+void ora_bmf_iterate_lockstep(const ora_bmf_params* p, const int32_t* users, const int32_t* items,
+                              const float* values, const int32_t* idx, int64_t n_idx, float* U,
+                              float* V, float* bu, float* bi, const int32_t* count_by_user,
+                              const int32_t* count_by_item, int32_t W, int32_t R) {
+    const int k = p->k;
+    const int64_t per = (n_idx + W - 1) / W;
+    const int64_t cap = (int64_t)W * R;
+    float* nu = (float*)malloc(sizeof(float) * (size_t)cap * (k + 1));
+    float* nv = (float*)malloc(sizeof(float) * (size_t)cap * (k + 1));
+    int32_t* su = (int32_t*)malloc(sizeof(int32_t) * (size_t)cap);
+    int32_t* si = (int32_t*)malloc(sizeof(int32_t) * (size_t)cap);
+    for (int64_t t = 0; t * R < per; ++t) {
+        int64_t m = 0;
+        for (int32_t w = 0; w < W; ++w)
+            for (int32_t r = 0; r < R; ++r) {
+                const int64_t pos = (int64_t)w * per + t * R + r;
+                if (t * R + r >= per || pos >= n_idx) continue;
+                const int32_t index = idx[pos], u = users[index], i = items[index];
+                float* Uo = nu + m * (k + 1);
+                float* Vo = nv + m * (k + 1);
+                memcpy(Uo, U + (int64_t)u * k, sizeof(float) * k);
+                memcpy(Vo, V + (int64_t)i * k, sizeof(float) * k);
+                float bu1 = bu[u], bi1 = bi[i];
+                const int32_t zero = 0;  // the rating's rows, copied: row 0 of Uo / Vo
+                ora_bmf_iterate(p, &zero, &zero, values + index, &zero, 1, Uo, Vo, &bu1, &bi1,
+                                count_by_user ? count_by_user + u : NULL,
+                                count_by_item ? count_by_item + i : NULL);
+                Uo[k] = bu1;
+                Vo[k] = bi1;
+                su[m] = u;
+                si[m] = i;
+                ++m;
+            }
+        for (int64_t x = 0; x < m; ++x) {
+            if (p->update_user) {
+                memcpy(U + (int64_t)su[x] * k, nu + x * (k + 1), sizeof(float) * k);
+                bu[su[x]] = nu[x * (k + 1) + k];
+            }
+            if (p->update_item) {
+                memcpy(V + (int64_t)si[x] * k, nv + x * (k + 1), sizeof(float) * k);
+                bi[si[x]] = nv[x * (k + 1) + k];
+            }
+        }
+    }
+    free(nu);
+    free(nv);
+    free(su);
+    free(si);
+}
+
 /* y summed over the user's rated items (MatrixExtensions.SumOfRows, DataType/MatrixExtensions.cs:
  * 125-135: float accumulation in list order), / sqrt(count) in double, cast to float -- the user
  * vector of SigmoidItemAsymmetricFactorModel (Iterate :104-107, PrecomputeUserFactors :316-331) */

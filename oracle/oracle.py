@@ -65,6 +65,9 @@ def lib():
         L.ora_bmf_params_sizeof.restype = ctypes.c_size_t
         L.ora_bmf_iterate.argtypes = [ctypes.c_void_p, _i32p, _i32p, _f32p, _i32p, ctypes.c_int64,
                                       _f32p, _f32p, _f32p, _f32p, _i32p, _i32p]
+        L.ora_bmf_iterate_lockstep.argtypes = [ctypes.c_void_p, _i32p, _i32p, _f32p, _i32p,
+                                               ctypes.c_int64, _f32p, _f32p, _f32p, _f32p, _i32p,
+                                               _i32p, ctypes.c_int32, ctypes.c_int32]
         L.ora_bmf_dsgd_epoch_mt.argtypes = [ctypes.c_void_p, _i32p, _i32p, _f32p, _i64p, _i32p,
                                             ctypes.c_int32, _i32p, ctypes.c_int32, _f32p, _f32p,
                                             _f32p, _f32p, _i32p, _i32p]
@@ -239,6 +242,25 @@ def bmf_iterate(users, items, values, indices, U, V, bu, bi, *, gb, min_rating, 
                           _p(bi, _f32p), _p(cu, _i32p), _p(ci, _i32p))
 
 
+def bmf_iterate_lockstep(users, items, values, indices, U, V, bu, bi, *, streams, step, gb,
+                         min_rating, range_, lr, bias_lr=1.0, bias_reg=0.01, reg_u=0.015,
+                         reg_i=0.015, loss=0, freq_reg=False, count_by_user=None,
+                         count_by_item=None):
+    """ora_bmf_iterate_lockstep: Hogwild's staleness restated (``streams`` contiguous chunks of
+    the stream, ``step`` ratings each per lockstep step, reads before the step, writes in stream
+    order) -- a model for the tests' Hogwild bands, not a reference behaviour.  In place."""
+    k = U.shape[1]
+    p = _BmfParams(k, loss, int(freq_reg), 1, 1, gb, min_rating, range_, lr, bias_lr, bias_reg,
+                   reg_u, reg_i)
+    cu = i32(count_by_user) if count_by_user is not None else None
+    ci = i32(count_by_item) if count_by_item is not None else None
+    idx = i32(indices)
+    lib().ora_bmf_iterate_lockstep(ctypes.byref(p), _p(users, _i32p), _p(items, _i32p),
+                                   _p(values, _f32p), _p(idx, _i32p), idx.size, _p(U, _f32p),
+                                   _p(V, _f32p), _p(bu, _f32p), _p(bi, _f32p), _p(cu, _i32p),
+                                   _p(ci, _i32p), int(streams), int(step))
+
+
 def bmf_dsgd_epoch_mt(users, items, values, blocks, subepochs, n_threads, U, V, bu, bi, *, gb,
                       min_rating, range_, lr, bias_lr=1.0, bias_reg=0.01, reg_u=0.015,
                       reg_i=0.015, loss=0, freq_reg=False, count_by_user=None,
@@ -280,13 +302,15 @@ def bmf_train(users, items, values, n_users, n_items, min_rating, max_rating, *,
               learn_rate=0.01, decay=1.0, reg_u=0.015, reg_i=0.015, bias_reg=0.01,
               bias_learn_rate=1.0, num_iter=30, init_mean=0.0, init_stddev=0.1, loss=0,
               frequency_regularization=False, max_threads=1, naive_parallelization=False,
-              bold_driver=False, rng=None, callback=None, order=None):
+              bold_driver=False, rng=None, callback=None, order=None, lockstep=None):
     """BiasedMatrixFactorization.Train() (:173-194) and NumIter x Iterate() (:197-222).
 
     Returns a dict with the model and the RNG-derived schedule (so a GPU run can be fed the
     identical RandomIndex / DSGD blocks). ``callback(epoch, state)`` after every epoch.
     ``order``: a visit order to use instead of the RNG's shuffle (the same InitModel with
     another permutation: the order noise of the sequential loop, for the Hogwild bands).
+    ``lockstep=(streams, step)``: the single-thread epochs run bmf_iterate_lockstep (the Hogwild
+    staleness model) instead of the sequential loop.
     """
     users, items, values = i32(users), i32(items), f32(values)
     rng = rng if rng is not None else Rng(seed)
@@ -366,7 +390,11 @@ def bmf_train(users, items, values, n_users, n_items, min_rating, max_rating, *,
         else:
             if random_index is None:
                 random_index = rng.shuffle(np.arange(len(users), dtype=np.int32))
-            bmf_iterate(users, items, values, random_index, U, V, bu, bi, lr=lr, **common)
+            if lockstep is None:
+                bmf_iterate(users, items, values, random_index, U, V, bu, bi, lr=lr, **common)
+            else:
+                bmf_iterate_lockstep(users, items, values, random_index, U, V, bu, bi, lr=lr,
+                                     streams=lockstep[0], step=lockstep[1], **common)
         lr = update_learn_rate(lr)  # UpdateLearnRate() at :221
         if callback is not None:
             callback(epoch, state)

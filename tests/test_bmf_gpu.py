@@ -8,8 +8,9 @@ Tolerances:
     the north-star bar.
   * HOGWILD reorders updates, so it matches statistically.  Its staleness on a hot item grows with
     (updates in flight) x sum_i p_i^2, which is large for tiny skewed sets: C1 tolerance 1e-2
-    (measured 0.007); on a C2-shaped set (100k Zipf items) 3e-3 after epochs 1 and 2 (C2 itself,
-    measured once with the 106-s oracle: 0.0014 after epoch 1, 0.0007 after epoch 2).
+    (measured 0.007).  On a C2-shaped set (100k Zipf items) the predictions stay within 1.5x the
+    sequential oracle's own order noise (three other shuffles) and the RMSE within twice the
+    oracle's staleness model (the launch's streams in lockstep; test_edge_cases_gpu.hogwild_band).
 """
 import numpy as np
 import pytest
@@ -188,11 +189,14 @@ def test_hogwild_statistical_parity_c2_shape():
     u, i, v = (t.numpy() for t in planted_ratings_torch(nu, ni, n + 100_000, seed=5, device="cpu"))
     tu, ti, tv = u[n:], i[n:], v[n:]
     u, i, v = u[:n].copy(), i[:n].copy(), v[:n].copy()
-    from test_edge_cases_gpu import hogwild_band, order_noise
+    from test_edge_cases_gpu import hogwild_band, lockstep_delta, order_noise
     # the sequential oracle's order noise after 1 and 2 epochs (same InitModel, three other
-    # shuffles), on the held-out ratings
+    # shuffles) and its staleness model (the launch's 352 streams in lockstep), on the held-out
+    # ratings
     noise = [order_noise(u, i, v, seed=1, k=64, num_iter=e, eval_set=(tu, ti, tv))
              for e in (1, 2)]
+    noise = [(*x, lockstep_delta(u, i, v, seed=1, k=64, num_iter=e, eval_set=(tu, ti, tv),
+                                 ref=x[0])) for e, x in zip((1, 2), noise)]
     res = {}
     for name, props in (("hogwild", dict(Schedule="hogwild")),
                         ("hogwild_coherent", dict(Schedule="hogwild_coherent")),
@@ -208,8 +212,8 @@ def test_hogwild_statistical_parity_c2_shape():
         res[name] = ok
     # Hogwild on XCD-owned item groups (xcd.hip; every item row cached in ONE XCD's L2, users
     # written through, one flushing wave per XCD), the same kernel behind a one-shard
-    # multi-device context (Gpus=0) and the coherent schedule: within 3x the sequential loop's
-    # own order noise after each epoch
+    # multi-device context (Gpus=0) and the coherent schedule: predictions within the sequential
+    # loop's own order noise, RMSE within the staleness model's band, after each epoch
     assert all(all(v_) for v_ in res.values()), res
 
 

@@ -4,8 +4,10 @@
   factors and biases within 1e-5 of the oracle after each epoch (the reference's own loop,
   BiasedMatrixFactorization.cs:264-310).
 * HOGWILD at every lanes-per-rating variant the kernel selects (k = 1 .. 256) on a set large enough
-  for the multi-workgroup, XCD-grouped path: train RMSE and mean |dpred| after 2 epochs within 3x
-  the sequential oracle's own order noise (the same InitModel over three other shuffles; printed).
+  for the multi-workgroup, XCD-grouped path: mean |dpred| after 2 epochs within 1.5x the
+  sequential oracle's own order noise (the same InitModel over three other shuffles), and the train
+  RMSE between the sequential loop's and twice the oracle's staleness model (the launch's streams
+  in lockstep, ora_bmf_iterate_lockstep), 3x the order noise of slack (all printed).
 * Degenerate data: no ratings at all (Iterate is a no-op), every rating on one user (one hot user
   row under Hogwild), ratings whose chunk ends are ragged (n not a multiple of 64).
 * Argument errors come back as MML_ERR_ARG, never as a device fault: k outside 1 .. 256, negative
@@ -88,15 +90,45 @@ def order_noise(u, i, v, *, seed, k, num_iter, eval_set, perm_seeds=(101, 102, 1
     return ref, d_rmse, d_pred
 
 
-def hogwild_band(name, rmse, pred, ref, d_rmse, d_pred):
-    """GPU Hogwild against the sequential oracle, held to 3x the oracle's own
-    order noise (|dRMSE| and mean |dpred|); the sign of dRMSE is printed (+ = Hogwild worse)."""
+def hogwild_streams(n, k):
+    """The Hogwild launch's streams and ratings per step (bmf.hip launch_hogwild: waves =
+    min(8192, n / 12000), blocks of 4 waves rounded up to the 8 XCD groups; a wave applies
+    64 / LPR ratings per step, LPR = lanes per rating, the power of two >= k / 4)."""
+    waves = min(256 * 32, max(1, n // 12000))
+    blocks = -(-((waves + 3) // 4) // 8) * 8
+    lpr = 1
+    while lpr < (k + 3) // 4:
+        lpr *= 2
+    return blocks * 4, 64 // lpr
+
+
+def lockstep_delta(u, i, v, *, seed, k, num_iter, eval_set, ref, **kw):
+    """The oracle with Hogwild's staleness (ora_bmf_iterate_lockstep: the GPU launch's streams in
+    lockstep, reads before each step, lost updates) minus the sequential oracle, on eval_set."""
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    r = Ratings(u, i, v)
+    eu, ei, ev = eval_set
+    st = O.bmf_train(u, i, v, nu, ni, r.scale_min, r.scale_max, seed=seed, k=k,
+                     num_iter=num_iter, lockstep=hogwild_streams(len(u), k), **kw)
+    p = O.bmf_predict(eu, ei, st["U"], st["V"], st["bu"], st["bi"], st["global_bias"],
+                      st["min_rating"], st["range_"]).astype(np.float64)
+    return float(np.sqrt(np.mean((p - ev) ** 2))) - ref[0]
+
+
+def hogwild_band(name, rmse, pred, ref, d_rmse, d_pred, d_lock):
+    """GPU Hogwild against the sequential oracle.  Its predictions may differ from
+    the oracle's by what another shuffle gives the oracle itself (mean |dpred| <= 1.5x the order
+    noise), and its RMSE lies between the sequential loop's and twice the staleness model's
+    (d_lock), with 3x the order noise of slack on both sides: Hogwild converges more slowly by the
+    updates its streams have in flight, which is what d_lock restates.  Prints the sign (+ =
+    Hogwild worse) and every ratio."""
     dr = rmse - ref[0]
     mad = float(np.mean(np.abs(pred - ref[1])))
     print(f"{name}: RMSE gpu {rmse:.6f} oracle {ref[0]:.6f} delta {dr:+.2e} (order noise "
-          f"{d_rmse:.2e}, ratio {abs(dr) / max(d_rmse, 1e-12):.2f}); mean |dpred| {mad:.3e} "
-          f"(order noise {d_pred:.3e}, ratio {mad / max(d_pred, 1e-12):.2f})")
-    return abs(dr) <= 3 * d_rmse and mad <= 3 * d_pred
+          f"{d_rmse:.2e}, ratio {abs(dr) / max(d_rmse, 1e-12):.2f}; staleness model {d_lock:+.2e}, "
+          f"ratio {dr / d_lock if d_lock else float('nan'):.2f}); mean |dpred| {mad:.3e} (order "
+          f"noise {d_pred:.3e}, ratio {mad / max(d_pred, 1e-12):.2f})")
+    return (-3 * d_rmse <= dr <= 2 * max(d_lock, 0.0) + 3 * d_rmse) and mad <= 1.5 * d_pred
 
 
 @pytest.mark.parametrize("k", [1, 8, 64, 100, 256])
@@ -104,13 +136,15 @@ def test_hogwild_lane_variants_statistical(k):
     # 300 k ratings: >= 16 waves' worth, so the XCD-grouped multi-workgroup kernel runs
     u, i, v = _planted(90 + k, 3000, 800, 300_000)
     ref, d_rmse, d_pred = order_noise(u, i, v, seed=2, k=k, num_iter=2, eval_set=(u, i, v))
+    d_lock = lockstep_delta(u, i, v, seed=2, k=k, num_iter=2, eval_set=(u, i, v), ref=ref)
     m = _train(u, i, v, seed=2, k=k, num_iter=2, Schedule="hogwild")
     pred = m.predict(u, i).astype(np.float64)
     rmse = float(np.sqrt(np.mean((pred - v) ** 2)))
     assert np.isfinite(m.user_factors).all() and np.isfinite(m.item_factors).all()
     # the per-rating trajectories differ (Hogwild's interleaving and the XCD-grouped visit
-    # order): held to the spread three other shuffles give the sequential loop itself
-    assert hogwild_band(f"hogwild k={k} (train set)", rmse, pred, ref, d_rmse, d_pred)
+    # order): held to the spread three other shuffles give the sequential loop itself, and to
+    # the staleness model for the RMSE's systematic offset
+    assert hogwild_band(f"hogwild k={k} (train set)", rmse, pred, ref, d_rmse, d_pred, d_lock)
 
 
 def test_no_ratings_iterate_is_a_noop():

@@ -62,9 +62,11 @@ def test_c3_eight_user_shards_auc_vs_one_handle():
         torch.cuda.empty_cache()
     d = [b - a for a, b in zip(res[1], res[8])]
     _log(f"C3 AUC one handle {res[1]}, 8 averaged shards {res[8]}, difference {d}")
-    assert all(a > 0.6 for a in res[1] + res[8]), res  # both learn the held-out positives
-    assert res[1][1] > res[1][0] and res[8][1] > res[8][0]
-    assert all(abs(x) <= 0.02 for x in d), d
+    # both learn the held-out positives (AUC 0.5 at random; ~0.82 after one epoch: the
+    # popularity of the Zipf items and their factors), and 8-way averaging costs no more than the
+    # C3 replica's GPU-vs-oracle band (measured -0.0012 / +0.0016)
+    assert all(a > 0.75 for a in res[1] + res[8]), res
+    assert all(abs(x) <= 0.005 for x in d), d
 
 
 def _bucket_rows(deg, picks, rs):

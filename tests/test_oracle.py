@@ -329,3 +329,18 @@ def test_iafm_items_rated_by_user_union_order():
     o2, it2 = m._feedback_lists(0)
     np.testing.assert_array_equal(o2, off)
     np.testing.assert_array_equal(it2, items)
+
+
+def test_lockstep_staleness_model_reduces_to_the_loop():
+    """ora_bmf_iterate_lockstep (the Hogwild bands' staleness model) with one stream of one rating
+    per step is the sequential loop, bit for bit; with many streams it trains, more slowly."""
+    from golden_cases import synth_ratings
+    u, i, v = synth_ratings(5, 200, 90, 4000)
+    runs = {}
+    for ls in (None, (1, 1), (32, 4)):
+        st = O.bmf_train(u, i, v, 200, 90, 1.0, 5.0, seed=3, k=8, num_iter=2, lockstep=ls)
+        runs[ls] = st
+    for key in ("U", "V", "bu", "bi"):
+        np.testing.assert_array_equal(runs[(1, 1)][key], runs[None][key])
+    assert not np.array_equal(runs[(32, 4)]["V"], runs[None]["V"])
+    assert np.isfinite(runs[(32, 4)]["U"]).all()
