@@ -231,7 +231,9 @@ def bench_c2(args):
     achieved = n_local * bpu / (avg_kernel_ms * 1e-3) / 1e9
     traffic, traffic_note = None, None
     if k == 64 and n_local == 100_000_000 and args.schedule == "hogwild":
-        traffic, traffic_note = pmc_traffic("r2_c2_traffic.json", avg_kernel_ms)
+        traffic, traffic_note = pmc_traffic("r4_c2_traffic.json", avg_kernel_ms)
+    kernel = (N.last_kernel("mml_bmf_last_kernel", h) or
+              f"bmf_sgd_ordered_kernel (schedule {args.schedule})")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -261,7 +263,7 @@ def bench_c2(args):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_note": traffic_note,
-                         "kernel": f"bmf_sgd_hogwild_kernel<RMSE,{max(1, (k + 3) // 4)}>",
+                         "kernel": kernel,
                          "kernel_avg_ms": avg_kernel_ms, "bytes_per_update": bpu},
             "cpu_baseline": cpu,
         }
@@ -471,11 +473,15 @@ def bench_c4(args):
     elapsed = max_over_ranks(time.perf_counter() - t0)
     ar = np.zeros(1, np.float32)
     N.check(N.lib().mml_bmf_last_allreduce_ms(h, N.ptr(ar, N._f32p)))
+    kernel = N.last_kernel("mml_bmf_last_kernel", h)
     rmse = evaluate()
     value = n_total * args.steps / elapsed
     avg_kernel_ms = float(np.mean(kernel_ms))
     bpu = bytes_per_update(k)
     achieved = n_local * bpu / (avg_kernel_ms * 1e-3) / 1e9
+    traffic, traffic_note = None, None
+    if world == 1 and k == 64 and n_total == 1_000_000_000:
+        traffic, traffic_note = pmc_traffic("r4_c4_traffic.json", avg_kernel_ms)
     cpu = None
     if cpu_sample is not None:
         cpu = cpu_baseline_dsgd(h, k, n_users, n_items, gb, cpu_sample, "C4")
@@ -509,8 +515,8 @@ def bench_c4(args):
             "allreduce_note": "device time of the last step's ncclAvg all-reduce of V||b_i "
                               "(HIP events around it on the library stream)" if world > 1 else None,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": f"bmf_sgd_hogwild_kernel<RMSE,{max(1, (k + 3) // 4)}>",
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_note": traffic_note, "kernel": kernel,
                          "kernel_avg_ms": avg_kernel_ms, "bytes_per_update": bpu,
                          "per": "GPU (rank 0's shard)"},
             "cpu_baseline": cpu,
@@ -606,8 +612,9 @@ def bench_bpr(args):
     achieved = n * bpu / (upd_ms * 1e-3) / 1e9
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_bpr(k, args.cpu_seconds)
     traffic, traffic_note = None, None
-    if k == 128 and n == 500_000_000 and args.sampler == "uniform_user":
-        traffic, traffic_note = pmc_traffic("r2_c3_traffic.json", upd_ms)
+    if k == 128 and n_total == 500_000_000 and args.sampler == "uniform_user" and world == 1:
+        traffic, traffic_note = pmc_traffic("r4_c3_traffic.json", upd_ms)
+    kernel = N.last_kernel("mml_bpr_last_kernel", h)
     line = {
         "metric": "BPR triple-updates/sec, BPRMF k=128 (C3)",
         "value": n_events * args.steps / elapsed,
@@ -628,7 +635,7 @@ def bench_bpr(args):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_note": traffic_note,
-                     "kernel": f"bpr_update_kernel<{max(1, (k + 3) // 4)}>",
+                     "kernel": kernel,
                      "kernel_avg_ms": upd_ms, "bytes_per_update": bpu,
                      "epoch_device_ms": avg_ms,
                      "sampler_ms": avg_ms - upd_ms,

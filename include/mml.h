@@ -51,9 +51,12 @@ mml_status mml_ctx_destroy(mml_ctx* ctx);
  * on the HOGWILD schedules split the ratings into user ranges of equal rating count and average
  * V || item biases with one RCCL all-reduce after every epoch; mml_bmf on the DSGD
  * schedule runs the reference's MaxThreads = G blocks (BiasedMatrixFactorization.cs:205-215) as a
- * ring: device d owns block rows [d G/n, (d+1) G/n), item groups move by peer copy to the device
- * whose rows visit them next, and the model equals the single-device DSGD model bit for bit
- * (G must be a multiple of n); mml_wrmf solves row shards and all-gathers them after each
+ * ring: device d is rank d, owns block rows [d G/n, (d+1) G/n), item groups move by ncclSend /
+ * ncclRecv to the rank whose rows visit them next, and the model equals the single-device DSGD
+ * model bit for bit (G must be a multiple of n; round 4: the same rank code runs one process per
+ * GPU, a one-device context with mml_ctx_comm_init, DSGD schedule, every rank given the whole
+ * rating set and the same blocks and sub-epoch sequence, get_model / predict / evaluate then
+ * collectives); mml_wrmf solves row shards and all-gathers them after each
  * half-step.  Each call returns when all devices have finished.  mml_bmf's user shards also run
  * the ORDERED schedule (ABI 6: each shard its own range in visit order, deterministic), and
  * mml_bmf_set_data_device takes arrays on the first listed device and shards them there (ABI 6).
@@ -263,6 +266,10 @@ mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const int32_t* ite
 /* Device time of the last mml_bmf_iterate's SGD kernels (HIP events on the library stream):
  * out[0] = ms for the whole epoch, out[1] = number of kernel launches in it. */
 mml_status mml_bmf_last_timing(mml_bmf* h, float* out);
+/* The dominant kernel of the last mml_bmf_iterate as rocprofv3 names the template instance, e.g.
+ * "bmf_sgd_hogwild_kernel<0, 16, 1, 14>" (ABI 9; empty before a Hogwild epoch); NUL-terminated,
+ * truncated to cap bytes. */
+mml_status mml_bmf_last_kernel(mml_bmf* h, char* buf, int32_t cap);
 /* BiasedMatrixFactorization.ComputeObjective (:496-552) on the device model and training data:
  * out[0] = ComputeLoss() (RMSE / MAE / logistic sum per params.loss, double), out[1] = the
  * complexity term; ComputeObjective = (float)(out[0] + out[1]).  BoldDriver's UpdateLearnRate
@@ -432,6 +439,9 @@ mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const int32_t* item
 /* out[0] = the last epoch's device time (ms), out[1] = its update kernel alone (the rest is the
  * triple sampler) */
 mml_status mml_bpr_last_timing(mml_bpr* h, float* out);
+/* The update kernel of the last Hogwild epoch as rocprofv3 names it, e.g.
+ * "bpr_update_kernel<32, false, 27>" (ABI 9); NUL-terminated, truncated to cap bytes. */
+mml_status mml_bpr_last_kernel(mml_bpr* h, char* buf, int32_t cap);
 /* The last epoch's sampled triples in sample order (n = Feedback.Count), e.g. for BPRMF's
  * loss_sample_* arrays (BPRMF.cs:136-150) or to check a sampler's distribution (ABI 3).  On a
  * multi-device context: each user shard's triples in its sample order, shard after shard (ABI 9;

@@ -129,6 +129,7 @@ SIGNATURES = {
     "mml_bmf_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
     "mml_bmf_evaluate": (_st, [_vp, _i32p, _i32p, _f32p, ctypes.c_int64, _f32p]),
     "mml_bmf_last_timing": (_st, [_vp, _f32p]),
+    "mml_bmf_last_kernel": (_st, [_vp, ctypes.c_char_p, ctypes.c_int32]),
     "mml_bmf_objective": (_st, [_vp, _f64p]),
     "mml_bmf_allreduce_items": (_st, [_vp]),
     "mml_bmf_last_allreduce_ms": (_st, [_vp, _f32p]),
@@ -144,6 +145,7 @@ SIGNATURES = {
     "mml_bpr_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
     "mml_bpr_apply_triples": (_st, [_vp, _i32p, _i32p, _i32p, ctypes.c_int64]),
     "mml_bpr_last_timing": (_st, [_vp, _f32p]),
+    "mml_bpr_last_kernel": (_st, [_vp, ctypes.c_char_p, ctypes.c_int32]),
     "mml_bmf_set_implicit_feedback": (_st, [_vp, ctypes.c_int32, ctypes.c_int32, _i64p, _i32p,
                                             _f32p, _f32p]),
     "mml_bmf_get_implicit_factors": (_st, [_vp, ctypes.c_int32, _f32p]),
@@ -308,3 +310,11 @@ def auc_held_out(symbol: str, h, candidates, users, items):
     for a in ok:  # float accumulation, in user order
         acc = np.float32(acc + a)
     return (float(np.float32(acc / np.float32(len(ok)))) if len(ok) else 0.0), int(len(ok)), out
+
+
+def last_kernel(symbol: str, h) -> str:
+    """mml_bmf_last_kernel / mml_bpr_last_kernel: the dominant kernel of the last epoch, as
+    rocprofv3 names the template instance."""
+    buf = ctypes.create_string_buffer(256)
+    check(getattr(lib(), symbol)(h, buf, len(buf)))
+    return buf.value.decode()

@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "mml_device.h"
@@ -1374,6 +1375,7 @@ __global__ __launch_bounds__(64) void asym_precompute_kernel(AsymSlot sl, int32_
 
 struct mml_bmf {
     mml_ctx* ctx = nullptr;
+    std::string last_kernel;  // the dominant kernel of the last epoch, as rocprof names it
     mml_bmf_params p{};
     int32_t n_users = 0, n_items = 0, k = 0, ld = 0, lpr = 0;
     mml::DeviceArray<float> U, V, bu, bi;
@@ -1436,6 +1438,17 @@ struct mml_bmf {
 namespace {
 
 void check_handle(mml_bmf* h) { MML_REQUIRE(h && h->ctx, "null handle"); }
+
+// "name<a, b, ...>": a kernel template's name as rocprofv3 prints it (integer arguments)
+std::string kernel_label(const char* name, std::initializer_list<int> args) {
+    std::string s = std::string(name) + "<";
+    bool first = true;
+    for (int a : args) {
+        s += (first ? "" : ", ") + std::to_string(a);
+        first = false;
+    }
+    return s + ">";
+}
 
 // bmf_predict1's kind: 0 BiasedMatrixFactorization (sigmoid), 1 MatrixFactorization (plain,
 // clipped), 2 SVDPlusPlus (biases, clipped)
@@ -1702,7 +1715,8 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
 #define MML_HOG1(LPR, VPL, AM)                                                                  \
     bmf_sgd_hogwild_kernel<LOSS, LPR, VPL, AM><<<(int)blocks, 256, 0, st>>>(                  \
         su, si, sr, goff, ng, wpg, h->U.get(), h->V.get(), h->bu.get(), h->bi.get(), ld4, vb, bb, \
-        ub, bub, mml::flushers_per_xcd(1), s, cu, ci)
+        ub, bub, mml::flushers_per_xcd(1), s, cu, ci);                                         \
+    h->last_kernel = kernel_label("bmf_sgd_hogwild_kernel", {LOSS, LPR, VPL, (int)(AM)})
 #ifdef MML_EXPERIMENTS
 #define MML_HOG_EXP(LPR, VPL)                                                      \
     case kAccItemL2 | kAccUserThru | kAccFlush | kAccUBiasPlain:                   \
@@ -3014,6 +3028,17 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
         MML_HIP(hipEventRecord(h->ctx->ev_end, st));
         MML_HIP(hipEventSynchronize(h->ctx->ev_end));
         MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));
+    });
+}
+
+extern "C" mml_status mml_bmf_last_kernel(mml_bmf* h, char* buf, int32_t cap) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(buf && cap > 0, "null buffer");
+        const std::string& k = h->shards.empty() ? h->last_kernel : h->shards[0]->last_kernel;
+        const size_t n = std::min<size_t>(k.size(), (size_t)cap - 1);
+        std::copy(k.begin(), k.begin() + n, buf);
+        buf[n] = 0;
     });
 }
 

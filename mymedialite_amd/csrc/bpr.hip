@@ -37,6 +37,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "mml_device.h"
@@ -778,6 +779,7 @@ inline int lanes_per_row(int k) {
 
 struct mml_bpr {
     mml_ctx* ctx = nullptr;
+    std::string last_kernel;  // the last epoch's update kernel, as rocprof names it
     mml_bpr_params p{};
     int32_t n_users = 0, n_items = 0, k = 0, ld = 0, lpr = 0;
     mml::DeviceArray<float> U, V, bias, ev_out;
@@ -1389,11 +1391,12 @@ void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff,
     const uint64_t u_all = (uint64_t)h->n_users * h->ld * 4;
     const uint32_t ub = (uint32_t)std::min<uint64_t>(u_all, 0xFFFFFFFFull);
     if (u_all >= (1ull << 32)) am &= ~kBprUThru;
-#define MML_UPD(AM)                                                                             \
-    bpr_update_kernel<LPR, SOFT, AM><<<(int)blocks, 64 * wpb, 0, st>>>(                        \
-        tu, ti, tj, goff, gcnt, ng, wpg, h->U.get(), h->V.get(), h->bias.get(), h->ld / 4, vb, bb, \
-        ub, \
-        mml::flushers_per_xcd(4), s)
+#define MML_UPD(AM)                                                                           \
+    bpr_update_kernel<LPR, SOFT, AM><<<(int)blocks, 64 * wpb, 0, st>>>(                      \
+        tu, ti, tj, goff, gcnt, ng, wpg, h->U.get(), h->V.get(), h->bias.get(), h->ld / 4, vb, \
+        bb, ub, mml::flushers_per_xcd(4), s);                                                  \
+    h->last_kernel = "bpr_update_kernel<" + std::to_string(LPR) + (SOFT ? ", true, " : ", false, ") + \
+                     std::to_string((int)(AM)) + ">"
     switch (am) {
         case kBprLdL2: MML_UPD(kBprLdL2); break;
         case kBprLdL2 | kBprJThru: MML_UPD(kBprLdL2 | kBprJThru); break;
@@ -1902,6 +1905,16 @@ extern "C" mml_status mml_bpr_set_rows(mml_bpr* h, int32_t side, int32_t n_rows,
             MML_HIP(hipMemcpyAsync(M + (int64_t)rows[x] * h->ld, values + (int64_t)x * h->k,
                                    sizeof(float) * h->k, hipMemcpyHostToDevice, st));
         MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+extern "C" mml_status mml_bpr_last_kernel(mml_bpr* h, char* buf, int32_t cap) {
+    return guard([&] {
+        MML_REQUIRE(h && buf && cap > 0, "null argument");
+        const std::string& k = h->shards.empty() ? h->last_kernel : h->shards[0]->last_kernel;
+        const size_t n = std::min<size_t>(k.size(), (size_t)cap - 1);
+        std::copy(k.begin(), k.begin() + n, buf);
+        buf[n] = 0;
     });
 }
 
