@@ -335,3 +335,107 @@ def test_model_averaging_rmse_cost_vs_single_trajectory():
     # (hot items overshoot), so the north star's averaging stays; DESIGN.md section 5.
     assert rmse[1] < rmse[2] < rmse[4]
     assert rmse[2] - rmse[1] <= 0.04 and rmse[4] - rmse[1] <= 0.07
+
+
+def _ring_worker(rank, world, port, out_dir, G):
+    """One rank of the DSGD ring (bmf.hip ring_epoch / ring_sync) with the oracle as its epoch and
+    gloo send / recv as its transport: block rows [r m, (r + 1) m), the same hold[] bookkeeping on
+    every rank, item groups packed, sent to their next holder and scattered there before each
+    sub-epoch, then the newest rows broadcast from their holders."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tests")]
+    import torch
+    import torch.distributed as dist
+
+    import oracle as O
+    from golden_cases import synth_ratings
+    from mymedialite_amd.distributed import init_host_group
+
+    init_host_group(world)
+    u, i, v = synth_ratings(17, 300, 200, 20000)
+    nu, ni, k, m = 300, 200, 6, G // world
+    r = O.Rng(3)  # InitModel, then PartitionUsersAndItems and the sub-epoch shuffles (same on all)
+    U = r.fill_normal(nu * k, 0, 0.1).reshape(nu, k)
+    V = r.fill_normal(ni * k, 0, 0.1).reshape(ni, k)
+    cu, ci = np.bincount(u, minlength=nu), np.bincount(i, minlength=ni)
+    U[cu == 0] = 0
+    V[ci == 0] = 0
+    bu, bi = np.zeros(nu, np.float32), np.zeros(ni, np.float32)
+    Gc, off, idx = O.partition_users_and_items(r, u, i, nu - 1, ni - 1, G)
+    assert Gc == G
+    ug, ig = np.full(nu, -1), np.full(ni, -1)
+    for b in range(G * G):
+        ug[u[idx[off[b]:off[b + 1]]]] = b // G
+        ig[i[idx[off[b]:off[b + 1]]]] = b % G
+    items_of = [np.nonzero(ig == c)[0] for c in range(G)]
+    kw = dict(gb=O.global_bias(v, 1.0, 5.0), min_rating=np.float32(1), range_=np.float32(4),
+              lr=np.float32(0.01), count_by_user=cu.astype(np.int32),
+              count_by_item=ci.astype(np.int32))
+    hold = [-1] * G
+    for _ in range(2):
+        seq = r.shuffle(np.arange(G, dtype=np.int32))
+        for sq in seq.tolist():
+            moves = []
+            for c in range(G):
+                to = ((c - sq) % G) // m
+                if hold[c] >= 0 and hold[c] != to and len(items_of[c]):
+                    moves.append((c, hold[c], to))
+                hold[c] = to
+            reqs = []
+            for c, frm, to in moves:  # the group's V rows || b_i, sent whole
+                if frm == rank:
+                    buf = torch.from_numpy(np.concatenate([V[items_of[c]].ravel(),
+                                                           bi[items_of[c]]]))
+                    reqs.append(dist.isend(buf, to))
+            for c, frm, to in moves:
+                if to == rank:
+                    buf = torch.empty(len(items_of[c]) * (k + 1), dtype=torch.float32)
+                    dist.recv(buf, frm)
+                    x = buf.numpy()
+                    V[items_of[c]] = x[: len(items_of[c]) * k].reshape(-1, k)
+                    bi[items_of[c]] = x[len(items_of[c]) * k:]
+            for q in reqs:
+                q.wait()
+            for j in range(rank * m, (rank + 1) * m):  # this rank's block rows of the sub-epoch
+                b = j * G + (sq + j) % G
+                O.bmf_iterate(u, i, v, idx[off[b]:off[b + 1]], U, V, bu, bi, **kw)
+    # ring_sync: every rank broadcasts its users' rows and the groups it holds
+    for q in range(world):
+        uids = np.nonzero((ug >= 0) & (ug // m == q))[0]
+        iids = np.concatenate([items_of[c] for c in range(G) if hold[c] == q] or
+                              [np.zeros(0, np.int64)])
+        buf = torch.from_numpy(np.concatenate([U[uids].ravel(), bu[uids], V[iids].ravel(),
+                                               bi[iids]]).astype(np.float32))
+        dist.broadcast(buf, q)
+        x = buf.numpy()
+        a = len(uids) * k
+        U[uids] = x[:a].reshape(-1, k)
+        bu[uids] = x[a:a + len(uids)]
+        a += len(uids)
+        V[iids] = x[a:a + len(iids) * k].reshape(-1, k)
+        bi[iids] = x[a + len(iids) * k:]
+    np.save(os.path.join(out_dir, f"ring{rank}.npy"),
+            np.concatenate([U.ravel(), V.ravel(), bu, bi]).astype(np.float64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_dsgd_ring_equals_single_process_dsgd(tmp_path):
+    """The DSGD ring's protocol (BiasedMatrixFactorization.cs:205-215) on 2 gloo
+    ranks with the oracle per rank: after the final broadcast both ranks hold the single-process
+    MaxThreads = G DSGD model bit for bit."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "oracle"))
+    import oracle as O
+    from golden_cases import synth_ratings
+    world, G = 2, 4
+    mp.spawn(_ring_worker, args=(world, _free_port(), str(tmp_path), G), nprocs=world, join=True)
+    u, i, v = synth_ratings(17, 300, 200, 20000)
+    st = O.bmf_train(u, i, v, 300, 200, 1.0, 5.0, seed=3, k=6, num_iter=2, max_threads=G)
+    ref = np.concatenate([st["U"].ravel(), st["V"].ravel(), st["bu"], st["bi"]])
+    for rk in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"ring{rk}.npy"), ref)
