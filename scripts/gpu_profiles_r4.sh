@@ -40,3 +40,12 @@ step pmc_c5 400 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE
 python scripts/pmc_summary.py gpurun_out/pmc_c5_$TAG wrmf > gpurun_out/pmc_c5_${TAG}_summary.txt 2>&1
 rm -rf gpurun_out/pmc_c5_$TAG
 head -30 gpurun_out/pmc_c5_${TAG}_summary.txt
+# A/B of the grouped BPR sampler against the two-pass sampler + XcdSplit partition (experiments
+# build; MML_BPR_GROUPED=0 selects the two-pass path): kernel stats of both
+export MML_LIB_PATH=variants/exp/libmml_hip.so
+for g in 1 0; do
+    export MML_BPR_GROUPED=$g
+    step prof_c3_grouped$g 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3g${g}_$TAG -o c3 -- python bench.py --workload c3 --steps 3 --warmup 1 --no-cpu-baseline
+    keep gpurun_out/prof_c3g${g}_$TAG "*kernel_stats.csv"
+    rm -rf gpurun_out/prof_c3g${g}_$TAG
+done
