@@ -282,7 +282,7 @@ def cpu_threads() -> int:
     return max(1, min(16, n))
 
 
-def pmc_traffic(name, kernel_ms):
+def pmc_traffic(name, kernel_ms, alg_bytes=None):
     """roofline.traffic (GB/s) from a committed PMC summary (scripts/pmc_traffic2.py): the
     guide-corrected FETCH_SIZE x 2 + WRITE_SIZE bytes per launch over this run's kernel time, and
     a note with the calibrated reading beside it."""
@@ -290,6 +290,10 @@ def pmc_traffic(name, kernel_ms):
     if not os.path.exists(tf):
         return None, None
     t = json.load(open(tf))
+    if alg_bytes is not None and abs(t["algorithmic_bytes_per_launch"] - alg_bytes) > 1e-3 * alg_bytes:
+        return None, (f"profiles/{name} was collected on launches of "
+                      f"{t['algorithmic_bytes_per_launch'] / 1e9:.1f} GB algorithmic, this run's "
+                      f"launches move {alg_bytes / 1e9:.1f} GB: not comparable")
     gbs = t["traffic_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9
     note = (f"PMC per launch ({'profiles/' + name}): FETCH_SIZE x2 + WRITE_SIZE = "
             f"{t['traffic_bytes_per_launch'] / 1e9:.1f} GB ({t['traffic_over_algorithmic']:.2f} x "
@@ -613,7 +617,7 @@ def bench_bpr(args):
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_bpr(k, args.cpu_seconds)
     traffic, traffic_note = None, None
     if k == 128 and n_total == 500_000_000 and args.sampler == "uniform_user" and world == 1:
-        traffic, traffic_note = pmc_traffic("r4_c3_traffic.json", upd_ms)
+        traffic, traffic_note = pmc_traffic("r4_c3_traffic.json", upd_ms, n * bpu)
     kernel = N.last_kernel("mml_bpr_last_kernel", h)
     line = {
         "metric": "BPR triple-updates/sec, BPRMF k=128 (C3)",

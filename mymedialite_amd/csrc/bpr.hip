@@ -389,111 +389,6 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
     }
 }
 
-// The default sampler writing each triple straight into the region of its XCD group (the group of
-// i, xcd.hip): the epoch's triples come out partitioned for the Hogwild update without the
-// count / scatter passes of XcdSplit::partition.  A block draws kGrpPer x 256 consecutive samples
-// (the same counter-based draws as bpr_sample_kernel: the same triples), ranks them per group in
-// LDS, reserves its run of each group's region with one global atomic per group, and writes.
-// Region g holds gcap[g] triples from gbeg[g]; gcnt[g] counts the triples it received.  A block
-// whose run would pass a region's end writes nothing of that group and raises *overflow (the
-// epoch is then redrawn through the two-pass path).  The order within a region follows the blocks'
-// atomics, not the sample index (the Hogwild update interleaves the triples anyway).
-constexpr int kGrpPer = 8;
-__global__ __launch_bounds__(256) void bpr_sample_grouped_kernel(
-    const int32_t* __restrict__ cols, const int32_t* __restrict__ eligible, int32_t n_eligible,
-    int64_t n_samples, int32_t n_items, uint64_t seed, const uint32_t* __restrict__ recs,
-    const uint8_t* __restrict__ group, const int64_t* __restrict__ gbeg,
-    const int64_t* __restrict__ gcap, unsigned long long* __restrict__ gcnt,
-    int32_t* __restrict__ xu, int32_t* __restrict__ xi, int32_t* __restrict__ xj,
-    int32_t* __restrict__ overflow) {
-    __shared__ int32_t cnt[8];
-    __shared__ int64_t base[8];
-    if (threadIdx.x < 8) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t b0 = (int64_t)blockIdx.x * (256 * kGrpPer);
-    int32_t su[kGrpPer], si[kGrpPer], sj[kGrpPer], rk[kGrpPer];
-    int64_t rb[kGrpPer];
-    uint32_t dg[kGrpPer];
-    // the draws of draw_uniform_user, phase by phase over the thread's kGrpPer samples: each
-    // phase's loads are independent of each other, so they are in flight together
-#pragma unroll
-    for (int t = 0; t < kGrpPer; ++t) {
-        const int64_t smp = b0 + t * 256 + threadIdx.x;
-        const uint32_t du = draw(seed, smp, 0, (uint32_t)n_eligible);
-        su[t] = smp < n_samples ? (eligible ? eligible[du] : (int32_t)du) : 0;
-    }
-#pragma unroll
-    for (int t = 0; t < kGrpPer; ++t) {
-        const UserRec ur = user_rec(recs + (int64_t)su[t] * kRecWords);
-        rb[t] = ur.rb;
-        dg[t] = (uint32_t)(ur.re - ur.rb);
-    }
-#pragma unroll
-    for (int t = 0; t < kGrpPer; ++t) {
-        const int64_t smp = b0 + t * 256 + threadIdx.x;
-        si[t] = cols[rb[t] + draw(seed, smp, 1, dg[t] ? dg[t] : 1)];
-        sj[t] = (int32_t)draw(seed, smp, 2, (uint32_t)n_items);
-    }
-#pragma unroll
-    for (int t = 0; t < kGrpPer; ++t) {
-        const int64_t smp = b0 + t * 256 + threadIdx.x;
-        rk[t] = -1;
-        if (smp >= n_samples) continue;
-        const uint32_t* rec = recs + (int64_t)su[t] * kRecWords;
-        for (uint32_t d = 3; bloom_maybe(rec, sj[t]) && row_has(cols, rb[t], rb[t] + dg[t], sj[t]);
-             ++d)
-            sj[t] = (int32_t)draw(seed, smp, d, (uint32_t)n_items);
-        rk[t] = atomicAdd(&cnt[group[si[t]]], 1);
-    }
-    __syncthreads();
-    if (threadIdx.x < 8) {
-        const int g = threadIdx.x;
-        base[g] = cnt[g] ? (int64_t)atomicAdd(&gcnt[g], (unsigned long long)cnt[g]) : 0;
-        if (cnt[g] && base[g] + cnt[g] > gcap[g]) {
-            atomicOr(overflow, 1);
-            base[g] = -1;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < kGrpPer; ++t) {
-        if (rk[t] < 0) continue;
-        const int g = group[si[t]];
-        if (base[g] < 0) continue;
-        const int64_t pos = gbeg[g] + base[g] + rk[t];
-        xu[pos] = su[t];
-        xi[pos] = si[t];
-        xj[pos] = sj[t];
-    }
-}
-
-// Each group's share of the default sampler's i: (1 / n_eligible) sum over the eligible users of
-// |S_u in g| / |S_u| (u uniform, then i uniform in S_u) -- the expected region sizes
-__global__ __launch_bounds__(256) void bpr_group_share_kernel(
-    const int64_t* __restrict__ off, const int32_t* __restrict__ cols,
-    const int32_t* __restrict__ eligible, int32_t n_eligible, const uint8_t* __restrict__ group,
-    double* __restrict__ share) {
-    __shared__ double acc[8];
-    if (threadIdx.x < 8) acc[threadIdx.x] = 0.0;
-    __syncthreads();
-    double mine[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n_eligible;
-         x += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t u = eligible ? eligible[x] : (int32_t)x;
-        const int64_t b = off[u], e = off[u + 1];
-        const double w = 1.0 / (double)(e - b);
-        for (int64_t c = b; c < e; ++c) {
-            const int g = group[cols[c]];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) mine[q] += q == g ? w : 0.0;
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) atomicAdd(&acc[q], mine[q]);
-    __syncthreads();
-    if (threadIdx.x < 8) atomicAdd(&share[threadIdx.x], acc[threadIdx.x]);
-}
-
 // USER_REPLACEMENT, after a stable sort of the keys (u << 32 | s) by u: head[u] = the position
 // of user u's first sample, so sample s's rank among its user's samples is its position - head[u]
 __global__ __launch_bounds__(256) void bpr_user_heads_kernel(const uint64_t* __restrict__ sorted,
@@ -559,14 +454,14 @@ constexpr int kBprFlush = 8;  // one wave per XCD writes its L2's dirty lines ba
 template <int LPR, bool SOFT, int AM>
 __global__ __launch_bounds__(256) void bpr_update_kernel(
     const int32_t* __restrict__ tu, const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
-    const int64_t* __restrict__ goff, const unsigned long long* __restrict__ gcnt, int32_t ng,
+    const int64_t* __restrict__ goff, int32_t ng,
     int32_t waves_per_group, float* U, float* V, float* bias, int32_t ld4, uint32_t v_bytes,
     uint32_t b_bytes, uint32_t u_bytes, int32_t flushers, BprScalars s) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const mml::GroupWave gw = mml::group_wave(goff, ng, waves_per_group,
                                               __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
-                                              blockDim.x >> 6, gcnt);
+                                              blockDim.x >> 6);
     const int64_t begin = gw.begin, end = gw.end;
     const int sub = lane / LPR, q = lane % LPR;
     float4* U4 = reinterpret_cast<float4*>(U);
@@ -797,15 +692,6 @@ struct mml_bpr {
     mml::DeviceArray<int32_t> xt_u, xt_i, xt_j;
     mml::DeviceArray<int64_t> span1;
     bool has_groups = false;
-    // the default sampler writing straight into per-group regions of xt_* (bpr_sample_grouped_
-    // kernel): region g = [rg_beg[g], rg_beg[g] + rg_cap[g]), rg_cnt[g] triples in it; sized for
-    // rg_n samples; grouped_last: the last epoch's triples sit in the regions
-    mml::DeviceArray<int64_t> rg_beg, rg_cap;
-    mml::DeviceArray<unsigned long long> rg_cnt;
-    mml::DeviceArray<int32_t> rg_over;
-    std::vector<int64_t> rg_beg_h;
-    int64_t rg_n = -1;
-    bool grouped_last = false;
     // multi-device context: one single-device handle per GPU over a user range ub[d] .. ub[d + 1]
     std::vector<mml_bpr*> shards;
     std::vector<int32_t> ub;
@@ -1382,8 +1268,8 @@ BprXcdMode bpr_xcd_mode(int sampler) {
 
 template <int LPR, bool SOFT>
 void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff,
-                       const unsigned long long* gcnt, const int32_t* tu, const int32_t* ti,
-                       const int32_t* tj, int64_t blocks, int wpb, const BprScalars& s,
+                       const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t blocks,
+                       int wpb, const BprScalars& s,
                        hipStream_t st) {
     const int32_t wpg = (int32_t)(blocks / ng * wpb);
     const uint32_t vb = (uint32_t)std::min<uint64_t>((uint64_t)h->n_items * h->ld * 4, 0xFFFFFFFFull);
@@ -1393,7 +1279,7 @@ void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff,
     if (u_all >= (1ull << 32)) am &= ~kBprUThru;
 #define MML_UPD(AM)                                                                           \
     bpr_update_kernel<LPR, SOFT, AM><<<(int)blocks, 64 * wpb, 0, st>>>(                      \
-        tu, ti, tj, goff, gcnt, ng, wpg, h->U.get(), h->V.get(), h->bias.get(), h->ld / 4, vb, \
+        tu, ti, tj, goff, ng, wpg, h->U.get(), h->V.get(), h->bias.get(), h->ld / 4, vb, \
         bb, ub, mml::flushers_per_xcd(4), s);                                                  \
     h->last_kernel = "bpr_update_kernel<" + std::to_string(LPR) + (SOFT ? ", true, " : ", false, ") + \
                      std::to_string((int)(AM)) + ">"
@@ -1411,14 +1297,14 @@ void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff,
 }
 
 void launch_update(mml_bpr* h, bool soft, int am, int32_t ng, const int64_t* goff,
-                   const unsigned long long* gcnt, const int32_t* tu, const int32_t* ti,
-                   const int32_t* tj, int64_t blocks, int wpb, const BprScalars& s,
+                   const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t blocks,
+                   int wpb, const BprScalars& s,
                    hipStream_t st) {
 #define MML_UPL(LPR)                                                                           \
     if (soft)                                                                                  \
-        launch_update_lpr<LPR, true>(h, am, ng, goff, gcnt, tu, ti, tj, blocks, wpb, s, st);   \
+        launch_update_lpr<LPR, true>(h, am, ng, goff, tu, ti, tj, blocks, wpb, s, st);   \
     else                                                                                       \
-        launch_update_lpr<LPR, false>(h, am, ng, goff, gcnt, tu, ti, tj, blocks, wpb, s, st)
+        launch_update_lpr<LPR, false>(h, am, ng, goff, tu, ti, tj, blocks, wpb, s, st)
     switch (h->lpr) {
         case 1: MML_UPL(1); break;
         case 2: MML_UPL(2); break;
@@ -1430,59 +1316,6 @@ void launch_update(mml_bpr* h, bool soft, int am, int32_t ng, const int64_t* gof
     }
 #undef MML_UPL
     MML_HIP(hipGetLastError());
-}
-
-}  // namespace
-
-namespace {
-
-// MML_BPR_GROUPED=0 keeps the two-pass sampler + XcdSplit::partition (A/B of the grouped sampler)
-bool grouped_sampler_enabled() {
-    static const bool v = [] {
-        const char* e = MML_EXPERIMENT_ENV("MML_BPR_GROUPED");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return v;
-}
-
-// The grouped sampler's regions for an epoch of n samples: region g gets its expected share of
-// the default sampler's i (bpr_group_share_kernel) + 8 standard deviations + one block's run, so an
-// overflow (then the two-pass path runs) is practically never seen.
-void plan_group_regions(mml_bpr* h, int64_t n, hipStream_t st) {
-    mml::DeviceArray<double> share;
-    share.alloc(8);
-    MML_HIP(hipMemsetAsync(share.get(), 0, 8 * sizeof(double), st));
-    const int32_t* elig = h->n_eligible == h->n_users ? nullptr : h->eligible.get();
-    bpr_group_share_kernel<<<grid_for(h->n_eligible, 256, 2048), 256, 0, st>>>(
-        h->off.get(), h->cols.get(), elig, h->n_eligible, h->xs.group.get(), share.get());
-    MML_HIP(hipGetLastError());
-    double sh[8];
-    MML_HIP(hipMemcpyAsync(sh, share.get(), sizeof(sh), hipMemcpyDeviceToHost, st));
-    MML_HIP(hipStreamSynchronize(st));
-    std::vector<int64_t> beg(8), cap(8);
-    int64_t total = 0;
-    for (int g = 0; g < 8; ++g) {
-        const double p = std::max(0.0, sh[g] / (double)h->n_eligible);
-        cap[g] = (int64_t)std::ceil(p * (double)n + 8.0 * std::sqrt(p * (double)n) +
-                                    256.0 * kGrpPer);
-        cap[g] = std::min(cap[g], n);
-        beg[g] = total;
-        total += cap[g];
-    }
-    h->xt_u.reserve(total);
-    h->xt_i.reserve(total);
-    h->xt_j.reserve(total);
-    h->rg_beg.alloc(8);
-    h->rg_cap.alloc(8);
-    h->rg_cnt.alloc(8);
-    h->rg_over.alloc(1);
-    MML_HIP(hipMemcpyAsync(h->rg_beg.get(), beg.data(), sizeof(int64_t) * 8,
-                           hipMemcpyHostToDevice, st));
-    MML_HIP(hipMemcpyAsync(h->rg_cap.get(), cap.data(), sizeof(int64_t) * 8,
-                           hipMemcpyHostToDevice, st));
-    MML_HIP(hipStreamSynchronize(st));
-    h->rg_beg_h = beg;
-    h->rg_n = n;
 }
 
 }  // namespace
@@ -1590,21 +1423,17 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         if (part && !h->has_groups) {
             h->xs.set_groups(st, mml::device_id_counts(st, h->cols.get(), h->nnz, h->n_items), 8);
             h->has_groups = true;
-            h->rg_n = -1;
         }
-        // the default sampler draws straight into the groups' regions (no tri_* copy, no
-        // count / scatter pass)
-        bool grouped = part && h->p.sampler == MML_BPR_SAMPLER_UNIFORM_USER &&
-                       grouped_sampler_enabled() && n <= (int64_t)INT32_MAX * 64;
-        if (grouped && h->rg_n != n) plan_group_regions(h, n, st);
-        auto alloc_tri = [&] {
-            if ((int64_t)h->tri_u.count < n) {
-                h->tri_u.alloc(n);
-                h->tri_i.alloc(n);
-                h->tri_j.alloc(n);
-            }
-        };
-        if (!fused && n > 0 && !grouped) alloc_tri();
+        if (!fused && n > 0 && (int64_t)h->tri_u.count < n) {
+            h->tri_u.alloc(n);
+            h->tri_i.alloc(n);
+            h->tri_j.alloc(n);
+        }
+        if (part && (int64_t)h->xt_u.count < n) {
+            h->xt_u.alloc(n);
+            h->xt_i.alloc(n);
+            h->xt_j.alloc(n);
+        }
         // USER_REPLACEMENT: rank keys, their sorted copy, per-user heads and the sort's scratch
         int rank_end_bit = 0;
         size_t rank_tmp_bytes = 0;
@@ -1623,27 +1452,8 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             if (h->rank_tmp.count < rank_tmp_bytes) h->rank_tmp.alloc(rank_tmp_bytes);
         }
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
-        if (grouped) {
-            MML_HIP(hipMemsetAsync(h->rg_cnt.get(), 0, 8 * sizeof(unsigned long long), st));
-            MML_HIP(hipMemsetAsync(h->rg_over.get(), 0, sizeof(int32_t), st));
-            const int32_t* elig = h->n_eligible == h->n_users ? nullptr : h->eligible.get();
-            const int64_t gb = (n + 256 * kGrpPer - 1) / (256 * kGrpPer);
-            bpr_sample_grouped_kernel<<<(int)gb, 256, 0, st>>>(
-                h->cols.get(), elig, h->n_eligible, n, h->n_items, seed, h->recs.get(),
-                h->xs.group.get(), h->rg_beg.get(), h->rg_cap.get(), h->rg_cnt.get(),
-                h->xt_u.get(), h->xt_i.get(), h->xt_j.get(), h->rg_over.get());
-            MML_HIP(hipGetLastError());
-            int32_t over = 0;
-            MML_HIP(hipMemcpyAsync(&over, h->rg_over.get(), sizeof(int32_t),
-                                   hipMemcpyDeviceToHost, st));
-            MML_HIP(hipStreamSynchronize(st));
-            if (over) {  // a region filled up: the same triples through the two-pass path
-                grouped = false;
-                alloc_tri();
-            }
-        }
-        if (!fused && n > 0 && !grouped) {
-            const int sgrid = (int)std::min<int64_t>(256 * 64, (n + 255) / 256);
+        const int sgrid = (int)std::min<int64_t>(256 * 64, (n + 255) / 256);
+        if (!fused && n > 0) {
             if (weighted) {
                 h->fail.alloc(1);
                 MML_HIP(hipMemsetAsync(h->fail.get(), 0, sizeof(int32_t), st));
@@ -1693,24 +1503,11 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         }
         int32_t ng = 1;
         const int64_t* goff = h->span1.get();
-        const unsigned long long* gcnt = nullptr;
         const int32_t *tu = h->tri_u.get(), *ti = h->tri_i.get(), *tj = h->tri_j.get();
         // the access flags need the buffer resource (V < 4 GiB) and, for the owner modes, the
         // groups; a one-workgroup epoch keeps plain accesses (one CU, one L2)
         const int am = v_fits && waves >= 16 && (part || !xm.partition) ? xm.am : 0;
-        if (grouped) {
-            ng = 8;
-            goff = h->rg_beg.get();
-            gcnt = h->rg_cnt.get();
-            tu = h->xt_u.get();
-            ti = h->xt_i.get();
-            tj = h->xt_j.get();
-        } else if (part) {  // stable partition of the sampled triples (XcdSplit)
-            if ((int64_t)h->xt_u.count < n) {
-                h->xt_u.alloc(n);
-                h->xt_i.alloc(n);
-                h->xt_j.alloc(n);
-            }
+        if (part) {  // stable partition of the sampled triples (XcdSplit)
             const int32_t* in[3] = {tu, ti, tj};
             int32_t* out[3] = {h->xt_u.get(), h->xt_i.get(), h->xt_j.get()};
             h->xs.partition(st, ti, n, 3, in, out);
@@ -1736,7 +1533,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             // triples in flight and no stale per-XCD replicas
             launch_apply_ordered(h, tu, ti, tj, n, s, st, 4, weighted_streams(h) / 4);
         } else if (!ordered && !fused && n > 0) {
-            launch_update(h, soft, am, ng, goff, gcnt, tu, ti, tj, blocks, 4, s, st);
+            launch_update(h, soft, am, ng, goff, tu, ti, tj, blocks, 4, s, st);
         } else if (fused) {
 #define MML_BPR(LPR)                                                                            \
     if (pair)                                                                                   \
@@ -1766,7 +1563,6 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));
         MML_HIP(hipEventElapsedTime(&h->last_update_ms, h->ctx->ev_mid, h->ctx->ev_end));
         h->has_triples = !fused && n > 0;
-        h->grouped_last = grouped;
     });
 }
 
@@ -1792,27 +1588,6 @@ extern "C" mml_status mml_bpr_last_triples(mml_bpr* h, int32_t* users, int32_t* 
                     "n must equal the epoch's sample count (Feedback.Count)");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
-        if (h->grouped_last) {  // the regions one after another (group order)
-            unsigned long long cnt[8];
-            MML_HIP(hipMemcpyAsync(cnt, h->rg_cnt.get(), sizeof(cnt), hipMemcpyDeviceToHost, st));
-            MML_HIP(hipStreamSynchronize(st));
-            int64_t o = 0;
-            for (int g = 0; g < 8; ++g) {
-                const int64_t b = h->rg_beg_h[g], c = (int64_t)cnt[g];
-                MML_REQUIRE(o + c <= n, "grouped triples exceed the epoch's sample count");
-                if (!c) continue;
-                MML_HIP(hipMemcpyAsync(users + o, h->xt_u.get() + b, sizeof(int32_t) * c,
-                                       hipMemcpyDeviceToHost, st));
-                MML_HIP(hipMemcpyAsync(items + o, h->xt_i.get() + b, sizeof(int32_t) * c,
-                                       hipMemcpyDeviceToHost, st));
-                MML_HIP(hipMemcpyAsync(other_items + o, h->xt_j.get() + b, sizeof(int32_t) * c,
-                                       hipMemcpyDeviceToHost, st));
-                o += c;
-            }
-            MML_HIP(hipStreamSynchronize(st));
-            MML_REQUIRE(o == n, "grouped triples do not add up to the epoch's sample count");
-            return;
-        }
         MML_HIP(hipMemcpyAsync(users, h->tri_u.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost,
                                st));
         MML_HIP(hipMemcpyAsync(items, h->tri_i.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost,

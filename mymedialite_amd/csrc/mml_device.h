@@ -27,9 +27,8 @@ __device__ __forceinline__ float load1_l2(__amdgpu_buffer_rsrc_t r, uint32_t byt
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 16));
 }
 
-// Stream spans of the XCD-owned item groups: group g's entries are [off[g], off[g + 1]), or
-// [off[g], off[g] + cnt[g]) when the groups are separate regions (cnt != null: BPR's grouped
-// sampler).  Block b serves group b % ng (blocks b and b + 8 share an XCD, probed by
+// Stream spans of the XCD-owned item groups: group g's entries are [off[g], off[g + 1]).  Block b
+// serves group b % ng (blocks b and b + 8 share an XCD, probed by
 // mml::xcd_groups), so each group's rows are only ever cached in one XCD's L2.  ng = 1: one span,
 // any block.
 struct GroupWave {
@@ -37,11 +36,10 @@ struct GroupWave {
 };
 __device__ __forceinline__ GroupWave group_wave(const int64_t* __restrict__ goff, int32_t ng,
                                                 int32_t waves_per_group, int wave_in_block,
-                                                int waves_per_block,
-                                                const unsigned long long* cnt = nullptr) {
+                                                int waves_per_block) {
     const int g = (int)(blockIdx.x % (uint32_t)ng);
     const int64_t w = (int64_t)(blockIdx.x / (uint32_t)ng) * waves_per_block + wave_in_block;
-    const int64_t g0 = goff[g], g1 = cnt ? g0 + (int64_t)cnt[g] : goff[g + 1];
+    const int64_t g0 = goff[g], g1 = goff[g + 1];
     const int64_t chunk = (g1 - g0 + waves_per_group - 1) / waves_per_group;
     const int64_t b = min(g0 + w * chunk, g1);
     return GroupWave{b, min(b + chunk, g1)};

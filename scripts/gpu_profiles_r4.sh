@@ -40,7 +40,8 @@ step pmc_c5 400 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE
 python scripts/pmc_summary.py gpurun_out/pmc_c5_$TAG wrmf > gpurun_out/pmc_c5_${TAG}_summary.txt 2>&1
 rm -rf gpurun_out/pmc_c5_$TAG
 head -30 gpurun_out/pmc_c5_${TAG}_summary.txt
-# A/B of the grouped BPR sampler against the two-pass sampler + XcdSplit partition (experiments
+# A/B of the grouped BPR sampler (removed after this A/B: 4 ms slower per C3 epoch) against the
+# two-pass sampler + XcdSplit partition (experiments
 # build; MML_BPR_GROUPED=0 selects the two-pass path): kernel stats of both
 export MML_LIB_PATH=variants/exp/libmml_hip.so
 for g in 1 0; do
