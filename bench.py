@@ -798,7 +798,7 @@ def wrmf_row_check(h, ku, ki, deg_u, deg_i, n_users, n_items, k):
     V1 = np.empty((n_items, k), np.float32)
     N.check(N.lib().mml_wrmf_get_model(h, N.ptr(U1, N._f32p), N.ptr(V1, N._f32p)))
     rs = np.random.default_rng(5)
-    out, n_rows = {}, 0
+    out, n_rows, n_side = {}, 0, {}
     for side, W, H, deg, picks in (
             ("user", U1, V0, deg_u.cpu().numpy(), [(1, 128, 64)]),
             ("item", V1, U1, deg_i.cpu().numpy(), [(1, 128, 8), (129, 8192, 8), (8193, 20000, 8)])):
@@ -811,9 +811,11 @@ def wrmf_row_check(h, ku, ki, deg_u, deg_i, n_users, n_items, k):
         rel = O.wrmf_rows_check(rows, *((ku, ki) if side == "user" else (ki, ku)), W, H, k)
         out[side] = float(rel.max())
         n_rows += len(rows)
+        n_side[side] = len(rows)
     return {"row_check_max_rel": max(out.values()), "row_check_by_side": out,
             "row_check_note": f"one further fp64-mode iteration after the timed ones; {n_rows} "
-                              f"sampled rows (64 user rows, 24 item rows over the Woodbury / "
+                              f"sampled rows ({n_side['user']} user rows, {n_side['item']} item rows "
+                              f"over the Woodbury / "
                               f"direct / split-Gram buckets) vs the oracle's fp64 row solve with "
                               f"exact float products (WRMF.cs:110-156), max |dW| / (1 + |W|); "
                               f"bar 2e-7 ({time.perf_counter() - t0:.0f} s)"}

@@ -1710,7 +1710,8 @@ wrmf_wood_cg_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, const int64_t* __restrict__ off,
     const int32_t* __restrict__ cols, const float* __restrict__ Q, int32_t k, float alpha,
     const float* __restrict__ S, float* __restrict__ Tout, int32_t max_it, float tol2,
-    float skip2, float abs2, int32_t cheb_m, float cheb_theta, float cheb_delta) {
+    float skip2, float abs2, int32_t cheb_m, float cheb_theta, float cheb_delta,
+    float cheb_acosh) {
     static_assert(NJ == 32 || NJ == 64 || NJ == 96 || NJ == 128, "NJ: 32, 64, 96 or 128");
     static_assert(NJ % PARTS == 0 && NJ / PARTS <= 64, "parts of <= 64 items");
     constexpr int HALVES = PARTS;
@@ -1818,20 +1819,38 @@ wrmf_wood_cg_kernel(
         float w = 0.0f, r = t < deg ? y : 0.0f, p = 0.0f, sv = 0.0f;
         float g_prev = 1.0f, a_prev = 1.0f, stop = 0.0f;
         if (cheb_m > 0) {
-            // Chebyshev iteration on the known spectrum [1/alpha, 1/alpha + 1] (centre theta,
+            // Chebyshev iteration on a spectrum bound [1/alpha, 1/alpha + b] (centre theta,
             // half-width delta): no inner products, so no block reduction and no barrier beyond
-            // the mat-vec's own; cheb_m updates take cheb_m - 1 mat-vecs
-            const float s1 = cheb_theta / cheb_delta;
-            float dv = r / cheb_theta, rho_p = 1.0f / s1;
-            for (int it = 0; it < cheb_m; ++it) {
+            // the mat-vec's own; m updates take m - 1 mat-vecs.  b = min(1, tr): Q_S Q_S^T <=
+            // Q^T Q <= I bounds it by 1 (the host's cheb_m, theta, delta), and its largest
+            // eigenvalue is at most its trace tr = sum_{j in S} |q_j|^2, which for a row of a
+            // few hundred entries out of hundreds of thousands is far below 1 (q_j's squared norm
+            // is item j's leverage, summing to k over all rows): the same relative error bound
+            // 2 / T_m(theta / delta) then takes m = acosh(2 / tol) / acosh(1 + 2 / (alpha b)) + 1
+            // updates instead of the worst case's (C5 users: ~4 instead of 10)
+            float qq = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NL; ++j) qq += q[j] * q[j];
+            const float tr = block_sum2<WAVES>(qq, 0.0f, sdot[1]).x;
+            int m = cheb_m;
+            float theta = cheb_theta, delta = cheb_delta;
+            if (cheb_acosh > 0.0f && tr < 1.0f) {
+                const float b = fmaxf(tr, 1e-20f);
+                m = min(cheb_m, (int)ceilf(cheb_acosh / acoshf(1.0f + 2.0f / (alpha * b))) + 1);
+                theta = ainv + 0.5f * b;
+                delta = 0.5f * b;
+            }
+            const float s1 = theta / delta;
+            float dv = r / theta, rho_p = 1.0f / s1;
+            for (int it = 0; it < m; ++it) {
                 w += dv;
-                if (it + 1 == cheb_m) break;
+                if (it + 1 == m) break;
                 if (t < NJ) sp[t] = dv;
                 __syncthreads();
                 const float uf = qt_times();
                 r -= (t < deg ? dv * ainv : 0.0f) + qs_times(uf);  // r -= C d
                 const float rho = 1.0f / (2.0f * s1 - rho_p);
-                dv = rho * rho_p * dv + (2.0f * rho / cheb_delta) * r;
+                dv = rho * rho_p * dv + (2.0f * rho / delta) * r;
                 rho_p = rho;
             }
         }
@@ -1936,26 +1955,32 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
     const int cheb_m = (S || main_cg || (debug_mask() & 64))
                            ? 0
                            : (int)std::ceil(std::acosh(2.0 / tol) / std::acosh(theta / delta)) + 1;
+    // the per-row bound's numerator (the kernel takes the smaller of the two counts)
+    static const bool row_bound = [] {  // MML_WRMF_CHEB_TRACE=0 (experiments builds): worst case only
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_CHEB_TRACE");
+        return !(e && std::string(e) == "0");
+    }();
+    const float cheb_acosh = row_bound ? (float)std::acosh(2.0 / tol) : -1.0f;
     if (g == 0)
         wrmf_wood_cg_kernel<32><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
                                                       max_it, tol2, skip2, abs2, cheb_m,
-                                                      (float)theta, (float)delta);
+                                                      (float)theta, (float)delta, cheb_acosh);
     else if (g == 1)
         wrmf_wood_cg_kernel<64><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
                                                       max_it, tol2, skip2, abs2, cheb_m,
-                                                      (float)theta, (float)delta);
+                                                      (float)theta, (float)delta, cheb_acosh);
     else if (wood128_parts() == 4)
         wrmf_wood_cg_kernel<128, 4><<<grid, 1024, 0, st>>>(
             rows, n, off, cols, Q, k, alpha, S, Tout, max_it, tol2, skip2, abs2, cheb_m,
-            (float)theta, (float)delta);
+            (float)theta, (float)delta, cheb_acosh);
     else if (g == 2 && wood96())
         wrmf_wood_cg_kernel<96><<<grid, 768, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
                                                       max_it, tol2, skip2, abs2, cheb_m,
-                                                      (float)theta, (float)delta);
+                                                      (float)theta, (float)delta, cheb_acosh);
     else
         wrmf_wood_cg_kernel<128><<<grid, 512, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
                                                        max_it, tol2, skip2, abs2, cheb_m,
-                                                       (float)theta, (float)delta);
+                                                       (float)theta, (float)delta, cheb_acosh);
 }
 
 // Y[yrow(r)] = scale * X[xrow(r)] * M for n rows (X, Y row-major [.. x k], M [k x k] row-major,
