@@ -52,7 +52,10 @@ constexpr int kSlots = (kTiles + kWaves - 1) / kWaves;   // 6 tiles per wave
 constexpr int kCH = 16;                                  // gathered vectors per LDS chunk
 constexpr int kHSW = 32 * kNR;                           // staged vector width
 constexpr int kPS = 34;                                  // panel row stride (conflict-free reads)
-constexpr int kRB = 4;    // Gram: raw fp32 chunks in the LDS ring (kRB - 1 chunks of gathers in flight)
+#ifndef MML_GRAM_RB  // A/B variants (scripts/build_variant.sh "-DMML_GRAM_RB=5")
+#define MML_GRAM_RB 4
+#endif
+constexpr int kRB = MML_GRAM_RB;  // Gram: raw fp32 chunks in the LDS ring (kRB - 1 chunks of gathers in flight)
 constexpr int kRS = 260;  // raw row stride in floats (1 KiB of row + pad: conflict-free reads)
 #ifdef MML_NO_GRAM_RING  // A/B variant (scripts/build_variant.sh): the register-staged Gram only
 constexpr bool kGramRing = false;
@@ -64,6 +67,11 @@ constexpr int kPP = 40;  // bf16 panel-plane row stride (80 B: conflict-free 16-
 constexpr bool kFactorX3 = false;
 #else
 constexpr bool kFactorX3 = true;
+#endif
+#ifdef MML_FACTOR_PRIO  // A/B variant (scripts/build_variant.sh): the lookahead wave at priority 2
+constexpr bool kFactorPrio = true;
+#else
+constexpr bool kFactorPrio = false;
 #endif
 constexpr int kDS = 33;                                  // diagonal-tile / reduction row stride
 constexpr int kTS = 33;                                  // T_J^T row stride (conflict-free rows)
@@ -1002,6 +1010,9 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
             __syncthreads();
             // (d) trailing update A'_IK -= L_KJ L_IJ^T, K > J; tile (J+1, J+1) first, then factored
             if (J + 1 < nt && (tdn % kWaves) == wave) {
+                // the lookahead is the factorisation's critical path: its wave issues first on a
+                // SIMD whose other wave is applying trailing updates (same matrix pipe)
+                if constexpr (kFactorPrio) __builtin_amdgcn_s_setprio(2);
                 const int own = tdn / kWaves;
 #pragma unroll
                 for (int s = 0; s < kSlots; ++s) {
@@ -1017,6 +1028,7 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
                     }
                 }
                 if (!(dbg & 1)) factor_tile(sm, acc, own, sm.tT[(J + 1) & 1]);
+                if constexpr (kFactorPrio) __builtin_amdgcn_s_setprio(0);
             }
 #pragma unroll
             for (int s = 0; s < kSlots; ++s) {
@@ -1883,6 +1895,204 @@ wrmf_wood_cg_kernel(
     }
 }
 
+// Woodbury rows of 65 .. 128 items on a 16 x 4 register block per thread.  Wave w owns items
+// 16 w .. 16 w + 15 of the row and lane l features 4 l .. 4 l + 3 (one float4 of each item's Q
+// row, so a gather is one 1 KiB row per wave-instruction).  Both mat-vecs of a step are register
+// FMAs over the block:
+//   z = Q_S u: 16 partial sums per lane, then a transposing butterfly inside the wave (16 values
+//     over 64 lanes: item j0 + l / 4 ends in lanes 4 j .. 4 j + 3), no LDS;
+//   u = Q_S^T p: p_j from v_readlane of its lane, 4 partial sums per lane, then the waves'
+//     partials summed through the LDS in wave order (the step's only barrier).
+// wrmf_wood_cg_kernel<128> spends three barriers and a 64-value butterfly per step, and its
+// z sums cross four waves through the LDS.  Same parameters, same arithmetic (Chebyshev main
+// solve, CG refinement), same output t.
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 4) void wrmf_wood_w16_kernel(
+    const int32_t* __restrict__ rows, int32_t n_list, const int64_t* __restrict__ off,
+    const int32_t* __restrict__ cols, const float* __restrict__ Q, int32_t k, float alpha,
+    const float* __restrict__ S, float* __restrict__ Tout, int32_t max_it, float tol2,
+    float skip2, float abs2, int32_t cheb_m, float cheb_theta, float cheb_delta,
+    float cheb_acosh) {
+    static_assert(WAVES >= 1 && WAVES <= 8, "16 items per wave, <= 128 items");
+    __shared__ float4 pu[2][WAVES][64];   // the waves' partial u, alternated per mat-vec
+    __shared__ float sdot[2][2 * WAVES];  // block_sum2, alternated per CG step
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int f0 = 4 * lane;
+    const bool vec = (k & 3) == 0;
+    const float ainv = 1.0f / alpha;
+    int par = 0;
+    for (int li = blockIdx.x; li < n_list; li += gridDim.x) {
+        const int32_t row = rows[li];
+        const int64_t rb = off[row];
+        const int deg = (int)(off[row + 1] - rb);
+        const int j0 = 16 * wave;
+        const int nloc = __builtin_amdgcn_readfirstlane(max(0, min(16, deg - j0)));
+        const bool live = j0 + (lane >> 2) < deg;  // the item this lane carries the state of
+        __syncthreads();  // the previous row is done with the LDS
+        float sf[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (S) {
+            // refinement: |d|_2 <= |L^-1|_2 |s|_2 (wrmf_wood_cg_kernel), a wave holds all of s
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                sf[c] = f0 + c < k ? S[(int64_t)li * k + f0 + c] : 0.0f;
+            float ss = (sf[0] * sf[0] + sf[1] * sf[1]) + (sf[2] * sf[2] + sf[3] * sf[3]);
+            ss = pstage<0>(ss);
+            ss = pstage<1>(ss);
+            ss = pstage<2>(ss);
+            ss = pstage<3>(ss);
+            ss = pstage<4>(ss);
+            ss = pstage<5>(ss);
+            if (ss <= skip2) {  // the same sum in every wave: a workgroup-uniform branch
+                if (wave == 0)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        if (f0 + c < k) Tout[(int64_t)li * k + f0 + c] = 0.0f;
+                continue;
+            }
+        }
+        const int idv = lane < nloc ? cols[rb + j0 + lane] : 0;
+        // qp[c][jp] = (Q_S[2 jp][f0 + c], Q_S[2 jp + 1][f0 + c]): item pairs as packed operands
+        f32x2 qp[4][8];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int id = __builtin_amdgcn_readlane(idv, j);
+            const float* src = Q + (int64_t)id * k + f0;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (j < nloc) {
+                if (vec) {
+                    if (f0 < k) v = *reinterpret_cast<const float4*>(src);
+                } else {
+                    v.x = f0 < k ? src[0] : 0.0f;
+                    v.y = f0 + 1 < k ? src[1] : 0.0f;
+                    v.z = f0 + 2 < k ? src[2] : 0.0f;
+                    v.w = f0 + 3 < k ? src[3] : 0.0f;
+                }
+            }
+            qp[0][j >> 1][j & 1] = v.x;
+            qp[1][j >> 1][j & 1] = v.y;
+            qp[2][j >> 1][j & 1] = v.z;
+            qp[3][j >> 1][j & 1] = v.w;
+        }
+        // z_j = sum_f Q_S[j][f] u_f for this wave's items: the lane's value for item j0 + l / 4
+        auto z_of = [&](const float (&u)[4]) -> float {
+            if (nloc == 0) return 0.0f;
+            float v[16];
+#pragma unroll
+            for (int jp = 0; jp < 8; ++jp) {
+                f32x2 a = qp[0][jp] * f32x2{u[0], u[0]};
+#pragma unroll
+                for (int c = 1; c < 4; ++c)
+                    a = __builtin_elementwise_fma(qp[c][jp], f32x2{u[c], u[c]}, a);
+                v[2 * jp] = a.x;
+                v[2 * jp + 1] = a.y;
+            }
+            XorReduce<16, 16, 0>::run(v, lane);
+            return v[0];
+        };
+        // u_f = sum_j Q_S[j][f] p_j (p_j = the state value of item j's lanes), every wave gets all
+        // four of its features, summed over the waves in order
+        auto u_of = [&](float pl, float (&u)[4]) {
+            float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (nloc > 0) {
+                f32x2 pp[8];
+#pragma unroll
+                for (int jp = 0; jp < 8; ++jp)
+                    pp[jp] = f32x2{lane_bcast(pl, 8 * jp), lane_bcast(pl, 8 * jp + 4)};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    f32x2 acc = qp[c][0] * pp[0];
+#pragma unroll
+                    for (int jp = 1; jp < 8; ++jp) acc = __builtin_elementwise_fma(qp[c][jp], pp[jp], acc);
+                    a[c] = acc.x + acc.y;
+                }
+            }
+            pu[par][wave][lane] = make_float4(a[0], a[1], a[2], a[3]);
+            __syncthreads();
+            float4 s = pu[par][0][lane];
+#pragma unroll
+            for (int w = 1; w < WAVES; ++w) {
+                const float4 x = pu[par][w][lane];
+                s.x += x.x;
+                s.y += x.y;
+                s.z += x.z;
+                s.w += x.w;
+            }
+            par ^= 1;
+            u[0] = s.x;
+            u[1] = s.y;
+            u[2] = s.z;
+            u[3] = s.w;
+        };
+        const float y = S ? z_of(sf) : (live ? 1.0f : 0.0f);
+        float w = 0.0f, r = live ? y : 0.0f, p = 0.0f, sv = 0.0f;
+        float g_prev = 1.0f, a_prev = 1.0f, stop = 0.0f;
+        float u[4];
+        if (cheb_m > 0) {
+            // Chebyshev iteration on [1/alpha, 1/alpha + b], b = min(1, trace) (wrmf_wood_cg_kernel)
+            f32x2 q2 = {0.0f, 0.0f};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int jp = 0; jp < 8; ++jp) q2 = __builtin_elementwise_fma(qp[c][jp], qp[c][jp], q2);
+            const float tr = block_sum2<WAVES>(q2.x + q2.y, 0.0f, sdot[1]).x;
+            int m = cheb_m;
+            float theta = cheb_theta, delta = cheb_delta;
+            if (cheb_acosh > 0.0f && tr < 1.0f) {
+                const float b = fmaxf(tr, 1e-20f);
+                m = min(cheb_m, (int)ceilf(cheb_acosh / acoshf(1.0f + 2.0f / (alpha * b))) + 1);
+                theta = ainv + 0.5f * b;
+                delta = 0.5f * b;
+            }
+            const float s1 = theta / delta;
+            float dv = r / theta, rho_p = 1.0f / s1;
+            for (int it = 0; it < m; ++it) {
+                w += dv;
+                if (it + 1 == m) break;
+                u_of(dv, u);
+                r -= (live ? dv * ainv : 0.0f) + z_of(u);  // r -= C d
+                const float rho = 1.0f / (2.0f * s1 - rho_p);
+                dv = rho * rho_p * dv + (2.0f * rho / delta) * r;
+                rho_p = rho;
+            }
+        }
+        // CG (Chronopoulos-Gear, one fused reduction per step): each item counted by one lane
+        const bool own = (lane & 3) == 0;
+        for (int it = 0; it <= (cheb_m > 0 ? -1 : max_it); ++it) {
+            u_of(r, u);
+            const float cr = (live ? r * ainv : 0.0f) + z_of(u);  // C r
+            const float2 gd = block_sum2<WAVES>(own ? r * r : 0.0f, own ? cr * r : 0.0f,
+                                                sdot[it & 1]);
+            if (it == 0) stop = fmaxf(tol2 * gd.x, abs2);
+            if (gd.x <= stop || it == max_it) break;
+            const float b = it == 0 ? 0.0f : gd.x / g_prev;
+            const float a = it == 0 ? gd.x / gd.y : gd.x / (gd.y - b * gd.x / a_prev);
+            p = r + b * p;
+            sv = cr + b * sv;  // C p
+            w += a * p;
+            r -= a * sv;
+            g_prev = gd.x;
+            a_prev = a;
+        }
+        u_of(live ? w : 0.0f, u);  // t = Q_S^T w
+        if (wave == 0)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (f0 + c < k) Tout[(int64_t)li * k + f0 + c] = S ? sf[c] - u[c] : u[c];
+    }
+}
+
+// MML_WRMF_WOOD16 (experiments builds): 0 = rows of 97 .. 128 items on wrmf_wood_cg_kernel<128>,
+// 2 = rows of 65 .. 96 items on wrmf_wood_w16_kernel<8> too (default 1: 97 .. 128 only)
+int wood_w16_mode() {
+    static const int v = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOOD16");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+bool wood_w16() { return wood_w16_mode() > 0; }
+
 // MML_WRMF_WOOD=chol keeps the Cholesky Woodbury kernel (A/B measurements); the default solves
 // the Woodbury rows by CG
 bool wood_cg() {
@@ -1961,7 +2171,11 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
         return !(e && std::string(e) == "0");
     }();
     const float cheb_acosh = row_bound ? (float)std::acosh(2.0 / tol) : -1.0f;
-    if (g == 0)
+    if ((g == 3 && wood_w16()) || (g == 2 && wood_w16_mode() == 2))
+        wrmf_wood_w16_kernel<8><<<grid, 64 * 8, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
+                                                         max_it, tol2, skip2, abs2, cheb_m,
+                                                         (float)theta, (float)delta, cheb_acosh);
+    else if (g == 0)
         wrmf_wood_cg_kernel<32><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
                                                       max_it, tol2, skip2, abs2, cheb_m,
                                                       (float)theta, (float)delta, cheb_acosh);
