@@ -68,11 +68,6 @@ constexpr bool kFactorX3 = false;
 #else
 constexpr bool kFactorX3 = true;
 #endif
-#ifdef MML_FACTOR_PRIO  // A/B variant (scripts/build_variant.sh): the lookahead wave at priority 2
-constexpr bool kFactorPrio = true;
-#else
-constexpr bool kFactorPrio = false;
-#endif
 constexpr int kDS = 33;                                  // diagonal-tile / reduction row stride
 constexpr int kTS = 33;                                  // T_J^T row stride (conflict-free rows)
 
@@ -1010,9 +1005,6 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
             __syncthreads();
             // (d) trailing update A'_IK -= L_KJ L_IJ^T, K > J; tile (J+1, J+1) first, then factored
             if (J + 1 < nt && (tdn % kWaves) == wave) {
-                // the lookahead is the factorisation's critical path: its wave issues first on a
-                // SIMD whose other wave is applying trailing updates (same matrix pipe)
-                if constexpr (kFactorPrio) __builtin_amdgcn_s_setprio(2);
                 const int own = tdn / kWaves;
 #pragma unroll
                 for (int s = 0; s < kSlots; ++s) {
@@ -1028,7 +1020,6 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
                     }
                 }
                 if (!(dbg & 1)) factor_tile(sm, acc, own, sm.tT[(J + 1) & 1]);
-                if constexpr (kFactorPrio) __builtin_amdgcn_s_setprio(0);
             }
 #pragma unroll
             for (int s = 0; s < kSlots; ++s) {
