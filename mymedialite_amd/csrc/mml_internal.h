@@ -169,6 +169,10 @@ struct WrmfTilePlan {
     struct Refine {
         DeviceArray<double> rpartial, x64, r64;
         DeviceArray<float> rf, df, factor;
+        // the direct rows' Gram vectors split once per half-step into three bf16 planes
+        // (wrmf_split_planes_kernel), of the H planes_of points at (h_rows + 1 rows)
+        DeviceArray<uint16_t> planes;
+        const float* planes_of = nullptr;
         // the last pass's largest relative correction (float bits): [0] direct rows, [1] Woodbury
         DeviceArray<unsigned> dmax;
     };

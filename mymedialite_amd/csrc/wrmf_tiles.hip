@@ -57,6 +57,11 @@ constexpr int kPS = 34;                                  // panel row stride (co
 #endif
 constexpr int kRB = MML_GRAM_RB;  // Gram: raw fp32 chunks in the LDS ring (kRB - 1 chunks of gathers in flight)
 constexpr int kRS = 260;  // raw row stride in floats (1 KiB of row + pad: conflict-free reads)
+constexpr int kPW = 256;  // pre-split plane row: k <= 256 bf16, zero-padded (512 B)
+#ifndef MML_GRAM_RBP  // A/B variants: chunks in the planes ring (kRBP - 1 chunks of gathers in flight)
+#define MML_GRAM_RBP 4
+#endif
+constexpr int kRBP = MML_GRAM_RBP;
 #ifdef MML_NO_GRAM_RING  // A/B variant (scripts/build_variant.sh): the register-staged Gram only
 constexpr bool kGramRing = false;
 #else
@@ -115,6 +120,9 @@ struct Smem {
             alignas(16) uint16_t pp[kNT][3][32][kPP];
         } fz;
         float red[kNT][32][kDS];        // backward: per-tile partial products
+        // Gram from pre-split planes (gram_accumulate_p3): kRB chunks x 3 planes x kCH vectors x
+        // kPW bf16, vector v's 16-B chunk ch at position ch ^ ((v & 3) << 2)
+        alignas(16) uint16_t gp[kRBP][3][kCH][kPW];
     } u;
     float tT[2][32][kTS];               // tT[c][m] = T_J[m][c], double-buffered (lookahead)
     float yv[kHSW];
@@ -639,6 +647,118 @@ __device__ __forceinline__ void gram_accumulate_x3g(Smem& sm, f32x16 (&acc)[kSlo
     }
 }
 
+// The same Gram from planes split ONCE per half-step (wrmf_split_planes_kernel: x = x0 + x1 + x2,
+// three bf16 rows of kPW per vector, row zrow all zero).  A chunk's 16 vectors go global -> LDS
+// (global_load_lds_dwordx4, three 1-KiB pieces per wave: vectors 2w and 2w + 1 of one plane) as a
+// vector-major image, and the MFMA operands come out of it transposed by ds_read_b64_tr_b16 (lane
+// (q, h) of a 32-feature block gets vectors 8h .. 8h + 7 of feature q: two reads of 4 vectors).
+// No conversion pass, no LDS stores from registers: per chunk a wave issues its gathers, waits for
+// the chunk kRB - 1 back, and runs the MFMAs.  The b-row tiles take A = the feature block and B =
+// 1 on feature kb (lane q = 0), three MFMAs (one per plane) instead of the VALU sums.
+// Swizzle: in the image, vector v's 16-B chunk ch sits at position ch ^ ((v & 3) << 2); the gather
+// lanes fetch the permuted source chunks (the DMA writes lane-linearly), and a transposed read's
+// four vectors v = 4m .. 4m + 3 then take four distinct 64-B bank groups (conflict-free).
+using v4s = __attribute__((ext_vector_type(4))) short;
+__device__ __forceinline__ v4s lds_tr16(const uint16_t* p) {
+    using lp = __attribute__((address_space(3))) v4s*;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lp)(__attribute__((address_space(3))) void*)(p));
+}
+__device__ __forceinline__ void gram_accumulate_p3(Smem& sm, f32x16 (&acc)[kSlots], Tiles& tl,
+                                                   int nslot, const int32_t* __restrict__ cols,
+                                                   int64_t b, int64_t e,
+                                                   const uint16_t* __restrict__ P, int64_t ps,
+                                                   int32_t zrow, int hsw) {
+    static_assert(kCH == 16 && kThreads == 512, "two vectors per wave and chunk");
+    static_assert(kRBP >= 3, "at least one chunk of gathers in flight beyond the current one");
+    const int t = opaque_tid(), lane = t & 63, q = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int ntb = hsw / 32 - 1;
+    if (e <= b) return;
+    const int64_t nch = (e - b + kCH - 1) / kCH;
+    const int vh = lane >> 5, v = 2 * wave + vh;
+    const int gpos = (lane & 31) ^ ((v & 3) << 2);  // the logical chunk this lane's DMA fetches
+    auto ids = [&](int64_t c, int32_t& i0, int32_t& i1) {
+        const int64_t e0 = b + c * kCH + 2 * wave;
+        i0 = e0 < e ? cols[e0] : zrow;
+        i1 = e0 + 1 < e ? cols[e0 + 1] : zrow;
+    };
+    auto gather = [&](int64_t c, int32_t i0, int32_t i1) {
+        const int slot = (int)(c % kRBP);
+        const uint16_t* src = P + (int64_t)(vh ? i1 : i0) * kPW + 8 * gpos;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+            glds16(reinterpret_cast<const float*>(src + p * ps),
+                   lds_addr_of(&sm.u.gp[slot][p][2 * wave][0]));
+    };
+    // transposed operand reads: lane 4 qq + pp of 16-lane group g4 addresses vector
+    // 8 (g4 >> 1) + 4 s + qq, features 32 X + 16 (g4 & 1) + 4 pp .. + 3
+    const int g4 = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    const int rowv = 8 * (g4 >> 1) + qq;
+    auto opnd = [&](int slot, int p, int X) -> bf16x8 {
+        const int ch = 4 * X + 2 * (g4 & 1) + (pp >> 1);
+        const uint16_t* a0 = &sm.u.gp[slot][p][rowv][8 * (ch ^ (qq << 2)) + 4 * (pp & 1)];
+        const v4s lo = lds_tr16(a0), hi = lds_tr16(a0 + 4 * kPW);
+        return bf16x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    };
+    const short one = q == 0 ? (short)0x3F80 : (short)0;  // bf16 1.0 on feature kb
+    const bf16x8 ones = {one, one, one, one, one, one, one, one};
+    __syncthreads();  // the LDS union may still be read by the previous row's last phase
+#pragma unroll
+    for (int c = 0; c < kRBP - 1; ++c) {
+        int32_t i0, i1;
+        ids(c, i0, i1);
+        gather(c, i0, i1);
+    }
+    int32_t n0, n1;  // the ids of the next chunk to gather
+    ids(kRBP - 1, n0, n1);
+    for (int64_t c = 0; c < nch; ++c) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * (kRBP - 2)) : "memory");  // chunk c landed
+        ring_barrier();  // chunk c visible; every wave is done with the slot of chunk c - 1
+        gather(c + kRBP - 1, n0, n1);  // into that slot (chunks past the end: the zero row)
+        ids(c + kRBP, n0, n1);
+        const int slot = (int)(c % kRBP);
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) {
+            if (s >= nslot || tl.I[s] < 0) continue;
+            bf16x8 A[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) A[p] = opnd(slot, p, tl.J[s]);
+            if (tl.I[s] == ntb) {  // row kb: sum_i h_i = the B operand 1 on feature kb
+                acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], ones, acc[s], 0, 0, 0);
+                acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], ones, acc[s], 0, 0, 0);
+                acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], ones, acc[s], 0, 0, 0);
+            } else {
+                bf16x8 B[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) B[p] = opnd(slot, p, tl.I[s]);
+                acc[s] = mfma_x3(A, B, acc[s]);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing loads (past the end)
+    __syncthreads();
+}
+
+// x = x0 + x1 + x2 (split3t) of every H row, as three bf16 planes of kPW per row (features >= k
+// and row n: 0): P[p * (n + 1) * kPW + r * kPW + f]
+__global__ __launch_bounds__(256) void wrmf_split_planes_kernel(const float* __restrict__ H,
+                                                                int64_t n, int32_t k,
+                                                                uint16_t* __restrict__ P) {
+    const int64_t ps = (n + 1) * kPW;
+    for (int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x; x < ps;
+         x += (int64_t)gridDim.x * 256) {
+        const int64_t r = x / kPW;
+        const int f = (int)(x - r * kPW);
+        const float h = (r < n && f < k) ? H[r * k + f] : 0.0f;
+        uint32_t a, b, c;
+        split3t(h, a, b, c);
+        P[x] = (uint16_t)(a >> 16);
+        P[ps + x] = (uint16_t)(b >> 16);
+        P[2 * ps + x] = (uint16_t)(c >> 16);
+    }
+}
+
 // Split Gram of the heavy rows: one workgroup per (row, segment of <= kSeg entries), fp64 atomics
 // into gram[(li * kTiles + tile) * 1024 + g * 64 + lane].
 struct Seg {
@@ -646,9 +766,11 @@ struct Seg {
     int64_t b, e;
 };
 
+template <bool PL>  // PL: the Gram from pre-split planes (P), else from the fp32 rows of H
 __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_gram_kernel(
     const Seg* __restrict__ segs, int32_t nseg, int32_t li0, const int32_t* __restrict__ cols,
-    const float* __restrict__ H, int32_t k, double* __restrict__ gram) {
+    const float* __restrict__ H, int32_t k, double* __restrict__ gram,
+    const uint16_t* __restrict__ P, int64_t ps, int32_t zrow) {
     __shared__ Smem sm;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nt = (k + 31) >> 5, nr = nt + 1;
@@ -662,7 +784,9 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_gram_kernel(
         for (int s = 0; s < kSlots; ++s)
 #pragma unroll
             for (int g = 0; g < 16; ++g) acc[s][g] = 0.0f;
-        if (kGramRing && (k & 3) == 0)
+        if constexpr (PL)
+            gram_accumulate_p3(sm, acc, tl, kSlots, cols, sg.b, sg.e, P, ps, zrow, 32 * nr);
+        else if (kGramRing && (k & 3) == 0)
             gram_accumulate_x3g(sm, acc, tl, kSlots, cols, sg.b, sg.e, H, k, 32 * nr);
         else
             gram_accumulate_x3(sm, acc, tl, kSlots, cols, sg.b, sg.e, H, k, 32 * nr);
@@ -833,13 +957,14 @@ __device__ __forceinline__ void back_substitute(Smem& sm, f32x16 (&acc)[kSlots],
 //   W_u = ((1 + alpha) / alpha) L^{-T} Q_S^T C^{-1} 1,  C = I / alpha + Q_S Q_S^T  (deg x deg).
 //   The kernel solves C v = 1 on the same tile machinery (kdim = 32 * ceil(deg_max / 32)) and
 //   writes t = Q_S^T v to Tout[list index]; W rows = c t L^{-1} follow as one batched GEMM.
-template <int MODE>
+template <int MODE, bool PL = false>  // PL (MODE 0): the Gram from pre-split planes
 __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, int32_t* __restrict__ counter,
     const int64_t* __restrict__ off, const int32_t* __restrict__ cols, float* __restrict__ W,
     const float* __restrict__ H, const float* __restrict__ HHt, const double* __restrict__ gram,
     int32_t k, int32_t kdim, float alpha, float* __restrict__ Tout, int32_t dbg,
-    const float* __restrict__ rhs, float* __restrict__ F) {
+    const float* __restrict__ rhs, float* __restrict__ F, const uint16_t* __restrict__ P = nullptr,
+    int64_t ps = 0, int32_t zrow = 0) {
     __shared__ Smem sm;
     const bool gram_x3 = !(dbg & 32);  // MML_WRMF_DEBUG & 32: the f32 MFMA Gram (A/B)
     const int wave = threadIdx.x >> 6;
@@ -883,7 +1008,9 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
             }
         } else if (!(dbg & 8)) {
             if constexpr (MODE == 0) {
-                if (gram_x3 && kGramRing && (k & 3) == 0)
+                if constexpr (PL)
+                    gram_accumulate_p3(sm, acc, tl, nslot, cols, rb, re, P, ps, zrow, hsw);
+                else if (gram_x3 && kGramRing && (k & 3) == 0)
                     gram_accumulate_x3g(sm, acc, tl, nslot, cols, rb, re, H, k, hsw);
                 else if (gram_x3)
                     gram_accumulate_x3(sm, acc, tl, nslot, cols, rb, re, H, k, hsw);
@@ -2929,6 +3056,16 @@ static double spectral_norm_lower(const std::vector<double>& Li, int k) {
     return 1.25 * std::sqrt(lam);
 }
 
+// MML_WRMF_PLANES=0 (experiments builds): the direct rows' Gram gathers fp32 rows and splits them
+// in the kernel (gram_accumulate_x3g) instead of reading planes split once per half-step
+bool use_planes() {
+    static const bool v = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_PLANES");
+        return !(e && std::string(e) == "0");
+    }();
+    return v;
+}
+
 void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,
                      const int64_t* off, const int32_t* cols, const double* HH, int32_t k,
                      double alpha, double reg, int& launches, const float* rhs) {
@@ -2985,6 +3122,29 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                 F = p.ws->factor.get();
             }
         }
+        // the Gram vectors as bf16 planes, split once per half-step (the refinement's refactoring
+        // passes reuse them), if they fit the free HBM with a margin; else the fp32 gathers
+        const uint16_t* P = nullptr;
+        const int64_t ps = (h_rows + 1) * kPW;
+        if (nh + p.n_light > 0 && use_planes()) {
+            if (!rhs) {
+                p.ws->planes_of = nullptr;
+                const size_t need = (size_t)3 * ps;
+                size_t free_b = 0, total_b = 0;
+                MML_HIP(hipMemGetInfo(&free_b, &total_b));
+                const size_t have = free_b + p.ws->planes.count * sizeof(uint16_t);
+                if (need <= p.ws->planes.count || need * sizeof(uint16_t) + total_b / 16 <= have) {
+                    if (need > p.ws->planes.count) p.ws->planes.alloc(need);
+                    const int blocks = (int)std::min<int64_t>((ps + 255) / 256, 256 * 64);
+                    wrmf_split_planes_kernel<<<blocks, 256, 0, st>>>(H, h_rows, k,
+                                                                     p.ws->planes.get());
+                    MML_HIP(hipGetLastError());
+                    ++launches;
+                    p.ws->planes_of = H;
+                }
+            }
+            if (p.ws->planes_of == H) P = p.ws->planes.get();
+        }
         // heavy rows: batches whose fp64 Grams fit the workspace
         const int64_t per_row = (int64_t)kTiles * 1024 * sizeof(double);
         const int64_t batch_rows = std::max<int64_t>(1, kGramBatchBytes / per_row);
@@ -2994,9 +3154,10 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             p.gram.alloc((size_t)std::min(nh, batch_rows) * kTiles * 1024);
             MML_HIP(hipMemsetAsync(p.gram.get(), 0, (size_t)(h1 - h0) * per_row, st));
             const int gg = (int)std::min<int64_t>(s1 - s0, grid_cap);
-            wrmf_tile_gram_kernel<<<gg, kThreads, 0, st>>>(
+            auto gk = P ? &wrmf_tile_gram_kernel<true> : &wrmf_tile_gram_kernel<false>;
+            gk<<<gg, kThreads, 0, st>>>(
                 reinterpret_cast<const Seg*>(p.segs.get()) + s0, (int32_t)(s1 - s0), (int32_t)h0,
-                cols, H, k, p.gram.get());
+                cols, H, k, p.gram.get(), P, ps, (int32_t)h_rows);
             MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
             const int gs = (int)std::min<int64_t>(h1 - h0, grid_cap);
             wrmf_tile_solve_kernel<0><<<gs, kThreads, 0, st>>>(
@@ -3009,9 +3170,10 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
         if (p.n_light > 0) {
             MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
             const int gs = (int)std::min<int64_t>(p.n_light, grid_cap);
-            wrmf_tile_solve_kernel<0><<<gs, kThreads, 0, st>>>(
+            auto sk = P ? &wrmf_tile_solve_kernel<0, true> : &wrmf_tile_solve_kernel<0, false>;
+            sk<<<gs, kThreads, 0, st>>>(
                 p.light.get(), p.n_light, p.counter.get(), off, cols, W, H, p.hht.get(), nullptr,
-                k, k, (float)alpha, nullptr, debug_mask(), rhs, F);
+                k, k, (float)alpha, nullptr, debug_mask(), rhs, F, P, ps, (int32_t)h_rows);
             MML_HIP(hipGetLastError());
             ++launches;
         }
