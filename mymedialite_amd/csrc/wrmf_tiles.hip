@@ -701,8 +701,7 @@ __device__ __forceinline__ void gram_accumulate_p3(Smem& sm, f32x16 (&acc)[kSlot
         const v4s lo = lds_tr16(a0), hi = lds_tr16(a0 + 4 * kPW);
         return bf16x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     };
-    const short one = q == 0 ? (short)0x3F80 : (short)0;  // bf16 1.0 on feature kb
-    const bf16x8 ones = {one, one, one, one, one, one, one, one};
+    const uint32_t one2 = q == 0 ? 0x3F803F80u : 0u;  // two bf16 1.0 on feature kb
     __syncthreads();  // the LDS union may still be read by the previous row's last phase
 #pragma unroll
     for (int c = 0; c < kRBP - 1; ++c) {
@@ -718,6 +717,9 @@ __device__ __forceinline__ void gram_accumulate_p3(Smem& sm, f32x16 (&acc)[kSlot
         gather(c + kRBP - 1, n0, n1);  // into that slot (chunks past the end: the zero row)
         ids(c + kRBP, n0, n1);
         const int slot = (int)(c % kRBP);
+        // (every slot with the same six MFMAs and no branch -- b-row tiles against (1, 0, 0), an
+        // empty slot on tile (0, 0) -- removes the accumulator copies the branches cause, but the
+        // 20 % more MFMAs cost more than the copies: split Gram 90 -> 98 ms, profiles/r4m_*)
 #pragma unroll
         for (int s = 0; s < kSlots; ++s) {
             if (s >= nslot || tl.I[s] < 0) continue;
@@ -725,6 +727,7 @@ __device__ __forceinline__ void gram_accumulate_p3(Smem& sm, f32x16 (&acc)[kSlot
 #pragma unroll
             for (int p = 0; p < 3; ++p) A[p] = opnd(slot, p, tl.J[s]);
             if (tl.I[s] == ntb) {  // row kb: sum_i h_i = the B operand 1 on feature kb
+                const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{one2, one2, one2, one2});
                 acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], ones, acc[s], 0, 0, 0);
                 acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], ones, acc[s], 0, 0, 0);
                 acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], ones, acc[s], 0, 0, 0);
@@ -966,6 +969,11 @@ __global__ __launch_bounds__(kThreads, 2) void wrmf_tile_solve_kernel(
     const float* __restrict__ rhs, float* __restrict__ F, const uint16_t* __restrict__ P = nullptr,
     int64_t ps = 0, int32_t zrow = 0) {
     __shared__ Smem sm;
+#ifndef MML_EXPERIMENTS
+    // the phase masks are switches of the experiments build: a constant here folds their branches
+    // (each one around an MFMA chain made the compiler copy the accumulators behind it)
+    dbg = 0;
+#endif
     const bool gram_x3 = !(dbg & 32);  // MML_WRMF_DEBUG & 32: the f32 MFMA Gram (A/B)
     const int wave = threadIdx.x >> 6;
     const int nt = (kdim + 31) >> 5, nr = nt + 1;
