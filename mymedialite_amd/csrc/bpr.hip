@@ -337,7 +337,8 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
     const int32_t* __restrict__ ev_i, int64_t n_samples, int32_t n_items, uint64_t seed,
     int32_t* __restrict__ tu, int32_t* __restrict__ ti, int32_t* __restrict__ tj,
     int32_t* __restrict__ fail, uint64_t* __restrict__ user_keys,
-    const uint32_t* __restrict__ recs) {
+    const uint32_t* __restrict__ recs, const uint8_t* __restrict__ gtab,
+    uint8_t* __restrict__ tg) {
     for (int64_t smp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; smp < n_samples;
          smp += (int64_t)gridDim.x * blockDim.x) {
         int32_t u, i = 0, j = 0;
@@ -346,6 +347,7 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
             tu[smp] = u;
             ti[smp] = i;
             tj[smp] = j;
+            if (tg) tg[smp] = gtab[i];  // the XCD partition's key, while i is at hand
             continue;
         }
         if constexpr (SAMPLER == MML_BPR_SAMPLER_UNIFORM_PAIR) {
@@ -384,7 +386,10 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
             }
         }
         tu[smp] = u;
-        if constexpr (SAMPLER != MML_BPR_SAMPLER_USER_REPLACEMENT) ti[smp] = i;
+        if constexpr (SAMPLER != MML_BPR_SAMPLER_USER_REPLACEMENT) {
+            ti[smp] = i;
+            if (tg) tg[smp] = gtab[i];
+        }
         tj[smp] = j;
     }
 }
@@ -690,6 +695,7 @@ struct mml_bpr {
     // i (stable), xt_* = the partitioned copy; span1 = {0, n} for the one-span launch
     mml::XcdSplit xs;
     mml::DeviceArray<int32_t> xt_u, xt_i, xt_j;
+    mml::DeviceArray<uint8_t> tri_g;  // the XCD group of each triple's i, written by the sampler
     mml::DeviceArray<int64_t> span1;
     bool has_groups = false;
     // multi-device context: one single-device handle per GPU over a user range ub[d] .. ub[d + 1]
@@ -1429,6 +1435,16 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             h->tri_i.alloc(n);
             h->tri_j.alloc(n);
         }
+        // the sampler writes each triple's group beside it (the resolve kernel of
+        // USER_REPLACEMENT draws i later: that sampler keeps the table lookups)
+        // MML_BPR_GROUP_BYTES=1 (experiments builds): the sampler writes each triple's group byte
+        // and the partition reads it instead of looking the group up (A/B pending: off by default)
+        static const bool group_bytes = [] {
+            const char* e = MML_EXPERIMENT_ENV("MML_BPR_GROUP_BYTES");
+            return e && std::string(e) == "1";
+        }();
+        const bool part_g = part && !user_repl && group_bytes;
+        if (part_g && (int64_t)h->tri_g.count < n) h->tri_g.alloc(n);
         if (part && (int64_t)h->xt_u.count < n) {
             h->xt_u.alloc(n);
             h->xt_i.alloc(n);
@@ -1462,7 +1478,8 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
     bpr_sample_kernel<KIND><<<sgrid, 256, 0, st>>>(                                            \
         h->off.get(), h->cols.get(), ELIG, h->n_eligible, h->ev_u.get(), h->ev_i.get(), n,    \
         h->n_items, seed, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), h->fail.get(),       \
-        h->rank_keys.get(), h->recs.get())
+        h->rank_keys.get(), h->recs.get(), part_g ? h->xs.group.get() : nullptr,             \
+        part_g ? h->tri_g.get() : nullptr)
             int32_t* elig = h->n_eligible == h->n_users ? nullptr : h->eligible.get();
             switch (h->p.sampler) {
                 case MML_BPR_SAMPLER_UNIFORM_PAIR:
@@ -1510,7 +1527,10 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         if (part) {  // stable partition of the sampled triples (XcdSplit)
             const int32_t* in[3] = {tu, ti, tj};
             int32_t* out[3] = {h->xt_u.get(), h->xt_i.get(), h->xt_j.get()};
-            h->xs.partition(st, ti, n, 3, in, out);
+            if (part_g)
+                h->xs.partition_groups(st, h->tri_g.get(), n, 3, in, out);
+            else
+                h->xs.partition(st, ti, n, 3, in, out);
             ng = 8;
             goff = h->xs.goff.get();
             tu = h->xt_u.get();

@@ -218,6 +218,10 @@ struct XcdSplit {
     // out[c][...] = in[c][...] reordered by group(key[x]), stable; goff written on the device
     void partition(hipStream_t st, const int32_t* key, int64_t n, int32_t npay,
                    const int32_t* const* in, int32_t* const* out);
+    // the same with each entry's group given as a byte (gkey[x] = group[key[x]], e.g. written by
+    // the BPR sampler beside its triple): no table lookups in the count and scatter passes
+    void partition_groups(hipStream_t st, const uint8_t* gkey, int64_t n, int32_t npay,
+                          const int32_t* const* in, int32_t* const* out);
 };
 std::vector<uint8_t> balanced_item_groups(const std::vector<int64_t>& weight, int32_t ng);
 // occurrences of each id in [0, n_ids) of a device id array, on the host

@@ -2697,8 +2697,15 @@ __global__ __launch_bounds__(256) void wrmf_resid_multi_kernel(const RMulti* __r
 // current chunk's 64 MFMAs per wave.  (Replaces the rocBLAS dgemm: the training path links no
 // vendor BLAS.)
 using f64x4 = __attribute__((ext_vector_type(4))) double;
-constexpr int kXB = 64, kXK = 16, kXN = 256, kXNP = kXN + 2, kXKP = kXK + 1;
-__global__ __launch_bounds__(256) void wrmf_xhh_kernel(const double* __restrict__ X,
+#ifndef MML_XHH_K  // A/B variants: the K chunk of wrmf_xhh_kernel (LDS 83 KB at 16, 42 KB at 8)
+#define MML_XHH_K 16
+#endif
+constexpr int kXB = 64, kXK = MML_XHH_K, kXN = 256, kXNP = kXN + 2, kXKP = kXK + 1;
+constexpr int kXV = kXK / 4;  // X values per thread and chunk
+#ifndef MML_XHH_WAVES  // A/B variants: minimum waves per SIMD of wrmf_xhh_kernel (register cap)
+#define MML_XHH_WAVES 1
+#endif
+__global__ __launch_bounds__(256, MML_XHH_WAVES) void wrmf_xhh_kernel(const double* __restrict__ X,
                                                        const double* __restrict__ HH, int64_t n,
                                                        int32_t k, double reg,
                                                        double* __restrict__ R) {
@@ -2712,25 +2719,25 @@ __global__ __launch_bounds__(256) void wrmf_xhh_kernel(const double* __restrict_
         for (int jt = 0; jt < 16; ++jt) acc[jt] = f64x4{0.0, 0.0, 0.0, 0.0};
         // staging of chunk c into buffer bb: HH rows c*16 .. +16 (all columns), X rows r0 .. r0+64
         // columns c*16 .. +16; zero past k and past n
-        double hv[16], xv[4];
+        double hv[kXK], xv[kXV];
         auto load = [&](int c) {
 #pragma unroll
-            for (int x = 0; x < 16; ++x) {  // 16 x 256 HH values: thread t -> row x, column t
+            for (int x = 0; x < kXK; ++x) {  // kXK x 256 HH values: thread t -> row x, column t
                 const int f = c * kXK + x;
                 hv[x] = (f < k && t < k) ? HH[(int64_t)f * k + t] : 0.0;
             }
 #pragma unroll
-            for (int x = 0; x < 4; ++x) {  // 64 x 16 X values: thread t -> row t / 4, col 4(t%4)+x
+            for (int x = 0; x < kXV; ++x) {  // 64 x kXK X values: row t / 4, col kXV (t % 4) + x
                 const int64_t row = r0 + (t >> 2);
-                const int f = c * kXK + 4 * (t & 3) + x;
+                const int f = c * kXK + kXV * (t & 3) + x;
                 xv[x] = (row < n && f < k) ? X[row * k + f] : 0.0;
             }
         };
         auto store = [&](int bb) {
 #pragma unroll
-            for (int x = 0; x < 16; ++x) sb[bb][x][t] = hv[x];
+            for (int x = 0; x < kXK; ++x) sb[bb][x][t] = hv[x];
 #pragma unroll
-            for (int x = 0; x < 4; ++x) sa[bb][t >> 2][4 * (t & 3) + x] = xv[x];
+            for (int x = 0; x < kXV; ++x) sa[bb][t >> 2][kXV * (t & 3) + x] = xv[x];
         };
         load(0);
         __syncthreads();  // the previous row block's last chunk has been read

@@ -36,8 +36,23 @@ __global__ __launch_bounds__(256) void xcd_probe_kernel(int32_t* __restrict__ ou
 // 500 M-entry partition at C3).
 constexpr int kSub = 4;
 
+// the group of entry x: group[key[x]], or (DIRECT) the byte gkey[x] the producer wrote
+template <bool DIRECT>
+__device__ __forceinline__ int32_t entry_key(const int32_t* __restrict__ key,
+                                             const uint8_t* __restrict__ gkey, int64_t x) {
+    if constexpr (DIRECT) return (int32_t)gkey[x];
+    return key[x];
+}
+template <bool DIRECT>
+__device__ __forceinline__ int entry_group(int32_t kx, const uint8_t* __restrict__ group) {
+    if constexpr (DIRECT) return kx;
+    return (int)group[kx];
+}
+
 // per (group, block) counts of one contiguous segment per block; groups by ballot, 8 per wave step
-__global__ __launch_bounds__(256) void xcd_count_kernel(const int32_t* __restrict__ key, int64_t n,
+template <bool DIRECT>
+__global__ __launch_bounds__(256) void xcd_count_kernel(const int32_t* __restrict__ key,
+                                                        const uint8_t* __restrict__ gkey, int64_t n,
                                                         int64_t seg,
                                                         const uint8_t* __restrict__ group,
                                                         int64_t* __restrict__ cnt, int32_t nblk) {
@@ -51,10 +66,10 @@ __global__ __launch_bounds__(256) void xcd_count_kernel(const int32_t* __restric
 #pragma unroll
         for (int u = 0; u < kSub; ++u) {
             const int64_t x = t + 256 * u + threadIdx.x;
-            kx[u] = x < b1 ? key[x] : -1;
+            kx[u] = x < b1 ? entry_key<DIRECT>(key, gkey, x) : -1;
         }
 #pragma unroll
-        for (int u = 0; u < kSub; ++u) g[u] = kx[u] >= 0 ? (int)group[kx[u]] : -1;
+        for (int u = 0; u < kSub; ++u) g[u] = kx[u] >= 0 ? entry_group<DIRECT>(kx[u], group) : -1;
 #pragma unroll
         for (int u = 0; u < kSub; ++u)
 #pragma unroll
@@ -76,7 +91,9 @@ struct Pay3 {
 // stable scatter: block b walks its segment in order; an entry of group g goes to base[g][b] +
 // (entries of group g before it in the segment).  Every thread keeps the 8 group runs; per tile the
 // waves' group counts go through the LDS (alternating buffers: one barrier per tile).
+template <bool DIRECT>
 __global__ __launch_bounds__(256) void xcd_scatter_kernel(const int32_t* __restrict__ key,
+                                                          const uint8_t* __restrict__ gkey,
                                                           int64_t n, int64_t seg,
                                                           const uint8_t* __restrict__ group,
                                                           const int64_t* __restrict__ base,
@@ -96,12 +113,12 @@ __global__ __launch_bounds__(256) void xcd_scatter_kernel(const int32_t* __restr
         for (int u = 0; u < kSub; ++u) {
             const int64_t x = t + 256 * u + threadIdx.x;
             const bool in = x < b1;
-            kx[u] = in ? key[x] : -1;
+            kx[u] = in ? entry_key<DIRECT>(key, gkey, x) : -1;
 #pragma unroll
             for (int c = 0; c < 3; ++c) pv[c][u] = in && c < npay ? p.in[c][x] : 0;
         }
 #pragma unroll
-        for (int u = 0; u < kSub; ++u) g[u] = kx[u] >= 0 ? (int)group[kx[u]] : -1;
+        for (int u = 0; u < kSub; ++u) g[u] = kx[u] >= 0 ? entry_group<DIRECT>(kx[u], group) : -1;
 #pragma unroll
         for (int u = 0; u < kSub; ++u) {
             int rank = 0;
@@ -232,27 +249,43 @@ void XcdSplit::set_table(hipStream_t st, const std::vector<uint8_t>& table) {
     MML_HIP(hipStreamSynchronize(st));
 }
 
-void XcdSplit::partition(hipStream_t st, const int32_t* key, int64_t n, int32_t npay,
-                         const int32_t* const* in, int32_t* const* out) {
-    MML_REQUIRE(ng == 8 && npay >= 1 && npay <= 3, "XcdSplit::partition: bad setup");
+namespace {
+template <bool DIRECT>
+void partition_impl(XcdSplit& xs, hipStream_t st, const int32_t* key, const uint8_t* gkey,
+                    int64_t n, int32_t npay, const int32_t* const* in, int32_t* const* out) {
+    MML_REQUIRE(xs.ng == 8 && npay >= 1 && npay <= 3, "XcdSplit::partition: bad setup");
     const int32_t nblk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 4095) / 4096));
     const int64_t seg = (n + nblk - 1) / nblk;
-    cnt.alloc((size_t)8 * nblk);
-    base.alloc((size_t)8 * nblk);
+    xs.cnt.alloc((size_t)8 * nblk);
+    xs.base.alloc((size_t)8 * nblk);
     size_t tb = 0;
-    MML_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.get(), base.get(), 8 * nblk, st));
-    if (tmp.count < tb) tmp.alloc(tb);
-    xcd_count_kernel<<<nblk, 256, 0, st>>>(key, n, seg, group.get(), cnt.get(), nblk);
+    MML_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, xs.cnt.get(), xs.base.get(), 8 * nblk, st));
+    if (xs.tmp.count < tb) xs.tmp.alloc(tb);
+    xcd_count_kernel<DIRECT><<<nblk, 256, 0, st>>>(key, gkey, n, seg, xs.group.get(), xs.cnt.get(),
+                                                   nblk);
     MML_HIP(hipGetLastError());
-    MML_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.get(), tb, cnt.get(), base.get(), 8 * nblk, st));
+    MML_HIP(hipcub::DeviceScan::ExclusiveSum(xs.tmp.get(), tb, xs.cnt.get(), xs.base.get(),
+                                             8 * nblk, st));
     Pay3 p{};
     for (int c = 0; c < npay; ++c) {
         p.in[c] = in[c];
         p.out[c] = out[c];
     }
-    xcd_scatter_kernel<<<nblk, 256, 0, st>>>(key, n, seg, group.get(), base.get(), nblk, npay, p);
-    xcd_offsets_kernel<<<1, 64, 0, st>>>(base.get(), nblk, n, goff.get());
+    xcd_scatter_kernel<DIRECT><<<nblk, 256, 0, st>>>(key, gkey, n, seg, xs.group.get(),
+                                                     xs.base.get(), nblk, npay, p);
+    xcd_offsets_kernel<<<1, 64, 0, st>>>(xs.base.get(), nblk, n, xs.goff.get());
     MML_HIP(hipGetLastError());
+}
+}  // namespace
+
+void XcdSplit::partition(hipStream_t st, const int32_t* key, int64_t n, int32_t npay,
+                         const int32_t* const* in, int32_t* const* out) {
+    partition_impl<false>(*this, st, key, nullptr, n, npay, in, out);
+}
+
+void XcdSplit::partition_groups(hipStream_t st, const uint8_t* gkey, int64_t n, int32_t npay,
+                                const int32_t* const* in, int32_t* const* out) {
+    partition_impl<true>(*this, st, nullptr, gkey, n, npay, in, out);
 }
 
 std::vector<int64_t> device_id_counts(hipStream_t st, const int32_t* ids, int64_t n,
