@@ -2697,13 +2697,16 @@ __global__ __launch_bounds__(256) void wrmf_resid_multi_kernel(const RMulti* __r
 // current chunk's 64 MFMAs per wave.  (Replaces the rocBLAS dgemm: the training path links no
 // vendor BLAS.)
 using f64x4 = __attribute__((ext_vector_type(4))) double;
-#ifndef MML_XHH_K  // A/B variants: the K chunk of wrmf_xhh_kernel (LDS 83 KB at 16, 42 KB at 8)
-#define MML_XHH_K 16
+#ifndef MML_XHH_K  // the K chunk of wrmf_xhh_kernel: LDS 42 KB at 8 (83 KB at 16: one workgroup per CU)
+#define MML_XHH_K 8
 #endif
 constexpr int kXB = 64, kXK = MML_XHH_K, kXN = 256, kXNP = kXN + 2, kXKP = kXK + 1;
 constexpr int kXV = kXK / 4;  // X values per thread and chunk
-#ifndef MML_XHH_WAVES  // A/B variants: minimum waves per SIMD of wrmf_xhh_kernel (register cap)
-#define MML_XHH_WAVES 1
+// two waves per SIMD: the accumulators move from AGPRs to VGPRs (192 registers, no spills) and two
+// workgroups share a CU.  With one (K chunk 16) the kernel held 358 registers and ran one wave per
+// SIMD: 23.8 -> 16.7 ms per C5 iteration (profiles/r4r_c5_*_kernel_stats.csv)
+#ifndef MML_XHH_WAVES
+#define MML_XHH_WAVES 2
 #endif
 __global__ __launch_bounds__(256, MML_XHH_WAVES) void wrmf_xhh_kernel(const double* __restrict__ X,
                                                        const double* __restrict__ HH, int64_t n,
