@@ -2398,7 +2398,12 @@ __global__ __launch_bounds__(256) void wrmf_split_mt_kernel(const float* __restr
 // wave w takes column tiles 2w and 2w + 1 for both row tiles (4 accumulators).  X is staged in K
 // halves of kRH columns (3 planes x 64 rows x (kRH + 8) bf16 = 52 KB of LDS: 3 workgroups per CU).
 constexpr int kRH = 128, kRHS = kRH + 8;
-__global__ __launch_bounds__(256) void wrmf_rows_matmul_x3_kernel(
+// three waves per SIMD: 163 VGPRs and no AGPRs (130 + 64 AGPRs at the default bounds: two waves),
+// three workgroups per CU in 3 x 52 KB of LDS: 20.9 -> 19.1 ms per C5 iteration (profiles/r4t_*)
+#ifndef MML_MATMUL_WAVES
+#define MML_MATMUL_WAVES 3
+#endif
+__global__ __launch_bounds__(256, MML_MATMUL_WAVES) void wrmf_rows_matmul_x3_kernel(
     const float* __restrict__ X, const int32_t* __restrict__ xrows, int64_t n,
     const uint16_t* __restrict__ MT, int32_t k, int32_t kpad, float scale, float* __restrict__ Y,
     const int32_t* __restrict__ yrows) {
@@ -2786,23 +2791,30 @@ __global__ __launch_bounds__(256) void wrmf_refine_rows_kernel(int op, int64_t r
                                                                const int64_t* __restrict__ off,
                                                                int wood,
                                                                unsigned* __restrict__ dmax) {
+    // one row per block step, the features across the threads: the row (and, for op 2, its type)
+    // is known per step instead of a 64-bit division per element
     float m[2] = {0.0f, 0.0f};
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * k;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t g = r0 * k + e;
-        switch (op) {
-            case 0: X[e] = (double)W[g]; break;
-            case 1: Rf[g] = (float)R[e]; break;
-            case 2: {
-                const double x = X[e] + (double)D[g];
-                X[e] = x;
-                const int64_t r = r0 + e / k, deg = off[r + 1] - off[r];
-                const float c = (float)(fabs((double)D[g]) / (1.0 + fabs(x)));
-                if (wood && deg >= 1 && deg <= 128) m[1] = fmaxf(m[1], c);
-                else m[0] = fmaxf(m[0], c);
-                break;
+    for (int64_t lr = blockIdx.x; lr < n; lr += gridDim.x) {
+        const int64_t row = r0 + lr;
+        const int64_t le = lr * k, ge = row * k;
+        int t = 0;
+        if (op == 2) {
+            const int64_t deg = off[row + 1] - off[row];
+            t = wood && deg >= 1 && deg <= 128 ? 1 : 0;
+        }
+        for (int f = threadIdx.x; f < k; f += blockDim.x) {
+            switch (op) {
+                case 0: X[le + f] = (double)W[ge + f]; break;
+                case 1: Rf[ge + f] = (float)R[le + f]; break;
+                case 2: {
+                    const double x = X[le + f] + (double)D[ge + f];
+                    X[le + f] = x;
+                    const float c = (float)(fabs((double)D[ge + f]) / (1.0 + fabs(x)));
+                    m[t] = fmaxf(m[t], c);
+                    break;
+                }
+                default: W[ge + f] = (float)X[le + f]; break;
             }
-            default: W[g] = (float)X[e]; break;
         }
     }
     if (op == 2)  // non-negative floats order like their bit patterns
@@ -2960,7 +2972,7 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
     p.ws->rf.reserve((size_t)n_w * k);
     p.ws->df.reserve((size_t)n_w * k);
     p.ws->rpartial.reserve(std::max<int64_t>(1, p.n_rslots) * (size_t)k);
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n * k + 255) / 256, 16384));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, 16384));
     auto rows = [&](int op) {
         wrmf_refine_rows_kernel<<<grid, 256, 0, st>>>(op, p.r0, n, k, W, p.ws->x64.get(),
                                                       p.ws->r64.get(), p.ws->rf.get(),
