@@ -748,12 +748,14 @@ def bench_wrmf(args):
                    "alpha": 1.0, "regularization": 0.015, "device_ingest_s": ingest_s},
         "roofline": {"bound": "mfma", "achieved": tflops, "peak": 157.3, "unit": "TFLOP/s",
                      "frac": tflops / 157.3, "traffic": None,
-                     "kernel": "wrmf_wood_cg_kernel + wrmf_tile_solve_kernel + "
-                               "wrmf_tile_gram_kernel + wrmf_gram_* (+ wrmf_resid_seg_kernel, "
-                               "wrmf_tile_resolve_kernel in the fp64 mode; whole iteration)",
+                     "kernel": "wrmf_wood_w16_kernel + wrmf_wood_cg_kernel + "
+                               "wrmf_tile_solve_kernel + wrmf_tile_gram_kernel + "
+                               "wrmf_split_planes_kernel + wrmf_gram_* (+ wrmf_resid_seg_kernel, "
+                               "wrmf_xhh_kernel, wrmf_tile_resolve_wave_kernel in the fp64 mode; "
+                               "whole iteration)",
                      "kernel_avg_ms": float(np.mean(ms)), "flops_per_iteration": flops_exec,
                      "flops_note": "executed algorithmic flops (bench.wrmf_executed_flops): "
-                                   "Woodbury rows (deg <= 128) by CG, 4 deg k per C mat-vec at "
+                                   "Woodbury rows (deg <= 128) by Chebyshev / CG, 4 deg k per C mat-vec at "
                                    "the cond(C) <= 1 + alpha step bound (an upper bound), + 2k^2; "
                                    "direct rows k(k+1)deg + k^3/3 + 2k^2 + 2 deg k; per half HH "
                                    "k(k+1)n and Q = H L^-T 2nk^2; per refinement pass the fp64 "
