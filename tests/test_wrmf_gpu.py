@@ -118,10 +118,13 @@ def test_wrmf_with_communicator_matches_single(k):
 
 @pytest.mark.parametrize("k,alpha,prec,tol", [(160, 1.0, "fp32", 2e-3), (256, 4.0, "fp32", 2e-3),
                                               (200, 0.0, "fp32", 2e-3), (160, 1.0, "fp64", 1e-4),
-                                              (256, 4.0, "fp64", 1e-4), (200, 0.0, "fp64", 1e-4)])
+                                              (256, 4.0, "fp64", 1e-4), (200, 0.0, "fp64", 1e-4),
+                                              (201, 1.0, "fp32", 2e-3), (201, 1.0, "fp64", 1e-4)])
 def test_wrmf_woodbury_and_direct_rows_match_oracle(k, alpha, prec, tol):
     """128 < k: rows with 1..128 entries take the Woodbury solve (all four 32-column groups),
-    longer rows the direct tile solve; alpha = 0 sends every row to the direct solve.  Enough
+    longer rows the direct tile solve; alpha = 0 sends every row to the direct solve.  k = 201
+    (not a multiple of 4) takes the scalar-load paths of the Woodbury and residual kernels and the
+    planes split's zero padding past k.  Enough
     users (280 > k) that HH + reg I is well conditioned: with fewer rows than factors the fp32 vs
     fp64 gap grows with cond(HH + reg I) ~ |H|^2 / reg, for any fp32 solver (measured per row on
     one half-step: Woodbury <= 9e-7, direct <= 6e-6, scripts/diag_wrmf_rows.py)."""
