@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 9
+#define MML_ABI_VERSION 10
 
 typedef int32_t mml_status;
 enum {
@@ -267,8 +267,9 @@ mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const int32_t* ite
  * out[0] = ms for the whole epoch, out[1] = number of kernel launches in it. */
 mml_status mml_bmf_last_timing(mml_bmf* h, float* out);
 /* The dominant kernel of the last mml_bmf_iterate as rocprofv3 names the template instance, e.g.
- * "bmf_sgd_hogwild_kernel<0, 16, 1, 14>" (ABI 9; empty before a Hogwild epoch); NUL-terminated,
- * truncated to cap bytes. */
+ * "bmf_sgd_hogwild_kernel<0, 16, 1, 14>" or "bmf_sgd_ordered_kernel<0, 1>" (ABI 9; cleared by
+ * every iterate, so empty after an epoch of the social / asymmetric models' kernels);
+ * NUL-terminated, truncated to cap bytes. */
 mml_status mml_bmf_last_kernel(mml_bmf* h, char* buf, int32_t cap);
 /* BiasedMatrixFactorization.ComputeObjective (:496-552) on the device model and training data:
  * out[0] = ComputeLoss() (RMSE / MAE / logistic sum per params.loss, double), out[1] = the
@@ -442,6 +443,12 @@ mml_status mml_bpr_last_timing(mml_bpr* h, float* out);
 /* The update kernel of the last Hogwild epoch as rocprofv3 names it, e.g.
  * "bpr_update_kernel<32, false, 27>" (ABI 9); NUL-terminated, truncated to cap bytes. */
 mml_status mml_bpr_last_kernel(mml_bpr* h, char* buf, int32_t cap);
+/* The HOGWILD epoch's launch width (ABI 10): 0 = the default (at least 65,536 triples per wave,
+ * at most 8,192 waves: C3's 500 M events run 7,648); waves > 0 = that many waves, rounded up to
+ * a multiple of 32 (8 XCD groups x 4 waves), at most 8,192.  Lets a smaller set replay a larger
+ * set's triples in flight -- the Hogwild staleness -- e.g. the C3-density AUC parity test.  No
+ * effect on the ORDERED schedule or on epochs below 16 waves' worth of triples. */
+mml_status mml_bpr_set_hogwild_waves(mml_bpr* h, int64_t waves);
 /* The last epoch's sampled triples in sample order (n = Feedback.Count), e.g. for BPRMF's
  * loss_sample_* arrays (BPRMF.cs:136-150) or to check a sampler's distribution (ABI 3).  On a
  * multi-device context: each user shard's triples in its sample order, shard after shard (ABI 9;

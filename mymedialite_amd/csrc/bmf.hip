@@ -1620,6 +1620,7 @@ void launch_ordered(mml_bmf* h, const int64_t* off, int32_t G, int32_t sub, int 
     }
 #undef MML_ORD
     MML_HIP(hipGetLastError());
+    h->last_kernel = kernel_label("bmf_sgd_ordered_kernel", {LOSS, km < 4 ? km : 4});
 }
 
 // The XCD-partitioned copy of the visit-order stream (built once per data set): items dealt into 8
@@ -1949,6 +1950,14 @@ void multi_create(mml_ctx* ctx, const mml_bmf_params* params, int32_t n_users, i
 }
 
 bool multi_dsgd(const mml_bmf* h) { return h->p.schedule == MML_SCHEDULE_DSGD; }
+bool ring_mode(const mml_bmf* h);
+// entry points that read or average the model outside the ring's collectives: a DSGD ring rank
+// holds stale copies of the rows other ranks trained since the last sync, so they are refused
+void no_ring(const mml_bmf* h, const char* what) {
+    if (ring_mode(h))
+        mml::fail(MML_ERR_STATE, std::string(what) + " is not available on a DSGD ring rank (the "
+                                 "ring's collectives are get_model, predict, evaluate, objective)");
+}
 template <class F>
 void ring_all(mml_bmf* h, F&& f);
 
@@ -2747,6 +2756,9 @@ extern "C" mml_status mml_bmf_set_data_device(mml_bmf* h, const int32_t* users,
         MML_REQUIRE(n >= 0 && n <= INT32_MAX, "rating count out of range");
         MML_REQUIRE(n == 0 || (users && items && values), "null rating arrays");
         if (h->ctx->multi()) return multi_set_data_device(h, users, items, values, n, order);
+        // a ring rank: every rank gets the newest model before the groups are forgotten (as
+        // mml_bmf_set_data)
+        if (ring_mode(h) && h->has_model) ring_sync(h);
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         h->has_data = false;
@@ -2968,6 +2980,7 @@ extern "C" mml_status mml_bmf_iterate(mml_bmf* h, float learn_rate,
             return;
         }
         MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede iterate");
+        h->last_kernel.clear();  // set again by the launch that runs (Hogwild / ordered / DSGD)
         const bool asym = is_asym(h);
         if (asym) {
             MML_REQUIRE(asym_ready(h), "set_implicit_feedback (each side the model uses) must "
@@ -3077,8 +3090,10 @@ extern "C" mml_status mml_bmf_predict(mml_bmf* h, const int32_t* users, const in
             return multi_predict(h, users, items, n, out);
         }
         MML_REQUIRE(h->has_model, "no model");
+        // a collective on a ring rank: every rank syncs before the per-rank argument checks, so a
+        // rank with an empty or bad slice cannot leave the others waiting in the broadcasts
+        if (ring_mode(h)) ring_sync(h);
         MML_REQUIRE(n >= 0 && (n == 0 || (users && items && out)), "bad arguments");
-        if (ring_mode(h)) ring_sync(h);  // a collective: every rank predicts
         if (n == 0) return;
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
@@ -3111,8 +3126,8 @@ extern "C" mml_status mml_bmf_evaluate(mml_bmf* h, const int32_t* users, const i
             return multi_evaluate(h, users, items, values, n, out);
         }
         MML_REQUIRE(h->has_model, "no model");
+        if (ring_mode(h)) ring_sync(h);  // a collective: every rank syncs before its own checks
         MML_REQUIRE(n > 0 && users && items && values && out, "bad arguments");
-        if (ring_mode(h)) ring_sync(h);  // a collective: every rank evaluates
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         upload_pairs(h, users, items, n);
@@ -3149,12 +3164,18 @@ extern "C" mml_status mml_bmf_objective(mml_bmf* h, double* out) {
         MML_REQUIRE(h->has_model && h->has_data && out, "model, data and out required");
         MML_REQUIRE(h->p.model == MML_MF_BIASED,
                     "ComputeObjective is defined for BiasedMatrixFactorization only");
+        // a ring rank (a collective): the newest model on every rank, and the loss over all n
+        // ratings in set_data order -- su holds only this rank's block rows
+        const bool ring = ring_mode(h);
+        if (ring) ring_sync(h);
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         const int g1 = grid_for(h->n, 256, 1024);
         const int g2 = grid_for((int64_t)h->n_users + h->n_items, 4, 1024);
         h->ev_partials.alloc(g1 + g2);
-        bmf_loss_kernel<<<g1, 256, 0, st>>>(h->su.get(), h->si.get(), h->sr.get(), h->n,
+        bmf_loss_kernel<<<g1, 256, 0, st>>>(ring ? h->raw_u.get() : h->su.get(),
+                                            ring ? h->raw_i.get() : h->si.get(),
+                                            ring ? h->raw_r.get() : h->sr.get(), h->n,
                                             h->n_users, h->n_items, h->U.get(), h->V.get(),
                                             h->bu.get(), h->bi.get(), h->k, h->ld, h->gb,
                                             h->min_rating, h->max_rating, h->p.loss,
@@ -3180,6 +3201,7 @@ extern "C" mml_status mml_bmf_allreduce_items(mml_bmf* h) {
     return guard([&] {
         check_handle(h);
         single_device_only(h);
+        no_ring(h, "allreduce_items");
         MML_REQUIRE(h->has_model, "no model");
         mml_ctx* c = h->ctx;
         if (c->nranks <= 1 && !c->comm) return;  // no communicator: nothing to average
@@ -3261,6 +3283,7 @@ extern "C" mml_status mml_bmf_fold_in(mml_bmf* h, int32_t n_fold, const int64_t*
     return guard([&] {
         check_handle(h);
         single_device_only(h);
+        no_ring(h, "fold_in");
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(!is_asym(h), "the asymmetric models have their own FoldIn (not on the GPU path)");
         MML_REQUIRE(n_fold >= 0 && num_iter >= 0, "negative sizes");
@@ -3359,6 +3382,7 @@ extern "C" mml_status mml_bmf_retrain(mml_bmf* h, int32_t side, int32_t n_rows,
     return guard([&] {
         check_handle(h);
         single_device_only(h);
+        no_ring(h, "retrain");
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(h->p.model == MML_MF_BIASED || h->p.model == MML_MF_PLAIN,
                     "RetrainUser / RetrainItem on the GPU: BiasedMatrixFactorization and "
@@ -3440,6 +3464,7 @@ extern "C" mml_status mml_bmf_predict_vectors(mml_bmf* h, int32_t n_vectors, con
     return guard([&] {
         check_handle(h);
         single_device_only(h);
+        no_ring(h, "predict_vectors");
         MML_REQUIRE(h->has_model, "no model");
         MML_REQUIRE(!is_asym(h), "the asymmetric models have their own FoldIn (not on the GPU path)");
         MML_REQUIRE(n_vectors >= 0 && n >= 0, "negative sizes");

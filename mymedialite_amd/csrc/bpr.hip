@@ -705,6 +705,7 @@ struct mml_bpr {
     mml::DeviceArray<float> avg_stage;
     hipEvent_t ev_ar0 = nullptr, ev_ar1 = nullptr;
     int64_t n_events = 0, nnz = 0;
+    int64_t hog_waves = 0;  // mml_bpr_set_hogwild_waves (0: by the epoch size)
     int32_t n_eligible = 0;
     bool has_data = false, has_model = false, has_order = false, has_triples = false;
     float last_ms = 0.0f, last_update_ms = 0.0f;
@@ -1393,6 +1394,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)65536;
         }();
         int64_t waves = std::min<int64_t>(256 * 32, std::max<int64_t>(1, n / min_chunk));
+        if (h->hog_waves > 0 && waves >= 16) waves = std::min<int64_t>(256 * 32, h->hog_waves);
         // fewer than 16 waves' worth of samples run as ONE workgroup: one CU, one L2, where 2+
         // workgroups on different XCDs would each cache the hot item rows and overwrite each
         // other's updates on write-back (bmf.hip launch_hogwild)
@@ -1701,6 +1703,15 @@ extern "C" mml_status mml_bpr_set_rows(mml_bpr* h, int32_t side, int32_t n_rows,
             MML_HIP(hipMemcpyAsync(M + (int64_t)rows[x] * h->ld, values + (int64_t)x * h->k,
                                    sizeof(float) * h->k, hipMemcpyHostToDevice, st));
         MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+extern "C" mml_status mml_bpr_set_hogwild_waves(mml_bpr* h, int64_t waves) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(waves >= 0 && waves <= 256 * 32, "waves must be in [0, 8192]");
+        h->hog_waves = waves;
+        for (mml_bpr* s : h->shards) s->hog_waves = waves;
     });
 }
 

@@ -14,11 +14,14 @@
  *
  * Build: oracle/Makefile (-O2 -ffp-contract=off: C# never contracts a*b+c into an FMA).
  */
+#define _GNU_SOURCE
 #include <math.h>
+#include <stdatomic.h>
 #include <stdint.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 /* ------------------------------------------------------------------------------------------
  * System.Random(int seed) -- .NET reference-source Knuth subtractive generator (BCL; called via
@@ -1090,6 +1093,108 @@ void ora_bpr_epoch(ora_rng* r, const ora_bpr_params* p, const int64_t* off, cons
     }
     free(rem);
     free(left);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Large-set drivers of the same arithmetic (C3-density checks).  Both produce exactly what the
+ * sequential loops above produce: the sampler draws from the RNG in the same order and
+ * UpdateFactors runs over the same triples in the same order.  They only overlap the memory
+ * latency of a 1 M x 1 M set -- triples do not depend on the factors (BPRMF.cs:216-226), so the
+ * sampler can run ahead of the updates, and the rows of the next triples can be prefetched.
+ * ---------------------------------------------------------------------------------------- */
+#define ORA_AHEAD 8
+
+static void ora_bpr_prefetch(const ora_bpr_params* p, const int32_t* t, const float* U,
+                             const float* V) {
+    const int64_t k = p->k;
+    for (int64_t f = 0; f < k; f += 16) {
+        __builtin_prefetch(U + (int64_t)t[0] * k + f, 1);
+        __builtin_prefetch(V + (int64_t)t[1] * k + f, 1);
+        __builtin_prefetch(V + (int64_t)t[2] * k + f, 1);
+    }
+}
+
+/* UpdateFactors over given triples in order (a replay of a recorded triple stream) */
+void ora_bpr_apply_triples(const ora_bpr_params* p, const int32_t* tu, const int32_t* ti,
+                           const int32_t* tj, int64_t n, float* U, float* V, float* bias) {
+    for (int64_t c = 0; c < n; c++) {
+        if (c + ORA_AHEAD < n) {
+            const int32_t t[3] = {tu[c + ORA_AHEAD], ti[c + ORA_AHEAD], tj[c + ORA_AHEAD]};
+            ora_bpr_prefetch(p, t, U, V);
+        }
+        ora_bpr_update(p, tu[c], ti[c], tj[c], U, V, bias);
+    }
+}
+
+#define ORA_RING (1 << 16)
+typedef struct {
+    ora_rng* r;
+    const ora_bpr_params* p;
+    const int64_t *off;
+    const int32_t *rows, *sorted;
+    int64_t n;
+    int32_t* ring; /* 3 * ORA_RING */
+    _Atomic int64_t head, tail;
+} ora_bpr_pipe;
+
+static void* ora_bpr_producer(void* arg) {
+    ora_bpr_pipe* q = (ora_bpr_pipe*)arg;
+    for (int64_t c = 0; c < q->n; c++) {
+        while (c - atomic_load_explicit(&q->tail, memory_order_acquire) >= ORA_RING) {
+        }
+        ora_bpr_sample_triple(q->r, q->p, q->off, q->rows, q->sorted, q->ring + 3 * (c % ORA_RING));
+        atomic_store_explicit(&q->head, c + 1, memory_order_release);
+    }
+    return NULL;
+}
+
+/* ora_bpr_epoch for the default sampler (SampleTriple per event, :216-226): one thread samples,
+ * the caller applies UpdateFactors in sample order, ORA_AHEAD triples' rows prefetched */
+void ora_bpr_epoch_pipelined(ora_rng* r, const ora_bpr_params* p, const int64_t* off,
+                             const int32_t* rows, const int32_t* sorted, int64_t num_events,
+                             float* U, float* V, float* bias, int32_t* trace) {
+    if (p->sampler != 0) {
+        ora_bpr_epoch(r, p, off, rows, sorted, num_events, U, V, bias, trace);
+        return;
+    }
+    ora_bpr_pipe* q = (ora_bpr_pipe*)calloc(1, sizeof(ora_bpr_pipe));
+    q->r = r;
+    q->p = p;
+    q->off = off;
+    q->rows = rows;
+    q->sorted = sorted;
+    q->n = num_events;
+    q->ring = (int32_t*)malloc(sizeof(int32_t) * 3 * ORA_RING);
+    atomic_init(&q->head, 0);
+    atomic_init(&q->tail, 0);
+    pthread_t th;
+    pthread_create(&th, NULL, ora_bpr_producer, q);
+    for (int64_t c = 0; c < num_events; c++) {
+        int64_t h;
+        while ((h = atomic_load_explicit(&q->head, memory_order_acquire)) <= c) {
+        }
+        if (c + ORA_AHEAD < h) ora_bpr_prefetch(p, q->ring + 3 * ((c + ORA_AHEAD) % ORA_RING), U, V);
+        const int32_t* t = q->ring + 3 * (c % ORA_RING);
+        if (trace) {
+            trace[3 * c] = t[0];
+            trace[3 * c + 1] = t[1];
+            trace[3 * c + 2] = t[2];
+        }
+        ora_bpr_update(p, t[0], t[1], t[2], U, V, bias);
+        atomic_store_explicit(&q->tail, c + 1, memory_order_release);
+    }
+    pthread_join(th, NULL);
+    free(q->ring);
+    free(q);
+}
+
+/* transparent huge pages for a large array before it is first written (fewer TLB misses on the
+ * random row accesses of the large-set drivers); advice only, no effect on any value */
+int ora_madvise_huge(void* ptr, int64_t bytes) {
+    const uintptr_t a = ((uintptr_t)ptr + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+    const uintptr_t e = ((uintptr_t)ptr + (uintptr_t)bytes) & ~(uintptr_t)((2u << 20) - 1);
+    if (e <= a) return 0;
+    return madvise((void*)a, e - a, MADV_HUGEPAGE);
 }
 
 /* ------------------------------------------------------------------------------------------

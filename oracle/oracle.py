@@ -114,6 +114,10 @@ def lib():
                                    ctypes.c_int64]
         L.ora_bpr_epoch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _i64p, _i32p, _i32p,
                                     ctypes.c_int64, _f32p, _f32p, _f32p, _i32p]
+        L.ora_bpr_epoch_pipelined.argtypes = L.ora_bpr_epoch.argtypes
+        L.ora_bpr_apply_triples.argtypes = [ctypes.c_void_p, _i32p, _i32p, _i32p, ctypes.c_int64,
+                                            _f32p, _f32p, _f32p]
+        L.ora_madvise_huge.argtypes = [ctypes.c_void_p, ctypes.c_int64]
         L.ora_asym_iterate.argtypes = [
             ctypes.c_void_p, _i32p, _i32p, _f32p, _i32p, ctypes.c_int64, _f32p, _f32p, _f32p,
             _f32p, _i32p, _i32p, _f32p, _i64p, _i32p, _f32p, _f32p, _i64p, _i32p, _f32p, _f32p,
@@ -760,10 +764,9 @@ def insertion_order_rows(rows_of, cols_of, n_rows):
 
 
 def sorted_rows(off, cols):
-    s = cols.copy()
-    for u in range(len(off) - 1):
-        s[off[u]:off[u + 1]].sort()
-    return s
+    """Each CSR row's columns sorted ascending (one lexsort over (row, col))."""
+    row = np.repeat(np.arange(len(off) - 1, dtype=np.int64), np.diff(off))
+    return i32(cols[np.lexsort((cols, row))])
 
 
 def bpr_train(users, items, n_users, n_items, *, seed=1, k=10, num_iter=30, learn_rate=0.05,
@@ -822,6 +825,48 @@ def bpr_epoch(rng: Rng, users, items, n_users, n_items, U, V, bias, *, learn_rat
     lib().ora_bpr_epoch(rng._buf, ctypes.byref(p), _p(off, _i64p), _p(rows, _i32p),
                         _p(srt, _i32p), len(users), _p(U, _f32p), _p(V, _f32p), _p(bias, _f32p),
                         None)
+
+
+def bpr_csr_distinct(users, items, n_users):
+    """insertion_order_rows + sorted_rows for DISTINCT (user, item) events: the HashSet rows in
+    first-insertion order are then the events stably sorted by user (for the large-set checks;
+    equal to the general form on distinct events, tests/test_oracle.py)."""
+    users, items = i32(users), i32(items)
+    order = np.argsort(users, kind="stable")
+    rows = items[order]
+    off = np.zeros(n_users + 1, np.int64)
+    off[1:] = np.cumsum(np.bincount(users, minlength=n_users))
+    return off, rows, sorted_rows(off, rows)
+
+
+def huge_empty(shape, dtype=np.float32):
+    """np.empty with transparent-huge-page advice before first touch (large factor matrices)."""
+    a = np.empty(shape, dtype)
+    lib().ora_madvise_huge(a.ctypes.data, a.nbytes)
+    return a
+
+
+def bpr_epoch_from(rng: Rng, off, rows, srt, n_events, U, V, bias, *, learn_rate=0.05,
+                   reg_u=0.0025, reg_i=0.0025, reg_j=0.00025, bias_reg=0.0, trace=None):
+    """One BPRMF.Iterate() with the default sampler (:216-226) on a prepared CSR, in place,
+    sampling on a second thread ahead of the updates (ora_bpr_epoch_pipelined: the same triples
+    and results as ora_bpr_epoch)."""
+    k = U.shape[1]
+    p = _BprParams(k, 1, 1, 1, learn_rate, reg_u, reg_i, reg_j, bias_reg, U.shape[0] - 1,
+                   V.shape[0] - 1, 0, 0, None, None, 0)
+    lib().ora_bpr_epoch_pipelined(rng._buf, ctypes.byref(p), _p(off, _i64p), _p(rows, _i32p),
+                                  _p(srt, _i32p), n_events, _p(U, _f32p), _p(V, _f32p),
+                                  _p(bias, _f32p), _p(trace, _i32p))
+
+
+def bpr_apply_triples(tu, ti, tj, U, V, bias, *, learn_rate=0.05, reg_u=0.0025, reg_i=0.0025,
+                      reg_j=0.00025, bias_reg=0.0):
+    """UpdateFactors (BPRMF.cs:330-374) over recorded triples in order, in place."""
+    tu, ti, tj = i32(tu), i32(ti), i32(tj)
+    p = _BprParams(U.shape[1], 1, 1, 1, learn_rate, reg_u, reg_i, reg_j, bias_reg, U.shape[0] - 1,
+                   V.shape[0] - 1, 0, 0, None, None, 0)
+    lib().ora_bpr_apply_triples(ctypes.byref(p), _p(tu, _i32p), _p(ti, _i32p), _p(tj, _i32p),
+                                len(tu), _p(U, _f32p), _p(V, _f32p), _p(bias, _f32p))
 
 
 def bpr_update(u, i, j, U, V, bias, *, learn_rate=0.05, reg_u=0.0025, reg_i=0.0025,

@@ -344,3 +344,63 @@ def test_lockstep_staleness_model_reduces_to_the_loop():
         np.testing.assert_array_equal(runs[(1, 1)][key], runs[None][key])
     assert not np.array_equal(runs[(32, 4)]["V"], runs[None]["V"])
     assert np.isfinite(runs[(32, 4)]["U"]).all()
+
+
+def _distinct_events(n_users=3000, n_items=2000, n=60_000, seed=4):
+    rs = np.random.default_rng(seed)
+    key = np.unique(rs.integers(0, n_users, n).astype(np.int64) * n_items +
+                    rs.integers(0, n_items, n))
+    key = key[rs.permutation(len(key))]
+    return (key // n_items).astype(np.int32), (key % n_items).astype(np.int32), n_users, n_items
+
+
+def test_bpr_csr_distinct_equals_insertion_order_rows():
+    """The large-set CSR (stable sort by user) equals the general HashSet-order restatement on
+    distinct events, and the lexsort sorted_rows equals a per-row sort."""
+    u, i, nu, ni = _distinct_events()
+    off, rows = O.insertion_order_rows(u, i, nu)
+    off2, rows2, srt2 = O.bpr_csr_distinct(u, i, nu)
+    np.testing.assert_array_equal(off, off2)
+    np.testing.assert_array_equal(rows, rows2)
+    loop = rows.copy()
+    for x in range(nu):
+        loop[off[x]:off[x + 1]].sort()
+    np.testing.assert_array_equal(srt2, loop)
+
+
+def test_bpr_pipelined_epoch_and_replay_equal_sequential_epoch():
+    """ora_bpr_epoch_pipelined (sampler thread ahead of the updates, prefetch) gives the triples,
+    the model and the RNG state of ora_bpr_epoch exactly; replaying its trace with
+    ora_bpr_apply_triples gives the same model again."""
+    u, i, nu, ni = _distinct_events()
+    k = 16
+    off, rows, srt = O.bpr_csr_distinct(u, i, nu)
+    runs = []
+    for pipelined in (False, True):
+        rng = O.Rng(5)
+        U = rng.fill_normal(nu * k, 0, 0.1).reshape(nu, k)
+        V = rng.fill_normal(ni * k, 0, 0.1).reshape(ni, k)
+        b = np.zeros(ni, np.float32)
+        U0, V0 = U.copy(), V.copy()
+        tr = np.empty(3 * len(u), np.int32)
+        if pipelined:
+            O.bpr_epoch_from(rng, off, rows, srt, len(u), U, V, b, trace=tr)
+        else:
+            p = O._BprParams(k, 1, 1, 1, 0.05, 0.0025, 0.0025, 0.00025, 0.0, nu - 1, ni - 1)
+            O.lib().ora_bpr_epoch(rng._buf, O.ctypes.byref(p), O._p(off, O._i64p),
+                                  O._p(rows, O._i32p), O._p(srt, O._i32p), len(u),
+                                  O._p(U, O._f32p), O._p(V, O._f32p), O._p(b, O._f32p),
+                                  O._p(tr, O._i32p))
+        runs.append((U, V, b, tr, rng.next_double(), U0, V0))
+    (U, V, b, tr, nd, U0, V0), (U2, V2, b2, tr2, nd2, _, _) = runs
+    np.testing.assert_array_equal(tr, tr2)
+    np.testing.assert_array_equal(U, U2)
+    np.testing.assert_array_equal(V, V2)
+    np.testing.assert_array_equal(b, b2)
+    assert nd == nd2
+    t = tr.reshape(-1, 3)
+    b3 = np.zeros(ni, np.float32)
+    O.bpr_apply_triples(t[:, 0], t[:, 1], t[:, 2], U0, V0, b3)
+    np.testing.assert_array_equal(U0, U)
+    np.testing.assert_array_equal(V0, V)
+    np.testing.assert_array_equal(b3, b)
