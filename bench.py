@@ -89,29 +89,38 @@ def main():
     ap.add_argument("--no-extras", action="store_true",
                     help="N = 1 default run: the C4 line only (no c2 / c3 / c5 keys)")
     args = ap.parse_args()
-    world = env_rank()[0]
+    world, rank, _ = env_rank()
+    init_host_group(world)  # one gloo group for the whole run (unique ids, timings, AUC sums)
     workload = args.workload or "c4"
     fn = {"c2": bench_c2, "c3": bench_bpr, "c4": bench_c4, "c5": bench_wrmf,
           "svdpp": bench_svdpp}[workload]
     if workload == "c2" and world > 1:
         raise SystemExit("C2 is the single-GPU configuration; N > 1 runs C4 (--workload c4)")
     line = fn(args)
-    if world == 1 and args.workload is None and not args.no_extras:
-        # the other configurations on the same GPU, as keys of the one line (BASELINE.json
-        # configs 2, 3 and 5)
-        for key, f, steps, warmup in (("c2", bench_c2, 10, 2), ("c3", bench_bpr, 2, 1),
-                                      ("c5", bench_wrmf, 2, 1)):
+    if args.workload is None and not args.no_extras:
+        # the other configurations as keys of the one line (BASELINE.json configs 2, 3 and 5):
+        # at N = 1 on the same GPU; at N > 1 (torch.distributed.run) C3 as BPRMF user shards with
+        # the per-epoch ncclAvg and C5 as WRMF row shards with the per-half-step all-gather, both
+        # strong scaling over the N = 1 data sets (C2 is the single-GPU configuration)
+        extras = ([("c2", bench_c2, 10, 2)] if world == 1 else []) + [
+            ("c3", bench_bpr, 2, 1), ("c5", bench_wrmf, 2, 1)]
+        for key, f, steps, warmup in extras:
             sub = argparse.Namespace(**vars(args))
             sub.steps, sub.warmup = steps, warmup
             torch.cuda.empty_cache()
             t0 = time.perf_counter()
             x = f(sub)
-            x["wall_s"] = time.perf_counter() - t0
-            for drop in ("n_gpus", "higher_is_better", "vs_baseline", "data"):
-                x.pop(drop, None)
-            line[key] = x
-            print(f"{key}: {x['value']:.4g} {x['unit']} ({x['wall_s']:.0f} s)", file=sys.stderr,
-                  flush=True)
+            wall = max_over_ranks(time.perf_counter() - t0)
+            if rank == 0:
+                x["wall_s"] = wall
+                for drop in ("n_gpus", "higher_is_better", "vs_baseline", "data"):
+                    x.pop(drop, None)
+                line[key] = x
+                print(f"{key}: {x['value']:.4g} {x['unit']} ({x['wall_s']:.0f} s)",
+                      file=sys.stderr, flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
     if line is not None:
         print(json.dumps(line), flush=True)
 
@@ -234,6 +243,8 @@ def bench_c2(args):
         traffic, traffic_note = pmc_traffic("r4_c2_traffic.json", avg_kernel_ms)
     kernel = (N.last_kernel("mml_bmf_last_kernel", h) or
               f"bmf_sgd_ordered_kernel (schedule {args.schedule})")
+    ceiling = (box_ceiling("mml_bmf_replay_traffic", h, avg_kernel_ms, n_local * bpu)
+               if args.schedule == "hogwild" else None)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -264,7 +275,9 @@ def bench_c2(args):
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_note": traffic_note,
                          "kernel": kernel,
-                         "kernel_avg_ms": avg_kernel_ms, "bytes_per_update": bpu},
+                         "kernel_avg_ms": avg_kernel_ms, "bytes_per_update": bpu,
+                         "box_ceiling": ceiling,
+                         "frac_of_box_ceiling": ceiling["frac_of_box_ceiling"] if ceiling else None},
             "cpu_baseline": cpu,
         }
     N.lib().mml_bmf_destroy(h)
@@ -301,6 +314,23 @@ def pmc_traffic(name, kernel_ms, alg_bytes=None):
             f"same-pattern calibration {t['traffic_calibrated_bytes_per_launch'] / 1e9:.1f} GB "
             f"({t['calibrated_over_algorithmic']:.2f} x)")
     return gbs, note
+
+
+def box_ceiling(symbol, h, kernel_ms, alg_bytes, reps=3):
+    """The dominant kernel's traffic replayed without its arithmetic on the same GPU in the same run
+    (mml_bmf_replay_traffic / mml_bpr_replay_traffic: same launch, stream, rows and access flags,
+    loaded values stored back unchanged, the model untouched), after the timed steps: the access
+    pattern's ceiling on THIS box, so box-to-box spread and kernel changes can be told apart."""
+    out = np.zeros(1, np.float32)
+    ms = []
+    for _ in range(reps):
+        N.check(getattr(N.lib(), symbol)(h, N.ptr(out, N._f32p)))
+        ms.append(float(out[0]))
+    r = float(np.median(ms))
+    return {"replay_ms": r, "replay_GBps": alg_bytes / (r * 1e-3) / 1e9,
+            "frac_of_box_ceiling": r / kernel_ms,
+            "note": f"{symbol}: the kernel's memory traffic with no arithmetic, median of {reps} "
+                    f"launches on this GPU; frac_of_box_ceiling = replay time / kernel time"}
 
 
 def cpu_model() -> str:
@@ -478,6 +508,8 @@ def bench_c4(args):
     ar = np.zeros(1, np.float32)
     N.check(N.lib().mml_bmf_last_allreduce_ms(h, N.ptr(ar, N._f32p)))
     kernel = N.last_kernel("mml_bmf_last_kernel", h)
+    ceiling = box_ceiling("mml_bmf_replay_traffic", h, float(np.mean(kernel_ms)),
+                          n_local * bytes_per_update(k))
     rmse = evaluate()
     value = n_total * args.steps / elapsed
     avg_kernel_ms = float(np.mean(kernel_ms))
@@ -522,13 +554,12 @@ def bench_c4(args):
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_note": traffic_note, "kernel": kernel,
                          "kernel_avg_ms": avg_kernel_ms, "bytes_per_update": bpu,
-                         "per": "GPU (rank 0's shard)"},
+                         "per": "GPU (rank 0's shard)", "box_ceiling": ceiling,
+                         "frac_of_box_ceiling": ceiling["frac_of_box_ceiling"]},
             "cpu_baseline": cpu,
         }
     N.lib().mml_bmf_destroy(h)
     ctx.close()
-    if world > 1:
-        torch.distributed.destroy_process_group()
     return line
 
 
@@ -596,6 +627,8 @@ def bench_bpr(args):
     if world > 1:
         torch.distributed.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
+    ar = np.zeros(1, np.float32)
+    N.check(N.lib().mml_bpr_last_allreduce_ms(h, N.ptr(ar, N._f32p)))
     # held-out AUC after the timed epochs (Eval.Items.Evaluate's AUC, Items.cs:126-209 /
     # AUC.cs:42-68, on the device): all 1M items as candidates in a seeded shuffled order
     t1 = time.perf_counter()
@@ -619,6 +652,8 @@ def bench_bpr(args):
     if k == 128 and n_total == 500_000_000 and args.sampler == "uniform_user" and world == 1:
         traffic, traffic_note = pmc_traffic("r4_c3_traffic.json", upd_ms, n * bpu)
     kernel = N.last_kernel("mml_bpr_last_kernel", h)
+    # the last epoch's triples again, against that epoch's update kernel
+    ceiling = box_ceiling("mml_bpr_replay_traffic", h, ums[-1], n * bpu)
     line = {
         "metric": "BPR triple-updates/sec, BPRMF k=128 (C3)",
         "value": n_events * args.steps / elapsed,
@@ -646,7 +681,12 @@ def bench_bpr(args):
                      "frac_epoch": n * bpu / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "frac_note": "frac = the update kernel alone; frac_epoch = the same bytes "
                                   "over the whole device epoch (sampler + XCD partition + "
-                                  "update)"},
+                                  "update)",
+                     "box_ceiling": ceiling,
+                     "frac_of_box_ceiling": ceiling["frac_of_box_ceiling"]},
+        "allreduce_ms": float(ar[0]) if world > 1 else None,
+        "allreduce_note": "device time of the last step's ncclAvg all-reduce of V||b (HIP "
+                          "events around it on the library stream)" if world > 1 else None,
         "auc": auc,
         "auc_users": int(acc[1].item()),
         "auc_note": (f"held-out AUC after {args.warmup + args.steps} epochs: 100k test users "
@@ -658,8 +698,6 @@ def bench_bpr(args):
     }
     N.lib().mml_bpr_destroy(h)
     ctx.close()
-    if world > 1:
-        torch.distributed.destroy_process_group()
     return line if rank == 0 else None
 
 
@@ -717,6 +755,8 @@ def bench_wrmf(args):
     if world > 1:
         torch.distributed.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
+    gather = np.zeros(1, np.float32)
+    N.check(N.lib().mml_wrmf_last_allgather_ms(h, N.ptr(gather, N._f32p)))
     ran = ctypes.c_int32(0)
     corr = np.zeros(8, np.float32)
     N.check(N.lib().mml_wrmf_last_refine_passes(h, ctypes.byref(ran), N.ptr(corr, N._f32p)))
@@ -780,6 +820,10 @@ def bench_wrmf(args):
         line.update(check)
     if world > 1:
         line["config"]["parallelism"] = f"row shards x{world}, RCCL all-gather per half-step"
+        line["allgather_ms"] = float(gather[0])
+        line["allgather_note"] = ("device time of the last iteration's two all-gathers (U after "
+                                  "the user half, V after the item half: grouped ncclBroadcast "
+                                  "of each rank's rows), rank 0")
     N.lib().mml_wrmf_destroy(h)
     ctx.close()
     return line if rank == 0 else None

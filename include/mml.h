@@ -276,6 +276,11 @@ mml_status mml_bmf_last_kernel(mml_bmf* h, char* buf, int32_t cap);
  * complexity term; ComputeObjective = (float)(out[0] + out[1]).  BoldDriver's UpdateLearnRate
  * (:225-244) compares consecutive values on the host. */
 mml_status mml_bmf_objective(mml_bmf* h, double* out);
+/* The HOGWILD epoch's memory traffic without its arithmetic (ABI 10): the same launch over the same
+ * stream, rows and biases with the same access flags, every loaded value stored back unchanged
+ * (the model is not modified).  *out_ms = its device time: the access pattern's ceiling on the GPU
+ * it runs on, which bench.py reports beside the epoch (frac_of_box_ceiling). */
+mml_status mml_bmf_replay_traffic(mml_bmf* h, float* out_ms);
 /* Multi-GPU (user shards): in-place RCCL all-reduce of item factors and item
  * biases over the context's communicator with ncclAvg (model averaging).  Stream-ordered (ABI 6):
  * the call returns once the collective is enqueued; the next call on the handle runs after it. */
@@ -440,6 +445,14 @@ mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const int32_t* item
 /* out[0] = the last epoch's device time (ms), out[1] = its update kernel alone (the rest is the
  * triple sampler) */
 mml_status mml_bpr_last_timing(mml_bpr* h, float* out);
+/* Device time of the last item average (ABI 10): mml_bpr_allreduce_items on a communicator, or the
+ * peer-copy average inside a repeated-device mml_bpr_iterate; waits for it; 0 when none ran. */
+mml_status mml_bpr_last_allreduce_ms(mml_bpr* h, float* out);
+/* The last HOGWILD epoch's update launch again without its arithmetic (ABI 10): the same triples,
+ * rows, biases, geometry and access flags, every loaded value stored back unchanged (the model is
+ * not modified).  *out_ms = its device time, the access pattern's ceiling on this GPU (bench.py
+ * frac_of_box_ceiling).  Needs a BPRMF (not SoftMargin) HOGWILD epoch before it. */
+mml_status mml_bpr_replay_traffic(mml_bpr* h, float* out_ms);
 /* The update kernel of the last Hogwild epoch as rocprofv3 names it, e.g.
  * "bpr_update_kernel<32, false, 27>" (ABI 9); NUL-terminated, truncated to cap bytes. */
 mml_status mml_bpr_last_kernel(mml_bpr* h, char* buf, int32_t cap);
@@ -514,6 +527,9 @@ mml_status mml_wrmf_retrain(mml_wrmf* h, int32_t side, int32_t n_rows, const int
 mml_status mml_wrmf_predict(mml_wrmf* h, const int32_t* users, const int32_t* items, int64_t n,
                             float* out);
 mml_status mml_wrmf_last_timing(mml_wrmf* h, float* out);
+/* Device time of the last mml_wrmf_iterate's two row-shard all-gathers (ABI 10; U after the user
+ * half, V after the item half; the slowest shard on a multi-device context); 0 on one rank. */
+mml_status mml_wrmf_last_allgather_ms(mml_wrmf* h, float* out);
 /* The most refinement passes a half-step of the last mml_wrmf_iterate ran (ABI 6);
  * corrections (nullable, [8]): per half-step (users 0..3, items 4..7) and pass, the largest
  * correction relative to 1 + |x| that decided whether another pass ran (0: not read back). */

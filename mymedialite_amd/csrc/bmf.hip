@@ -105,6 +105,10 @@ struct RatingStep {
 // delta = err * i_f - Regularization * u_f in float, widened to double; Inc adds
 // (float)(current_learnrate * delta).
 constexpr int kPlainMF = 8;
+// The Hogwild kernel's memory traffic without its arithmetic (mml_bmf_replay_traffic): the same
+// launch, stream, rows, biases and access flags, every loaded value stored back unchanged -- the
+// access pattern's own ceiling on the GPU it runs on, measured beside the epoch (bench.py)
+constexpr int kReplayTraffic = 9;
 
 template <>
 struct RatingStep<kPlainMF> {
@@ -339,38 +343,69 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
     auto apply = [&](int32_t u, int32_t i, float r, const float4 (&pu)[VPL],
                      const float4 (&qi)[VPL], float bu_u, float bi_i) {
         const int64_t ou = (int64_t)u * ld4 + q, oi = (int64_t)i * ld4 + q;
-        float part = 0.0f;
+        if constexpr (LOSS == kReplayTraffic) {
+            // the loaded values, opaque to the compiler, stored with the epoch's access flags
+            float4 a[VPL], c[VPL];
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) {
-            part += pu[v].x * qi[v].x;
-            part += pu[v].y * qi[v].y;
-            part += pu[v].z * qi[v].z;
-            part += pu[v].w * qi[v].w;
-        }
-        part = group_sum<LPR>(part);
-        const RatingStep<LOSS> st(s, part, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
-        if (biased && q == 0) {
-            if constexpr (BTH)
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, st.new_bu), burs,
-                                                      (uint32_t)u * 4u, 0, 16);
-            else
-                store1<COH>(bu + u, st.new_bu);
-            store1<COH>(bi + i, st.new_bi);
-        }
+            for (int v = 0; v < VPL; ++v) {
+                a[v] = pu[v];
+                c[v] = qi[v];
+                asm volatile("" : "+v"(a[v].x), "+v"(a[v].y), "+v"(a[v].z), "+v"(a[v].w));
+                asm volatile("" : "+v"(c[v].x), "+v"(c[v].y), "+v"(c[v].z), "+v"(c[v].w));
+            }
+            asm volatile("" : "+v"(bu_u), "+v"(bi_i) : "v"(r));
+            if (q == 0) {
+                if constexpr (BTH)
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bu_u), burs,
+                                                          (uint32_t)u * 4u, 0, 16);
+                else
+                    store1<COH>(bu + u, bu_u);
+                store1<COH>(bi + i, bi_i);
+            }
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) {
-            const float4 a = pu[v], c = qi[v];
-            const float4 nu = make_float4(st.new_u(s, a.x, c.x), st.new_u(s, a.y, c.y),
-                                          st.new_u(s, a.z, c.z), st.new_u(s, a.w, c.w));
-            if constexpr (UTH)
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, nu), urs,
-                    (uint32_t)(ou + LPR * v) * 16u, 0, 16);
-            else
-                store4<COH>(U4 + ou + LPR * v, nu);
-            store4<COH>(V4 + oi + LPR * v,
-                        make_float4(st.new_i(s, a.x, c.x), st.new_i(s, a.y, c.y),
-                                    st.new_i(s, a.z, c.z), st.new_i(s, a.w, c.w)));
+            for (int v = 0; v < VPL; ++v) {
+                if constexpr (UTH)
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, a[v]),
+                        urs, (uint32_t)(ou + LPR * v) * 16u, 0, 16);
+                else
+                    store4<COH>(U4 + ou + LPR * v, a[v]);
+                store4<COH>(V4 + oi + LPR * v, c[v]);
+            }
+        } else {
+            float part = 0.0f;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+                part += pu[v].x * qi[v].x;
+                part += pu[v].y * qi[v].y;
+                part += pu[v].z * qi[v].z;
+                part += pu[v].w * qi[v].w;
+            }
+            part = group_sum<LPR>(part);
+            const RatingStep<LOSS> st(s, part, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
+            if (biased && q == 0) {
+                if constexpr (BTH)
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, st.new_bu),
+                                                          burs, (uint32_t)u * 4u, 0, 16);
+                else
+                    store1<COH>(bu + u, st.new_bu);
+                store1<COH>(bi + i, st.new_bi);
+            }
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+                const float4 a = pu[v], c = qi[v];
+                const float4 nu = make_float4(st.new_u(s, a.x, c.x), st.new_u(s, a.y, c.y),
+                                              st.new_u(s, a.z, c.z), st.new_u(s, a.w, c.w));
+                if constexpr (UTH)
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, nu), urs,
+                        (uint32_t)(ou + LPR * v) * 16u, 0, 16);
+                else
+                    store4<COH>(U4 + ou + LPR * v, nu);
+                store4<COH>(V4 + oi + LPR * v,
+                            make_float4(st.new_i(s, a.x, c.x), st.new_i(s, a.y, c.y),
+                                        st.new_i(s, a.z, c.z), st.new_i(s, a.w, c.w)));
+            }
         }
     };
     for (int64_t base = begin; base < end; base += 64) {
@@ -1410,6 +1445,10 @@ struct mml_bmf {
     mml::XcdSplit xs;
     mml::DeviceArray<int32_t> xu, xi, xr;  // xr holds the float ratings' bits
     bool has_xstream = false;
+    // user phases of the XCD stream (hogwild_phases): phase-major, XCD-group-minor spans, so that
+    // one launch per phase touches 1/P of U; poff = the P * 8 + 1 span offsets (device)
+    int32_t n_phases = 1;
+    mml::DeviceArray<int64_t> poff;
     // multi-device context: one single-device handle per GPU over a user range ub[d] .. ub[d + 1]
     // (U, b_u trained there; V, b_i replicated and averaged after every epoch)
     std::vector<mml_bmf*> shards;
@@ -1514,6 +1553,7 @@ void finish_data(mml_bmf* h, const int32_t* order_dev) {
     h->G = 0;
     h->has_positions = false;
     h->has_xstream = false;
+    h->n_phases = 1;
     h->has_data = true;
 }
 
@@ -1644,6 +1684,125 @@ void ensure_xstream(mml_bmf* h) {
     h->has_xstream = true;
 }
 
+// the phase of a user: a fixed hash, so every phase is a random 1/P of the users whatever the id
+// order of the data set
+__device__ __forceinline__ int32_t user_phase(int32_t u, int32_t P) {
+    return (int32_t)(mml::mix64((uint64_t)(uint32_t)u ^ 0x6A09E667F3BCC909ull) % (uint64_t)P);
+}
+
+// key of stream position x of the XCD stream: phase of its user * 8 + its XCD group
+__global__ __launch_bounds__(256) void phase_keys_kernel(const int32_t* __restrict__ xu,
+                                                         const int64_t* __restrict__ goff,
+                                                         int64_t n, int32_t P,
+                                                         uint16_t* __restrict__ key,
+                                                         int32_t* __restrict__ idx) {
+    int64_t g_off[9];
+#pragma unroll
+    for (int g = 0; g < 9; ++g) g_off[g] = goff[g];
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        int g = 0;
+#pragma unroll
+        for (int c = 1; c < 8; ++c) g += x >= g_off[c];
+        key[x] = (uint16_t)(user_phase(xu[x], P) * 8 + g);
+        idx[x] = (int32_t)x;
+    }
+}
+
+__global__ __launch_bounds__(256) void gather3_kernel(const int32_t* __restrict__ idx, int64_t n,
+                                                      const int32_t* __restrict__ a,
+                                                      const int32_t* __restrict__ b,
+                                                      const int32_t* __restrict__ c,
+                                                      int32_t* __restrict__ oa,
+                                                      int32_t* __restrict__ ob,
+                                                      int32_t* __restrict__ oc) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t y = idx[x];
+        oa[x] = a[y];
+        ob[x] = b[y];
+        oc[x] = c[y];
+    }
+}
+
+// span offsets of the sorted keys: off[k] = first position with key >= k, k = 0 .. nk
+__global__ __launch_bounds__(256) void key_offsets_kernel(const uint16_t* __restrict__ key,
+                                                          int64_t n, int32_t nk,
+                                                          int64_t* __restrict__ off) {
+    const int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > nk) return;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int32_t)key[mid] < k) lo = mid + 1;
+        else hi = mid;
+    }
+    off[k] = lo;
+}
+
+// MML_HOGWILD_PHASES (experiments): user phases of the Hogwild epoch.  P > 1 splits every XCD
+// group's stream into P phases by a hash of the user (stable: the visit order is kept within a
+// phase) and runs one launch per phase, so a launch touches 1/P of U -- a phase's rows then stay
+// in the 256 MB Infinity Cache between a user's ratings instead of coming from HBM each time.
+static int32_t hogwild_phases_env() {
+    static const int32_t m = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_HOGWILD_PHASES");
+        return e ? std::max(0, std::min(32, std::atoi(e))) : -1;
+    }();
+    return m;
+}
+int32_t hogwild_phases(const mml_bmf* h) {
+    const int32_t e = hogwild_phases_env();
+    if (e >= 0) return std::max(1, e);
+    return 1;
+}
+
+// the XCD stream reordered phase-major (built once per data set and phase count)
+void ensure_phases(mml_bmf* h, int32_t P) {
+    if (h->n_phases == P) return;
+    hipStream_t st = h->ctx->stream;
+    const int64_t n = h->n;
+    if (P <= 1) {  // back to the plain XCD stream order
+        h->has_xstream = false;
+        h->n_phases = 1;
+        ensure_xstream(h);
+        return;
+    }
+    const int nk = P * 8;
+    int end_bit = 1;
+    while ((1 << end_bit) < nk) ++end_bit;
+    mml::DeviceArray<uint16_t> key, key_s;
+    mml::DeviceArray<int32_t> idx, idx_s;
+    key.alloc(n);
+    key_s.alloc(n);
+    idx.alloc(n);
+    idx_s.alloc(n);
+    phase_keys_kernel<<<grid_for(n), 256, 0, st>>>(h->xu.get(), h->xs.goff.get(), n, P, key.get(),
+                                                   idx.get());
+    MML_HIP(hipGetLastError());
+    size_t tmp_bytes = 0;
+    MML_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, key.get(), key_s.get(),
+                                               idx.get(), idx_s.get(), n, 0, end_bit, st));
+    mml::DeviceArray<uint8_t> tmp;
+    tmp.alloc(std::max<size_t>(1, tmp_bytes));
+    MML_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.get(), tmp_bytes, key.get(), key_s.get(),
+                                               idx.get(), idx_s.get(), n, 0, end_bit, st));
+    mml::DeviceArray<int32_t> ou, oi, orr;
+    ou.alloc(n);
+    oi.alloc(n);
+    orr.alloc(n);
+    gather3_kernel<<<grid_for(n), 256, 0, st>>>(idx_s.get(), n, h->xu.get(), h->xi.get(),
+                                                h->xr.get(), ou.get(), oi.get(), orr.get());
+    h->poff.alloc(nk + 1);
+    key_offsets_kernel<<<(nk + 1 + 255) / 256, 256, 0, st>>>(key_s.get(), n, nk, h->poff.get());
+    MML_HIP(hipGetLastError());
+    MML_HIP(hipStreamSynchronize(st));
+    h->xu.swap(ou);
+    h->xi.swap(oi);
+    h->xr.swap(orr);
+    h->n_phases = P;
+}
+
 // MML_HOGWILD_XCD: 4 (default) = XCD-owned item groups with L2-served item loads, user rows written
 // through and flushing waves; 1 = the groups with L2-served item loads only, 2 = the groups
 // with plain loads, 3 = 1 + user rows written through, 4 = 3 + flushing waves (mml::flushers_per_xcd),
@@ -1703,7 +1862,14 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
 #endif
             default: am = kAccItemL2; break;
         }
+        // user phases: one launch per phase over the phase-major stream
+        const int32_t P = hogwild_phases(h);
+        if (P != h->n_phases) ensure_phases(h, P);
+        su = h->xu.get();
+        si = h->xi.get();
+        sr = reinterpret_cast<const float*>(h->xr.get());
     }
+    const int32_t phases = ng == 8 ? h->n_phases : 1;
     int64_t blocks = (waves + 3) / 4;
     blocks = (blocks + ng - 1) / ng * ng;
     const int32_t wpg = (int32_t)(blocks / ng * 4);
@@ -1715,7 +1881,7 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     const uint32_t bub = (uint32_t)((uint64_t)h->n_users * sizeof(float));
 #define MML_HOG1(LPR, VPL, AM)                                                                  \
     bmf_sgd_hogwild_kernel<LOSS, LPR, VPL, AM><<<(int)blocks, 256, 0, st>>>(                  \
-        su, si, sr, goff, ng, wpg, h->U.get(), h->V.get(), h->bu.get(), h->bi.get(), ld4, vb, bb, \
+        su, si, sr, go, ng, wpg, h->U.get(), h->V.get(), h->bu.get(), h->bi.get(), ld4, vb, bb,   \
         ub, bub, mml::flushers_per_xcd(1), s, cu, ci);                                         \
     h->last_kernel = kernel_label("bmf_sgd_hogwild_kernel", {LOSS, LPR, VPL, (int)(AM)})
 #ifdef MML_EXPERIMENTS
@@ -1739,14 +1905,17 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
         default: MML_HOG1(LPR, VPL, kAccPlain); break;                           \
     }
     // one float4 of U_u and of V_i per lane (VPL 2 measured equal, VPL 4 10 % slower on C2)
-    switch (h->lpr) {
-        case 1: MML_HOGV(1, 1); break;
-        case 2: MML_HOGV(2, 1); break;
-        case 4: MML_HOGV(4, 1); break;
-        case 8: MML_HOGV(8, 1); break;
-        case 16: MML_HOGV(16, 1); break;
-        case 32: MML_HOGV(32, 1); break;
-        default: MML_HOGV(64, 1); break;
+    for (int32_t ph = 0; ph < phases; ++ph) {
+        const int64_t* go = phases > 1 ? h->poff.get() + 8 * ph : goff;
+        switch (h->lpr) {
+            case 1: MML_HOGV(1, 1); break;
+            case 2: MML_HOGV(2, 1); break;
+            case 4: MML_HOGV(4, 1); break;
+            case 8: MML_HOGV(8, 1); break;
+            case 16: MML_HOGV(16, 1); break;
+            case 32: MML_HOGV(32, 1); break;
+            default: MML_HOGV(64, 1); break;
+        }
     }
 #undef MML_HOGV
 #undef MML_HOG_EXP
@@ -3052,6 +3221,29 @@ extern "C" mml_status mml_bmf_last_kernel(mml_bmf* h, char* buf, int32_t cap) {
         const size_t n = std::min<size_t>(k.size(), (size_t)cap - 1);
         std::copy(k.begin(), k.begin() + n, buf);
         buf[n] = 0;
+    });
+}
+
+extern "C" mml_status mml_bmf_replay_traffic(mml_bmf* h, float* out_ms) {
+    return guard([&] {
+        check_handle(h);
+        single_device_only(h);
+        MML_REQUIRE(out_ms, "out is null");
+        MML_REQUIRE(h->has_data && h->has_model, "set_data and set_model must precede the replay");
+        MML_REQUIRE(h->p.model <= MML_MF_PLAIN && !is_asym(h) &&
+                        (h->p.schedule == MML_SCHEDULE_HOGWILD ||
+                         h->p.schedule == MML_SCHEDULE_HOGWILD_COHERENT),
+                    "the traffic replay covers the BiasedMF / MF Hogwild epoch");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        BmfScalars sc{};
+        const std::string label = h->last_kernel;
+        MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
+        if (h->n > 0) launch_hogwild<kReplayTraffic>(h, sc, nullptr, nullptr);
+        MML_HIP(hipEventRecord(h->ctx->ev_end, st));
+        MML_HIP(hipEventSynchronize(h->ctx->ev_end));
+        MML_HIP(hipEventElapsedTime(out_ms, h->ctx->ev_begin, h->ctx->ev_end));
+        h->last_kernel = label;
     });
 }
 

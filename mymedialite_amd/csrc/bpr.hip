@@ -450,6 +450,8 @@ constexpr int kBprJThru = 2;  // V_j / b_j stored sc1: write-through, dropped fr
 constexpr int kBprIThru = 4;  // V_i / b_i stored sc1 as well: every item row lives memory-side
 constexpr int kBprUThru = 16;  // U_u loaded sc1 and stored sc1 (write-through): no stale user
                                // rows in any XCD's L2 (U < 4 GiB only: buffer addressing)
+constexpr int kBprReplay = 32;  // (mml_bpr_replay_traffic) the same loads, every value stored
+                                // back unchanged with the same flags: the traffic, no arithmetic
 constexpr int kBprFlush = 8;  // one wave per XCD writes its L2's dirty lines back after every 64
                               // triples it applies (agent release fence = buffer_wbl2): the owner's
                               // hot rows reach memory, where the other XCDs read them as j, within
@@ -510,6 +512,45 @@ __global__ __launch_bounds__(256) void bpr_update_kernel(
                 hj = mml::load4_l2(vrs, (uint32_t)oj * 16u);
                 bi = mml::load1_l2(brs, (uint32_t)i * 4u);
                 bj = mml::load1_l2(brs, (uint32_t)j * 4u);
+            }
+            if constexpr ((AM & kBprReplay) != 0) {
+                asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z), "+v"(w.w));
+                asm volatile("" : "+v"(hi.x), "+v"(hi.y), "+v"(hi.z), "+v"(hi.w));
+                asm volatile("" : "+v"(hj.x), "+v"(hj.y), "+v"(hj.z), "+v"(hj.w));
+                asm volatile("" : "+v"(bi), "+v"(bj));
+                using u4 = __attribute__((ext_vector_type(4))) uint32_t;
+                if (q == 0) {
+                    if constexpr ((AM & kBprIThru) != 0)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bi), brs,
+                                                              (uint32_t)i * 4u, 0, 16);
+                    else
+                        bias[i] = bi;
+                    if (s.update_j) {
+                        if constexpr ((AM & kBprJThru) != 0)
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bj),
+                                                                  brs, (uint32_t)j * 4u, 0, 16);
+                        else
+                            bias[j] = bj;
+                    }
+                }
+                if constexpr ((AM & kBprUThru) != 0)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, w), urs,
+                                                           (uint32_t)ou * 16u, 0, 16);
+                else
+                    U4[ou] = w;
+                if constexpr ((AM & kBprIThru) != 0)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, hi), vrs,
+                                                           (uint32_t)oi * 16u, 0, 16);
+                else
+                    V4[oi] = hi;
+                if (s.update_j) {
+                    if constexpr ((AM & kBprJThru) != 0)
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, hj), vrs,
+                                                               (uint32_t)oj * 16u, 0, 16);
+                    else
+                        V4[oj] = hj;
+                }
+                continue;
             }
             double part = (double)(w.x * (hi.x - hj.x));
             part += (double)(w.y * (hi.y - hj.y));
@@ -704,6 +745,18 @@ struct mml_bpr {
     // a repeated-device context: the item average by peer copies (mml::peer_average)
     mml::DeviceArray<float> avg_stage;
     hipEvent_t ev_ar0 = nullptr, ev_ar1 = nullptr;
+    bool has_ar = false;  // ev_ar0 / ev_ar1 bracket the last item average
+    // the last Hogwild update launch, for mml_bpr_replay_traffic (its triples stay in tri_* / xt_*
+    // until the next epoch)
+    struct {
+        bool valid = false, soft = false;
+        int am = 0, wpb = 4;
+        int32_t ng = 1;
+        const int64_t* goff = nullptr;
+        const int32_t *tu = nullptr, *ti = nullptr, *tj = nullptr;
+        int64_t blocks = 0;
+        BprScalars s{};
+    } last_launch;
     int64_t n_events = 0, nnz = 0;
     int64_t hog_waves = 0;  // mml_bpr_set_hogwild_waves (0: by the epoch size)
     int32_t n_eligible = 0;
@@ -837,6 +890,10 @@ extern "C" mml_status mml_bpr_destroy(mml_bpr* h) {
         }
         (void)hipSetDevice(h->ctx->device);
         (void)hipStreamSynchronize(h->ctx->stream);
+        if (h->ev_ar0) {
+            (void)hipEventDestroy(h->ev_ar0);
+            (void)hipEventDestroy(h->ev_ar1);
+        }
         delete h;
     });
 }
@@ -1303,6 +1360,31 @@ void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff,
 #undef MML_UPD
 }
 
+// the release access modes with the replay bit (mml_bpr_replay_traffic)
+template <int LPR>
+void launch_replay_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff, const int32_t* tu,
+                       const int32_t* ti, const int32_t* tj, int64_t blocks, int wpb,
+                       const BprScalars& s, hipStream_t st) {
+    const int32_t wpg = (int32_t)(blocks / ng * wpb);
+    const uint32_t vb = (uint32_t)std::min<uint64_t>((uint64_t)h->n_items * h->ld * 4, 0xFFFFFFFFull);
+    const uint32_t bb = (uint32_t)((uint64_t)h->n_items * 4);
+    const uint64_t u_all = (uint64_t)h->n_users * h->ld * 4;
+    const uint32_t ub = (uint32_t)std::min<uint64_t>(u_all, 0xFFFFFFFFull);
+#define MML_REP(AM)                                                                           \
+    bpr_update_kernel<LPR, false, (AM) | kBprReplay><<<(int)blocks, 64 * wpb, 0, st>>>(       \
+        tu, ti, tj, goff, ng, wpg, h->U.get(), h->V.get(), h->bias.get(), h->ld / 4, vb, bb, ub, \
+        mml::flushers_per_xcd(4), s)
+    switch (am) {
+        case kBprLdL2 | kBprJThru | kBprFlush: MML_REP(kBprLdL2 | kBprJThru | kBprFlush); break;
+        case kBprLdL2 | kBprJThru | kBprFlush | kBprUThru:
+            MML_REP(kBprLdL2 | kBprJThru | kBprFlush | kBprUThru);
+            break;
+        case 0: MML_REP(0); break;
+        default: mml::fail(MML_ERR_STATE, "the traffic replay covers the release access modes");
+    }
+#undef MML_REP
+}
+
 void launch_update(mml_bpr* h, bool soft, int am, int32_t ng, const int64_t* goff,
                    const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t blocks,
                    int wpb, const BprScalars& s,
@@ -1366,6 +1448,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
                 mml::peer_average(ctxs, arr, {(int64_t)h->n_items * s0->ld, (int64_t)h->n_items},
                                   h->avg_stage, h->ev_ar0, h->ev_ar1);
                 MML_HIP(hipEventSynchronize(h->ev_ar1));
+                h->has_ar = true;
             } else {
                 mml::on_devices(h->ctx, epoch);
                 mml::on_devices(h->ctx,
@@ -1557,6 +1640,9 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             launch_apply_ordered(h, tu, ti, tj, n, s, st, 4, weighted_streams(h) / 4);
         } else if (!ordered && !fused && n > 0) {
             launch_update(h, soft, am, ng, goff, tu, ti, tj, blocks, 4, s, st);
+            int am_run = am;  // launch_update_lpr drops the user write-through past 4 GiB of U
+            if ((uint64_t)h->n_users * h->ld * 4 >= (1ull << 32)) am_run &= ~kBprUThru;
+            h->last_launch = {true, soft, am_run, 4, ng, goff, tu, ti, tj, blocks, s};
         } else if (fused) {
 #define MML_BPR(LPR)                                                                            \
     if (pair)                                                                                   \
@@ -1792,11 +1878,69 @@ extern "C" mml_status mml_bpr_allreduce_items(mml_bpr* h) {
         // model averaging inside the collective (ncclAvg), stream-ordered: the next epoch's
         // kernels and every download run on this stream after it
         const size_t nv = (size_t)h->n_items * h->ld;
+        if (!h->ev_ar0) {
+            MML_HIP(hipEventCreate(&h->ev_ar0));
+            MML_HIP(hipEventCreate(&h->ev_ar1));
+        }
+        MML_HIP(hipEventRecord(h->ev_ar0, st));
         MML_RCCL(ncclGroupStart());
         MML_RCCL(ncclAllReduce(h->V.get(), h->V.get(), nv, ncclFloat, ncclAvg, c->comm, st));
         MML_RCCL(ncclAllReduce(h->bias.get(), h->bias.get(), (size_t)h->n_items, ncclFloat,
                                ncclAvg, c->comm, st));
         MML_RCCL(ncclGroupEnd());
+        MML_HIP(hipEventRecord(h->ev_ar1, st));
+        h->has_ar = true;
+    });
+}
+
+extern "C" mml_status mml_bpr_replay_traffic(mml_bpr* h, float* out_ms) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx && out_ms, "null argument");
+        bpr_single_device_only(h);
+        const auto& L = h->last_launch;
+        MML_REQUIRE(L.valid && !L.soft && h->has_triples,
+                    "the traffic replay repeats the last BPRMF Hogwild update launch: run a "
+                    "HOGWILD epoch first");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
+        switch (h->lpr) {
+            case 1: launch_replay_lpr<1>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
+            case 2: launch_replay_lpr<2>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
+            case 4: launch_replay_lpr<4>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
+            case 8: launch_replay_lpr<8>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
+            case 16: launch_replay_lpr<16>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
+            case 32: launch_replay_lpr<32>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
+            default: launch_replay_lpr<64>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
+        }
+        MML_HIP(hipGetLastError());
+        MML_HIP(hipEventRecord(h->ctx->ev_end, st));
+        MML_HIP(hipEventSynchronize(h->ctx->ev_end));
+        MML_HIP(hipEventElapsedTime(out_ms, h->ctx->ev_begin, h->ctx->ev_end));
+    });
+}
+
+extern "C" mml_status mml_bpr_last_allreduce_ms(mml_bpr* h, float* out) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx && out, "null argument");
+        *out = 0.0f;
+        auto one = [](mml_bpr* x, mml_ctx* c) {
+            if (!x->has_ar) return 0.0f;
+            c->activate();
+            float ms = 0.0f;
+            MML_HIP(hipEventSynchronize(x->ev_ar1));
+            MML_HIP(hipEventElapsedTime(&ms, x->ev_ar0, x->ev_ar1));
+            return ms;
+        };
+        if (h->ctx->multi()) {
+            if (h->has_ar) {  // the peer average, on shard 0's device
+                *out = one(h, h->shards[0]->ctx);
+                return;
+            }
+            for (mml_bpr* s : h->shards) *out = std::max(*out, one(s, s->ctx));
+            return;
+        }
+        *out = one(h, h->ctx);
     });
 }
 

@@ -535,6 +535,8 @@ struct mml_wrmf {
     mml::DeviceArray<double> HH, partial;
     bool has_data = false, has_model = false;
     float last_ms = 0.0f;
+    float last_gather_ms = 0.0f;             // the last iterate's two all-gathers (device time)
+    hipEvent_t ev_g[4] = {nullptr, nullptr, nullptr, nullptr};
     int32_t last_launches = 0;
     int32_t last_refine = 0;  // the most refinement passes a half-step of the last iterate ran
     float last_corr[8] = {};  // per half-step (users, items) and pass: the max relative correction
@@ -758,6 +760,8 @@ extern "C" mml_status mml_wrmf_destroy(mml_wrmf* h) {
         }
         (void)hipSetDevice(h->ctx->device);
         (void)hipStreamSynchronize(h->ctx->stream);
+        for (hipEvent_t e : h->ev_g)
+            if (e) (void)hipEventDestroy(e);
         delete h;
     });
 }
@@ -938,15 +942,33 @@ extern "C" mml_status mml_wrmf_iterate(mml_wrmf* h) {
         const int rk = h->shard_rank;
         // WRMF.Iterate (:68-73): users from items, then items from the updated users; with
         // several ranks each solves its row shard and the shards are all-gathered in between
+        const bool gather = h->shard_nranks > 1;
+        if (gather && !h->ev_g[0])
+            for (hipEvent_t& e : h->ev_g) MML_HIP(hipEventCreate(&e));
         half_step(h, h->U.get(), h->ub[rk], h->ub[rk + 1], h->V.get(), h->n_items, h->uoff.get(),
                   h->ucols.get(), h->n_users, launches);
-        if (h->shard_nranks > 1) allgather_rows(h, h->U.get(), h->ub);
+        if (gather) {
+            MML_HIP(hipEventRecord(h->ev_g[0], st));
+            allgather_rows(h, h->U.get(), h->ub);
+            MML_HIP(hipEventRecord(h->ev_g[1], st));
+        }
         half_step(h, h->V.get(), h->ib[rk], h->ib[rk + 1], h->U.get(), h->n_users, h->ioff.get(),
                   h->icols.get(), h->n_items, launches);
-        if (h->shard_nranks > 1) allgather_rows(h, h->V.get(), h->ib);
+        if (gather) {
+            MML_HIP(hipEventRecord(h->ev_g[2], st));
+            allgather_rows(h, h->V.get(), h->ib);
+            MML_HIP(hipEventRecord(h->ev_g[3], st));
+        }
         MML_HIP(hipEventRecord(h->ctx->ev_end, st));
         MML_HIP(hipEventSynchronize(h->ctx->ev_end));
         MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));
+        h->last_gather_ms = 0.0f;
+        if (gather) {
+            float a = 0.0f, b = 0.0f;
+            MML_HIP(hipEventElapsedTime(&a, h->ev_g[0], h->ev_g[1]));
+            MML_HIP(hipEventElapsedTime(&b, h->ev_g[2], h->ev_g[3]));
+            h->last_gather_ms = a + b;
+        }
         h->last_launches = launches;
     });
 }
@@ -1025,6 +1047,14 @@ extern "C" mml_status mml_wrmf_retrain(mml_wrmf* h, int32_t side, int32_t n_rows
                                    256, 0, st>>>(wsub.get(), drows.get(), n_rows, h->k, W);
         MML_HIP(hipGetLastError());
         MML_HIP(hipStreamSynchronize(st));
+    });
+}
+
+extern "C" mml_status mml_wrmf_last_allgather_ms(mml_wrmf* h, float* out) {
+    return guard([&] {
+        MML_REQUIRE(h && out, "null argument");
+        *out = h->last_gather_ms;
+        for (mml_wrmf* s : h->shards) *out = std::max(*out, s->last_gather_ms);
     });
 }
 
