@@ -281,6 +281,15 @@ mml_status mml_bmf_objective(mml_bmf* h, double* out);
  * (the model is not modified).  *out_ms = its device time: the access pattern's ceiling on the GPU
  * it runs on, which bench.py reports beside the epoch (frac_of_box_ceiling). */
 mml_status mml_bmf_replay_traffic(mml_bmf* h, float* out_ms);
+/* User phases of the HOGWILD epoch (ABI 10).  The XCD-partitioned stream is split into P phases by
+ * a fixed hash of the user (the visit order kept within a phase) and the epoch runs one launch per
+ * phase, so a launch touches 1/P of U and its rows stay in the 256 MB Infinity Cache between a
+ * user's ratings.  phases = 0 (default): one phase per 96 MiB of the active users' rows, at most
+ * 32 (C4: 26; C2: 3; sets under 96 MiB of U: 1); 1 = one launch over the whole stream.  Every
+ * rating is still visited once per epoch.  mml_bmf_last_phases reports the count the last epoch
+ * used. */
+mml_status mml_bmf_set_hogwild_phases(mml_bmf* h, int32_t phases);
+mml_status mml_bmf_last_phases(mml_bmf* h, int32_t* out);
 /* Multi-GPU (user shards): in-place RCCL all-reduce of item factors and item
  * biases over the context's communicator with ncclAvg (model averaging).  Stream-ordered (ABI 6):
  * the call returns once the collective is enqueued; the next call on the handle runs after it. */

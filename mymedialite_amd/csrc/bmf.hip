@@ -27,7 +27,8 @@
 //            per rating (float4 each), 64/LPR ratings per wave step, dot product by xor-shuffle
 //            reduction, plain (racy) stores of the updated rows -- Hogwild! semantics.
 //   HOGWILD_COHERENT  the same with sc1 (agent-coherent) row and bias accesses, see load4 below.
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // rocprim/iterator/texture_cache_iterator.hpp uses memset on the host
+#include <rocprim/rocprim.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -1448,6 +1449,8 @@ struct mml_bmf {
     // user phases of the XCD stream (hogwild_phases): phase-major, XCD-group-minor spans, so that
     // one launch per phase touches 1/P of U; poff = the P * 8 + 1 span offsets (device)
     int32_t n_phases = 1;
+    int32_t phases_req = 0;       // mml_bmf_set_hogwild_phases (0: by the active users' bytes)
+    int64_t active_users = -1;    // users with a rating in this handle (ensure_xstream)
     mml::DeviceArray<int64_t> poff;
     // multi-device context: one single-device handle per GPU over a user range ub[d] .. ub[d + 1]
     // (U, b_u trained there; V, b_i replicated and averaged after every epoch)
@@ -1578,15 +1581,16 @@ void build_positions(mml_bmf* h, const int32_t* keys, const int32_t* cnt, int32_
     int end_bit = 1;
     while (end_bit < 31 && (1 << end_bit) < n_keys) ++end_bit;
     size_t b1 = 0, b2 = 0;
-    MML_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, keys, ksorted.get(), iota.get(),
+    MML_HIP(rocprim::radix_sort_pairs(nullptr, b1, keys, ksorted.get(), iota.get(),
                                                pos.get(), (int)n, 0, end_bit, st));
-    MML_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, b2, wide.get(), off.get() + 1, n_keys, st));
+    MML_HIP(rocprim::inclusive_scan(nullptr, b2, wide.get(), off.get() + 1, n_keys,
+            rocprim::plus<int64_t>(), st));
     mml::DeviceArray<uint8_t> tmp;
     tmp.alloc(std::max(b1, b2));
-    MML_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.get(), b1, keys, ksorted.get(), iota.get(),
+    MML_HIP(rocprim::radix_sort_pairs(tmp.get(), b1, keys, ksorted.get(), iota.get(),
                                                pos.get(), (int)n, 0, end_bit, st));
-    MML_HIP(hipcub::DeviceScan::InclusiveSum(tmp.get(), b2, wide.get(), off.get() + 1, n_keys,
-                                             st));
+    MML_HIP(rocprim::inclusive_scan(tmp.get(), b2, wide.get(), off.get() + 1, n_keys,
+            rocprim::plus<int64_t>(), st));
     MML_HIP(hipStreamSynchronize(st));
 }
 
@@ -1673,6 +1677,12 @@ void ensure_xstream(mml_bmf* h) {
         MML_HIP(hipMemcpyAsync(ci.data(), h->cnt_i.get(), sizeof(int32_t) * h->n_items,
                                hipMemcpyDeviceToHost, st));
     MML_HIP(hipStreamSynchronize(st));
+    std::vector<int32_t> cu(h->n_users);
+    if (h->n_users > 0)
+        MML_HIP(hipMemcpyAsync(cu.data(), h->cnt_u.get(), sizeof(int32_t) * h->n_users,
+                               hipMemcpyDeviceToHost, st));
+    MML_HIP(hipStreamSynchronize(st));
+    h->active_users = std::count_if(cu.begin(), cu.end(), [](int32_t c) { return c > 0; });
     h->xs.set_groups(st, std::vector<int64_t>(ci.begin(), ci.end()), 8);
     h->xu.alloc(h->n);
     h->xi.alloc(h->n);
@@ -1751,10 +1761,18 @@ static int32_t hogwild_phases_env() {
     }();
     return m;
 }
+// Default: one phase per 96 MiB of the active users' rows, at most 32.  Measured on one MI355X
+// (profiles/r5c_*): C4 (10 M users, 2.56 GB of U) 218.7 ms per epoch in one phase, 196.3 in 8,
+// 180.3 in 16, 178.8 in 32 (replay ceilings 215.6 / 186.7 / 175.7 / 174.7 ms); C2 (256 MB of U)
+// 22.3 ms in one phase, 20.0 in 2, 20.1 in 4; the test RMSE after 8 (C4) and 12 (C2) epochs
+// unchanged within the run-to-run spread (C4 0.63100 / 0.63092 / 0.63113 / 0.63103).
 int32_t hogwild_phases(const mml_bmf* h) {
     const int32_t e = hogwild_phases_env();
     if (e >= 0) return std::max(1, e);
-    return 1;
+    if (h->phases_req > 0) return h->phases_req;
+    const uint64_t bytes = (uint64_t)std::max<int64_t>(0, h->active_users) * h->ld * sizeof(float);
+    const uint64_t per = 96ull << 20;
+    return (int32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, (bytes + per - 1) / per));
 }
 
 // the XCD stream reordered phase-major (built once per data set and phase count)
@@ -1781,11 +1799,11 @@ void ensure_phases(mml_bmf* h, int32_t P) {
                                                    idx.get());
     MML_HIP(hipGetLastError());
     size_t tmp_bytes = 0;
-    MML_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, key.get(), key_s.get(),
+    MML_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, key.get(), key_s.get(),
                                                idx.get(), idx_s.get(), n, 0, end_bit, st));
     mml::DeviceArray<uint8_t> tmp;
     tmp.alloc(std::max<size_t>(1, tmp_bytes));
-    MML_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.get(), tmp_bytes, key.get(), key_s.get(),
+    MML_HIP(rocprim::radix_sort_pairs(tmp.get(), tmp_bytes, key.get(), key_s.get(),
                                                idx.get(), idx_s.get(), n, 0, end_bit, st));
     mml::DeviceArray<int32_t> ou, oi, orr;
     ou.alloc(n);
@@ -3221,6 +3239,23 @@ extern "C" mml_status mml_bmf_last_kernel(mml_bmf* h, char* buf, int32_t cap) {
         const size_t n = std::min<size_t>(k.size(), (size_t)cap - 1);
         std::copy(k.begin(), k.begin() + n, buf);
         buf[n] = 0;
+    });
+}
+
+extern "C" mml_status mml_bmf_set_hogwild_phases(mml_bmf* h, int32_t phases) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(phases >= 0 && phases <= 32, "phases must be in [0, 32]");
+        h->phases_req = phases;
+        for (mml_bmf* s : h->shards) s->phases_req = phases;
+    });
+}
+
+extern "C" mml_status mml_bmf_last_phases(mml_bmf* h, int32_t* out) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(out, "out is null");
+        *out = h->shards.empty() ? h->n_phases : h->shards[0]->n_phases;
     });
 }
 

@@ -33,7 +33,8 @@
 // Update (Hogwild!, LPR lanes per triple, one float4 per lane of U_u, V_i, V_j): the reference's
 // float/double arithmetic -- x_uij = (b_i - b_j) + sum_f (double)(w_f * (h_if - h_jf)), double
 // sigmoid, double deltas, float stores -- with the f-sum as per-lane partials + xor butterfly.
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // rocprim/iterator/texture_cache_iterator.hpp uses memset on the host
+#include <rocprim/rocprim.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -1548,7 +1549,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             int ub = 0;
             while (ub < 32 && ((uint32_t)(h->n_users - 1) >> ub) != 0) ++ub;
             rank_end_bit = 32 + std::max(ub, 1);
-            MML_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, rank_tmp_bytes, h->rank_keys.get(),
+            MML_HIP(rocprim::radix_sort_keys(nullptr, rank_tmp_bytes, h->rank_keys.get(),
                                                       h->rank_sorted.get(), n, 32, rank_end_bit,
                                                       st));
             if (h->rank_tmp.count < rank_tmp_bytes) h->rank_tmp.alloc(rank_tmp_bytes);
@@ -1583,7 +1584,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
 #undef MML_SMP
             MML_HIP(hipGetLastError());
             if (user_repl) {
-                MML_HIP(hipcub::DeviceRadixSort::SortKeys(h->rank_tmp.get(), rank_tmp_bytes,
+                MML_HIP(rocprim::radix_sort_keys(h->rank_tmp.get(), rank_tmp_bytes,
                                                           h->rank_keys.get(), h->rank_sorted.get(),
                                                           n, 32, rank_end_bit, st));
                 bpr_user_heads_kernel<<<sgrid, 256, 0, st>>>(h->rank_sorted.get(), n,

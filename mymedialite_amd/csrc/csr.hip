@@ -4,7 +4,8 @@
 // HashSet rows; on the device they are CSR rows, sorted and de-duplicated:
 //   key = row << 32 | col  ->  radix sort (hipCUB)  ->  unique  ->  per-row counts  ->  scan.
 // 500M events (C3) take a few hundred ms instead of a host sort of minutes.
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // rocprim/iterator/texture_cache_iterator.hpp uses memset on the host
+#include <rocprim/rocprim.hpp>
 
 #include <vector>
 
@@ -92,17 +93,17 @@ void build_csr_device(const int32_t* rows, const int32_t* cols, int64_t n, int32
     MML_REQUIRE(!bad, "event user/item id out of range");
     const int end_bit = 32 + bits_for((uint32_t)(n_rows - 1));
     size_t tmp_bytes = 0;
-    MML_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys.get(), sorted.get(), n, 0,
+    MML_HIP(rocprim::radix_sort_keys(nullptr, tmp_bytes, keys.get(), sorted.get(), n, 0,
                                               end_bit, st));
     size_t tmp2 = 0;
-    MML_HIP(hipcub::DeviceSelect::Unique(nullptr, tmp2, sorted.get(), keys.get(), nsel.get(), n,
-                                         st));
+    MML_HIP(rocprim::unique(nullptr, tmp2, sorted.get(), keys.get(), nsel.get(), n,
+            rocprim::equal_to<uint64_t>(), st));
     DeviceArray<uint8_t> tmp;
     tmp.alloc(std::max(tmp_bytes, tmp2));
-    MML_HIP(hipcub::DeviceRadixSort::SortKeys(tmp.get(), tmp_bytes, keys.get(), sorted.get(), n, 0,
+    MML_HIP(rocprim::radix_sort_keys(tmp.get(), tmp_bytes, keys.get(), sorted.get(), n, 0,
                                               end_bit, st));
-    MML_HIP(hipcub::DeviceSelect::Unique(tmp.get(), tmp2, sorted.get(), keys.get(), nsel.get(), n,
-                                         st));
+    MML_HIP(rocprim::unique(tmp.get(), tmp2, sorted.get(), keys.get(), nsel.get(), n,
+            rocprim::equal_to<uint64_t>(), st));
     int64_t nnz = 0;
     MML_HIP(hipMemcpyAsync(&nnz, nsel.get(), sizeof(int64_t), hipMemcpyDeviceToHost, st));
     MML_HIP(hipStreamSynchronize(st));
@@ -120,11 +121,11 @@ void build_csr_device(const int32_t* rows, const int32_t* cols, int64_t n, int32
     MML_HIP(hipGetLastError());
     MML_HIP(hipMemsetAsync(out.off.get(), 0, sizeof(int64_t), st));
     size_t tmp3 = 0;
-    MML_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tmp3, deg64.get(), out.off.get() + 1,
-                                             n_rows, st));
+    MML_HIP(rocprim::inclusive_scan(nullptr, tmp3, deg64.get(), out.off.get() + 1, n_rows,
+            rocprim::plus<int64_t>(), st));
     tmp.alloc(std::max(tmp.count, tmp3));
-    MML_HIP(hipcub::DeviceScan::InclusiveSum(tmp.get(), tmp3, deg64.get(), out.off.get() + 1,
-                                             n_rows, st));
+    MML_HIP(rocprim::inclusive_scan(tmp.get(), tmp3, deg64.get(), out.off.get() + 1, n_rows,
+            rocprim::plus<int64_t>(), st));
     MML_HIP(hipMemcpyAsync(out.deg_host.data(), deg.get(), sizeof(int32_t) * n_rows,
                            hipMemcpyDeviceToHost, st));
     MML_HIP(hipStreamSynchronize(st));

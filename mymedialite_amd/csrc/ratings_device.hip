@@ -17,7 +17,8 @@
 // other rating spellings, any malformed line -- for the reference's exact error text) runs the host
 // reader and uploads its arrays: the result is the same either way, and device_parsed says which
 // path ran.
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // rocprim/iterator/texture_cache_iterator.hpp uses memset on the host
+#include <rocprim/rocprim.hpp>
 
 #include <algorithm>
 #include <cstdint>
@@ -337,20 +338,22 @@ void map_keys_device(hipStream_t st, const int64_t* keys, int64_t N, const std::
     rs.alloc(N);
     // canonical keys are < 10^18 < 2^60
     size_t tmp_b = 0;
-    MML_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_b, keys, ks.get(), rows.get(), rs.get(),
+    MML_HIP(rocprim::radix_sort_pairs(nullptr, tmp_b, keys, ks.get(), rows.get(), rs.get(),
                                                N, 0, 60, st));
     mml::DeviceArray<uint8_t> tmp;
     tmp.alloc(tmp_b);
-    MML_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.get(), tmp_b, keys, ks.get(), rows.get(), rs.get(),
+    MML_HIP(rocprim::radix_sort_pairs(tmp.get(), tmp_b, keys, ks.get(), rows.get(), rs.get(),
                                                N, 0, 60, st));
     rows.reset();
     flag.alloc(N);
     dix.alloc(N);
     rf_heads_kernel<<<grid_of(N), 256, 0, st>>>(ks.get(), N, flag.get());
     size_t scan_b = 0;
-    MML_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_b, flag.get(), dix.get(), N, st));
+    MML_HIP(rocprim::inclusive_scan(nullptr, scan_b, flag.get(), dix.get(), N,
+            rocprim::plus<int32_t>(), st));
     tmp.reserve(scan_b);
-    MML_HIP(hipcub::DeviceScan::InclusiveSum(tmp.get(), scan_b, flag.get(), dix.get(), N, st));
+    MML_HIP(rocprim::inclusive_scan(tmp.get(), scan_b, flag.get(), dix.get(), N,
+            rocprim::plus<int32_t>(), st));
     int32_t D = 0;
     MML_HIP(hipMemcpyAsync(&D, dix.get() + N - 1, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     MML_HIP(hipStreamSynchronize(st));
@@ -369,10 +372,10 @@ void map_keys_device(hipStream_t st, const int64_t* keys, int64_t N, const std::
     dfirst_s.alloc(D);
     order_s.alloc(D);
     size_t sort2_b = 0;
-    MML_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort2_b, dfirst.get(), dfirst_s.get(),
+    MML_HIP(rocprim::radix_sort_pairs(nullptr, sort2_b, dfirst.get(), dfirst_s.get(),
                                                order.get(), order_s.get(), D, 0, 32, st));
     tmp.reserve(sort2_b);
-    MML_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.get(), sort2_b, dfirst.get(), dfirst_s.get(),
+    MML_HIP(rocprim::radix_sort_pairs(tmp.get(), sort2_b, dfirst.get(), dfirst_s.get(),
                                                order.get(), order_s.get(), D, 0, 32, st));
     std::vector<int32_t> first_s(D);
     MML_HIP(hipMemcpyAsync(first_s.data(), dfirst_s.get(), sizeof(int32_t) * D,
@@ -531,16 +534,20 @@ extern "C" mml_status mml_rating_file_read_device(mml_ctx* ctx, const char* path
         MML_HIP(hipGetLastError());
         MML_HIP(hipMemsetAsync(at.get(), 0, sizeof(int64_t), st));
         size_t tb = 0;
-        MML_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, rows.get(), at.get() + 1, nseg, st));
+        MML_HIP(rocprim::inclusive_scan(nullptr, tb, rows.get(), at.get() + 1, nseg,
+                rocprim::plus<int64_t>(), st));
         mml::DeviceArray<uint8_t> tmp;
         tmp.alloc(tb);
-        MML_HIP(hipcub::DeviceScan::InclusiveSum(tmp.get(), tb, rows.get(), at.get() + 1, nseg, st));
+        MML_HIP(rocprim::inclusive_scan(tmp.get(), tb, rows.get(), at.get() + 1, nseg,
+                rocprim::plus<int64_t>(), st));
         mml::DeviceArray<int64_t> nl_sum;
         nl_sum.alloc(1);
         size_t rb = 0;
-        MML_HIP(hipcub::DeviceReduce::Sum(nullptr, rb, lines.get(), nl_sum.get(), nseg, st));
+        MML_HIP(rocprim::reduce(nullptr, rb, lines.get(), nl_sum.get(), (int64_t)0, nseg,
+                rocprim::plus<int64_t>(), st));
         tmp.reserve(rb);
-        MML_HIP(hipcub::DeviceReduce::Sum(tmp.get(), rb, lines.get(), nl_sum.get(), nseg, st));
+        MML_HIP(rocprim::reduce(tmp.get(), rb, lines.get(), nl_sum.get(), (int64_t)0, nseg,
+                rocprim::plus<int64_t>(), st));
         int64_t counts[2] = {0, 0};
         MML_HIP(hipMemcpyAsync(&counts[0], nl_sum.get(), sizeof(int64_t), hipMemcpyDeviceToHost, st));
         MML_HIP(hipMemcpyAsync(&counts[1], at.get() + nseg, sizeof(int64_t), hipMemcpyDeviceToHost,

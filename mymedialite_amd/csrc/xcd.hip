@@ -10,7 +10,8 @@
 // launch maps group g to blocks b with b % 8 == g -- blocks that share one XCD (dispatch deals
 // blocks round-robin over the XCDs; mml::xcd_groups probes that on the device before relying on
 // it).  Every access to an item row then comes from one XCD, whose single L2 holds the row.
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // rocprim/iterator/texture_cache_iterator.hpp uses memset on the host
+#include <rocprim/rocprim.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -259,13 +260,14 @@ void partition_impl(XcdSplit& xs, hipStream_t st, const int32_t* key, const uint
     xs.cnt.alloc((size_t)8 * nblk);
     xs.base.alloc((size_t)8 * nblk);
     size_t tb = 0;
-    MML_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, xs.cnt.get(), xs.base.get(), 8 * nblk, st));
+    MML_HIP(rocprim::exclusive_scan(nullptr, tb, xs.cnt.get(), xs.base.get(), (int64_t)0,
+                                    8 * nblk, rocprim::plus<int64_t>(), st));
     if (xs.tmp.count < tb) xs.tmp.alloc(tb);
     xcd_count_kernel<DIRECT><<<nblk, 256, 0, st>>>(key, gkey, n, seg, xs.group.get(), xs.cnt.get(),
                                                    nblk);
     MML_HIP(hipGetLastError());
-    MML_HIP(hipcub::DeviceScan::ExclusiveSum(xs.tmp.get(), tb, xs.cnt.get(), xs.base.get(),
-                                             8 * nblk, st));
+    MML_HIP(rocprim::exclusive_scan(xs.tmp.get(), tb, xs.cnt.get(), xs.base.get(), (int64_t)0,
+                                    8 * nblk, rocprim::plus<int64_t>(), st));
     Pay3 p{};
     for (int c = 0; c < npay; ++c) {
         p.in[c] = in[c];

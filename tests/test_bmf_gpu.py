@@ -117,11 +117,19 @@ def test_c1_standin_rmse_parity():
     print(f"C1 ordered: gpu RMSE {out['RMSE']:.6f} oracle {rmse_ref:.6f} (nu={nu})")
     assert abs(out["RMSE"] - rmse_ref) <= 1e-4
     assert abs(out["MAE"] - mae_ref) <= 1e-4
-    # hogwild: same data, statistical parity
+    # hogwild: same data, statistical parity -- the band of tests/test_edge_cases_gpu.py
+    # (hogwild_band): the sequential oracle's own order noise over three other RandomIndex
+    # shuffles, and the lockstep staleness model of the launch's 4 in-order streams
+    from test_edge_cases_gpu import hogwild_band, lockstep_delta, order_noise
     m2, _ = gpu_train(tu_, ti_, tv_, seed=1, k=10, num_iter=30, Schedule="hogwild")
     out2 = m2.evaluate(Ratings(eu, ei, ev))
     print(f"C1 hogwild: gpu RMSE {out2['RMSE']:.6f} oracle {rmse_ref:.6f}")
-    assert abs(out2["RMSE"] - rmse_ref) <= 1e-2
+    ev_set = (eu, ei, ev.astype(np.float64))
+    ref, d_rmse, d_pred = order_noise(tu_, ti_, tv_, seed=1, k=10, num_iter=30, eval_set=ev_set)
+    d_lock = lockstep_delta(tu_, ti_, tv_, seed=1, k=10, num_iter=30, eval_set=ev_set, ref=ref)
+    pred = m2.predict(eu, ei).astype(np.float64)
+    rmse2 = float(np.sqrt(np.mean((pred - ev) ** 2)))
+    assert hogwild_band("C1 hogwild", rmse2, pred, ref, d_rmse, d_pred, d_lock)
 
 
 @pytest.mark.parametrize("k", [1, 5, 16, 64, 100, 128, 256])

@@ -99,6 +99,8 @@ def hogwild_streams(n, k):
     lpr = 1
     while lpr < (k + 3) // 4:
         lpr *= 2
+    if waves < 16:  # a small epoch: ONE workgroup of 4 waves (one CU, one L2)
+        return 4, 64 // lpr
     return blocks * 4, 64 // lpr
 
 
@@ -195,9 +197,18 @@ def test_one_hot_user_and_ragged_chunks(schedule):
         assert _maxdiff(m.user_factors, st["U"]) <= 1e-5
         assert _maxdiff(m.item_factors, st["V"]) <= 1e-5
     else:
-        # degenerate on purpose: every wave updates the one user row at once (robustness: the
-        # run completes with finite factors and learns; the band is loose, the value printed)
-        assert abs(rmse - rmse_ref) <= 1e-1
+        # degenerate on purpose: every stream updates the one user row at once.  The offset is
+        # Hogwild's staleness on that row, restated by the lockstep model (every stream reads the
+        # row before the step and the last write wins): the RMSE lies between the sequential
+        # loop's and twice the model's offset, with 3x the order noise of slack (hogwild_band's
+        # RMSE bound; the per-prediction bound does not apply to one shared row)
+        ref_e, d_rmse, _ = order_noise(u, i, v, seed=3, k=16, num_iter=1, eval_set=(u, i, v))
+        d_lock = lockstep_delta(u, i, v, seed=3, k=16, num_iter=1, eval_set=(u, i, v),
+                                ref=ref_e)
+        dr = rmse - ref_e[0]
+        print(f"one hot user, hogwild: delta {dr:+.3e}, staleness model {d_lock:+.3e} (ratio "
+              f"{dr / d_lock if d_lock else float('nan'):.2f}), order noise {d_rmse:.2e}")
+        assert -3 * d_rmse <= dr <= 2 * max(d_lock, 0.0) + 3 * d_rmse
 
 
 def test_argument_errors_are_status_codes():

@@ -99,18 +99,16 @@ def test_bmf_multi_device_context_one_shard():
     assert m._ctx.nranks == 1
     # Both handles run Hogwild, so neither is bit-reproducible: the shard path is held to the
     # same statistical bar as the single-device one, against the sequential oracle on the same
-    # data, seed and properties (2e-2 after 3 epochs on 300 items: the steep part of the curve,
-    # where the updates in flight matter most; measured: oracle 1.4309, single 1.4393, multi
-    # 1.4320)
-    r = Ratings(u, i, v)
-    st = O.bmf_train(u, i, v, r.max_user_id + 1, r.max_item_id + 1, r.scale_min, r.scale_max,
-                     seed=4, k=16, num_iter=3)
-    p = O.bmf_predict(tu, ti, st["U"], st["V"], st["bu"], st["bi"], st["global_bias"],
-                      st["min_rating"], st["range_"])
-    ref = O.rating_eval(p, tv)[0]
-    print(f"BMF RMSE oracle {ref:.5f} single {res['single'][1]:.5f} multi(1 shard) {rmse:.5f}")
-    assert abs(res["single"][1] - ref) <= 2e-2
-    assert abs(rmse - ref) <= 2e-2
+    # data, seed and properties -- hogwild_band (tests/test_edge_cases_gpu.py): the oracle's own
+    # order noise over three other shuffles and the lockstep staleness model of the launch
+    from test_edge_cases_gpu import hogwild_band, lockstep_delta, order_noise
+    ev_set = (tu, ti, tv.astype(np.float64))
+    ref, d_rmse, d_pred = order_noise(u, i, v, seed=4, k=16, num_iter=3, eval_set=ev_set)
+    d_lock = lockstep_delta(u, i, v, seed=4, k=16, num_iter=3, eval_set=ev_set, ref=ref)
+    for name, (mm, rm) in res.items():
+        pred = mm.predict(tu, ti).astype(np.float64)
+        assert hogwild_band(f"BMF hogwild {name}", float(np.sqrt(np.mean((pred - tv) ** 2))),
+                            pred, ref, d_rmse, d_pred, d_lock)
     md = m.get_model()
     q = BiasedMatrixFactorization(NumFactors=16, NumIter=0, Schedule="hogwild")
     q.ratings = Ratings(u, i, v)
