@@ -86,6 +86,9 @@ def main():
                     help="default: c4 at every N (BiasedMF k=64, 1B ratings, strong scaling; at "
                          "N = 1 + the c2 / c3 / c5 keys); c2: 1M x 100k, 100M ratings, one GPU; "
                          "c3: BPRMF k=128 (N > 1: user shards); c5: WRMF k=256")
+    ap.add_argument("--phases", type=int, default=0,
+                    help="user phases of the Hogwild epochs (mml_bmf_set_hogwild_phases / "
+                         "mml_bpr_set_hogwild_phases): 0 = the library's default, 1 = none")
     ap.add_argument("--no-extras", action="store_true",
                     help="N = 1 default run: the C4 line only (no c2 / c3 / c5 keys)")
     args = ap.parse_args()
@@ -167,6 +170,7 @@ def bench_c2(args):
     h = N._vp()
     N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(params), n_users_total, n_items,
                                    ctypes.byref(h)))
+    N.check(N.lib().mml_bmf_set_hogwild_phases(h, args.phases))
     if ring:  # a multi-device context takes host arrays and deals them out in set_blocks
         hu_, hi_, hv_ = users.cpu().numpy(), items.cpu().numpy(), values.cpu().numpy()
         N.check(N.lib().mml_bmf_set_data(h, N.ptr(hu_, N._i32p), N.ptr(hi_, N._i32p),
@@ -455,6 +459,7 @@ def bench_c4(args):
     h = N._vp()
     N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(params), n_users, n_items,
                                    ctypes.byref(h)))
+    N.check(N.lib().mml_bmf_set_hogwild_phases(h, args.phases))
     t0 = time.perf_counter()
     N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
                                             values.data_ptr(), n_local, None))
@@ -508,6 +513,8 @@ def bench_c4(args):
     ar = np.zeros(1, np.float32)
     N.check(N.lib().mml_bmf_last_allreduce_ms(h, N.ptr(ar, N._f32p)))
     kernel = N.last_kernel("mml_bmf_last_kernel", h)
+    phases = ctypes.c_int32(0)
+    N.check(N.lib().mml_bmf_last_phases(h, ctypes.byref(phases)))
     ceiling = box_ceiling("mml_bmf_replay_traffic", h, float(np.mean(kernel_ms)),
                           n_local * bytes_per_update(k))
     rmse = evaluate()
@@ -543,7 +550,7 @@ def bench_c4(args):
                        "num_factors": k, "ratings_total": n_total, "ratings_per_gpu": n_local,
                        "users": n_users, "items": n_items, "schedule": "hogwild",
                        "parallelism": f"user-shard x{world}", "generate_s": gen_s,
-                       "device_ingest_s": ingest_s},
+                       "device_ingest_s": ingest_s, "user_phases": phases.value},
             "final_rmse": rmse,
             "initial_rmse": rmse0,
             "epochs_trained": args.warmup + args.steps,
@@ -598,6 +605,7 @@ def bench_bpr(args):
     h = N._vp()
     N.check(N.lib().mml_bpr_create(ctx.handle, ctypes.byref(p), n_users, n_items,
                                    ctypes.byref(h)))
+    N.check(N.lib().mml_bpr_set_hogwild_phases(h, args.phases))
     t0 = time.perf_counter()
     N.check(N.lib().mml_bpr_set_data_device(h, users.data_ptr(), items.data_ptr(), n, None))
     ingest_s = time.perf_counter() - t0
@@ -652,6 +660,8 @@ def bench_bpr(args):
     if k == 128 and n_total == 500_000_000 and args.sampler == "uniform_user" and world == 1:
         traffic, traffic_note = pmc_traffic("r4_c3_traffic.json", upd_ms, n * bpu)
     kernel = N.last_kernel("mml_bpr_last_kernel", h)
+    phases = ctypes.c_int32(0)
+    N.check(N.lib().mml_bpr_last_phases(h, ctypes.byref(phases)))
     # the last epoch's triples again, against that epoch's update kernel
     ceiling = box_ceiling("mml_bpr_replay_traffic", h, ums[-1], n * bpu)
     line = {
@@ -670,7 +680,8 @@ def bench_bpr(args):
                                               "uniform_user" else ""),
                    "parallelism": f"user-shard x{world}" + (
                        ", per-epoch RCCL all-reduce of V||b" if world > 1 else ""),
-                   "device_ingest_s": ingest_s},
+                   "device_ingest_s": ingest_s,
+                   "user_phases": phases.value},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_note": traffic_note,

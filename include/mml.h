@@ -471,6 +471,16 @@ mml_status mml_bpr_last_kernel(mml_bpr* h, char* buf, int32_t cap);
  * set's triples in flight -- the Hogwild staleness -- e.g. the C3-density AUC parity test.  No
  * effect on the ORDERED schedule or on epochs below 16 waves' worth of triples. */
 mml_status mml_bpr_set_hogwild_waves(mml_bpr* h, int64_t waves);
+/* User phases of the default sampler's HOGWILD epoch (ABI 10; the BiasedMF form is
+ * mml_bmf_set_hogwild_phases).  The eligible users are split into P phases by a fixed hash; the
+ * sampler draws the epoch's triples phase by phase -- each phase's share of the Feedback.Count
+ * triples in proportion to its users, u uniform within the phase, so every user keeps SampleUser's
+ * probability 1 / n_eligible per triple (BPRMF.cs:300-310) -- and each phase is partitioned by
+ * XCD group and updated by its own launch, which then touches 1/P of U.  phases = 0 (default):
+ * one phase per 96 MiB of the eligible users' rows, at most 64 (C3: 51); 1 = one draw over all
+ * users.  mml_bpr_last_phases: the count the last epoch used. */
+mml_status mml_bpr_set_hogwild_phases(mml_bpr* h, int32_t phases);
+mml_status mml_bpr_last_phases(mml_bpr* h, int32_t* out);
 /* The last epoch's sampled triples in sample order (n = Feedback.Count), e.g. for BPRMF's
  * loss_sample_* arrays (BPRMF.cs:136-150) or to check a sampler's distribution (ABI 3).  On a
  * multi-device context: each user shard's triples in its sample order, shard after shard (ABI 9;

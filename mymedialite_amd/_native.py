@@ -150,6 +150,8 @@ SIGNATURES = {
     "mml_bpr_last_allreduce_ms": (_st, [_vp, _f32p]),
     "mml_bmf_replay_traffic": (_st, [_vp, _f32p]),
     "mml_bmf_set_hogwild_phases": (_st, [_vp, ctypes.c_int32]),
+    "mml_bpr_set_hogwild_phases": (_st, [_vp, ctypes.c_int32]),
+    "mml_bpr_last_phases": (_st, [_vp, ctypes.POINTER(ctypes.c_int32)]),
     "mml_bmf_last_phases": (_st, [_vp, ctypes.POINTER(ctypes.c_int32)]),
     "mml_bpr_replay_traffic": (_st, [_vp, _f32p]),
     "mml_wrmf_last_allgather_ms": (_st, [_vp, _f32p]),

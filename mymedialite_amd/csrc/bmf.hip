@@ -1766,6 +1766,12 @@ static int32_t hogwild_phases_env() {
 // 180.3 in 16, 178.8 in 32 (replay ceilings 215.6 / 186.7 / 175.7 / 174.7 ms); C2 (256 MB of U)
 // 22.3 ms in one phase, 20.0 in 2, 20.1 in 4; the test RMSE after 8 (C4) and 12 (C2) epochs
 // unchanged within the run-to-run spread (C4 0.63100 / 0.63092 / 0.63113 / 0.63103).
+// A phase also gathers each user's ratings of an epoch into 1/P of it, so at the end of an epoch
+// the users of the early phases were last updated further back while the items kept moving: a
+// lag that is visible while the items still move a lot per epoch (800 k users x 16 M ratings,
+// RMSE after epochs 1-4 in 3 phases +0.3e-4 ... +1.9e-4 and in 8 phases +3.4e-4 ... +4.6e-4 over
+// one phase, run to run spread ~1e-4; tests/test_phases_gpu.py) and gone near convergence (C4
+// after 8 epochs: 0.63100 in one phase, 0.63092 / 0.63113 / 0.63103 in 16 / 8 / 32).
 int32_t hogwild_phases(const mml_bmf* h) {
     const int32_t e = hogwild_phases_env();
     if (e >= 0) return std::max(1, e);

@@ -314,14 +314,31 @@ constexpr int64_t kAutoOrderedBelow = 16 * 16384;
 // The default sampler's triple of sample smp (IterateWithoutReplacementUniformUser: SampleUser,
 // SampleItemPair, BPRMF.cs:290-310): u uniform over the eligible users, i uniform over S_u, j
 // uniform over the items outside S_u (Bloom filter, then the row)
+// User phases (bpr_phases): sample smp of phase p = the p with ptri[p] <= smp < ptri[p + 1] draws u
+// uniformly over the phase's eligible users ph_users[ph_uoff[p] .. ph_uoff[p + 1]), and every
+// phase holds triples in proportion to its users, so each user is still drawn with probability
+// 1 / n_eligible per triple (SampleUser, BPRMF.cs:300-310); the triples come out phase-major.
+struct BprPhases {
+    const int32_t* users = nullptr;  // eligible users ordered by phase (stable)
+    const int32_t* uoff = nullptr;   // [P + 1]
+    const int64_t* tri = nullptr;    // [P + 1]
+    int32_t n = 1;
+};
 __device__ __forceinline__ void draw_uniform_user(const int32_t* __restrict__ cols,
                                                   const int32_t* __restrict__ eligible,
                                                   int32_t n_eligible, int32_t n_items,
                                                   uint64_t seed, const uint32_t* __restrict__ recs,
                                                   int64_t smp, int32_t& u, int32_t& i,
-                                                  int32_t& j) {
-    const uint32_t du = draw(seed, smp, 0, (uint32_t)n_eligible);
-    u = eligible ? eligible[du] : (int32_t)du;
+                                                  int32_t& j, const BprPhases& ph, int& p) {
+    if (ph.n > 1) {
+        // p is carried over a thread's ascending samples: it only moves forward
+        while (p + 1 < ph.n && smp >= ph.tri[p + 1]) ++p;
+        const int32_t b = ph.uoff[p];
+        u = ph.users[b + (int32_t)draw(seed, smp, 0, (uint32_t)(ph.uoff[p + 1] - b))];
+    } else {
+        const uint32_t du = draw(seed, smp, 0, (uint32_t)n_eligible);
+        u = eligible ? eligible[du] : (int32_t)du;
+    }
     const uint32_t* rec = recs + (int64_t)u * kRecWords;
     const UserRec ur = user_rec(rec);
     i = cols[ur.rb + draw(seed, smp, 1, (uint32_t)(ur.re - ur.rb))];
@@ -339,12 +356,14 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
     int32_t* __restrict__ tu, int32_t* __restrict__ ti, int32_t* __restrict__ tj,
     int32_t* __restrict__ fail, uint64_t* __restrict__ user_keys,
     const uint32_t* __restrict__ recs, const uint8_t* __restrict__ gtab,
-    uint8_t* __restrict__ tg) {
+    uint8_t* __restrict__ tg, BprPhases ph) {
+    int ph_p = 0;
     for (int64_t smp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; smp < n_samples;
          smp += (int64_t)gridDim.x * blockDim.x) {
         int32_t u, i = 0, j = 0;
         if constexpr (SAMPLER == MML_BPR_SAMPLER_UNIFORM_USER) {
-            draw_uniform_user(cols, eligible, n_eligible, n_items, seed, recs, smp, u, i, j);
+            draw_uniform_user(cols, eligible, n_eligible, n_items, seed, recs, smp, u, i, j, ph,
+                              ph_p);
             tu[smp] = u;
             ti[smp] = i;
             tj[smp] = j;
@@ -757,9 +776,19 @@ struct mml_bpr {
         const int32_t *tu = nullptr, *ti = nullptr, *tj = nullptr;
         int64_t blocks = 0;
         BprScalars s{};
+        int32_t phases = 1;
+        const int64_t* poff = nullptr;  // phases > 1: 8 span offsets per phase
     } last_launch;
     int64_t n_events = 0, nnz = 0;
     int64_t hog_waves = 0;  // mml_bpr_set_hogwild_waves (0: by the epoch size)
+    // user phases of the default sampler's epoch (bpr_phases): the eligible users ordered by
+    // phase, per-phase user and triple offsets, the partitioned triples' span offsets
+    std::vector<int32_t> elig_host;
+    int32_t n_phases = 1, phases_req = 0, last_phases = 1;
+    int64_t phases_for_n = -1;
+    std::vector<int64_t> ptri_host;
+    mml::DeviceArray<int32_t> ph_users, ph_uoff;
+    mml::DeviceArray<int64_t> ph_tri, poff, ph_zero;  // ph_zero: 8 zero offsets
     int32_t n_eligible = 0;
     bool has_data = false, has_model = false, has_order = false, has_triples = false;
     float last_ms = 0.0f, last_update_ms = 0.0f;
@@ -934,9 +963,13 @@ void bpr_ingest(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t 
     MML_HIP(hipGetLastError());
     h->n_events = n;
     h->n_eligible = (int32_t)elig.size();
+    h->n_phases = 1;
+    h->phases_for_n = -1;
     h->eligible.alloc(elig.size());
     MML_HIP(hipMemcpyAsync(h->eligible.get(), elig.data(), sizeof(int32_t) * elig.size(),
                            hipMemcpyHostToDevice, st));
+    MML_HIP(hipStreamSynchronize(st));
+    h->elig_host.swap(elig);
     MML_REQUIRE(h->p.sampler != MML_BPR_SAMPLER_USER_REPLACEMENT || n <= (int64_t)UINT32_MAX,
                 "USER_REPLACEMENT ranks samples with 32-bit indices: at most 2^32 - 1 events");
     h->has_triples = false;
@@ -1331,6 +1364,80 @@ BprXcdMode bpr_xcd_mode(int sampler) {
     }
 }
 
+// the phase of a user (the BiasedMF epoch's hash, bmf.hip user_phase): a random 1/P of the users
+inline int32_t bpr_user_phase(int32_t u, int32_t P) {
+    uint64_t x = (uint64_t)(uint32_t)u ^ 0x6A09E667F3BCC909ull;
+    x += 0x9E3779B97F4A7C15ull;  // splitmix64's finaliser (mml_device.h mix64)
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return (int32_t)((x ^ (x >> 31)) % (uint64_t)P);
+}
+
+// User phases of the default sampler's Hogwild epoch.  Default: one phase per 96 MiB of the
+// eligible users' rows, at most 64 (C3: 10 M users x 512 B -> 51), so one update launch touches
+// a phase's U rows, which then stay in the 256 MB Infinity Cache between a user's triples.
+int32_t bpr_phases(const mml_bpr* h) {
+    static const int32_t env = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_BPR_PHASES");
+        return e ? std::max(0, std::min(64, std::atoi(e))) : -1;
+    }();
+    int32_t P;
+    if (env >= 0) P = std::max(1, env);
+    else if (h->phases_req > 0) P = h->phases_req;
+    else {
+        const uint64_t bytes = (uint64_t)h->n_eligible * h->ld * sizeof(float);
+        const uint64_t per = 96ull << 20;
+        P = (int32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, (bytes + per - 1) / per));
+    }
+    return std::max(1, std::min(P, h->n_eligible));
+}
+
+// the phase-ordered eligible users and the per-phase triple counts of an n-triple epoch
+void ensure_bpr_phases(mml_bpr* h, int32_t P, int64_t n) {
+    if (h->n_phases == P && h->phases_for_n == n) return;
+    hipStream_t st = h->ctx->stream;
+    h->n_phases = P;
+    h->phases_for_n = n;
+    if (P <= 1) return;
+    std::vector<int32_t> cnt(P + 1, 0);
+    std::vector<int32_t> ph(h->elig_host.size());
+    for (size_t x = 0; x < ph.size(); ++x) {
+        ph[x] = bpr_user_phase(h->elig_host[x], P);
+        ++cnt[ph[x] + 1];
+    }
+    for (int32_t p = 0; p < P; ++p) cnt[p + 1] += cnt[p];
+    std::vector<int32_t> users(ph.size()), at(cnt.begin(), cnt.end() - 1);
+    for (size_t x = 0; x < ph.size(); ++x) users[at[ph[x]]++] = h->elig_host[x];
+    // triples per phase in proportion to its users (cumulative rounding): each user is drawn with
+    // probability 1 / n_eligible per triple, as SampleUser draws it
+    std::vector<int64_t> tri(P + 1, 0);
+    for (int32_t p = 1; p <= P; ++p)
+        tri[p] = (int64_t)((long double)n * cnt[p] / (long double)h->n_eligible + 0.5L);
+    tri[P] = n;
+    h->ph_users.alloc(users.size());
+    h->ph_uoff.alloc(P + 1);
+    h->ph_tri.alloc(P + 1);
+    h->poff.alloc((size_t)8 * P + 1);
+    h->ph_zero.alloc(8);
+    MML_HIP(hipMemsetAsync(h->ph_zero.get(), 0, sizeof(int64_t) * 8, st));
+    MML_HIP(hipMemcpyAsync(h->ph_users.get(), users.data(), sizeof(int32_t) * users.size(),
+                           hipMemcpyHostToDevice, st));
+    MML_HIP(hipMemcpyAsync(h->ph_uoff.get(), cnt.data(), sizeof(int32_t) * (P + 1),
+                           hipMemcpyHostToDevice, st));
+    MML_HIP(hipMemcpyAsync(h->ph_tri.get(), tri.data(), sizeof(int64_t) * (P + 1),
+                           hipMemcpyHostToDevice, st));
+    MML_HIP(hipMemcpyAsync(h->poff.get() + (size_t)8 * P, &tri[P], sizeof(int64_t),
+                           hipMemcpyHostToDevice, st));
+    MML_HIP(hipStreamSynchronize(st));
+    h->ptri_host.swap(tri);
+}
+
+// a phase's partition offsets (relative to its first triple) into the epoch's span offsets
+__global__ void phase_span_kernel(const int64_t* __restrict__ goff, int64_t base,
+                                  int64_t* __restrict__ out) {
+    if (threadIdx.x < 8) out[threadIdx.x] = base + goff[threadIdx.x];
+}
+
 template <int LPR, bool SOFT>
 void launch_update_lpr(mml_bpr* h, int am, int32_t ng, const int64_t* goff,
                        const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t blocks,
@@ -1532,6 +1639,18 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         }();
         const bool part_g = part && !user_repl && group_bytes;
         if (part_g && (int64_t)h->tri_g.count < n) h->tri_g.alloc(n);
+        // user phases: the default sampler draws the epoch phase by phase, one update launch each
+        const int32_t P =
+            part_g && h->p.sampler == MML_BPR_SAMPLER_UNIFORM_USER ? bpr_phases(h) : 1;
+        ensure_bpr_phases(h, P, n);
+        BprPhases ph;
+        if (P > 1) {
+            ph.users = h->ph_users.get();
+            ph.uoff = h->ph_uoff.get();
+            ph.tri = h->ph_tri.get();
+            ph.n = P;
+        }
+        h->last_phases = P;
         if (part && (int64_t)h->xt_u.count < n) {
             h->xt_u.alloc(n);
             h->xt_i.alloc(n);
@@ -1566,7 +1685,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         h->off.get(), h->cols.get(), ELIG, h->n_eligible, h->ev_u.get(), h->ev_i.get(), n,    \
         h->n_items, seed, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), h->fail.get(),       \
         h->rank_keys.get(), h->recs.get(), part_g ? h->xs.group.get() : nullptr,             \
-        part_g ? h->tri_g.get() : nullptr)
+        part_g ? h->tri_g.get() : nullptr, ph)
             int32_t* elig = h->n_eligible == h->n_users ? nullptr : h->eligible.get();
             switch (h->p.sampler) {
                 case MML_BPR_SAMPLER_UNIFORM_PAIR:
@@ -1614,12 +1733,28 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         if (part) {  // stable partition of the sampled triples (XcdSplit)
             const int32_t* in[3] = {tu, ti, tj};
             int32_t* out[3] = {h->xt_u.get(), h->xt_i.get(), h->xt_j.get()};
-            if (part_g)
+            if (P > 1) {  // each phase partitioned on its own: spans phase-major, group-minor
+                for (int32_t p = 0; p < P; ++p) {
+                    const int64_t b = h->ptri_host[p], m = h->ptri_host[p + 1] - b;
+                    if (m == 0) {  // an empty phase: its 8 spans are empty at b
+                        phase_span_kernel<<<1, 64, 0, st>>>(h->ph_zero.get(), b,
+                                                             h->poff.get() + (size_t)8 * p);
+                        continue;
+                    }
+                    const int32_t* inp[3] = {tu + b, ti + b, tj + b};
+                    int32_t* outp[3] = {out[0] + b, out[1] + b, out[2] + b};
+                    h->xs.partition_groups(st, h->tri_g.get() + b, m, 3, inp, outp);
+                    phase_span_kernel<<<1, 64, 0, st>>>(h->xs.goff.get(), b,
+                                                         h->poff.get() + (size_t)8 * p);
+                }
+                MML_HIP(hipGetLastError());
+            } else if (part_g) {
                 h->xs.partition_groups(st, h->tri_g.get(), n, 3, in, out);
-            else
+            } else {
                 h->xs.partition(st, ti, n, 3, in, out);
+            }
             ng = 8;
-            goff = h->xs.goff.get();
+            goff = P > 1 ? h->poff.get() : h->xs.goff.get();
             tu = h->xt_u.get();
             ti = h->xt_i.get();
             tj = h->xt_j.get();
@@ -1640,10 +1775,11 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             // triples in flight and no stale per-XCD replicas
             launch_apply_ordered(h, tu, ti, tj, n, s, st, 4, weighted_streams(h) / 4);
         } else if (!ordered && !fused && n > 0) {
-            launch_update(h, soft, am, ng, goff, tu, ti, tj, blocks, 4, s, st);
+            for (int32_t p = 0; p < P; ++p)
+                launch_update(h, soft, am, ng, goff + (size_t)8 * p, tu, ti, tj, blocks, 4, s, st);
             int am_run = am;  // launch_update_lpr drops the user write-through past 4 GiB of U
             if ((uint64_t)h->n_users * h->ld * 4 >= (1ull << 32)) am_run &= ~kBprUThru;
-            h->last_launch = {true, soft, am_run, 4, ng, goff, tu, ti, tj, blocks, s};
+            h->last_launch = {true, soft, am_run, 4, ng, goff, tu, ti, tj, blocks, s, P, goff};
         } else if (fused) {
 #define MML_BPR(LPR)                                                                            \
     if (pair)                                                                                   \
@@ -1793,6 +1929,22 @@ extern "C" mml_status mml_bpr_set_rows(mml_bpr* h, int32_t side, int32_t n_rows,
     });
 }
 
+extern "C" mml_status mml_bpr_set_hogwild_phases(mml_bpr* h, int32_t phases) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        MML_REQUIRE(phases >= 0 && phases <= 64, "phases must be in [0, 64]");
+        h->phases_req = phases;
+        for (mml_bpr* s : h->shards) s->phases_req = phases;
+    });
+}
+
+extern "C" mml_status mml_bpr_last_phases(mml_bpr* h, int32_t* out) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx && out, "null argument");
+        *out = h->shards.empty() ? h->last_phases : h->shards[0]->last_phases;
+    });
+}
+
 extern "C" mml_status mml_bpr_set_hogwild_waves(mml_bpr* h, int64_t waves) {
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
@@ -1905,14 +2057,20 @@ extern "C" mml_status mml_bpr_replay_traffic(mml_bpr* h, float* out_ms) {
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
-        switch (h->lpr) {
-            case 1: launch_replay_lpr<1>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
-            case 2: launch_replay_lpr<2>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
-            case 4: launch_replay_lpr<4>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
-            case 8: launch_replay_lpr<8>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
-            case 16: launch_replay_lpr<16>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
-            case 32: launch_replay_lpr<32>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
-            default: launch_replay_lpr<64>(h, L.am, L.ng, L.goff, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st); break;
+        for (int32_t p = 0; p < L.phases; ++p) {
+            const int64_t* go = L.goff + (size_t)8 * p;
+#define MML_RPL(LPR) \
+    launch_replay_lpr<LPR>(h, L.am, L.ng, go, L.tu, L.ti, L.tj, L.blocks, L.wpb, L.s, st)
+            switch (h->lpr) {
+                case 1: MML_RPL(1); break;
+                case 2: MML_RPL(2); break;
+                case 4: MML_RPL(4); break;
+                case 8: MML_RPL(8); break;
+                case 16: MML_RPL(16); break;
+                case 32: MML_RPL(32); break;
+                default: MML_RPL(64); break;
+            }
+#undef MML_RPL
         }
         MML_HIP(hipGetLastError());
         MML_HIP(hipEventRecord(h->ctx->ev_end, st));

@@ -364,6 +364,15 @@ def scenario_ring(nd, G, epochs=3):
     final = bmf_model(hs, nu, ni, k)
     L.mml_bmf_destroy(hs)
     single_ctx.close()
+    bad = []
+    for r in range(nd):
+        after = comm[r][5]
+        rows = np.nonzero(np.any(after[0] != final[0], axis=1))[0]
+        if len(rows):
+            bad.append(f"rank {r}: {len(rows)} user rows differ (users {rows[:8].tolist()}...), "
+                       f"V rows differing {int(np.any(after[1] != final[1], axis=1).sum())}")
+    if bad:
+        print("set_data_device after ring epochs: " + "; ".join(bad), flush=True)
     for r in range(nd):
         _, obj, refused, st, ev, after = comm[r]
         assert np.all(np.abs(obj - obj_single) <= 1e-9 * np.abs(obj_single)), (obj, obj_single)

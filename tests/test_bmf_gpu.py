@@ -126,10 +126,11 @@ def test_c1_standin_rmse_parity():
     print(f"C1 hogwild: gpu RMSE {out2['RMSE']:.6f} oracle {rmse_ref:.6f}")
     ev_set = (eu, ei, ev.astype(np.float64))
     ref, d_rmse, d_pred = order_noise(tu_, ti_, tv_, seed=1, k=10, num_iter=30, eval_set=ev_set)
-    d_lock = lockstep_delta(tu_, ti_, tv_, seed=1, k=10, num_iter=30, eval_set=ev_set, ref=ref)
+    d_lock, d_pl = lockstep_delta(tu_, ti_, tv_, seed=1, k=10, num_iter=30, eval_set=ev_set,
+                                  ref=ref, with_pred=True)
     pred = m2.predict(eu, ei).astype(np.float64)
     rmse2 = float(np.sqrt(np.mean((pred - ev) ** 2)))
-    assert hogwild_band("C1 hogwild", rmse2, pred, ref, d_rmse, d_pred, d_lock)
+    assert hogwild_band("C1 hogwild", rmse2, pred, ref, d_rmse, d_pred, d_lock, d_pl)
 
 
 @pytest.mark.parametrize("k", [1, 5, 16, 64, 100, 128, 256])

@@ -12,7 +12,8 @@ sampler records, the XCD partition and a 7,648-wave Hogwild launch.  This set ha
   + UpdateFactors, BPRMF.cs:129-226, 330-374) for 2 epochs from it, with System.Random seed 7, and
   1 epoch with seed 8 (the oracle's own seed spread);
 * the GPU's HOGWILD epochs at this set's default launch (768 waves) and at C3's launch width
-  (mml_bpr_set_hogwild_waves: 7,648 waves, C3's triples in flight over C3's item distribution);
+  (mml_bpr_set_hogwild_waves: 7,648 waves, C3's triples in flight over C3's item distribution),
+  both with the default user phases (mml_bpr_set_hogwild_phases: 6 here, 51 at C3);
 * the ORDERED semantics of the device sampler: the GPU's sampled triples applied in sample order by
   the oracle's UpdateFactors (the ORDERED kernel equals that replay bit for bit,
   tests/test_multi_gpu.py), which separates the sampler's distribution from Hogwild staleness.
@@ -185,7 +186,10 @@ def test_c3_density_auc_parity_gpu_vs_exact_stream_oracle():
         tri.append(hog.triples(n))
         res[("hogwild", e + 1)] = auc()[0]
     kernel = N.last_kernel("mml_bpr_last_kernel", hog.h)
-    _log(f"GPU hogwild (default width, {kernel}): {[res[('hogwild', e + 1)] for e in range(EPOCHS)]}")
+    phases = ctypes.c_int32(0)
+    N.check(N.lib().mml_bpr_last_phases(hog.h, ctypes.byref(phases)))
+    _log(f"GPU hogwild (default width, {kernel}, {phases.value} user phases): "
+         f"{[res[('hogwild', e + 1)] for e in range(EPOCHS)]}")
 
     # ORDERED semantics of the device sampler: its triples applied in order by the oracle
     replay = {}

@@ -86,7 +86,9 @@ def test_bmf_multi_device_context_one_shard():
     """BiasedMatrixFactorization with Gpus=0 (mml_ctx_create_multi over one device): the user-
     shard path trains, Predict / Evaluate route through the shard, and the model gathered from it
     predicts exactly what a single-device handle with that model predicts."""
-    u, i, v = synth_ratings(5, 2000, 300, 120_000)
+    # 300 k ratings: the XCD-grouped 32-wave launch, the regime the staleness model restates
+    # (tests/test_edge_cases_gpu.py lane variants); 120 k ratings ran one 4-wave workgroup
+    u, i, v = synth_ratings(5, 2000, 300, 300_000)
     tu, ti, tv = synth_ratings(6, 2000, 300, 5000)
     res = {}
     for name, props in (("single", dict(Device=0)), ("multi", dict(Gpus="0"))):
@@ -104,11 +106,12 @@ def test_bmf_multi_device_context_one_shard():
     from test_edge_cases_gpu import hogwild_band, lockstep_delta, order_noise
     ev_set = (tu, ti, tv.astype(np.float64))
     ref, d_rmse, d_pred = order_noise(u, i, v, seed=4, k=16, num_iter=3, eval_set=ev_set)
-    d_lock = lockstep_delta(u, i, v, seed=4, k=16, num_iter=3, eval_set=ev_set, ref=ref)
+    d_lock, d_pl = lockstep_delta(u, i, v, seed=4, k=16, num_iter=3, eval_set=ev_set, ref=ref,
+                                  with_pred=True)
     for name, (mm, rm) in res.items():
         pred = mm.predict(tu, ti).astype(np.float64)
         assert hogwild_band(f"BMF hogwild {name}", float(np.sqrt(np.mean((pred - tv) ** 2))),
-                            pred, ref, d_rmse, d_pred, d_lock)
+                            pred, ref, d_rmse, d_pred, d_lock, d_pl)
     md = m.get_model()
     q = BiasedMatrixFactorization(NumFactors=16, NumIter=0, Schedule="hogwild")
     q.ratings = Ratings(u, i, v)
