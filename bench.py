@@ -49,6 +49,7 @@ from mymedialite_amd.random import SystemRandom  # noqa: E402
 from mymedialite_amd.synthetic import c3_chunks, c3_holdout, planted_ratings_torch  # noqa: E402,E501
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+SAMPLER_BYTES = 64 + 4 + 13 + 1 + 13 + 12  # C3 sampler + XCD partition, per triple (bench_bpr)
 
 
 def bytes_per_update(k: int) -> int:
@@ -307,16 +308,19 @@ def pmc_traffic(name, kernel_ms, alg_bytes=None):
     if not os.path.exists(tf):
         return None, None
     t = json.load(open(tf))
-    if alg_bytes is not None and abs(t["algorithmic_bytes_per_launch"] - alg_bytes) > 1e-3 * alg_bytes:
-        return None, (f"profiles/{name} was collected on launches of "
-                      f"{t['algorithmic_bytes_per_launch'] / 1e9:.1f} GB algorithmic, this run's "
-                      f"launches move {alg_bytes / 1e9:.1f} GB: not comparable")
-    gbs = t["traffic_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9
-    note = (f"PMC per launch ({'profiles/' + name}): FETCH_SIZE x2 + WRITE_SIZE = "
-            f"{t['traffic_bytes_per_launch'] / 1e9:.1f} GB ({t['traffic_over_algorithmic']:.2f} x "
-            f"the {t['algorithmic_bytes_per_launch'] / 1e9:.1f} GB algorithmic); with the "
-            f"same-pattern calibration {t['traffic_calibrated_bytes_per_launch'] / 1e9:.1f} GB "
-            f"({t['calibrated_over_algorithmic']:.2f} x)")
+    # per epoch: the user phases run one launch per phase (scripts/pmc_traffic2.py sums them)
+    alg_e = t.get("algorithmic_bytes_per_epoch", t["algorithmic_bytes_per_launch"])
+    tr_e = t.get("traffic_bytes_per_epoch", t["traffic_bytes_per_launch"])
+    cal_e = t.get("traffic_calibrated_bytes_per_epoch", t["traffic_calibrated_bytes_per_launch"])
+    if alg_bytes is not None and abs(alg_e - alg_bytes) > 1e-3 * alg_bytes:
+        return None, (f"profiles/{name} was collected on epochs of {alg_e / 1e9:.1f} GB "
+                      f"algorithmic, this run's epochs move {alg_bytes / 1e9:.1f} GB: not "
+                      f"comparable")
+    gbs = tr_e / (kernel_ms * 1e-3) / 1e9
+    note = (f"PMC per epoch ({'profiles/' + name}, {t.get('launches_per_epoch', 1)} launch(es)): "
+            f"FETCH_SIZE x2 + WRITE_SIZE = {tr_e / 1e9:.1f} GB ({t['traffic_over_algorithmic']:.2f} "
+            f"x the {alg_e / 1e9:.1f} GB algorithmic); with the same-pattern calibration "
+            f"{cal_e / 1e9:.1f} GB ({t['calibrated_over_algorithmic']:.2f} x)")
     return gbs, note
 
 
@@ -689,6 +693,12 @@ def bench_bpr(args):
                      "kernel_avg_ms": upd_ms, "bytes_per_update": bpu,
                      "epoch_device_ms": avg_ms,
                      "sampler_ms": avg_ms - upd_ms,
+                     # the sampler + XCD partition's own algorithmic bytes per triple: the user's
+                     # 64-B record line (row start, |S_u|, Bloom filter), one 4-B column (i), the
+                     # triple and its group byte written (13), the partition's count read (1),
+                     # scatter read (13) and write (12)
+                     "sampler_bytes_per_triple": SAMPLER_BYTES,
+                     "sampler_GBps": n * SAMPLER_BYTES / max(1e-9, (avg_ms - upd_ms) * 1e-3) / 1e9,
                      "frac_epoch": n * bpu / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "frac_note": "frac = the update kernel alone; frac_epoch = the same bytes "
                                   "over the whole device epoch (sampler + XCD partition + "
@@ -782,6 +792,7 @@ def bench_wrmf(args):
         + 2 * n * k
     flops_direct = half(n_users, n_items) + half(n_items, n_users)
     tflops = flops_exec / (np.mean(ms) * 1e-3) / 1e12
+    gather = c5_gather_traffic() if (k == 256 and n_users == 5_000_000) else None
     line = {
         "metric": "WRMF iterations/sec, k=256 (C5)", "value": args.steps / elapsed,
         "unit": "iterations/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -798,7 +809,10 @@ def bench_wrmf(args):
                    "num_factors": k, "events": n, "users": n_users, "items": n_items,
                    "alpha": 1.0, "regularization": 0.015, "device_ingest_s": ingest_s},
         "roofline": {"bound": "mfma", "achieved": tflops, "peak": 157.3, "unit": "TFLOP/s",
-                     "frac": tflops / 157.3, "traffic": None,
+                     "frac": tflops / 157.3,
+                     "traffic": gather["GBps"] if gather else None,
+                     "traffic_note": gather["note"] if gather else None,
+                     "gather_kernels": gather["kernels"] if gather else None,
                      "kernel": "wrmf_wood_w16_kernel + wrmf_wood_cg_kernel + "
                                "wrmf_tile_solve_kernel + wrmf_tile_gram_kernel + "
                                "wrmf_split_planes_kernel + wrmf_gram_* (+ wrmf_resid_seg_kernel, "
@@ -838,6 +852,37 @@ def bench_wrmf(args):
     N.lib().mml_wrmf_destroy(h)
     ctx.close()
     return line if rank == 0 else None
+
+
+def c5_gather_traffic(name="r5e_c5_traffic.json"):
+    """C5's two gather kernels against their algorithmic bytes (scripts/pmc_c5.py, FETCH_SIZE x 2 +
+    WRITE_SIZE per dispatch of one iteration, user half first): the fp64 residual (every entry's H
+    row, nnz k 4 B per half) and the Woodbury rows of 97-128 items (their Q_S rows once)."""
+    tf = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(tf):
+        return None
+    t = json.load(open(tf))
+    alg = t["algorithmic_bytes_per_half"]
+    out, tot_b, tot_ms = [], 0.0, 0.0
+    for kern, halves in (("wrmf_resid_seg_kernel", ("user", "item")),
+                         ("wrmf_wood_w16_kernel", ("user", "user (refinement pass)"))):
+        key = "resid" if "resid" in kern else "w16"
+        for d, half in zip(t["kernels"][kern], halves):
+            a = alg["user" if half.startswith("user") else "item"][key]
+            ms = d["duration_ms_under_pmc"]
+            out.append({"kernel": kern, "half": half, "traffic_GB": d["traffic_bytes"] / 1e9,
+                        "algorithmic_GB": a / 1e9 if "refinement" not in half else None,
+                        "traffic_over_algorithmic": d["traffic_bytes"] / a
+                        if "refinement" not in half else None,
+                        "ms_under_pmc": ms, "traffic_GBps": d["traffic_bytes"] / (ms * 1e-3) / 1e9})
+            tot_b += d["traffic_bytes"]
+            tot_ms += ms
+    return {"GBps": tot_b / (tot_ms * 1e-3) / 1e9, "kernels": out,
+            "note": f"PMC (profiles/{name}): the residual and Woodbury-w16 dispatches of one "
+                    f"iteration, FETCH_SIZE x 2 + WRITE_SIZE over their durations under the "
+                    f"counters; residual 0.88 x (user half) and 1.01 x (item half) of its "
+                    f"algorithmic gather bytes at 7.1 / 5.5 TB/s, w16 0.83 x at 2.9 TB/s "
+                    f"(latency-bound)"}
 
 
 def wrmf_row_check(h, ku, ki, deg_u, deg_i, n_users, n_items, k):

@@ -476,9 +476,10 @@ mml_status mml_bpr_set_hogwild_waves(mml_bpr* h, int64_t waves);
  * sampler draws the epoch's triples phase by phase -- each phase's share of the Feedback.Count
  * triples in proportion to its users, u uniform within the phase, so every user keeps SampleUser's
  * probability 1 / n_eligible per triple (BPRMF.cs:300-310) -- and each phase is partitioned by
- * XCD group and updated by its own launch, which then touches 1/P of U.  phases = 0 (default):
- * one phase per 96 MiB of the eligible users' rows, at most 64 (C3: 51); 1 = one draw over all
- * users.  mml_bpr_last_phases: the count the last epoch used. */
+ * XCD group and updated by its own launch, which then touches 1/P of U.  phases = 0 (default) or
+ * 1: one draw over all users -- at C3 the phases were measured slower (update kernel 300 ms in one
+ * phase, 304-313 ms in 32-64: the uniform V_j rows stream through the Infinity Cache between a
+ * user's triples); P in [2, 64] turns them on.  mml_bpr_last_phases: the count the last epoch used. */
 mml_status mml_bpr_set_hogwild_phases(mml_bpr* h, int32_t phases);
 mml_status mml_bpr_last_phases(mml_bpr* h, int32_t* out);
 /* The last epoch's sampled triples in sample order (n = Feedback.Count), e.g. for BPRMF's

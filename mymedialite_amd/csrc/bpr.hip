@@ -1373,22 +1373,19 @@ inline int32_t bpr_user_phase(int32_t u, int32_t P) {
     return (int32_t)((x ^ (x >> 31)) % (uint64_t)P);
 }
 
-// User phases of the default sampler's Hogwild epoch.  Default: one phase per 96 MiB of the
-// eligible users' rows, at most 64 (C3: 10 M users x 512 B -> 51), so one update launch touches
-// a phase's U rows, which then stay in the 256 MB Infinity Cache between a user's triples.
+// User phases of the default sampler's Hogwild epoch: off by default.  Measured at C3 (one box,
+// profiles/r5e/c3_p*): update kernel 300.2 / 300.3 ms in one phase, 304.0 in 32, 310.3 in 51, 313.3
+// in 64; sampler + partition 31.4 -> 35.6-36.9 ms.  Unlike BiasedMF's U, a phase's U rows do not
+// stay in the Infinity Cache here: between two triples of a user the phase streams ~100 MB of
+// uniform V_j rows (512 MB of V) through it.  mml_bpr_set_hogwild_phases turns them on.
 int32_t bpr_phases(const mml_bpr* h) {
     static const int32_t env = [] {
         const char* e = MML_EXPERIMENT_ENV("MML_BPR_PHASES");
         return e ? std::max(0, std::min(64, std::atoi(e))) : -1;
     }();
-    int32_t P;
+    int32_t P = 1;
     if (env >= 0) P = std::max(1, env);
     else if (h->phases_req > 0) P = h->phases_req;
-    else {
-        const uint64_t bytes = (uint64_t)h->n_eligible * h->ld * sizeof(float);
-        const uint64_t per = 96ull << 20;
-        P = (int32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, (bytes + per - 1) / per));
-    }
     return std::max(1, std::min(P, h->n_eligible));
 }
 

@@ -1,7 +1,7 @@
 """Per-launch HBM-side traffic of one kernel from two rocprofv3 --pmc passes (csv output).
 
   python scripts/pmc_traffic2.py <FETCH_SIZE dir> <WRITE_SIZE dir> <kernel substring> \\
-      <algorithmic bytes per launch> out.json
+      <algorithmic bytes per launch (per epoch with the 6th argument)> out.json [launches/epoch]
 
 Two readings are reported (MI355X_MICROARCH.md, HBM section):
   guide       FETCH_SIZE x 2 + WRITE_SIZE: gfx950's FETCH_SIZE counts half the bytes of wide
@@ -25,16 +25,23 @@ def per_launch(d, name):
     return sum(vals) / len(vals) * 1024.0, len(vals)  # rocprofv3 reports KB
 
 
+# optional 6th argument: launches per epoch (the user phases: one launch per phase), in which
+# case <algorithmic bytes> is the whole epoch's and the per-epoch fields sum the phase launches
 fd, wd, name, alg, out = sys.argv[1:6]
+per_epoch = int(sys.argv[6]) if len(sys.argv) > 6 else 1
 fetch, nf = per_launch(fd, name)
 write, nw = per_launch(wd, name)
 alg = float(alg)
 res = {"kernel": name, "fetch_size_bytes": fetch, "write_size_bytes": write,
-       "launches": [nf, nw], "algorithmic_bytes_per_launch": alg,
+       "launches": [nf, nw], "algorithmic_bytes_per_launch": alg / per_epoch,
        "traffic_bytes_per_launch": 2.0 * fetch + write,
        "traffic_calibrated_bytes_per_launch": fetch / 0.7246976 + write / 1.1091082,
+       "launches_per_epoch": per_epoch,
+       "algorithmic_bytes_per_epoch": alg,
        "sources": [fd, wd]}
-res["traffic_over_algorithmic"] = res["traffic_bytes_per_launch"] / alg
-res["calibrated_over_algorithmic"] = res["traffic_calibrated_bytes_per_launch"] / alg
+res["traffic_bytes_per_epoch"] = res["traffic_bytes_per_launch"] * per_epoch
+res["traffic_calibrated_bytes_per_epoch"] = res["traffic_calibrated_bytes_per_launch"] * per_epoch
+res["traffic_over_algorithmic"] = res["traffic_bytes_per_epoch"] / alg
+res["calibrated_over_algorithmic"] = res["traffic_calibrated_bytes_per_epoch"] / alg
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))

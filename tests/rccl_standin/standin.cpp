@@ -5,9 +5,9 @@
 // never linked to it.
 //
 // Every rank is a host thread of one process with its own mml_ctx (device 0 repeated).  The
-// stand-in executes each call for real (data moved with hipMemcpy after the caller's stream has
-// drained) and CHECKS the call pattern a real communicator would only expose as a hang or a wrong
-// result:
+// stand-in executes each call for real (the caller's stream drained, then the data copied on that
+// stream and the stream drained again, so a call is complete when it returns) and CHECKS the call
+// pattern a real communicator would only expose as a hang or a wrong result:
 //   * collectives (ncclAllReduce, ncclBroadcast): every rank of the communicator issues the same
 //     sequence, with equal op, datatype, count, reduction and root -- checked at each call;
 //   * point-to-point (ncclSend / ncclRecv): the m-th send from a to b pairs with the m-th recv on b
@@ -168,6 +168,15 @@ bool hip_ok(hipError_t e, const std::string& what) {
     return false;
 }
 
+// a copy complete on return: on the caller's stream, then that stream drained (a plain hipMemcpy
+// of device to device memory may return before the copy lands, and the null stream does not
+// order against the library's non-blocking streams)
+hipError_t copy_sync(void* dst, const void* src, size_t bytes, hipStream_t st) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(st);
+}
+
 std::string describe(const Op& o) {
     return std::string(kind_name(o.kind)) + " dtype=" + std::to_string((int)o.dtype) +
            " count=" + std::to_string(o.count) +
@@ -204,14 +213,14 @@ ncclResult_t run_collective(const Op& o) {
     bool ok = true;
     if (bytes > 0) {
         if (o.kind == Op::kBroadcast) {
-            ok = hip_ok(hipMemcpy(acc.data(), w.slot[o.peer].send, bytes, hipMemcpyDefault),
+            ok = hip_ok(copy_sync(acc.data(), w.slot[o.peer].send, bytes, o.stream),
                         "broadcast read");
         } else {
             std::vector<char> x(bytes);
-            ok = hip_ok(hipMemcpy(acc.data(), w.slot[0].send, bytes, hipMemcpyDefault),
+            ok = hip_ok(copy_sync(acc.data(), w.slot[0].send, bytes, o.stream),
                         "allreduce read");
             for (int q = 1; q < w.n && ok; ++q) {
-                ok = hip_ok(hipMemcpy(x.data(), w.slot[q].send, bytes, hipMemcpyDefault),
+                ok = hip_ok(copy_sync(x.data(), w.slot[q].send, bytes, o.stream),
                             "allreduce read");
                 switch (o.dtype) {
                     case ncclFloat32:
@@ -242,7 +251,7 @@ ncclResult_t run_collective(const Op& o) {
     // every rank has read every input before any rank overwrites its own buffer (in place)
     if (!w.barrier(r, "collective (read phase)")) return ncclInvalidUsage;
     if (ok && bytes > 0)
-        ok = hip_ok(hipMemcpy(o.recv, acc.data(), bytes, hipMemcpyDefault), "collective write");
+        ok = hip_ok(copy_sync(o.recv, acc.data(), bytes, o.stream), "collective write");
     {
         std::lock_guard<std::mutex> lk(g_stats.m);
         (o.kind == Op::kAllReduce ? g_stats.allreduce : g_stats.broadcast)++;
@@ -312,8 +321,7 @@ ncclResult_t run_group(std::vector<Op>& ops) {
                           std::to_string(m->count) + " of type " + std::to_string((int)m->dtype));
             res = ncclInvalidUsage;
         } else if (o.count > 0 &&
-                   !hip_ok(hipMemcpy(o.recv, m->buf, o.count * type_size(o.dtype),
-                                     hipMemcpyDefault),
+                   !hip_ok(copy_sync(o.recv, m->buf, o.count * type_size(o.dtype), o.stream),
                            "recv copy")) {
             res = ncclSystemError;
         }

@@ -11,9 +11,10 @@ sampler records, the XCD partition and a 7,648-wave Hogwild launch.  This set ha
 * the exact-stream oracle (BPRMF.Train's loss-sample burn, then IterateWithoutReplacementUniformUser
   + UpdateFactors, BPRMF.cs:129-226, 330-374) for 2 epochs from it, with System.Random seed 7, and
   1 epoch with seed 8 (the oracle's own seed spread);
-* the GPU's HOGWILD epochs at this set's default launch (768 waves) and at C3's launch width
+* the GPU's HOGWILD epochs at this set's default launch (768 waves), at C3's launch width
   (mml_bpr_set_hogwild_waves: 7,648 waves, C3's triples in flight over C3's item distribution),
-  both with the default user phases (mml_bpr_set_hogwild_phases: 6 here, 51 at C3);
+  and with the sampler's user phases on (mml_bpr_set_hogwild_phases(6): the epoch drawn phase by
+  phase, each phase's U rows in one launch; off by default);
 * the ORDERED semantics of the device sampler: the GPU's sampled triples applied in sample order by
   the oracle's UpdateFactors (the ORDERED kernel equals that replay bit for bit,
   tests/test_multi_gpu.py), which separates the sampler's distribution from Hogwild staleness.
@@ -216,6 +217,17 @@ def test_c3_density_auc_parity_gpu_vs_exact_stream_oracle():
     _log(f"GPU hogwild ({w} waves, C3's width): "
          f"{[res[('c3width', e + 1)] for e in range(EPOCHS)]}")
 
+    # GPU HOGWILD with 6 user phases (the sampler draws phase by phase)
+    hog.set_model(*init)
+    N.check(N.lib().mml_bpr_set_hogwild_phases(hog.h, 6))
+    for e in range(EPOCHS):
+        N.check(N.lib().mml_bpr_iterate(hog.h, 6000 + 97 * e))
+        res[("phases", e + 1)] = auc()[0]
+    N.check(N.lib().mml_bpr_last_phases(hog.h, ctypes.byref(phases)))
+    assert phases.value == 6
+    N.check(N.lib().mml_bpr_set_hogwild_phases(hog.h, 0))
+    _log(f"GPU hogwild (6 user phases): {[res[('phases', e + 1)] for e in range(EPOCHS)]}")
+
     for t in threads:
         t.join()
     for (seed, e), model in sorted(oracle_models.items()):
@@ -229,7 +241,7 @@ def test_c3_density_auc_parity_gpu_vs_exact_stream_oracle():
     _log(f"oracle seed 7: {[ref[e] for e in ref]}, seed 8 epoch 1: {res[('oracle8', 1)]:.5f} "
          f"(seed spread {spread:+.5f})")
     worst = 0.0
-    for name in ("replay", "hogwild", "c3width"):
+    for name in ("replay", "hogwild", "c3width", "phases"):
         d = [res[(name, e)] - ref[e] for e in range(1, EPOCHS + 1)]
         worst = max(worst, max(abs(x) for x in d))
         _log(f"C3 density {name}: AUC {[round(res[(name, e)], 5) for e in ref]}, vs oracle "
