@@ -245,7 +245,7 @@ def bench_c2(args):
     achieved = n_local * bpu / (avg_kernel_ms * 1e-3) / 1e9
     traffic, traffic_note = None, None
     if k == 64 and n_local == 100_000_000 and args.schedule == "hogwild":
-        traffic, traffic_note = pmc_traffic("r4_c2_traffic.json", avg_kernel_ms)
+        traffic, traffic_note = pmc_traffic("r5_c2_traffic.json", avg_kernel_ms)
     kernel = (N.last_kernel("mml_bmf_last_kernel", h) or
               f"bmf_sgd_ordered_kernel (schedule {args.schedule})")
     ceiling = (box_ceiling("mml_bmf_replay_traffic", h, avg_kernel_ms, n_local * bpu)
@@ -528,7 +528,7 @@ def bench_c4(args):
     achieved = n_local * bpu / (avg_kernel_ms * 1e-3) / 1e9
     traffic, traffic_note = None, None
     if world == 1 and k == 64 and n_total == 1_000_000_000:
-        traffic, traffic_note = pmc_traffic("r4_c4_traffic.json", avg_kernel_ms)
+        traffic, traffic_note = pmc_traffic("r5_c4_traffic.json", avg_kernel_ms)
     cpu = None
     if cpu_sample is not None:
         cpu = cpu_baseline_dsgd(h, k, n_users, n_items, gb, cpu_sample, "C4")
@@ -662,7 +662,7 @@ def bench_bpr(args):
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_bpr(k, args.cpu_seconds)
     traffic, traffic_note = None, None
     if k == 128 and n_total == 500_000_000 and args.sampler == "uniform_user" and world == 1:
-        traffic, traffic_note = pmc_traffic("r4_c3_traffic.json", upd_ms, n * bpu)
+        traffic, traffic_note = pmc_traffic("r5_c3_traffic.json", upd_ms, n * bpu)
     kernel = N.last_kernel("mml_bpr_last_kernel", h)
     phases = ctypes.c_int32(0)
     N.check(N.lib().mml_bpr_last_phases(h, ctypes.byref(phases)))

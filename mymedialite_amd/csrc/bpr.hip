@@ -1378,6 +1378,9 @@ inline int32_t bpr_user_phase(int32_t u, int32_t P) {
 // in 64; sampler + partition 31.4 -> 35.6-36.9 ms.  Unlike BiasedMF's U, a phase's U rows do not
 // stay in the Infinity Cache here: between two triples of a user the phase streams ~100 MB of
 // uniform V_j rows (512 MB of V) through it.  mml_bpr_set_hogwild_phases turns them on.
+// Phases for the sampler alone (triples drawn phase by phase, then partitioned and updated as one
+// epoch) were measured too: sampler 32.7 -> 35.5 ms at 16 / 51 / 64 phases, the update unchanged
+// (profiles/r5g/), so they were not kept.
 int32_t bpr_phases(const mml_bpr* h) {
     static const int32_t env = [] {
         const char* e = MML_EXPERIMENT_ENV("MML_BPR_PHASES");
