@@ -86,6 +86,13 @@ __device__ __forceinline__ int opaque_tid() {
     return t;
 }
 
+// an empty use of a loaded value: the load cannot then be sunk under the select that consumes it
+// (a load under a branch is waited for before the branch joins, so a batch of gathers written as
+// selected loads ran one at a time)
+__device__ __forceinline__ void keep_loaded(float4& g) {
+    asm volatile("" : "+v"(g.x), "+v"(g.y), "+v"(g.z), "+v"(g.w));
+}
+
 __device__ __forceinline__ float lane_bcast(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
@@ -2032,7 +2039,7 @@ wrmf_wood_cg_kernel(
 // wrmf_wood_cg_kernel<128> spends three barriers and a 64-value butterfly per step, and its
 // z sums cross four waves through the LDS.  Same parameters, same arithmetic (Chebyshev main
 // solve, CG refinement), same output t.
-template <int WAVES>
+template <int WAVES, bool VEC>  // VEC: k % 4 == 0 (a feature quad is one 16-B load)
 __global__ __launch_bounds__(64 * WAVES, 4) void wrmf_wood_w16_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, const int64_t* __restrict__ off,
     const int32_t* __restrict__ cols, const float* __restrict__ Q, int32_t k, float alpha,
@@ -2045,14 +2052,27 @@ __global__ __launch_bounds__(64 * WAVES, 4) void wrmf_wood_w16_kernel(
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int f0 = 4 * lane;
-    const bool vec = (k & 3) == 0;
+    constexpr bool vec = VEC;
     const float ainv = 1.0f / alpha;
     int par = 0;
-    for (int li = blockIdx.x; li < n_list; li += gridDim.x) {
-        const int32_t row = rows[li];
-        const int64_t rb = off[row];
-        const int deg = (int)(off[row + 1] - rb);
-        const int j0 = 16 * wave;
+    const int j0 = 16 * wave;
+    // a row's item ids: rows[li] -> off[row] -> cols is a chain of three dependent loads ahead of
+    // the Q gathers, so the next row's are fetched while this row computes (after its gathers are
+    // issued).  The cols load is clamped into the row, no branch around it: the lanes past the
+    // wave's items hold a valid id, whose gathered row is zeroed (j >= nloc)
+    auto ids_of = [&](int l, int32_t& r, int64_t& b, int& d) -> int {
+        r = rows[l];
+        b = off[r];
+        d = (int)(off[r + 1] - b);
+        return cols[d > 0 ? b + min(j0 + lane, d - 1) : 0];
+    };
+    int32_t row = 0, row_n = 0;
+    int64_t rb = 0, rb_n = 0;
+    int deg = 0, deg_n = 0, idv = 0, idv_n = 0;
+    if ((int)blockIdx.x < n_list) idv = ids_of(blockIdx.x, row, rb, deg);
+    for (int li = blockIdx.x; li < n_list;
+         li += gridDim.x, row = row_n, rb = rb_n, deg = deg_n, idv = idv_n) {
+        const int ln = min(li + (int)gridDim.x, n_list - 1);  // (the last row: fetched again)
         const int nloc = __builtin_amdgcn_readfirstlane(max(0, min(16, deg - j0)));
         const bool live = j0 + (lane >> 2) < deg;  // the item this lane carries the state of
         __syncthreads();  // the previous row is done with the LDS
@@ -2074,31 +2094,54 @@ __global__ __launch_bounds__(64 * WAVES, 4) void wrmf_wood_w16_kernel(
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
                         if (f0 + c < k) Tout[(int64_t)li * k + f0 + c] = 0.0f;
+                idv_n = ids_of(ln, row_n, rb_n, deg_n);
                 continue;
             }
         }
-        const int idv = lane < nloc ? cols[rb + j0 + lane] : 0;
         // qp[c][jp] = (Q_S[2 jp][f0 + c], Q_S[2 jp + 1][f0 + c]): item pairs as packed operands
         f32x2 qp[4][8];
+        if constexpr (vec) {
+            // all 16 row loads in flight at once: no branch around a load (a load under a branch
+            // is waited for before the join, which serialised the 16 gathers); the slots past the
+            // wave's items re-read a valid row (ids_of) and are zeroed after the loads
+            float4 g[16];
+            const int fo = f0 < k ? f0 : 0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int id = __builtin_amdgcn_readlane(idv, j);
-            const float* src = Q + (int64_t)id * k + f0;
-            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (j < nloc) {
-                if (vec) {
-                    if (f0 < k) v = *reinterpret_cast<const float4*>(src);
-                } else {
+            for (int j = 0; j < 16; ++j) {
+                const int id = __builtin_amdgcn_readlane(idv, j);
+                g[j] = *reinterpret_cast<const float4*>(Q + (int64_t)id * k + fo);
+            }
+            // the next row's ids after all 16 gathers (the wait counter is in order: a gather
+            // issued after them would make the first use of these wait for the ids too)
+            __builtin_amdgcn_sched_barrier(0);
+            idv_n = ids_of(ln, row_n, rb_n, deg_n);
+            keep_loaded(g[0]);  // (the compiler sank slot 0's load under its select)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const bool ok = j < nloc && f0 < k;
+                qp[0][j >> 1][j & 1] = ok ? g[j].x : 0.0f;
+                qp[1][j >> 1][j & 1] = ok ? g[j].y : 0.0f;
+                qp[2][j >> 1][j & 1] = ok ? g[j].z : 0.0f;
+                qp[3][j >> 1][j & 1] = ok ? g[j].w : 0.0f;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int id = __builtin_amdgcn_readlane(idv, j);
+                const float* src = Q + (int64_t)id * k + f0;
+                float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (j < nloc) {
                     v.x = f0 < k ? src[0] : 0.0f;
                     v.y = f0 + 1 < k ? src[1] : 0.0f;
                     v.z = f0 + 2 < k ? src[2] : 0.0f;
                     v.w = f0 + 3 < k ? src[3] : 0.0f;
                 }
+                qp[0][j >> 1][j & 1] = v.x;
+                qp[1][j >> 1][j & 1] = v.y;
+                qp[2][j >> 1][j & 1] = v.z;
+                qp[3][j >> 1][j & 1] = v.w;
             }
-            qp[0][j >> 1][j & 1] = v.x;
-            qp[1][j >> 1][j & 1] = v.y;
-            qp[2][j >> 1][j & 1] = v.z;
-            qp[3][j >> 1][j & 1] = v.w;
+            idv_n = ids_of(ln, row_n, rb_n, deg_n);
         }
         // z_j = sum_f Q_S[j][f] u_f for this wave's items: the lane's value for item j0 + l / 4
         auto z_of = [&](const float (&u)[4]) -> float {
@@ -2298,9 +2341,9 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
     }();
     const float cheb_acosh = row_bound ? (float)std::acosh(2.0 / tol) : -1.0f;
     if ((g == 3 && wood_w16()) || (g == 2 && wood_w16_mode() == 2))
-        wrmf_wood_w16_kernel<8><<<grid, 64 * 8, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
-                                                         max_it, tol2, skip2, abs2, cheb_m,
-                                                         (float)theta, (float)delta, cheb_acosh);
+        ((k & 3) == 0 ? &wrmf_wood_w16_kernel<8, true> : &wrmf_wood_w16_kernel<8, false>)<<<
+            grid, 64 * 8, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout, max_it, tol2, skip2,
+                                   abs2, cheb_m, (float)theta, (float)delta, cheb_acosh);
     else if (g == 0)
         wrmf_wood_cg_kernel<32><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
                                                       max_it, tol2, skip2, abs2, cheb_m,
@@ -2431,20 +2474,7 @@ __global__ __launch_bounds__(256, MML_MATMUL_WAVES) void wrmf_rows_matmul_x3_ker
         for (int k0 = 0; k0 < kpad; k0 += kRH) {
             const int kw = min(kRH, kpad - k0);  // a multiple of 16
             __syncthreads();  // the previous half's reads (and the row ids' writes) are done
-            for (int x = 4 * t; x < 64 * kw; x += 4 * 256) {  // 4 consecutive k of one row
-                const int i = x / kw, fl = x - i * kw, f = k0 + fl;
-                float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-                const int64_t sr = srow[0][i];
-                if (sr >= 0) {
-                    const float* src = X + sr * k;
-                    if (vec && f + 3 < k) {
-                        const float4 v4 = *reinterpret_cast<const float4*>(src + f);
-                        v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] = f + j < k ? src[f + j] : 0.0f;
-                    }
-                }
+            auto put = [&](int i, int fl, const float (&v)[4]) {
                 uint32_t a[4], b[4], c[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) split3t(v[j], a[j], b[j], c[j]);
@@ -2454,6 +2484,43 @@ __global__ __launch_bounds__(256, MML_MATMUL_WAVES) void wrmf_rows_matmul_x3_ker
                     make_uint2(pack_hi(b[0], b[1]), pack_hi(b[2], b[3]));
                 *reinterpret_cast<uint2*>(&xs[2][i * kRHS + fl]) =
                     make_uint2(pack_hi(c[0], c[1]), pack_hi(c[2], c[3]));
+            };
+            if (vec) {
+                // the half's kRH / 16 row gathers per thread issued together (clamped addresses,
+                // zeroed after): under a branch each was waited for before the next went out
+                constexpr int kG = kRH / 16;
+                float4 g[kG];
+#pragma unroll
+                for (int it = 0; it < kG; ++it) {  // 4 consecutive k of one row
+                    const int x = 4 * t + 1024 * it, i = min(x / kw, 63), f = k0 + x - i * kw;
+                    const int64_t sr = srow[0][i];
+                    g[it] = *reinterpret_cast<const float4*>(X + (sr >= 0 ? sr : 0) * k +
+                                                             (f + 3 < k ? f : 0));
+                }
+#pragma unroll
+                for (int it = 0; it < kG; ++it) {
+                    const int x = 4 * t + 1024 * it;
+                    keep_loaded(g[it]);
+                    if (x < 64 * kw) {
+                        const int i = x / kw, fl = x - i * kw;
+                        const bool ok = srow[0][i] >= 0 && k0 + fl + 3 < k;
+                        const float v[4] = {ok ? g[it].x : 0.0f, ok ? g[it].y : 0.0f,
+                                            ok ? g[it].z : 0.0f, ok ? g[it].w : 0.0f};
+                        put(i, fl, v);
+                    }
+                }
+            } else {
+                for (int x = 4 * t; x < 64 * kw; x += 4 * 256) {  // 4 consecutive k of one row
+                    const int i = x / kw, fl = x - i * kw, f = k0 + fl;
+                    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                    const int64_t sr = srow[0][i];
+                    if (sr >= 0) {
+                        const float* src = X + sr * k;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] = f + j < k ? src[f + j] : 0.0f;
+                    }
+                    put(i, fl, v);
+                }
             }
             __syncthreads();
             for (int kc = 0; kc < kw; kc += 16) {
@@ -2624,20 +2691,32 @@ __global__ __launch_bounds__(256) void wrmf_resid_seg_kernel(
             const int32_t my = lane < n ? cols[e0 + lane] : 0;
             for (int x0 = 0; x0 < n; x0 += kResE) {
                 float v[kResE][4];
+                if (vec) {
+                    // the kResE row loads issued together, none under a branch (entries past the
+                    // segment read row my = 0 and are zeroed after): a load under a branch was
+                    // waited for before the next one was issued
+                    float4 g[kResE];
+                    const int fo = f0 < k ? f0 : 0;
 #pragma unroll
-                for (int u = 0; u < kResE; ++u) {
-                    v[u][0] = v[u][1] = v[u][2] = v[u][3] = 0.0f;
-                    if (x0 + u < n) {  // wave-uniform; entries past the segment have h = 0
-                        const float* hr = H + (int64_t)__builtin_amdgcn_readlane(my, x0 + u) * k;
-                        if (vec) {
-                            if (f0 < k) {
-                                const float4 q = *reinterpret_cast<const float4*>(hr + f0);
-                                v[u][0] = q.x;
-                                v[u][1] = q.y;
-                                v[u][2] = q.z;
-                                v[u][3] = q.w;
-                            }
-                        } else {
+                    for (int u = 0; u < kResE; ++u)
+                        g[u] = *reinterpret_cast<const float4*>(
+                            H + (int64_t)__builtin_amdgcn_readlane(my, x0 + u) * k + fo);
+#pragma unroll
+                    for (int u = 0; u < kResE; ++u) {
+                        keep_loaded(g[u]);
+                        const bool ok = x0 + u < n && f0 < k;  // entries past the segment: h = 0
+                        v[u][0] = ok ? g[u].x : 0.0f;
+                        v[u][1] = ok ? g[u].y : 0.0f;
+                        v[u][2] = ok ? g[u].z : 0.0f;
+                        v[u][3] = ok ? g[u].w : 0.0f;
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < kResE; ++u) {
+                        v[u][0] = v[u][1] = v[u][2] = v[u][3] = 0.0f;
+                        if (x0 + u < n) {  // wave-uniform; entries past the segment have h = 0
+                            const float* hr =
+                                H + (int64_t)__builtin_amdgcn_readlane(my, x0 + u) * k;
 #pragma unroll
                             for (int j = 0; j < 4; ++j) v[u][j] = f0 + j < k ? hr[f0 + j] : 0.0f;
                         }
@@ -2727,29 +2806,37 @@ __global__ __launch_bounds__(256, MML_XHH_WAVES) void wrmf_xhh_kernel(const doub
         for (int jt = 0; jt < 16; ++jt) acc[jt] = f64x4{0.0, 0.0, 0.0, 0.0};
         // staging of chunk c into buffer bb: HH rows c*16 .. +16 (all columns), X rows r0 .. r0+64
         // columns c*16 .. +16; zero past k and past n
+        // the chunk's loads go out unconditionally (clamped in-range addresses; the values past k
+        // or n are zeroed when stored to LDS): a select around a load became a branch, and each
+        // load was waited for before the next was issued, so the prefetch of chunk c + 1 did not
+        // fly under chunk c's MFMAs
         double hv[kXK], xv[kXV];
         auto load = [&](int c) {
+            const int tc = t < k ? t : k - 1;
 #pragma unroll
             for (int x = 0; x < kXK; ++x) {  // kXK x 256 HH values: thread t -> row x, column t
-                const int f = c * kXK + x;
-                hv[x] = (f < k && t < k) ? HH[(int64_t)f * k + t] : 0.0;
+                const int f = min(c * kXK + x, k - 1);
+                hv[x] = HH[(int64_t)f * k + tc];
             }
+            const int64_t row = min(r0 + (t >> 2), n - 1);
 #pragma unroll
             for (int x = 0; x < kXV; ++x) {  // 64 x kXK X values: row t / 4, col kXV (t % 4) + x
-                const int64_t row = r0 + (t >> 2);
-                const int f = c * kXK + kXV * (t & 3) + x;
-                xv[x] = (row < n && f < k) ? X[row * k + f] : 0.0;
+                const int f = min(c * kXK + kXV * (t & 3) + x, k - 1);
+                xv[x] = X[row * k + f];
             }
         };
-        auto store = [&](int bb) {
+        auto store = [&](int bb, int c) {
 #pragma unroll
-            for (int x = 0; x < kXK; ++x) sb[bb][x][t] = hv[x];
+            for (int x = 0; x < kXK; ++x) sb[bb][x][t] = (c * kXK + x < k && t < k) ? hv[x] : 0.0;
+            const bool rin = r0 + (t >> 2) < n;
 #pragma unroll
-            for (int x = 0; x < kXV; ++x) sa[bb][t >> 2][kXV * (t & 3) + x] = xv[x];
+            for (int x = 0; x < kXV; ++x)
+                sa[bb][t >> 2][kXV * (t & 3) + x] =
+                    (rin && c * kXK + kXV * (t & 3) + x < k) ? xv[x] : 0.0;
         };
         load(0);
         __syncthreads();  // the previous row block's last chunk has been read
-        store(0);
+        store(0, 0);
         __syncthreads();
         for (int c = 0; c < nk; ++c) {
             const int bb = c & 1;
@@ -2762,18 +2849,30 @@ __global__ __launch_bounds__(256, MML_XHH_WAVES) void wrmf_xhh_kernel(const doub
                     acc[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, sb[bb][4 * s + kk][16 * jt + i],
                                                                    acc[jt], 0, 0, 0);
             }
-            if (c + 1 < nk) store(bb ^ 1);
+            if (c + 1 < nk) store(bb ^ 1, c + 1);
             __syncthreads();
         }
         // D layout: column 16 jt + (lane & 15), row 4 v + (lane >> 4) of the wave's 16 rows
+        // X's values for two column tiles loaded together (clamped addresses, no branch), then the
+        // in-range stores
 #pragma unroll
-        for (int jt = 0; jt < 16; ++jt) {
-            const int col = 16 * jt + i;
-            if (col >= k) continue;
+        for (int j2 = 0; j2 < 16; j2 += 2) {
+            double xe[2][4];
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int64_t row = r0 + 16 * wave + 4 * v + kk;
-                if (row < n) R[row * k + col] = -acc[jt][v] - reg * X[row * k + col];
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int64_t row = min(r0 + 16 * wave + 4 * v + kk, n - 1);
+                    xe[u][v] = X[row * k + min(16 * (j2 + u) + i, k - 1)];
+                }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int col = 16 * (j2 + u) + i;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int64_t row = r0 + 16 * wave + 4 * v + kk;
+                    if (col < k && row < n) R[row * k + col] = -acc[j2 + u][v] - reg * xe[u][v];
+                }
             }
         }
     }
