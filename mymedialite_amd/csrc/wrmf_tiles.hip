@@ -2252,11 +2252,14 @@ __global__ __launch_bounds__(64 * WAVES, 4) void wrmf_wood_w16_kernel(
 }
 
 // MML_WRMF_WOOD16 (experiments builds): 0 = rows of 97 .. 128 items on wrmf_wood_cg_kernel<128>,
-// 2 = rows of 65 .. 96 items on wrmf_wood_w16_kernel<8> too (default 1: 97 .. 128 only)
+// 1 = 97 .. 128 only, 2 (default) = rows of 65 .. 96 items on wrmf_wood_w16_kernel<8> too, 3 = those
+// on wrmf_wood_w16_kernel<6>.  With its gathers issued together (round 5) the w16 kernel takes the
+// 65 .. 96-item rows in less time than wrmf_wood_cg_kernel<96, 3>: C5 127.0 + 36.2 -> 156.8 ms per
+// iteration for both buckets (profiles/r5j/); in round 4 it was 45 ms against 36 for that bucket
 int wood_w16_mode() {
     static const int v = [] {
         const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOOD16");
-        return e ? std::atoi(e) : 1;
+        return e ? std::atoi(e) : 2;
     }();
     return v;
 }
@@ -2340,7 +2343,11 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
         return !(e && std::string(e) == "0");
     }();
     const float cheb_acosh = row_bound ? (float)std::acosh(2.0 / tol) : -1.0f;
-    if ((g == 3 && wood_w16()) || (g == 2 && wood_w16_mode() == 2))
+    if (g == 2 && wood_w16_mode() == 3)
+        ((k & 3) == 0 ? &wrmf_wood_w16_kernel<6, true> : &wrmf_wood_w16_kernel<6, false>)<<<
+            grid, 64 * 6, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout, max_it, tol2, skip2,
+                                   abs2, cheb_m, (float)theta, (float)delta, cheb_acosh);
+    else if ((g == 3 && wood_w16()) || (g == 2 && wood_w16_mode() == 2))
         ((k & 3) == 0 ? &wrmf_wood_w16_kernel<8, true> : &wrmf_wood_w16_kernel<8, false>)<<<
             grid, 64 * 8, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout, max_it, tol2, skip2,
                                    abs2, cheb_m, (float)theta, (float)delta, cheb_acosh);

@@ -51,7 +51,8 @@ def test_c3_eight_user_shards_auc_vs_one_handle():
         t1 = time.perf_counter()
         N.check(N.lib().mml_bpr_set_data_device(h, users.data_ptr(), items.data_ptr(), n, None))
         N.check(N.lib().mml_bpr_init_model(h, 2, 0.0, 0.1))
-        aucs = []
+        aucs = [N.auc_held_out("mml_bpr_auc", h, cand, te_u, te_i)[0]]  # InitModel
+        _log(f"C3 x{nd}: InitModel AUC {aucs[0]:.5f}")
         for e in range(2):
             N.check(N.lib().mml_bpr_iterate(h, 2000 + 97 * e))
             aucs.append(N.auc_held_out("mml_bpr_auc", h, cand, te_u, te_i)[0])
@@ -60,12 +61,20 @@ def test_c3_eight_user_shards_auc_vs_one_handle():
         N.lib().mml_bpr_destroy(h)
         ctx.close()
         torch.cuda.empty_cache()
-    d = [b - a for a, b in zip(res[1], res[8])]
-    _log(f"C3 AUC one handle {res[1]}, 8 averaged shards {res[8]}, difference {d}")
-    # both learn the held-out positives (AUC 0.5 at random; ~0.82 after one epoch: the
-    # popularity of the Zipf items and their factors), and 8-way averaging costs no more than the
-    # C3 replica's GPU-vs-oracle band (measured -0.0012 / +0.0016)
-    assert all(a > 0.75 for a in res[1] + res[8]), res
+    d = [b - a for a, b in zip(res[1][1:], res[8][1:])]
+    _log(f"C3 AUC (InitModel, epoch 1, epoch 2) one handle {res[1]}, 8 averaged shards {res[8]}, "
+         f"difference {d}; epoch 2 - epoch 1: one handle {res[1][2] - res[1][1]:+.5f}, 8 shards "
+         f"{res[8][2] - res[8][1]:+.5f} (the exact-stream oracle at C3's density: +0.00344, "
+         f"tests/test_bpr_c3_density_gpu.py)")
+    # learning, in the form the exact-stream oracle pins at C3's density (1M users x 1M items,
+    # degree 50: InitModel 0.501 -> 0.810 after one epoch, tests/test_bpr_c3_density_gpu.py):
+    # the first epoch lifts the held-out AUC from InitModel's ~0.5 by more than 0.1, for both;
+    # whether the second epoch adds or takes back a few 1e-3 depends on the density (10x the users
+    # per item here), so it is printed, not asserted
+    for nd in (1, 8):
+        assert abs(res[nd][0] - 0.5) < 0.02, res
+        assert res[nd][1] > res[nd][0] + 0.1 and res[nd][2] > res[nd][0] + 0.1, res
+    # and 8-way averaging costs no more than the GPU-vs-oracle band (|dAUC| <= 0.005)
     assert all(abs(x) <= 0.005 for x in d), d
 
 
