@@ -854,35 +854,32 @@ def bench_wrmf(args):
     return line if rank == 0 else None
 
 
-def c5_gather_traffic(name="r5e_c5_traffic.json"):
-    """C5's two gather kernels against their algorithmic bytes (scripts/pmc_c5.py, FETCH_SIZE x 2 +
-    WRITE_SIZE per dispatch of one iteration, user half first): the fp64 residual (every entry's H
-    row, nnz k 4 B per half) and the Woodbury rows of 97-128 items (their Q_S rows once)."""
+def c5_gather_traffic(name="r5n_c5_traffic.json"):
+    """C5's gather kernels against their algorithmic bytes (scripts/pmc_c5.py, FETCH_SIZE x 2 +
+    WRITE_SIZE per dispatch of one iteration, in launch order): the fp64 residual (every entry's H
+    row, nnz k 4 B per half) and the Woodbury rows on the w16 kernel (their Q_S rows once)."""
     tf = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(tf):
         return None
     t = json.load(open(tf))
-    alg = t["algorithmic_bytes_per_half"]
     out, tot_b, tot_ms = [], 0.0, 0.0
-    for kern, halves in (("wrmf_resid_seg_kernel", ("user", "item")),
-                         ("wrmf_wood_w16_kernel", ("user", "user (refinement pass)"))):
-        key = "resid" if "resid" in kern else "w16"
-        for d, half in zip(t["kernels"][kern], halves):
-            a = alg["user" if half.startswith("user") else "item"][key]
-            ms = d["duration_ms_under_pmc"]
-            out.append({"kernel": kern, "half": half, "traffic_GB": d["traffic_bytes"] / 1e9,
-                        "algorithmic_GB": a / 1e9 if "refinement" not in half else None,
-                        "traffic_over_algorithmic": d["traffic_bytes"] / a
-                        if "refinement" not in half else None,
+    for kern in ("wrmf_resid_seg_kernel", "wrmf_wood_w16_kernel"):
+        for d in t["kernels"][kern]:
+            a, ms = d["algorithmic_bytes"], d["duration_ms_under_pmc"]
+            out.append({"kernel": kern, "rows": d["label"], "traffic_GB": d["traffic_bytes"] / 1e9,
+                        "algorithmic_GB": a / 1e9 if a else None,
+                        "traffic_over_algorithmic": d["traffic_bytes"] / a if a else None,
                         "ms_under_pmc": ms, "traffic_GBps": d["traffic_bytes"] / (ms * 1e-3) / 1e9})
             tot_b += d["traffic_bytes"]
             tot_ms += ms
+    main = [o for o in out if o["traffic_over_algorithmic"] is not None]
+    summary = "; ".join(f"{o['kernel'].replace('_kernel', '').replace('wrmf_', '')} {o['rows']}: "
+                        f"{o['traffic_over_algorithmic']:.2f} x at {o['traffic_GBps'] / 1e3:.1f} TB/s"
+                        for o in main)
     return {"GBps": tot_b / (tot_ms * 1e-3) / 1e9, "kernels": out,
             "note": f"PMC (profiles/{name}): the residual and Woodbury-w16 dispatches of one "
                     f"iteration, FETCH_SIZE x 2 + WRITE_SIZE over their durations under the "
-                    f"counters; residual 0.88 x (user half) and 1.01 x (item half) of its "
-                    f"algorithmic gather bytes at 7.1 / 5.5 TB/s, w16 0.83 x at 2.9 TB/s "
-                    f"(latency-bound)"}
+                    f"counters, against their algorithmic gather bytes: {summary}"}
 
 
 def wrmf_row_check(h, ku, ki, deg_u, deg_i, n_users, n_items, k):

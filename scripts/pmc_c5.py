@@ -7,8 +7,10 @@ next #3).  Run on the GPU box (the C5 degrees come from synthetic.c5_events on t
 Algorithmic bytes per half-step (k = 256, fp32 rows of 1 KiB, WRMF.cs:110-156):
   * wrmf_resid_seg_kernel (fp64 residual b - A x of the refinement pass): every entry of the half
     gathers its H row -> nnz k 4 B;
-  * wrmf_wood_w16_kernel (Woodbury rows of 97..128 items): every such row gathers its Q_S rows
-    once -> sum(deg) k 4 B over those rows.
+  * wrmf_wood_w16_kernel (Woodbury rows of 65..96 and of 97..128 items, one dispatch per bucket,
+    main solve then refinement pass): every such row gathers its Q_S rows once -> sum(deg) k 4 B
+    over the bucket's rows (a refinement dispatch skips the rows whose correction bound is below
+    target, so it has no fixed algorithmic count).
 Traffic = FETCH_SIZE x 2 + WRITE_SIZE (MI355X_MICROARCH.md, gfx950 FETCH_SIZE counts half the bytes
 of 16-B-per-lane reads), per dispatch; the dispatches of one iteration are listed in order (user
 half first) so each can be read against its half's algorithmic bytes."""
@@ -46,17 +48,31 @@ def main():
     deg_i = torch.bincount((key % ni).to(torch.int64), minlength=ni)
     nnz = int(key.numel())
     row = k * 4
+    def bucket(deg, lo, hi):
+        m = (deg >= lo) & (deg <= hi)
+        return int(deg[m].sum().item()) * row, int(m.sum().item())
     alg = {}
     for side, deg in (("user", deg_u), ("item", deg_i)):
-        w16 = (deg >= 97) & (deg <= 128)
-        alg[side] = {"resid": nnz * row, "w16": int(deg[w16].sum().item()) * row,
-                     "w16_rows": int(w16.sum().item())}
+        b2, n2 = bucket(deg, 65, 96)
+        b3, n3 = bucket(deg, 97, 128)
+        alg[side] = {"resid": nnz * row, "w16_65_96": b2, "w16_65_96_rows": n2,
+                     "w16_97_128": b3, "w16_97_128_rows": n3}
+    # the dispatches of one iteration in launch order (wrmf_tile_solve / wrmf_tile_refine): the
+    # residual once per half; the w16 kernel per Woodbury bucket, main solve then refinement pass
+    # (the item half has no Woodbury rows at C5)
+    labels = {"wrmf_resid_seg_kernel": [("user", alg["user"]["resid"]),
+                                        ("item", alg["item"]["resid"])],
+              "wrmf_wood_w16_kernel": [("user 65-96", alg["user"]["w16_65_96"]),
+                                       ("user 97-128", alg["user"]["w16_97_128"]),
+                                       ("user 65-96 (refinement pass)", None),
+                                       ("user 97-128 (refinement pass)", None)]}
     res = {"algorithmic_bytes_per_half": alg, "nnz": nnz, "kernels": {}}
     for name in ("wrmf_resid_seg_kernel", "wrmf_wood_w16_kernel"):
         f, w = dispatches(fd, name), dispatches(wd, name)
         res["kernels"][name] = [
-            {"fetch_bytes": a[0], "write_bytes": b[0], "traffic_bytes": 2 * a[0] + b[0],
-             "duration_ms_under_pmc": a[1] * 1e-6} for a, b in zip(f, w)]
+            {"label": lab, "algorithmic_bytes": ab, "fetch_bytes": a[0], "write_bytes": b[0],
+             "traffic_bytes": 2 * a[0] + b[0], "duration_ms_under_pmc": a[1] * 1e-6}
+            for a, b, (lab, ab) in zip(f, w, labels[name])]
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res))
 
