@@ -1,4 +1,4 @@
-"""TEST INFRASTRUCTURE ONLY -- the library's RCCL communicator branches at 2-3 ranks on one GPU.
+"""TEST INFRASTRUCTURE ONLY -- the library's RCCL communicator branches at 2-4 ranks on one GPU.
 
 Run by tests/test_rccl_standin_gpu.py in a fresh subprocess with MML_LIB_PATH pointing at
 tests/rccl_standin/libmml_hip_standin.so: libmml_hip.so's own objects linked against the checking
@@ -403,7 +403,11 @@ def main():
                      ("wrmf2_k256", lambda: scenario_wrmf(2, 256, 3)),
                      ("wrmf3_k256", lambda: scenario_wrmf(3, 256, 3)),
                      ("ring2", lambda: scenario_ring(2, 4)),
-                     ("ring3", lambda: scenario_ring(3, 6))):
+                     ("ring3", lambda: scenario_ring(3, 6)),
+                     ("bmf4", lambda: scenario_bmf_average(4)),
+                     ("bpr4", lambda: scenario_bpr_average(4)),
+                     ("wrmf4_k256", lambda: scenario_wrmf(4, 256, 3)),
+                     ("ring4", lambda: scenario_ring(4, 8))):
         t1 = time.perf_counter()
         before = report()
         msg = fn()
