@@ -1990,12 +1990,15 @@ wrmf_wood_cg_kernel(
             for (int it = 0; it < m; ++it) {
                 w += dv;
                 if (it + 1 == m) break;
+                // the step's coefficients (scalars of the row alone) before the barrier, so their
+                // division's latency hides behind it; the same float operations as after it
+                const float rho = 1.0f / (2.0f * s1 - rho_p);
+                const float c1 = rho * rho_p, c2 = 2.0f * rho / delta;
                 if (t < NJ) sp[t] = dv;
                 __syncthreads();
                 const float uf = qt_times();
                 r -= (t < deg ? dv * ainv : 0.0f) + qs_times(uf);  // r -= C d
-                const float rho = 1.0f / (2.0f * s1 - rho_p);
-                dv = rho * rho_p * dv + (2.0f * rho / delta) * r;
+                dv = c1 * dv + c2 * r;
                 rho_p = rho;
             }
         }
@@ -2218,10 +2221,12 @@ __global__ __launch_bounds__(64 * WAVES, 4) void wrmf_wood_w16_kernel(
             for (int it = 0; it < m; ++it) {
                 w += dv;
                 if (it + 1 == m) break;
+                // the step's coefficients before u_of's barrier (as in wrmf_wood_cg_kernel)
+                const float rho = 1.0f / (2.0f * s1 - rho_p);
+                const float c1 = rho * rho_p, c2 = 2.0f * rho / delta;
                 u_of(dv, u);
                 r -= (live ? dv * ainv : 0.0f) + z_of(u);  // r -= C d
-                const float rho = 1.0f / (2.0f * s1 - rho_p);
-                dv = rho * rho_p * dv + (2.0f * rho / delta) * r;
+                dv = c1 * dv + c2 * r;
                 rho_p = rho;
             }
         }
@@ -2674,9 +2679,10 @@ __device__ __forceinline__ double pstage_f64(double x) {
 // are its segment's ids and its rows, so thousands of waves keep the gathers in flight.  The order
 // of every sum is fixed (deterministic).
 constexpr int kResE = 8;
+template <typename XT>  // X: fp64 rows, or (first pass) the fp32 W rows, widened on load
 __global__ __launch_bounds__(256) void wrmf_resid_seg_kernel(
     const RSeg* __restrict__ segs, int64_t nseg, const int32_t* __restrict__ cols,
-    const float* __restrict__ H, int32_t k, const double* __restrict__ X, double alpha,
+    const float* __restrict__ H, int32_t k, const XT* __restrict__ X, double alpha,
     double* __restrict__ R, double* __restrict__ partial) {
     static_assert(kResE == 8, "the butterfly below reduces 8 entries");
     const int lane = threadIdx.x & 63, f0 = 4 * lane;
@@ -2686,7 +2692,7 @@ __global__ __launch_bounds__(256) void wrmf_resid_seg_kernel(
     const bool vec = (k & 3) == 0;
     for (int64_t s = wave0; s < nseg; s += nwave) {
         const RSeg sg = segs[s];
-        const double* xr = X + (int64_t)sg.row * k;
+        const XT* xr = X + (int64_t)sg.row * k;
         double x[4], acc[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -2799,7 +2805,8 @@ constexpr int kXV = kXK / 4;  // X values per thread and chunk
 #ifndef MML_XHH_WAVES
 #define MML_XHH_WAVES 2
 #endif
-__global__ __launch_bounds__(256, MML_XHH_WAVES) void wrmf_xhh_kernel(const double* __restrict__ X,
+template <typename XT>  // X: fp64 rows, or (first pass) the fp32 W rows, widened on load
+__global__ __launch_bounds__(256, MML_XHH_WAVES) void wrmf_xhh_kernel(const XT* __restrict__ X,
                                                        const double* __restrict__ HH, int64_t n,
                                                        int32_t k, double reg,
                                                        double* __restrict__ R) {
@@ -2885,9 +2892,10 @@ __global__ __launch_bounds__(256, MML_XHH_WAVES) void wrmf_xhh_kernel(const doub
     }
 }
 
-// op 0: X = W; 1: Rf = R; 2: X += D, and dmax[t] = max |D| / (1 + |X|) over the rows of type t
-// (0 direct, 1 Woodbury: 1 <= deg <= kWood when wood): the size of the correction relative to the
-// solution, i.e. the error the pass removed; 3: W = X
+// op 0: X = W; 1: Rf = R; 2: X += D and W = (float) X, and dmax[t] = max |D| / (1 + |X|) over the
+// rows of type t (0 direct, 1 Woodbury: 1 <= deg <= kWood when wood): the size of the correction
+// relative to the solution, i.e. the error the pass removed; 3: W = X; 4: op 2 on the first pass,
+// whose x is W itself (X = (double) W + D: no op 0 before it, no op 3 after the last pass)
 __global__ __launch_bounds__(256) void wrmf_refine_rows_kernel(int op, int64_t r0, int64_t n,
                                                                int32_t k, float* __restrict__ W,
                                                                double* __restrict__ X,
@@ -2904,7 +2912,7 @@ __global__ __launch_bounds__(256) void wrmf_refine_rows_kernel(int op, int64_t r
         const int64_t row = r0 + lr;
         const int64_t le = lr * k, ge = row * k;
         int t = 0;
-        if (op == 2) {
+        if (op == 2 || op == 4) {
             const int64_t deg = off[row + 1] - off[row];
             t = wood && deg >= 1 && deg <= 128 ? 1 : 0;
         }
@@ -2912,9 +2920,11 @@ __global__ __launch_bounds__(256) void wrmf_refine_rows_kernel(int op, int64_t r
             switch (op) {
                 case 0: X[le + f] = (double)W[ge + f]; break;
                 case 1: Rf[ge + f] = (float)R[le + f]; break;
-                case 2: {
-                    const double x = X[le + f] + (double)D[ge + f];
+                case 2:
+                case 4: {
+                    const double x = (op == 4 ? (double)W[ge + f] : X[le + f]) + (double)D[ge + f];
                     X[le + f] = x;
+                    W[ge + f] = (float)x;
                     const float c = (float)(fabs((double)D[ge + f]) / (1.0 + fabs(x)));
                     m[t] = fmaxf(m[t], c);
                     break;
@@ -2923,7 +2933,7 @@ __global__ __launch_bounds__(256) void wrmf_refine_rows_kernel(int op, int64_t r
             }
         }
     }
-    if (op == 2)  // non-negative floats order like their bit patterns
+    if (op == 2 || op == 4)  // non-negative floats order like their bit patterns
         for (int t = 0; t < 2; ++t) {
             float v = m[t];
             for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
@@ -3086,18 +3096,30 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
                                                       p.ws->dmax.get());
         ++launches;
     };
-    rows(0);
+    // the first pass reads x as the fp32 W rows (widened on load, exactly) instead of a widened
+    // copy, and every pass's x += d also writes W = (float) x: no X = W pass before the first
+    // residual, no W = X pass after the last (C5: ~7 ms per iteration of row traffic)
+    const float* w0 = W + p.r0 * (int64_t)k;  // local row lr = W row r0 + lr
     int32_t done = 0;
     for (int32_t pass = 0; pass < passes; ++pass) {
         // R = -X (HH + reg I) on the fp64 matrix cores, then + sum_i c_i h_i per row
         const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((n + kXB - 1) / kXB, 2048));
-        wrmf_xhh_kernel<<<gx, 256, 0, st>>>(p.ws->x64.get(), HH, n, k, reg, p.ws->r64.get());
+        if (pass == 0)
+            wrmf_xhh_kernel<float><<<gx, 256, 0, st>>>(w0, HH, n, k, reg, p.ws->r64.get());
+        else
+            wrmf_xhh_kernel<double><<<gx, 256, 0, st>>>(p.ws->x64.get(), HH, n, k, reg,
+                                                        p.ws->r64.get());
         ++launches;
         if (p.n_rsegs > 0) {
             const int gs = (int)std::min<int64_t>((p.n_rsegs + 3) / 4, 8192);  // 4 waves
-            wrmf_resid_seg_kernel<<<gs, 256, 0, st>>>(
-                reinterpret_cast<const RSeg*>(p.rsegs.get()), p.n_rsegs, cols, H, k, p.ws->x64.get(),
-                alpha, p.ws->r64.get(), p.ws->rpartial.get());
+            const RSeg* sg = reinterpret_cast<const RSeg*>(p.rsegs.get());
+            if (pass == 0)
+                wrmf_resid_seg_kernel<float><<<gs, 256, 0, st>>>(
+                    sg, p.n_rsegs, cols, H, k, w0, alpha, p.ws->r64.get(), p.ws->rpartial.get());
+            else
+                wrmf_resid_seg_kernel<double><<<gs, 256, 0, st>>>(
+                    sg, p.n_rsegs, cols, H, k, p.ws->x64.get(), alpha, p.ws->r64.get(),
+                    p.ws->rpartial.get());
         }
         if (p.n_rmulti > 0)
             wrmf_resid_multi_kernel<<<(int)std::min<int64_t>(p.n_rmulti, 8192), 256, 0, st>>>(
@@ -3109,7 +3131,7 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
         wrmf_tile_solve(st, p, p.ws->df.get(), H, h_rows, off, cols, HH, k, alpha, reg, launches,
                         p.ws->rf.get());
         MML_HIP(hipMemsetAsync(p.ws->dmax.get(), 0, 2 * sizeof(unsigned), st));
-        rows(2);
+        rows(pass == 0 ? 4 : 2);
         launches += 3;
         ++done;
         if (pass + 1 < passes) {  // another pass only while the correction was large
@@ -3119,7 +3141,6 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
             if (stop(d)) break;
         }
     }
-    rows(3);
     MML_HIP(hipGetLastError());
     return done;
 }
