@@ -164,6 +164,16 @@ struct WrmfTilePlan {
     // per half-step: false when the tiles do not fit the free HBM (the refinement then
     // refactors each row instead).
     bool keep_factor = false;
+    // the item half's pipeline (fp64 mode, no Woodbury rows in the plan): the light rows in nbatch
+    // contiguous row ranges (the light list range-major, degree-descending within a range), so the
+    // first refinement pass's residual of range b (X (HH + reg I), the data term, R -> Rf) runs on
+    // `side` while the main solve of range b + 1 runs on the handle's stream
+    int32_t nbatch = 1;
+    std::vector<int32_t> b_light;                // nbatch + 1 light-list offsets
+    std::vector<int64_t> b_row, b_seg, b_multi;  // nbatch + 1 local-row / rseg / rmulti offsets
+    hipStream_t side = nullptr;
+    std::vector<hipEvent_t> ev;
+    bool residual_ready = false;  // pass 0's R and Rf were computed inside wrmf_tile_solve
     // the refinement's buffers (factor tiles, x and r in fp64, residual / correction rows): only
     // needed inside one half-step, so both plans of a handle point at ONE workspace (ws)
     struct Refine {

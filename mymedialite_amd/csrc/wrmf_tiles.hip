@@ -2270,6 +2270,25 @@ int wood_w16_mode() {
 }
 bool wood_w16() { return wood_w16_mode() > 0; }
 
+// the item half's pipeline: the direct rows' first-pass residual of a row range runs on a second
+// stream under the next range's main solve (wrmf_tile_plan, wrmf_tile_solve).  MML_WRMF_PIPE=n
+// (experiments builds): n row ranges, 1 = off; MML_WRMF_PIPE_GRID: the residual kernel's grid
+// while it shares the CUs with the solve
+int32_t pipe_batches() {
+    static const int32_t v = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_PIPE");
+        return e ? std::max(1, std::min(16, std::atoi(e))) : 4;
+    }();
+    return v;
+}
+int pipe_grid() {
+    static const int v = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_PIPE_GRID");
+        return e ? std::max(64, std::atoi(e)) : 8192;
+    }();
+    return v;
+}
+
 // MML_WRMF_WOOD=chol keeps the Cholesky Woodbury kernel (A/B measurements); the default solves
 // the Woodbury rows by CG
 bool wood_cg() {
@@ -2679,36 +2698,39 @@ __device__ __forceinline__ double pstage_f64(double x) {
 // are its segment's ids and its rows, so thousands of waves keep the gathers in flight.  The order
 // of every sum is fixed (deterministic).
 constexpr int kResE = 8;
-template <typename XT>  // X: fp64 rows, or (first pass) the fp32 W rows, widened on load
-__global__ __launch_bounds__(256) void wrmf_resid_seg_kernel(
+// X: fp64 rows, or (first pass) the fp32 W rows, widened on load.  VEC: k % 4 == 0 (a feature quad
+// is one 16-B load).  Five waves per SIMD (<= 96 VGPRs): a wave per SIMD then fits beside the tile
+// solve's two (2 x 208 registers) when a batch's residual runs under the next batch's solve.
+template <typename XT, bool VEC>
+__global__ __launch_bounds__(256, 5) void wrmf_resid_seg_kernel(
     const RSeg* __restrict__ segs, int64_t nseg, const int32_t* __restrict__ cols,
     const float* __restrict__ H, int32_t k, const XT* __restrict__ X, double alpha,
-    double* __restrict__ R, double* __restrict__ partial) {
+    double* __restrict__ R, double* __restrict__ partial, int set) {
     static_assert(kResE == 8, "the butterfly below reduces 8 entries");
     const int lane = threadIdx.x & 63, f0 = 4 * lane;
     const int64_t wave0 =
         (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int64_t nwave = (int64_t)gridDim.x * 4;
-    const bool vec = (k & 3) == 0;
+    constexpr bool vec = VEC;
     for (int64_t s = wave0; s < nseg; s += nwave) {
         const RSeg sg = segs[s];
         const XT* xr = X + (int64_t)sg.row * k;
-        double x[4], acc[4];
+        XT x[4];  // kept in X's own type (widened at each use: exact), 4 registers fewer for fp32
+        double acc[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            x[j] = f0 + j < k ? xr[f0 + j] : 0.0;
+            x[j] = f0 + j < k ? xr[f0 + j] : XT(0);
             acc[j] = 0.0;
         }
         for (int64_t e0 = sg.b; e0 < sg.e; e0 += 64) {
             const int n = (int)min((int64_t)64, sg.e - e0);
             const int32_t my = lane < n ? cols[e0 + lane] : 0;
             for (int x0 = 0; x0 < n; x0 += kResE) {
-                float v[kResE][4];
-                if (vec) {
+                float4 g[kResE];  // the entries' h_i features f0 .. f0 + 3 (0 past the segment)
+                if constexpr (vec) {
                     // the kResE row loads issued together, none under a branch (entries past the
-                    // segment read row my = 0 and are zeroed after): a load under a branch was
-                    // waited for before the next one was issued
-                    float4 g[kResE];
+                    // segment read row my = 0 and are zeroed in place after): a load under a
+                    // branch was waited for before the next one was issued
                     const int fo = f0 < k ? f0 : 0;
 #pragma unroll
                     for (int u = 0; u < kResE; ++u)
@@ -2717,29 +2739,26 @@ __global__ __launch_bounds__(256) void wrmf_resid_seg_kernel(
 #pragma unroll
                     for (int u = 0; u < kResE; ++u) {
                         keep_loaded(g[u]);
-                        const bool ok = x0 + u < n && f0 < k;  // entries past the segment: h = 0
-                        v[u][0] = ok ? g[u].x : 0.0f;
-                        v[u][1] = ok ? g[u].y : 0.0f;
-                        v[u][2] = ok ? g[u].z : 0.0f;
-                        v[u][3] = ok ? g[u].w : 0.0f;
+                        if (!(x0 + u < n && f0 < k)) g[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                     }
                 } else {
 #pragma unroll
                     for (int u = 0; u < kResE; ++u) {
-                        v[u][0] = v[u][1] = v[u][2] = v[u][3] = 0.0f;
+                        float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
                         if (x0 + u < n) {  // wave-uniform; entries past the segment have h = 0
                             const float* hr =
                                 H + (int64_t)__builtin_amdgcn_readlane(my, x0 + u) * k;
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) v[u][j] = f0 + j < k ? hr[f0 + j] : 0.0f;
+                            for (int j = 0; j < 4; ++j) v[j] = f0 + j < k ? hr[f0 + j] : 0.0f;
                         }
+                        g[u] = make_float4(v[0], v[1], v[2], v[3]);
                     }
                 }
                 double t[kResE];
 #pragma unroll
                 for (int u = 0; u < kResE; ++u)
-                    t[u] = (double)v[u][0] * x[0] + (double)v[u][1] * x[1] +
-                           (double)v[u][2] * x[2] + (double)v[u][3] * x[3];
+                    t[u] = (double)g[u].x * (double)x[0] + (double)g[u].y * (double)x[1] +
+                           (double)g[u].z * (double)x[2] + (double)g[u].w * (double)x[3];
                 double a4[4], a2[2];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) a4[u] = tstage_f64<0>(t[u], t[u + 4], lane);
@@ -2752,8 +2771,10 @@ __global__ __launch_bounds__(256) void wrmf_resid_seg_kernel(
 #pragma unroll
                 for (int u = 0; u < kResE; ++u) {
                     const double c = (1.0 + alpha) - alpha * readlane_f64(a1, 8 * u);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[j] += c * (double)v[u][j];
+                    acc[0] += c * (double)g[u].x;
+                    acc[1] += c * (double)g[u].y;
+                    acc[2] += c * (double)g[u].z;
+                    acc[3] += c * (double)g[u].w;
                 }
             }
         }
@@ -2762,7 +2783,7 @@ __global__ __launch_bounds__(256) void wrmf_resid_seg_kernel(
             const int f = f0 + j;
             if (f < k) {
                 if (sg.slot < 0)
-                    R[(int64_t)sg.row * k + f] += acc[j];
+                    R[(int64_t)sg.row * k + f] = set ? acc[j] : R[(int64_t)sg.row * k + f] + acc[j];
                 else
                     partial[(int64_t)sg.slot * k + f] = acc[j];
             }
@@ -2774,13 +2795,13 @@ __global__ __launch_bounds__(256) void wrmf_resid_seg_kernel(
 __global__ __launch_bounds__(256) void wrmf_resid_multi_kernel(const RMulti* __restrict__ m,
                                                                int64_t n, int32_t k,
                                                                const double* __restrict__ partial,
-                                                               double* __restrict__ R) {
+                                                               double* __restrict__ R, int set) {
     for (int64_t x = blockIdx.x; x < n; x += gridDim.x) {
         const RMulti r = m[x];
         for (int f = threadIdx.x; f < k; f += blockDim.x) {
             double v = 0.0;
             for (int s = 0; s < r.nslot; ++s) v += partial[(int64_t)(r.slot0 + s) * k + f];
-            R[(int64_t)r.row * k + f] += v;
+            R[(int64_t)r.row * k + f] = set ? v : R[(int64_t)r.row * k + f] + v;
         }
     }
 }
@@ -2809,7 +2830,7 @@ template <typename XT>  // X: fp64 rows, or (first pass) the fp32 W rows, widene
 __global__ __launch_bounds__(256, MML_XHH_WAVES) void wrmf_xhh_kernel(const XT* __restrict__ X,
                                                        const double* __restrict__ HH, int64_t n,
                                                        int32_t k, double reg,
-                                                       double* __restrict__ R) {
+                                                       double* __restrict__ R, int add) {
     __shared__ double sb[2][kXK][kXNP];
     __shared__ double sa[2][kXB][kXKP];
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, i = lane & 15, kk = lane >> 4;
@@ -2885,7 +2906,10 @@ __global__ __launch_bounds__(256, MML_XHH_WAVES) void wrmf_xhh_kernel(const XT* 
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
                     const int64_t row = r0 + 16 * wave + 4 * v + kk;
-                    if (col < k && row < n) R[row * k + col] = -acc[j2 + u][v] - reg * xe[u][v];
+                    if (col < k && row < n) {
+                        const double t = -acc[j2 + u][v] - reg * xe[u][v];
+                        R[row * k + col] = add ? R[row * k + col] + t : t;
+                    }
                 }
             }
         }
@@ -2974,6 +2998,45 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
     light.resize(acc);
     for (int32_t r = (int32_t)r0; r < (int32_t)r1; ++r)
         if (!is_wood(r) && deg[r] <= kHeavy) light[bucket[kHeavy - deg[r]]++] = r;
+    // the pipeline's row ranges (wrmf_tile_solve): only without Woodbury rows, whose solve comes
+    // after the light rows' and whose W every range's residual would need
+    size_t n_wood_rows = 0;
+    for (auto& w : wood) n_wood_rows += w.size();
+    const int32_t want = pipe_batches();
+    p.nbatch = 1;
+    p.b_row.assign({0, r1 - r0});
+    if (want > 1 && n_wood_rows == 0 && (int64_t)light.size() >= (int64_t)want * 4096) {
+        // ranges of equal light work (Gram entries + a factorisation's worth per row), the light
+        // list range-major and degree-descending within a range (each range's work queue still
+        // ends on short rows)
+        int64_t total = 0;
+        for (int32_t r : light) total += deg[r] + 256;
+        std::vector<int32_t> cut(want + 1, (int32_t)r1);
+        cut[0] = (int32_t)r0;
+        int64_t run = 0;
+        int b = 1;
+        std::vector<char> is_light(r1 - r0, 0);
+        for (int32_t r : light) is_light[r - r0] = 1;
+        for (int32_t r = (int32_t)r0; r < (int32_t)r1 && b < want; ++r) {
+            if (is_light[r - r0]) run += deg[r] + 256;
+            if (run * want >= total * b) cut[b++] = r + 1;
+        }
+        std::vector<int32_t> by(light.size());
+        p.b_light.assign(want + 1, 0);
+        p.b_row.assign(want + 1, 0);
+        size_t at = 0;
+        for (int x = 0; x < want; ++x) {
+            p.b_row[x] = cut[x] - r0;
+            p.b_light[x] = (int32_t)at;
+            for (int32_t r : light)  // light is degree-descending: the range's rows in that order
+                if (r >= cut[x] && r < cut[x + 1]) by[at++] = r;
+        }
+        p.b_row[want] = r1 - r0;
+        p.b_light[want] = (int32_t)at;
+        light.swap(by);
+        p.nbatch = want;
+    }
+    if (p.nbatch == 1) p.b_light.assign({0, (int32_t)light.size()});
     for (int g = 0; g < 4; ++g) {
         p.n_wood[g] = (int32_t)wood[g].size();
         p.wood[g].alloc(std::max<size_t>(1, wood[g].size()));
@@ -3010,7 +3073,15 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
     std::vector<RSeg> rs;
     std::vector<RMulti> rm;
     int32_t slots = 0;
+    p.b_seg.assign(p.nbatch + 1, 0);
+    p.b_multi.assign(p.nbatch + 1, 0);
+    int nb = 0;
     for (int64_t r = r0; r < r1; ++r) {
+        while (nb < p.nbatch && r - r0 >= p.b_row[nb]) {  // the range starting at this row
+            p.b_seg[nb] = (int64_t)rs.size();
+            p.b_multi[nb] = (int64_t)rm.size();
+            ++nb;
+        }
         const int64_t b = begin[r], e = begin[r + 1];
         if (e == b) continue;
         const int32_t lr = (int32_t)(r - r0);
@@ -3021,6 +3092,10 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
         const int32_t s0 = slots;
         for (int64_t x = b; x < e; x += kRSeg) rs.push_back(RSeg{lr, slots++, x, std::min(e, x + kRSeg)});
         rm.push_back(RMulti{lr, s0, slots - s0, 0});
+    }
+    for (; nb <= p.nbatch; ++nb) {
+        p.b_seg[nb] = (int64_t)rs.size();
+        p.b_multi[nb] = (int64_t)rm.size();
     }
     p.r0 = r0;
     p.r1 = r1;
@@ -3038,7 +3113,62 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
     MML_HIP(hipStreamSynchronize(st));
 }
 
-WrmfTilePlan::~WrmfTilePlan() = default;
+WrmfTilePlan::~WrmfTilePlan() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    if (side) (void)hipStreamDestroy(side);
+}
+
+// the first refinement pass's residual over local rows [lr0, lr1) of a plan (its entry segments
+// [sg0, sg1) and multi-segment rows [m0, m1), which the plan keeps in row order): R = -X (HH + reg I)
+// with x = the fp32 W rows widened on load, + sum_i c_i h_i, then Rf = (float) R.
+// part 1: the dense term first (it sets R), then the data term added; part 2 (the pipeline, on the
+// side stream): the data term only, setting R (R was zeroed, so rows without entries read 0);
+// part 3 (after the pipeline): the dense term added, then Rf.  a + b = b + a in IEEE arithmetic, so
+// both orders give every R bit for bit.
+static void first_residual(hipStream_t s, WrmfTilePlan& p, float* W, const float* H,
+                           const int32_t* cols, const double* HH, int32_t k, double alpha,
+                           double reg, int64_t lr0, int64_t lr1, int64_t sg0, int64_t sg1,
+                           int64_t m0, int64_t m1, int grid_cap, int& launches, int part = 1) {
+    const int64_t n = lr1 - lr0;
+    if (n <= 0) return;
+    const float* w0 = W + (p.r0 + lr0) * (int64_t)k;
+    double* r = p.ws->r64.get() + lr0 * (int64_t)k;
+    auto dense = [&](int add) {
+        const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((n + kXB - 1) / kXB, 2048));
+        wrmf_xhh_kernel<float><<<gx, 256, 0, s>>>(w0, HH, n, k, reg, r, add);
+        ++launches;
+    };
+    if (part == 1) dense(0);
+    if (part != 3) {
+        const int set = part == 2;
+        if (sg1 > sg0) {
+            const int gs = (int)std::min<int64_t>((sg1 - sg0 + 3) / 4, grid_cap);  // 4 waves
+            const RSeg* sg = reinterpret_cast<const RSeg*>(p.rsegs.get()) + sg0;
+            // segment rows are local to r0: X is W from row r0 on, R the whole half's r64
+            (((k & 3) == 0) ? &wrmf_resid_seg_kernel<float, true>
+                            : &wrmf_resid_seg_kernel<float, false>)<<<gs, 256, 0, s>>>(
+                sg, sg1 - sg0, cols, H, k, W + p.r0 * (int64_t)k, alpha, p.ws->r64.get(),
+                p.ws->rpartial.get(), set);
+            ++launches;
+        }
+        if (m1 > m0) {
+            wrmf_resid_multi_kernel<<<(int)std::min<int64_t>(m1 - m0, 8192), 256, 0, s>>>(
+                reinterpret_cast<const RMulti*>(p.rmulti.get()) + m0, m1 - m0, k,
+                p.ws->rpartial.get(), p.ws->r64.get(), set);
+            ++launches;
+        }
+    }
+    if (part == 2) {
+        MML_HIP(hipGetLastError());
+        return;
+    }
+    if (part == 3) dense(1);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, 16384));
+    wrmf_refine_rows_kernel<<<grid, 256, 0, s>>>(1, p.r0 + lr0, n, k, W, nullptr, r,
+                                                 p.ws->rf.get(), nullptr, nullptr, 0, nullptr);
+    ++launches;
+    MML_HIP(hipGetLastError());
+}
 
 // a further pass runs while the last correction was larger than these (relative to 1 + |x|), per
 // row type.  The error left after a pass is the correction times the pass's contraction.  Direct
@@ -3099,34 +3229,35 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
     // the first pass reads x as the fp32 W rows (widened on load, exactly) instead of a widened
     // copy, and every pass's x += d also writes W = (float) x: no X = W pass before the first
     // residual, no W = X pass after the last (C5: ~7 ms per iteration of row traffic)
-    const float* w0 = W + p.r0 * (int64_t)k;  // local row lr = W row r0 + lr
     int32_t done = 0;
     for (int32_t pass = 0; pass < passes; ++pass) {
-        // R = -X (HH + reg I) on the fp64 matrix cores, then + sum_i c_i h_i per row
-        const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((n + kXB - 1) / kXB, 2048));
-        if (pass == 0)
-            wrmf_xhh_kernel<float><<<gx, 256, 0, st>>>(w0, HH, n, k, reg, p.ws->r64.get());
-        else
+        // R = -X (HH + reg I) on the fp64 matrix cores, then + sum_i c_i h_i per row, R -> Rf
+        if (pass == 0 && p.residual_ready) {
+            // computed range by range under the main solve (wrmf_tile_solve's pipeline)
+        } else if (pass == 0) {
+            first_residual(st, p, W, H, cols, HH, k, alpha, reg, 0, n, 0, p.n_rsegs, 0,
+                           p.n_rmulti, 8192, launches);
+        } else {
+            const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((n + kXB - 1) / kXB, 2048));
             wrmf_xhh_kernel<double><<<gx, 256, 0, st>>>(p.ws->x64.get(), HH, n, k, reg,
-                                                        p.ws->r64.get());
-        ++launches;
-        if (p.n_rsegs > 0) {
-            const int gs = (int)std::min<int64_t>((p.n_rsegs + 3) / 4, 8192);  // 4 waves
-            const RSeg* sg = reinterpret_cast<const RSeg*>(p.rsegs.get());
-            if (pass == 0)
-                wrmf_resid_seg_kernel<float><<<gs, 256, 0, st>>>(
-                    sg, p.n_rsegs, cols, H, k, w0, alpha, p.ws->r64.get(), p.ws->rpartial.get());
-            else
-                wrmf_resid_seg_kernel<double><<<gs, 256, 0, st>>>(
+                                                        p.ws->r64.get(), 0);
+            ++launches;
+            if (p.n_rsegs > 0) {
+                const int gs = (int)std::min<int64_t>((p.n_rsegs + 3) / 4, 8192);  // 4 waves
+                const RSeg* sg = reinterpret_cast<const RSeg*>(p.rsegs.get());
+                (((k & 3) == 0) ? &wrmf_resid_seg_kernel<double, true>
+                                : &wrmf_resid_seg_kernel<double, false>)<<<gs, 256, 0, st>>>(
                     sg, p.n_rsegs, cols, H, k, p.ws->x64.get(), alpha, p.ws->r64.get(),
-                    p.ws->rpartial.get());
+                    p.ws->rpartial.get(), 0);
+            }
+            if (p.n_rmulti > 0)
+                wrmf_resid_multi_kernel<<<(int)std::min<int64_t>(p.n_rmulti, 8192), 256, 0, st>>>(
+                    reinterpret_cast<const RMulti*>(p.rmulti.get()), p.n_rmulti, k,
+                    p.ws->rpartial.get(), p.ws->r64.get(), 0);
+            MML_HIP(hipGetLastError());
+            rows(1);
         }
-        if (p.n_rmulti > 0)
-            wrmf_resid_multi_kernel<<<(int)std::min<int64_t>(p.n_rmulti, 8192), 256, 0, st>>>(
-                reinterpret_cast<const RMulti*>(p.rmulti.get()), p.n_rmulti, k, p.ws->rpartial.get(),
-                p.ws->r64.get());
-        MML_HIP(hipGetLastError());
-        rows(1);
+        p.residual_ready = false;
         // D = A^{-1} R on the fp32 solver (rows outside [r0, r1) are not read)
         wrmf_tile_solve(st, p, p.ws->df.get(), H, h_rows, off, cols, HH, k, alpha, reg, launches,
                         p.ws->rf.get());
@@ -3324,28 +3455,72 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             MML_HIP(hipGetLastError());
             launches += 2;
         }
-        if (p.n_light > 0) {
+        auto sk = P ? &wrmf_tile_solve_kernel<0, true> : &wrmf_tile_solve_kernel<0, false>;
+        auto solve_light = [&](int64_t l0, int64_t l1) {  // light-list slice [l0, l1)
+            if (l1 <= l0) return;
             MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
-            const int gs = (int)std::min<int64_t>(p.n_light, grid_cap);
-            auto sk = P ? &wrmf_tile_solve_kernel<0, true> : &wrmf_tile_solve_kernel<0, false>;
+            const int gs = (int)std::min<int64_t>(l1 - l0, grid_cap);
             sk<<<gs, kThreads, 0, st>>>(
-                p.light.get(), p.n_light, p.counter.get(), off, cols, W, H, p.hht.get(), nullptr,
-                k, k, (float)alpha, nullptr, debug_mask(), rhs, F, P, ps, (int32_t)h_rows);
+                p.light.get() + l0, (int32_t)(l1 - l0), p.counter.get(), off, cols, W, H,
+                p.hht.get(), nullptr, k, k, (float)alpha, nullptr, debug_mask(), rhs,
+                F ? F + (size_t)l0 * tile_floats : nullptr, P, ps, (int32_t)h_rows);
             MML_HIP(hipGetLastError());
             ++launches;
+        };
+        // the deferred backward substitutions: W rows hold y, the kept tiles L
+        auto back = [&](const int32_t* list, int64_t n, const float* Fl) {
+            if (n <= 0) return;
+            const int64_t blocks = std::min<int64_t>((n + kRvWaves - 1) / kRvWaves, 256 * 16);
+            wrmf_tile_resolve_wave_kernel<<<(int)blocks, 64 * kRvWaves, 0, st>>>(
+                list, (int32_t)n, off, Fl, W, k, W, 1);
+            ++launches;
+        };
+        // the pipeline (fp64 mode, no Woodbury rows): range b's first-pass residual on the side
+        // stream under range b + 1's solve; the side stream must belong to this stream's device
+        bool pipe = F && p.nbatch > 1 && p.n_wood[0] + p.n_wood[1] + p.n_wood[2] + p.n_wood[3] == 0;
+        if (pipe) {
+            int dev_cur = -1, dev_st = -1;
+            MML_HIP(hipGetDevice(&dev_cur));
+            MML_HIP(hipStreamGetDevice(st, &dev_st));
+            pipe = dev_cur == dev_st;
         }
-        if (F) {  // the deferred backward substitutions: W rows hold y, the kept tiles L
-            auto back = [&](const int32_t* list, int64_t n, const float* Fl) {
-                if (n <= 0) return;
-                const int64_t blocks = std::min<int64_t>((n + kRvWaves - 1) / kRvWaves, 256 * 16);
-                wrmf_tile_resolve_wave_kernel<<<(int)blocks, 64 * kRvWaves, 0, st>>>(
-                    list, (int32_t)n, off, Fl, W, k, W, 1);
-                ++launches;
-            };
+        if (pipe) {
+            if (!p.side) MML_HIP(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
+            while ((int)p.ev.size() < p.nbatch + 1) {
+                hipEvent_t e;
+                MML_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                p.ev.push_back(e);
+            }
+            const int64_t n = p.r1 - p.r0;
+            p.ws->r64.reserve((size_t)n * k);  // the sizes wrmf_tile_refine reserves
+            p.ws->rf.reserve((size_t)p.r1 * k);
+            p.ws->rpartial.reserve(std::max<int64_t>(1, p.n_rslots) * (size_t)k);
+            MML_HIP(hipMemsetAsync(p.ws->r64.get(), 0, sizeof(double) * (size_t)n * k, st));
             back(p.heavy_dev.get(), nh, F + (size_t)p.n_light * tile_floats);
-            back(p.light.get(), p.n_light, F);
-            MML_HIP(hipGetLastError());
+            for (int b = 0; b < p.nbatch; ++b) {
+                solve_light(p.b_light[b], p.b_light[b + 1]);
+                back(p.light.get() + p.b_light[b], p.b_light[b + 1] - p.b_light[b],
+                     F + (size_t)p.b_light[b] * tile_floats);
+                MML_HIP(hipEventRecord(p.ev[b], st));
+                MML_HIP(hipStreamWaitEvent(p.side, p.ev[b], 0));
+                first_residual(p.side, p, W, H, cols, HH, k, alpha, reg, p.b_row[b],
+                               p.b_row[b + 1], p.b_seg[b], p.b_seg[b + 1], p.b_multi[b],
+                               p.b_multi[b + 1], pipe_grid(), launches, 2);
+            }
+            MML_HIP(hipEventRecord(p.ev[p.nbatch], p.side));
+            MML_HIP(hipStreamWaitEvent(st, p.ev[p.nbatch], 0));
+            // the dense term (the fp64 MFMA kernel takes whole SIMDs: not beside the solve)
+            first_residual(st, p, W, H, cols, HH, k, alpha, reg, 0, n, 0, 0, 0, 0, 8192, launches,
+                           3);
+            p.residual_ready = true;
+        } else {
+            solve_light(0, p.n_light);
+            if (F) {
+                back(p.heavy_dev.get(), nh, F + (size_t)p.n_light * tile_floats);
+                back(p.light.get(), p.n_light, F);
+            }
         }
+        MML_HIP(hipGetLastError());
     }
     int64_t nw = 0, nw_max = 0;
     for (int g = 0; g < 4; ++g) {
