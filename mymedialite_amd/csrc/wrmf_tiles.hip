@@ -3485,6 +3485,9 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             pipe = dev_cur == dev_st;
         }
         if (pipe) {
+            // (the side stream at the least or greatest priority, or the handle's stream at the
+            // greatest, measured the same: 741.8 / 744.0 / 742.2 ms against 741.3 / 743.9,
+            // profiles/r5u/)
             if (!p.side) MML_HIP(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
             while ((int)p.ev.size() < p.nbatch + 1) {
                 hipEvent_t e;
