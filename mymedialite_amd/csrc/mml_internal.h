@@ -174,6 +174,10 @@ struct WrmfTilePlan {
     hipStream_t side = nullptr;
     std::vector<hipEvent_t> ev;
     bool residual_ready = false;  // pass 0's R and Rf were computed inside wrmf_tile_solve
+    // HH = H^T H computed on `side` (half_step) while the hot rows' split Gram runs: the solve
+    // waits on hh_done before the HH tiles (nullptr: HH is already on the stream)
+    hipEvent_t hh_start = nullptr, hh_done = nullptr;
+    bool hh_pending = false;
     // the refinement's buffers (factor tiles, x and r in fp64, residual / correction rows): only
     // needed inside one half-step, so both plans of a handle point at ONE workspace (ws)
     struct Refine {
@@ -195,6 +199,9 @@ struct WrmfTilePlan {
 };
 void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p, int64_t r0,
                     int64_t r1, bool woodbury);  // rows [r0, r1) of this rank
+// the plan's second stream (created on first use), or nullptr when `st` is not on the current
+// device (a multi-device context's rank: no second stream)
+hipStream_t wrmf_plan_side(WrmfTilePlan& p, hipStream_t st);
 // rhs == nullptr: W rows <- A^{-1} b (fp32).  rhs (W-shaped, fp32): W rows <- A^{-1} rhs rows,
 // reusing the tables the preceding plain call of the same half-step built.
 void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, int64_t h_rows,

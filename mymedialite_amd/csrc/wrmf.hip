@@ -606,12 +606,38 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
     const int tiles = nt * (nt + 1) / 2;
     const int nparts = h->nparts;
     const int64_t rps = (h_rows + nparts - 1) / nparts;
-    wrmf_gram_partial_kernel<<<dim3(tiles, nparts), 256, 0, st>>>(H, h_rows, k, rps,
+    const bool tiles_path = k > 128 && !use_blocked_solver();
+    // HH = H^T H on the plan's second stream while the hot rows' split Gram runs (it needs H
+    // only), when the half has hot rows and no Woodbury rows (those read HH on the host first)
+    hipStream_t hs = st;
+    mml::WrmfTilePlan* dplan = nullptr;
+    static const bool hh_side = [] {  // MML_WRMF_HH_SIDE=0 (experiments builds): HH on st (A/B)
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_HH_SIDE");
+        return !(e && std::string(e) == "0");
+    }();
+    if (tiles_path && r1 > r0 && hh_side) {
+        mml::WrmfTilePlan& pl = plan_in ? *plan_in : W == h->U.get() ? h->uplan : h->iplan;
+        if (!pl.heavy.empty() && pl.n_wood[0] + pl.n_wood[1] + pl.n_wood[2] + pl.n_wood[3] == 0) {
+            hipStream_t side = mml::wrmf_plan_side(pl, st);
+            if (side) {
+                if (!pl.hh_start) MML_HIP(hipEventCreateWithFlags(&pl.hh_start, hipEventDisableTiming));
+                if (!pl.hh_done) MML_HIP(hipEventCreateWithFlags(&pl.hh_done, hipEventDisableTiming));
+                MML_HIP(hipEventRecord(pl.hh_start, st));  // H is final on st
+                MML_HIP(hipStreamWaitEvent(side, pl.hh_start, 0));
+                hs = side;
+                dplan = &pl;
+            }
+        }
+    }
+    wrmf_gram_partial_kernel<<<dim3(tiles, nparts), 256, 0, hs>>>(H, h_rows, k, rps,
                                                                  h->partial.get());
-    wrmf_gram_reduce_kernel<<<(k * k + 255) / 256, 256, 0, st>>>(h->partial.get(), nparts, k,
+    wrmf_gram_reduce_kernel<<<(k * k + 255) / 256, 256, 0, hs>>>(h->partial.get(), nparts, k,
                                                                   h->HH.get());
     launches += 2;
-    const bool tiles_path = k > 128 && !use_blocked_solver();
+    if (dplan) {
+        MML_HIP(hipEventRecord(dplan->hh_done, hs));
+        dplan->hh_pending = true;
+    }
     if (r1 <= r0) {
         // a rank without rows in this half still joins the ranks' refinement decisions
         if (tiles_path && !plan_in) {

@@ -3113,7 +3113,18 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
     MML_HIP(hipStreamSynchronize(st));
 }
 
+hipStream_t wrmf_plan_side(WrmfTilePlan& p, hipStream_t st) {
+    int dev_cur = -1, dev_st = -1;
+    MML_HIP(hipGetDevice(&dev_cur));
+    MML_HIP(hipStreamGetDevice(st, &dev_st));
+    if (dev_cur != dev_st) return nullptr;
+    if (!p.side) MML_HIP(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
+    return p.side;
+}
+
 WrmfTilePlan::~WrmfTilePlan() {
+    if (hh_start) (void)hipEventDestroy(hh_start);
+    if (hh_done) (void)hipEventDestroy(hh_done);
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
     if (side) (void)hipStreamDestroy(side);
 }
@@ -3360,11 +3371,18 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
     MML_REQUIRE(k > 128 && k <= 256, "tile solver covers 128 < k <= 256");
     const int nt = (k + 31) >> 5, nr = nt + 1;
     const int ntile = nt * nr - nt * (nt - 1) / 2;
-    if (!rhs) {  // a refinement pass reuses the half-step's HHt, L^{-1} and Q
+    // the HH tiles (HHt); when HH is still being computed on the side stream (half_step), after
+    // the first split Gram batch, which does not read them
+    auto hh_tiles = [&]() {
+        if (p.hh_pending) {
+            MML_HIP(hipStreamWaitEvent(st, p.hh_done, 0));
+            p.hh_pending = false;
+        }
         p.hht.alloc((size_t)kTiles * 1024);
         wrmf_tile_hh_kernel<<<(ntile * 1024 + 255) / 256, 256, 0, st>>>(HH, k, reg, p.hht.get());
         ++launches;
-    }
+    };
+    if (!rhs && !p.hh_pending) hh_tiles();  // a refinement pass reuses the half-step's tables
     const int grid_cap = 256 * 2;  // 256 CUs; a second resident workgroup where registers allow
     const int64_t nh = (int64_t)p.heavy.size();
     const size_t tile_floats = (size_t)kTiles * 1024;
@@ -3446,6 +3464,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             gk<<<gg, kThreads, 0, st>>>(
                 reinterpret_cast<const Seg*>(p.segs.get()) + s0, (int32_t)(s1 - s0), (int32_t)h0,
                 cols, H, k, p.gram.get(), P, ps, (int32_t)h_rows);
+            if (!rhs && p.hh_pending) hh_tiles();
             MML_HIP(hipMemsetAsync(p.counter.get(), 0, sizeof(int32_t), st));
             const int gs = (int)std::min<int64_t>(h1 - h0, grid_cap);
             wrmf_tile_solve_kernel<0><<<gs, kThreads, 0, st>>>(
@@ -3455,6 +3474,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             MML_HIP(hipGetLastError());
             launches += 2;
         }
+        if (!rhs && p.hh_pending) hh_tiles();  // no hot rows: HH before the light rows
         auto sk = P ? &wrmf_tile_solve_kernel<0, true> : &wrmf_tile_solve_kernel<0, false>;
         auto solve_light = [&](int64_t l0, int64_t l1) {  // light-list slice [l0, l1)
             if (l1 <= l0) return;
