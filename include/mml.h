@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 10
+#define MML_ABI_VERSION 11
 
 typedef int32_t mml_status;
 enum {
@@ -550,6 +550,13 @@ mml_status mml_wrmf_last_timing(mml_wrmf* h, float* out);
 /* Device time of the last mml_wrmf_iterate's two row-shard all-gathers (ABI 10; U after the user
  * half, V after the item half; the slowest shard on a multi-device context); 0 on one rank. */
 mml_status mml_wrmf_last_allgather_ms(mml_wrmf* h, float* out);
+/* The item half's pipeline (ABI 11; 128 < k <= 256, fp64 mode): the direct rows of a half-step with
+ * no Woodbury rows are solved in `ranges` contiguous row ranges, and range b's first refinement
+ * residual runs on a second stream under range b + 1's solve; HH of such a half is computed on that
+ * stream under the hot rows' split Gram.  The model is the serial path's bit for bit.  ranges = 0
+ * (default): 4 ranges where a half has >= 4 x 4,096 direct rows; 1: off; 2 .. 16: that many.  Takes
+ * effect at the next mml_wrmf_iterate. */
+mml_status mml_wrmf_set_pipeline(mml_wrmf* h, int32_t ranges);
 /* The most refinement passes a half-step of the last mml_wrmf_iterate ran (ABI 6);
  * corrections (nullable, [8]): per half-step (users 0..3, items 4..7) and pass, the largest
  * correction relative to 1 + |x| that decided whether another pass ran (0: not read back). */

@@ -155,6 +155,7 @@ SIGNATURES = {
     "mml_bmf_last_phases": (_st, [_vp, ctypes.POINTER(ctypes.c_int32)]),
     "mml_bpr_replay_traffic": (_st, [_vp, _f32p]),
     "mml_wrmf_last_allgather_ms": (_st, [_vp, _f32p]),
+    "mml_wrmf_set_pipeline": (_st, [_vp, ctypes.c_int32]),
     "mml_bmf_set_implicit_feedback": (_st, [_vp, ctypes.c_int32, ctypes.c_int32, _i64p, _i32p,
                                             _f32p, _f32p]),
     "mml_bmf_get_implicit_factors": (_st, [_vp, ctypes.c_int32, _f32p]),

@@ -197,8 +197,9 @@ struct WrmfTilePlan {
     WrmfTilePlan& operator=(const WrmfTilePlan&) = delete;
     ~WrmfTilePlan();
 };
+// pipe: the item half's pipeline ranges (0: the library's default, 1: off)
 void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p, int64_t r0,
-                    int64_t r1, bool woodbury);  // rows [r0, r1) of this rank
+                    int64_t r1, bool woodbury, int32_t pipe = 0);  // rows [r0, r1) of this rank
 // the plan's second stream (created on first use), or nullptr when `st` is not on the current
 // device (a multi-device context's rank: no second stream)
 hipStream_t wrmf_plan_side(WrmfTilePlan& p, hipStream_t st);

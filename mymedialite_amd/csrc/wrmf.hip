@@ -542,6 +542,9 @@ struct mml_wrmf {
     float last_corr[8] = {};  // per half-step (users, items) and pass: the max relative correction
     int32_t nparts = 1;
     int64_t nnz = 0;
+    // the item half's pipeline (mml_wrmf_set_pipeline): 0 = the default row ranges, 1 = off (the
+    // residual after the whole solve, HH on the handle's stream), n = n ranges
+    int32_t pipe_req = 0;
     mml::DeviceArray<uint8_t> hhp;  // HH + reg I, block-packed (k > 64 path)
     mml::WrmfTilePlan uplan, iplan;  // k > 128: matrix-core row solves (wrmf_tiles.hip)
     // row shards (one process per GPU): rank r solves rows [ub[r], ub[r+1]) of U and
@@ -615,7 +618,7 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
         const char* e = MML_EXPERIMENT_ENV("MML_WRMF_HH_SIDE");
         return !(e && std::string(e) == "0");
     }();
-    if (tiles_path && r1 > r0 && hh_side) {
+    if (tiles_path && r1 > r0 && hh_side && h->pipe_req != 1) {
         mml::WrmfTilePlan& pl = plan_in ? *plan_in : W == h->U.get() ? h->uplan : h->iplan;
         if (!pl.heavy.empty() && pl.n_wood[0] + pl.n_wood[1] + pl.n_wood[2] + pl.n_wood[3] == 0) {
             hipStream_t side = mml::wrmf_plan_side(pl, st);
@@ -702,8 +705,10 @@ void ensure_shards(mml_wrmf* h) {
         // the half-steps run one after another on one stream: one refinement workspace for both
         h->iplan.ws = &h->uplan.own;
         const bool wood = h->p.alpha > 0.0 && !no_woodbury();
-        mml::wrmf_tile_plan(h->udeg, h->ctx->stream, h->uplan, h->ub[rk], h->ub[rk + 1], wood);
-        mml::wrmf_tile_plan(h->ideg, h->ctx->stream, h->iplan, h->ib[rk], h->ib[rk + 1], wood);
+        mml::wrmf_tile_plan(h->udeg, h->ctx->stream, h->uplan, h->ub[rk], h->ub[rk + 1], wood,
+                            h->pipe_req);
+        mml::wrmf_tile_plan(h->ideg, h->ctx->stream, h->iplan, h->ib[rk], h->ib[rk + 1], wood,
+                            h->pipe_req);
     }
     h->shard_nranks = nr;
     h->shard_rank = rk;
@@ -1063,7 +1068,8 @@ extern "C" mml_status mml_wrmf_retrain(mml_wrmf* h, int32_t side, int32_t n_rows
         const int64_t h_rows = side == 0 ? h->n_items : h->n_users;
         mml::WrmfTilePlan plan;
         if (h->k > 128)
-            mml::wrmf_tile_plan(deg, st, plan, 0, n_rows, h->p.alpha > 0.0 && !no_woodbury());
+            mml::wrmf_tile_plan(deg, st, plan, 0, n_rows, h->p.alpha > 0.0 && !no_woodbury(),
+                                h->pipe_req);
         int launches = 0;
         h->last_refine = 0;
         std::fill(h->last_corr, h->last_corr + 8, 0.0f);
@@ -1081,6 +1087,21 @@ extern "C" mml_status mml_wrmf_last_allgather_ms(mml_wrmf* h, float* out) {
         MML_REQUIRE(h && out, "null argument");
         *out = h->last_gather_ms;
         for (mml_wrmf* s : h->shards) *out = std::max(*out, s->last_gather_ms);
+    });
+}
+
+extern "C" mml_status mml_wrmf_set_pipeline(mml_wrmf* h, int32_t ranges) {
+    return guard([&] {
+        MML_REQUIRE(h, "null argument");
+        MML_REQUIRE(ranges >= 0 && ranges <= 16, "pipeline ranges: 0 (default), 1 (off) .. 16");
+        h->pipe_req = ranges;
+        h->shard_nranks = 0;  // the row plans are rebuilt at the next iterate
+        h->shard_rank = -1;
+        for (mml_wrmf* s : h->shards) {
+            s->pipe_req = ranges;
+            s->shard_nranks = 0;
+            s->shard_rank = -1;
+        }
     });
 }
 

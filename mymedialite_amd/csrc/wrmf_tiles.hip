@@ -2975,7 +2975,7 @@ constexpr int64_t kGramBatchBytes = (int64_t)1 << 30;
 namespace mml {
 
 void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePlan& p, int64_t r0,
-                    int64_t r1, bool woodbury) {
+                    int64_t r1, bool woodbury, int32_t pipe) {
     const int32_t n = (int32_t)deg.size();
     p.woodbury = woodbury;
     // light rows by degree, descending (longest first: the work queue then ends on short rows)
@@ -3002,7 +3002,7 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
     // after the light rows' and whose W every range's residual would need
     size_t n_wood_rows = 0;
     for (auto& w : wood) n_wood_rows += w.size();
-    const int32_t want = pipe_batches();
+    const int32_t want = pipe > 0 ? std::min(16, pipe) : pipe_batches();
     p.nbatch = 1;
     p.b_row.assign({0, r1 - r0});
     if (want > 1 && n_wood_rows == 0 && (int64_t)light.size() >= (int64_t)want * 4096) {

@@ -260,3 +260,39 @@ def test_wrmf_fp64_lands_on_exact_product_solution(case, k, alpha, iters):
     # the refinement ran until its correction was below the per-row-type stop (wrmf_tiles.hip
     # kRefineStopDirect / kRefineStopWood)
     assert 1 <= ran.value <= 3
+
+
+def test_wrmf_item_pipeline_equals_serial_bit_for_bit():
+    """The item half's pipeline (mml_wrmf_set_pipeline, ABI 11): range b's first-pass residual on a
+    second stream under range b + 1's solve, the dense term added after, HH under the hot rows'
+    split Gram -- the serial path's model bit for bit.  400 k users x 40 k
+    items, 40 M events (items Zipf(0.8): no Woodbury item rows, hot items above 8,192 entries),
+    k = 256, fp64 mode, 2 iterations; serial (1), the default (0: 4 ranges) and 7 ranges."""
+    import ctypes
+    import torch
+    from mymedialite_amd import _native as N
+    from mymedialite_amd.synthetic import c5_events
+    nu, ni, k = 400_000, 40_000, 256
+    users, items = c5_events(nu, ni, 100, torch.device("cuda:0"))
+    n = int(users.numel())
+    out = {}
+    for ranges in (1, 0, 7):
+        ctx = N.Context(0)
+        p = N.WrmfParams(k, 1, 1.0, 0.015)
+        h = N._vp()
+        N.check(N.lib().mml_wrmf_create(ctx.handle, ctypes.byref(p), nu, ni, ctypes.byref(h)))
+        N.check(N.lib().mml_wrmf_set_pipeline(h, ranges))
+        N.check(N.lib().mml_wrmf_set_data_device(h, users.data_ptr(), items.data_ptr(), n))
+        N.check(N.lib().mml_wrmf_init_model(h, 5, 0.0, 0.1))
+        for _ in range(2):
+            N.check(N.lib().mml_wrmf_iterate(h))
+        U = np.empty((nu, k), np.float32)
+        V = np.empty((ni, k), np.float32)
+        N.check(N.lib().mml_wrmf_get_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p)))
+        N.lib().mml_wrmf_destroy(h)
+        ctx.close()
+        out[ranges] = (U, V)
+        print(f"pipeline ranges {ranges}: |V| {np.abs(V).max():.4g}", flush=True)
+    for ranges in (0, 7):
+        np.testing.assert_array_equal(out[1][0].view(np.uint32), out[ranges][0].view(np.uint32))
+        np.testing.assert_array_equal(out[1][1].view(np.uint32), out[ranges][1].view(np.uint32))
