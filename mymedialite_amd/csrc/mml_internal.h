@@ -174,6 +174,7 @@ struct WrmfTilePlan {
     hipStream_t side = nullptr;
     std::vector<hipEvent_t> ev;
     bool residual_ready = false;  // pass 0's R and Rf were computed inside wrmf_tile_solve
+    bool light_corr_ready = false;  // and the light rows' pass-0 corrections (df) too
     // HH = H^T H computed on `side` (half_step) while the hot rows' split Gram runs: the solve
     // waits on hh_done before the HH tiles (nullptr: HH is already on the stream)
     hipEvent_t hh_start = nullptr, hh_done = nullptr;

@@ -1317,7 +1317,9 @@ __device__ __forceinline__ void wave_sync() {
 }
 // backward_only: rhs holds y = L^{-1} b already (the main solve's forward result, deferred here
 // from wrmf_tile_solve_kernel), and may alias W: the wave reads its row into LDS before writing.
-__global__ __launch_bounds__(64 * kRvWaves) void wrmf_tile_resolve_wave_kernel(
+// (five waves per SIMD, <= 96 VGPRs: a wave per SIMD fits beside the tile solve's two when the
+// item half's pipeline runs a range's correction under the next range's solve)
+__global__ __launch_bounds__(64 * kRvWaves, 5) void wrmf_tile_resolve_wave_kernel(
     const int32_t* __restrict__ rows, int32_t n_list, const int64_t* __restrict__ off,
     const float* __restrict__ F, const float* rhs, int32_t k, float* W, int32_t backward_only) {
     __shared__ RvSmem smem[kRvWaves];
@@ -2705,7 +2707,7 @@ template <typename XT, bool VEC>
 __global__ __launch_bounds__(256, 5) void wrmf_resid_seg_kernel(
     const RSeg* __restrict__ segs, int64_t nseg, const int32_t* __restrict__ cols,
     const float* __restrict__ H, int32_t k, const XT* __restrict__ X, double alpha,
-    double* __restrict__ R, double* __restrict__ partial, int set) {
+    double* __restrict__ R, double* __restrict__ partial) {
     static_assert(kResE == 8, "the butterfly below reduces 8 entries");
     const int lane = threadIdx.x & 63, f0 = 4 * lane;
     const int64_t wave0 =
@@ -2783,7 +2785,7 @@ __global__ __launch_bounds__(256, 5) void wrmf_resid_seg_kernel(
             const int f = f0 + j;
             if (f < k) {
                 if (sg.slot < 0)
-                    R[(int64_t)sg.row * k + f] = set ? acc[j] : R[(int64_t)sg.row * k + f] + acc[j];
+                    R[(int64_t)sg.row * k + f] += acc[j];
                 else
                     partial[(int64_t)sg.slot * k + f] = acc[j];
             }
@@ -2795,13 +2797,13 @@ __global__ __launch_bounds__(256, 5) void wrmf_resid_seg_kernel(
 __global__ __launch_bounds__(256) void wrmf_resid_multi_kernel(const RMulti* __restrict__ m,
                                                                int64_t n, int32_t k,
                                                                const double* __restrict__ partial,
-                                                               double* __restrict__ R, int set) {
+                                                               double* __restrict__ R) {
     for (int64_t x = blockIdx.x; x < n; x += gridDim.x) {
         const RMulti r = m[x];
         for (int f = threadIdx.x; f < k; f += blockDim.x) {
             double v = 0.0;
             for (int s = 0; s < r.nslot; ++s) v += partial[(int64_t)(r.slot0 + s) * k + f];
-            R[(int64_t)r.row * k + f] = set ? v : R[(int64_t)r.row * k + f] + v;
+            R[(int64_t)r.row * k + f] += v;
         }
     }
 }
@@ -3132,10 +3134,10 @@ WrmfTilePlan::~WrmfTilePlan() {
 // the first refinement pass's residual over local rows [lr0, lr1) of a plan (its entry segments
 // [sg0, sg1) and multi-segment rows [m0, m1), which the plan keeps in row order): R = -X (HH + reg I)
 // with x = the fp32 W rows widened on load, + sum_i c_i h_i, then Rf = (float) R.
-// part 1: the dense term first (it sets R), then the data term added; part 2 (the pipeline, on the
-// side stream): the data term only, setting R (R was zeroed, so rows without entries read 0);
-// part 3 (after the pipeline): the dense term added, then Rf.  a + b = b + a in IEEE arithmetic, so
-// both orders give every R bit for bit.
+// part 1: the dense term (it sets R), then the data term added, then Rf.  The pipeline splits it:
+// part 4 (the handle's stream, right after the range's solve): the dense term added to R = 0;
+// part 2 (the side stream): the data term added, then Rf.  0 + t = t, so R is part 1's bit for bit
+// (a -0 dense term becomes +0: the same correction and W).
 static void first_residual(hipStream_t s, WrmfTilePlan& p, float* W, const float* H,
                            const int32_t* cols, const double* HH, int32_t k, double alpha,
                            double reg, int64_t lr0, int64_t lr1, int64_t sg0, int64_t sg1,
@@ -3150,8 +3152,12 @@ static void first_residual(hipStream_t s, WrmfTilePlan& p, float* W, const float
         ++launches;
     };
     if (part == 1) dense(0);
-    if (part != 3) {
-        const int set = part == 2;
+    if (part == 4) {
+        dense(1);
+        MML_HIP(hipGetLastError());
+        return;
+    }
+    {
         if (sg1 > sg0) {
             const int gs = (int)std::min<int64_t>((sg1 - sg0 + 3) / 4, grid_cap);  // 4 waves
             const RSeg* sg = reinterpret_cast<const RSeg*>(p.rsegs.get()) + sg0;
@@ -3159,21 +3165,16 @@ static void first_residual(hipStream_t s, WrmfTilePlan& p, float* W, const float
             (((k & 3) == 0) ? &wrmf_resid_seg_kernel<float, true>
                             : &wrmf_resid_seg_kernel<float, false>)<<<gs, 256, 0, s>>>(
                 sg, sg1 - sg0, cols, H, k, W + p.r0 * (int64_t)k, alpha, p.ws->r64.get(),
-                p.ws->rpartial.get(), set);
+                p.ws->rpartial.get());
             ++launches;
         }
         if (m1 > m0) {
             wrmf_resid_multi_kernel<<<(int)std::min<int64_t>(m1 - m0, 8192), 256, 0, s>>>(
                 reinterpret_cast<const RMulti*>(p.rmulti.get()) + m0, m1 - m0, k,
-                p.ws->rpartial.get(), p.ws->r64.get(), set);
+                p.ws->rpartial.get(), p.ws->r64.get());
             ++launches;
         }
     }
-    if (part == 2) {
-        MML_HIP(hipGetLastError());
-        return;
-    }
-    if (part == 3) dense(1);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, 16384));
     wrmf_refine_rows_kernel<<<grid, 256, 0, s>>>(1, p.r0 + lr0, n, k, W, nullptr, r,
                                                  p.ws->rf.get(), nullptr, nullptr, 0, nullptr);
@@ -3259,12 +3260,12 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
                 (((k & 3) == 0) ? &wrmf_resid_seg_kernel<double, true>
                                 : &wrmf_resid_seg_kernel<double, false>)<<<gs, 256, 0, st>>>(
                     sg, p.n_rsegs, cols, H, k, p.ws->x64.get(), alpha, p.ws->r64.get(),
-                    p.ws->rpartial.get(), 0);
+                    p.ws->rpartial.get());
             }
             if (p.n_rmulti > 0)
                 wrmf_resid_multi_kernel<<<(int)std::min<int64_t>(p.n_rmulti, 8192), 256, 0, st>>>(
                     reinterpret_cast<const RMulti*>(p.rmulti.get()), p.n_rmulti, k,
-                    p.ws->rpartial.get(), p.ws->r64.get(), 0);
+                    p.ws->rpartial.get(), p.ws->r64.get());
             MML_HIP(hipGetLastError());
             rows(1);
         }
@@ -3406,7 +3407,10 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             ++launches;
         };
         resolve(p.heavy_dev.get(), nh, p.ws->factor.get() + (size_t)p.n_light * tile_floats);
-        resolve(p.light.get(), p.n_light, p.ws->factor.get());
+        if (p.light_corr_ready && W == p.ws->df.get() && rhs == p.ws->rf.get())
+            p.light_corr_ready = false;  // the pipeline already solved them (wrmf_tile_solve)
+        else
+            resolve(p.light.get(), p.n_light, p.ws->factor.get());
         MML_HIP(hipGetLastError());
     } else {
         // the factors of the direct rows, kept when refinement passes follow (fp64 mode)
@@ -3518,24 +3522,37 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             p.ws->r64.reserve((size_t)n * k);  // the sizes wrmf_tile_refine reserves
             p.ws->rf.reserve((size_t)p.r1 * k);
             p.ws->rpartial.reserve(std::max<int64_t>(1, p.n_rslots) * (size_t)k);
+            p.ws->df.reserve((size_t)p.r1 * k);
             MML_HIP(hipMemsetAsync(p.ws->r64.get(), 0, sizeof(double) * (size_t)n * k, st));
             back(p.heavy_dev.get(), nh, F + (size_t)p.n_light * tile_floats);
             for (int b = 0; b < p.nbatch; ++b) {
-                solve_light(p.b_light[b], p.b_light[b + 1]);
-                back(p.light.get() + p.b_light[b], p.b_light[b + 1] - p.b_light[b],
-                     F + (size_t)p.b_light[b] * tile_floats);
+                const int64_t l0 = p.b_light[b], l1 = p.b_light[b + 1];
+                solve_light(l0, l1);
+                back(p.light.get() + l0, l1 - l0, F + (size_t)l0 * tile_floats);
+                // the dense term on this stream (the fp64 MFMA kernel takes whole SIMDs), between
+                // the ranges' solves
+                first_residual(st, p, W, H, cols, HH, k, alpha, reg, p.b_row[b], p.b_row[b + 1],
+                               0, 0, 0, 0, 8192, launches, 4);
                 MML_HIP(hipEventRecord(p.ev[b], st));
                 MML_HIP(hipStreamWaitEvent(p.side, p.ev[b], 0));
+                // the data term, Rf, and the range's light rows' corrections on their kept
+                // factors, beside range b + 1's solve
                 first_residual(p.side, p, W, H, cols, HH, k, alpha, reg, p.b_row[b],
                                p.b_row[b + 1], p.b_seg[b], p.b_seg[b + 1], p.b_multi[b],
                                p.b_multi[b + 1], pipe_grid(), launches, 2);
+                if (l1 > l0) {
+                    const int64_t blocks =
+                        std::min<int64_t>((l1 - l0 + kRvWaves - 1) / kRvWaves, 256 * 16);
+                    wrmf_tile_resolve_wave_kernel<<<(int)blocks, 64 * kRvWaves, 0, p.side>>>(
+                        p.light.get() + l0, (int32_t)(l1 - l0), off, F + (size_t)l0 * tile_floats,
+                        p.ws->rf.get(), k, p.ws->df.get(), 0);
+                    ++launches;
+                }
             }
             MML_HIP(hipEventRecord(p.ev[p.nbatch], p.side));
             MML_HIP(hipStreamWaitEvent(st, p.ev[p.nbatch], 0));
-            // the dense term (the fp64 MFMA kernel takes whole SIMDs: not beside the solve)
-            first_residual(st, p, W, H, cols, HH, k, alpha, reg, 0, n, 0, 0, 0, 0, 8192, launches,
-                           3);
             p.residual_ready = true;
+            p.light_corr_ready = true;
         } else {
             solve_light(0, p.n_light);
             if (F) {
