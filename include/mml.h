@@ -228,7 +228,8 @@ mml_status mml_bmf_destroy(mml_bmf* h);
  * NULL = identity.  The device keeps the ratings permuted into visit order (coalesced stream). */
 mml_status mml_bmf_set_data(mml_bmf* h, const int32_t* users, const int32_t* items,
                             const float* values, int64_t n, const int32_t* order);
-/* Same, from arrays already resident in this context's HBM (device pointers). */
+/* Same, from arrays already resident in this context's HBM (device pointers).  The call first waits
+ * for the work queued on the device, so the arrays may be produced on any stream. */
 mml_status mml_bmf_set_data_device(mml_bmf* h, const int32_t* users_device,
                                    const int32_t* items_device, const float* values_device,
                                    int64_t n, const int32_t* order_device);

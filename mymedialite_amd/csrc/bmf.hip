@@ -2948,6 +2948,9 @@ extern "C" mml_status mml_bmf_set_data_device(mml_bmf* h, const int32_t* users,
         check_handle(h);
         MML_REQUIRE(n >= 0 && n <= INT32_MAX, "rating count out of range");
         MML_REQUIRE(n == 0 || (users && items && values), "null rating arrays");
+        // the arrays may come from any stream of the caller's (e.g. torch's): wait for the device
+        h->ctx->activate();
+        MML_HIP(hipDeviceSynchronize());
         if (h->ctx->multi()) return multi_set_data_device(h, users, items, values, n, order);
         // a ring rank: every rank gets the newest model before the groups are forgotten (as
         // mml_bmf_set_data)

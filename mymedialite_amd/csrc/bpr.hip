@@ -1153,6 +1153,9 @@ extern "C" mml_status mml_bpr_set_data_device(mml_bpr* h, const int32_t* users,
     return guard([&] {
         MML_REQUIRE(h && h->ctx, "null handle");
         MML_REQUIRE(n >= 1 && users && items, "need >= 1 event");
+        // the arrays may come from any stream of the caller's (e.g. torch's): wait for the device
+        h->ctx->activate();
+        MML_HIP(hipDeviceSynchronize());
         MML_REQUIRE(!order || (h->p.sampler != MML_BPR_SAMPLER_UNIFORM_USER &&
                                h->p.sampler != MML_BPR_SAMPLER_USER_REPLACEMENT),
                     "a device order is not used by the user-sampling samplers");

@@ -847,6 +847,8 @@ extern "C" mml_status mml_wrmf_set_data_device(mml_wrmf* h, const int32_t* users
         MML_REQUIRE(!h->ctx->multi(), "a multi-device context takes host arrays (set_data)");
         MML_REQUIRE(n >= 0 && (n == 0 || (users && items)), "bad event arrays");
         h->ctx->activate();
+        // the arrays may come from any stream of the caller's (e.g. torch's): wait for the device
+        MML_HIP(hipDeviceSynchronize());
         hipStream_t st = h->ctx->stream;
         h->has_data = false;
         mml::DeviceCsr ucsr, icsr;

@@ -34,6 +34,7 @@ def save(dst, nu=400_000, ni=40_000, per_user=100, k=256, iters=2):
     dev = torch.device("cuda:0")
     users, items = c5_events(nu, ni, per_user, dev)
     n = int(users.numel())
+    torch.cuda.synchronize()  # generated on torch's stream; the library reads on its own
     ctx = N.Context(0)
     p = N.WrmfParams(k, 1, 1.0, 0.015)
     h = N._vp()
