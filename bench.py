@@ -90,6 +90,9 @@ def main():
     ap.add_argument("--phases", type=int, default=0,
                     help="user phases of the Hogwild epochs (mml_bmf_set_hogwild_phases / "
                          "mml_bpr_set_hogwild_phases): 0 = the library's default, 1 = none")
+    ap.add_argument("--bpr-prefetch", type=int, default=1, choices=[0, 1],
+                    help="C3: draw each next epoch's triples beside the update "
+                         "(mml_bpr_set_next_seed); 0 = sample at the start of each epoch")
     ap.add_argument("--no-extras", action="store_true",
                     help="N = 1 default run: the C4 line only (no c2 / c3 / c5 keys)")
     args = ap.parse_args()
@@ -618,21 +621,29 @@ def bench_bpr(args):
     N.check(N.lib().mml_bpr_init_model(h, 2, 0.0, 0.1))  # same seed: V identical on every rank
     timing = np.zeros(2, np.float32)
 
-    def step(seed):
-        N.check(N.lib().mml_bpr_iterate(h, seed))
+    # every epoch's seed; with the prefetch, epoch e draws epoch e + 1's triples beside its update
+    # (mml_bpr_set_next_seed), the last timed epoch included (seeds[-1]): each timed step holds
+    # one epoch's sampling, the first timed epoch's having been drawn by the last warmup epoch
+    seeds = ([1000 + 97 * w + rank for w in range(args.warmup)] +
+             [2000 + 97 * s_ + rank for s_ in range(args.steps)] + [3000 + rank])
+
+    def step(x):
+        if args.bpr_prefetch:
+            N.check(N.lib().mml_bpr_set_next_seed(h, ctypes.c_uint64(seeds[x + 1])))
+        N.check(N.lib().mml_bpr_iterate(h, seeds[x]))
         N.lib().mml_bpr_last_timing(h, N.ptr(timing, N._f32p))
         if world > 1:  # stream-ordered ncclAvg: the next epoch's kernels queue behind it
             N.check(N.lib().mml_bpr_allreduce_items(h))
 
     for w in range(args.warmup):
-        step(1000 + 97 * w + rank)
+        step(w)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     ms, ums = [], []
     t0 = time.perf_counter()
     for st_ in range(args.steps):
-        step(2000 + 97 * st_ + rank)
+        step(args.warmup + st_)
         ms.append(float(timing[0]))
         ums.append(float(timing[1]))
     torch.cuda.synchronize()
@@ -693,16 +704,21 @@ def bench_bpr(args):
                      "kernel_avg_ms": upd_ms, "bytes_per_update": bpu,
                      "epoch_device_ms": avg_ms,
                      "sampler_ms": avg_ms - upd_ms,
+                     "sampler_prefetched": bool(args.bpr_prefetch),
                      # the sampler + XCD partition's own algorithmic bytes per triple: the user's
                      # 64-B record line (row start, |S_u|, Bloom filter), one 4-B column (i), the
                      # triple and its group byte written (13), the partition's count read (1),
                      # scatter read (13) and write (12)
                      "sampler_bytes_per_triple": SAMPLER_BYTES,
-                     "sampler_GBps": n * SAMPLER_BYTES / max(1e-9, (avg_ms - upd_ms) * 1e-3) / 1e9,
+                     "sampler_GBps": None if args.bpr_prefetch else
+                     n * SAMPLER_BYTES / max(1e-9, (avg_ms - upd_ms) * 1e-3) / 1e9,
                      "frac_epoch": n * bpu / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "frac_note": "frac = the update kernel alone; frac_epoch = the same bytes "
                                   "over the whole device epoch (sampler + XCD partition + "
-                                  "update)",
+                                  "update; with sampler_prefetched the next epoch's sampler and "
+                                  "partition run beside the update on a second stream and the "
+                                  "epoch ends when both are done, sampler_ms = the part the "
+                                  "update did not cover)",
                      "box_ceiling": ceiling,
                      "frac_of_box_ceiling": ceiling["frac_of_box_ceiling"]},
         "allreduce_ms": float(ar[0]) if world > 1 else None,

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 11
+#define MML_ABI_VERSION 12
 
 typedef int32_t mml_status;
 enum {
@@ -432,6 +432,14 @@ mml_status mml_bpr_init_model(mml_bpr* h, uint64_t seed, double mean, double std
 /* One epoch = BPRMF.Iterate() (:160-178): Feedback.Count sampled triples, each followed by
  * UpdateFactors (:330-374).  seed keys the counter-based sampler (e.g. drawn from the host RNG). */
 mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed);
+/* The seed the NEXT mml_bpr_iterate will be called with (ABI 12).  The following mml_bpr_iterate
+ * then draws that epoch's triples on a second stream beside its own update (the triples depend on
+ * the seed and the data only, not on the model), and the epoch after it starts at its update.
+ * The same triples either way: an iterate with another seed draws its own.  One-shot; applies to
+ * the partitioned HOGWILD epoch without user phases (not WEIGHTED, not USER_REPLACEMENT); costs a
+ * second set of triple buffers (28 bytes per event).  A multi-device handle passes seed + d x
+ * 0x9E3779B97F4A7C15 to device d, as mml_bpr_iterate does. */
+mml_status mml_bpr_set_next_seed(mml_bpr* h, uint64_t seed);
 /* UpdateFactors(u[x], i[x], j[x], true, true, UpdateJ) for x = 0 .. n-1 strictly in order, with
  * the reference's arithmetic and summation order (bit-faithful to the managed loop): the exact
  * path for a host that draws its own triples (e.g. the C# SampleTriple on System.Random). */
@@ -453,7 +461,8 @@ mml_status mml_bpr_set_rows(mml_bpr* h, int32_t side, int32_t n_rows, const int3
 mml_status mml_bpr_predict(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t n,
                            float* out);
 /* out[0] = the last epoch's device time (ms), out[1] = its update kernel alone (the rest is the
- * triple sampler) */
+ * triple sampler; with mml_bpr_set_next_seed, the part of the next epoch's sampling that the
+ * update did not cover) */
 mml_status mml_bpr_last_timing(mml_bpr* h, float* out);
 /* Device time of the last item average (ABI 10): mml_bpr_allreduce_items on a communicator, or the
  * peer-copy average inside a repeated-device mml_bpr_iterate; waits for it; 0 when none ran. */

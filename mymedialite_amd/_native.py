@@ -142,6 +142,7 @@ SIGNATURES = {
     "mml_bpr_get_model": (_st, [_vp, _f32p, _f32p, _f32p]),
     "mml_bpr_init_model": (_st, [_vp, ctypes.c_uint64, ctypes.c_double, ctypes.c_double]),
     "mml_bpr_iterate": (_st, [_vp, ctypes.c_uint64]),
+    "mml_bpr_set_next_seed": (_st, [_vp, ctypes.c_uint64]),
     "mml_bpr_predict": (_st, [_vp, _i32p, _i32p, ctypes.c_int64, _f32p]),
     "mml_bpr_apply_triples": (_st, [_vp, _i32p, _i32p, _i32p, ctypes.c_int64]),
     "mml_bpr_last_timing": (_st, [_vp, _f32p]),

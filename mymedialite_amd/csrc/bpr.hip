@@ -736,6 +736,14 @@ inline int lanes_per_row(int k) {
     return lpr;
 }
 
+// one epoch's triples: as sampled (u, i, j and the group byte of i), partitioned by that group
+// (xu, xi, xj) and the partition's 9 group offsets
+struct BprTriples {
+    mml::DeviceArray<int32_t> u, i, j, xu, xi, xj;
+    mml::DeviceArray<uint8_t> g;
+    mml::DeviceArray<int64_t> goff;
+};
+
 }  // namespace
 
 struct mml_bpr {
@@ -746,17 +754,25 @@ struct mml_bpr {
     mml::DeviceArray<float> U, V, bias, ev_out;
     mml::DeviceArray<int64_t> off;
     mml::DeviceArray<int32_t> cols, eligible, ev_u, ev_i, q_u, q_i;
-    mml::DeviceArray<int32_t> tri_u, tri_i, tri_j;  // the epoch's triples (two-phase epoch)
+    // the epoch's triples (two-phase epoch) in two sets, so that the next epoch's can be drawn
+    // beside this epoch's update (mml_bpr_set_next_seed); cur = the last epoch's set
+    BprTriples tb[2];
+    int32_t cur = 0;
+    // the draw ahead: its stream and events, the seed it was asked for, the set that holds it
+    hipStream_t side = nullptr;
+    hipEvent_t ev_pf_go = nullptr, ev_pf_done = nullptr, ev_upd = nullptr;
+    bool next_seed_set = false, pf_ready = false, last_prefetched = false;
+    uint64_t next_seed = 0, pf_seed = 0;
+    int64_t pf_n = -1;
+    int32_t pf_buf = 0;
     mml::DeviceArray<int32_t> fail;                 // WEIGHTED sampler: a sample ran out of draws
     mml::DeviceArray<uint32_t> recs;                // per-user sampler records (row, |S_u|, Bloom)
     mml::DeviceArray<uint64_t> rank_keys, rank_sorted;  // USER_REPLACEMENT: (u << 32 | s)
     mml::DeviceArray<int64_t> rank_head;                // USER_REPLACEMENT: first position per user
     mml::DeviceArray<uint8_t> rank_tmp;                 // its radix-sort scratch
     // Hogwild on XCD-owned item groups (xcd.hip): the epoch's triples partitioned by the group of
-    // i (stable), xt_* = the partitioned copy; span1 = {0, n} for the one-span launch
+    // i (stable, into the set's xu / xi / xj); span1 = {0, n} for the one-span launch
     mml::XcdSplit xs;
-    mml::DeviceArray<int32_t> xt_u, xt_i, xt_j;
-    mml::DeviceArray<uint8_t> tri_g;  // the XCD group of each triple's i, written by the sampler
     mml::DeviceArray<int64_t> span1;
     bool has_groups = false;
     // multi-device context: one single-device handle per GPU over a user range ub[d] .. ub[d + 1]
@@ -766,7 +782,7 @@ struct mml_bpr {
     mml::DeviceArray<float> avg_stage;
     hipEvent_t ev_ar0 = nullptr, ev_ar1 = nullptr;
     bool has_ar = false;  // ev_ar0 / ev_ar1 bracket the last item average
-    // the last Hogwild update launch, for mml_bpr_replay_traffic (its triples stay in tri_* / xt_*
+    // the last Hogwild update launch, for mml_bpr_replay_traffic (its triples stay in tb[cur]
     // until the next epoch)
     struct {
         bool valid = false, soft = false;
@@ -924,6 +940,13 @@ extern "C" mml_status mml_bpr_destroy(mml_bpr* h) {
             (void)hipEventDestroy(h->ev_ar0);
             (void)hipEventDestroy(h->ev_ar1);
         }
+        if (h->side) {
+            (void)hipStreamSynchronize(h->side);
+            (void)hipStreamDestroy(h->side);
+            (void)hipEventDestroy(h->ev_pf_go);
+            (void)hipEventDestroy(h->ev_pf_done);
+            (void)hipEventDestroy(h->ev_upd);
+        }
         delete h;
     });
 }
@@ -973,6 +996,7 @@ void bpr_ingest(mml_bpr* h, const int32_t* users, const int32_t* items, int64_t 
     MML_REQUIRE(h->p.sampler != MML_BPR_SAMPLER_USER_REPLACEMENT || n <= (int64_t)UINT32_MAX,
                 "USER_REPLACEMENT ranks samples with 32-bit indices: at most 2^32 - 1 events");
     h->has_triples = false;
+    h->pf_ready = false;  // triples drawn ahead belong to the old data
     h->has_groups = false;
     h->span1.alloc(2);
     const int64_t span[2] = {0, n};
@@ -1626,22 +1650,15 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             h->xs.set_groups(st, mml::device_id_counts(st, h->cols.get(), h->nnz, h->n_items), 8);
             h->has_groups = true;
         }
-        if (!fused && n > 0 && (int64_t)h->tri_u.count < n) {
-            h->tri_u.alloc(n);
-            h->tri_i.alloc(n);
-            h->tri_j.alloc(n);
-        }
-        // the sampler writes each triple's group beside it (the resolve kernel of
-        // USER_REPLACEMENT draws i later: that sampler keeps the table lookups)
         // the sampler writes each triple's group byte and the partition reads it instead of
         // looking the group up: sampler + partition 35.9 -> 32.7 ms per C3 epoch, same AUC
         // (profiles/r4r_c3_*.log; MML_BPR_GROUP_BYTES=0 in experiments builds: table lookups)
+        // (the resolve kernel of USER_REPLACEMENT draws i later: that sampler keeps the lookups)
         static const bool group_bytes = [] {
             const char* e = MML_EXPERIMENT_ENV("MML_BPR_GROUP_BYTES");
             return !(e && std::string(e) == "0");
         }();
         const bool part_g = part && !user_repl && group_bytes;
-        if (part_g && (int64_t)h->tri_g.count < n) h->tri_g.alloc(n);
         // user phases: the default sampler draws the epoch phase by phase, one update launch each
         const int32_t P =
             part_g && h->p.sampler == MML_BPR_SAMPLER_UNIFORM_USER ? bpr_phases(h) : 1;
@@ -1654,11 +1671,30 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             ph.n = P;
         }
         h->last_phases = P;
-        if (part && (int64_t)h->xt_u.count < n) {
-            h->xt_u.alloc(n);
-            h->xt_i.alloc(n);
-            h->xt_j.alloc(n);
-        }
+        // the partitioned Hogwild epoch can draw the next epoch's triples beside its update
+        // (mml_bpr_set_next_seed): the triples depend on the seed and the data, not on the model.
+        // Not with phases (their span offsets are shared), WEIGHTED (a host check) or
+        // USER_REPLACEMENT (a sort on shared scratch).
+        const bool pf_path = part && P == 1 && !weighted && !user_repl && blocks > 1;
+        const bool pre = pf_path && h->pf_ready && h->pf_seed == seed && h->pf_n == n;
+        if (pre) h->cur = h->pf_buf;  // this epoch's triples were drawn ahead
+        h->pf_ready = false;
+        BprTriples& T = h->tb[h->cur];
+        auto ensure = [&](BprTriples& X) {
+            if (!fused && n > 0 && (int64_t)X.u.count < n) {
+                X.u.alloc(n);
+                X.i.alloc(n);
+                X.j.alloc(n);
+            }
+            if (part_g && (int64_t)X.g.count < n) X.g.alloc(n);
+            if (part && (int64_t)X.xu.count < n) {
+                X.xu.alloc(n);
+                X.xi.alloc(n);
+                X.xj.alloc(n);
+            }
+            if (!X.goff.get()) X.goff.alloc(9);
+        };
+        ensure(T);
         // USER_REPLACEMENT: rank keys, their sorted copy, per-user heads and the sort's scratch
         int rank_end_bit = 0;
         size_t rank_tmp_bytes = 0;
@@ -1672,23 +1708,21 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             while (ub < 32 && ((uint32_t)(h->n_users - 1) >> ub) != 0) ++ub;
             rank_end_bit = 32 + std::max(ub, 1);
             MML_HIP(rocprim::radix_sort_keys(nullptr, rank_tmp_bytes, h->rank_keys.get(),
-                                                      h->rank_sorted.get(), n, 32, rank_end_bit,
-                                                      st));
+                                             h->rank_sorted.get(), n, 32, rank_end_bit, st));
             if (h->rank_tmp.count < rank_tmp_bytes) h->rank_tmp.alloc(rank_tmp_bytes);
         }
-        MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
         const int sgrid = (int)std::min<int64_t>(256 * 64, (n + 255) / 256);
-        if (!fused && n > 0) {
+        // the sampler into set X with seed sd on stream s
+        auto sample = [&](BprTriples& X, uint64_t sd, hipStream_t s) {
             if (weighted) {
                 h->fail.alloc(1);
-                MML_HIP(hipMemsetAsync(h->fail.get(), 0, sizeof(int32_t), st));
+                MML_HIP(hipMemsetAsync(h->fail.get(), 0, sizeof(int32_t), s));
             }
 #define MML_SMP(KIND, ELIG)                                                                     \
-    bpr_sample_kernel<KIND><<<sgrid, 256, 0, st>>>(                                            \
+    bpr_sample_kernel<KIND><<<sgrid, 256, 0, s>>>(                                             \
         h->off.get(), h->cols.get(), ELIG, h->n_eligible, h->ev_u.get(), h->ev_i.get(), n,    \
-        h->n_items, seed, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), h->fail.get(),       \
-        h->rank_keys.get(), h->recs.get(), part_g ? h->xs.group.get() : nullptr,             \
-        part_g ? h->tri_g.get() : nullptr, ph)
+        h->n_items, sd, X.u.get(), X.i.get(), X.j.get(), h->fail.get(), h->rank_keys.get(),    \
+        h->recs.get(), part_g ? h->xs.group.get() : nullptr, part_g ? X.g.get() : nullptr, ph)
             int32_t* elig = h->n_eligible == h->n_users ? nullptr : h->eligible.get();
             switch (h->p.sampler) {
                 case MML_BPR_SAMPLER_UNIFORM_PAIR:
@@ -1707,64 +1741,70 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             MML_HIP(hipGetLastError());
             if (user_repl) {
                 MML_HIP(rocprim::radix_sort_keys(h->rank_tmp.get(), rank_tmp_bytes,
-                                                          h->rank_keys.get(), h->rank_sorted.get(),
-                                                          n, 32, rank_end_bit, st));
-                bpr_user_heads_kernel<<<sgrid, 256, 0, st>>>(h->rank_sorted.get(), n,
-                                                             h->rank_head.get());
-                bpr_resolve_user_replacement_kernel<<<sgrid, 256, 0, st>>>(
-                    h->rank_sorted.get(), n, h->rank_head.get(), h->off.get(), h->cols.get(), seed,
-                    h->tri_i.get());
+                                                 h->rank_keys.get(), h->rank_sorted.get(), n, 32,
+                                                 rank_end_bit, s));
+                bpr_user_heads_kernel<<<sgrid, 256, 0, s>>>(h->rank_sorted.get(), n,
+                                                            h->rank_head.get());
+                bpr_resolve_user_replacement_kernel<<<sgrid, 256, 0, s>>>(
+                    h->rank_sorted.get(), n, h->rank_head.get(), h->off.get(), h->cols.get(), sd,
+                    X.i.get());
                 MML_HIP(hipGetLastError());
             }
             if (weighted) {
                 int32_t bad = 0;
                 MML_HIP(hipMemcpyAsync(&bad, h->fail.get(), sizeof(int32_t),
-                                       hipMemcpyDeviceToHost, st));
-                MML_HIP(hipStreamSynchronize(st));
+                                       hipMemcpyDeviceToHost, s));
+                MML_HIP(hipStreamSynchronize(s));
                 if (bad)
                     mml::fail(MML_ERR_STATE,
                               "WeightedBPRMF: a user's items hold (nearly) all the event mass; no "
                               "negative item found in 65536 draws (the reference loops for ever)");
             }
-        }
-        int32_t ng = 1;
-        const int64_t* goff = h->span1.get();
-        const int32_t *tu = h->tri_u.get(), *ti = h->tri_i.get(), *tj = h->tri_j.get();
-        // the access flags need the buffer resource (V < 4 GiB) and, for the owner modes, the
-        // groups; a one-workgroup epoch keeps plain accesses (one CU, one L2)
-        const int am = v_fits && waves >= 16 && (part || !xm.partition) ? xm.am : 0;
-        if (part) {  // stable partition of the sampled triples (XcdSplit)
-            const int32_t* in[3] = {tu, ti, tj};
-            int32_t* out[3] = {h->xt_u.get(), h->xt_i.get(), h->xt_j.get()};
+        };
+        // the stable partition of set X's triples by the group of i (XcdSplit) on stream s
+        auto partition = [&](BprTriples& X, hipStream_t s) {
+            const int32_t* in[3] = {X.u.get(), X.i.get(), X.j.get()};
+            int32_t* out[3] = {X.xu.get(), X.xi.get(), X.xj.get()};
             if (P > 1) {  // each phase partitioned on its own: spans phase-major, group-minor
                 for (int32_t p = 0; p < P; ++p) {
                     const int64_t b = h->ptri_host[p], m = h->ptri_host[p + 1] - b;
                     if (m == 0) {  // an empty phase: its 8 spans are empty at b
-                        phase_span_kernel<<<1, 64, 0, st>>>(h->ph_zero.get(), b,
-                                                             h->poff.get() + (size_t)8 * p);
+                        phase_span_kernel<<<1, 64, 0, s>>>(h->ph_zero.get(), b,
+                                                            h->poff.get() + (size_t)8 * p);
                         continue;
                     }
-                    const int32_t* inp[3] = {tu + b, ti + b, tj + b};
+                    const int32_t* inp[3] = {in[0] + b, in[1] + b, in[2] + b};
                     int32_t* outp[3] = {out[0] + b, out[1] + b, out[2] + b};
-                    h->xs.partition_groups(st, h->tri_g.get() + b, m, 3, inp, outp);
-                    phase_span_kernel<<<1, 64, 0, st>>>(h->xs.goff.get(), b,
-                                                         h->poff.get() + (size_t)8 * p);
+                    h->xs.partition_groups(s, X.g.get() + b, m, 3, inp, outp);
+                    phase_span_kernel<<<1, 64, 0, s>>>(h->xs.goff.get(), b,
+                                                        h->poff.get() + (size_t)8 * p);
                 }
                 MML_HIP(hipGetLastError());
             } else if (part_g) {
-                h->xs.partition_groups(st, h->tri_g.get(), n, 3, in, out);
+                h->xs.partition_groups(s, X.g.get(), n, 3, in, out, X.goff.get());
             } else {
-                h->xs.partition(st, ti, n, 3, in, out);
+                h->xs.partition(s, X.i.get(), n, 3, in, out, X.goff.get());
             }
+        };
+        MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
+        if (!fused && n > 0 && !pre) sample(T, seed, st);
+        int32_t ng = 1;
+        const int64_t* goff = h->span1.get();
+        const int32_t *tu = T.u.get(), *ti = T.i.get(), *tj = T.j.get();
+        // the access flags need the buffer resource (V < 4 GiB) and, for the owner modes, the
+        // groups; a one-workgroup epoch keeps plain accesses (one CU, one L2)
+        const int am = v_fits && waves >= 16 && (part || !xm.partition) ? xm.am : 0;
+        if (part) {
+            if (!pre) partition(T, st);
             ng = 8;
-            goff = P > 1 ? h->poff.get() : h->xs.goff.get();
-            tu = h->xt_u.get();
-            ti = h->xt_i.get();
-            tj = h->xt_j.get();
+            goff = P > 1 ? h->poff.get() : T.goff.get();
+            tu = T.xu.get();
+            ti = T.xi.get();
+            tj = T.xj.get();
         }
         MML_HIP(hipEventRecord(h->ctx->ev_mid, st));
         if (ordered && n > 0)
-            launch_apply_ordered(h, h->tri_u.get(), h->tri_i.get(), h->tri_j.get(), n, s, st);
+            launch_apply_ordered(h, T.u.get(), T.i.get(), T.j.get(), n, s, st);
         if (!ordered && !fused && n > 0 && blocks == 1) {
             // a small epoch (< 16 waves' worth): Hogwild with one stream per wave of ONE CU, each
             // applied in order (the lanes own factors, the exact arithmetic): 4 triples in flight
@@ -1807,11 +1847,54 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
 #undef MML_BPR
         }
         MML_HIP(hipGetLastError());
+        // the next epoch's triples into the other set on the second stream, beside the update;
+        // the epoch ends when both are done, so its time holds one epoch's sampling either way
+        const bool pf = pf_path && h->next_seed_set && n > 0;
+        if (pf) {
+            BprTriples& X = h->tb[h->cur ^ 1];
+            ensure(X);
+            if (!h->side) {
+                MML_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+                MML_HIP(hipEventCreateWithFlags(&h->ev_pf_go, hipEventDisableTiming));
+                MML_HIP(hipEventCreateWithFlags(&h->ev_pf_done, hipEventDisableTiming));
+                MML_HIP(hipEventCreate(&h->ev_upd));
+            }
+            MML_HIP(hipEventRecord(h->ev_upd, st));
+            // after this epoch's partition (ev_mid: the partition's scratch is shared)
+            MML_HIP(hipStreamWaitEvent(h->side, h->ctx->ev_mid, 0));
+            sample(X, h->next_seed, h->side);
+            partition(X, h->side);
+            MML_HIP(hipEventRecord(h->ev_pf_done, h->side));
+            MML_HIP(hipStreamWaitEvent(st, h->ev_pf_done, 0));
+            h->pf_ready = true;
+            h->pf_seed = h->next_seed;
+            h->pf_n = n;
+            h->pf_buf = h->cur ^ 1;
+        }
+        h->next_seed_set = false;
+        h->last_prefetched = pre;
         MML_HIP(hipEventRecord(h->ctx->ev_end, st));
         MML_HIP(hipEventSynchronize(h->ctx->ev_end));
         MML_HIP(hipEventElapsedTime(&h->last_ms, h->ctx->ev_begin, h->ctx->ev_end));
-        MML_HIP(hipEventElapsedTime(&h->last_update_ms, h->ctx->ev_mid, h->ctx->ev_end));
+        MML_HIP(hipEventElapsedTime(&h->last_update_ms, h->ctx->ev_mid,
+                                    pf ? h->ev_upd : h->ctx->ev_end));
         h->has_triples = !fused && n > 0;
+    });
+}
+
+extern "C" mml_status mml_bpr_set_next_seed(mml_bpr* h, uint64_t seed) {
+    return guard([&] {
+        MML_REQUIRE(h && h->ctx, "null handle");
+        if (h->ctx->multi()) {  // each device's seed as mml_bpr_iterate derives it
+            for (size_t d = 0; d < h->shards.size(); ++d) {
+                const mml_status st =
+                    mml_bpr_set_next_seed(h->shards[d], seed + 0x9E3779B97F4A7C15ull * d);
+                if (st != MML_OK) mml::fail(st, mml_last_error());
+            }
+            return;
+        }
+        h->next_seed = seed;
+        h->next_seed_set = true;
     });
 }
 
@@ -1837,12 +1920,11 @@ extern "C" mml_status mml_bpr_last_triples(mml_bpr* h, int32_t* users, int32_t* 
                     "n must equal the epoch's sample count (Feedback.Count)");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
-        MML_HIP(hipMemcpyAsync(users, h->tri_u.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost,
+        const BprTriples& T = h->tb[h->cur];
+        MML_HIP(hipMemcpyAsync(users, T.u.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+        MML_HIP(hipMemcpyAsync(items, T.i.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+        MML_HIP(hipMemcpyAsync(other_items, T.j.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost,
                                st));
-        MML_HIP(hipMemcpyAsync(items, h->tri_i.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost,
-                               st));
-        MML_HIP(hipMemcpyAsync(other_items, h->tri_j.get(), sizeof(int32_t) * n,
-                               hipMemcpyDeviceToHost, st));
         MML_HIP(hipStreamSynchronize(st));
     });
 }

@@ -234,13 +234,15 @@ struct XcdSplit {
     void set_groups(hipStream_t st, const std::vector<int64_t>& weight, int32_t groups);
     // an explicit group per key (< 8), e.g. the device that owns a user (multi-device set_data)
     void set_table(hipStream_t st, const std::vector<uint8_t>& table);
-    // out[c][...] = in[c][...] reordered by group(key[x]), stable; goff written on the device
+    // out[c][...] = in[c][...] reordered by group(key[x]), stable; the 9 group offsets written on
+    // the device into goff_out (nullptr: goff)
     void partition(hipStream_t st, const int32_t* key, int64_t n, int32_t npay,
-                   const int32_t* const* in, int32_t* const* out);
+                   const int32_t* const* in, int32_t* const* out, int64_t* goff_out = nullptr);
     // the same with each entry's group given as a byte (gkey[x] = group[key[x]], e.g. written by
     // the BPR sampler beside its triple): no table lookups in the count and scatter passes
     void partition_groups(hipStream_t st, const uint8_t* gkey, int64_t n, int32_t npay,
-                          const int32_t* const* in, int32_t* const* out);
+                          const int32_t* const* in, int32_t* const* out,
+                          int64_t* goff_out = nullptr);
 };
 std::vector<uint8_t> balanced_item_groups(const std::vector<int64_t>& weight, int32_t ng);
 // occurrences of each id in [0, n_ids) of a device id array, on the host

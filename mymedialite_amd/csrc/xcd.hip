@@ -253,7 +253,8 @@ void XcdSplit::set_table(hipStream_t st, const std::vector<uint8_t>& table) {
 namespace {
 template <bool DIRECT>
 void partition_impl(XcdSplit& xs, hipStream_t st, const int32_t* key, const uint8_t* gkey,
-                    int64_t n, int32_t npay, const int32_t* const* in, int32_t* const* out) {
+                    int64_t n, int32_t npay, const int32_t* const* in, int32_t* const* out,
+                    int64_t* goff_out) {
     MML_REQUIRE(xs.ng == 8 && npay >= 1 && npay <= 3, "XcdSplit::partition: bad setup");
     const int32_t nblk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 4095) / 4096));
     const int64_t seg = (n + nblk - 1) / nblk;
@@ -275,19 +276,21 @@ void partition_impl(XcdSplit& xs, hipStream_t st, const int32_t* key, const uint
     }
     xcd_scatter_kernel<DIRECT><<<nblk, 256, 0, st>>>(key, gkey, n, seg, xs.group.get(),
                                                      xs.base.get(), nblk, npay, p);
-    xcd_offsets_kernel<<<1, 64, 0, st>>>(xs.base.get(), nblk, n, xs.goff.get());
+    xcd_offsets_kernel<<<1, 64, 0, st>>>(xs.base.get(), nblk, n,
+                                         goff_out ? goff_out : xs.goff.get());
     MML_HIP(hipGetLastError());
 }
 }  // namespace
 
 void XcdSplit::partition(hipStream_t st, const int32_t* key, int64_t n, int32_t npay,
-                         const int32_t* const* in, int32_t* const* out) {
-    partition_impl<false>(*this, st, key, nullptr, n, npay, in, out);
+                         const int32_t* const* in, int32_t* const* out, int64_t* goff_out) {
+    partition_impl<false>(*this, st, key, nullptr, n, npay, in, out, goff_out);
 }
 
 void XcdSplit::partition_groups(hipStream_t st, const uint8_t* gkey, int64_t n, int32_t npay,
-                                const int32_t* const* in, int32_t* const* out) {
-    partition_impl<true>(*this, st, nullptr, gkey, n, npay, in, out);
+                                const int32_t* const* in, int32_t* const* out,
+                                int64_t* goff_out) {
+    partition_impl<true>(*this, st, nullptr, gkey, n, npay, in, out, goff_out);
 }
 
 std::vector<int64_t> device_id_counts(hipStream_t st, const int32_t* ids, int64_t n,

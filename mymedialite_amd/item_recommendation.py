@@ -444,13 +444,33 @@ class BPRMF(_MFBase):
                                           N.ptr(bias, N._f32p)))
         self._host = dict(U=U, V=V, bias=bias)
 
-    def iterate(self):
-        """Iterate() (:160-178): one epoch of Feedback.Count sampled triples on the GPU.  The
-        device sampler is keyed by a 62-bit seed drawn from MyMediaLite.Random per epoch."""
+    @staticmethod
+    def _draw_seed() -> int:
         rng = Random.get_instance()
-        seed = (rng.next(2147483647) << 31) ^ rng.next(2147483647)
+        return (rng.next(2147483647) << 31) ^ rng.next(2147483647)
+
+    def iterate(self, _seed=None, _next_seed=None):
+        """Iterate() (:160-178): one epoch of Feedback.Count sampled triples on the GPU.  The
+        device sampler is keyed by a 62-bit seed drawn from MyMediaLite.Random per epoch.  (train()
+        passes the epoch's seed and the next one, which the library draws beside this epoch's
+        update: mml_bpr_set_next_seed.)"""
+        seed = self._draw_seed() if _seed is None else _seed
+        if _next_seed is not None:
+            N.check(N.lib().mml_bpr_set_next_seed(self._h, ctypes.c_uint64(_next_seed)))
         N.check(N.lib().mml_bpr_iterate(self._h, ctypes.c_uint64(seed)))
         self._host = None
+
+    def train(self):
+        """MF.Train (MF.cs:61-67): InitModel, then NumIter epochs.  Epoch e + 1's seed is drawn
+        before epoch e runs, the same draws in the same order as one per Iterate() (the epochs draw
+        nothing else), so the library samples each next epoch beside the current update."""
+        self.init_model()
+        n = int(self.NumIter)
+        seed = self._draw_seed() if n > 0 else None
+        for e in range(n):
+            nxt = self._draw_seed() if e + 1 < n else None
+            self.iterate(seed, nxt)
+            seed = nxt
 
     def last_epoch_ms(self) -> float:
         out = np.zeros(2, np.float32)
