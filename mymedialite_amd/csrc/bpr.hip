@@ -1713,13 +1713,13 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
         }
         const int sgrid = (int)std::min<int64_t>(256 * 64, (n + 255) / 256);
         // the sampler into set X with seed sd on stream s
-        auto sample = [&](BprTriples& X, uint64_t sd, hipStream_t s) {
+        auto sample = [&](BprTriples& X, uint64_t sd, hipStream_t s, int grid) {
             if (weighted) {
                 h->fail.alloc(1);
                 MML_HIP(hipMemsetAsync(h->fail.get(), 0, sizeof(int32_t), s));
             }
 #define MML_SMP(KIND, ELIG)                                                                     \
-    bpr_sample_kernel<KIND><<<sgrid, 256, 0, s>>>(                                             \
+    bpr_sample_kernel<KIND><<<grid, 256, 0, s>>>(                                              \
         h->off.get(), h->cols.get(), ELIG, h->n_eligible, h->ev_u.get(), h->ev_i.get(), n,    \
         h->n_items, sd, X.u.get(), X.i.get(), X.j.get(), h->fail.get(), h->rank_keys.get(),    \
         h->recs.get(), part_g ? h->xs.group.get() : nullptr, part_g ? X.g.get() : nullptr, ph)
@@ -1787,7 +1787,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             }
         };
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
-        if (!fused && n > 0 && !pre) sample(T, seed, st);
+        if (!fused && n > 0 && !pre) sample(T, seed, st, sgrid);
         int32_t ng = 1;
         const int64_t* goff = h->span1.get();
         const int32_t *tu = T.u.get(), *ti = T.i.get(), *tj = T.j.get();
@@ -1862,7 +1862,9 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             MML_HIP(hipEventRecord(h->ev_upd, st));
             // after this epoch's partition (ev_mid: the partition's scratch is shared)
             MML_HIP(hipStreamWaitEvent(h->side, h->ctx->ev_mid, 0));
-            sample(X, h->next_seed, h->side);
+            // (a thinner sampler disturbs the update no less: grids of 256 / 1,024 / 4,096 / 16,384
+            // workgroups gave epochs of 333.3 / 327.4 / 323.3 / 324.6 ms, profiles/r5aj/)
+            sample(X, h->next_seed, h->side, sgrid);
             partition(X, h->side);
             MML_HIP(hipEventRecord(h->ev_pf_done, h->side));
             MML_HIP(hipStreamWaitEvent(st, h->ev_pf_done, 0));
