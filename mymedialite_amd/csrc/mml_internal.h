@@ -164,6 +164,7 @@ struct WrmfTilePlan {
     // per half-step: false when the tiles do not fit the free HBM (the refinement then
     // refactors each row instead).
     bool keep_factor = false;
+    bool refined = false;  // fp64 refinement passes follow the half-step's solve (wood main target)
     // the item half's pipeline (fp64 mode, no Woodbury rows in the plan): the light rows in nbatch
     // contiguous row ranges (the light list range-major, degree-descending within a range), so the
     // first refinement pass's residual of range b (X (HH + reg I), the data term, R -> Rf) runs on

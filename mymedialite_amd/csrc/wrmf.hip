@@ -662,6 +662,7 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
     } else {
         mml::WrmfTilePlan& plan = plan_in ? *plan_in : W == h->U.get() ? h->uplan : h->iplan;
         plan.keep_factor = h->p.refine_passes > 0;
+        plan.refined = h->p.refine_passes > 0;
         mml::wrmf_tile_solve(st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha,
                              h->p.regularization, launches);
         const int32_t done = mml::wrmf_tile_refine(

@@ -2324,13 +2324,16 @@ int wood128_parts() {
     }();
     return v;
 }
-// lnorm: |L^{-1}|_2 (refinement only)
+// lnorm: |L^{-1}|_2 (refinement only); refined: fp64 refinement passes follow this main solve
 void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const int64_t* off,
                     const int32_t* cols, const float* Q, int32_t k, float alpha, float* Tout,
-                    const float* S, double lnorm = 0.0) {
+                    const float* S, double lnorm = 0.0, bool refined = false) {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, 256 * 4));
     // main solve: relative residual 1e-6 (fp32 CG stagnates not far below: a tighter target
-    // just runs to max_it on trained factors).  A refinement correction d: 3e-3.  The pass's
+    // just runs to max_it on trained factors), 1e-5 when the fp64 refinement follows and corrects
+    // the rest (C5: the users' largest correction stays 0 / 0 / 1e-8 with 1e-6 / 1e-5 / 1e-4 and
+    // the iteration takes 723.3 / 712.7 / 707.9 ms, profiles/r5al/).  A refinement correction d:
+    // 3e-3.  The pass's
     // contraction on Woodbury rows is set by fp32 rounding in the CG as much as by this target
     // (1e-4 measured 0.027 .. 0.06 on the tests' sets, no better than 3e-3), so the error left is
     // bounded by further passes instead (kRefineStopWood), and C5, whose Woodbury corrections are
@@ -2339,7 +2342,11 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
         const char* e = MML_EXPERIMENT_ENV("MML_WRMF_REFINE_TOL");
         return e ? std::atof(e) : 3e-3;
     }();
-    const double tol = S ? refine_tol : 1e-6;
+    static const double main_tol = [] {  // MML_WRMF_MAIN_TOL (experiments builds): A/B
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_MAIN_TOL");
+        return e ? std::atof(e) : 1e-5;
+    }();
+    const double tol = S ? refine_tol : refined ? main_tol : 1e-6;
     const double rho = (std::sqrt(1.0 + alpha) - 1.0) / (std::sqrt(1.0 + alpha) + 1.0);
     // MML_WRMF_DEBUG & 64 (timing only): no CG step, the gathers and the t = Q_S^T w pass alone
     const int max_it = (debug_mask() & 64) ? 0
@@ -2352,7 +2359,7 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
     const double sk = S && lnorm > 0.0 ? wood_abs / lnorm : 0.0, ab = sk / alpha;
     const float skip2 = S ? (float)(sk * sk) : -1.0f, abs2 = (float)(ab * ab);
     // the main solve by Chebyshev iteration: error <= 2 / T_m(theta / delta) relative, so
-    // m = acosh(2 / tol) / acosh(theta / delta) updates, + 1 for fp32 (alpha = 1: 10 updates and 9
+    // m = acosh(2 / tol) / acosh(theta / delta) updates, + 1 for fp32 (alpha = 1: 9 updates and 8
     // mat-vecs, against 13 mat-vecs and 13 block reductions for the CG at its step cap);
     // MML_WRMF_WOOD_MAIN=cg (experiments builds) keeps the CG
     static const bool main_cg = [] {
@@ -3633,7 +3640,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                 nullptr, nullptr);
         } else if (wood_cg()) {
             launch_wood_cg(st, g, p.wood[g].get(), p.n_wood[g], off, cols, p.qbuf.get(), k,
-                           (float)alpha, p.tbuf.get(), nullptr);
+                           (float)alpha, p.tbuf.get(), nullptr, 0.0, p.refined);
         } else {
             auto* L = g == 0 ? &launch_wood<1> : g == 1 ? &launch_wood<2>
                       : g == 2 ? &launch_wood<3> : &launch_wood<4>;
