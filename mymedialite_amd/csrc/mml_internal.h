@@ -151,6 +151,7 @@ struct WrmfTilePlan {
     DeviceArray<float> linv, linvt, qbuf, tbuf;  // L^{-1}, L^{-T} of HH + reg I; Q = H L^{-T}; t rows
     DeviceArray<uint16_t> linv_x3, linvt_x3;    // their bf16 planes, transposed (row GEMMs)
     DeviceArray<float> sbuf;                      // refinement: s = L^{-1} r per Woodbury row
+    DeviceArray<int32_t> crow, cpos, ccount;      // refinement: the rows the screen left, count
     double linv_norm = 0.0;                       // |L^{-1}|_2 (estimate, 1.25 margin)
     bool woodbury = false;                        // rows with 1 <= deg <= 128 take Woodbury
     // fp64 iterative refinement (wrmf_tile_refine): the residual's entry segments (rows with

@@ -1858,7 +1858,7 @@ wrmf_wood_cg_kernel(
     const int32_t* __restrict__ cols, const float* __restrict__ Q, int32_t k, float alpha,
     const float* __restrict__ S, float* __restrict__ Tout, int32_t max_it, float tol2,
     float skip2, float abs2, int32_t cheb_m, float cheb_theta, float cheb_delta,
-    float cheb_acosh) {
+    float cheb_acosh, const int32_t* __restrict__ spos) {
     static_assert(NJ == 32 || NJ == 64 || NJ == 96 || NJ == 128, "NJ: 32, 64, 96 or 128");
     static_assert(NJ % PARTS == 0 && NJ / PARTS <= 64, "parts of <= 64 items");
     constexpr int HALVES = PARTS;
@@ -1886,13 +1886,14 @@ wrmf_wood_cg_kernel(
             // refinement, d = L^-T (s - Q_S^T w) with C w = Q_S s: |d|_2 <= |L^-1|_2 |s|_2 (the
             // middle factor I - Q_S^T C^-1 Q_S has norm <= 1), so a row whose bound is below the
             // absolute target keeps d = 0 without gathering Q_S
-            sf = fon && half == 0 ? S[(int64_t)li * k + f] : 0.0f;
+            const int64_t sl = spos ? spos[li] : li;  // s of list entry spos[li] (the screen)
+            sf = fon && half == 0 ? S[sl * k + f] : 0.0f;
             const float2 ss = block_sum2<WAVES>(sf * sf, 0.0f, sdot[1]);
             if (ss.x <= skip2) {
                 if (fon && half == 0) Tout[(int64_t)li * k + f] = 0.0f;
                 continue;
             }
-            if (half != 0) sf = fon ? S[(int64_t)li * k + f] : 0.0f;
+            if (half != 0) sf = fon ? S[sl * k + f] : 0.0f;
         }
         if (t < NJ) sid[t] = t < deg ? cols[rb + t] : 0;
         __syncthreads();
@@ -2050,7 +2051,7 @@ __global__ __launch_bounds__(64 * WAVES, 4) void wrmf_wood_w16_kernel(
     const int32_t* __restrict__ cols, const float* __restrict__ Q, int32_t k, float alpha,
     const float* __restrict__ S, float* __restrict__ Tout, int32_t max_it, float tol2,
     float skip2, float abs2, int32_t cheb_m, float cheb_theta, float cheb_delta,
-    float cheb_acosh) {
+    float cheb_acosh, const int32_t* __restrict__ spos) {
     static_assert(WAVES >= 1 && WAVES <= 8, "16 items per wave, <= 128 items");
     __shared__ float4 pu[2][WAVES][64];   // the waves' partial u, alternated per mat-vec
     __shared__ float sdot[2][2 * WAVES];  // block_sum2, alternated per CG step
@@ -2084,9 +2085,10 @@ __global__ __launch_bounds__(64 * WAVES, 4) void wrmf_wood_w16_kernel(
         float sf[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         if (S) {
             // refinement: |d|_2 <= |L^-1|_2 |s|_2 (wrmf_wood_cg_kernel), a wave holds all of s
+            const int64_t sl = spos ? spos[li] : li;  // s of list entry spos[li] (the screen)
 #pragma unroll
             for (int c = 0; c < 4; ++c)
-                sf[c] = f0 + c < k ? S[(int64_t)li * k + f0 + c] : 0.0f;
+                sf[c] = f0 + c < k ? S[sl * k + f0 + c] : 0.0f;
             float ss = (sf[0] * sf[0] + sf[1] * sf[1]) + (sf[2] * sf[2] + sf[3] * sf[3]);
             ss = pstage<0>(ss);
             ss = pstage<1>(ss);
@@ -2324,10 +2326,56 @@ int wood128_parts() {
     }();
     return v;
 }
+// the refinement's absolute target for a Woodbury row's correction (A/B in experiments builds)
+double wood_abs() {
+    static const double v = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOOD_ABS");
+        return e ? std::atof(e) : kWoodAbs;
+    }();
+    return v;
+}
+// a refinement row with |s|_2^2 <= this keeps d = 0 (|d|_2 <= |L^-1|_2 |s|_2)
+float wood_skip2(double lnorm) {
+    const double sk = lnorm > 0.0 ? wood_abs() / lnorm : 0.0;
+    return (float)(sk * sk);
+}
+
+// The refinement's screen ahead of the Woodbury kernels.  A list entry whose |s|_2^2 (in fp64 here)
+// is below the kernels' skip bound by a 1e-4 margin is one they would skip: its correction row D is
+// zeroed here (what the row GEMM makes of t = 0).  The kernels' own fp32 sums are within ~1e-6 of
+// the fp64 one.  The other entries go to a compact list (row, list position; in any order, rows are
+// independent), and the kernels decide those, as without the screen.  C5's users: all skip.
+__global__ __launch_bounds__(256) void wrmf_wood_screen_kernel(
+    const int32_t* __restrict__ rows, int32_t n, const float* __restrict__ S, int32_t k,
+    double lim, float* __restrict__ D, int32_t* __restrict__ crow, int32_t* __restrict__ cpos,
+    int32_t* __restrict__ count) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+    for (int64_t li = w0; li < n; li += nw) {
+        double ss = 0.0;
+        for (int f = lane; f < k; f += 64) {
+            const double v = S[li * k + f];
+            ss += v * v;
+        }
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+        ss = __shfl(ss, 0);  // lane 0's sum for every lane: one decision per wave
+        const int32_t r = rows[li];
+        if (ss <= lim) {
+            for (int f = lane; f < k; f += 64) D[(int64_t)r * k + f] = 0.0f;
+        } else if (lane == 0) {
+            const int32_t c = atomicAdd(count, 1);
+            crow[c] = r;
+            cpos[c] = (int32_t)li;
+        }
+    }
+}
+
 // lnorm: |L^{-1}|_2 (refinement only); refined: fp64 refinement passes follow this main solve
+// spos (refinement after wrmf_wood_screen_kernel): list entry li's s is S row spos[li]
 void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const int64_t* off,
                     const int32_t* cols, const float* Q, int32_t k, float alpha, float* Tout,
-                    const float* S, double lnorm = 0.0, bool refined = false) {
+                    const float* S, double lnorm = 0.0, bool refined = false,
+                    const int32_t* spos = nullptr) {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, 256 * 4));
     // main solve: relative residual 1e-6 (fp32 CG stagnates not far below: a tighter target
     // just runs to max_it on trained factors), 1e-5 when the fp64 refinement follows and corrects
@@ -2352,12 +2400,8 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
     const int max_it = (debug_mask() & 64) ? 0
                        : std::min(200, (int)std::ceil(std::log(tol) / std::log(rho)) + 4);
     const float tol2 = (float)(tol * tol);
-    static const double wood_abs = [] {  // A/B of the absolute target (experiments builds)
-        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOOD_ABS");
-        return e ? std::atof(e) : kWoodAbs;
-    }();
-    const double sk = S && lnorm > 0.0 ? wood_abs / lnorm : 0.0, ab = sk / alpha;
-    const float skip2 = S ? (float)(sk * sk) : -1.0f, abs2 = (float)(ab * ab);
+    const double sk = S && lnorm > 0.0 ? wood_abs() / lnorm : 0.0, ab = sk / alpha;
+    const float skip2 = S ? wood_skip2(lnorm) : -1.0f, abs2 = (float)(ab * ab);
     // the main solve by Chebyshev iteration: error <= 2 / T_m(theta / delta) relative, so
     // m = acosh(2 / tol) / acosh(theta / delta) updates, + 1 for fp32 (alpha = 1: 9 updates and 8
     // mat-vecs, against 13 mat-vecs and 13 block reductions for the CG at its step cap);
@@ -2379,31 +2423,31 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
     if (g == 2 && wood_w16_mode() == 3)
         ((k & 3) == 0 ? &wrmf_wood_w16_kernel<6, true> : &wrmf_wood_w16_kernel<6, false>)<<<
             grid, 64 * 6, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout, max_it, tol2, skip2,
-                                   abs2, cheb_m, (float)theta, (float)delta, cheb_acosh);
+                                   abs2, cheb_m, (float)theta, (float)delta, cheb_acosh, spos);
     else if ((g == 3 && wood_w16()) || (g == 2 && wood_w16_mode() == 2))
         ((k & 3) == 0 ? &wrmf_wood_w16_kernel<8, true> : &wrmf_wood_w16_kernel<8, false>)<<<
             grid, 64 * 8, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout, max_it, tol2, skip2,
-                                   abs2, cheb_m, (float)theta, (float)delta, cheb_acosh);
+                                   abs2, cheb_m, (float)theta, (float)delta, cheb_acosh, spos);
     else if (g == 0)
         wrmf_wood_cg_kernel<32><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
                                                       max_it, tol2, skip2, abs2, cheb_m,
-                                                      (float)theta, (float)delta, cheb_acosh);
+                                                      (float)theta, (float)delta, cheb_acosh, spos);
     else if (g == 1)
         wrmf_wood_cg_kernel<64><<<grid, 256, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
                                                       max_it, tol2, skip2, abs2, cheb_m,
-                                                      (float)theta, (float)delta, cheb_acosh);
+                                                      (float)theta, (float)delta, cheb_acosh, spos);
     else if (wood128_parts() == 4)
         wrmf_wood_cg_kernel<128, 4><<<grid, 1024, 0, st>>>(
             rows, n, off, cols, Q, k, alpha, S, Tout, max_it, tol2, skip2, abs2, cheb_m,
-            (float)theta, (float)delta, cheb_acosh);
+            (float)theta, (float)delta, cheb_acosh, spos);
     else if (g == 2 && wood96())
         wrmf_wood_cg_kernel<96><<<grid, 768, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
                                                       max_it, tol2, skip2, abs2, cheb_m,
-                                                      (float)theta, (float)delta, cheb_acosh);
+                                                      (float)theta, (float)delta, cheb_acosh, spos);
     else
         wrmf_wood_cg_kernel<128><<<grid, 512, 0, st>>>(rows, n, off, cols, Q, k, alpha, S, Tout,
                                                        max_it, tol2, skip2, abs2, cheb_m,
-                                                       (float)theta, (float)delta, cheb_acosh);
+                                                       (float)theta, (float)delta, cheb_acosh, spos);
 }
 
 // Y[yrow(r)] = scale * X[xrow(r)] * M for n rows (X, Y row-major [.. x k], M [k x k] row-major,
@@ -3582,8 +3626,31 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             rows_matmul(st, rhs, p.wood[g].get(), p.n_wood[g], p.linvt.get(), p.linvt_x3.get(), k,
                         1.0f, p.sbuf.get(), nullptr);
             if (wood_cg()) {
-                launch_wood_cg(st, g, p.wood[g].get(), p.n_wood[g], off, cols, p.qbuf.get(), k,
-                               (float)alpha, p.tbuf.get(), p.sbuf.get(), p.linv_norm);
+                // the rows whose correction is 0 by the bound are settled here; the kernels and
+                // the row GEMM run on the rest (none for C5's users)
+                p.crow.reserve(nw_max);
+                p.cpos.reserve(nw_max);
+                p.ccount.reserve(1);
+                MML_HIP(hipMemsetAsync(p.ccount.get(), 0, sizeof(int32_t), st));
+                const double lim = (double)wood_skip2(p.linv_norm) * (1.0 - 1e-4);
+                const int sg = (int)std::min<int64_t>((p.n_wood[g] + 3) / 4, 4096);
+                wrmf_wood_screen_kernel<<<sg, 256, 0, st>>>(p.wood[g].get(), p.n_wood[g],
+                                                            p.sbuf.get(), k, lim, W, p.crow.get(),
+                                                            p.cpos.get(), p.ccount.get());
+                int32_t m = 0;
+                MML_HIP(hipMemcpyAsync(&m, p.ccount.get(), sizeof(int32_t), hipMemcpyDeviceToHost,
+                                       st));
+                MML_HIP(hipStreamSynchronize(st));
+                if (m > 0) {
+                    launch_wood_cg(st, g, p.crow.get(), m, off, cols, p.qbuf.get(), k,
+                                   (float)alpha, p.tbuf.get(), p.sbuf.get(), p.linv_norm, false,
+                                   p.cpos.get());
+                    rows_matmul(st, p.tbuf.get(), nullptr, m, p.linv.get(), p.linv_x3.get(), k,
+                                1.0f, W, p.crow.get());
+                }
+                MML_HIP(hipGetLastError());
+                launches += 4;
+                continue;
             } else {
                 auto* L = g == 0 ? &launch_wood<1> : g == 1 ? &launch_wood<2>
                           : g == 2 ? &launch_wood<3> : &launch_wood<4>;

@@ -12,6 +12,8 @@ build, once per setting, and compare the saved models:
       python scripts/check_wrmf_pipe_identity.py save gpurun_out/wrmf_pipe.npz
   python scripts/check_wrmf_pipe_identity.py compare gpurun_out/wrmf_serial.npz gpurun_out/wrmf_pipe.npz
 
+The same script compares two libraries (MML_LIB_PATH) on any set: save DST USERS ITEMS PER_USER.
+
 The set: 400 k users x 40 k items, 100 positives per user (items Zipf(0.8), synthetic.c5_events),
 k = 256, fp64 mode, 2 iterations -- the item half has > 4 x 4,096 direct rows, no Woodbury rows (the
 rarest item still has ~230 entries) and hot rows (> 8,192 entries), so every new path runs.
@@ -64,7 +66,7 @@ def compare(a, b):
 
 
 if __name__ == "__main__":
-    if sys.argv[1] == "save":
-        save(sys.argv[2])
+    if sys.argv[1] == "save":  # save DST [users items per_user]: another set (e.g. two libraries)
+        save(sys.argv[2], *[int(x) for x in sys.argv[3:6]])
     else:
         sys.exit(compare(sys.argv[2], sys.argv[3]))
