@@ -152,6 +152,13 @@ struct WrmfTilePlan {
     DeviceArray<uint16_t> linv_x3, linvt_x3;    // their bf16 planes, transposed (row GEMMs)
     DeviceArray<float> sbuf;                      // refinement: s = L^{-1} r per Woodbury row
     DeviceArray<int32_t> crow, cpos, ccount;      // refinement: the rows the screen left, count
+    int64_t screen_left = 0;  // refinement: Woodbury rows any pass left to the kernels (or unknown)
+    // refinement: the handle's stream waits on this before the pass's x += d row update (the
+    // speculative HH of the next half-step is still reading W; consumed by the first pass)
+    hipEvent_t pre_update_wait = nullptr;
+    // refinement: issued right after the first pass's dense term (the speculative HH, so that it
+    // runs beside the memory-bound data term rather than the dense term's fp64 MFMAs)
+    std::function<void(hipStream_t)> after_dense;
     double linv_norm = 0.0;                       // |L^{-1}|_2 (estimate, 1.25 margin)
     bool woodbury = false;                        // rows with 1 <= deg <= 128 take Woodbury
     // fp64 iterative refinement (wrmf_tile_refine): the residual's entry segments (rows with

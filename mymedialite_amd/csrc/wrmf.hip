@@ -546,6 +546,11 @@ struct mml_wrmf {
     // residual after the whole solve, HH on the handle's stream), n = n ranges
     int32_t pipe_req = 0;
     mml::DeviceArray<uint8_t> hhp;  // HH + reg I, block-packed (k > 64 path)
+    // the items' HH = U^T U computed from the users' solve while the users' refinement runs
+    // (half_step); valid when that refinement left U as it was (every Woodbury row screened)
+    mml::DeviceArray<double> HHspec;
+    hipEvent_t spec_go = nullptr, spec_done = nullptr;
+    bool spec_valid = false;
     mml::WrmfTilePlan uplan, iplan;  // k > 128: matrix-core row solves (wrmf_tiles.hip)
     // row shards (one process per GPU): rank r solves rows [ub[r], ub[r+1]) of U and
     // [ib[r], ib[r+1]) of V; the halves are exchanged by an all-gather (grouped broadcasts)
@@ -573,6 +578,15 @@ bool no_woodbury() {
     static const bool v = [] {
         const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOODBURY");
         return e && std::string(e) == "0";
+    }();
+    return v;
+}
+
+// MML_WRMF_SPEC_HH=0 (experiments builds): the items' HH after the users' refinement (A/B)
+bool spec_hh() {
+    static const bool v = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_SPEC_HH");
+        return !(e && std::string(e) == "0");
     }();
     return v;
 }
@@ -614,11 +628,14 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
     // only), when the half has hot rows and no Woodbury rows (those read HH on the host first)
     hipStream_t hs = st;
     mml::WrmfTilePlan* dplan = nullptr;
+    // the users' half-step already computed this HH from U, which its refinement left unchanged
+    const bool spec = h->spec_valid && H == h->U.get() && h_rows == h->n_users;
+    h->spec_valid = false;
     static const bool hh_side = [] {  // MML_WRMF_HH_SIDE=0 (experiments builds): HH on st (A/B)
         const char* e = MML_EXPERIMENT_ENV("MML_WRMF_HH_SIDE");
         return !(e && std::string(e) == "0");
     }();
-    if (tiles_path && r1 > r0 && hh_side && h->pipe_req != 1) {
+    if (tiles_path && r1 > r0 && hh_side && h->pipe_req != 1 && !spec) {
         mml::WrmfTilePlan& pl = plan_in ? *plan_in : W == h->U.get() ? h->uplan : h->iplan;
         if (!pl.heavy.empty() && pl.n_wood[0] + pl.n_wood[1] + pl.n_wood[2] + pl.n_wood[3] == 0) {
             hipStream_t side = mml::wrmf_plan_side(pl, st);
@@ -632,11 +649,16 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
             }
         }
     }
-    wrmf_gram_partial_kernel<<<dim3(tiles, nparts), 256, 0, hs>>>(H, h_rows, k, rps,
-                                                                 h->partial.get());
-    wrmf_gram_reduce_kernel<<<(k * k + 255) / 256, 256, 0, hs>>>(h->partial.get(), nparts, k,
-                                                                  h->HH.get());
-    launches += 2;
+    if (spec) {
+        MML_HIP(hipStreamWaitEvent(st, h->spec_done, 0));
+        h->HH.swap(h->HHspec);  // the same kernels over the same rows: the same HH
+    } else {
+        wrmf_gram_partial_kernel<<<dim3(tiles, nparts), 256, 0, hs>>>(H, h_rows, k, rps,
+                                                                     h->partial.get());
+        wrmf_gram_reduce_kernel<<<(k * k + 255) / 256, 256, 0, hs>>>(h->partial.get(), nparts, k,
+                                                                      h->HH.get());
+        launches += 2;
+    }
     if (dplan) {
         MML_HIP(hipEventRecord(dplan->hh_done, hs));
         dplan->hh_pending = true;
@@ -665,11 +687,47 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
         plan.refined = h->p.refine_passes > 0;
         mml::wrmf_tile_solve(st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha,
                              h->p.regularization, launches);
+        // the items' HH = U^T U from the solved U on the second stream while the refinement
+        // runs: one rank, all of U solved here, every row a Woodbury row (the refinement then
+        // leaves U as it is when the screen settles every row: x += 0, and a -0 that becomes +0
+        // does not change a sum that starts from +0)
+        const bool spec_users = !plan_in && W == h->U.get() && plan.refined && r0 == 0 &&
+                                r1 == h->n_users && h->shard_nranks == 1 && plan.n_light == 0 &&
+                                plan.heavy.empty() && spec_hh();
+        hipStream_t sside = spec_users ? mml::wrmf_plan_side(plan, st) : nullptr;
+        if (sside) {
+            if (!h->spec_go) {
+                MML_HIP(hipEventCreateWithFlags(&h->spec_go, hipEventDisableTiming));
+                MML_HIP(hipEventCreateWithFlags(&h->spec_done, hipEventDisableTiming));
+            }
+            h->HHspec.reserve((size_t)k * k);
+            const int64_t rps_u = (h->n_users + nparts - 1) / nparts;  // as the items' half-step
+            // issued by the refinement after its dense term: beside the data term's gathers
+            // (beside the dense term's fp64 MFMAs it slowed them 15 -> 32 ms, profiles/r5ax/)
+            plan.after_dense = [h, sside, W, k, rps_u, tiles, nparts, &launches](hipStream_t s) {
+                MML_HIP(hipEventRecord(h->spec_go, s));
+                MML_HIP(hipStreamWaitEvent(sside, h->spec_go, 0));
+                wrmf_gram_partial_kernel<<<dim3(tiles, nparts), 256, 0, sside>>>(
+                    W, h->n_users, k, rps_u, h->partial.get());
+                wrmf_gram_reduce_kernel<<<(k * k + 255) / 256, 256, 0, sside>>>(
+                    h->partial.get(), nparts, k, h->HHspec.get());
+                MML_HIP(hipEventRecord(h->spec_done, sside));
+                launches += 2;
+            };
+            plan.pre_update_wait = h->spec_done;
+        }
         const int32_t done = mml::wrmf_tile_refine(
             st, plan, W, H, h_rows, off, cols, h->HH.get(), k, h->p.alpha, h->p.regularization,
             h->p.refine_passes, launches, h->last_corr + (W == h->U.get() ? 0 : 4),
             plan_in ? nullptr : h->ctx);
         h->last_refine = std::max(h->last_refine, done);
+        if (sside) {
+            plan.pre_update_wait = nullptr;  // (no pass ran: nothing waited)
+            MML_REQUIRE(!plan.after_dense, "the speculative HH was not issued");
+            h->spec_valid = done == 1 && plan.screen_left == 0;
+            if (!h->spec_valid)  // U changed: the items' half-step computes its own HH
+                MML_HIP(hipStreamWaitEvent(st, h->spec_done, 0));
+        }
     }
     MML_HIP(hipGetLastError());
     launches += 1;
@@ -794,6 +852,8 @@ extern "C" mml_status mml_wrmf_destroy(mml_wrmf* h) {
         (void)hipStreamSynchronize(h->ctx->stream);
         for (hipEvent_t e : h->ev_g)
             if (e) (void)hipEventDestroy(e);
+        if (h->spec_go) (void)hipEventDestroy(h->spec_go);
+        if (h->spec_done) (void)hipEventDestroy(h->spec_done);
         delete h;
     });
 }
@@ -970,6 +1030,7 @@ extern "C" mml_status mml_wrmf_iterate(mml_wrmf* h) {
         hipStream_t st = h->ctx->stream;
         int launches = 0;
         h->last_refine = 0;
+        h->spec_valid = false;
         std::fill(h->last_corr, h->last_corr + 8, 0.0f);
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
         ensure_shards(h);

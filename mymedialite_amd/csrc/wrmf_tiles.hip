@@ -3293,6 +3293,10 @@ static void first_residual(hipStream_t s, WrmfTilePlan& p, float* W, const float
         ++launches;
     };
     if (part == 1) dense(0);
+    if (part == 1 && p.after_dense) {
+        p.after_dense(s);
+        p.after_dense = nullptr;
+    }
     if (part == 4) {
         dense(1);
         MML_HIP(hipGetLastError());
@@ -3379,6 +3383,7 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
     // copy, and every pass's x += d also writes W = (float) x: no X = W pass before the first
     // residual, no W = X pass after the last (C5: ~7 ms per iteration of row traffic)
     int32_t done = 0;
+    p.screen_left = 0;
     for (int32_t pass = 0; pass < passes; ++pass) {
         // R = -X (HH + reg I) on the fp64 matrix cores, then + sum_i c_i h_i per row, R -> Rf
         if (pass == 0 && p.residual_ready) {
@@ -3411,6 +3416,10 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
         wrmf_tile_solve(st, p, p.ws->df.get(), H, h_rows, off, cols, HH, k, alpha, reg, launches,
                         p.ws->rf.get());
         MML_HIP(hipMemsetAsync(p.ws->dmax.get(), 0, 2 * sizeof(unsigned), st));
+        if (p.pre_update_wait) {
+            MML_HIP(hipStreamWaitEvent(st, p.pre_update_wait, 0));
+            p.pre_update_wait = nullptr;
+        }
         rows(pass == 0 ? 4 : 2);
         launches += 3;
         ++done;
@@ -3727,6 +3736,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                 MML_HIP(hipMemcpyAsync(&m, p.ccount.get(), sizeof(int32_t), hipMemcpyDeviceToHost,
                                        st));
                 MML_HIP(hipStreamSynchronize(st));
+                p.screen_left += m;
                 if (m > 0) {
                     launch_wood_cg(st, g, p.crow.get(), m, off, cols, p.qbuf.get(), k,
                                    (float)alpha, p.tbuf.get(), p.sbuf.get(), p.linv_norm, false,
@@ -3738,6 +3748,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                 launches += 4;
                 continue;
             } else {
+                p.screen_left += p.n_wood[g];  // no screen: the rows' corrections are unknown
                 auto* L = g == 0 ? &launch_wood<1> : g == 1 ? &launch_wood<2>
                           : g == 2 ? &launch_wood<3> : &launch_wood<4>;
                 L(st, p.wood[g].get(), p.n_wood[g], p.counter.get(), off, cols, p.qbuf.get(), k,

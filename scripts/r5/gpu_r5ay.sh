@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round 5, batch AW: the items' HH from the users' solve, beside the users' refinement (speculative), issued after the dense term.
+# Models bit-identical to the previous library on two sets, the WRMF tests,
+# then C5 timed against the previous library on one box.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp
+source scripts/gpu_steps.sh
+C=scripts/check_wrmf_pipe_identity.py
+step r5ay_id_big_prev 300 env MML_LIB_PATH=variants/prev/libmml_hip.so python -u $C save gpurun_out/big_prev.npz
+step r5ay_id_big_new 300 python -u $C save gpurun_out/big_new.npz
+step r5ay_id_big_cmp 120 python -u $C compare gpurun_out/big_prev.npz gpurun_out/big_new.npz
+step r5ay_id_small_prev 300 env MML_LIB_PATH=variants/prev/libmml_hip.so python -u $C save gpurun_out/small_prev.npz 3000 2000 100
+step r5ay_id_small_new 300 python -u $C save gpurun_out/small_new.npz 3000 2000 100
+step r5ay_id_small_cmp 120 python -u $C compare gpurun_out/small_prev.npz gpurun_out/small_new.npz
+rm -f gpurun_out/*.npz
+step r5ay_wrmf_tests 500 $PYT --timeout 240 tests/test_wrmf_gpu.py
+step r5ay_standin 300 $PYT --timeout 300 tests/test_rccl_standin_gpu.py
+step r5ay_c5_new 300 python -u bench.py --workload c5 --steps 5 --warmup 1 --no-cpu-baseline
+step r5ay_c5_prev 300 env MML_LIB_PATH=variants/prev/libmml_hip.so python -u bench.py --workload c5 --steps 5 --warmup 1 --no-cpu-baseline
+step r5ay_c5_new2 300 python -u bench.py --workload c5 --steps 5 --warmup 1 --no-cpu-baseline
+step r5ay_c5_prev2 300 env MML_LIB_PATH=variants/prev/libmml_hip.so python -u bench.py --workload c5 --steps 5 --warmup 1 --no-cpu-baseline
+step r5ay_trace_c5 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_c5_r5ay -o c5 -- python bench.py --workload c5 --steps 2 --warmup 1 --no-cpu-baseline
+cp "$(find gpurun_out/trace_c5_r5ay -name "*kernel_trace.csv" | head -n 1)" gpurun_out/r5ay_c5_kernel_trace.csv
+rm -rf gpurun_out/trace_c5_r5ay
