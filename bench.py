@@ -279,6 +279,7 @@ def bench_c2(args):
                                        if ring else f"user-shard x{world}")},
             "final_rmse": rmse,
             "initial_rmse": rmse0,
+            "slice_epoch_rmse": slice_rmse,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_note": traffic_note,
@@ -395,18 +396,15 @@ def cpu_baseline(h, k, n_users, n_items, gb, seconds, sample):
             **host, "single_thread": single}
 
 
-def cpu_baseline_dsgd(h, k, n_users, n_items, gb, sample, name):
+def cpu_baseline_dsgd(model, k, n_users, n_items, gb, sample, name, test=None):
     """The oracle's MaxThreads = T DSGD epoch (BiasedMatrixFactorization.cs:205-215, blocks from
     MultiCore.PartitionUsersAndItems) on T = this process's cores over a slice of the stream, from
-    the GPU model's current state (C4's CPU baseline on a 100M-rating slice)."""
+    `model` = (U, V, b_u, b_i), the GPU's InitModel (C4's CPU baseline on a
+    100M-rating slice).  With test = (users, items, ratings): the test RMSE after that epoch
+    (Eval/Ratings.cs:96-139 on ora_bmf_predict), the oracle's number beside the GPU's."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    U = np.empty((n_users, k), np.float32)
-    V = np.empty((n_items, k), np.float32)
-    bu = np.empty(n_users, np.float32)
-    bi = np.empty(n_items, np.float32)
-    N.check(N.lib().mml_bmf_get_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
-                                      N.ptr(bu, N._f32p), N.ptr(bi, N._f32p)))
+    U, V, bu, bi = (a.copy() for a in model)
     u, i, v = sample
     n = len(u)
     kw = dict(gb=np.float32(gb), min_rating=np.float32(1), range_=np.float32(4), lr=0.01)
@@ -417,12 +415,46 @@ def cpu_baseline_dsgd(h, k, n_users, n_items, gb, sample, name):
     t0 = time.perf_counter()
     O.bmf_dsgd_epoch_mt(u, i, v, blocks, seq, T, U, V, bu, bi, **kw)
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "rating-updates/s", "cores": T, "kind": "port",
-            "sample": f"one DSGD epoch (MaxThreads={T}: {blocks[0]}x{blocks[0]} user x item blocks, "
-                      f"BiasedMatrixFactorization.cs:205-215) over a {n}-rating slice of the "
-                      f"{name} stream (its first ratings), k={k}, oracle C restatement on {T} "
-                      f"threads, {dt:.1f} s",
-            "cpu_model": cpu_model(), "nproc": os.cpu_count(), "process_cpus": T}
+    out = {"value": n / dt, "unit": "rating-updates/s", "cores": T, "kind": "port",
+           "sample": f"one DSGD epoch (MaxThreads={T}: {blocks[0]}x{blocks[0]} user x item blocks, "
+                     f"BiasedMatrixFactorization.cs:205-215) over a {n}-rating slice of the "
+                     f"{name} stream (its first ratings), from the GPU's InitModel, k={k}, oracle C "
+                     f"restatement on {T} threads, {dt:.1f} s",
+           "cpu_model": cpu_model(), "nproc": os.cpu_count(), "process_cpus": T}
+    if test is not None:
+        tu, ti, tv = test
+        p = O.bmf_predict(tu, ti, U, V, bu, bi, np.float32(gb), np.float32(1), np.float32(4))
+        out["test_rmse_after_epoch"] = float(O.rating_eval(p, tv)[0])
+    return out
+
+
+def gpu_slice_epoch(model, k, n_users, n_items, gb, sample, test):
+    """The GPU beside cpu_baseline_dsgd: a handle over the same slice, set_model(InitModel), one
+    default HOGWILD epoch, the test RMSE (mml_bmf_evaluate) -- the library's number for the same
+    epoch from the same start."""
+    u, i, v = sample
+    ctx = N.Context(0)
+    params = N.BmfParams(k, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
+    h = N._vp()
+    N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(params), n_users, n_items,
+                                   ctypes.byref(h)))
+    try:
+        N.check(N.lib().mml_bmf_set_data(h, N.ptr(u, N._i32p), N.ptr(i, N._i32p),
+                                         N.ptr(v, N._f32p), len(u), None))
+        U, V, bu, bi = model
+        N.check(N.lib().mml_bmf_set_model(h, N.ptr(U, N._f32p), N.ptr(V, N._f32p),
+                                          N.ptr(bu, N._f32p), N.ptr(bi, N._f32p), gb, 1.0, 5.0))
+        N.check(N.lib().mml_bmf_iterate(h, 0.01, None))
+        tu, ti, tv = test
+        out = np.zeros(2, np.float32)
+        N.check(N.lib().mml_bmf_evaluate(h, N.ptr(tu, N._i32p), N.ptr(ti, N._i32p),
+                                         N.ptr(tv, N._f32p), len(tu), N.ptr(out, N._f32p)))
+        phases = ctypes.c_int32(0)
+        N.check(N.lib().mml_bmf_last_phases(h, ctypes.byref(phases)))
+        return float(out[0]), phases.value
+    finally:
+        N.lib().mml_bmf_destroy(h)
+        ctx.close()
 
 
 def c4_shard(rank, world, n_total, n_users, n_items, n_test, device, chunks=64):
@@ -483,6 +515,11 @@ def bench_c4(args):
     # item side starts identical on every rank (same seed), as after a broadcast.
     N.check(N.lib().mml_bmf_init_model(h, 4, 0.0, 0.1, gb, 1.0, 5.0))
     tus, tis, tvs = tu.cpu().numpy(), ti.cpu().numpy(), tv.cpu().numpy()
+    init = None
+    if cpu_sample is not None:  # the InitModel, for the oracle-vs-GPU epoch on the slice
+        init = (np.empty((n_users, k), np.float32), np.empty((n_items, k), np.float32),
+                np.empty(n_users, np.float32), np.empty(n_items, np.float32))
+        N.check(N.lib().mml_bmf_get_model(h, *[N.ptr(a, N._f32p) for a in init]))
     lr = 0.01
 
     def evaluate():
@@ -532,9 +569,28 @@ def bench_c4(args):
     traffic, traffic_note = None, None
     if world == 1 and k == 64 and n_total == 1_000_000_000:
         traffic, traffic_note = pmc_traffic("r5_c4_traffic.json", avg_kernel_ms)
-    cpu = None
+    N.lib().mml_bmf_destroy(h)
+    h = None
+    cpu, slice_rmse = None, None
     if cpu_sample is not None:
-        cpu = cpu_baseline_dsgd(h, k, n_users, n_items, gb, cpu_sample, "C4")
+        # the slice's own test ratings (users with a rating in it), for the RMSE beside final_rmse
+        seen = np.zeros(n_users, bool)
+        seen[cpu_sample[0]] = True
+        m_t = seen[tus]
+        slice_test = (tus[m_t].copy(), tis[m_t].copy(), tvs[m_t].copy())
+        cpu = cpu_baseline_dsgd(init, k, n_users, n_items, gb, cpu_sample, "C4", slice_test)
+        g_rmse, g_phases = gpu_slice_epoch(init, k, n_users, n_items, gb, cpu_sample, slice_test)
+        o_rmse = cpu["test_rmse_after_epoch"]
+        slice_rmse = {"gpu": g_rmse, "oracle": o_rmse, "gpu_minus_oracle": g_rmse - o_rmse,
+                      "test_ratings": int(m_t.sum()), "gpu_user_phases": g_phases,
+                      "note": f"one epoch over the cpu_baseline's {len(cpu_sample[0])}-rating slice "
+                              f"from the same InitModel: the GPU's default HOGWILD epoch vs the "
+                              f"oracle's MaxThreads={cpu['cores']} DSGD epoch (the reference's "
+                              f"multi-core schedule, BiasedMatrixFactorization.cs:205-215), test "
+                              f"RMSE on the slice users' test ratings (Eval/Ratings.cs:96-139); the "
+                              f"26-phase order lag at 100M ratings is pinned against the sequential "
+                              f"oracle by tests/test_phases_c4_gpu.py"}
+        del init
     line = None
     if rank == 0:
         line = {
@@ -560,6 +616,7 @@ def bench_c4(args):
                        "device_ingest_s": ingest_s, "user_phases": phases.value},
             "final_rmse": rmse,
             "initial_rmse": rmse0,
+            "slice_epoch_rmse": slice_rmse,
             "epochs_trained": args.warmup + args.steps,
             "allreduce_ms": float(ar[0]) if world > 1 else None,
             "allreduce_note": "device time of the last step's ncclAvg all-reduce of V||b_i "
@@ -572,7 +629,6 @@ def bench_c4(args):
                          "frac_of_box_ceiling": ceiling["frac_of_box_ceiling"]},
             "cpu_baseline": cpu,
         }
-    N.lib().mml_bmf_destroy(h)
     ctx.close()
     return line
 
@@ -913,7 +969,7 @@ def wrmf_row_check(h, ku, ki, deg_u, deg_i, n_users, n_items, k):
     V1 = np.empty((n_items, k), np.float32)
     N.check(N.lib().mml_wrmf_get_model(h, N.ptr(U1, N._f32p), N.ptr(V1, N._f32p)))
     rs = np.random.default_rng(5)
-    out, n_rows, n_side = {}, 0, {}
+    out, out_ref, n_rows, n_side = {}, {}, 0, {}
     for side, W, H, deg, picks in (
             ("user", U1, V0, deg_u.cpu().numpy(), [(1, 128, 64)]),
             ("item", V1, U1, deg_i.cpu().numpy(), [(1, 128, 8), (129, 8192, 8), (8193, 20000, 8)])):
@@ -923,11 +979,20 @@ def wrmf_row_check(h, ku, ki, deg_u, deg_i, n_users, n_items, k):
             if len(c):
                 rows.append(rs.choice(c, size=min(cnt, len(c)), replace=False))
         rows = np.sort(np.concatenate(rows))
-        rel = O.wrmf_rows_check(rows, *((ku, ki) if side == "user" else (ki, ku)), W, H, k)
+        ids = (ku, ki) if side == "user" else (ki, ku)
+        rel = O.wrmf_rows_check(rows, *ids, W, H, k)
         out[side] = float(rel.max())
+        out_ref[side] = float(O.wrmf_rows_check(rows, *ids, W, H, k,
+                                                reference_products=True).max())
         n_rows += len(rows)
         n_side[side] = len(rows)
     return {"row_check_max_rel": max(out.values()), "row_check_by_side": out,
+            "row_check_reference_products": max(out_ref.values()),
+            "row_check_reference_products_by_side": out_ref,
+            "row_check_reference_products_note": "the same rows against the reference's own "
+                                                 "arithmetic: every product rounded to float "
+                                                 "before its double sum, in HH and in the row's "
+                                                 "Gram (WRMF.cs:98-106, 116-124)",
             "row_check_note": f"one further fp64-mode iteration after the timed ones; {n_rows} "
                               f"sampled rows ({n_side['user']} user rows, {n_side['item']} item rows "
                               f"over the Woodbury / "

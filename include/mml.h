@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MML_ABI_VERSION 12
+#define MML_ABI_VERSION 13
 
 typedef int32_t mml_status;
 enum {
@@ -291,6 +291,15 @@ mml_status mml_bmf_replay_traffic(mml_bmf* h, float* out_ms);
  * used. */
 mml_status mml_bmf_set_hogwild_phases(mml_bmf* h, int32_t phases);
 mml_status mml_bmf_last_phases(mml_bmf* h, int32_t* out);
+/* The stream the last HOGWILD epoch ran on an 8-XCD device (ABI 13; single-device handles): the n
+ * ratings (n = the handle's count) in the order the launches walk them -- phase-major, XCD-group
+ * minor, the RandomIndex visit order kept inside a span -- and the phases * 8 + 1 span offsets
+ * (phase p, group g = span p * 8 + g); *n_spans = phases * 8.  The sequential Iterate()
+ * (BiasedMatrixFactorization.cs:264-310) over this order is the epoch without Hogwild's concurrency
+ * (tests/test_phases_c4_gpu.py).  MML_ERR_ARG before such an epoch. */
+mml_status mml_bmf_hogwild_stream(mml_bmf* h, int32_t* users, int32_t* items, float* values,
+                                  int64_t n, int64_t* span_offsets, int32_t cap_offsets,
+                                  int32_t* n_spans);
 /* Multi-GPU (user shards): in-place RCCL all-reduce of item factors and item
  * biases over the context's communicator with ncclAvg (model averaging).  Stream-ordered (ABI 6):
  * the call returns once the collective is enqueued; the next call on the handle runs after it. */
@@ -476,8 +485,8 @@ mml_status mml_bpr_replay_traffic(mml_bpr* h, float* out_ms);
  * "bpr_update_kernel<32, false, 27>" (ABI 9); NUL-terminated, truncated to cap bytes. */
 mml_status mml_bpr_last_kernel(mml_bpr* h, char* buf, int32_t cap);
 /* The HOGWILD epoch's launch width (ABI 10): 0 = the default (at least 65,536 triples per wave,
- * at most 8,192 waves: C3's 500 M events run 7,648); waves > 0 = that many waves, rounded up to
- * a multiple of 32 (8 XCD groups x 4 waves), at most 8,192.  Lets a smaller set replay a larger
+ * at most 8,192 waves: C3's 500 M events run 7,648); waves > 0 = that many waves, at least 32,
+ * rounded up to a multiple of 32 (8 XCD groups x 4 waves), at most 8,192.  Lets a smaller set replay a larger
  * set's triples in flight -- the Hogwild staleness -- e.g. the C3-density AUC parity test.  No
  * effect on the ORDERED schedule or on epochs below 16 waves' worth of triples. */
 mml_status mml_bpr_set_hogwild_waves(mml_bpr* h, int64_t waves);

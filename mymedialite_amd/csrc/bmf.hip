@@ -1781,16 +1781,18 @@ int32_t hogwild_phases(const mml_bmf* h) {
     return (int32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, (bytes + per - 1) / per));
 }
 
-// the XCD stream reordered phase-major (built once per data set and phase count)
+// the XCD stream reordered phase-major (built once per data set and phase count).  The phase keys
+// take each position's XCD group from xs.goff, i.e. from the group-major order: a stream already
+// sorted for another phase count is rebuilt group-major first (P <= 1 stops there).
 void ensure_phases(mml_bmf* h, int32_t P) {
     if (h->n_phases == P) return;
     hipStream_t st = h->ctx->stream;
     const int64_t n = h->n;
-    if (P <= 1) {  // back to the plain XCD stream order
+    if (h->n_phases > 1 || P <= 1) {
         h->has_xstream = false;
         h->n_phases = 1;
         ensure_xstream(h);
-        return;
+        if (P <= 1) return;
     }
     const int nk = P * 8;
     int end_bit = 1;
@@ -3265,6 +3267,36 @@ extern "C" mml_status mml_bmf_last_phases(mml_bmf* h, int32_t* out) {
         check_handle(h);
         MML_REQUIRE(out, "out is null");
         *out = h->shards.empty() ? h->n_phases : h->shards[0]->n_phases;
+    });
+}
+
+extern "C" mml_status mml_bmf_hogwild_stream(mml_bmf* h, int32_t* users, int32_t* items,
+                                             float* values, int64_t n, int64_t* span_offsets,
+                                             int32_t cap_offsets, int32_t* n_spans) {
+    return guard([&] {
+        check_handle(h);
+        single_device_only(h);
+        MML_REQUIRE(users && items && values && span_offsets && n_spans, "null output");
+        MML_REQUIRE(h->has_data && n == h->n, "n must equal the handle's rating count");
+        MML_REQUIRE(h->has_xstream,
+                    "no XCD-grouped stream: run a HOGWILD epoch on an 8-XCD device first");
+        const int32_t spans = h->n_phases * 8;
+        MML_REQUIRE(cap_offsets >= spans + 1, "span_offsets holds fewer than phases * 8 + 1");
+        h->ctx->activate();
+        hipStream_t st = h->ctx->stream;
+        if (n > 0) {
+            MML_HIP(hipMemcpyAsync(users, h->xu.get(), sizeof(int32_t) * n,
+                                   hipMemcpyDeviceToHost, st));
+            MML_HIP(hipMemcpyAsync(items, h->xi.get(), sizeof(int32_t) * n,
+                                   hipMemcpyDeviceToHost, st));
+            MML_HIP(hipMemcpyAsync(values, h->xr.get(), sizeof(float) * n,
+                                   hipMemcpyDeviceToHost, st));
+        }
+        const int64_t* off = h->n_phases > 1 ? h->poff.get() : h->xs.goff.get();
+        MML_HIP(hipMemcpyAsync(span_offsets, off, sizeof(int64_t) * (spans + 1),
+                               hipMemcpyDeviceToHost, st));
+        MML_HIP(hipStreamSynchronize(st));
+        *n_spans = spans;
     });
 }
 

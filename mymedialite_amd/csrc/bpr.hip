@@ -1612,7 +1612,9 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)65536;
         }();
         int64_t waves = std::min<int64_t>(256 * 32, std::max<int64_t>(1, n / min_chunk));
-        if (h->hog_waves > 0 && waves >= 16) waves = std::min<int64_t>(256 * 32, h->hog_waves);
+        // an override keeps the partitioned multi-workgroup launch: at least 32 waves (8 groups x 4)
+        if (h->hog_waves > 0 && waves >= 16)
+            waves = std::min<int64_t>(256 * 32, std::max<int64_t>(32, h->hog_waves));
         // fewer than 16 waves' worth of samples run as ONE workgroup: one CU, one L2, where 2+
         // workgroups on different XCDs would each cache the hot item rows and overwrite each
         // other's updates on write-back (bmf.hip launch_hogwild)

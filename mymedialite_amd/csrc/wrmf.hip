@@ -695,6 +695,15 @@ void half_step(mml_wrmf* h, float* W, int64_t r0, int64_t r1, const float* H, in
                                 r1 == h->n_users && h->shard_nranks == 1 && plan.n_light == 0 &&
                                 plan.heavy.empty() && spec_hh();
         hipStream_t sside = spec_users ? mml::wrmf_plan_side(plan, st) : nullptr;
+        // the hooks capture this call's locals: cleared on every way out of it, a throw included,
+        // so no later refinement calls a stale one
+        struct HookReset {
+            mml::WrmfTilePlan& p;
+            ~HookReset() {
+                p.after_dense = nullptr;
+                p.pre_update_wait = nullptr;
+            }
+        } hook_reset{plan};
         if (sside) {
             if (!h->spec_go) {
                 MML_HIP(hipEventCreateWithFlags(&h->spec_go, hipEventDisableTiming));

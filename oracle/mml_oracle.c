@@ -160,7 +160,19 @@ void ora_bmf_iterate(const ora_bmf_params* p, const int32_t* users, const int32_
                      const int32_t* count_by_item) {
     const int k = p->k;
     const float lr = p->learn_rate;
+    enum { AHEAD = 32 };  /* rows requested AHEAD ratings early: a cache hint, the order is kept */
     for (int64_t n = 0; n < n_idx; n++) {
+        if (n + AHEAD < n_idx) {
+            const int32_t ahead = idx[n + AHEAD];
+            const char* pu = (const char*)(U + (int64_t)users[ahead] * k);
+            const char* pv = (const char*)(V + (int64_t)items[ahead] * k);
+            for (int c = 0; c < k * 4; c += 64) {
+                __builtin_prefetch(pu + c, 1);
+                __builtin_prefetch(pv + c, 1);
+            }
+            __builtin_prefetch(bu + users[ahead], 1);
+            __builtin_prefetch(bi + items[ahead], 1);
+        }
         int32_t index = idx[n];
         int32_t u = users[index];
         int32_t i = items[index];
@@ -227,29 +239,35 @@ void ora_bmf_iterate_lockstep(const ora_bmf_params* p, const int32_t* users, con
     float* nv = (float*)malloc(sizeof(float) * (size_t)cap * (k + 1));
     int32_t* su = (int32_t*)malloc(sizeof(int32_t) * (size_t)cap);
     int32_t* si = (int32_t*)malloc(sizeof(int32_t) * (size_t)cap);
+    int64_t* sp = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap);
     for (int64_t t = 0; t * R < per; ++t) {
-        int64_t m = 0;
+        int64_t m = 0;  /* the step's ratings in stream order */
         for (int32_t w = 0; w < W; ++w)
             for (int32_t r = 0; r < R; ++r) {
                 const int64_t pos = (int64_t)w * per + t * R + r;
                 if (t * R + r >= per || pos >= n_idx) continue;
-                const int32_t index = idx[pos], u = users[index], i = items[index];
-                float* Uo = nu + m * (k + 1);
-                float* Vo = nv + m * (k + 1);
-                memcpy(Uo, U + (int64_t)u * k, sizeof(float) * k);
-                memcpy(Vo, V + (int64_t)i * k, sizeof(float) * k);
-                float bu1 = bu[u], bi1 = bi[i];
-                const int32_t zero = 0;  // the rating's rows, copied: row 0 of Uo / Vo
-                ora_bmf_iterate(p, &zero, &zero, values + index, &zero, 1, Uo, Vo, &bu1, &bi1,
-                                count_by_user ? count_by_user + u : NULL,
-                                count_by_item ? count_by_item + i : NULL);
-                Uo[k] = bu1;
-                Vo[k] = bi1;
-                su[m] = u;
-                si[m] = i;
-                ++m;
+                sp[m++] = pos;
             }
+        /* every rating of the step from the model before the step: independent, so on threads
+         * (OpenMP); the results land in the step's buffers, the model is not touched */
+#pragma omp parallel for schedule(static)
         for (int64_t x = 0; x < m; ++x) {
+            const int32_t index = idx[sp[x]], u = users[index], i = items[index];
+            float* Uo = nu + x * (k + 1);
+            float* Vo = nv + x * (k + 1);
+            memcpy(Uo, U + (int64_t)u * k, sizeof(float) * k);
+            memcpy(Vo, V + (int64_t)i * k, sizeof(float) * k);
+            float bu1 = bu[u], bi1 = bi[i];
+            const int32_t zero = 0;  // the rating's rows, copied: row 0 of Uo / Vo
+            ora_bmf_iterate(p, &zero, &zero, values + index, &zero, 1, Uo, Vo, &bu1, &bi1,
+                            count_by_user ? count_by_user + u : NULL,
+                            count_by_item ? count_by_item + i : NULL);
+            Uo[k] = bu1;
+            Vo[k] = bi1;
+            su[x] = u;
+            si[x] = i;
+        }
+        for (int64_t x = 0; x < m; ++x) {  /* writes in stream order: the last one stays */
             if (p->update_user) {
                 memcpy(U + (int64_t)su[x] * k, nu + x * (k + 1), sizeof(float) * k);
                 bu[su[x]] = nu[x * (k + 1) + k];
@@ -264,6 +282,7 @@ void ora_bmf_iterate_lockstep(const ora_bmf_params* p, const int32_t* users, con
     free(nv);
     free(su);
     free(si);
+    free(sp);
 }
 
 /* y summed over the user's rated items (MatrixExtensions.SumOfRows, DataType/MatrixExtensions.cs:

@@ -947,19 +947,41 @@ def item_eval_auc(U, V, bias, train_users, train_items, test_users, test_items, 
     return float(auc), int(nu.value)
 
 
-def wrmf_rows_check(rows, row_ids, col_ids, W, H, k, alpha=1.0, reg=0.015):
+def wrmf_square_float_products(H, dev, chunk=1 << 20):
+    """ComputeSquareMatrix (WRMF.cs:94-108) for a large H: HH[f1, f2] = sum_i (float)(H[i, f1] *
+    H[i, f2]) summed in double -- each product rounded to float as the reference does, the sum
+    in double (its order differs from the reference's loop only at double rounding).  On `dev`."""
+    import torch
+    Ht = torch.from_numpy(np.ascontiguousarray(H)).to(dev, torch.float32)
+    k = Ht.shape[1]
+    HH = torch.zeros((k, k), dtype=torch.float64, device=dev)
+    for r0 in range(0, Ht.shape[0], chunk):
+        Hc = Ht[r0:r0 + chunk]
+        for f in range(k):
+            HH[f] += (Hc[:, f:f + 1] * Hc).to(torch.float64).sum(0)
+    return HH.cpu().numpy()
+
+
+def wrmf_rows_check(rows, row_ids, col_ids, W, H, k, alpha=1.0, reg=0.015,
+                    reference_products=False):
     """Checker for a library WRMF half-step at full size (the oracle solves only the sampled rows):
     rows = sorted row ids; row_ids / col_ids = the distinct (row, col) entries of the half's CSR
     (torch tensors on the GPU, or numpy); W = the library's solved rows' matrix, H = the matrix it
     solved from.  Each sampled row is solved by WRMF.Optimize(u) (WRMF.cs:110-156) in fp64 with
     exact float products (ora_wrmf_optimize_rows_exact), HH = H^T H in fp64 (on the GPU when H is
-    large).  Returns per-row max |W_lib - W_oracle| / (1 + max |W_oracle|)."""
+    large) -- or, with reference_products, with the reference's own arithmetic: every product
+    rounded to float before its double sum, in HH (wrmf_square_float_products) and in the row's
+    Gram (ora_wrmf_optimize_rows, WRMF.cs:98-106, 116-124).  Returns per-row
+    max |W_lib - W_oracle| / (1 + max |W_oracle|)."""
     import torch
     rows = np.asarray(rows, np.int64)
     dev = row_ids.device if isinstance(row_ids, torch.Tensor) else torch.device("cpu")
-    Ht = torch.from_numpy(np.ascontiguousarray(H)).to(dev, torch.float64)
-    HH = (Ht.T @ Ht).cpu().numpy()
-    del Ht
+    if reference_products:
+        HH = wrmf_square_float_products(H, dev)
+    else:
+        Ht = torch.from_numpy(np.ascontiguousarray(H)).to(dev, torch.float64)
+        HH = (Ht.T @ Ht).cpu().numpy()
+        del Ht
     r_t = row_ids if isinstance(row_ids, torch.Tensor) else torch.from_numpy(row_ids)
     c_t = col_ids if isinstance(col_ids, torch.Tensor) else torch.from_numpy(col_ids)
     n_rows = int(max(int(r_t.max().item()) + 1, rows.max() + 1))
@@ -973,8 +995,9 @@ def wrmf_rows_check(rows, row_ids, col_ids, W, H, k, alpha=1.0, reg=0.015):
     off[1:] = np.cumsum(np.searchsorted(r_, rows, side="right") -
                         np.searchsorted(r_, rows, side="left"))
     Wr = np.zeros((len(rows), k), np.float32)
-    lib().ora_wrmf_optimize_rows_exact(_p(off, _i64p), _p(c_, _i32p), 0, len(rows), len(rows),
-                                       _p(Wr, _f32p), _p(f32(H), _f32p), _p(HH, _f64p), k,
-                                       float(alpha), float(reg))
+    solve = lib().ora_wrmf_optimize_rows if reference_products else \
+        lib().ora_wrmf_optimize_rows_exact
+    solve(_p(off, _i64p), _p(c_, _i32p), 0, len(rows), len(rows), _p(Wr, _f32p),
+          _p(f32(H), _f32p), _p(HH, _f64p), k, float(alpha), float(reg))
     got = np.asarray(W)[rows]
     return np.abs(got - Wr).max(1) / (1.0 + np.abs(Wr).max(1))

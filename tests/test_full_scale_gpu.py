@@ -91,7 +91,8 @@ def _bucket_rows(deg, picks, rs):
 def test_c5_row_solves_match_oracle_at_full_size():
     """WRMF C5 (5M x 500k, 500M events, k = 256, fp64 mode), one iteration; sampled
     user rows (solved from V_0) and item rows (solved from U_1) vs the oracle's fp64 row solve with
-    exact float products (the system the fp64 refinement solves), HH = H^T H in fp64."""
+    exact float products (the system the fp64 refinement solves), HH = H^T H in fp64 -- and vs the
+    reference's own arithmetic (float-rounded products, ComputeSquareMatrix's HH), both <= 2e-7."""
     import torch
     from mymedialite_amd.synthetic import c5_events
     dev = torch.device("cuda:0")
@@ -127,9 +128,16 @@ def test_c5_row_solves_match_oracle_at_full_size():
             ("item", V1, U1, deg_i, [(1, 128, 24), (129, 8192, 24), (8193, 40000, 16)])):
         rows = _bucket_rows(deg, picks, rs)
         t1 = time.perf_counter()
-        rel = O.wrmf_rows_check(rows, *((ku, ki) if side == "user" else (ki, ku)), W, H, k)
-        worst[side] = float(rel.max())
+        ids = (ku, ki) if side == "user" else (ki, ku)
+        rel = O.wrmf_rows_check(rows, *ids, W, H, k)
+        # the same rows against the reference's own arithmetic (every product
+        # rounded to float before its double sum, WRMF.cs:98-106, 116-124)
+        rel_ref = O.wrmf_rows_check(rows, *ids, W, H, k, reference_products=True)
+        worst[side] = (float(rel.max()), float(rel_ref.max()))
         _log(f"C5 {side} rows: {len(rows)} (deg {int(deg[rows].min())}..{int(deg[rows].max())}), "
-             f"max |dW| / (1 + |W|) = {rel.max():.3e} (oracle {time.perf_counter() - t1:.1f} s)")
+             f"max |dW| / (1 + |W|) = {rel.max():.3e} vs exact products, {rel_ref.max():.3e} vs "
+             f"the reference's float products (oracle {time.perf_counter() - t1:.1f} s)")
         assert rel.max() <= 2e-7, (side, rows[np.argmax(rel)], deg[rows[np.argmax(rel)]])
-    _log(f"C5 row check max relative error: {worst}")
+        assert rel_ref.max() <= 2e-7, (side, rows[np.argmax(rel_ref)],
+                                       deg[rows[np.argmax(rel_ref)]])
+    _log(f"C5 row check max relative error (exact products, reference products): {worst}")

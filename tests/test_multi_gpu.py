@@ -462,53 +462,3 @@ def test_bmf_user_shards_device_data_equals_host_data():
         ctx.close()
     for a, b in zip(*out):
         np.testing.assert_array_equal(a, b)
-
-
-def test_c4_model_averaging_cost_on_hip():
-    """the full C4 set (1B ratings, 10M users x 100k items, the 64 seeded chunks of
-    bench.py) trained 3 epochs by one handle (N = 1) and by 8 user shards on one GPU (the N = 8
-    decomposition emulated: each shard trains its eighth with the whole GPU, then the library
-    averages V || b_i), both from the same device InitModel.  Prints and bounds the test-RMSE cost
-    of 8-way averaging at C4 scale."""
-    import time
-    import torch
-    from mymedialite_amd.synthetic import c4_chunks
-    dev = torch.device("cuda:0")
-    n_total, nu, ni, k = 1_000_000_000, 10_000_000, 100_000, 64
-    (users, items, values), (tu, ti, tv), _ = c4_chunks(0, 1, n_total, nu, ni, 1_000_000, dev)
-    mean = float(values.double().mean().item())
-    avg = np.float32((np.float32(mean) - np.float32(1.0)) / np.float32(4.0))
-    gb = float(np.float32(np.log(avg / (1 - avg))))
-    tus, tis, tvs = tu.cpu().numpy(), ti.cpu().numpy(), tv.cpu().numpy()
-    res = {}
-    for nd in (1, 8):
-        ctx = N.Context(0 if nd == 1 else [0] * nd)
-        p = N.BmfParams(k, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
-        h = N._vp()
-        N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(p), nu, ni, ctypes.byref(h)))
-        N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
-                                                values.data_ptr(), n_total, None))
-        N.check(N.lib().mml_bmf_init_model(h, 4, 0.0, 0.1, gb, 1.0, 5.0))
-        rm, ep_ms, ar_ms = [], [], []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            N.check(N.lib().mml_bmf_iterate(h, 0.01, None))
-            ep_ms.append((time.perf_counter() - t0) * 1e3)
-            if nd > 1:
-                x = np.zeros(1, np.float32)
-                N.check(N.lib().mml_bmf_last_allreduce_ms(h, N.ptr(x, N._f32p)))
-                ar_ms.append(float(x[0]))
-            out = np.zeros(2, np.float32)
-            N.check(N.lib().mml_bmf_evaluate(h, N.ptr(tus, N._i32p), N.ptr(tis, N._i32p),
-                                             N.ptr(tvs, N._f32p), len(tus), N.ptr(out, N._f32p)))
-            rm.append(float(out[0]))
-        res[nd] = rm
-        print(f"C4 N={nd}: test RMSE per epoch {rm}, host ms per epoch {ep_ms}, average ms {ar_ms}")
-        N.lib().mml_bmf_destroy(h)
-        ctx.close()
-        torch.cuda.empty_cache()
-    d = [b - a for a, b in zip(res[1], res[8])]
-    print(f"C4 RMSE cost of 8-way averaging per epoch: {d}")
-    assert all(r < 0.76 for r in res[8])  # both learn (initial test RMSE 0.757)
-    assert res[8][-1] < res[8][0] and res[1][-1] < res[1][0]
-    assert all(x < 0.05 for x in d), d

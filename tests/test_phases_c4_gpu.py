@@ -1,0 +1,362 @@
+"""The headline's Hogwild schedule pinned against the oracle on a C4-shaped set.
+
+C4 (bench.py) runs BiasedMF k=64 Hogwild over 10 M users x 100 k items in 26 user phases
+(bmf.hip hogwild_phases: one phase per 96 MiB of active user rows).  The phases only reorder the
+epoch's visit: phase-major, XCD-group minor, the RandomIndex order kept inside a span.  This set
+has C4's users and items, so the default is the same 26 phases, with 100 M ratings (10 per user).
+
+The library exports the stream its launches walked (mml_bmf_hogwild_stream). The oracle runs over
+exactly that stream from the GPU's InitModel, twice:
+  * the sequential Iterate() (ora_bmf_iterate = BiasedMatrixFactorization.cs:264-310): what the
+    order alone costs the reference's own loop. The phase-order lag is oracle(P) - oracle(1);
+  * hogwild_band's staleness model (ora_bmf_iterate_lockstep): each launch = one phase, cut into
+    the launch's waves, 4 ratings per wave step.
+Per epoch, the GPU at 1, 8 and 26 (default) phases must sit between the sequential oracle on its own
+order and twice the staleness model's offset. The slack is 3x the GPU's run-to-run spread + 2e-5
+on both sides (hogwild_band's rule; each configuration trains twice). Every lag is printed. The
+stream itself is checked to hold every rating once, each item in one XCD group's spans only, and
+each user in one phase only.
+
+The second test pins C4's 8-way user-shard averaging (bench.py at N = 8) the same
+way. Eight shards on one GPU (the repeated-device context, one phase) train and average V || b_i
+after every epoch. The oracle does the same: 8 user shards over the one-phase stream, sequential
+and lockstep, then their average. The GPU's 8-shard run and its one-handle run must each sit in
+their band. Their difference, the averaging cost, is printed beside the oracle's.
+"""
+import ctypes
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import oracle as O
+from mymedialite_amd import _native as N
+
+# the oracle's runs: about 1 minute (100 M) and 2 minutes (1 B) on the box's cores
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1200)]
+
+NU, NI, N_TRAIN, N_TEST, K, EPOCHS = 10_000_000, 100_000, 100_000_000, 1_000_000, 64, 3
+LR, SEED = 0.01, 4
+
+
+def _say(msg):
+    print(msg, flush=True)
+    sys.stdout.flush()
+
+
+@pytest.fixture(scope="module")
+def c4_shaped():
+    import torch
+    from mymedialite_amd.synthetic import planted_ratings_torch
+    dev = torch.device("cuda:0")
+    users, items, values = planted_ratings_torch(NU, NI, N_TRAIN, seed=41, device=dev)
+    test = tuple(x.cpu().numpy() for x in planted_ratings_torch(NU, NI, N_TEST, seed=42,
+                                                                 device=dev))
+    # Train(): the global bias from Ratings.Average (BiasedMatrixFactorization.cs:186-190)
+    mean = float(np.float32(values.double().sum().item() / N_TRAIN))
+    avg = np.float32((np.float32(mean) - np.float32(1.0)) / np.float32(4.0))
+    gb = float(np.float32(np.log(avg / (1 - avg))))
+    yield (users, items, values), test, gb
+    del users, items, values
+    torch.cuda.empty_cache()
+
+
+def _results(jobs):
+    """Waits for the oracle jobs, with a line every 30 s (a silent run reads as hung)."""
+    from concurrent.futures import wait
+    t0 = time.perf_counter()
+    while True:
+        done, pending = wait(list(jobs.values()), timeout=30)
+        if not pending:
+            return {key: f.result() for key, f in jobs.items()}
+        _say(f"  ... oracle: {len(done)} of {len(jobs)} runs done ({time.perf_counter() - t0:.0f} s)")
+
+
+def _evaluate(h, test):
+    tu, ti, tv = test
+    out = np.zeros(2, np.float32)
+    N.check(N.lib().mml_bmf_evaluate(h, N.ptr(tu, N._i32p), N.ptr(ti, N._i32p),
+                                     N.ptr(tv, N._f32p), len(tu), N.ptr(out, N._f32p)))
+    return float(out[0])
+
+
+def _gpu(data, test, gb, *, phases=0, devices=0, want_init=False, want_stream=False):
+    """One training run: RMSE after each epoch; optionally the InitModel and the exported stream."""
+    users, items, values = data
+    n = users.numel()
+    ctx = N.Context(devices)
+    p = N.BmfParams(K, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
+    h = N._vp()
+    N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(p), NU, NI, ctypes.byref(h)))
+    out = {}
+    try:
+        N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
+                                                values.data_ptr(), n, None))
+        N.check(N.lib().mml_bmf_set_hogwild_phases(h, phases))
+        N.check(N.lib().mml_bmf_init_model(h, SEED, 0.0, 0.1, gb, 1.0, 5.0))
+        if want_init:
+            m = (np.empty((NU, K), np.float32), np.empty((NI, K), np.float32),
+                 np.empty(NU, np.float32), np.empty(NI, np.float32))
+            N.check(N.lib().mml_bmf_get_model(h, *[N.ptr(a, N._f32p) for a in m]))
+            out["init"] = m
+        rmse = []
+        for _ in range(EPOCHS):
+            N.check(N.lib().mml_bmf_iterate(h, LR, None))
+            rmse.append(_evaluate(h, test))
+        out["rmse"] = np.array(rmse)
+        used = ctypes.c_int32(0)
+        N.check(N.lib().mml_bmf_last_phases(h, ctypes.byref(used)))
+        out["phases"] = used.value
+        if want_stream:
+            su = np.empty(n, np.int32)
+            si = np.empty(n, np.int32)
+            sv = np.empty(n, np.float32)
+            off = np.zeros(8 * 32 + 1, np.int64)
+            spans = ctypes.c_int32(0)
+            N.check(N.lib().mml_bmf_hogwild_stream(h, N.ptr(su, N._i32p), N.ptr(si, N._i32p),
+                                                   N.ptr(sv, N._f32p), n,
+                                                   N.ptr(off, N._i64p), len(off),
+                                                   ctypes.byref(spans)))
+            out["stream"] = (su, si, sv, off[: spans.value + 1].copy())
+    finally:
+        N.lib().mml_bmf_destroy(h)
+        ctx.close()
+    return out
+
+
+def _multiset_hash(u, i, v):
+    """Order-independent checksum of the (user, item, rating) triples (wrapping uint64 sum)."""
+    x = (u.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)) ^ \
+        (i.astype(np.uint64) * np.uint64(0xC2B2AE3D27D4EB4F)) ^ \
+        (v.view(np.uint32).astype(np.uint64) << np.uint64(40))
+    x ^= x >> np.uint64(29)
+    x *= np.uint64(0xBF58476D1CE4E5B9)
+    x ^= x >> np.uint64(32)
+    with np.errstate(over="ignore"):
+        return int(np.sum(x, dtype=np.uint64))
+
+
+def _check_stream(stream, P, ref_hash):
+    """Every rating once; each item in the spans of one XCD group; each user in one phase."""
+    su, si, sv, off = stream
+    assert len(off) == 8 * P + 1 and off[0] == 0 and off[-1] == len(su)
+    assert np.all(np.diff(off) >= 0)
+    assert _multiset_hash(su, si, sv) == ref_hash
+    groups_of_item = np.zeros(NI, np.int8)
+    for g in range(8):
+        seen = np.zeros(NI, bool)
+        for ph in range(P):
+            seen[si[off[8 * ph + g]:off[8 * ph + g + 1]]] = True
+        groups_of_item += seen
+    assert groups_of_item.max() == 1, "an item's ratings lie in spans of two XCD groups"
+    phases_of_user = np.zeros(NU, np.int8)
+    for ph in range(P):
+        seen = np.zeros(NU, bool)
+        seen[su[off[8 * ph]:off[8 * ph + 8]]] = True
+        phases_of_user += seen
+    assert phases_of_user.max() == 1, "a user's ratings lie in two phases"
+
+
+def _hogwild_streams(n):
+    """The launch's waves and ratings per wave step at k = 64 (tests/test_edge_cases_gpu.py
+    hogwild_streams; with phases every launch keeps the whole epoch's wave count)."""
+    from test_edge_cases_gpu import hogwild_streams
+    return hogwild_streams(n, K)
+
+
+def _oracle_run(name, init, stream, test, gb, *, lockstep=False, shards=None, epochs=EPOCHS):
+    """The oracle over `stream` = (users, items, ratings, span offsets) from `init`, EPOCHS times;
+    test RMSE per epoch.
+      * lockstep=False: the sequential Iterate() (BiasedMatrixFactorization.cs:264-310) in stream
+        order;
+      * lockstep=True: the staleness model of hogwild_band (ora_bmf_iterate_lockstep): every launch
+        = one phase's 8 spans cut into the launch's waves, 4 ratings per wave step, reads before
+        the step, writes in stream order;
+      * shards = user bounds: each user shard runs over its own ratings (stream order) from the
+        same item side, then V || b_i are averaged over the shards (bench.py at N > 1; the shard's
+        launch has its own wave count)."""
+    U, V, bu, bi = (a.copy() for a in init)
+    su, si, sv, off = stream
+    kw = dict(gb=np.float32(gb), min_rating=np.float32(1.0), range_=np.float32(4.0), lr=LR)
+    tu, ti, tv = test
+
+    def run(idx, U_, V_, bu_, bi_, n_waves):
+        if lockstep:
+            W, R = n_waves
+            O.bmf_iterate_lockstep(su, si, sv, idx, U_, V_, bu_, bi_, streams=W, step=R, **kw)
+        else:
+            O.bmf_iterate(su, si, sv, idx, U_, V_, bu_, bi_, **kw)
+
+    if shards is None:
+        P = (len(off) - 1) // 8
+        launches = [np.arange(off[8 * p], off[8 * p + 8], dtype=np.int32) for p in range(P)]
+        waves = _hogwild_streams(len(su))
+    else:
+        shard_of = np.searchsorted(shards, su, side="right") - 1
+        idx = [np.flatnonzero(shard_of == d).astype(np.int32) for d in range(len(shards) - 1)]
+    rmse = []
+    t0 = time.perf_counter()
+    for e in range(epochs):
+        if shards is None:
+            for x in launches:
+                run(x, U, V, bu, bi, waves)
+        else:
+            parts = [(V.copy(), bi.copy()) for _ in idx]
+
+            def one(d):
+                run(idx[d], U, parts[d][0], bu, parts[d][1], _hogwild_streams(len(idx[d])))
+            with ThreadPoolExecutor(len(idx)) as ex:  # disjoint user rows, own item copies
+                list(ex.map(one, range(len(idx))))
+            V = parts[0][0].copy()
+            bi = parts[0][1].copy()
+            for pv, pb in parts[1:]:
+                V += pv
+                bi += pb
+            V /= np.float32(len(idx))
+            bi /= np.float32(len(idx))
+        p = O.bmf_predict(tu, ti, U, V, bu, bi, np.float32(gb), np.float32(1.0), np.float32(4.0))
+        rmse.append(O.rating_eval(p, tv)[0])
+        _say(f"  oracle {name}: epoch {e + 1} RMSE {rmse[-1]:.6f} "
+             f"({time.perf_counter() - t0:.0f} s)")
+    return np.array(rmse)
+
+
+@pytest.fixture(scope="module")
+def runs(c4_shaped):
+    """GPU: every configuration twice (one phase, 8, the default 26; 8 user shards averaged, one
+    phase); oracle: the sequential loop and the staleness model on each configuration's stream."""
+    from mymedialite_amd.distributed import balanced_user_shards
+    data, test, gb = c4_shaped
+    users, items, values = (x.cpu().numpy() for x in data)
+    ref_hash = _multiset_hash(users, items, values)
+    del users, items, values
+    gpu, streams, init = {}, {}, None
+    for key, kw in ((1, dict(phases=1)), (8, dict(phases=8)), (26, dict(phases=0)),
+                    ("8 shards", dict(phases=1, devices=[0] * 8))):
+        reps = []
+        for rep in range(2):
+            o = _gpu(data, test, gb, want_init=(key == 1 and rep == 0),
+                     want_stream=(rep == 0 and "devices" not in kw), **kw)
+            init = o.get("init", init)
+            if "stream" in o:
+                assert o["phases"] == key  # 10 M active users x 256 B: 26 phases of 96 MiB
+                streams[key] = o["stream"]
+            reps.append(o["rmse"])
+            _say(f"  gpu {key}{' phases' if key != '8 shards' else ''} run {rep + 1}: "
+                 f"RMSE per epoch {np.round(o['rmse'], 6)}")
+        gpu[key] = np.array(reps)
+    for P, st in streams.items():
+        _check_stream(st, P, ref_hash)
+    bounds = balanced_user_shards(np.bincount(streams[1][0], minlength=NU), 8)
+    jobs = {}
+    with ThreadPoolExecutor(8) as ex:
+        for P, st in streams.items():
+            for ls in (False, True):
+                jobs[(P, ls)] = ex.submit(_oracle_run, f"{P} phases{' lockstep' if ls else ''}",
+                                          init, st, test, gb, lockstep=ls)
+        for ls in (False, True):
+            jobs[("8 shards", ls)] = ex.submit(_oracle_run,
+                                               f"8 shards{' lockstep' if ls else ''}", init,
+                                               streams[1], test, gb, lockstep=ls, shards=bounds)
+        ora = _results(jobs)
+    return gpu, ora
+
+
+def _band(name, gpu_runs, seq, lock, noise, epochs=None):
+    """hogwild_band's RMSE rule (tests/test_edge_cases_gpu.py) per epoch: the GPU between the
+    sequential oracle on its own order and twice the staleness model's offset, on whichever side
+    of the sequential loop the model falls (at 1B ratings its stale reads help: the offset is
+    negative), with 3x the GPU's run-to-run spread (+ 2e-5) of slack on both sides."""
+    g = gpu_runs.mean(axis=0)[:epochs]
+    d, d_lock = g - seq, lock - seq
+    lo = 2 * np.minimum(d_lock, 0) - 3 * noise - 2e-5
+    hi = 2 * np.maximum(d_lock, 0) + 3 * noise + 2e-5
+    ok = bool(np.all((lo <= d) & (d <= hi)))
+    _say(f"{name}: gpu {np.round(g, 6)} oracle {np.round(seq, 6)} gpu - oracle {d} ; staleness "
+         f"model {d_lock} ; band [{lo}, {hi}] -> {'ok' if ok else 'OUT'}")
+    return ok, g
+
+
+def test_phase_lag_pinned_to_the_oracle(runs):
+    gpu, ora = runs
+    noise = max(float(np.max(np.abs(r[0] - r[1]))) for r in gpu.values())
+    _say(f"\ngpu run-to-run spread (max over the configurations): {noise:.2e}")
+    ok, g = {}, {}
+    for P in (1, 8, 26):
+        ok[P], g[P] = _band(f"{P} phases", gpu[P], ora[(P, False)], ora[(P, True)], noise)
+    for P in (8, 26):
+        _say(f"{P} phases, lag vs one phase: oracle (the order alone) "
+             f"{ora[(P, False)] - ora[(1, False)]}, gpu {g[P] - g[1]}")
+    for r in gpu.values():
+        assert np.all(np.diff(r, axis=1) < 0)  # every run learns every epoch
+    assert all(ok.values()), ok
+
+
+def test_eight_shard_average_pinned_to_the_oracle(runs):
+    gpu, ora = runs
+    noise = max(float(np.max(np.abs(r[0] - r[1]))) for r in gpu.values())
+    ok8, g8 = _band("8 user shards averaged", gpu["8 shards"], ora[("8 shards", False)],
+                    ora[("8 shards", True)], noise)
+    ok1, g1 = _band("one handle", gpu[1], ora[(1, False)], ora[(1, True)], noise)
+    _say(f"averaging cost (8 shards - one handle, one phase): gpu {g8 - g1} oracle "
+         f"{ora[('8 shards', False)] - ora[(1, False)]}")
+    assert ok8 and ok1
+
+
+def test_c4_eight_shard_average_at_full_scale():
+    """The full C4 set (1B ratings, 10M users x 100k items, the 64 seeded chunks of bench.py):
+    one handle and 8 user shards on one GPU (the N = 8 decomposition emulated: each shard trains
+    its eighth with the whole GPU, then the library averages V || b_i), one phase, 3 epochs each,
+    twice each, from the same device InitModel.  The oracle at this size (1B sequential updates
+    per epoch) runs the first epoch: the one-handle stream and its 8 user shards, sequential and
+    lockstep.  After epoch 1 both GPU runs sit in their hogwild bands. After epochs 2 and 3 the GPU's
+    averaging cost stays within the oracle's epoch-1 cost + the band's slack. Replaces round 5's bare
+    < 0.05."""
+    import torch
+    from mymedialite_amd.distributed import balanced_user_shards
+    from mymedialite_amd.synthetic import c4_chunks
+    dev = torch.device("cuda:0")
+    n_total = 1_000_000_000
+    (users, items, values), test, _ = c4_chunks(0, 1, n_total, NU, NI, 1_000_000, dev)
+    test = tuple(x.cpu().numpy() for x in test)
+    mean = float(values.double().mean().item())
+    avg = np.float32((np.float32(mean) - np.float32(1.0)) / np.float32(4.0))
+    gb = float(np.float32(np.log(avg / (1 - avg))))
+    data = (users, items, values)
+    gpu, stream, init = {}, None, None
+    for key, kw in ((1, dict(phases=1)), ("8 shards", dict(phases=1, devices=[0] * 8))):
+        reps = []
+        for rep in range(2):
+            o = _gpu(data, test, gb, want_init=(key == 1 and rep == 0),
+                     want_stream=(key == 1 and rep == 0), **kw)
+            init = o.get("init", init)
+            stream = o.get("stream", stream)
+            reps.append(o["rmse"])
+            _say(f"  C4 gpu {key} run {rep + 1}: RMSE per epoch {np.round(o['rmse'], 6)}")
+        gpu[key] = np.array(reps)
+        torch.cuda.empty_cache()
+    del data, users, items, values
+    torch.cuda.empty_cache()
+    bounds = balanced_user_shards(np.bincount(stream[0], minlength=NU), 8)
+    with ThreadPoolExecutor(4) as ex:
+        jobs = {(key, ls): ex.submit(_oracle_run, f"C4 {key}{' lockstep' if ls else ''}", init,
+                                     stream, test, gb, lockstep=ls, epochs=1,
+                                     shards=bounds if key == "8 shards" else None)
+                for key in (1, "8 shards") for ls in (False, True)}
+        ora = _results(jobs)
+    noise = max(float(np.max(np.abs(r[0] - r[1]))) for r in gpu.values())
+    _say(f"\nC4 gpu run-to-run spread: {noise:.2e}")
+    ok8, _ = _band("C4 8 user shards, epoch 1", gpu["8 shards"], ora[("8 shards", False)],
+                   ora[("8 shards", True)], noise, epochs=1)
+    ok1, _ = _band("C4 one handle, epoch 1", gpu[1], ora[(1, False)], ora[(1, True)], noise,
+                   epochs=1)
+    cost_g = gpu["8 shards"].mean(axis=0) - gpu[1].mean(axis=0)
+    cost_o = float(ora[("8 shards", False)][0] - ora[(1, False)][0])
+    _say(f"C4 averaging cost per epoch: gpu {cost_g}; oracle epoch 1 {cost_o:.3e}")
+    assert ok8 and ok1
+    assert np.all(cost_g[1:] <= cost_o + 3 * noise + 2e-5), (cost_g, cost_o)
+    for r in gpu.values():
+        assert np.all(np.diff(r, axis=1) < 0)

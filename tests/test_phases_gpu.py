@@ -75,3 +75,78 @@ def test_user_phases_within_the_visit_order_spread():
     assert (p1, pa, p8) == (1, 3, 8)
     assert np.all(np.abs(auto - one) <= band), (auto - one, band)
     assert one[-1] < one[0] < 1.2  # the set is learnable and learned
+
+
+def _stream(h, n):
+    su, si = np.empty(n, np.int32), np.empty(n, np.int32)
+    sv = np.empty(n, np.float32)
+    off = np.zeros(8 * 32 + 1, np.int64)
+    spans = ctypes.c_int32(0)
+    N.check(N.lib().mml_bmf_hogwild_stream(h, N.ptr(su, N._i32p), N.ptr(si, N._i32p),
+                                           N.ptr(sv, N._f32p), n, N.ptr(off, N._i64p), len(off),
+                                           ctypes.byref(spans)))
+    return su, si, sv, off[: spans.value + 1]
+
+
+def test_phase_count_changes_on_one_handle():
+    """3 -> 8 -> 1 -> 3 phases on ONE handle.  Each epoch's stream (what its launches
+    walked, mml_bmf_hogwild_stream) holds every rating once, keeps each item in the spans of one
+    XCD group (the L2 that owns its row), each user in one phase; and the stream after 3 -> 8 -> 1
+    -> 3 equals the one a fresh handle builds for 3 phases."""
+    import torch
+    from mymedialite_amd.synthetic import planted_ratings_torch
+    nu, ni, n = 800_000, 50_000, 4_000_000
+    users, items, values = planted_ratings_torch(nu, ni, n, seed=23, device=torch.device("cuda:0"))
+    ref = np.sort(users.cpu().numpy().astype(np.int64) * ni + items.cpu().numpy())
+    vsum = float(values.double().sum().item())
+
+    def handle():
+        ctx = N.Context(0)
+        p = N.BmfParams(K, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
+        h = N._vp()
+        N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(p), nu, ni, ctypes.byref(h)))
+        N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
+                                                values.data_ptr(), n, None))
+        N.check(N.lib().mml_bmf_init_model(h, 4, 0.0, 0.1, 0.51, 1.0, 5.0))
+        return ctx, h
+
+    ctx, h = handle()
+    e = np.zeros(0, np.int32)
+    # no Hogwild epoch yet: nothing to export
+    assert N.lib().mml_bmf_hogwild_stream(h, N.ptr(e, N._i32p), N.ptr(e, N._i32p),
+                                          N.ptr(np.zeros(0, np.float32), N._f32p), n,
+                                          N.ptr(np.zeros(300, np.int64), N._i64p), 300,
+                                          ctypes.byref(ctypes.c_int32())) == -1
+    last = None
+    for P in (3, 8, 1, 3):
+        N.check(N.lib().mml_bmf_set_hogwild_phases(h, P))
+        N.check(N.lib().mml_bmf_iterate(h, 0.01, None))
+        su, si, sv, off = _stream(h, n)
+        assert len(off) == 8 * P + 1 and off[0] == 0 and off[-1] == n
+        assert np.array_equal(np.sort(su.astype(np.int64) * ni + si), ref)
+        assert float(sv.astype(np.float64).sum()) == vsum
+        g_of = np.repeat(np.arange(8 * P) % 8, np.diff(off)).astype(np.int8)
+        lo = np.full(ni, 9, np.int8)
+        hi = np.full(ni, -1, np.int8)
+        np.minimum.at(lo, si, g_of)
+        np.maximum.at(hi, si, g_of)
+        used = lo <= 7
+        assert np.array_equal(lo[used], hi[used]), f"{P} phases: an item in two XCD groups' spans"
+        p_of = np.repeat(np.arange(8 * P) // 8, np.diff(off)).astype(np.int8)
+        plo = np.full(nu, 127, np.int8)
+        phi = np.full(nu, -1, np.int8)
+        np.minimum.at(plo, su, p_of)
+        np.maximum.at(phi, su, p_of)
+        used = phi >= 0
+        assert np.array_equal(plo[used], phi[used]), f"{P} phases: a user in two phases"
+        last = (su, si, sv, off)
+    N.lib().mml_bmf_destroy(h)
+    ctx.close()
+    ctx, h = handle()
+    N.check(N.lib().mml_bmf_set_hogwild_phases(h, 3))
+    N.check(N.lib().mml_bmf_iterate(h, 0.01, None))
+    fresh = _stream(h, n)
+    N.lib().mml_bmf_destroy(h)
+    ctx.close()
+    for a, b in zip(last, fresh):
+        assert np.array_equal(a, b)

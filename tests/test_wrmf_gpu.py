@@ -275,7 +275,7 @@ def test_wrmf_item_pipeline_equals_serial_bit_for_bit():
     nu, ni, k = 400_000, 40_000, 256
     users, items = c5_events(nu, ni, 100, torch.device("cuda:0"))
     n = int(users.numel())
-    torch.cuda.synchronize()  # generated on torch's stream; the library reads on its own
+    # generated on torch's stream: mml_wrmf_set_data_device waits for it (no caller-side sync)
     out = {}
     for ranges in (1, 0, 7):
         ctx = N.Context(0)
