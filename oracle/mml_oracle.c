@@ -227,12 +227,15 @@ void ora_bmf_iterate(const ora_bmf_params* p, const int32_t* users, const int32_
  * GPU kernel); at step t every stream takes its next R ratings.  All ratings of a step read the
  * model as it was before the step (ora_bmf_iterate's arithmetic on those values), then their
  * results are written in stream order, so a later stream's write of a row replaces an earlier
- * one's (the lost update of two wavefronts writing one row).  W = 1, R = 1 is ora_bmf_iterate. */
+ * one's (the lost update of two wavefronts writing one row).  W = 1, R = 1 is ora_bmf_iterate.
+ * threads: how many threads compute a step's updates (the result does not depend on it). */
 void ora_bmf_iterate_lockstep(const ora_bmf_params* p, const int32_t* users, const int32_t* items,
                               const float* values, const int32_t* idx, int64_t n_idx, float* U,
                               float* V, float* bu, float* bi, const int32_t* count_by_user,
-                              const int32_t* count_by_item, int32_t W, int32_t R) {
+                              const int32_t* count_by_item, int32_t W, int32_t R,
+                              int32_t threads) {
     const int k = p->k;
+    const int nt = threads > 0 ? threads : 1;
     const int64_t per = (n_idx + W - 1) / W;
     const int64_t cap = (int64_t)W * R;
     float* nu = (float*)malloc(sizeof(float) * (size_t)cap * (k + 1));
@@ -249,8 +252,9 @@ void ora_bmf_iterate_lockstep(const ora_bmf_params* p, const int32_t* users, con
                 sp[m++] = pos;
             }
         /* every rating of the step from the model before the step: independent, so on threads
-         * (OpenMP); the results land in the step's buffers, the model is not touched */
-#pragma omp parallel for schedule(static)
+         * (OpenMP, `threads` of them); the results land in the step's buffers, the model is not
+         * touched */
+#pragma omp parallel for schedule(static) num_threads(nt) if (nt > 1)
         for (int64_t x = 0; x < m; ++x) {
             const int32_t index = idx[sp[x]], u = users[index], i = items[index];
             float* Uo = nu + x * (k + 1);

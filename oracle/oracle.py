@@ -43,6 +43,9 @@ def lib():
     if _lib is None:
         if not os.path.exists(_SO):
             build()
+        # idle OpenMP threads of the lockstep model sleep instead of spinning beside the other
+        # oracle runs of a test (read by libgomp when the library loads)
+        os.environ.setdefault("OMP_WAIT_POLICY", "PASSIVE")
         L = ctypes.CDLL(_SO)
         L.ora_rng_sizeof.restype = ctypes.c_size_t
         L.ora_rng_init.argtypes = [ctypes.c_void_p, ctypes.c_int32]
@@ -67,7 +70,8 @@ def lib():
                                       _f32p, _f32p, _f32p, _f32p, _i32p, _i32p]
         L.ora_bmf_iterate_lockstep.argtypes = [ctypes.c_void_p, _i32p, _i32p, _f32p, _i32p,
                                                ctypes.c_int64, _f32p, _f32p, _f32p, _f32p, _i32p,
-                                               _i32p, ctypes.c_int32, ctypes.c_int32]
+                                               _i32p, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_int32]
         L.ora_bmf_dsgd_epoch_mt.argtypes = [ctypes.c_void_p, _i32p, _i32p, _f32p, _i64p, _i32p,
                                             ctypes.c_int32, _i32p, ctypes.c_int32, _f32p, _f32p,
                                             _f32p, _f32p, _i32p, _i32p]
@@ -249,10 +253,11 @@ def bmf_iterate(users, items, values, indices, U, V, bu, bi, *, gb, min_rating, 
 def bmf_iterate_lockstep(users, items, values, indices, U, V, bu, bi, *, streams, step, gb,
                          min_rating, range_, lr, bias_lr=1.0, bias_reg=0.01, reg_u=0.015,
                          reg_i=0.015, loss=0, freq_reg=False, count_by_user=None,
-                         count_by_item=None):
+                         count_by_item=None, threads=1):
     """ora_bmf_iterate_lockstep: Hogwild's staleness restated (``streams`` contiguous chunks of
     the stream, ``step`` ratings each per lockstep step, reads before the step, writes in stream
-    order) -- a model for the tests' Hogwild bands, not a reference behaviour.  In place."""
+    order) -- a model for the tests' Hogwild bands, not a reference behaviour.  In place.
+    ``threads`` compute a step's updates (OpenMP; the result is the same for any count)."""
     k = U.shape[1]
     p = _BmfParams(k, loss, int(freq_reg), 1, 1, gb, min_rating, range_, lr, bias_lr, bias_reg,
                    reg_u, reg_i)
@@ -262,7 +267,7 @@ def bmf_iterate_lockstep(users, items, values, indices, U, V, bu, bi, *, streams
     lib().ora_bmf_iterate_lockstep(ctypes.byref(p), _p(users, _i32p), _p(items, _i32p),
                                    _p(values, _f32p), _p(idx, _i32p), idx.size, _p(U, _f32p),
                                    _p(V, _f32p), _p(bu, _f32p), _p(bi, _f32p), _p(cu, _i32p),
-                                   _p(ci, _i32p), int(streams), int(step))
+                                   _p(ci, _i32p), int(streams), int(step), int(threads))
 
 
 def bmf_dsgd_epoch_mt(users, items, values, blocks, subepochs, n_threads, U, V, bu, bi, *, gb,

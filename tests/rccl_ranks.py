@@ -1,4 +1,4 @@
-"""TEST INFRASTRUCTURE ONLY -- the library's RCCL communicator branches at 2-4 ranks on one GPU.
+"""TEST INFRASTRUCTURE ONLY -- the library's RCCL communicator branches at 2-8 ranks on one GPU.
 
 Run by tests/test_rccl_standin_gpu.py in a fresh subprocess with MML_LIB_PATH pointing at
 tests/rccl_standin/libmml_hip_standin.so: libmml_hip.so's own objects linked against the checking
@@ -96,10 +96,17 @@ def cpp_bounds(users, n_users, parts):
     return b
 
 
-def ratings(seed=21, nu=600, ni=250, n=30000, k=16):
+def ratings(seed=21, nu=600, ni=250, n=30000, k=16, zipf=False):
+    """Uniform users; items uniform, or (zipf) C4's Zipf(0.8) popularity over a permutation
+    (SURVEY 8(d)), so the user-shard bounds split a C4-shaped set."""
     rs = np.random.default_rng(seed)
     u = rs.integers(0, nu, n).astype(np.int32)
-    i = rs.integers(0, ni, n).astype(np.int32)
+    if zipf:
+        from mymedialite_amd.synthetic import zipf_cdf
+        i = rs.permutation(ni)[np.minimum(np.searchsorted(zipf_cdf(ni, 0.8), rs.random(n)),
+                                          ni - 1)].astype(np.int32)
+    else:
+        i = rs.integers(0, ni, n).astype(np.int32)
     v = rs.integers(1, 6, n).astype(np.float32)
     U = rs.normal(0, 0.1, (nu, k)).astype(np.float32)
     V = rs.normal(0, 0.1, (ni, k)).astype(np.float32)
@@ -129,8 +136,9 @@ def bmf_set_model(h, U, V, nu, ni, gb=0.3):
                                 N.ptr(np.zeros(ni, np.float32), N._f32p), gb, 1.0, 5.0))
 
 
-def scenario_bmf_average(nd, epochs=3):
-    u, i, v, U, V, nu, ni, k = ratings(21 + nd)
+def scenario_bmf_average(nd, epochs=3, c4_shaped=False):
+    u, i, v, U, V, nu, ni, k = (ratings(21 + nd, nu=20000, ni=2000, n=200000, k=64, zipf=True)
+                                if c4_shaped else ratings(21 + nd))
     params = N.BmfParams(k, N.LOSS_RMSE, 0, N.SCHEDULE_ORDERED, 1.0, 0.01, 0.015, 0.015)
     ctx = N.Context([0] * nd)
     h = bmf_create(ctx, params, nu, ni)
@@ -284,8 +292,9 @@ def scenario_wrmf(nd, k, passes, iters=2):
 
 
 # ------------------------------------------------------------------ DSGD ring
-def scenario_ring(nd, G, epochs=3):
-    u, i, v, U, V, nu, ni, k = ratings(40 + nd, n=40000)
+def scenario_ring(nd, G, epochs=3, c4_shaped=False):
+    u, i, v, U, V, nu, ni, k = (ratings(40 + nd, nu=20000, ni=2000, n=200000, k=64, zipf=True)
+                                if c4_shaped else ratings(40 + nd, n=40000))
     params = N.BmfParams(k, N.LOSS_RMSE, 0, N.SCHEDULE_DSGD, 1.0, 0.01, 0.015, 0.015)
     rng = SystemRandom(1)
     off = np.zeros(G * G + 1, np.int64)
@@ -407,7 +416,13 @@ def main():
                      ("bmf4", lambda: scenario_bmf_average(4)),
                      ("bpr4", lambda: scenario_bpr_average(4)),
                      ("wrmf4_k256", lambda: scenario_wrmf(4, 256, 3)),
-                     ("ring4", lambda: scenario_ring(4, 8))):
+                     ("ring4", lambda: scenario_ring(4, 8)),
+                     # the deployment width: 8 ranks, C4-shaped user shards
+                     ("bmf8", lambda: scenario_bmf_average(8, c4_shaped=True)),
+                     ("bpr8", lambda: scenario_bpr_average(8)),
+                     ("wrmf8_k256", lambda: scenario_wrmf(8, 256, 3)),
+                     ("ring8", lambda: scenario_ring(8, 8, c4_shaped=True)),
+                     ("ring8_g16", lambda: scenario_ring(8, 16))):
         t1 = time.perf_counter()
         before = report()
         msg = fn()

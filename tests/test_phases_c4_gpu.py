@@ -167,7 +167,8 @@ def _hogwild_streams(n):
     return hogwild_streams(n, K)
 
 
-def _oracle_run(name, init, stream, test, gb, *, lockstep=False, shards=None, epochs=EPOCHS):
+def _oracle_run(name, init, stream, test, gb, *, lockstep=False, shards=None, epochs=EPOCHS,
+                threads=1):
     """The oracle over `stream` = (users, items, ratings, span offsets) from `init`, EPOCHS times;
     test RMSE per epoch.
       * lockstep=False: the sequential Iterate() (BiasedMatrixFactorization.cs:264-310) in stream
@@ -186,7 +187,8 @@ def _oracle_run(name, init, stream, test, gb, *, lockstep=False, shards=None, ep
     def run(idx, U_, V_, bu_, bi_, n_waves):
         if lockstep:
             W, R = n_waves
-            O.bmf_iterate_lockstep(su, si, sv, idx, U_, V_, bu_, bi_, streams=W, step=R, **kw)
+            O.bmf_iterate_lockstep(su, si, sv, idx, U_, V_, bu_, bi_, streams=W, step=R,
+                                   threads=threads, **kw)
         else:
             O.bmf_iterate(su, si, sv, idx, U_, V_, bu_, bi_, **kw)
 
@@ -251,17 +253,16 @@ def runs(c4_shaped):
     for P, st in streams.items():
         _check_stream(st, P, ref_hash)
     bounds = balanced_user_shards(np.bincount(streams[1][0], minlength=NU), 8)
-    jobs = {}
-    with ThreadPoolExecutor(8) as ex:
-        for P, st in streams.items():
-            for ls in (False, True):
-                jobs[(P, ls)] = ex.submit(_oracle_run, f"{P} phases{' lockstep' if ls else ''}",
-                                          init, st, test, gb, lockstep=ls)
-        for ls in (False, True):
-            jobs[("8 shards", ls)] = ex.submit(_oracle_run,
-                                               f"8 shards{' lockstep' if ls else ''}", init,
-                                               streams[1], test, gb, lockstep=ls, shards=bounds)
-        ora = _results(jobs)
+    # the box's 16 cores: the three orders, sequential (1 thread each) and lockstep (4 each),
+    # then the 8 user shards (8 threads each way)
+    with ThreadPoolExecutor(6) as ex:
+        ora = _results({(P, ls): ex.submit(_oracle_run, f"{P} phases{' lockstep' if ls else ''}",
+                                           init, st, test, gb, lockstep=ls, threads=4)
+                        for P, st in streams.items() for ls in (False, True)})
+    with ThreadPoolExecutor(2) as ex:
+        ora.update(_results({("8 shards", ls): ex.submit(
+            _oracle_run, f"8 shards{' lockstep' if ls else ''}", init, streams[1], test, gb,
+            lockstep=ls, shards=bounds) for ls in (False, True)}))
     return gpu, ora
 
 
@@ -341,12 +342,20 @@ def test_c4_eight_shard_average_at_full_scale():
     del data, users, items, values
     torch.cuda.empty_cache()
     bounds = balanced_user_shards(np.bincount(stream[0], minlength=NU), 8)
-    with ThreadPoolExecutor(4) as ex:
-        jobs = {(key, ls): ex.submit(_oracle_run, f"C4 {key}{' lockstep' if ls else ''}", init,
-                                     stream, test, gb, lockstep=ls, epochs=1,
-                                     shards=bounds if key == "8 shards" else None)
-                for key in (1, "8 shards") for ls in (False, True)}
+    # the one-handle epoch (sequential: 1 core; lockstep: 8) beside the shards' (8 cores each
+    # way, one after the other)
+    with ThreadPoolExecutor(3) as ex:
+        jobs = {(1, ls): ex.submit(_oracle_run, f"C4 1{' lockstep' if ls else ''}", init, stream,
+                                   test, gb, lockstep=ls, epochs=1, threads=8)
+                for ls in (False, True)}
+
+        def shards():
+            return {("8 shards", ls): _oracle_run(f"C4 8 shards{' lockstep' if ls else ''}",
+                                                  init, stream, test, gb, lockstep=ls, epochs=1,
+                                                  shards=bounds) for ls in (False, True)}
+        jobs["shards"] = ex.submit(shards)
         ora = _results(jobs)
+        ora.update(ora.pop("shards"))
     noise = max(float(np.max(np.abs(r[0] - r[1]))) for r in gpu.values())
     _say(f"\nC4 gpu run-to-run spread: {noise:.2e}")
     ok8, _ = _band("C4 8 user shards, epoch 1", gpu["8 shards"], ora[("8 shards", False)],

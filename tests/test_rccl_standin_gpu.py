@@ -1,4 +1,5 @@
-"""The library's RCCL communicator branches at 2-4 ranks on one GPU.
+"""The library's RCCL communicator branches at 2-8 ranks on one GPU (8 ranks,
+the deployment width).
 
 tests/rccl_ranks.py runs in a fresh subprocess with libmml_hip_standin.so (the library's own
 objects linked against the checking stand-in tests/rccl_standin/standin.cpp instead of librccl):
@@ -36,11 +37,12 @@ def test_communicator_branches_equal_peer_transport():
     assert res["ok"] and not rep["errors"] and rep["unmatched_sends"] == 0, rep
     calls = {s["scenario"]: s["calls"] for s in res["scenarios"]}
     # every communicator branch ran: the averages, the all-gathers, the ring's transfers
-    for name in ("bmf2", "bmf3", "bmf4", "bpr2", "bpr3", "bpr4"):
+    for name in ("bmf2", "bmf3", "bmf4", "bmf8", "bpr2", "bpr3", "bpr4", "bpr8"):
         assert calls[name]["allreduce"] > 0, calls[name]
-    for name in ("wrmf2_k64", "wrmf2_k256", "wrmf3_k256", "wrmf4_k256"):
+    for name in ("wrmf2_k64", "wrmf2_k256", "wrmf3_k256", "wrmf4_k256", "wrmf8_k256"):
         assert calls[name]["broadcast"] > 0, calls[name]
     assert calls["wrmf2_k256"]["allreduce"] > 0  # the refinement's ncclMax decisions
-    for name in ("ring2", "ring3", "ring4"):
+    assert calls["wrmf8_k256"]["allreduce"] > 0
+    for name in ("ring2", "ring3", "ring4", "ring8", "ring8_g16"):
         assert calls[name]["send"] > 0 and calls[name]["send"] == calls[name]["recv"], calls[name]
         assert calls[name]["broadcast"] > 0, calls[name]
