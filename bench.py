@@ -279,7 +279,6 @@ def bench_c2(args):
                                        if ring else f"user-shard x{world}")},
             "final_rmse": rmse,
             "initial_rmse": rmse0,
-            "slice_epoch_rmse": slice_rmse,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_note": traffic_note,
