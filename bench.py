@@ -430,7 +430,7 @@ def cpu_baseline_dsgd(model, k, n_users, n_items, gb, sample, name, test=None):
 def gpu_slice_epoch(model, k, n_users, n_items, gb, sample, test):
     """The GPU beside cpu_baseline_dsgd: a handle over the same slice, set_model(InitModel), one
     default HOGWILD epoch, the test RMSE (mml_bmf_evaluate) -- the library's number for the same
-    epoch from the same start."""
+    epoch from the same start -- and the stream that epoch walked (mml_bmf_hogwild_stream)."""
     u, i, v = sample
     ctx = N.Context(0)
     params = N.BmfParams(k, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
@@ -450,10 +450,56 @@ def gpu_slice_epoch(model, k, n_users, n_items, gb, sample, test):
                                          N.ptr(tv, N._f32p), len(tu), N.ptr(out, N._f32p)))
         phases = ctypes.c_int32(0)
         N.check(N.lib().mml_bmf_last_phases(h, ctypes.byref(phases)))
-        return float(out[0]), phases.value
+        n = len(u)
+        su, si, sv = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.float32)
+        off = np.zeros(8 * 32 + 1, np.int64)
+        spans = ctypes.c_int32(0)
+        N.check(N.lib().mml_bmf_hogwild_stream(h, N.ptr(su, N._i32p), N.ptr(si, N._i32p),
+                                               N.ptr(sv, N._f32p), n, N.ptr(off, N._i64p),
+                                               len(off), ctypes.byref(spans)))
+        return float(out[0]), phases.value, (su, si, sv, off[: spans.value + 1].copy())
     finally:
         N.lib().mml_bmf_destroy(h)
         ctx.close()
+
+
+def oracle_slice_epochs(model, k, gb, sample, stream, test):
+    """The reference's own loop beside gpu_slice_epoch, from the same InitModel, one epoch each,
+    test RMSE: the sequential Iterate() (BiasedMatrixFactorization.cs:264-310) over the stream
+    the GPU walked, and over the slice's own visit order; and the Hogwild staleness model of the
+    tests (ora_bmf_iterate_lockstep: each phase one launch of the GPU's waves, 4 ratings per wave
+    step) over the GPU's stream."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    kw = dict(gb=np.float32(gb), min_rating=np.float32(1), range_=np.float32(4), lr=0.01)
+    tu, ti, tv = test
+    su, si, sv, off = stream
+    n = len(su)
+    waves = min(256 * 32, max(1, n // 12000))
+    waves = -(-((waves + 3) // 4) // 8) * 8 * 4  # bmf.hip launch_hogwild: blocks of 4, 8 groups
+    lpr = 1
+    while lpr < (k + 3) // 4:
+        lpr *= 2
+
+    def rmse(U, V, bu, bi):
+        p = O.bmf_predict(tu, ti, U, V, bu, bi, np.float32(gb), np.float32(1), np.float32(4))
+        return float(O.rating_eval(p, tv)[0])
+    out = {}
+    t0 = time.perf_counter()
+    m = [a.copy() for a in model]
+    O.bmf_iterate(su, si, sv, np.arange(n, dtype=np.int32), *m, **kw)
+    out["sequential_gpu_order"] = rmse(*m)
+    m = [a.copy() for a in model]
+    for p in range((len(off) - 1) // 8):
+        O.bmf_iterate_lockstep(su, si, sv, np.arange(off[8 * p], off[8 * p + 8], dtype=np.int32),
+                               *m, streams=waves, step=64 // lpr, threads=cpu_threads(), **kw)
+    out["lockstep_gpu_order"] = rmse(*m)
+    u, i, v = sample
+    m = [a.copy() for a in model]
+    O.bmf_iterate(u, i, v, np.arange(len(u), dtype=np.int32), *m, **kw)
+    out["sequential_visit_order"] = rmse(*m)
+    out["seconds"] = time.perf_counter() - t0
+    return out
 
 
 def c4_shard(rank, world, n_total, n_users, n_items, n_test, device, chunks=64):
@@ -578,17 +624,28 @@ def bench_c4(args):
         m_t = seen[tus]
         slice_test = (tus[m_t].copy(), tis[m_t].copy(), tvs[m_t].copy())
         cpu = cpu_baseline_dsgd(init, k, n_users, n_items, gb, cpu_sample, "C4", slice_test)
-        g_rmse, g_phases = gpu_slice_epoch(init, k, n_users, n_items, gb, cpu_sample, slice_test)
-        o_rmse = cpu["test_rmse_after_epoch"]
-        slice_rmse = {"gpu": g_rmse, "oracle": o_rmse, "gpu_minus_oracle": g_rmse - o_rmse,
-                      "test_ratings": int(m_t.sum()), "gpu_user_phases": g_phases,
+        g_rmse, g_phases, g_stream = gpu_slice_epoch(init, k, n_users, n_items, gb, cpu_sample,
+                                                     slice_test)
+        ora = oracle_slice_epochs(init, k, gb, cpu_sample, g_stream, slice_test)
+        del g_stream
+        o_seq = ora["sequential_gpu_order"]
+        slice_rmse = {"gpu": g_rmse, "gpu_user_phases": g_phases,
+                      "oracle_sequential_gpu_order": o_seq,
+                      "gpu_minus_oracle_sequential": g_rmse - o_seq,
+                      "oracle_lockstep_gpu_order": ora["lockstep_gpu_order"],
+                      "staleness_model_offset": ora["lockstep_gpu_order"] - o_seq,
+                      "oracle_sequential_visit_order": ora["sequential_visit_order"],
+                      "oracle_dsgd": cpu["test_rmse_after_epoch"],
+                      "test_ratings": int(m_t.sum()),
                       "note": f"one epoch over the cpu_baseline's {len(cpu_sample[0])}-rating slice "
-                              f"from the same InitModel: the GPU's default HOGWILD epoch vs the "
-                              f"oracle's MaxThreads={cpu['cores']} DSGD epoch (the reference's "
-                              f"multi-core schedule, BiasedMatrixFactorization.cs:205-215), test "
-                              f"RMSE on the slice users' test ratings (Eval/Ratings.cs:96-139); the "
-                              f"26-phase order lag at 100M ratings is pinned against the sequential "
-                              f"oracle by tests/test_phases_c4_gpu.py"}
+                              f"from the same InitModel, test RMSE on the slice users' test "
+                              f"ratings (Eval/Ratings.cs:96-139): the GPU's default HOGWILD epoch; "
+                              f"the oracle's sequential Iterate() (BiasedMatrixFactorization.cs:"
+                              f"264-310) over the stream the GPU walked (mml_bmf_hogwild_stream) "
+                              f"and over the slice's visit order; the tests' Hogwild staleness "
+                              f"model on the GPU's stream; the oracle's MaxThreads="
+                              f"{cpu['cores']} DSGD epoch (:205-215). Oracle legs "
+                              f"{ora['seconds']:.0f} s, after the timed region"}
         del init
     line = None
     if rank == 0:

@@ -1,0 +1,126 @@
+"""C5's engine split from rocprofv3 --pmc passes over ONE iteration (scripts/c5_iter.py --iters 1):
+per wrmf_* kernel the matrix-core busy fraction, the matrix-core flops by data type and the VALU
+flops, and the same over the iteration (an honest C5 roofline).
+
+  python scripts/pmc_c5_engines.py <busy dir> <mops dir|-> <valu dir|-> <iteration ms> out.json
+
+Counters (gfx950; MI355X_MICROARCH.md):
+  * SQ_VALU_MFMA_BUSY_CYCLES: matrix-core busy cycles summed over the SIMDs; GRBM_GUI_ACTIVE:
+    GPU-busy cycles summed over the 8 XCDs.  Busy fraction of a dispatch = MFMA_BUSY /
+    (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); of the iteration = sum MFMA_BUSY / (f_clk x iteration wall
+    x 1024), f_clk = sum (GRBM_GUI_ACTIVE / 8) / sum duration over the dispatches.
+  * SQ_INSTS_VALU_MFMA_MOPS_{BF16,F32,F64}: matrix-core math in units of 512 flops.
+  * SQ_INSTS_VALU_{FMA,ADD,MUL}_{F32,F64}: VALU instructions per wave (64 lanes; FMA = 2 flops).
+Peaks (MI355X_MICROARCH.md): BF16 MFMA 2,516.6 TF dense, FP32 MFMA 157.3 TF, FP64 MFMA 78.6 TF,
+FP32 VALU 157.3 TF, FP64 VALU 78.6 TF."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+PEAK_TF = {"mfma_bf16": 2516.6, "mfma_f32": 157.3, "mfma_f64": 78.6, "valu_f32": 157.3,
+           "valu_f64": 78.6}
+
+
+def load(d):
+    """{dispatch: {"kernel", "dur_ns", counters...}} from rocprofv3 csv output."""
+    out = defaultdict(dict)
+    if not d or d == "-" or not os.path.isdir(d):
+        return out
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            x = out[int(r["Dispatch_Id"])]
+            x["kernel"] = r["Kernel_Name"]
+            x["dur_ns"] = float(r.get("End_Timestamp", 0) or 0) - float(r.get("Start_Timestamp", 0) or 0)
+            x[r["Counter_Name"]] = x.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return out
+
+
+def short(name):
+    s = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    depth = 0
+    for x, ch in enumerate(s):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            return s[:x]
+    return s
+
+
+def main():
+    busy_d, mops_d, valu_d, iter_ms, dst = sys.argv[1:6]
+    iter_ms = float(iter_ms)
+    passes = [load(busy_d), load(mops_d), load(valu_d)]
+    kern = defaultdict(lambda: defaultdict(float))
+    for p in passes:
+        for d, x in p.items():
+            if not x.get("kernel", "").replace("void ", "").startswith("wrmf_"):
+                continue
+            k = kern[short(x["kernel"])]
+            for c, v in x.items():
+                if c not in ("kernel", "dur_ns"):
+                    k[c] += v
+            if p is passes[0]:
+                k["dispatches"] += 1
+                k["ms"] += x["dur_ns"] / 1e6
+    rows, tot = {}, defaultdict(float)
+    for name, k in sorted(kern.items(), key=lambda t: -t[1]["ms"]):
+        r = {"dispatches": int(k["dispatches"]), "ms_under_pmc": k["ms"]}
+        g = k.get("GRBM_GUI_ACTIVE", 0.0)
+        if g:
+            r["mfma_busy_frac"] = k.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (g / 8 * 1024)
+            r["clock_GHz"] = g / 8 / (k["ms"] * 1e-3) / 1e9 if k["ms"] else None
+            if k.get("SQ_WAVE_CYCLES"):
+                r["wait_any_over_wave_cycles"] = k.get("SQ_WAIT_ANY", 0.0) / k["SQ_WAVE_CYCLES"]
+        fl = {"mfma_bf16": 512.0 * k.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0),
+              "mfma_f32": 512.0 * k.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0),
+              "mfma_f64": 512.0 * k.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0),
+              "valu_f32": 64.0 * (2 * k.get("SQ_INSTS_VALU_FMA_F32", 0.0) +
+                                  k.get("SQ_INSTS_VALU_ADD_F32", 0.0) +
+                                  k.get("SQ_INSTS_VALU_MUL_F32", 0.0)),
+              "valu_f64": 64.0 * (2 * k.get("SQ_INSTS_VALU_FMA_F64", 0.0) +
+                                  k.get("SQ_INSTS_VALU_ADD_F64", 0.0) +
+                                  k.get("SQ_INSTS_VALU_MUL_F64", 0.0))}
+        r["flops"] = fl
+        for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"):
+            tot[c] += k.get(c, 0.0)
+        tot["ms"] += k["ms"]
+        for e, v in fl.items():
+            tot["flops_" + e] += v
+        rows[name] = r
+    clk = tot["GRBM_GUI_ACTIVE"] / 8 / (tot["ms"] * 1e-3) if tot["ms"] else 0.0
+    it_s = iter_ms * 1e-3
+    engines = {}
+    for e, peak in PEAK_TF.items():
+        f = tot["flops_" + e]
+        engines[e] = {"tflop_per_iteration": f / 1e12, "achieved_tflops": f / it_s / 1e12,
+                      "peak_tflops": peak, "frac": f / it_s / 1e12 / peak}
+    res = {
+        "iteration_ms": iter_ms,
+        "kernels_ms_under_pmc": tot["ms"],
+        "clock_GHz": clk / 1e9,
+        "mfma_busy_frac_iteration": tot["SQ_VALU_MFMA_BUSY_CYCLES"] / (clk * it_s * 1024)
+        if clk else None,
+        "mfma_busy_frac_kernel_time": tot["SQ_VALU_MFMA_BUSY_CYCLES"] /
+        (tot["GRBM_GUI_ACTIVE"] / 8 * 1024) if tot["GRBM_GUI_ACTIVE"] else None,
+        "engines": engines,
+        "kernels": rows,
+        "note": "one C5 iteration (scripts/c5_iter.py --iters 1) under rocprofv3 --pmc, wrmf_* "
+                "dispatches only; iteration_ms from the same script without the profiler; "
+                "mfma_busy_frac_iteration over the iteration's wall time at the counters' mean "
+                "clock, mfma_busy_frac_kernel_time over the kernels' own (serialised) time",
+    }
+    json.dump(res, open(dst, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
+    for name, r in rows.items():
+        print(f"{name:48s} {r['dispatches']:3d} {r['ms_under_pmc']:8.1f} ms  busy "
+              f"{r.get('mfma_busy_frac', float('nan')):.3f}  " +
+              " ".join(f"{e} {v / 1e12:.2f}" for e, v in r["flops"].items() if v))
+
+
+if __name__ == "__main__":
+    main()
