@@ -1,7 +1,7 @@
 """C5 (WRMF k=256, 5M users x 500k items, 500M positives, fp64 mode) for the profilers: data in
 HBM, InitModel, then `--iters` WRMF.Iterate() calls (WRMF.cs:68-73); prints each iteration's device
-ms (mml_wrmf_last_timing).  Under rocprofv3 --pmc run it with --iters 1, so every wrmf_* dispatch of
-the profile belongs to one iteration (scripts/pmc_c5_engines.py).
+ms (mml_wrmf_last_timing).  Under rocprofv3 --pmc run it with --iters 2: scripts/pmc_c5_engines.py
+reads the second iteration's dispatches (the first starts from InitModel).
 
   python scripts/c5_iter.py [--iters N]"""
 import argparse

@@ -1,4 +1,5 @@
-"""C5's engine split from rocprofv3 --pmc passes over ONE iteration (scripts/c5_iter.py --iters 1):
+"""C5's engine split from rocprofv3 --pmc passes over the LAST iteration of scripts/c5_iter.py
+(--iters 2: the first iteration starts from InitModel and runs fewer Chebyshev steps):
 per wrmf_* kernel the matrix-core busy fraction, the matrix-core flops by data type and the VALU
 flops, and the same over the iteration (an honest C5 roofline).
 
@@ -55,11 +56,20 @@ def main():
     busy_d, mops_d, valu_d, iter_ms, dst = sys.argv[1:6]
     iter_ms = float(iter_ms)
     passes = [load(busy_d), load(mops_d), load(valu_d)]
+
+    def last_iteration(p):
+        """The dispatches from the last iteration's first kernel on: its users' half starts with
+        the second-to-last wrmf_gram_partial (one per half-step)."""
+        marks = sorted(d for d, x in p.items() if short(x.get("kernel", "")) ==
+                       "wrmf_gram_partial_kernel")
+        return {d: x for d, x in p.items() if len(marks) < 2 or d >= marks[-2]}
+    passes = [last_iteration(p) for p in passes]
     kern = defaultdict(lambda: defaultdict(float))
     for p in passes:
         for d, x in p.items():
-            if not x.get("kernel", "").replace("void ", "").startswith("wrmf_"):
-                continue
+            nm = short(x.get("kernel", ""))
+            if not nm.startswith("wrmf_") or nm.startswith("wrmf_init_normal"):
+                continue  # the iteration's kernels (not InitModel, not the data set's sorts)
             k = kern[short(x["kernel"])]
             for c, v in x.items():
                 if c not in ("kernel", "dur_ns"):
@@ -109,8 +119,9 @@ def main():
         (tot["GRBM_GUI_ACTIVE"] / 8 * 1024) if tot["GRBM_GUI_ACTIVE"] else None,
         "engines": engines,
         "kernels": rows,
-        "note": "one C5 iteration (scripts/c5_iter.py --iters 1) under rocprofv3 --pmc, wrmf_* "
-                "dispatches only; iteration_ms from the same script without the profiler; "
+        "note": "the last of 2 C5 iterations (scripts/c5_iter.py --iters 2) under rocprofv3 --pmc, "
+                "wrmf_* dispatches only; iteration_ms = the same script's last iteration without "
+                "the profiler; "
                 "mfma_busy_frac_iteration over the iteration's wall time at the counters' mean "
                 "clock, mfma_busy_frac_kernel_time over the kernels' own (serialised) time",
     }
