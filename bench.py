@@ -971,6 +971,9 @@ def bench_wrmf(args):
     }
     if check is not None:
         line.update(check)
+    eng = c5_engine_split(float(np.mean(ms))) if (k == 256 and n_users == 5_000_000) else None
+    if eng is not None:
+        line["roofline"].update(eng)
     if world > 1:
         line["config"]["parallelism"] = f"row shards x{world}, RCCL all-gather per half-step"
         line["allgather_ms"] = float(gather[0])
@@ -980,6 +983,37 @@ def bench_wrmf(args):
     N.lib().mml_wrmf_destroy(h)
     ctx.close()
     return line if rank == 0 else None
+
+
+def c5_engine_split(iter_ms, name="r6_c5_engines.json"):
+    """C5's engines, from the committed PMC passes over one iteration of HEAD
+    (scripts/pmc_c5_engines.py): the iteration's matrix-core busy fraction, and the flops the
+    counters saw per engine (SQ_INSTS_VALU_MFMA_MOPS_* x 512, SQ_INSTS_VALU_{FMA,ADD,MUL}_* x 64)
+    over THIS run's iteration time against each engine's peak.  roofline.frac stays the executed
+    algorithmic flops over the FP32 MFMA peak; these fields say which engine ran them and how busy
+    the matrix cores were."""
+    tf = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(tf):
+        return None
+    t = json.load(open(tf))
+    split = {}
+    for e, v in t["engines"].items():
+        tfl = v["tflop_per_iteration"]
+        split[e] = {"tflop_per_iteration": tfl, "achieved_tflops": tfl / (iter_ms * 1e-3),
+                    "peak_tflops": v["peak_tflops"],
+                    "frac": tfl / (iter_ms * 1e-3) / v["peak_tflops"]}
+    busy = {n: r.get("mfma_busy_frac") for n, r in t["kernels"].items()
+            if r.get("mfma_busy_frac") and r["ms_under_pmc"] > 5.0}
+    return {"mfma_busy_frac": t["mfma_busy_frac_iteration"],
+            "mfma_busy_frac_by_kernel": busy,
+            "engine_split": split,
+            "engine_note": f"profiles/{name}: PMC passes over one C5 iteration of this tree "
+                           f"(scripts/r6/gpu_r6_pmc_c5.sh); mfma_busy_frac = "
+                           f"SQ_VALU_MFMA_BUSY_CYCLES over the iteration's wall time x clock x 1024 "
+                           f"SIMDs; engine_split = the counters' flops per engine (bf16x3 products "
+                           f"counted as the bf16 MFMAs they run as) over this run's iteration time; "
+                           f"roofline.frac (executed algorithmic flops / FP32 MFMA peak) is a rate, "
+                           f"not a matrix-core utilisation"}
 
 
 def c5_gather_traffic(name="r5n_c5_traffic.json"):
