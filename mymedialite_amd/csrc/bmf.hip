@@ -423,6 +423,42 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
         asm volatile("" ::"v"(my_u), "v"(my_i), "v"(my_r));
         const int cnt = (int)min((int64_t)64, end - base);
         // (requesting step t + 1's rows before step t's stores was measured 4 % slower on C2)
+#if defined(MML_HOGWILD_PF) && MML_HOGWILD_PF
+        // (experiments: the same again with the user phases, step t + 1's rows before step t's
+        // update)
+        {
+            float4 pu[VPL], qi[VPL];
+            float bu_u = 0.0f, bi_i = 0.0f;
+            int32_t u = group_fetch<LPR>(my_u, 0, lane), i = group_fetch<LPR>(my_i, 0, lane);
+            float r = group_fetch<LPR>(my_r, 0, lane);
+            if (sub < cnt) fetch(u, i, pu, qi, bu_u, bi_i);
+            for (int step = 0; step < cnt; step += RPW) {
+                const int src = step + sub, nstep = step + RPW;
+                float4 pn[VPL], qn[VPL];
+                float bun = 0.0f, bin = 0.0f;
+                int32_t un = 0, in_ = 0;
+                float rn = 0.0f;
+                if (nstep < cnt) {
+                    un = group_fetch<LPR>(my_u, nstep, lane);
+                    in_ = group_fetch<LPR>(my_i, nstep, lane);
+                    rn = group_fetch<LPR>(my_r, nstep, lane);
+                    if (nstep + sub < cnt) fetch(un, in_, pn, qn, bun, bin);
+                }
+                if (src < cnt) apply(u, i, r, pu, qi, bu_u, bi_i);
+                u = un;
+                i = in_;
+                r = rn;
+                bu_u = bun;
+                bi_i = bin;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v) {
+                    pu[v] = pn[v];
+                    qi[v] = qn[v];
+                }
+            }
+        }
+        continue;
+#endif
         for (int step = 0; step < cnt; step += RPW) {
             const int src = step + sub;
             // lanes past cnt read lane min(src, 63): a real (loaded or zeroed) entry, unused
