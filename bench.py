@@ -614,6 +614,21 @@ def bench_c4(args):
     traffic, traffic_note = None, None
     if world == 1 and k == 64 and n_total == 1_000_000_000:
         traffic, traffic_note = pmc_traffic("r5_c4_traffic.json", avg_kernel_ms)
+    # the phase schedule's RMSE lag at C4 itself: the same handle, InitModel again, the same epochs
+    # in one phase (after the timed region; tests/test_phases_c4_gpu.py pins the lag against the
+    # oracle over the exported stream on a C4-shaped 100 M set)
+    phase_lag = None
+    if world == 1 and phases.value > 1:
+        N.check(N.lib().mml_bmf_set_hogwild_phases(h, 1))
+        N.check(N.lib().mml_bmf_init_model(h, 4, 0.0, 0.1, gb, 1.0, 5.0))
+        for _ in range(args.warmup + args.steps):
+            N.check(N.lib().mml_bmf_iterate(h, lr, None))
+        r1 = evaluate()
+        phase_lag = {"final_rmse_one_phase": r1, "lag": rmse - r1,
+                     "note": f"final_rmse ({phases.value} user phases) minus the same "
+                             f"{args.warmup + args.steps} epochs from the same InitModel in one "
+                             f"phase, on this GPU after the timed region (both Hogwild: the "
+                             f"run-to-run spread is ~1e-4)"}
     N.lib().mml_bmf_destroy(h)
     h = None
     cpu, slice_rmse = None, None
@@ -672,6 +687,7 @@ def bench_c4(args):
                        "device_ingest_s": ingest_s, "user_phases": phases.value},
             "final_rmse": rmse,
             "initial_rmse": rmse0,
+            "phase_lag_c4": phase_lag,
             "slice_epoch_rmse": slice_rmse,
             "epochs_trained": args.warmup + args.steps,
             "allreduce_ms": float(ar[0]) if world > 1 else None,

@@ -91,3 +91,39 @@ def test_prefetched_triples_are_the_epochs_own(sampler):
     # the updates ran on the prefetched, partitioned sets: the Hogwild spread, far from what
     # other triples give
     assert d_pre < 0.5 * d_other and d_wrong < 0.5 * d_other
+
+
+def test_hogwild_waves_override_keeps_the_partitioned_launch():
+    """mml_bpr_set_hogwild_waves(1 .. 31) on an epoch of >= 16 waves' worth of triples
+    used to drop to ONE workgroup (the small-epoch path) without the XCD partition.  The override
+    now keeps at least 32 waves (8 groups x 4): an override of 4 takes the time of an override of
+    32, and both draw the same triples (the sampler does not depend on the launch width)."""
+    import time
+    users, items = _data()
+    times, tris = {}, {}
+    for w in (32, 4, 32, 4):
+        ctx = N.Context(0)
+        p = N.BprParams(K, N.BPR_SAMPLER_UNIFORM_USER, 1, 0.05, 0.0025, 0.0025, 0.00025, 0.0, 0,
+                        N.BPR_SCHEDULE_HOGWILD)
+        h = N._vp()
+        N.check(N.lib().mml_bpr_create(ctx.handle, ctypes.byref(p), NU, NI, ctypes.byref(h)))
+        n = int(users.numel())
+        N.check(N.lib().mml_bpr_set_data_device(h, users.data_ptr(), items.data_ptr(), n, None))
+        N.check(N.lib().mml_bpr_init_model(h, 5, 0.0, 0.1))
+        N.check(N.lib().mml_bpr_set_hogwild_waves(h, w))
+        N.check(N.lib().mml_bpr_iterate(h, ctypes.c_uint64(11)))  # warm: plans, groups
+        t = np.zeros(2, np.float32)
+        t0 = time.perf_counter()
+        N.check(N.lib().mml_bpr_iterate(h, ctypes.c_uint64(12)))
+        times.setdefault(w, []).append(time.perf_counter() - t0)
+        N.check(N.lib().mml_bpr_last_timing(h, N.ptr(t, N._f32p)))
+        a, b, c = (np.empty(n, np.int32) for _ in range(3))
+        N.check(N.lib().mml_bpr_last_triples(h, N.ptr(a, N._i32p), N.ptr(b, N._i32p),
+                                             N.ptr(c, N._i32p), n))
+        tris[w] = (a, b, c)
+        N.lib().mml_bpr_destroy(h)
+        ctx.close()
+    print(f"\nwaves override 32: {times[32]} s, override 4: {times[4]} s")
+    for x, y in zip(tris[32], tris[4]):
+        np.testing.assert_array_equal(x, y)
+    assert min(times[4]) < 2.0 * min(times[32]) + 0.05, times
