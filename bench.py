@@ -454,10 +454,13 @@ def gpu_slice_epoch(model, k, n_users, n_items, gb, sample, test):
         su, si, sv = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.float32)
         off = np.zeros(8 * 32 + 1, np.int64)
         spans = ctypes.c_int32(0)
-        N.check(N.lib().mml_bmf_hogwild_stream(h, N.ptr(su, N._i32p), N.ptr(si, N._i32p),
-                                               N.ptr(sv, N._f32p), n, N.ptr(off, N._i64p),
-                                               len(off), ctypes.byref(spans)))
-        return float(out[0]), phases.value, (su, si, sv, off[: spans.value + 1].copy())
+        st = N.lib().mml_bmf_hogwild_stream(h, N.ptr(su, N._i32p), N.ptr(si, N._i32p),
+                                            N.ptr(sv, N._f32p), n, N.ptr(off, N._i64p), len(off),
+                                            ctypes.byref(spans))
+        # (no XCD-grouped stream, e.g. a device without 8 XCD groups: the oracle legs then run
+        # over the slice's visit order only)
+        stream = (su, si, sv, off[: spans.value + 1].copy()) if st == N.MML_OK else None
+        return float(out[0]), phases.value, stream
     finally:
         N.lib().mml_bmf_destroy(h)
         ctx.close()
@@ -473,8 +476,8 @@ def oracle_slice_epochs(model, k, gb, sample, stream, test):
     import oracle as O
     kw = dict(gb=np.float32(gb), min_rating=np.float32(1), range_=np.float32(4), lr=0.01)
     tu, ti, tv = test
-    su, si, sv, off = stream
-    n = len(su)
+    su, si, sv, off = stream if stream is not None else (None,) * 4
+    n = len(sample[0])
     waves = min(256 * 32, max(1, n // 12000))
     waves = -(-((waves + 3) // 4) // 8) * 8 * 4  # bmf.hip launch_hogwild: blocks of 4, 8 groups
     lpr = 1
@@ -484,16 +487,18 @@ def oracle_slice_epochs(model, k, gb, sample, stream, test):
     def rmse(U, V, bu, bi):
         p = O.bmf_predict(tu, ti, U, V, bu, bi, np.float32(gb), np.float32(1), np.float32(4))
         return float(O.rating_eval(p, tv)[0])
-    out = {}
+    out = {"sequential_gpu_order": None, "lockstep_gpu_order": None}
     t0 = time.perf_counter()
-    m = [a.copy() for a in model]
-    O.bmf_iterate(su, si, sv, np.arange(n, dtype=np.int32), *m, **kw)
-    out["sequential_gpu_order"] = rmse(*m)
-    m = [a.copy() for a in model]
-    for p in range((len(off) - 1) // 8):
-        O.bmf_iterate_lockstep(su, si, sv, np.arange(off[8 * p], off[8 * p + 8], dtype=np.int32),
-                               *m, streams=waves, step=64 // lpr, threads=cpu_threads(), **kw)
-    out["lockstep_gpu_order"] = rmse(*m)
+    if stream is not None:
+        m = [a.copy() for a in model]
+        O.bmf_iterate(su, si, sv, np.arange(n, dtype=np.int32), *m, **kw)
+        out["sequential_gpu_order"] = rmse(*m)
+        m = [a.copy() for a in model]
+        for p in range((len(off) - 1) // 8):
+            O.bmf_iterate_lockstep(su, si, sv,
+                                   np.arange(off[8 * p], off[8 * p + 8], dtype=np.int32), *m,
+                                   streams=waves, step=64 // lpr, threads=cpu_threads(), **kw)
+        out["lockstep_gpu_order"] = rmse(*m)
     u, i, v = sample
     m = [a.copy() for a in model]
     O.bmf_iterate(u, i, v, np.arange(len(u), dtype=np.int32), *m, **kw)
@@ -644,11 +649,12 @@ def bench_c4(args):
         ora = oracle_slice_epochs(init, k, gb, cpu_sample, g_stream, slice_test)
         del g_stream
         o_seq = ora["sequential_gpu_order"]
+        o_lock = ora["lockstep_gpu_order"]
         slice_rmse = {"gpu": g_rmse, "gpu_user_phases": g_phases,
                       "oracle_sequential_gpu_order": o_seq,
-                      "gpu_minus_oracle_sequential": g_rmse - o_seq,
-                      "oracle_lockstep_gpu_order": ora["lockstep_gpu_order"],
-                      "staleness_model_offset": ora["lockstep_gpu_order"] - o_seq,
+                      "gpu_minus_oracle_sequential": None if o_seq is None else g_rmse - o_seq,
+                      "oracle_lockstep_gpu_order": o_lock,
+                      "staleness_model_offset": None if o_seq is None else o_lock - o_seq,
                       "oracle_sequential_visit_order": ora["sequential_visit_order"],
                       "oracle_dsgd": cpu["test_rmse_after_epoch"],
                       "test_ratings": int(m_t.sum()),
