@@ -742,6 +742,7 @@ struct BprTriples {
     mml::DeviceArray<int32_t> u, i, j, xu, xi, xj;
     mml::DeviceArray<uint8_t> g;
     mml::DeviceArray<int64_t> goff;
+    bool partitioned = false;  // (experiments: MML_BPR_PF_MODE) xu / xi / xj hold a partition
 };
 
 }  // namespace
@@ -1787,6 +1788,7 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             } else {
                 h->xs.partition(s, X.i.get(), n, 3, in, out, X.goff.get());
             }
+            X.partitioned = true;
         };
         MML_HIP(hipEventRecord(h->ctx->ev_begin, st));
         if (!fused && n > 0 && !pre) sample(T, seed, st, sgrid);
@@ -1866,8 +1868,23 @@ extern "C" mml_status mml_bpr_iterate(mml_bpr* h, uint64_t seed) {
             MML_HIP(hipStreamWaitEvent(h->side, h->ctx->ev_mid, 0));
             // (a thinner sampler disturbs the update no less: grids of 256 / 1,024 / 4,096 / 16,384
             // workgroups gave epochs of 333.3 / 327.4 / 323.3 / 324.6 ms, profiles/r5aj/)
+#ifdef MML_EXPERIMENTS
+            // MML_BPR_PF_MODE (timing A/B only, the triples go stale): 1 = the next epoch's sampler
+            // without its partition, 2 = neither, once the set holds a partition
+            static const int pf_mode = [] {
+                const char* e = MML_EXPERIMENT_ENV("MML_BPR_PF_MODE");
+                return e ? std::atoi(e) : 0;
+            }();
+            if (pf_mode == 0 || !X.partitioned) {
+                sample(X, h->next_seed, h->side, sgrid);
+                partition(X, h->side);
+            } else if (pf_mode == 1) {
+                sample(X, h->next_seed, h->side, sgrid);
+            }
+#else
             sample(X, h->next_seed, h->side, sgrid);
             partition(X, h->side);
+#endif
             MML_HIP(hipEventRecord(h->ev_pf_done, h->side));
             MML_HIP(hipStreamWaitEvent(st, h->ev_pf_done, 0));
             h->pf_ready = true;
