@@ -83,14 +83,15 @@ def _evaluate(h, test):
     return float(out[0])
 
 
-def _gpu(data, test, gb, *, phases=0, devices=0, want_init=False, want_stream=False):
+def _gpu(data, test, gb, *, phases=0, devices=0, want_init=False, want_stream=False, nu=NU,
+         ni=NI, k=K, epochs=EPOCHS):
     """One training run: RMSE after each epoch; optionally the InitModel and the exported stream."""
     users, items, values = data
     n = users.numel()
     ctx = N.Context(devices)
-    p = N.BmfParams(K, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
+    p = N.BmfParams(k, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
     h = N._vp()
-    N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(p), NU, NI, ctypes.byref(h)))
+    N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(p), nu, ni, ctypes.byref(h)))
     out = {}
     try:
         N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
@@ -98,12 +99,12 @@ def _gpu(data, test, gb, *, phases=0, devices=0, want_init=False, want_stream=Fa
         N.check(N.lib().mml_bmf_set_hogwild_phases(h, phases))
         N.check(N.lib().mml_bmf_init_model(h, SEED, 0.0, 0.1, gb, 1.0, 5.0))
         if want_init:
-            m = (np.empty((NU, K), np.float32), np.empty((NI, K), np.float32),
-                 np.empty(NU, np.float32), np.empty(NI, np.float32))
+            m = (np.empty((nu, k), np.float32), np.empty((ni, k), np.float32),
+                 np.empty(nu, np.float32), np.empty(ni, np.float32))
             N.check(N.lib().mml_bmf_get_model(h, *[N.ptr(a, N._f32p) for a in m]))
             out["init"] = m
         rmse = []
-        for _ in range(EPOCHS):
+        for _ in range(epochs):
             N.check(N.lib().mml_bmf_iterate(h, LR, None))
             rmse.append(_evaluate(h, test))
         out["rmse"] = np.array(rmse)
@@ -139,36 +140,36 @@ def _multiset_hash(u, i, v):
         return int(np.sum(x, dtype=np.uint64))
 
 
-def _check_stream(stream, P, ref_hash):
+def _check_stream(stream, P, ref_hash, nu=NU, ni=NI):
     """Every rating once; each item in the spans of one XCD group; each user in one phase."""
     su, si, sv, off = stream
     assert len(off) == 8 * P + 1 and off[0] == 0 and off[-1] == len(su)
     assert np.all(np.diff(off) >= 0)
     assert _multiset_hash(su, si, sv) == ref_hash
-    groups_of_item = np.zeros(NI, np.int8)
+    groups_of_item = np.zeros(ni, np.int8)
     for g in range(8):
-        seen = np.zeros(NI, bool)
+        seen = np.zeros(ni, bool)
         for ph in range(P):
             seen[si[off[8 * ph + g]:off[8 * ph + g + 1]]] = True
         groups_of_item += seen
     assert groups_of_item.max() == 1, "an item's ratings lie in spans of two XCD groups"
-    phases_of_user = np.zeros(NU, np.int8)
+    phases_of_user = np.zeros(nu, np.int8)
     for ph in range(P):
-        seen = np.zeros(NU, bool)
+        seen = np.zeros(nu, bool)
         seen[su[off[8 * ph]:off[8 * ph + 8]]] = True
         phases_of_user += seen
     assert phases_of_user.max() == 1, "a user's ratings lie in two phases"
 
 
-def _hogwild_streams(n):
+def _hogwild_streams(n, k=K):
     """The launch's waves and ratings per wave step at k = 64 (tests/test_edge_cases_gpu.py
     hogwild_streams; with phases every launch keeps the whole epoch's wave count)."""
     from test_edge_cases_gpu import hogwild_streams
-    return hogwild_streams(n, K)
+    return hogwild_streams(n, k)
 
 
 def _oracle_run(name, init, stream, test, gb, *, lockstep=False, shards=None, epochs=EPOCHS,
-                threads=1):
+                threads=1, k=K):
     """The oracle over `stream` = (users, items, ratings, span offsets) from `init`, EPOCHS times;
     test RMSE per epoch.
       * lockstep=False: the sequential Iterate() (BiasedMatrixFactorization.cs:264-310) in stream
@@ -195,7 +196,7 @@ def _oracle_run(name, init, stream, test, gb, *, lockstep=False, shards=None, ep
     if shards is None:
         P = (len(off) - 1) // 8
         launches = [np.arange(off[8 * p], off[8 * p + 8], dtype=np.int32) for p in range(P)]
-        waves = _hogwild_streams(len(su))
+        waves = _hogwild_streams(len(su), k)
     else:
         shard_of = np.searchsorted(shards, su, side="right") - 1
         idx = [np.flatnonzero(shard_of == d).astype(np.int32) for d in range(len(shards) - 1)]
@@ -209,7 +210,7 @@ def _oracle_run(name, init, stream, test, gb, *, lockstep=False, shards=None, ep
             parts = [(V.copy(), bi.copy()) for _ in idx]
 
             def one(d):
-                run(idx[d], U, parts[d][0], bu, parts[d][1], _hogwild_streams(len(idx[d])))
+                run(idx[d], U, parts[d][0], bu, parts[d][1], _hogwild_streams(len(idx[d]), k))
             with ThreadPoolExecutor(len(idx)) as ex:  # disjoint user rows, own item copies
                 list(ex.map(one, range(len(idx))))
             V = parts[0][0].copy()

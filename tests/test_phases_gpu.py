@@ -3,18 +3,15 @@ hogwild_phases): the stream split into P phases by a hash of the user, one launc
 rating visited once per epoch (BiasedMatrixFactorization.cs:264-310 -- the visit order inside a
 phase is the reference's RandomIndex order, as in the one-phase epoch).
 
-The phases only change WHEN a rating is visited, like another RandomIndex shuffle would -- and
-they gather each user's ratings of an epoch into 1/P of it, so at an epoch's end the early phases'
-users were last updated further back while the items kept moving (a lag that shrinks as the
-items settle; bmf.hip hogwild_phases).  The band is the reference's own sensitivity to the visit
-order: the one-phase epoch on three RandomIndex permutations, the largest pairwise RMSE spread
-after each epoch (each run is a Hogwild run, so the spread includes its run-to-run noise).  The
-default phase count must stay within 3x that spread + 1e-4 of the one-phase run after every
-epoch; 8 phases (past the default here) are printed with their lag.  The phase lag itself is
-pinned against the oracle run over the exported stream, at 8 and at C4's 26 phases, in
-tests/test_phases_c4_gpu.py (the lag is the order's own cost to the reference's loop, so a band
-made of visit-order spreads alone is not the bound for it)."""
+The phases change WHEN a rating is visited: they gather each user's ratings of an epoch into 1/P of
+it, so at an epoch's end the early phases' users were last updated further back while the items
+kept moving.  That lag is the order's own cost to the reference's loop.  So the band is not a
+visit-order spread (round 5's form, which one run then left).  It is the oracle run over the exact
+stream the launches walked (mml_bmf_hogwild_stream), sequential and in the lockstep staleness
+model, as in tests/test_phases_c4_gpu.py at C4's 26 phases: here 800 k users x 16 M ratings, the
+default 3 phases and 8, 4 epochs, each configuration trained twice for the run-to-run spread."""
 import ctypes
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import pytest
@@ -26,58 +23,48 @@ pytestmark = pytest.mark.gpu
 NU, NI, N_TRAIN, K, EPOCHS = 800_000, 50_000, 16_000_000, 64, 4
 
 
-def _train(users, items, values, tu, ti, tv, phases, order=None):
-    ctx = N.Context(0)
-    p = N.BmfParams(K, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
-    h = N._vp()
-    N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(p), NU, NI, ctypes.byref(h)))
-    N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
-                                            values.data_ptr(), len(users),
-                                            None if order is None else order.data_ptr()))
-    N.check(N.lib().mml_bmf_set_hogwild_phases(h, phases))
-    N.check(N.lib().mml_bmf_init_model(h, 4, 0.0, 0.1, 0.51, 1.0, 5.0))
-    rmse = []
-    for _ in range(EPOCHS):
-        N.check(N.lib().mml_bmf_iterate(h, 0.01, None))
-        out = np.zeros(2, np.float32)
-        N.check(N.lib().mml_bmf_evaluate(h, N.ptr(tu, N._i32p), N.ptr(ti, N._i32p),
-                                         N.ptr(tv, N._f32p), len(tu), N.ptr(out, N._f32p)))
-        rmse.append(float(out[0]))
-    used = ctypes.c_int32(0)
-    N.check(N.lib().mml_bmf_last_phases(h, ctypes.byref(used)))
-    N.lib().mml_bmf_destroy(h)
-    ctx.close()
-    return np.array(rmse), used.value
-
-
-def test_user_phases_within_the_visit_order_spread():
+def test_user_phases_pinned_to_the_oracle():
     import torch
     from mymedialite_amd.synthetic import planted_ratings_torch
+    from test_phases_c4_gpu import (_band, _check_stream, _gpu, _multiset_hash, _oracle_run,
+                                    _results, _say)
     dev = torch.device("cuda:0")
-    users, items, values = planted_ratings_torch(NU, NI, N_TRAIN, seed=21, device=dev)
-    tu, ti, tv = (x.cpu().numpy() for x in planted_ratings_torch(NU, NI, 1_000_000, seed=22,
+    data = planted_ratings_torch(NU, NI, N_TRAIN, seed=21, device=dev)
+    test = tuple(x.cpu().numpy() for x in planted_ratings_torch(NU, NI, 1_000_000, seed=22,
                                                                  device=dev))
-    orders = []
-    for seed in (5, 6):
-        g = torch.Generator(device=dev)
-        g.manual_seed(seed)
-        orders.append(torch.randperm(N_TRAIN, generator=g, device=dev).to(torch.int32))
-    one, p1 = _train(users, items, values, tu, ti, tv, 1)
-    others = [_train(users, items, values, tu, ti, tv, 1, order=o)[0] for o in orders]
-    auto, pa = _train(users, items, values, tu, ti, tv, 0)
-    eight, p8 = _train(users, items, values, tu, ti, tv, 8)
-    runs = [one] + others
-    spread = np.max([np.abs(a - b) for x, a in enumerate(runs) for b in runs[x + 1:]], axis=0)
-    band = 3 * spread + 1e-4
-    print(f"\nRMSE per epoch: one phase {np.round(one, 6)}, other visit orders "
-          f"{[np.round(o, 6) for o in others]}, {pa} phases (default) {np.round(auto, 6)} "
-          f"(d {np.round(auto - one, 6)}), 8 phases {np.round(eight, 6)} "
-          f"(d {np.round(eight - one, 6)}); order spread {np.round(spread, 6)}, band "
-          f"{np.round(band, 6)}")
-    # 800k users x 256 B = 205 MB of active rows: 3 phases of <= 96 MiB
-    assert (p1, pa, p8) == (1, 3, 8)
-    assert np.all(np.abs(auto - one) <= band), (auto - one, band)
-    assert one[-1] < one[0] < 1.2  # the set is learnable and learned
+    gb = 0.51
+    shape = dict(nu=NU, ni=NI, k=K, epochs=EPOCHS)
+    ref_hash = _multiset_hash(*(x.cpu().numpy() for x in data))
+    gpu, streams, init = {}, {}, None
+    for P in (1, 0, 8):
+        reps = []
+        for rep in range(2):
+            o = _gpu(data, test, gb, phases=P, want_init=(P == 1 and rep == 0),
+                     want_stream=(rep == 0), **shape)
+            init = o.get("init", init)
+            if "stream" in o:
+                streams[o["phases"]] = o["stream"]
+            reps.append(o["rmse"])
+        gpu[o["phases"]] = np.array(reps)
+    # 800 k users x 256 B = 205 MB of active rows: 3 phases of <= 96 MiB by default
+    assert sorted(gpu) == [1, 3, 8]
+    for P, st in streams.items():
+        _check_stream(st, P, ref_hash, nu=NU, ni=NI)
+    with ThreadPoolExecutor(6) as ex:
+        ora = _results({(P, ls): ex.submit(_oracle_run, f"{P} phases{' lockstep' if ls else ''}",
+                                           init, st, test, gb, lockstep=ls, epochs=EPOCHS,
+                                           threads=2, k=K)
+                        for P, st in streams.items() for ls in (False, True)})
+    noise = max(float(np.max(np.abs(r[0] - r[1]))) for r in gpu.values())
+    _say(f"\ngpu run-to-run spread: {noise:.2e}")
+    ok = {P: _band(f"{P} phases", gpu[P], ora[(P, False)], ora[(P, True)], noise)[0]
+          for P in (1, 3, 8)}
+    for P in (3, 8):
+        _say(f"{P} phases, lag vs one phase: oracle {ora[(P, False)] - ora[(1, False)]}, gpu "
+             f"{gpu[P].mean(axis=0) - gpu[1].mean(axis=0)}")
+    for r in gpu.values():
+        assert r[0][-1] < r[0][0] < 1.2  # the set is learnable and learned
+    assert all(ok.values()), ok
 
 
 def _stream(h, n):
@@ -153,3 +140,50 @@ def test_phase_count_changes_on_one_handle():
     ctx.close()
     for a, b in zip(last, fresh):
         assert np.array_equal(a, b)
+
+
+def test_hogwild_stream_argument_errors():
+    """mml_bmf_hogwild_stream (ABI 13) refuses what it cannot answer, never faults: a wrong n, too
+    few span offsets, a multi-device context; and on a set below 16 waves' worth (the one-workgroup
+    epoch, no XCD-grouped stream) it reports that no stream exists."""
+    rs = np.random.default_rng(3)
+    nu, ni, n = 3000, 800, 400_000
+    u = rs.integers(0, nu, n).astype(np.int32)
+    i = rs.integers(0, ni, n).astype(np.int32)
+    v = rs.integers(1, 6, n).astype(np.float32)
+
+    def run(devices, n_use):
+        ctx = N.Context(devices)
+        p = N.BmfParams(16, N.LOSS_RMSE, 0, N.SCHEDULE_HOGWILD, 1.0, 0.01, 0.015, 0.015)
+        h = N._vp()
+        N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(p), nu, ni, ctypes.byref(h)))
+        N.check(N.lib().mml_bmf_set_data(h, N.ptr(u[:n_use], N._i32p), N.ptr(i[:n_use], N._i32p),
+                                         N.ptr(v[:n_use], N._f32p), n_use, None))
+        N.check(N.lib().mml_bmf_init_model(h, 4, 0.0, 0.1, 0.5, 1.0, 5.0))
+        N.check(N.lib().mml_bmf_iterate(h, 0.01, None))
+        return ctx, h
+
+    def export(h, n_arg, cap):
+        a, b = np.empty(max(n_arg, 1), np.int32), np.empty(max(n_arg, 1), np.int32)
+        c = np.empty(max(n_arg, 1), np.float32)
+        off = np.zeros(max(cap, 1), np.int64)
+        spans = ctypes.c_int32(0)
+        st = N.lib().mml_bmf_hogwild_stream(h, N.ptr(a, N._i32p), N.ptr(b, N._i32p),
+                                            N.ptr(c, N._f32p), n_arg, N.ptr(off, N._i64p), cap,
+                                            ctypes.byref(spans))
+        return st, spans.value, off
+    ctx, h = run(0, n)  # 400 k ratings: 33 waves, the XCD-grouped epoch
+    st, spans, off = export(h, n, 9)
+    assert st == N.MML_OK and spans == 8 and off[0] == 0 and off[8] == n
+    assert export(h, n - 1, 9)[0] == -1        # n is not the handle's count
+    assert export(h, n, 8)[0] == -1            # fewer than phases * 8 + 1 offsets
+    N.lib().mml_bmf_destroy(h)
+    ctx.close()
+    ctx, h = run(0, 20_000)  # one-workgroup epoch: no XCD-grouped stream
+    assert export(h, 20_000, 9)[0] == -1
+    N.lib().mml_bmf_destroy(h)
+    ctx.close()
+    ctx, h = run([0, 0], n)  # user shards on a repeated-device context
+    assert export(h, n, 9)[0] == -5  # MML_ERR_STATE
+    N.lib().mml_bmf_destroy(h)
+    ctx.close()
