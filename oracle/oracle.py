@@ -373,7 +373,8 @@ def bmf_train(users, items, values, n_users, n_items, min_rating, max_rating, *,
     s = ratings_average_exact(values) if len(values) <= 200000 else float(
         np.sum(values, dtype=np.float64))
     avg_f = np.float32(np.float32(s) / np.float32(len(values)))
-    avg = np.float32(np.float32(avg_f - np.float32(min_rating)) / range_)
+    with np.errstate(divide="ignore", invalid="ignore"):  # min == max: 0 / 0 = NaN, as in C#
+        avg = np.float32(np.float32(avg_f - np.float32(min_rating)) / range_)
     gb = np.float32(math.log(float(avg) / (1.0 - float(avg))))
     common = dict(gb=gb, min_rating=np.float32(min_rating), range_=range_,
                   bias_lr=bias_learn_rate, bias_reg=bias_reg, reg_u=reg_u, reg_i=reg_i, loss=loss,
@@ -546,7 +547,8 @@ def asym_train(users, items, values, n_users, n_items, min_rating, max_rating, *
     bi = np.zeros(n_items, np.float32)
     range_ = np.float32(np.float32(max_rating) - np.float32(min_rating))
     avg_f = np.float32(np.float32(ratings_average_exact(values)) / np.float32(len(values)))
-    avg = np.float32(np.float32(avg_f - np.float32(min_rating)) / range_)
+    with np.errstate(divide="ignore", invalid="ignore"):  # min == max: 0 / 0 = NaN, as in C#
+        avg = np.float32(np.float32(avg_f - np.float32(min_rating)) / range_)
     gb = np.float32(math.log(float(avg) / (1.0 - float(avg))))
     if mode >= 3:
         gb = avg_f  # global_bias = ratings.Average (MatrixFactorization.Train)
@@ -634,7 +636,8 @@ def socialmf_train(users, items, values, n_users, n_items, min_rating, max_ratin
     range_ = np.float32(np.float32(max_rating) - np.float32(min_rating))
     s = ratings_average_exact(values)
     avg_f = np.float32(np.float32(s) / np.float32(len(values)))
-    avg = np.float32(np.float32(avg_f - np.float32(min_rating)) / range_)
+    with np.errstate(divide="ignore", invalid="ignore"):  # min == max: 0 / 0 = NaN, as in C#
+        avg = np.float32(np.float32(avg_f - np.float32(min_rating)) / range_)
     gb = np.float32(math.log(float(avg) / (1.0 - float(avg))))
     p = _BmfParams(k, loss, 0, 1, 1, gb, min_rating, range_, learn_rate, bias_learn_rate,
                    bias_reg, reg_u, reg_i)
