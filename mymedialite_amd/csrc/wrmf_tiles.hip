@@ -516,16 +516,6 @@ __device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_addr) {
         : "v"(gsrc), "s"(lds_addr)
         : "memory");
 }
-// one dword per lane global -> LDS (lane l's to lds_addr + 4 l)
-__device__ __forceinline__ void glds4(const float* gsrc, uint32_t lds_addr) {
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_addr)
-        : "memory");
-}
 __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
@@ -2065,9 +2055,6 @@ __global__ __launch_bounds__(64 * WAVES, 4) void wrmf_wood_w16_kernel(
     static_assert(WAVES >= 1 && WAVES <= 8, "16 items per wave, <= 128 items");
     __shared__ float4 pu[2][WAVES][64];   // the waves' partial u, alternated per mat-vec
     __shared__ float sdot[2][2 * WAVES];  // block_sum2, alternated per CG step
-#if defined(MML_W16_PF) && MML_W16_PF
-    __shared__ float pf_sink[64];
-#endif
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int f0 = 4 * lane;
@@ -2144,17 +2131,6 @@ __global__ __launch_bounds__(64 * WAVES, 4) void wrmf_wood_w16_kernel(
                 qp[2][j >> 1][j & 1] = ok ? g[j].z : 0.0f;
                 qp[3][j >> 1][j & 1] = ok ? g[j].w : 0.0f;
             }
-#if defined(MML_W16_PF) && MML_W16_PF
-            // (experiments: A/B) the next row's Q rows toward the caches while this row's steps
-            // run: two 128-B lines per lane (item lane / 4 of the wave's next slice), loaded
-            // global -> LDS into a sink nothing reads, so no register waits for them
-            {
-                const int idn = __shfl(idv_n, lane >> 2);
-                const int o0 = min(64 * (lane & 3), k - 1), o1 = min(64 * (lane & 3) + 32, k - 1);
-                glds4(Q + (int64_t)idn * k + o0, lds_addr_of(pf_sink));
-                glds4(Q + (int64_t)idn * k + o1, lds_addr_of(pf_sink));
-            }
-#endif
         } else {
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
@@ -2282,9 +2258,6 @@ __global__ __launch_bounds__(64 * WAVES, 4) void wrmf_wood_w16_kernel(
             for (int c = 0; c < 4; ++c)
                 if (f0 + c < k) Tout[(int64_t)li * k + f0 + c] = S ? sf[c] - u[c] : u[c];
     }
-#if defined(MML_W16_PF) && MML_W16_PF
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sink's loads land before the LDS is freed
-#endif
 }
 
 // MML_WRMF_WOOD16 (experiments builds): 0 = rows of 97 .. 128 items on wrmf_wood_cg_kernel<128>,
