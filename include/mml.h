@@ -573,8 +573,9 @@ mml_status mml_wrmf_last_allgather_ms(mml_wrmf* h, float* out);
  * no Woodbury rows are solved in `ranges` contiguous row ranges, and range b's first refinement
  * residual runs on a second stream under range b + 1's solve; HH of such a half is computed on that
  * stream under the hot rows' split Gram.  The model is the serial path's bit for bit.  ranges = 0
- * (default): 4 ranges where a half has >= 4 x 4,096 direct rows; 1: off; 2 .. 16: that many.  Takes
- * effect at the next mml_wrmf_iterate. */
+ * (default): 12 ranges, or one per 4,096 direct rows where a half has fewer, and none below
+ * 4 x 4,096 direct rows (round 5's default was 4 ranges); 1: off; 2 .. 16: that many where the half
+ * has >= 4,096 direct rows per range.  Takes effect at the next mml_wrmf_iterate. */
 mml_status mml_wrmf_set_pipeline(mml_wrmf* h, int32_t ranges);
 /* The most refinement passes a half-step of the last mml_wrmf_iterate ran (ABI 6);
  * corrections (nullable, [8]): per half-step (users 0..3, items 4..7) and pass, the largest

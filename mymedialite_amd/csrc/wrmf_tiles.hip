@@ -2277,11 +2277,13 @@ bool wood_w16() { return wood_w16_mode() > 0; }
 // the item half's pipeline: the direct rows' first-pass residual of a row range runs on a second
 // stream under the next range's main solve (wrmf_tile_plan, wrmf_tile_solve).  MML_WRMF_PIPE=n
 // (experiments builds): n row ranges, 1 = off; MML_WRMF_PIPE_GRID: the residual kernel's grid
-// while it shares the CUs with the solve
+// while it shares the CUs with the solve.  12 by default (round 6, C5 per iteration on one box,
+// two runs each: 4 ranges 685.2 / 690.0 ms, 8 677.5 / 680.6, 12 676.6 / 679.3, 16 676.8 / 676.2,
+// profiles/r6/pipe_sweep/): the last range's residual, which runs alone, is shorter
 int32_t pipe_batches() {
     static const int32_t v = [] {
         const char* e = MML_EXPERIMENT_ENV("MML_WRMF_PIPE");
-        return e ? std::max(1, std::min(16, std::atoi(e))) : 4;
+        return e ? std::max(1, std::min(16, std::atoi(e))) : 12;
     }();
     return v;
 }
@@ -3145,7 +3147,13 @@ void wrmf_tile_plan(const std::vector<int64_t>& deg, hipStream_t st, WrmfTilePla
     // after the light rows' and whose W every range's residual would need
     size_t n_wood_rows = 0;
     for (auto& w : wood) n_wood_rows += w.size();
-    const int32_t want = pipe > 0 ? std::min(16, pipe) : pipe_batches();
+    // the default: pipe_batches() ranges, fewer where the half has fewer than 4,096 light rows per
+    // range (and none below 4 such ranges, as before round 6's 12)
+    int32_t want = pipe > 0 ? std::min(16, pipe) : pipe_batches();
+    if (pipe <= 0 && want > 4) {
+        const int64_t fit = (int64_t)light.size() / 4096;
+        want = fit >= 4 ? (int32_t)std::min<int64_t>(want, fit) : want;
+    }
     p.nbatch = 1;
     p.b_row.assign({0, r1 - r0});
     if (want > 1 && n_wood_rows == 0 && (int64_t)light.size() >= (int64_t)want * 4096) {

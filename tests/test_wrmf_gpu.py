@@ -267,7 +267,8 @@ def test_wrmf_item_pipeline_equals_serial_bit_for_bit():
     second stream under range b + 1's solve, the dense term added after, HH under the hot rows'
     split Gram -- the serial path's model bit for bit.  400 k users x 40 k
     items, 40 M events (items Zipf(0.8): no Woodbury item rows, hot items above 8,192 entries),
-    k = 256, fp64 mode, 2 iterations; serial (1), the default (0: 4 ranges) and 7 ranges."""
+    k = 256, fp64 mode, 2 iterations; serial (1), the default (0: here 9 ranges, one per 4,096 of
+    the ~39 k direct item rows, at most 12) and 7 ranges."""
     import ctypes
     import torch
     from mymedialite_amd import _native as N
