@@ -2378,7 +2378,17 @@ void launch_wood_cg(hipStream_t st, int g, const int32_t* rows, int32_t n, const
                     const int32_t* cols, const float* Q, int32_t k, float alpha, float* Tout,
                     const float* S, double lnorm = 0.0, bool refined = false,
                     const int32_t* spos = nullptr) {
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, 256 * 4));
+    // 32 workgroups per CU, 16 times the w16 kernel's resident two: a workgroup's rows are a
+    // shorter run, so the two resident ones drift out of step (one gathers while the other runs
+    // its steps) and the launch ends on shorter tails.  C5 per iteration on one box, two runs each
+    // (profiles/r6/wood_grid/): grid 512 674.9 / 677.9 ms, 1,024 (round 5) 669.7 / 671.7, 2,048
+    // 665.8 / 665.2, 8,192 659.8 / 661.5, up to 1 M the same.  MML_WRMF_WOOD_GRID (experiments
+    // builds): A/B
+    static const int64_t grid_cap = [] {
+        const char* e = MML_EXPERIMENT_ENV("MML_WRMF_WOOD_GRID");
+        return e ? std::max<int64_t>(256, std::atoll(e)) : (int64_t)256 * 32;
+    }();
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n, grid_cap));
     // main solve: relative residual 1e-6 (fp32 CG stagnates not far below: a tighter target
     // just runs to max_it on trained factors), 1e-5 when the fp64 refinement follows and corrects
     // the rest (C5: the users' largest correction stays 0 / 0 / 1e-8 with 1e-6 / 1e-5 / 1e-4 and
