@@ -2287,6 +2287,15 @@ int32_t pipe_batches() {
     }();
     return v;
 }
+// grid caps of the row kernels, for A/B in experiments builds (the release build: the defaults)
+int64_t exp_grid(const char* name, int64_t def) {
+    const char* e = MML_EXPERIMENT_ENV(name);
+    return e ? std::max<int64_t>(64, std::atoll(e)) : def;
+}
+int64_t rv_grid() {
+    static const int64_t v = exp_grid("MML_WRMF_RV_GRID", 256 * 16);
+    return v;
+}
 int pipe_grid() {
     static const int v = [] {
         const char* e = MML_EXPERIMENT_ENV("MML_WRMF_PIPE_GRID");
@@ -3306,7 +3315,8 @@ static void first_residual(hipStream_t s, WrmfTilePlan& p, float* W, const float
     const float* w0 = W + (p.r0 + lr0) * (int64_t)k;
     double* r = p.ws->r64.get() + lr0 * (int64_t)k;
     auto dense = [&](int add) {
-        const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((n + kXB - 1) / kXB, 2048));
+        static const int64_t xg = exp_grid("MML_WRMF_XHH_GRID", 2048);
+        const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((n + kXB - 1) / kXB, xg));
         wrmf_xhh_kernel<float><<<gx, 256, 0, s>>>(w0, HH, n, k, reg, r, add);
         ++launches;
     };
@@ -3407,8 +3417,9 @@ int32_t wrmf_tile_refine(hipStream_t st, WrmfTilePlan& p, float* W, const float*
         if (pass == 0 && p.residual_ready) {
             // computed range by range under the main solve (wrmf_tile_solve's pipeline)
         } else if (pass == 0) {
+            static const int rg = (int)exp_grid("MML_WRMF_RESID_GRID", 8192);
             first_residual(st, p, W, H, cols, HH, k, alpha, reg, 0, n, 0, p.n_rsegs, 0,
-                           p.n_rmulti, 8192, launches);
+                           p.n_rmulti, rg, launches);
         } else {
             const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((n + kXB - 1) / kXB, 2048));
             wrmf_xhh_kernel<double><<<gx, 256, 0, st>>>(p.ws->x64.get(), HH, n, k, reg,
@@ -3564,7 +3575,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                 wrmf_tile_resolve_kernel<<<(int)std::min<int64_t>(n, grid_cap), kThreads, 0, st>>>(
                     list, (int32_t)n, p.counter.get(), off, Fl, rhs, k, W);
             } else {
-                const int64_t blocks = std::min<int64_t>((n + kRvWaves - 1) / kRvWaves, 256 * 16);
+                const int64_t blocks = std::min<int64_t>((n + kRvWaves - 1) / kRvWaves, rv_grid());
                 wrmf_tile_resolve_wave_kernel<<<(int)blocks, 64 * kRvWaves, 0, st>>>(
                     list, (int32_t)n, off, Fl, rhs, k, W, 0);
             }
@@ -3627,7 +3638,11 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
             const int64_t s0 = p.seg_first[h0], s1 = p.seg_first[h1];
             p.gram.alloc((size_t)std::min(nh, batch_rows) * kTiles * 1024);
             MML_HIP(hipMemsetAsync(p.gram.get(), 0, (size_t)(h1 - h0) * per_row, st));
-            const int gg = (int)std::min<int64_t>(s1 - s0, grid_cap);
+            static const int64_t gram_grid = [] {  // MML_WRMF_GRAM_GRID (experiments): A/B
+                const char* e = MML_EXPERIMENT_ENV("MML_WRMF_GRAM_GRID");
+                return e ? std::max<int64_t>(256, std::atoll(e)) : (int64_t)256 * 2;
+            }();
+            const int gg = (int)std::min<int64_t>(s1 - s0, gram_grid);
             auto gk = P ? &wrmf_tile_gram_kernel<true> : &wrmf_tile_gram_kernel<false>;
             gk<<<gg, kThreads, 0, st>>>(
                 reinterpret_cast<const Seg*>(p.segs.get()) + s0, (int32_t)(s1 - s0), (int32_t)h0,
@@ -3658,7 +3673,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
         // the deferred backward substitutions: W rows hold y, the kept tiles L
         auto back = [&](const int32_t* list, int64_t n, const float* Fl) {
             if (n <= 0) return;
-            const int64_t blocks = std::min<int64_t>((n + kRvWaves - 1) / kRvWaves, 256 * 16);
+            const int64_t blocks = std::min<int64_t>((n + kRvWaves - 1) / kRvWaves, rv_grid());
             wrmf_tile_resolve_wave_kernel<<<(int)blocks, 64 * kRvWaves, 0, st>>>(
                 list, (int32_t)n, off, Fl, W, k, W, 1);
             ++launches;
@@ -3706,7 +3721,7 @@ void wrmf_tile_solve(hipStream_t st, WrmfTilePlan& p, float* W, const float* H, 
                                p.b_multi[b + 1], pipe_grid(), launches, 2);
                 if (l1 > l0) {
                     const int64_t blocks =
-                        std::min<int64_t>((l1 - l0 + kRvWaves - 1) / kRvWaves, 256 * 16);
+                        std::min<int64_t>((l1 - l0 + kRvWaves - 1) / kRvWaves, rv_grid());
                     wrmf_tile_resolve_wave_kernel<<<(int)blocks, 64 * kRvWaves, 0, p.side>>>(
                         p.light.get() + l0, (int32_t)(l1 - l0), off, F + (size_t)l0 * tile_floats,
                         p.ws->rf.get(), k, p.ws->df.get(), 0);
