@@ -3,7 +3,11 @@
 per wrmf_* kernel the matrix-core busy fraction, the matrix-core flops by data type and the VALU
 flops, and the same over the iteration (an honest C5 roofline).
 
-  python scripts/pmc_c5_engines.py <busy dir> <mops dir|-> <valu dir|-> <iteration ms> out.json
+  python scripts/pmc_c5_engines.py <busy dir> <mops dir|-> <valu dir|-> <iteration ms> out.json \
+      [<FETCH_SIZE dir> <WRITE_SIZE dir>]
+
+With the two traffic passes each kernel also gets its HBM bytes, FETCH_SIZE x 2 + WRITE_SIZE in KB
+(gfx950: FETCH_SIZE counts half the bytes of wide coalesced reads; MI355X_MICROARCH.md).
 
 Counters (gfx950; MI355X_MICROARCH.md):
   * SQ_VALU_MFMA_BUSY_CYCLES: matrix-core busy cycles summed over the SIMDs; GRBM_GUI_ACTIVE:
@@ -54,8 +58,9 @@ def short(name):
 
 def main():
     busy_d, mops_d, valu_d, iter_ms, dst = sys.argv[1:6]
+    fetch_d, write_d = (sys.argv[6:8] + ["-", "-"])[:2]
     iter_ms = float(iter_ms)
-    passes = [load(busy_d), load(mops_d), load(valu_d)]
+    passes = [load(busy_d), load(mops_d), load(valu_d), load(fetch_d), load(write_d)]
 
     def last_iteration(p):
         """The dispatches from the last iteration's first kernel on: its users' half starts with
@@ -96,6 +101,10 @@ def main():
                                   k.get("SQ_INSTS_VALU_ADD_F64", 0.0) +
                                   k.get("SQ_INSTS_VALU_MUL_F64", 0.0))}
         r["flops"] = fl
+        if "FETCH_SIZE" in k or "WRITE_SIZE" in k:
+            hb = (2.0 * k.get("FETCH_SIZE", 0.0) + k.get("WRITE_SIZE", 0.0)) * 1024.0
+            r["hbm_GB"] = hb / 1e9
+            r["hbm_TBps"] = hb / (k["ms"] * 1e-3) / 1e12 if k["ms"] else None
         for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"):
             tot[c] += k.get(c, 0.0)
         tot["ms"] += k["ms"]
@@ -126,10 +135,20 @@ def main():
                 "clock, mfma_busy_frac_kernel_time over the kernels' own (serialised) time",
     }
     json.dump(res, open(dst, "w"), indent=1)
-    print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
+    print(f"iteration {iter_ms:.1f} ms (unprofiled), clock {res['clock_GHz']:.2f} GHz, MFMA busy over "
+          f"the iteration {res['mfma_busy_frac_iteration']:.3f}, over the kernels' serialised time "
+          f"{res['mfma_busy_frac_kernel_time']:.3f}")
+    print("engine flops per iteration (TFLOP) / achieved TF/s / fraction of that engine's peak:")
+    for e, v in engines.items():
+        print(f"  {e:10s} {v['tflop_per_iteration']:8.2f} {v['achieved_tflops']:8.1f} {v['frac']:.4f}")
+    print(f"{'kernel':42s} {'n':>3s} {'ms':>7s} {'busy':>6s} {'wait/wave':>9s} {'HBM GB':>8s} "
+          f"{'TB/s':>5s}  flops (TFLOP)")
     for name, r in rows.items():
-        print(f"{name:48s} {r['dispatches']:3d} {r['ms_under_pmc']:8.1f} ms  busy "
-              f"{r.get('mfma_busy_frac', float('nan')):.3f}  " +
+        hb, tb = r.get("hbm_GB"), r.get("hbm_TBps")
+        print(f"{name:42s} {r['dispatches']:3d} {r['ms_under_pmc']:7.1f} "
+              f"{r.get('mfma_busy_frac', float('nan')):6.3f} "
+              f"{r.get('wait_any_over_wave_cycles', float('nan')):9.3f} "
+              f"{hb if hb is not None else float('nan'):8.1f} {tb if tb is not None else float('nan'):5.2f}  " +
               " ".join(f"{e} {v / 1e12:.2f}" for e, v in r["flops"].items() if v))
 
 
