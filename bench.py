@@ -57,6 +57,19 @@ def bytes_per_update(k: int) -> int:
     return 16 * k + 28
 
 
+def runs_bytes(k: int, n: int, runs: int) -> int:
+    """The user-runs epoch's algorithmic bytes (bmf.hip bmf_sgd_runs_kernel): per update the
+    stream (12 B), V_i and b_i read and written (8k + 8 B); per run U_u and b_u read and written
+    once (8k + 8 B).  bytes_per_update charges every update a U_u and b_u round trip instead."""
+    return n * (8 * k + 20) + runs * (8 * k + 8)
+
+
+def last_runs(h) -> int:
+    r = ctypes.c_int64(0)
+    N.check(N.lib().mml_bmf_last_runs(h, ctypes.byref(r)))
+    return r.value
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -87,6 +100,10 @@ def main():
                     help="default: c4 at every N (BiasedMF k=64, 1B ratings, strong scaling; at "
                          "N = 1 + the c2 / c3 / c5 keys); c2: 1M x 100k, 100M ratings, one GPU; "
                          "c3: BPRMF k=128 (N > 1: user shards); c5: WRMF k=256")
+    ap.add_argument("--runs", type=int, default=-1, choices=[-1, 0, 1],
+                    help="user runs of the BiasedMF Hogwild epochs (mml_bmf_set_hogwild_runs): "
+                         "-1 = the library's default (on unless --phases is set), 0 = the user "
+                         "phases, 1 = on")
     ap.add_argument("--phases", type=int, default=0,
                     help="user phases of the Hogwild epochs (mml_bmf_set_hogwild_phases / "
                          "mml_bpr_set_hogwild_phases): 0 = the library's default, 1 = none")
@@ -175,6 +192,7 @@ def bench_c2(args):
     N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(params), n_users_total, n_items,
                                    ctypes.byref(h)))
     N.check(N.lib().mml_bmf_set_hogwild_phases(h, args.phases))
+    N.check(N.lib().mml_bmf_set_hogwild_runs(h, args.runs))
     if ring:  # a multi-device context takes host arrays and deals them out in set_blocks
         hu_, hi_, hv_ = users.cpu().numpy(), items.cpu().numpy(), values.cpu().numpy()
         N.check(N.lib().mml_bmf_set_data(h, N.ptr(hu_, N._i32p), N.ptr(hi_, N._i32p),
@@ -244,14 +262,18 @@ def bench_c2(args):
     total_updates = n_local * world * args.steps
     value = total_updates / elapsed
     avg_kernel_ms = float(np.mean(kernel_ms))
-    bpu = bytes_per_update(k)
-    achieved = n_local * bpu / (avg_kernel_ms * 1e-3) / 1e9
+    n_runs = last_runs(h) if args.schedule == "hogwild" and not ring else 0
+    alg = runs_bytes(k, n_local, n_runs) if n_runs else n_local * bytes_per_update(k)
+    bpu = alg / n_local
+    achieved = alg / (avg_kernel_ms * 1e-3) / 1e9
     traffic, traffic_note = None, None
-    if k == 64 and n_local == 100_000_000 and args.schedule == "hogwild":
+    if k == 64 and n_local == 100_000_000 and args.schedule == "hogwild" and not n_runs:
         traffic, traffic_note = pmc_traffic("r5_c2_traffic.json", avg_kernel_ms)
+    if n_runs and k == 64 and n_local == 100_000_000:
+        traffic, traffic_note = pmc_traffic("r6_c2_runs_traffic.json", avg_kernel_ms)
     kernel = (N.last_kernel("mml_bmf_last_kernel", h) or
               f"bmf_sgd_ordered_kernel (schedule {args.schedule})")
-    ceiling = (box_ceiling("mml_bmf_replay_traffic", h, avg_kernel_ms, n_local * bpu)
+    ceiling = (box_ceiling("mml_bmf_replay_traffic", h, avg_kernel_ms, alg)
                if args.schedule == "hogwild" else None)
 
     cpu = None
@@ -450,6 +472,7 @@ def gpu_slice_epoch(model, k, n_users, n_items, gb, sample, test):
                                          N.ptr(tv, N._f32p), len(tu), N.ptr(out, N._f32p)))
         phases = ctypes.c_int32(0)
         N.check(N.lib().mml_bmf_last_phases(h, ctypes.byref(phases)))
+        runs = last_runs(h)
         n = len(u)
         su, si, sv = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.float32)
         off = np.zeros(8 * 32 + 1, np.int64)
@@ -460,13 +483,13 @@ def gpu_slice_epoch(model, k, n_users, n_items, gb, sample, test):
         # (no XCD-grouped stream, e.g. a device without 8 XCD groups: the oracle legs then run
         # over the slice's visit order only)
         stream = (su, si, sv, off[: spans.value + 1].copy()) if st == N.MML_OK else None
-        return float(out[0]), phases.value, stream
+        return float(out[0]), phases.value, runs, stream
     finally:
         N.lib().mml_bmf_destroy(h)
         ctx.close()
 
 
-def oracle_slice_epochs(model, k, gb, sample, stream, test):
+def oracle_slice_epochs(model, k, gb, sample, stream, test, runs=0):
     """The reference's own loop beside gpu_slice_epoch, from the same InitModel, one epoch each,
     test RMSE: the sequential Iterate() (BiasedMatrixFactorization.cs:264-310) over the stream
     the GPU walked, and over the slice's own visit order; and the Hogwild staleness model of the
@@ -497,7 +520,9 @@ def oracle_slice_epochs(model, k, gb, sample, stream, test):
         for p in range((len(off) - 1) // 8):
             O.bmf_iterate_lockstep(su, si, sv,
                                    np.arange(off[8 * p], off[8 * p + 8], dtype=np.int32), *m,
-                                   streams=waves, step=64 // lpr, threads=cpu_threads(), **kw)
+                                   # the user runs: every lane group a stream, one rating a step
+                                   streams=waves * (64 // lpr) if runs else waves,
+                                   step=1 if runs else 64 // lpr, threads=cpu_threads(), **kw)
         out["lockstep_gpu_order"] = rmse(*m)
     u, i, v = sample
     m = [a.copy() for a in model]
@@ -549,6 +574,7 @@ def bench_c4(args):
     N.check(N.lib().mml_bmf_create(ctx.handle, ctypes.byref(params), n_users, n_items,
                                    ctypes.byref(h)))
     N.check(N.lib().mml_bmf_set_hogwild_phases(h, args.phases))
+    N.check(N.lib().mml_bmf_set_hogwild_runs(h, args.runs))
     t0 = time.perf_counter()
     N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
                                             values.data_ptr(), n_local, None))
@@ -609,31 +635,35 @@ def bench_c4(args):
     kernel = N.last_kernel("mml_bmf_last_kernel", h)
     phases = ctypes.c_int32(0)
     N.check(N.lib().mml_bmf_last_phases(h, ctypes.byref(phases)))
-    ceiling = box_ceiling("mml_bmf_replay_traffic", h, float(np.mean(kernel_ms)),
-                          n_local * bytes_per_update(k))
+    n_runs = last_runs(h)
+    alg = runs_bytes(k, n_local, n_runs) if n_runs else n_local * bytes_per_update(k)
+    ceiling = box_ceiling("mml_bmf_replay_traffic", h, float(np.mean(kernel_ms)), alg)
     rmse = evaluate()
     value = n_total * args.steps / elapsed
     avg_kernel_ms = float(np.mean(kernel_ms))
-    bpu = bytes_per_update(k)
-    achieved = n_local * bpu / (avg_kernel_ms * 1e-3) / 1e9
+    bpu = alg / n_local
+    achieved = alg / (avg_kernel_ms * 1e-3) / 1e9
     traffic, traffic_note = None, None
     if world == 1 and k == 64 and n_total == 1_000_000_000:
-        traffic, traffic_note = pmc_traffic("r5_c4_traffic.json", avg_kernel_ms)
+        traffic, traffic_note = pmc_traffic("r6_c4_runs_traffic.json" if n_runs else
+                                            "r5_c4_traffic.json", avg_kernel_ms)
     # the phase schedule's RMSE lag at C4 itself: the same handle, InitModel again, the same epochs
     # in one phase (after the timed region; tests/test_phases_c4_gpu.py pins the lag against the
     # oracle over the exported stream on a C4-shaped 100 M set)
     phase_lag = None
-    if world == 1 and phases.value > 1:
+    if world == 1 and (phases.value > 1 or n_runs):
         N.check(N.lib().mml_bmf_set_hogwild_phases(h, 1))
+        N.check(N.lib().mml_bmf_set_hogwild_runs(h, 0))
         N.check(N.lib().mml_bmf_init_model(h, 4, 0.0, 0.1, gb, 1.0, 5.0))
         for _ in range(args.warmup + args.steps):
             N.check(N.lib().mml_bmf_iterate(h, lr, None))
         r1 = evaluate()
         phase_lag = {"final_rmse_one_phase": r1, "lag": rmse - r1,
-                     "note": f"final_rmse ({phases.value} user phases) minus the same "
-                             f"{args.warmup + args.steps} epochs from the same InitModel in one "
-                             f"phase, on this GPU after the timed region (both Hogwild: the "
-                             f"run-to-run spread is ~1e-4)"}
+                     "note": f"final_rmse ("
+                             f"{f'{n_runs} user runs' if n_runs else f'{phases.value} user phases'})"
+                             f" minus the same {args.warmup + args.steps} epochs from the same "
+                             f"InitModel in one phase without runs, on this GPU after the timed "
+                             f"region (both Hogwild: the run-to-run spread is ~1e-4)"}
     N.lib().mml_bmf_destroy(h)
     h = None
     cpu, slice_rmse = None, None
@@ -644,13 +674,13 @@ def bench_c4(args):
         m_t = seen[tus]
         slice_test = (tus[m_t].copy(), tis[m_t].copy(), tvs[m_t].copy())
         cpu = cpu_baseline_dsgd(init, k, n_users, n_items, gb, cpu_sample, "C4", slice_test)
-        g_rmse, g_phases, g_stream = gpu_slice_epoch(init, k, n_users, n_items, gb, cpu_sample,
-                                                     slice_test)
-        ora = oracle_slice_epochs(init, k, gb, cpu_sample, g_stream, slice_test)
+        g_rmse, g_phases, g_runs, g_stream = gpu_slice_epoch(init, k, n_users, n_items, gb,
+                                                             cpu_sample, slice_test)
+        ora = oracle_slice_epochs(init, k, gb, cpu_sample, g_stream, slice_test, g_runs)
         del g_stream
         o_seq = ora["sequential_gpu_order"]
         o_lock = ora["lockstep_gpu_order"]
-        slice_rmse = {"gpu": g_rmse, "gpu_user_phases": g_phases,
+        slice_rmse = {"gpu": g_rmse, "gpu_user_phases": g_phases, "gpu_user_runs": g_runs,
                       "oracle_sequential_gpu_order": o_seq,
                       "gpu_minus_oracle_sequential": None if o_seq is None else g_rmse - o_seq,
                       "oracle_lockstep_gpu_order": o_lock,
@@ -690,7 +720,8 @@ def bench_c4(args):
                        "num_factors": k, "ratings_total": n_total, "ratings_per_gpu": n_local,
                        "users": n_users, "items": n_items, "schedule": "hogwild",
                        "parallelism": f"user-shard x{world}", "generate_s": gen_s,
-                       "device_ingest_s": ingest_s, "user_phases": phases.value},
+                       "device_ingest_s": ingest_s, "user_phases": phases.value,
+                       "user_runs": n_runs},
             "final_rmse": rmse,
             "initial_rmse": rmse0,
             "phase_lag_c4": phase_lag,

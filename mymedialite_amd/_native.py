@@ -154,6 +154,8 @@ SIGNATURES = {
     "mml_bpr_set_hogwild_phases": (_st, [_vp, ctypes.c_int32]),
     "mml_bpr_last_phases": (_st, [_vp, ctypes.POINTER(ctypes.c_int32)]),
     "mml_bmf_last_phases": (_st, [_vp, ctypes.POINTER(ctypes.c_int32)]),
+    "mml_bmf_set_hogwild_runs": (_st, [_vp, ctypes.c_int32]),
+    "mml_bmf_last_runs": (_st, [_vp, _i64p]),
     "mml_bmf_hogwild_stream": (_st, [_vp, _i32p, _i32p, _f32p, ctypes.c_int64, _i64p,
                                      ctypes.c_int32, _i32p]),
     "mml_bpr_replay_traffic": (_st, [_vp, _f32p]),

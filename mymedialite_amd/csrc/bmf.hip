@@ -475,6 +475,139 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
     }
 }
 
+// HOGWILD in user runs (mml_bmf_set_hogwild_runs, ABI 14).  Each XCD group's span is sorted by
+// user (ensure_runs: stable, so a user's ratings keep their visit order), so a user's ratings of
+// one group form a run.  Every lane group (LPR lanes, one rating at a time) walks its own
+// contiguous slice of the wave's chunk, both slice ends moved to run starts, so a run belongs to
+// one lane group: U_u and b_u are loaded once at the run's start (write-through mode, past any
+// stale L2 copy), updated in registers rating after rating -- the reference's sequential
+// arithmetic within the run -- and written through once at its end.  The item rows and biases
+// keep the XCD-owned L2-served accesses and the racy Hogwild stores.  Where the phase schedule
+// moves every rating's U row through the L2 twice (read, dirty write-back), a run moves it once
+// each way.  A user's runs of the 8 groups are kept apart in time by ensure_runs' per-group
+// rotation of the user order (group g starts its span at user g U / 8).
+#ifndef MML_RUNS_WPE  // (experiments: A/B) the runs kernel's waves-per-SIMD bound
+#define MML_RUNS_WPE 1
+#endif
+template <int LOSS, int LPR, int AM>
+__global__ __launch_bounds__(256, MML_RUNS_WPE) void bmf_sgd_runs_kernel(
+    const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
+    const int64_t* __restrict__ goff, int32_t ng, int32_t waves_per_group, float* U, float* V,
+    float* bu, float* bi, int32_t ld4, uint32_t v_bytes, uint32_t bi_bytes, uint32_t u_bytes,
+    uint32_t bu_bytes, int32_t flushers, BmfScalars s, const int32_t* __restrict__ cnt_u,
+    const int32_t* __restrict__ cnt_i) {
+    static_assert(LPR >= 1 && LPR <= 64, "lanes per rating");
+    constexpr int RPW = 64 / LPR;  // lane groups (runs in flight) per wave
+    constexpr bool IL2 = (AM & kAccItemL2) != 0, UTH = (AM & kAccUserThru) != 0;
+    constexpr bool biased = LOSS != kPlainMF;
+    const int lane = threadIdx.x & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const mml::GroupWave gw = mml::group_wave(goff, ng, waves_per_group, wib, blockDim.x >> 6);
+    const int grp = (int)(blockIdx.x % (uint32_t)ng);
+    const int64_t g0 = goff[grp], g1 = goff[grp + 1];
+    const int sub = lane / LPR, q = lane % LPR;
+    float4* U4 = reinterpret_cast<float4*>(U);
+    float4* V4 = reinterpret_cast<float4*>(V);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t vrs = mml::buffer_rsrc(V, v_bytes);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t brs = mml::buffer_rsrc(bi, bi_bytes);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t urs = mml::buffer_rsrc(U, u_bytes);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t burs = mml::buffer_rsrc(bu, bu_bytes);
+    [[maybe_unused]] const bool flusher =
+        (AM & kAccFlush) != 0 && (threadIdx.x >> 6) == 0 &&
+        (blockIdx.x >> 3) % max(1u, (gridDim.x >> 3) / (uint32_t)flushers) == 0;
+    // this lane group's slice; a bound inside a run moves to the run's end (the same move for the
+    // slices on both sides of it, so every run has exactly one owner)
+    const int64_t per = (gw.end - gw.begin + RPW - 1) / RPW;
+    auto run_start = [&](int64_t x) {
+        while (x > g0 && x < g1 && su[x] == su[x - 1]) ++x;
+        return x;
+    };
+    const int64_t b = run_start(min(gw.begin + sub * per, gw.end));
+    const int64_t e = run_start(min(gw.begin + (sub + 1) * per, gw.end));
+    // the wave's trip count: the longest slice (wave-uniform)
+    int64_t steps = e - b;
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1) steps = max(steps, (int64_t)__shfl_xor((long long)steps, o));
+    steps = __builtin_amdgcn_readfirstlane((int)steps);
+    int32_t cur = -1;
+    float4 pu = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float bu_u = 0.0f;
+    const int64_t ou0 = q;  // this lane's float4 of a row
+    auto put_user = [&]() {  // the run's U_u and b_u, written through
+        const int64_t ou = (int64_t)cur * ld4 + ou0;
+        if constexpr (UTH)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, pu), urs,
+                (uint32_t)ou * 16u, 0, 16);
+        else
+            store4<false>(U4 + ou, pu);
+        if (biased && q == 0) {
+            if constexpr (UTH)
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bu_u), burs,
+                                                      (uint32_t)cur * 4u, 0, 16);
+            else
+                bu[cur] = bu_u;
+        }
+    };
+    int32_t my_u = 0, my_i = 0;
+    float my_r = 0.0f;
+    for (int64_t t = 0; t < steps; ++t) {
+        if ((t % LPR) == 0) {
+            if constexpr ((AM & kAccFlush) != 0)
+                if (flusher) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            // the next LPR entries of every slice, one per lane of its group
+            const int64_t x = b + t + q;
+            const bool in = x < e;
+            my_u = in ? su[x] : -1;
+            my_i = in ? si[x] : 0;
+            my_r = in ? sr[x] : 0.0f;
+        }
+        const int src = sub * LPR + (int)(t % LPR);
+        const int32_t u = __shfl(my_u, src);
+        const int32_t i = __shfl(my_i, src);
+        const float r = __shfl(my_r, src);
+        if (u < 0) continue;  // this slice is done (lane-group divergent)
+        if (u != cur) {  // a run starts: the previous one's row goes out, this one's comes in
+            if (cur >= 0) put_user();
+            cur = u;
+            const int64_t ou = (int64_t)u * ld4 + ou0;
+            if constexpr (UTH) pu = mml::load4_l2(urs, (uint32_t)ou * 16u);
+            else pu = U4[ou];
+            if constexpr (biased) {
+                if constexpr (UTH) bu_u = mml::load1_l2(burs, (uint32_t)u * 4u);
+                else bu_u = bu[u];
+            }
+        }
+        const int64_t oi = (int64_t)i * ld4 + ou0;
+        float4 qi;
+        float bi_i = 0.0f;
+        if constexpr (IL2) qi = mml::load4_l2(vrs, (uint32_t)oi * 16u);
+        else qi = V4[oi];
+        if constexpr (biased) {
+            if constexpr (IL2) bi_i = mml::load1_l2(brs, (uint32_t)i * 4u);
+            else bi_i = bi[i];
+        }
+        if constexpr (LOSS == kReplayTraffic) {
+            asm volatile("" : "+v"(qi.x), "+v"(qi.y), "+v"(qi.z), "+v"(qi.w), "+v"(bi_i) : "v"(r));
+            if (q == 0) bi[i] = bi_i;
+            V4[oi] = qi;
+        } else {
+            float part = ((pu.x * qi.x + pu.y * qi.y) + pu.z * qi.z) + pu.w * qi.w;
+            part = group_sum<LPR>(part);
+            const RatingStep<LOSS> st(s, part, bu_u, bi_i, r, cnt_u, cnt_i, u, i);
+            if (biased) {
+                bu_u = st.new_bu;
+                if (q == 0) bi[i] = st.new_bi;
+            }
+            V4[oi] = make_float4(st.new_i(s, pu.x, qi.x), st.new_i(s, pu.y, qi.y),
+                                 st.new_i(s, pu.z, qi.z), st.new_i(s, pu.w, qi.w));
+            pu = make_float4(st.new_u(s, pu.x, qi.x), st.new_u(s, pu.y, qi.y),
+                             st.new_u(s, pu.z, qi.z), st.new_u(s, pu.w, qi.w));
+        }
+    }
+    if (cur >= 0) put_user();
+}
+
 // BiasedMatrixFactorization.Predict(int,int) (:313-325): double score, float dot in order.
 // plain: MatrixFactorization.Predict(int,int) (MatrixFactorization.cs:251-258 + :205-217):
 // global_bias for ids beyond the model, else global_bias + dot clipped to [min, max].
@@ -1488,6 +1621,12 @@ struct mml_bmf {
     int32_t phases_req = 0;       // mml_bmf_set_hogwild_phases (0: by the active users' bytes)
     int64_t active_users = -1;    // users with a rating in this handle (ensure_xstream)
     mml::DeviceArray<int64_t> poff;
+    // user runs (mml_bmf_set_hogwild_runs): every XCD group's span of the group-major stream
+    // sorted by user, rotated per group (ensure_runs); the spans are xs.goff's
+    int32_t runs_req = -1;  // -1: on unless mml_bmf_set_hogwild_phases chose a phase count
+    bool has_runs = false, last_runs = false;  // last_runs: the last Hogwild epoch ran in runs
+    int64_t n_runs = 0;                        // runs of the runs stream (ensure_runs)
+    mml::DeviceArray<int32_t> rxu, rxi, rxr;
     // multi-device context: one single-device handle per GPU over a user range ub[d] .. ub[d + 1]
     // (U, b_u trained there; V, b_i replicated and averaged after every epoch)
     std::vector<mml_bmf*> shards;
@@ -1593,6 +1732,7 @@ void finish_data(mml_bmf* h, const int32_t* order_dev) {
     h->has_positions = false;
     h->has_xstream = false;
     h->n_phases = 1;
+    h->has_runs = false;
     h->has_data = true;
 }
 
@@ -1865,6 +2005,98 @@ void ensure_phases(mml_bmf* h, int32_t P) {
     h->n_phases = P;
 }
 
+// key of position x of the group-major stream for the user runs: group * n_users + the user's
+// rank in the group's rotated order (group g starts at user g n_users / 8, so a user's runs of the
+// 8 groups come ~1/8 of an epoch apart)
+__global__ __launch_bounds__(256) void run_keys_kernel(const int32_t* __restrict__ xu,
+                                                       const int64_t* __restrict__ goff, int64_t n,
+                                                       int32_t n_users, uint32_t* __restrict__ key,
+                                                       int32_t* __restrict__ idx) {
+    int64_t g_off[9];
+#pragma unroll
+    for (int g = 0; g < 9; ++g) g_off[g] = goff[g];
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        int g = 0;
+#pragma unroll
+        for (int c = 1; c < 8; ++c) g += x >= g_off[c];
+        const int64_t shift = (int64_t)g * n_users / 8;
+        const int64_t rot = ((int64_t)xu[x] - shift + n_users) % n_users;
+        key[x] = (uint32_t)((int64_t)g * n_users + rot);
+        idx[x] = (int32_t)x;
+    }
+}
+
+// runs of the runs stream: positions that start a group span or follow another user's rating
+__global__ __launch_bounds__(256) void count_runs_kernel(const int32_t* __restrict__ su,
+                                                         const int64_t* __restrict__ goff,
+                                                         int64_t n,
+                                                         unsigned long long* __restrict__ out) {
+    int64_t g_off[9];
+#pragma unroll
+    for (int g = 0; g < 9; ++g) g_off[g] = goff[g];
+    unsigned long long c = 0;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        bool start = x == 0 || su[x] != su[x - 1];
+#pragma unroll
+        for (int g = 1; g < 8; ++g) start = start || x == g_off[g];
+        c += start ? 1 : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
+// the user-runs stream (built once per data set): the group-major XCD stream, each group's span
+// stably sorted by the rotated user order
+void ensure_runs(mml_bmf* h) {
+    if (h->has_runs) return;
+    if (h->n_phases != 1) ensure_phases(h, 1);
+    ensure_xstream(h);
+    MML_REQUIRE((int64_t)h->n_users * 8 < (1ll << 31), "user runs: at most 2^28 users");
+    hipStream_t st = h->ctx->stream;
+    const int64_t n = h->n;
+    int end_bit = 1;
+    while ((1ll << end_bit) < (int64_t)h->n_users * 8) ++end_bit;
+    mml::DeviceArray<uint32_t> key, key_s;
+    mml::DeviceArray<int32_t> idx, idx_s;
+    key.alloc(n);
+    key_s.alloc(n);
+    idx.alloc(n);
+    idx_s.alloc(n);
+    run_keys_kernel<<<grid_for(n), 256, 0, st>>>(h->xu.get(), h->xs.goff.get(), n, h->n_users,
+                                                 key.get(), idx.get());
+    MML_HIP(hipGetLastError());
+    size_t tmp_bytes = 0;
+    MML_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, key.get(), key_s.get(), idx.get(),
+                                      idx_s.get(), n, 0, end_bit, st));
+    mml::DeviceArray<uint8_t> tmp;
+    tmp.alloc(std::max<size_t>(1, tmp_bytes));
+    MML_HIP(rocprim::radix_sort_pairs(tmp.get(), tmp_bytes, key.get(), key_s.get(), idx.get(),
+                                      idx_s.get(), n, 0, end_bit, st));
+    key.reset();
+    key_s.reset();
+    idx.reset();
+    tmp.reset();
+    h->rxu.alloc(n);
+    h->rxi.alloc(n);
+    h->rxr.alloc(n);
+    gather3_kernel<<<grid_for(n), 256, 0, st>>>(idx_s.get(), n, h->xu.get(), h->xi.get(),
+                                                h->xr.get(), h->rxu.get(), h->rxi.get(),
+                                                h->rxr.get());
+    MML_HIP(hipGetLastError());
+    mml::DeviceArray<unsigned long long> cnt;
+    cnt.alloc(1);
+    MML_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(unsigned long long), st));
+    count_runs_kernel<<<grid_for(n), 256, 0, st>>>(h->rxu.get(), h->xs.goff.get(), n, cnt.get());
+    MML_HIP(hipGetLastError());
+    unsigned long long runs = 0;
+    MML_HIP(hipMemcpyAsync(&runs, cnt.get(), sizeof(runs), hipMemcpyDeviceToHost, st));
+    MML_HIP(hipStreamSynchronize(st));
+    h->n_runs = n > 0 ? (int64_t)runs : 0;
+    h->has_runs = true;
+}
+
 // MML_HOGWILD_XCD: 4 (default) = XCD-owned item groups with L2-served item loads, user rows written
 // through and flushing waves; 1 = the groups with L2-served item loads only, 2 = the groups
 // with plain loads, 3 = 1 + user rows written through, 4 = 3 + flushing waves (mml::flushers_per_xcd),
@@ -1900,6 +2132,7 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
     const int32_t *su = h->su.get(), *si = h->si.get();
     const float* sr = h->sr.get();
     int am = coh ? kAccCoherent : kAccPlain;
+    bool runs = false;
     if (waves < 16) {
         waves = 4;
     } else if (!coh && xmode > 0 && v_bytes < (1ull << 32) && mml::xcd_groups(h->ctx) == 8) {
@@ -1924,14 +2157,26 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
 #endif
             default: am = kAccItemL2; break;
         }
-        // user phases: one launch per phase over the phase-major stream
-        const int32_t P = hogwild_phases(h);
-        if (P != h->n_phases) ensure_phases(h, P);
-        su = h->xu.get();
-        si = h->xi.get();
-        sr = reinterpret_cast<const float*>(h->xr.get());
+        const bool want_runs =
+            h->runs_req > 0 || (h->runs_req < 0 && h->phases_req == 0 && hogwild_phases_env() < 0);
+        if (want_runs && (am & kAccUserThru) != 0) {
+            // user runs: one launch over the group-major stream sorted by user within a group
+            ensure_runs(h);
+            runs = true;
+            su = h->rxu.get();
+            si = h->rxi.get();
+            sr = reinterpret_cast<const float*>(h->rxr.get());
+        } else {
+            // user phases: one launch per phase over the phase-major stream
+            const int32_t P = hogwild_phases(h);
+            if (P != h->n_phases) ensure_phases(h, P);
+            su = h->xu.get();
+            si = h->xi.get();
+            sr = reinterpret_cast<const float*>(h->xr.get());
+        }
     }
-    const int32_t phases = ng == 8 ? h->n_phases : 1;
+    const int32_t phases = ng == 8 && !runs ? h->n_phases : 1;
+    if (LOSS != kReplayTraffic) h->last_runs = runs;
     int64_t blocks = (waves + 3) / 4;
     blocks = (blocks + ng - 1) / ng * ng;
     const int32_t wpg = (int32_t)(blocks / ng * 4);
@@ -1966,6 +2211,29 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
         MML_HOG_EXP(LPR, VPL)                                                    \
         default: MML_HOG1(LPR, VPL, kAccPlain); break;                           \
     }
+#define MML_RUN1(LPR, AM)                                                                        \
+    bmf_sgd_runs_kernel<LOSS, LPR, AM><<<(int)blocks, 256, 0, st>>>(                              \
+        su, si, sr, goff, ng, wpg, h->U.get(), h->V.get(), h->bu.get(), h->bi.get(), ld4, vb, bb, \
+        ub, bub, mml::flushers_per_xcd(1), s, cu, ci);                                           \
+    h->last_kernel = kernel_label("bmf_sgd_runs_kernel", {LOSS, LPR, (int)(AM)})
+// (no flushing waves: a group's item rows are read by its own XCD only, and the runs write U_u
+// through; with them C4 was 112.3 / 113.2 against 107.0 / 107.3 ms per epoch, profiles/r6/runs/)
+#define MML_RUNV(LPR) MML_RUN1(LPR, kAccItemL2 | kAccUserThru)
+    if (runs) {
+        switch (h->lpr) {
+            case 1: MML_RUNV(1); break;
+            case 2: MML_RUNV(2); break;
+            case 4: MML_RUNV(4); break;
+            case 8: MML_RUNV(8); break;
+            case 16: MML_RUNV(16); break;
+            case 32: MML_RUNV(32); break;
+            default: MML_RUNV(64); break;
+        }
+        MML_HIP(hipGetLastError());
+        return;
+    }
+#undef MML_RUNV
+#undef MML_RUN1
     // one float4 of U_u and of V_i per lane (VPL 2 measured equal, VPL 4 10 % slower on C2)
     for (int32_t ph = 0; ph < phases; ++ph) {
         const int64_t* go = phases > 1 ? h->poff.get() + 8 * ph : goff;
@@ -3298,6 +3566,24 @@ extern "C" mml_status mml_bmf_set_hogwild_phases(mml_bmf* h, int32_t phases) {
     });
 }
 
+extern "C" mml_status mml_bmf_set_hogwild_runs(mml_bmf* h, int32_t on) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(on >= -1 && on <= 1, "on must be -1 (default), 0 or 1");
+        h->runs_req = on;
+        for (mml_bmf* s : h->shards) s->runs_req = on;
+    });
+}
+
+extern "C" mml_status mml_bmf_last_runs(mml_bmf* h, int64_t* out) {
+    return guard([&] {
+        check_handle(h);
+        MML_REQUIRE(out, "out is null");
+        const mml_bmf* s = h->shards.empty() ? h : h->shards[0];
+        *out = s->last_runs ? s->n_runs : 0;
+    });
+}
+
 extern "C" mml_status mml_bmf_last_phases(mml_bmf* h, int32_t* out) {
     return guard([&] {
         check_handle(h);
@@ -3316,19 +3602,20 @@ extern "C" mml_status mml_bmf_hogwild_stream(mml_bmf* h, int32_t* users, int32_t
         MML_REQUIRE(h->has_data && n == h->n, "n must equal the handle's rating count");
         MML_REQUIRE(h->has_xstream,
                     "no XCD-grouped stream: run a HOGWILD epoch on an 8-XCD device first");
-        const int32_t spans = h->n_phases * 8;
+        const bool runs = h->last_runs && h->has_runs;  // the user-runs stream (one launch)
+        const int32_t spans = runs ? 8 : h->n_phases * 8;
         MML_REQUIRE(cap_offsets >= spans + 1, "span_offsets holds fewer than phases * 8 + 1");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
         if (n > 0) {
-            MML_HIP(hipMemcpyAsync(users, h->xu.get(), sizeof(int32_t) * n,
+            MML_HIP(hipMemcpyAsync(users, (runs ? h->rxu : h->xu).get(), sizeof(int32_t) * n,
                                    hipMemcpyDeviceToHost, st));
-            MML_HIP(hipMemcpyAsync(items, h->xi.get(), sizeof(int32_t) * n,
+            MML_HIP(hipMemcpyAsync(items, (runs ? h->rxi : h->xi).get(), sizeof(int32_t) * n,
                                    hipMemcpyDeviceToHost, st));
-            MML_HIP(hipMemcpyAsync(values, h->xr.get(), sizeof(float) * n,
+            MML_HIP(hipMemcpyAsync(values, (runs ? h->rxr : h->xr).get(), sizeof(float) * n,
                                    hipMemcpyDeviceToHost, st));
         }
-        const int64_t* off = h->n_phases > 1 ? h->poff.get() : h->xs.goff.get();
+        const int64_t* off = h->n_phases > 1 && !runs ? h->poff.get() : h->xs.goff.get();
         MML_HIP(hipMemcpyAsync(span_offsets, off, sizeof(int64_t) * (spans + 1),
                                hipMemcpyDeviceToHost, st));
         MML_HIP(hipStreamSynchronize(st));

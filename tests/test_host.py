@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert set(declared) == set(N.SIGNATURES), set(declared) ^ set(N.SIGNATURES)
-    assert L.mml_abi_version() == 13
+    assert L.mml_abi_version() == 14
 
 
 def test_no_device_is_an_error_not_a_crash():

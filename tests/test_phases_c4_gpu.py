@@ -84,7 +84,7 @@ def _evaluate(h, test):
 
 
 def _gpu(data, test, gb, *, phases=0, devices=0, want_init=False, want_stream=False, nu=NU,
-         ni=NI, k=K, epochs=EPOCHS):
+         ni=NI, k=K, epochs=EPOCHS, runs=0):
     """One training run: RMSE after each epoch; optionally the InitModel and the exported stream."""
     users, items, values = data
     n = users.numel()
@@ -97,6 +97,7 @@ def _gpu(data, test, gb, *, phases=0, devices=0, want_init=False, want_stream=Fa
         N.check(N.lib().mml_bmf_set_data_device(h, users.data_ptr(), items.data_ptr(),
                                                 values.data_ptr(), n, None))
         N.check(N.lib().mml_bmf_set_hogwild_phases(h, phases))
+        N.check(N.lib().mml_bmf_set_hogwild_runs(h, runs))
         N.check(N.lib().mml_bmf_init_model(h, SEED, 0.0, 0.1, gb, 1.0, 5.0))
         if want_init:
             m = (np.empty((nu, k), np.float32), np.empty((ni, k), np.float32),
@@ -169,14 +170,15 @@ def _hogwild_streams(n, k=K):
 
 
 def _oracle_run(name, init, stream, test, gb, *, lockstep=False, shards=None, epochs=EPOCHS,
-                threads=1, k=K):
+                threads=1, k=K, streams=None):
     """The oracle over `stream` = (users, items, ratings, span offsets) from `init`, EPOCHS times;
     test RMSE per epoch.
       * lockstep=False: the sequential Iterate() (BiasedMatrixFactorization.cs:264-310) in stream
         order;
       * lockstep=True: the staleness model of hogwild_band (ora_bmf_iterate_lockstep): every launch
         = one phase's 8 spans cut into the launch's waves, 4 ratings per wave step, reads before
-        the step, writes in stream order;
+        the step, writes in stream order; streams = (W, R) instead of the phase kernel's (the
+        user runs: every lane group a stream, one rating per step);
       * shards = user bounds: each user shard runs over its own ratings (stream order) from the
         same item side, then V || b_i are averaged over the shards (bench.py at N > 1; the shard's
         launch has its own wave count)."""
@@ -196,7 +198,7 @@ def _oracle_run(name, init, stream, test, gb, *, lockstep=False, shards=None, ep
     if shards is None:
         P = (len(off) - 1) // 8
         launches = [np.arange(off[8 * p], off[8 * p + 8], dtype=np.int32) for p in range(P)]
-        waves = _hogwild_streams(len(su), k)
+        waves = streams or _hogwild_streams(len(su), k)
     else:
         shard_of = np.searchsorted(shards, su, side="right") - 1
         idx = [np.flatnonzero(shard_of == d).astype(np.int32) for d in range(len(shards) - 1)]
