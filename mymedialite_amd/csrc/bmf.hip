@@ -484,8 +484,55 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
 // arithmetic within the run -- and written through once at its end.  The item rows and biases
 // keep the XCD-owned L2-served accesses and the racy Hogwild stores.  Where the phase schedule
 // moves every rating's U row through the L2 twice (read, dirty write-back), a run moves it once
-// each way.  A user's runs of the 8 groups are kept apart in time by ensure_runs' per-group
-// rotation of the user order (group g starts its span at user g U / 8).
+// each way.  A user's runs of the 8 groups are kept apart in time by the slices' rotated walks
+// (run_slice).
+//
+// A lane group's slice of the runs stream: [b, e) of its wave's chunk, both ends moved to run
+// starts (the same move for the slices on both sides of a bound, so every run has exactly one
+// owner), walked from rot = the run start 1/8 grp of the way in, wrapping round to b.  A group's
+// span is sorted by user and the slices of the 8 groups cover about the same users, so a user
+// sits at about the same place in its slice in every group: the rotation puts its 8 runs ~1/8 of
+// a slice's walk apart in time, and no two XCDs hold one user's row in registers at once.
+struct RunSlice {
+    int64_t b, e, rot;
+    __device__ __forceinline__ int64_t at(int64_t t) const {  // position of walk step t
+        const int64_t x = rot + t;
+        return x >= e ? x - (e - b) : x;
+    }
+};
+template <int RPW>
+__device__ __forceinline__ RunSlice run_slice(const int32_t* __restrict__ su, int64_t g0,
+                                              int64_t g1, const mml::GroupWave& gw, int sub,
+                                              int grp) {
+    const int64_t per = (gw.end - gw.begin + RPW - 1) / RPW;
+    auto run_start = [&](int64_t x) {
+        while (x > g0 && x < g1 && su[x] == su[x - 1]) ++x;
+        return x;
+    };
+    RunSlice r;
+    r.b = run_start(min(gw.begin + sub * per, gw.end));
+    r.e = run_start(min(gw.begin + (sub + 1) * per, gw.end));
+    r.rot = r.e > r.b ? run_start(r.b + (r.e - r.b) * grp / 8) : r.b;
+    if (r.rot >= r.e) r.rot = r.b;
+    return r;
+}
+
+// the walk order of the runs kernel's launch (mml_bmf_hogwild_stream): walk[b + t] = the stream
+// position lane group (block, wave, sub) applies at step t
+template <int RPW>
+__global__ __launch_bounds__(256) void runs_walk_kernel(const int32_t* __restrict__ su,
+                                                        const int64_t* __restrict__ goff,
+                                                        int32_t ng, int32_t waves_per_group,
+                                                        int32_t* __restrict__ walk) {
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    const mml::GroupWave gw = mml::group_wave(goff, ng, waves_per_group, wib, blockDim.x >> 6);
+    const int grp = (int)(blockIdx.x % (uint32_t)ng);
+    const int sub = lane / (64 / RPW), q = lane % (64 / RPW);
+    const RunSlice sl = run_slice<RPW>(su, goff[grp], goff[grp + 1], gw, sub, grp);
+    for (int64_t t = q; t < sl.e - sl.b; t += 64 / RPW) walk[sl.b + t] = (int32_t)sl.at(t);
+}
+
 #ifndef MML_RUNS_WPE  // (experiments: A/B) the runs kernel's waves-per-SIMD bound
 #define MML_RUNS_WPE 1
 #endif
@@ -515,17 +562,10 @@ __global__ __launch_bounds__(256, MML_RUNS_WPE) void bmf_sgd_runs_kernel(
     [[maybe_unused]] const bool flusher =
         (AM & kAccFlush) != 0 && (threadIdx.x >> 6) == 0 &&
         (blockIdx.x >> 3) % max(1u, (gridDim.x >> 3) / (uint32_t)flushers) == 0;
-    // this lane group's slice; a bound inside a run moves to the run's end (the same move for the
-    // slices on both sides of it, so every run has exactly one owner)
-    const int64_t per = (gw.end - gw.begin + RPW - 1) / RPW;
-    auto run_start = [&](int64_t x) {
-        while (x > g0 && x < g1 && su[x] == su[x - 1]) ++x;
-        return x;
-    };
-    const int64_t b = run_start(min(gw.begin + sub * per, gw.end));
-    const int64_t e = run_start(min(gw.begin + (sub + 1) * per, gw.end));
+    const RunSlice sl = run_slice<RPW>(su, g0, g1, gw, sub, grp);
+    const int64_t b = sl.b, e = sl.e, len = e - b;
     // the wave's trip count: the longest slice (wave-uniform)
-    int64_t steps = e - b;
+    int64_t steps = len;
 #pragma unroll
     for (int o = LPR; o < 64; o <<= 1) steps = max(steps, (int64_t)__shfl_xor((long long)steps, o));
     steps = __builtin_amdgcn_readfirstlane((int)steps);
@@ -555,9 +595,9 @@ __global__ __launch_bounds__(256, MML_RUNS_WPE) void bmf_sgd_runs_kernel(
         if ((t % LPR) == 0) {
             if constexpr ((AM & kAccFlush) != 0)
                 if (flusher) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            // the next LPR entries of every slice, one per lane of its group
-            const int64_t x = b + t + q;
-            const bool in = x < e;
+            // the next LPR entries of every slice, one per lane of its group, in walk order
+            const bool in = t + q < len;
+            const int64_t x = sl.at(t + q);
             my_u = in ? su[x] : -1;
             my_i = in ? si[x] : 0;
             my_r = in ? sr[x] : 0.0f;
@@ -1622,10 +1662,12 @@ struct mml_bmf {
     int64_t active_users = -1;    // users with a rating in this handle (ensure_xstream)
     mml::DeviceArray<int64_t> poff;
     // user runs (mml_bmf_set_hogwild_runs): every XCD group's span of the group-major stream
-    // sorted by user, rotated per group (ensure_runs); the spans are xs.goff's
+    // sorted by user (ensure_runs); the spans are xs.goff's
     int32_t runs_req = -1;  // -1: on unless mml_bmf_set_hogwild_phases chose a phase count
     bool has_runs = false, last_runs = false;  // last_runs: the last Hogwild epoch ran in runs
     int64_t n_runs = 0;                        // runs of the runs stream (ensure_runs)
+    int64_t run_blocks = 0;                    // the last runs launch's geometry (the export)
+    int32_t run_wpg = 0;
     mml::DeviceArray<int32_t> rxu, rxi, rxr;
     // multi-device context: one single-device handle per GPU over a user range ub[d] .. ub[d + 1]
     // (U, b_u trained there; V, b_i replicated and averaged after every epoch)
@@ -2005,9 +2047,7 @@ void ensure_phases(mml_bmf* h, int32_t P) {
     h->n_phases = P;
 }
 
-// key of position x of the group-major stream for the user runs: group * n_users + the user's
-// rank in the group's rotated order (group g starts at user g n_users / 8, so a user's runs of the
-// 8 groups come ~1/8 of an epoch apart)
+// key of position x of the group-major stream for the user runs: group * n_users + the user
 __global__ __launch_bounds__(256) void run_keys_kernel(const int32_t* __restrict__ xu,
                                                        const int64_t* __restrict__ goff, int64_t n,
                                                        int32_t n_users, uint32_t* __restrict__ key,
@@ -2020,9 +2060,7 @@ __global__ __launch_bounds__(256) void run_keys_kernel(const int32_t* __restrict
         int g = 0;
 #pragma unroll
         for (int c = 1; c < 8; ++c) g += x >= g_off[c];
-        const int64_t shift = (int64_t)g * n_users / 8;
-        const int64_t rot = ((int64_t)xu[x] - shift + n_users) % n_users;
-        key[x] = (uint32_t)((int64_t)g * n_users + rot);
+        key[x] = (uint32_t)((int64_t)g * n_users + xu[x]);
         idx[x] = (int32_t)x;
     }
 }
@@ -2048,7 +2086,7 @@ __global__ __launch_bounds__(256) void count_runs_kernel(const int32_t* __restri
 }
 
 // the user-runs stream (built once per data set): the group-major XCD stream, each group's span
-// stably sorted by the rotated user order
+// stably sorted by user
 void ensure_runs(mml_bmf* h) {
     if (h->has_runs) return;
     if (h->n_phases != 1) ensure_phases(h, 1);
@@ -2220,6 +2258,10 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
 // through; with them C4 was 112.3 / 113.2 against 107.0 / 107.3 ms per epoch, profiles/r6/runs/)
 #define MML_RUNV(LPR) MML_RUN1(LPR, kAccItemL2 | kAccUserThru)
     if (runs) {
+        if (LOSS != kReplayTraffic) {
+            h->run_blocks = blocks;
+            h->run_wpg = wpg;
+        }
         switch (h->lpr) {
             case 1: MML_RUNV(1); break;
             case 2: MML_RUNV(2); break;
@@ -3607,13 +3649,34 @@ extern "C" mml_status mml_bmf_hogwild_stream(mml_bmf* h, int32_t* users, int32_t
         MML_REQUIRE(cap_offsets >= spans + 1, "span_offsets holds fewer than phases * 8 + 1");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
+        mml::DeviceArray<int32_t> wu, wi, wr;
+        const int32_t *eu = h->xu.get(), *ei = h->xi.get(), *er = h->xr.get();
+        if (runs && n > 0) {
+            // the order the lane groups walked: each slice from its rotated start, wrapping round
+            mml::DeviceArray<int32_t> walk;
+            walk.alloc(n);
+            const int rpw = 64 / h->lpr;
+            auto wk = rpw == 64 ? &runs_walk_kernel<64> : rpw == 32 ? &runs_walk_kernel<32>
+                      : rpw == 16 ? &runs_walk_kernel<16> : rpw == 8 ? &runs_walk_kernel<8>
+                      : rpw == 4 ? &runs_walk_kernel<4> : rpw == 2 ? &runs_walk_kernel<2>
+                      : &runs_walk_kernel<1>;
+            wk<<<(int)h->run_blocks, 256, 0, st>>>(h->rxu.get(), h->xs.goff.get(), 8, h->run_wpg,
+                                                   walk.get());
+            wu.alloc(n);
+            wi.alloc(n);
+            wr.alloc(n);
+            gather3_kernel<<<grid_for(n), 256, 0, st>>>(walk.get(), n, h->rxu.get(), h->rxi.get(),
+                                                        h->rxr.get(), wu.get(), wi.get(), wr.get());
+            MML_HIP(hipGetLastError());
+            MML_HIP(hipStreamSynchronize(st));
+            eu = wu.get();
+            ei = wi.get();
+            er = wr.get();
+        }
         if (n > 0) {
-            MML_HIP(hipMemcpyAsync(users, (runs ? h->rxu : h->xu).get(), sizeof(int32_t) * n,
-                                   hipMemcpyDeviceToHost, st));
-            MML_HIP(hipMemcpyAsync(items, (runs ? h->rxi : h->xi).get(), sizeof(int32_t) * n,
-                                   hipMemcpyDeviceToHost, st));
-            MML_HIP(hipMemcpyAsync(values, (runs ? h->rxr : h->xr).get(), sizeof(float) * n,
-                                   hipMemcpyDeviceToHost, st));
+            MML_HIP(hipMemcpyAsync(users, eu, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+            MML_HIP(hipMemcpyAsync(items, ei, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+            MML_HIP(hipMemcpyAsync(values, er, sizeof(float) * n, hipMemcpyDeviceToHost, st));
         }
         const int64_t* off = h->n_phases > 1 && !runs ? h->poff.get() : h->xs.goff.get();
         MML_HIP(hipMemcpyAsync(span_offsets, off, sizeof(int64_t) * (spans + 1),

@@ -9,8 +9,8 @@ sequential Iterate() and hogwild_band's staleness model with the runs kernel's s
 group a stream, one rating per step).  Per epoch the GPU must sit in that band (3x its run-to-run
 spread + 2e-5 of slack).  The order's own cost to the reference's loop, oracle(runs order) -
 oracle(one-phase order), is printed beside the GPU's lag against its one-phase epoch.  The stream
-must hold every rating once, each item in one XCD group's span, each user in one run per group
-span, and each span's users in the group's rotated order."""
+must hold every rating once, each item in one XCD group's span, and each user in one run per
+group span."""
 import ctypes
 from concurrent.futures import ThreadPoolExecutor
 
@@ -23,13 +23,14 @@ NU, NI, N_TRAIN, K, EPOCHS = 800_000, 50_000, 16_000_000, 64, 4
 
 
 def _check_runs_stream(stream, nu):
+    """In the walk order each user's ratings of a group span are one contiguous run."""
     su, si, sv, off = stream
     for g in range(8):
-        u = su[off[g]:off[g + 1]].astype(np.int64)
+        u = su[off[g]:off[g + 1]]
         if len(u) == 0:
             continue
-        rot = (u - g * nu // 8) % nu
-        assert np.all(np.diff(rot) >= 0), f"group {g}: users not in the rotated order"
+        blocks = 1 + int(np.count_nonzero(u[1:] != u[:-1]))
+        assert blocks == len(np.unique(u)), f"group {g}: a user's ratings in two runs"
 
 
 def test_user_runs_pinned_to_the_oracle():
