@@ -292,14 +292,16 @@ mml_status mml_bmf_replay_traffic(mml_bmf* h, float* out_ms);
 mml_status mml_bmf_set_hogwild_phases(mml_bmf* h, int32_t phases);
 mml_status mml_bmf_last_phases(mml_bmf* h, int32_t* out);
 /* User runs of the HOGWILD epoch (ABI 14).  Every XCD group's span is sorted by user (stably: a
- * user's ratings keep their visit order), and one launch walks it with every lane group owning
- * whole runs of one user in a slice of the span, walked from 1/8 g of the way in (group g) and
- * wrapping round, so a user's 8 runs are ~1/8 of a slice apart in time: U_u and b_u are read once
- * per run, updated in registers rating after rating and written through once.  on = -1 (default): on unless mml_bmf_set_hogwild_phases chose a phase count; 1: on; 0:
- * off (the user phases).  Needs U under 4 GiB and the XCD groups, else the phases run.  C4: 107 ms
- * per epoch against 178-194 ms in 26 phases, the same RMSE.  The visit order changes:
- * mml_bmf_hogwild_stream exports it, and the sequential Iterate() over it is the tests' reference
- * (tests/test_runs_gpu.py).  mml_bmf_last_runs: the runs of the last epoch (0: it ran without). */
+ * user's ratings keep their visit order); the epoch runs as 8 launches over strata (users in 8
+ * blocks of equal rating count; launch s gives group g block (g + s) mod 8, so no two XCDs hold one
+ * user's row), and every lane group owns whole runs of one user: U_u and b_u are read once per run,
+ * updated in registers rating after rating and written through once.  on = -1 (default): on from
+ * 16 M ratings unless mml_bmf_set_hogwild_phases chose a phase count; 1: on; 0: off (the user
+ * phases).  Needs U under 4 GiB and the XCD groups, else the phases run.  C4: ~110 ms per epoch
+ * against 178-194 ms in 26 phases, the same RMSE.  The visit order changes:
+ * mml_bmf_hogwild_stream exports it (launch-major, group-minor: 64 spans), and the sequential
+ * Iterate() over it is the tests' reference (tests/test_runs_gpu.py).  mml_bmf_last_runs: the runs
+ * of the last epoch (0: it ran without). */
 mml_status mml_bmf_set_hogwild_runs(mml_bmf* h, int32_t on);
 mml_status mml_bmf_last_runs(mml_bmf* h, int64_t* out);
 /* The stream the last HOGWILD epoch ran on an 8-XCD device (ABI 13; single-device handles): the n

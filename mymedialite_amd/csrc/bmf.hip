@@ -484,62 +484,40 @@ __global__ __launch_bounds__(256) void bmf_sgd_hogwild_kernel(
 // arithmetic within the run -- and written through once at its end.  The item rows and biases
 // keep the XCD-owned L2-served accesses and the racy Hogwild stores.  Where the phase schedule
 // moves every rating's U row through the L2 twice (read, dirty write-back), a run moves it once
-// each way.  A user's runs of the 8 groups are kept apart in time by the slices' rotated walks
-// (run_slice).
+// each way.  A user's runs of the 8 groups must never be in flight at once (one write-back would
+// drop the other's updates), so the epoch runs as 8 launches over DSGD-like strata: users in 8
+// blocks of equal rating count, launch s gives group g the ratings of user block (g + s) mod 8
+// (ensure_runs), so no two XCDs ever hold rows of one user block.
 //
-// A lane group's slice of the runs stream: [b, e) of its wave's chunk, both ends moved to run
+// A lane group's slice of a stratum's span: [b, e) of its wave's chunk, both ends moved to run
 // starts (the same move for the slices on both sides of a bound, so every run has exactly one
-// owner), walked from rot = the run start 1/8 grp of the way in, wrapping round to b.  A group's
-// span is sorted by user and the slices of the 8 groups cover about the same users, so a user
-// sits at about the same place in its slice in every group: the rotation puts its 8 runs ~1/8 of
-// a slice's walk apart in time, and no two XCDs hold one user's row in registers at once.
+// owner), walked in order.
 struct RunSlice {
-    int64_t b, e, rot;
-    __device__ __forceinline__ int64_t at(int64_t t) const {  // position of walk step t
-        const int64_t x = rot + t;
-        return x >= e ? x - (e - b) : x;
-    }
+    int64_t b, e;
+    __device__ __forceinline__ int64_t at(int64_t t) const { return b + t; }
 };
 template <int RPW>
 __device__ __forceinline__ RunSlice run_slice(const int32_t* __restrict__ su, int64_t g0,
-                                              int64_t g1, const mml::GroupWave& gw, int sub,
-                                              int grp) {
+                                              int64_t g1, const mml::GroupWave& gw, int sub) {
     const int64_t per = (gw.end - gw.begin + RPW - 1) / RPW;
     auto run_start = [&](int64_t x) {
         while (x > g0 && x < g1 && su[x] == su[x - 1]) ++x;
         return x;
     };
-    RunSlice r;
-    r.b = run_start(min(gw.begin + sub * per, gw.end));
-    r.e = run_start(min(gw.begin + (sub + 1) * per, gw.end));
-    r.rot = r.e > r.b ? run_start(r.b + (r.e - r.b) * grp / 8) : r.b;
-    if (r.rot >= r.e) r.rot = r.b;
-    return r;
+    return RunSlice{run_start(min(gw.begin + sub * per, gw.end)),
+                    run_start(min(gw.begin + (sub + 1) * per, gw.end))};
 }
 
-// the walk order of the runs kernel's launch (mml_bmf_hogwild_stream): walk[b + t] = the stream
-// position lane group (block, wave, sub) applies at step t
-template <int RPW>
-__global__ __launch_bounds__(256) void runs_walk_kernel(const int32_t* __restrict__ su,
-                                                        const int64_t* __restrict__ goff,
-                                                        int32_t ng, int32_t waves_per_group,
-                                                        int32_t* __restrict__ walk) {
-    const int lane = threadIdx.x & 63;
-    const int wib = threadIdx.x >> 6;
-    const mml::GroupWave gw = mml::group_wave(goff, ng, waves_per_group, wib, blockDim.x >> 6);
-    const int grp = (int)(blockIdx.x % (uint32_t)ng);
-    const int sub = lane / (64 / RPW), q = lane % (64 / RPW);
-    const RunSlice sl = run_slice<RPW>(su, goff[grp], goff[grp + 1], gw, sub, grp);
-    for (int64_t t = q; t < sl.e - sl.b; t += 64 / RPW) walk[sl.b + t] = (int32_t)sl.at(t);
-}
-
+#ifndef MML_RUNS_PF  // (experiments: A/B) the next step's item row requested a step ahead
+#define MML_RUNS_PF 0
+#endif
 #ifndef MML_RUNS_WPE  // (experiments: A/B) the runs kernel's waves-per-SIMD bound
 #define MML_RUNS_WPE 1
 #endif
 template <int LOSS, int LPR, int AM>
 __global__ __launch_bounds__(256, MML_RUNS_WPE) void bmf_sgd_runs_kernel(
     const int32_t* __restrict__ su, const int32_t* __restrict__ si, const float* __restrict__ sr,
-    const int64_t* __restrict__ goff, int32_t ng, int32_t waves_per_group, float* U, float* V,
+    const int64_t* __restrict__ spans, int32_t waves_per_group, float* U, float* V,
     float* bu, float* bi, int32_t ld4, uint32_t v_bytes, uint32_t bi_bytes, uint32_t u_bytes,
     uint32_t bu_bytes, int32_t flushers, BmfScalars s, const int32_t* __restrict__ cnt_u,
     const int32_t* __restrict__ cnt_i) {
@@ -549,9 +527,17 @@ __global__ __launch_bounds__(256, MML_RUNS_WPE) void bmf_sgd_runs_kernel(
     constexpr bool biased = LOSS != kPlainMF;
     const int lane = threadIdx.x & 63;
     const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const mml::GroupWave gw = mml::group_wave(goff, ng, waves_per_group, wib, blockDim.x >> 6);
-    const int grp = (int)(blockIdx.x % (uint32_t)ng);
-    const int64_t g0 = goff[grp], g1 = goff[grp + 1];
+    // this launch's stratum of group grp: [spans[2 grp], spans[2 grp + 1]) (ensure_runs), cut
+    // into the group's waves as mml::group_wave cuts a span
+    const int grp = (int)(blockIdx.x % 8u);
+    const int64_t g0 = spans[2 * grp], g1 = spans[2 * grp + 1];
+    mml::GroupWave gw;
+    {
+        const int64_t w = (int64_t)(blockIdx.x / 8u) * (blockDim.x >> 6) + wib;
+        const int64_t chunk = (g1 - g0 + waves_per_group - 1) / waves_per_group;
+        gw.begin = min(g0 + w * chunk, g1);
+        gw.end = min(gw.begin + chunk, g1);
+    }
     const int sub = lane / LPR, q = lane % LPR;
     float4* U4 = reinterpret_cast<float4*>(U);
     float4* V4 = reinterpret_cast<float4*>(V);
@@ -562,7 +548,7 @@ __global__ __launch_bounds__(256, MML_RUNS_WPE) void bmf_sgd_runs_kernel(
     [[maybe_unused]] const bool flusher =
         (AM & kAccFlush) != 0 && (threadIdx.x >> 6) == 0 &&
         (blockIdx.x >> 3) % max(1u, (gridDim.x >> 3) / (uint32_t)flushers) == 0;
-    const RunSlice sl = run_slice<RPW>(su, g0, g1, gw, sub, grp);
+    const RunSlice sl = run_slice<RPW>(su, g0, g1, gw, sub);
     const int64_t b = sl.b, e = sl.e, len = e - b;
     // the wave's trip count: the longest slice (wave-uniform)
     int64_t steps = len;
@@ -591,6 +577,11 @@ __global__ __launch_bounds__(256, MML_RUNS_WPE) void bmf_sgd_runs_kernel(
     };
     int32_t my_u = 0, my_i = 0;
     float my_r = 0.0f;
+#if MML_RUNS_PF
+    float4 qn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float bn = 0.0f;
+    bool have = false;
+#endif
     for (int64_t t = 0; t < steps; ++t) {
         if ((t % LPR) == 0) {
             if constexpr ((AM & kAccFlush) != 0)
@@ -621,12 +612,34 @@ __global__ __launch_bounds__(256, MML_RUNS_WPE) void bmf_sgd_runs_kernel(
         const int64_t oi = (int64_t)i * ld4 + ou0;
         float4 qi;
         float bi_i = 0.0f;
-        if constexpr (IL2) qi = mml::load4_l2(vrs, (uint32_t)oi * 16u);
-        else qi = V4[oi];
-        if constexpr (biased) {
-            if constexpr (IL2) bi_i = mml::load1_l2(brs, (uint32_t)i * 4u);
-            else bi_i = bi[i];
+        auto load_item = [&](int32_t it, float4& q4, float& b1) {
+            const int64_t o = (int64_t)it * ld4 + ou0;
+            if constexpr (IL2) q4 = mml::load4_l2(vrs, (uint32_t)o * 16u);
+            else q4 = V4[o];
+            if constexpr (biased) {
+                if constexpr (IL2) b1 = mml::load1_l2(brs, (uint32_t)it * 4u);
+                else b1 = bi[it];
+            }
+        };
+#if MML_RUNS_PF
+        // the row of this step came with the previous one (same staged block); the next step's is
+        // requested now, ahead of this step's arithmetic and stores
+        if (have) {
+            qi = qn;
+            bi_i = bn;
+        } else {
+            load_item(i, qi, bi_i);
         }
+        have = false;
+        int32_t inx = -1;
+        if ((int)((t + 1) % LPR) != 0 && t + 1 < len) {
+            inx = __shfl(my_i, src + 1);
+            load_item(inx, qn, bn);
+            have = true;
+        }
+#else
+        load_item(i, qi, bi_i);
+#endif
         if constexpr (LOSS == kReplayTraffic) {
             asm volatile("" : "+v"(qi.x), "+v"(qi.y), "+v"(qi.z), "+v"(qi.w), "+v"(bi_i) : "v"(r));
             if (q == 0) bi[i] = bi_i;
@@ -639,10 +652,17 @@ __global__ __launch_bounds__(256, MML_RUNS_WPE) void bmf_sgd_runs_kernel(
                 bu_u = st.new_bu;
                 if (q == 0) bi[i] = st.new_bi;
             }
-            V4[oi] = make_float4(st.new_i(s, pu.x, qi.x), st.new_i(s, pu.y, qi.y),
-                                 st.new_i(s, pu.z, qi.z), st.new_i(s, pu.w, qi.w));
+            const float4 nv = make_float4(st.new_i(s, pu.x, qi.x), st.new_i(s, pu.y, qi.y),
+                                          st.new_i(s, pu.z, qi.z), st.new_i(s, pu.w, qi.w));
+            V4[oi] = nv;
             pu = make_float4(st.new_u(s, pu.x, qi.x), st.new_u(s, pu.y, qi.y),
                              st.new_u(s, pu.z, qi.z), st.new_u(s, pu.w, qi.w));
+#if MML_RUNS_PF
+            if (inx == i) {  // the same item next (a repeated rating): this step's new row
+                qn = nv;
+                if (biased) bn = st.new_bi;
+            }
+#endif
         }
     }
     if (cur >= 0) put_user();
@@ -1666,8 +1686,10 @@ struct mml_bmf {
     int32_t runs_req = -1;  // -1: on unless mml_bmf_set_hogwild_phases chose a phase count
     bool has_runs = false, last_runs = false;  // last_runs: the last Hogwild epoch ran in runs
     int64_t n_runs = 0;                        // runs of the runs stream (ensure_runs)
-    int64_t run_blocks = 0;                    // the last runs launch's geometry (the export)
-    int32_t run_wpg = 0;
+    // the strata: launch s gives group g user block (g + s) % 8; rspan[16 s + 2 g, + 1] = its
+    // [begin, end) in the runs stream (device, and run_spans on the host)
+    mml::DeviceArray<int64_t> rspan;
+    std::vector<int64_t> run_spans;
     mml::DeviceArray<int32_t> rxu, rxi, rxr;
     // multi-device context: one single-device handle per GPU over a user range ub[d] .. ub[d + 1]
     // (U, b_u trained there; V, b_i replicated and averaged after every epoch)
@@ -2085,8 +2107,25 @@ __global__ __launch_bounds__(256) void count_runs_kernel(const int32_t* __restri
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
 }
 
+// first position of the sorted keys >= thr[t], t = 0 .. nt
+__global__ __launch_bounds__(256) void key_thresholds_kernel(const uint32_t* __restrict__ key,
+                                                             int64_t n,
+                                                             const int64_t* __restrict__ thr,
+                                                             int32_t nt,
+                                                             int64_t* __restrict__ off) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nt) return;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)key[mid] < thr[t]) lo = mid + 1;
+        else hi = mid;
+    }
+    off[t] = lo;
+}
+
 // the user-runs stream (built once per data set): the group-major XCD stream, each group's span
-// stably sorted by user
+// stably sorted by user, and its 8 x 8 strata (user blocks of equal rating count x XCD groups)
 void ensure_runs(mml_bmf* h) {
     if (h->has_runs) return;
     if (h->n_phases != 1) ensure_phases(h, 1);
@@ -2112,6 +2151,47 @@ void ensure_runs(mml_bmf* h) {
     tmp.alloc(std::max<size_t>(1, tmp_bytes));
     MML_HIP(rocprim::radix_sort_pairs(tmp.get(), tmp_bytes, key.get(), key_s.get(), idx.get(),
                                       idx_s.get(), n, 0, end_bit, st));
+    // user blocks of equal rating count: ub[b] = the first user of block b
+    std::vector<int32_t> cu(h->n_users);
+    if (h->n_users > 0)
+        MML_HIP(hipMemcpyAsync(cu.data(), h->cnt_u.get(), sizeof(int32_t) * h->n_users,
+                               hipMemcpyDeviceToHost, st));
+    MML_HIP(hipStreamSynchronize(st));
+    std::vector<int64_t> ub(9, h->n_users);
+    ub[0] = 0;
+    {
+        int64_t run = 0;
+        int b = 1;
+        for (int32_t u = 0; u < h->n_users && b < 8; ++u) {
+            run += cu[u];
+            while (b < 8 && run * 8 >= n * b) ub[b++] = u + 1;
+        }
+    }
+    std::vector<int64_t> thr(8 * 9);
+    for (int g = 0; g < 8; ++g)
+        for (int b = 0; b <= 8; ++b) thr[9 * g + b] = (int64_t)g * h->n_users + ub[b];
+    mml::DeviceArray<int64_t> thr_d, off_d;
+    thr_d.alloc(thr.size());
+    off_d.alloc(thr.size());
+    MML_HIP(hipMemcpyAsync(thr_d.get(), thr.data(), sizeof(int64_t) * thr.size(),
+                           hipMemcpyHostToDevice, st));
+    key_thresholds_kernel<<<1, 128, 0, st>>>(key_s.get(), n, thr_d.get(), (int32_t)thr.size(),
+                                             off_d.get());
+    MML_HIP(hipGetLastError());
+    std::vector<int64_t> off(thr.size());
+    MML_HIP(hipMemcpyAsync(off.data(), off_d.get(), sizeof(int64_t) * off.size(),
+                           hipMemcpyDeviceToHost, st));
+    MML_HIP(hipStreamSynchronize(st));
+    h->run_spans.assign(8 * 16, 0);
+    for (int sx = 0; sx < 8; ++sx)
+        for (int g = 0; g < 8; ++g) {
+            const int b = (g + sx) % 8;
+            h->run_spans[16 * sx + 2 * g] = off[9 * g + b];
+            h->run_spans[16 * sx + 2 * g + 1] = off[9 * g + b + 1];
+        }
+    h->rspan.alloc(h->run_spans.size());
+    MML_HIP(hipMemcpyAsync(h->rspan.get(), h->run_spans.data(),
+                           sizeof(int64_t) * h->run_spans.size(), hipMemcpyHostToDevice, st));
     key.reset();
     key_s.reset();
     idx.reset();
@@ -2195,8 +2275,13 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
 #endif
             default: am = kAccItemL2; break;
         }
+        // the default (runs_req -1) from 16 M ratings: on the small skewed sets of the edge-case
+        // and shard tests (300 k ratings over 300-800 items, a wave's slices a few runs long) the
+        // runs measured up to 2x the phase kernel's Hogwild offset, so those keep the phases
+        constexpr int64_t kRunsMinRatings = 16000000;
         const bool want_runs =
-            h->runs_req > 0 || (h->runs_req < 0 && h->phases_req == 0 && hogwild_phases_env() < 0);
+            h->runs_req > 0 || (h->runs_req < 0 && h->phases_req == 0 && hogwild_phases_env() < 0 &&
+                                n >= kRunsMinRatings);
         if (want_runs && (am & kAccUserThru) != 0) {
             // user runs: one launch over the group-major stream sorted by user within a group
             ensure_runs(h);
@@ -2250,18 +2335,15 @@ void launch_hogwild(mml_bmf* h, const BmfScalars& s, const int32_t* cu, const in
         default: MML_HOG1(LPR, VPL, kAccPlain); break;                           \
     }
 #define MML_RUN1(LPR, AM)                                                                        \
-    bmf_sgd_runs_kernel<LOSS, LPR, AM><<<(int)blocks, 256, 0, st>>>(                              \
-        su, si, sr, goff, ng, wpg, h->U.get(), h->V.get(), h->bu.get(), h->bi.get(), ld4, vb, bb, \
-        ub, bub, mml::flushers_per_xcd(1), s, cu, ci);                                           \
+    for (int sx = 0; sx < 8; ++sx)                                                                \
+        bmf_sgd_runs_kernel<LOSS, LPR, AM><<<(int)blocks, 256, 0, st>>>(                          \
+            su, si, sr, h->rspan.get() + 16 * sx, wpg, h->U.get(), h->V.get(), h->bu.get(),      \
+            h->bi.get(), ld4, vb, bb, ub, bub, mml::flushers_per_xcd(1), s, cu, ci);              \
     h->last_kernel = kernel_label("bmf_sgd_runs_kernel", {LOSS, LPR, (int)(AM)})
 // (no flushing waves: a group's item rows are read by its own XCD only, and the runs write U_u
 // through; with them C4 was 112.3 / 113.2 against 107.0 / 107.3 ms per epoch, profiles/r6/runs/)
 #define MML_RUNV(LPR) MML_RUN1(LPR, kAccItemL2 | kAccUserThru)
     if (runs) {
-        if (LOSS != kReplayTraffic) {
-            h->run_blocks = blocks;
-            h->run_wpg = wpg;
-        }
         switch (h->lpr) {
             case 1: MML_RUNV(1); break;
             case 2: MML_RUNV(2); break;
@@ -3644,41 +3726,39 @@ extern "C" mml_status mml_bmf_hogwild_stream(mml_bmf* h, int32_t* users, int32_t
         MML_REQUIRE(h->has_data && n == h->n, "n must equal the handle's rating count");
         MML_REQUIRE(h->has_xstream,
                     "no XCD-grouped stream: run a HOGWILD epoch on an 8-XCD device first");
-        const bool runs = h->last_runs && h->has_runs;  // the user-runs stream (one launch)
-        const int32_t spans = runs ? 8 : h->n_phases * 8;
+        const bool runs = h->last_runs && h->has_runs;  // the user-runs strata (8 launches)
+        const int32_t spans = runs ? 64 : h->n_phases * 8;
         MML_REQUIRE(cap_offsets >= spans + 1, "span_offsets holds fewer than phases * 8 + 1");
         h->ctx->activate();
         hipStream_t st = h->ctx->stream;
-        mml::DeviceArray<int32_t> wu, wi, wr;
-        const int32_t *eu = h->xu.get(), *ei = h->xi.get(), *er = h->xr.get();
-        if (runs && n > 0) {
-            // the order the lane groups walked: each slice from its rotated start, wrapping round
-            mml::DeviceArray<int32_t> walk;
-            walk.alloc(n);
-            const int rpw = 64 / h->lpr;
-            auto wk = rpw == 64 ? &runs_walk_kernel<64> : rpw == 32 ? &runs_walk_kernel<32>
-                      : rpw == 16 ? &runs_walk_kernel<16> : rpw == 8 ? &runs_walk_kernel<8>
-                      : rpw == 4 ? &runs_walk_kernel<4> : rpw == 2 ? &runs_walk_kernel<2>
-                      : &runs_walk_kernel<1>;
-            wk<<<(int)h->run_blocks, 256, 0, st>>>(h->rxu.get(), h->xs.goff.get(), 8, h->run_wpg,
-                                                   walk.get());
-            wu.alloc(n);
-            wi.alloc(n);
-            wr.alloc(n);
-            gather3_kernel<<<grid_for(n), 256, 0, st>>>(walk.get(), n, h->rxu.get(), h->rxi.get(),
-                                                        h->rxr.get(), wu.get(), wi.get(), wr.get());
-            MML_HIP(hipGetLastError());
+        if (runs) {
+            // launch-major, group-minor: the strata in the order the 8 launches walk them
+            int64_t at = 0;
+            for (int x = 0; x < 64; ++x) {
+                const int64_t b = h->run_spans[2 * x], e = h->run_spans[2 * x + 1];
+                span_offsets[x] = at;
+                if (e > b) {
+                    MML_HIP(hipMemcpyAsync(users + at, h->rxu.get() + b, sizeof(int32_t) * (e - b),
+                                           hipMemcpyDeviceToHost, st));
+                    MML_HIP(hipMemcpyAsync(items + at, h->rxi.get() + b, sizeof(int32_t) * (e - b),
+                                           hipMemcpyDeviceToHost, st));
+                    MML_HIP(hipMemcpyAsync(values + at, h->rxr.get() + b, sizeof(float) * (e - b),
+                                           hipMemcpyDeviceToHost, st));
+                }
+                at += e - b;
+            }
+            span_offsets[64] = at;
             MML_HIP(hipStreamSynchronize(st));
-            eu = wu.get();
-            ei = wi.get();
-            er = wr.get();
+            MML_REQUIRE(at == n, "the strata do not cover the stream");
+            *n_spans = spans;
+            return;
         }
         if (n > 0) {
-            MML_HIP(hipMemcpyAsync(users, eu, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
-            MML_HIP(hipMemcpyAsync(items, ei, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
-            MML_HIP(hipMemcpyAsync(values, er, sizeof(float) * n, hipMemcpyDeviceToHost, st));
+            MML_HIP(hipMemcpyAsync(users, h->xu.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+            MML_HIP(hipMemcpyAsync(items, h->xi.get(), sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+            MML_HIP(hipMemcpyAsync(values, h->xr.get(), sizeof(float) * n, hipMemcpyDeviceToHost, st));
         }
-        const int64_t* off = h->n_phases > 1 && !runs ? h->poff.get() : h->xs.goff.get();
+        const int64_t* off = h->n_phases > 1 ? h->poff.get() : h->xs.goff.get();
         MML_HIP(hipMemcpyAsync(span_offsets, off, sizeof(int64_t) * (spans + 1),
                                hipMemcpyDeviceToHost, st));
         MML_HIP(hipStreamSynchronize(st));

@@ -3,14 +3,16 @@ bmf_sgd_runs_kernel / ensure_runs): every XCD group's span sorted by user, so a 
 one group form a run that one lane group applies in order, U_u and b_u held in registers across it
 (BiasedMatrixFactorization.cs:264-310 within the run).
 
-The runs change the visit order, so the reference here is the oracle over the exact stream the
-launch walked (mml_bmf_hogwild_stream), as for the user phases (tests/test_phases_gpu.py): the
+The epoch runs as 8 launches over strata (user blocks of equal rating count x XCD groups, launch s
+gives group g block (g + s) mod 8), so no user's row is in two XCDs' registers at once.  The runs
+change the visit order, so the reference here is the oracle over the exact stream the launches
+walked (mml_bmf_hogwild_stream: launch-major, group-minor), as for the user phases (tests/test_phases_gpu.py): the
 sequential Iterate() and hogwild_band's staleness model with the runs kernel's streams (every lane
 group a stream, one rating per step).  Per epoch the GPU must sit in that band (3x its run-to-run
 spread + 2e-5 of slack).  The order's own cost to the reference's loop, oracle(runs order) -
 oracle(one-phase order), is printed beside the GPU's lag against its one-phase epoch.  The stream
-must hold every rating once, each item in one XCD group's span, and each user in one run per
-group span."""
+must hold every rating once, each item in one XCD group's spans, each launch's groups disjoint
+users, and each user in one run per stratum."""
 import ctypes
 from concurrent.futures import ThreadPoolExecutor
 
@@ -22,15 +24,29 @@ pytestmark = pytest.mark.gpu
 NU, NI, N_TRAIN, K, EPOCHS = 800_000, 50_000, 16_000_000, 64, 4
 
 
-def _check_runs_stream(stream, nu):
-    """In the walk order each user's ratings of a group span are one contiguous run."""
+def _check_runs_stream(stream, ref_hash, ni):
+    """The 8 launches x 8 groups of strata: every rating once; each item in one XCD group's spans;
+    in each launch the 8 groups' users disjoint (no user's row in two XCDs at once); each user's
+    ratings of a stratum one contiguous run."""
+    from test_phases_c4_gpu import _multiset_hash
     su, si, sv, off = stream
-    for g in range(8):
-        u = su[off[g]:off[g + 1]]
-        if len(u) == 0:
-            continue
-        blocks = 1 + int(np.count_nonzero(u[1:] != u[:-1]))
-        assert blocks == len(np.unique(u)), f"group {g}: a user's ratings in two runs"
+    assert len(off) == 65 and off[0] == 0 and off[-1] == len(su) and np.all(np.diff(off) >= 0)
+    assert _multiset_hash(su, si, sv) == ref_hash
+    group_of_item = np.full(ni, -1, np.int8)
+    for x in range(64):
+        items = np.unique(si[off[x]:off[x + 1]])
+        seen = group_of_item[items]
+        assert np.all((seen == -1) | (seen == x % 8)), "an item in two XCD groups' spans"
+        group_of_item[items] = x % 8
+    for launch in range(8):
+        users = [np.unique(su[off[8 * launch + g]:off[8 * launch + g + 1]]) for g in range(8)]
+        allu = np.concatenate(users)
+        assert len(np.unique(allu)) == len(allu), f"launch {launch}: a user in two groups"
+    for x in range(64):
+        u = su[off[x]:off[x + 1]]
+        if len(u):
+            assert 1 + int(np.count_nonzero(u[1:] != u[:-1])) == len(np.unique(u)), \
+                f"span {x}: a user's ratings in two runs"
 
 
 def test_user_runs_pinned_to_the_oracle():
@@ -58,9 +74,8 @@ def test_user_runs_pinned_to_the_oracle():
                 streams[mode] = o["stream"]
             reps.append(o["rmse"])
         gpu[mode] = np.array(reps)
-    for st in streams.values():
-        _check_stream(st, 1, ref_hash, nu=NU, ni=NI)
-    _check_runs_stream(streams["runs"], NU)
+    _check_stream(streams["one phase"], 1, ref_hash, nu=NU, ni=NI)
+    _check_runs_stream(streams["runs"], ref_hash, NI)
     waves, rpw = hogwild_streams(N_TRAIN, K)
     model = {"one phase": None, "runs": (waves * rpw, 1)}
     with ThreadPoolExecutor(4) as ex:
@@ -111,8 +126,8 @@ def test_runs_switch_on_one_handle():
                                                    len(off), ctypes.byref(spans)))
             assert _multiset_hash(su, si, sv) == ref
             if on:
-                assert spans.value == 8
-                _check_runs_stream((su, si, sv, off[:9]), nu)
+                assert spans.value == 64
+                _check_runs_stream((su, si, sv, off[:65]), ref, ni)
                 runs_streams.append((su, si, sv))
         for a, b in zip(*runs_streams):
             assert np.array_equal(a, b)
