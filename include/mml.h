@@ -307,8 +307,8 @@ mml_status mml_bmf_last_runs(mml_bmf* h, int64_t* out);
 /* The stream the last HOGWILD epoch ran on an 8-XCD device (ABI 13; single-device handles): the n
  * ratings (n = the handle's count) in the order the launches walk them -- phase-major, XCD-group
  * minor, the RandomIndex visit order kept inside a span -- and the phases * 8 + 1 span offsets
- * (phase p, group g = span p * 8 + g); *n_spans = phases * 8 (with user runs, ABI 14: the runs
- * stream and its 8 group spans).  The sequential Iterate()
+ * (phase p, group g = span p * 8 + g); *n_spans = phases * 8 (with user runs, ABI 14: the 8
+ * launches' strata, launch s group g = span s * 8 + g, 64 spans).  The sequential Iterate()
  * (BiasedMatrixFactorization.cs:264-310) over this order is the epoch without Hogwild's concurrency
  * (tests/test_phases_c4_gpu.py).  MML_ERR_ARG before such an epoch. */
 mml_status mml_bmf_hogwild_stream(mml_bmf* h, int32_t* users, int32_t* items, float* values,
